@@ -1,0 +1,135 @@
+#!/usr/bin/env python3
+"""Headline benchmark: raft_large inference throughput (image pairs / s) on
+Sintel-shaped 440x1024 frames (436 padded to /8, like scripts/validate_sintel.py
+of the reference), 32 refinement iterations, all 32 upsampled predictions
+produced (the reference's output), bf16 compute on the native HIP kernels with
+the whole forward replayed as one hipGraph.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
+launched by torch.distributed.run, one rank per GPU (RCCL).  Weak scaling:
+each rank processes ``--batch`` pairs per step (default 4, so 8 GPUs = the
+BASELINE config's batch of 32).  Each timed step includes the host->device
+copy of the input pair (the reference times H2D + forward as well,
+validate_sintel.py:185-186).  Timing: W untimed warmup steps, then exactly K
+steps bracketed by barrier + synchronize; the MAX over ranks is reported.
+Weights are random-init (no network for checkpoints), data is synthetic, so
+EPE is not measurable here and is reported as null.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+BASELINE_FPS = 11.8  # README.md:9 of the reference (RTX 3090 Ti, raft_large, 32 iters, batch 1)
+METRIC = "image-pairs/sec + Sintel-clean EPE, raft_large 32 iters at 1/2/4/8 MI355X"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4, help="image pairs per GPU per step")
+    ap.add_argument("--arch", default="raft_large", choices=["raft_large", "raft_small"])
+    ap.add_argument("--height", type=int, default=440)
+    ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--iters", type=int, default=32)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-h2d", action="store_true", help="inputs already resident on the GPU")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} != WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+        pg = dist
+
+    from jax_raft_amd import raft_large, raft_small
+
+    model, _ = (raft_large if args.arch == "raft_large" else raft_small)(seed=0)
+    model = model.to(dev).eval()
+    B, H, W = args.batch, args.height, args.width
+    g = torch.Generator().manual_seed(1234 + rank)
+    img1 = (torch.rand(B, H, W, 3, generator=g) * 2 - 1)
+    img2 = (torch.rand(B, H, W, 3, generator=g) * 2 - 1)
+    if args.no_h2d:
+        img1, img2 = img1.to(dev), img2.to(dev)
+    else:
+        img1, img2 = img1.pin_memory(), img2.pin_memory()
+
+    def step():
+        a = img1.to(dev, non_blocking=True)
+        b = img2.to(dev, non_blocking=True)
+        return model(a, b, num_flow_updates=args.iters, use_graph=not args.no_graph)
+
+    def barrier():
+        if pg is not None:
+            pg.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        out = step()
+    torch.cuda.synchronize(dev)
+    assert out.shape == (args.iters, B, H, W, 2) and bool(torch.isfinite(out[-1]).all())
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    barrier()
+    dt = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if pg is not None:
+        pg.all_reduce(dt, op=pg.ReduceOp.MAX)
+    elapsed = dt.item()
+    ms_per_step = 1000.0 * elapsed / args.steps
+    pairs_per_s = world * B * args.steps / elapsed
+    if rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": round(pairs_per_s, 3),
+            "unit": "image-pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(pairs_per_s / BASELINE_FPS, 3) if args.arch == "raft_large" and args.iters == 32 else None,
+            "dtype": "bf16",
+            "data": "synthetic (random Sintel-shaped 440x1024 frames, random-init weights; EPE not measurable)",
+            "epe_sintel_clean": None,
+            "config": {
+                "model": args.arch,
+                "global_batch": world * B,
+                "per_gpu_batch": B,
+                "image_size": [H, W],
+                "seq_len": None,
+                "num_flow_updates": args.iters,
+                "outputs": "all iterations upsampled (reference semantics)",
+                "hipgraph": not args.no_graph,
+                "h2d_in_timed_region": not args.no_h2d,
+                "parallelism": f"dp{world}",
+            },
+        }
+        print(json.dumps(rec), flush=True)
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,292 @@
+// All-pairs correlation pyramid and radius-r pyramid lookup (gfx950).
+//
+// Reference: CorrBlock in jax_raft/model.py:403-481 -- build_pyramid
+// (matmul / sqrt(C) then 2x2 VALID avg-pool L-1 times, :418-446, :472-481) and
+// index_pyramid (grid_sample of a (2r+1)^2 window around coords/2^l,
+// :448-470; grid_sample itself :24-34).
+//
+// corr_pyramid_kernel: one MFMA GEMM tile = 128 query pixels (A operand,
+// rows) x a 2-D 8x16 block of target pixels (B operand, columns).  Because
+// the target tile is a spatially aligned 8x16 block, every pyramid level's
+// 2x2 pooling is formed in-register (tile pairs for y, lane shuffles for x)
+// and all L levels are written by the same kernel: the level-0 volume is
+// never re-read to build the pyramid.  Floor semantics: only cells whose
+// full 2^l x 2^l footprint is inside the map are emitted.
+//
+// corr_lookup_kernel: one wave per query pixel; lane = (level, window
+// column).  All (2r+1)^2 samples of a level share one fractional offset, so
+// each lane loads one (2r+2)-tall column of the level map, interpolates
+// vertically, and takes the horizontal neighbour column from lane+1 via a
+// shuffle.  Output channels follow the reference order
+// l*(2r+1)^2 + i*(2r+1) + j (x-offset i-r is the slow index), staged in LDS
+// and written as 16-B vectors, zero-padded to the consumer's channel stride.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int BK = 64;
+JR_DEVICE int swz(int row) { return (row >> 1) & 7; }
+
+// 4 waves x (TM=2 query tiles of 16) = 128 queries; TN = 8 target rows x 16 cols.
+constexpr int CQ = 128;
+constexpr int TY = 8, TX = 16;
+constexpr int CT = TY * TX;
+
+__global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restrict__ f1, const bf16* __restrict__ f2,
+                                                           int h, int w, int C, int cs, float* __restrict__ l0,
+                                                           float* __restrict__ l1, float* __restrict__ l2,
+                                                           float* __restrict__ l3, int nlev, float scale) {
+  constexpr int TM = 2, TN = 8;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (CQ + CT) * BK];
+  const int P = h * w;
+  const int b = blockIdx.z;
+  const int q0 = blockIdx.x * CQ;
+  const int ntx = (w + TX - 1) / TX;
+  const int ty0 = (blockIdx.y / ntx) * TY;
+  const int tx0 = (blockIdx.y % ntx) * TX;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ch = tid & 7;
+  const bf16* A = f1 + (long)b * P * cs;
+  const bf16* Bm = f2 + (long)b * P * cs;
+
+  // each thread loads 4 query rows and 4 target rows (chunk ch of 8)
+  long aoff[4], boff[4];
+  bool aok[4], bok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (tid >> 3) + 32 * i;
+    const int q = q0 + r;
+    aok[i] = q < P;
+    aoff[i] = (long)(aok[i] ? q : 0) * cs;
+    const int ty = ty0 + (r >> 4), tx = tx0 + (r & 15);
+    bok[i] = ty < h && tx < w;
+    boff[i] = (long)(bok[i] ? ty * w + tx : 0) * cs;
+  }
+  u32x4 ar[4], br[4];
+  auto load = [&](int ks) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ar[i] = aok[i] ? *(const u32x4*)(A + aoff[i] + ks * BK + ch * 8) : u32x4{0u, 0u, 0u, 0u};
+      br[i] = bok[i] ? *(const u32x4*)(Bm + boff[i] + ks * BK + ch * 8) : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store = [&](int buf) {
+    bf16* sA = smem + buf * (CQ + CT) * BK;
+    bf16* sB = sA + CQ * BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      *(u32x4*)(sA + r * BK + ((ch ^ swz(r)) << 3)) = ar[i];
+      *(u32x4*)(sB + r * BK + ((ch ^ swz(r)) << 3)) = br[i];
+    }
+  };
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int c = 0; c < TN; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nks = C / BK;
+  load(0);
+  store(0);
+  __syncthreads();
+  const int li = lane & 15, lq = lane >> 4;
+  for (int ks = 0; ks < nks; ++ks) {
+    const int cur = ks & 1;
+    const bool more = ks + 1 < nks;
+    if (more) load(ks + 1);
+    const bf16* sA = smem + cur * (CQ + CT) * BK;
+    const bf16* sB = sA + CQ * BK;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + lq;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int row = wave * (TM * 16) + tm * 16 + li;
+        af[tm] = *(const bf16x8*)(sA + row * BK + ((chunk ^ swz(row)) << 3));
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int row = tn * 16 + li;
+        bfr[tn] = *(const bf16x8*)(sB + row * BK + ((chunk ^ swz(row)) << 3));
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tm], bfr[tn], acc[tm][tn], 0, 0, 0);
+    }
+    if (more) store(cur ^ 1);
+    __syncthreads();
+  }
+
+  // Epilogue: D[query = qbase + 4*lq + r][target = (ty0 + tn, tx0 + li)]
+  const int x0 = tx0 + li;
+  const int h1 = h >> 1, w1 = w >> 1, h2 = h1 >> 1, w2 = w1 >> 1, h3 = h2 >> 1, w3 = w2 >> 1;
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = q0 + wave * (TM * 16) + tm * 16 + 4 * lq + r;
+      const bool qok = q < P;
+      float v[TN];
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) v[tn] = acc[tm][tn][r] * scale;
+      // level 0
+      if (qok && x0 < w) {
+        float* dst = l0 + ((long)b * P + q) * P;
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          if (ty0 + tn < h) dst[(ty0 + tn) * w + x0] = v[tn];
+      }
+      if (nlev < 2) continue;
+      // level 1: pairs of rows (tn, tn+1), lanes (li, li^1)
+      float v1[TN / 2];
+#pragma unroll
+      for (int t = 0; t < TN / 2; ++t) {
+        const float s = v[2 * t] + v[2 * t + 1];
+        v1[t] = 0.25f * (s + __shfl_xor(s, 1));
+      }
+      {
+        const int X1 = x0 >> 1;
+        if (qok && (li & 1) == 0 && X1 < w1) {
+          float* dst = l1 + ((long)b * P + q) * (h1 * w1);
+#pragma unroll
+          for (int t = 0; t < TN / 2; ++t) {
+            const int Y1 = (ty0 >> 1) + t;
+            if (Y1 < h1) dst[Y1 * w1 + X1] = v1[t];
+          }
+        }
+      }
+      if (nlev < 3) continue;
+      float v2[TN / 4];
+#pragma unroll
+      for (int t = 0; t < TN / 4; ++t) {
+        const float s = v1[2 * t] + v1[2 * t + 1];
+        v2[t] = 0.25f * (s + __shfl_xor(s, 2));
+      }
+      {
+        const int X2 = x0 >> 2;
+        if (qok && (li & 3) == 0 && X2 < w2) {
+          float* dst = l2 + ((long)b * P + q) * (h2 * w2);
+#pragma unroll
+          for (int t = 0; t < TN / 4; ++t) {
+            const int Y2 = (ty0 >> 2) + t;
+            if (Y2 < h2) dst[Y2 * w2 + X2] = v2[t];
+          }
+        }
+      }
+      if (nlev < 4) continue;
+      {
+        const float s = v2[0] + v2[1];
+        const float v3 = 0.25f * (s + __shfl_xor(s, 4));
+        const int X3 = x0 >> 3;
+        const int Y3 = ty0 >> 3;
+        if (qok && (li & 7) == 0 && X3 < w3 && Y3 < h3) {
+          l3[((long)b * P + q) * (h3 * w3) + Y3 * w3 + X3] = v3;
+        }
+      }
+    }
+  }
+}
+
+struct LevelPtrs {
+  const float* p[8];
+};
+
+// blockDim = 256 (4 queries / block); lane = level*16 + i
+__global__ __launch_bounds__(256) void corr_lookup_kernel(LevelPtrs lv, int nlev, int total, int h, int w, int radius,
+                                                          const float* __restrict__ coords, bf16* __restrict__ out,
+                                                          int ocs) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
+  bf16* stage = (bf16*)dyn_smem;  // [4][ocs]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = blockIdx.x * 4 + wave;
+  const int S = 2 * radius + 1;
+  bf16* st = stage + wave * ocs;
+  // zero the staging row (covers channel padding)
+  for (int c = lane; c < ocs; c += 64) st[c] = f2bf(0.f);
+  __syncthreads();
+  if (q < total) {
+    const int P = h * w;
+    const int b = q / P;
+    const int lvl = lane >> 4;
+    const int i = lane & 15;
+    const float x = coords[2 * (long)q];
+    const float y = coords[2 * (long)q + 1];
+    float vv[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) vv[j] = 0.f;
+    float fx = 0.f;
+    const bool lane_on = lvl < nlev && i <= S;
+    if (lane_on) {
+      const float sc = 1.0f / (float)(1 << lvl);
+      const float cx = x * sc, cy = y * sc;
+      const float flx = floorf(cx), fly = floorf(cy);
+      fx = cx - flx;
+      const float fy = cy - fly;
+      const int hl = h >> lvl, wl = w >> lvl;
+      const int col = (int)flx - radius + i;
+      const int row0 = (int)fly - radius;
+      const float* map = lv.p[lvl] + (long)q * (hl * wl) - (long)b * 0;  // level maps are [B*P][hl][wl]
+      const bool colok = (unsigned)col < (unsigned)wl;
+      float prev = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (j <= S) {
+          const int rr = row0 + j;
+          const float cur = (colok && (unsigned)rr < (unsigned)hl) ? map[rr * wl + col] : 0.f;
+          if (j > 0) vv[j - 1] = (1.f - fy) * prev + fy * cur;
+          prev = cur;
+        }
+      }
+    }
+    // horizontal interpolation with the neighbouring column (lane + 1)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float nb = __shfl_down(vv[j], 1);
+      vv[j] = (1.f - fx) * vv[j] + fx * nb;
+    }
+    if (lvl < nlev && i < S) {
+      const int base = lvl * S * S + i * S;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (j < S) st[base + j] = f2bf(vv[j]);
+    }
+  }
+  __syncthreads();
+  if (q < total) {
+    bf16* dst = out + (long)q * ocs;
+    for (int c = lane * 8; c < ocs; c += 64 * 8) *(u32x4*)(dst + c) = *(const u32x4*)(st + c);
+  }
+}
+
+}  // namespace
+
+extern "C" int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int w, int C, int cs, float* lvl0,
+                               float* lvl1, float* lvl2, float* lvl3, int num_levels, float scale,
+                               hipStream_t stream) {
+  if (C % BK != 0 || cs % 8 != 0 || num_levels < 1 || num_levels > 4) return (int)hipErrorInvalidValue;
+  const int P = h * w;
+  dim3 grid((P + CQ - 1) / CQ, ((h + TY - 1) / TY) * ((w + TX - 1) / TX), B);
+  hipLaunchKernelGGL(corr_pyramid_kernel, grid, dim3(256), 0, stream, (const bf16*)f1, (const bf16*)f2, h, w, C, cs,
+                     lvl0, lvl1, lvl2, lvl3, num_levels, scale);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jr_corr_lookup(const float* const* levels, int num_levels, int B, int h, int w, int radius,
+                              const float* coords, void* out, int out_cstride, hipStream_t stream) {
+  const int S = 2 * radius + 1;
+  if (num_levels > 4 || S + 1 > 16 || out_cstride % 8 != 0 || out_cstride < num_levels * S * S)
+    return (int)hipErrorInvalidValue;
+  LevelPtrs lv;
+  for (int l = 0; l < 8; ++l) lv.p[l] = l < num_levels ? levels[l] : nullptr;
+  const int total = B * h * w;
+  dim3 grid((total + 3) / 4);
+  const size_t smem = 4 * out_cstride * sizeof(bf16);
+  hipLaunchKernelGGL(corr_lookup_kernel, grid, dim3(256), smem, stream, lv, num_levels, total, h, w, radius, coords,
+                     (bf16*)out, out_cstride);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,263 @@
+// Memory-bound kernels: flow upsampling (convex + bilinear), norm statistics /
+// application, input preparation and small buffer helpers (gfx950).
+//
+// Reference semantics:
+//   upsample_flow            jax_raft/model.py:69-98
+//   resize_with_aligned_corners (bilinear, align_corners)  model.py:43-66
+//   InstanceNorm / BatchNorm (Flax)                         model.py:147,157,706-711
+//   make_coords_grid                                        model.py:37-40
+//   image normalisation / NHWC staging                      scripts/validate_sintel.py:177-183
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+// One wave per low-res pixel, lane = sub-pixel s = a*8 + b.
+__global__ __launch_bounds__(256) void upsample_convex_kernel(const bf16* __restrict__ mask, int mcs,
+                                                              const float* __restrict__ flow, int B, int h, int w,
+                                                              float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int P = h * w;
+  if (p >= B * P) return;
+  const int b = p / P;
+  const int rem = p - b * P;
+  const int y = rem / w, x = rem - y * w;
+  const bf16* mp = mask + (long)p * mcs + lane;
+  float lg[9];
+  float mx = -3.0e38f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    lg[k] = bf2f(mp[k * 64]);
+    mx = fmaxf(mx, lg[k]);
+  }
+  float s = 0.f, ux = 0.f, uy = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int yy = y + k / 3 - 1, xx = x + k % 3 - 1;
+    const float e = __expf(lg[k] - mx);
+    s += e;
+    if ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w) {
+      const float* fp = flow + 2 * ((long)b * P + yy * w + xx);
+      ux += e * fp[0];
+      uy += e * fp[1];
+    }
+  }
+  const float inv = 8.0f / s;
+  const int a = lane >> 3, bb = lane & 7;
+  const long W8 = 8L * w;
+  float* op = out + 2 * (((long)b * 8 * h + 8 * y + a) * W8 + 8 * x + bb);
+  *(float2*)op = make_float2(ux * inv, uy * inv);
+}
+
+__global__ void upsample_bilinear_kernel(const float* __restrict__ flow, int B, int h, int w,
+                                         float* __restrict__ out) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int H8 = 8 * h, W8 = 8 * w;
+  const long total = (long)B * H8 * W8;
+  if (idx >= total) return;
+  const int X = idx % W8;
+  const long t = idx / W8;
+  const int Y = t % H8;
+  const int b = t / H8;
+  const float sx = (w > 1) ? (float)(w - 1) / (float)(W8 - 1) : 0.f;
+  const float sy = (h > 1) ? (float)(h - 1) / (float)(H8 - 1) : 0.f;
+  const float xi = X * sx, yi = Y * sy;
+  int x0 = (int)floorf(xi), y0 = (int)floorf(yi);
+  x0 = min(max(x0, 0), w - 1);
+  y0 = min(max(y0, 0), h - 1);
+  const int x1 = min(x0 + 1, w - 1), y1 = min(y0 + 1, h - 1);
+  const float wx = xi - x0, wy = yi - y0;
+  const float2* f = (const float2*)flow + (long)b * h * w;
+  const float2 a = f[y0 * w + x0], c = f[y0 * w + x1], d = f[y1 * w + x0], e = f[y1 * w + x1];
+  const float top_x = a.x + wx * (c.x - a.x), top_y = a.y + wx * (c.y - a.y);
+  const float bot_x = d.x + wx * (e.x - d.x), bot_y = d.y + wx * (e.y - d.y);
+  ((float2*)out)[idx] = make_float2(8.f * (top_x + wy * (bot_x - top_x)), 8.f * (top_y + wy * (bot_y - top_y)));
+}
+
+// stats[n][c][0..1] += sum / sumsq.  blockDim 256; C/8 threads per row.
+__global__ __launch_bounds__(256) void channel_stats_kernel(const bf16* __restrict__ x, int HW, int C, int rows_per_block,
+                                                            float* __restrict__ stats) {
+  __shared__ float red[256][17];
+  const int n = blockIdx.y;
+  const int cg = C >> 3;
+  const int tid = threadIdx.x;
+  const int g = tid % cg;
+  const int rg = tid / cg;
+  const int nrg = 256 / cg;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(r0 + rows_per_block, HW);
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
+  if (rg < nrg) {
+    const bf16* base = x + (long)n * HW * C + g * 8;
+    for (int r = r0 + rg; r < r1; r += nrg) {
+      const bf16x8 v = *(const bf16x8*)(base + (long)r * C);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = bf2f(v[j]);
+        s[j] += f;
+        q[j] += f * f;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[tid][j] = s[j]; red[tid][8 + j] = q[j]; }
+  __syncthreads();
+  // reduce over row-groups: thread t < cg*16 handles (group t%cg, value t/cg)
+  for (int t = tid; t < cg * 16; t += 256) {
+    const int gg = t % cg, vi = t / cg;
+    float acc = 0.f;
+    for (int k = 0; k < nrg; ++k) acc += red[k * cg + gg][vi];
+    const int c = gg * 8 + (vi & 7);
+    atomicAdd(&stats[((long)n * C + c) * 2 + (vi >> 3)], acc);
+  }
+}
+
+// y = act(xn + rn): 8 channels per thread
+__global__ void norm_act_kernel(const bf16* __restrict__ x, const float* __restrict__ sx, int mode_x,
+                                const float* __restrict__ gx, const float* __restrict__ bx,
+                                const bf16* __restrict__ r, const float* __restrict__ sr, int mode_r,
+                                const float* __restrict__ gr, const float* __restrict__ br, bf16* __restrict__ y,
+                                int N, int HW, int C, float eps, int relu) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cg = C >> 3;
+  const long total = (long)N * HW * cg;
+  if (idx >= total) return;
+  const int g = idx % cg;
+  const long pix = idx / cg;
+  const int n = pix / HW;
+  const int c0 = g * 8;
+  auto norm8 = [&](const bf16* src, const float* st, int mode, const float* gam, const float* bet, float* o) {
+    const bf16x8 v = *(const bf16x8*)(src + pix * C + c0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float f = bf2f(v[j]);
+      const int c = c0 + j;
+      if (mode == 1) {
+        const float inv = 1.0f / (float)HW;
+        const float m = st[((long)n * C + c) * 2] * inv;
+        const float var = fmaxf(st[((long)n * C + c) * 2 + 1] * inv - m * m, 0.f);
+        f = (f - m) * rsqrtf(var + eps);
+      } else if (mode == 2) {
+        float s0 = 0.f, s1 = 0.f;
+        for (int k = 0; k < N; ++k) { s0 += st[((long)k * C + c) * 2]; s1 += st[((long)k * C + c) * 2 + 1]; }
+        const float inv = 1.0f / ((float)HW * (float)N);
+        const float m = s0 * inv;
+        const float var = fmaxf(s1 * inv - m * m, 0.f);
+        f = (f - m) * rsqrtf(var + eps);
+      }
+      if (gam) f *= gam[c];
+      if (bet) f += bet[c];
+      o[j] = f;
+    }
+  };
+  float a[8];
+  norm8(x, sx, mode_x, gx, bx, a);
+  if (relu & 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = fmaxf(a[j], 0.f);
+  }
+  if (r) {
+    float b[8];
+    norm8(r, sr, mode_r, gr, br, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += b[j];
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f2bf((relu & 2) ? fmaxf(a[j], 0.f) : a[j]);
+  *(bf16x8*)(y + pix * C + c0) = o;
+}
+
+__global__ void prep_images_kernel(const float* __restrict__ i1, const float* __restrict__ i2, int B, long HW,
+                                   bf16* __restrict__ out) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = 2L * B * HW;
+  if (idx >= total) return;
+  const long half = (long)B * HW;
+  const float* src = idx < half ? i1 + idx * 3 : i2 + (idx - half) * 3;
+  bf16x8 o;
+  o[0] = f2bf(src[0]); o[1] = f2bf(src[1]); o[2] = f2bf(src[2]);
+#pragma unroll
+  for (int j = 3; j < 8; ++j) o[j] = f2bf(0.f);
+  *(bf16x8*)(out + idx * 8) = o;
+}
+
+__global__ void init_coords_kernel(float* __restrict__ coords, int B, int h, int w) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)B * h * w;
+  if (idx >= total) return;
+  const int rem = idx % (h * w);
+  coords[2 * idx] = (float)(rem % w);
+  coords[2 * idx + 1] = (float)(rem / w);
+}
+
+__global__ void copy_channels_kernel(const bf16* __restrict__ src, int scs, int soff, bf16* __restrict__ dst, int dcs,
+                                     int doff, int M, int C) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)M * C;
+  if (idx >= total) return;
+  const long m = idx / C;
+  const int c = idx - m * C;
+  dst[m * dcs + doff + c] = src[m * scs + soff + c];
+}
+
+inline unsigned nblk(long total, int bs) { return (unsigned)((total + bs - 1) / bs); }
+
+}  // namespace
+
+extern "C" int jr_upsample_convex(const void* mask, int mask_cstride, const float* flow, int B, int h, int w,
+                                  float* out, hipStream_t stream) {
+  const int total = B * h * w;
+  hipLaunchKernelGGL(upsample_convex_kernel, dim3((total + 3) / 4), dim3(256), 0, stream, (const bf16*)mask,
+                     mask_cstride, flow, B, h, w, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jr_upsample_bilinear(const float* flow, int B, int h, int w, float* out, hipStream_t stream) {
+  const long total = (long)B * 64 * h * w;
+  hipLaunchKernelGGL(upsample_bilinear_kernel, dim3(nblk(total, 256)), dim3(256), 0, stream, flow, B, h, w, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jr_channel_stats(const void* x, int N, int HW, int C, float* stats, hipStream_t stream) {
+  if (C % 8 != 0 || C > 2048 || (C / 8) > 256) return (int)hipErrorInvalidValue;
+  const int rows_per_block = 1024;
+  dim3 grid((HW + rows_per_block - 1) / rows_per_block, N);
+  hipLaunchKernelGGL(channel_stats_kernel, grid, dim3(256), 0, stream, (const bf16*)x, HW, C, rows_per_block, stats);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jr_norm_act(const void* x, const float* sx, int mode_x, const float* gamma, const float* beta,
+                           const void* res, const float* sr, int mode_r, const float* gamma_r, const float* beta_r,
+                           void* y, int N, int HW, int C, float eps, int relu, hipStream_t stream) {
+  if (C % 8 != 0) return (int)hipErrorInvalidValue;
+  const long total = (long)N * HW * (C / 8);
+  hipLaunchKernelGGL(norm_act_kernel, dim3(nblk(total, 256)), dim3(256), 0, stream, (const bf16*)x, sx, mode_x, gamma,
+                     beta, (const bf16*)res, sr, mode_r, gamma_r, beta_r, (bf16*)y, N, HW, C, eps, relu);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jr_prep_images(const float* img1, const float* img2, int B, int H, int W, void* out,
+                              hipStream_t stream) {
+  const long total = 2L * B * H * W;
+  hipLaunchKernelGGL(prep_images_kernel, dim3(nblk(total, 256)), dim3(256), 0, stream, img1, img2, B, (long)H * W,
+                     (bf16*)out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jr_init_coords(float* coords, int B, int h, int w, hipStream_t stream) {
+  const long total = (long)B * h * w;
+  hipLaunchKernelGGL(init_coords_kernel, dim3(nblk(total, 256)), dim3(256), 0, stream, coords, B, h, w);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jr_copy_channels(const void* src, int s_cstride, int s_coff, void* dst, int d_cstride, int d_coff,
+                                int M, int C, hipStream_t stream) {
+  const long total = (long)M * C;
+  hipLaunchKernelGGL(copy_channels_kernel, dim3(nblk(total, 256)), dim3(256), 0, stream, (const bf16*)src, s_cstride,
+                     s_coff, (bf16*)dst, d_cstride, d_coff, M, C);
+  return (int)hipGetLastError();
+}

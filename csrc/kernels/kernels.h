@@ -1,0 +1,103 @@
+// Host-visible launcher API of the jax_raft_amd HIP kernels (gfx950 only).
+// Every launcher is capture-safe: no allocation, no synchronisation, only
+// kernel launches on the given stream.  Returns a hipError_t as int.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+extern "C" {
+
+// ---------------------------------------------------------------------------
+// Implicit-GEMM NHWC convolution (MFMA bf16, fp32 accumulate) with fused
+// epilogues.  GEMM view: D[co][pixel] = W[co][k] * im2col(X)[pixel][k],
+// k = (kh, kw, cin8-chunk) flattened, cin padded to a multiple of 8.
+// ---------------------------------------------------------------------------
+enum ConvEpi : int {
+  EPI_STD = 0,    // bias (+residual) -> act -> *alpha -> store (bf16|fp32) (+copy)
+  EPI_GRU_A = 1,  // channels [0,Hd): z = sigmoid -> zbuf ; [Hd,2Hd): r = sigmoid -> rh = r*h32 -> y
+  EPI_GRU_B = 2,  // q = tanh ; h = (1-z) h + z q -> h32, y (bf16 copy of h), y2 (second copy)
+  EPI_FLOW = 3,   // delta = acc+bias (2 ch): coords += delta ; flow = coords - coords0 -> flow32, y/y2 (bf16)
+};
+
+struct ConvParams {
+  // input activation (bf16 NHWC with channel stride/offset)
+  const void* x;
+  int N, H, W;
+  int x_cstride, x_coff;
+  int cin8;         // input channels used for K, multiple of 8
+  int KH, KW, SH, SW, PH, PW;
+  int OH, OW;
+  int M;            // N*OH*OW
+  // packed weights [cout_pad][kpad] bf16 and fp32 bias [cout]
+  const void* w;
+  int kpad;         // multiple of 64
+  int nkc;          // KH*KW*cin8/8 valid 8-chunks
+  int cout;         // real output channels
+  int cout_pad;     // rows present in w (multiple of 16)
+  const float* bias;
+  float alpha;
+  int act;
+  int split;        // ACT_SPLIT_TANH_RELU threshold channel
+  // primary output
+  void* y; int y_cstride, y_coff; int y_fp32;
+  // optional second bf16 output copy (same channels)
+  void* y2; int y2_cstride, y2_coff;
+  // optional residual (bf16), added before the activation
+  const void* res; int res_cstride, res_coff;
+  int res_post;     // 0: act(v + res) ; 1: relu(act(v) + res)  (ResidualBlock tail, model.py:184)
+  // fused-epilogue extras
+  float* h32;       // GRU: fp32 hidden state [M][hidden]
+  void* zbuf;       // GRU: z gate (bf16) [M][hidden]
+  int hidden;
+  float* coords;    // FLOW: fp32 [M][2]
+  float* flow32;    // FLOW: fp32 [M][2]
+  void* y3; int y3_cstride, y3_coff;  // FLOW: third bf16 flow copy
+};
+
+// cfg: 0 = 128co x 128px, 1 = 64co x 128px, 2 = 128co x 64px, 3 = 16co x 256px, 4 = 64co x 64px
+int jr_conv_forward(const ConvParams* p, int cfg, int epi, hipStream_t stream);
+
+// ---------------------------------------------------------------------------
+// Instance/batch-norm statistics and normalisation.
+// ---------------------------------------------------------------------------
+// stats[n][c][2] += (sum, sumsq) over pixels of x (bf16 NHWC, C channels, contiguous).
+int jr_channel_stats(const void* x, int N, int HW, int C, float* stats, hipStream_t stream);
+// y = post( pre(xn) + rn ), xn = (x - mean_x) * rstd_x * gamma + beta (mode_x), rn likewise for res.
+// mode: 0 = identity, 1 = instance (stats per n), 2 = batch (stats summed over n).
+// relu bit 0: relu on xn before the residual add; bit 1: relu on the sum.
+int jr_norm_act(const void* x, const float* sx, int mode_x, const float* gamma, const float* beta,
+                const void* res, const float* sr, int mode_r, const float* gamma_r, const float* beta_r,
+                void* y, int N, int HW, int C, float eps, int relu, hipStream_t stream);
+
+// ---------------------------------------------------------------------------
+// Correlation pyramid (MFMA all-pairs GEMM, pooling fused) and lookup.
+// ---------------------------------------------------------------------------
+// f1, f2: bf16 [B][h*w][C] (channel stride cs).  levels[l]: fp32 [B][h*w][h_l][w_l].
+int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int w, int C, int cs,
+                    float* lvl0, float* lvl1, float* lvl2, float* lvl3, int num_levels, float scale,
+                    hipStream_t stream);
+// coords fp32 [B][h*w][2]; out bf16 [B*h*w][out_cstride] channels l*(2r+1)^2 + i*(2r+1) + j,
+// zero-filled up to out_cstride.
+int jr_corr_lookup(const float* const* levels, int num_levels, int B, int h, int w, int radius,
+                   const float* coords, void* out, int out_cstride, hipStream_t stream);
+
+// ---------------------------------------------------------------------------
+// Flow upsampling x8.
+// ---------------------------------------------------------------------------
+// mask bf16 [B*h*w][576] (already scaled), flow fp32 [B*h*w][2] -> out fp32 [B][8h][8w][2]
+int jr_upsample_convex(const void* mask, int mask_cstride, const float* flow, int B, int h, int w,
+                       float* out, hipStream_t stream);
+int jr_upsample_bilinear(const float* flow, int B, int h, int w, float* out, hipStream_t stream);
+
+// ---------------------------------------------------------------------------
+// Misc.
+// ---------------------------------------------------------------------------
+// img1,img2 fp32 NHWC [B][H][W][3] -> bf16 [2B][H][W][8] (img1 batch first), channels 3..7 = 0.
+int jr_prep_images(const float* img1, const float* img2, int B, int H, int W, void* out, hipStream_t stream);
+// coords[b][y][x] = (x, y); flow32 = 0
+int jr_init_coords(float* coords, int B, int h, int w, hipStream_t stream);
+// copy bf16 channel slice: dst[m][doff + c] = src[m][soff + c], c < C
+int jr_copy_channels(const void* src, int s_cstride, int s_coff, void* dst, int d_cstride, int d_coff,
+                     int M, int C, hipStream_t stream);
+
+}  // extern "C"

@@ -1,0 +1,460 @@
+// jax_raft_amd native runtime: TORCH_LIBRARY ops over the gfx950 kernels and
+// a plan executor with hipGraph capture.
+//
+// The reference has no native code; XLA emits its kernels
+// and runs the refinement loop as a device while-loop (jax_raft/model.py:589-603,
+// nn.scan).  Here the equivalent runtime is explicit:
+//   * every kernel is reachable as an eager op (torch.ops.jax_raft_amd.*),
+//     used by the autograd/unfused path and by the tests;
+//   * a `Plan` records launch closures (prologue / loop body / epilogue) once,
+//     with all pointers, shapes and tile configs resolved, and either launches
+//     them straight from C++ (no per-op Python overhead) or captures the whole
+//     N-iteration forward into one hipGraph and replays it.
+#include <torch/custom_class.h>
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include <functional>
+#include <vector>
+
+#include "../kernels/kernels.h"
+
+namespace jr {
+
+using TList = c10::List<c10::optional<at::Tensor>>;
+using IList = std::vector<int64_t>;
+using Launch = std::function<int(hipStream_t, int)>;
+
+static inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+static inline at::Tensor opt(const TList& t, size_t i) {
+  if (i >= t.size()) return at::Tensor();
+  c10::optional<at::Tensor> v = t.get(i);
+  return v.has_value() ? *v : at::Tensor();
+}
+static inline void* ptr(const at::Tensor& t) { return t.defined() ? t.data_ptr() : nullptr; }
+static inline int cs(const at::Tensor& t) { return t.defined() ? (int)t.size(-1) : 0; }
+
+#define JR_CHECK_OK(expr)                                                                 \
+  do {                                                                                    \
+    int e__ = (expr);                                                                     \
+    TORCH_CHECK(e__ == 0, "jax_raft_amd kernel launch failed: ", hipGetErrorString((hipError_t)e__)); \
+  } while (0)
+
+static void check_bf16(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.defined(), name, " must be defined");
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+static void check_f32(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.defined(), name, " must be defined");
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+// ----------------------------------------------------------------------- conv
+// t = [x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3]
+// i = [N, H, W, x_coff, cin8, KH, KW, SH, SW, PH, PW, cout, act, split,
+//      y_coff, y2_coff, res_coff, hidden, y3_coff, epi, cfg, res_post]
+static Launch make_conv(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep) {
+  TORCH_CHECK(i.size() == 22, "conv: expected 22 ints");
+  at::Tensor x = opt(t, 0), w = opt(t, 1), bias = opt(t, 2), y = opt(t, 3), y2 = opt(t, 4), res = opt(t, 5);
+  at::Tensor h32 = opt(t, 6), zbuf = opt(t, 7), coords = opt(t, 8), flow32 = opt(t, 9), y3 = opt(t, 10);
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_f32(bias, "bias");
+  TORCH_CHECK(y.defined() && y.is_contiguous(), "y");
+  ConvParams p{};
+  p.x = x.data_ptr();
+  p.N = (int)i[0]; p.H = (int)i[1]; p.W = (int)i[2];
+  p.x_cstride = cs(x); p.x_coff = (int)i[3]; p.cin8 = (int)i[4];
+  p.KH = (int)i[5]; p.KW = (int)i[6]; p.SH = (int)i[7]; p.SW = (int)i[8]; p.PH = (int)i[9]; p.PW = (int)i[10];
+  p.OH = (p.H + 2 * p.PH - p.KH) / p.SH + 1;
+  p.OW = (p.W + 2 * p.PW - p.KW) / p.SW + 1;
+  p.M = p.N * p.OH * p.OW;
+  p.w = w.data_ptr(); p.kpad = (int)w.size(1); p.cout_pad = (int)w.size(0);
+  p.nkc = p.KH * p.KW * p.cin8 / 8;
+  p.cout = (int)i[11]; p.bias = bias.data_ptr<float>(); p.alpha = (float)alpha;
+  p.act = (int)i[12]; p.split = (int)i[13];
+  p.y = y.data_ptr(); p.y_cstride = cs(y); p.y_coff = (int)i[14]; p.y_fp32 = y.scalar_type() == at::kFloat;
+  p.y2 = ptr(y2); p.y2_cstride = cs(y2); p.y2_coff = (int)i[15];
+  p.res = ptr(res); p.res_cstride = cs(res); p.res_coff = (int)i[16]; p.res_post = (int)i[21];
+  p.h32 = h32.defined() ? h32.data_ptr<float>() : nullptr; p.hidden = (int)i[17];
+  p.zbuf = ptr(zbuf);
+  p.coords = coords.defined() ? coords.data_ptr<float>() : nullptr;
+  p.flow32 = flow32.defined() ? flow32.data_ptr<float>() : nullptr;
+  p.y3 = ptr(y3); p.y3_cstride = cs(y3); p.y3_coff = (int)i[18];
+  const int epi = (int)i[19], cfg = (int)i[20];
+  // Shape / alignment contract of conv_igemm.hip.
+  TORCH_CHECK(p.cin8 % 8 == 0 && p.cin8 > 0, "conv: cin8 must be a positive multiple of 8");
+  TORCH_CHECK(p.x_cstride % 8 == 0 && p.x_coff % 8 == 0 && p.x_coff + p.cin8 <= p.x_cstride,
+              "conv: input channel slice must be 8-aligned and inside the tensor");
+  TORCH_CHECK((int64_t)p.N * p.H * p.W * p.x_cstride <= x.numel(), "conv: input tensor too small");
+  TORCH_CHECK(p.kpad % 64 == 0 && p.kpad >= p.KH * p.KW * p.cin8, "conv: packed weight K mismatch");
+  TORCH_CHECK(p.cout_pad % 16 == 0 && p.cout_pad >= p.cout && bias.numel() >= p.cout, "conv: packed weight rows");
+  TORCH_CHECK(p.OH > 0 && p.OW > 0, "conv: empty output");
+  TORCH_CHECK(p.y_cstride % 8 == 0, "conv: output channel stride must be a multiple of 8");
+  TORCH_CHECK((int64_t)p.M * p.y_cstride <= y.numel(), "conv: output tensor too small");
+  if (epi == EPI_STD) {
+    TORCH_CHECK(p.y_coff % 8 == 0 && p.y_coff + p.cout <= p.y_cstride, "conv: output slice");
+    TORCH_CHECK(y.scalar_type() == at::kBFloat16 || y.scalar_type() == at::kFloat, "conv: output dtype");
+    if (y2.defined()) { check_bf16(y2, "y2"); TORCH_CHECK(p.y2_cstride % 8 == 0 && p.y2_coff % 8 == 0, "y2 align"); }
+    if (res.defined()) { check_bf16(res, "res"); TORCH_CHECK(p.res_cstride % 8 == 0 && p.res_coff % 8 == 0, "res align"); }
+    if (h32.defined()) { check_f32(h32, "h32"); TORCH_CHECK(h32.numel() >= (int64_t)p.M * p.hidden, "h32 size"); }
+  } else if (epi == EPI_GRU_A) {
+    check_f32(h32, "h32"); check_f32(zbuf, "zbuf"); check_bf16(y, "y");
+    TORCH_CHECK(p.cout == 2 * p.hidden && p.hidden % 16 == 0, "GRU-A: cout must be 2*hidden, hidden % 16 == 0");
+    TORCH_CHECK(p.y_coff % 8 == 0, "GRU-A align");
+  } else if (epi == EPI_GRU_B) {
+    check_f32(h32, "h32"); check_f32(zbuf, "zbuf"); check_bf16(y, "y");
+    TORCH_CHECK(p.cout == p.hidden && p.hidden % 16 == 0, "GRU-B: cout must be hidden");
+    TORCH_CHECK(p.y_coff % 8 == 0, "GRU-B align");
+    if (y2.defined()) { check_bf16(y2, "y2"); TORCH_CHECK(p.y2_coff % 8 == 0, "y2 align"); }
+  } else if (epi == EPI_FLOW) {
+    check_f32(coords, "coords"); check_f32(flow32, "flow32"); check_bf16(y, "y");
+    TORCH_CHECK(p.cout == 2, "FLOW: cout must be 2");
+  } else {
+    TORCH_CHECK(false, "conv: unknown epilogue ", epi);
+  }
+  TORCH_CHECK(cfg >= 0 && cfg <= 4, "conv: unknown tile config ", cfg);
+  if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3}) if (v.defined()) keep->push_back(v);
+  return [p, epi, cfg](hipStream_t s, int) { return jr_conv_forward(&p, cfg, epi, s); };
+}
+
+// --------------------------------------------------------------- correlation
+// t = [f1, f2, l0, l1, l2, l3], i = [B, h, w, C, num_levels]
+static Launch make_corr(const TList& t, const IList& i, double scale, std::vector<at::Tensor>* keep) {
+  at::Tensor f1 = opt(t, 0), f2 = opt(t, 1);
+  check_bf16(f1, "f1"); check_bf16(f2, "f2");
+  const int B = (int)i[0], h = (int)i[1], w = (int)i[2], C = (int)i[3], L = (int)i[4];
+  TORCH_CHECK(L >= 1 && L <= 4, "corr: 1..4 levels");
+  TORCH_CHECK(C % 64 == 0, "corr: feature channels must be a multiple of 64");
+  TORCH_CHECK(f1.numel() >= (int64_t)B * h * w * cs(f1) && f2.numel() == f1.numel() && cs(f1) == cs(f2), "corr: fmap shapes");
+  float* lv[4] = {nullptr, nullptr, nullptr, nullptr};
+  int hl = h, wl = w;
+  for (int l = 0; l < L; ++l) {
+    at::Tensor v = opt(t, 2 + l);
+    check_f32(v, "level");
+    TORCH_CHECK(v.numel() >= (int64_t)B * h * w * hl * wl, "corr: level ", l, " too small");
+    lv[l] = v.data_ptr<float>();
+    if (keep) keep->push_back(v);
+    hl >>= 1; wl >>= 1;
+  }
+  if (keep) { keep->push_back(f1); keep->push_back(f2); }
+  const void* a = f1.data_ptr();
+  const void* b = f2.data_ptr();
+  const int fcs = cs(f1);
+  const float sc = (float)scale;
+  return [=](hipStream_t s, int) { return jr_corr_pyramid(a, b, B, h, w, C, fcs, lv[0], lv[1], lv[2], lv[3], L, sc, s); };
+}
+
+// t = [coords, out, l0, l1, l2, l3], i = [num_levels, B, h, w, radius]
+static Launch make_lookup(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor coords = opt(t, 0), out = opt(t, 1);
+  check_f32(coords, "coords"); check_bf16(out, "out");
+  const int L = (int)i[0], B = (int)i[1], h = (int)i[2], w = (int)i[3], r = (int)i[4];
+  const int S = 2 * r + 1;
+  TORCH_CHECK(L >= 1 && L <= 4 && S + 1 <= 16, "lookup: levels / radius out of range");
+  TORCH_CHECK(cs(out) % 8 == 0 && cs(out) >= L * S * S, "lookup: output channel stride");
+  TORCH_CHECK(out.numel() >= (int64_t)B * h * w * cs(out) && coords.numel() >= (int64_t)B * h * w * 2, "lookup: sizes");
+  std::vector<const float*> lv(4, nullptr);
+  int hl = h, wl = w;
+  for (int l = 0; l < L; ++l) {
+    at::Tensor v = opt(t, 2 + l);
+    check_f32(v, "level");
+    TORCH_CHECK(hl >= 2 && wl >= 2, "lookup: pyramid level too small");
+    TORCH_CHECK(v.numel() >= (int64_t)B * h * w * hl * wl, "lookup: level size");
+    lv[l] = v.data_ptr<float>();
+    if (keep) keep->push_back(v);
+    hl >>= 1; wl >>= 1;
+  }
+  if (keep) { keep->push_back(coords); keep->push_back(out); }
+  const float* cp = coords.data_ptr<float>();
+  void* op = out.data_ptr();
+  const int ocs = cs(out);
+  return [=](hipStream_t s, int) { return jr_corr_lookup(lv.data(), L, B, h, w, r, cp, op, ocs, s); };
+}
+
+// ------------------------------------------------------------------ upsample
+// t = [mask, flow, out], i = [B, h, w, out_iter_stride]
+static Launch make_upsample_convex(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor mask = opt(t, 0), flow = opt(t, 1), out = opt(t, 2);
+  check_bf16(mask, "mask"); check_f32(flow, "flow"); check_f32(out, "out");
+  const int B = (int)i[0], h = (int)i[1], w = (int)i[2];
+  const int64_t stride = i[3];
+  TORCH_CHECK(cs(mask) >= 576, "upsample: mask needs 576 channels");
+  TORCH_CHECK(out.numel() >= (int64_t)B * 64 * h * w * 2, "upsample: output too small");
+  if (keep) { keep->push_back(mask); keep->push_back(flow); keep->push_back(out); }
+  const void* mp = mask.data_ptr();
+  const float* fp = flow.data_ptr<float>();
+  float* op = out.data_ptr<float>();
+  const int64_t cap = out.numel();
+  const int mcs = cs(mask);
+  return [=](hipStream_t s, int it) {
+    const int64_t off = stride * it;
+    if (off + (int64_t)B * 64 * h * w * 2 > cap) return (int)hipErrorInvalidValue;
+    return jr_upsample_convex(mp, mcs, fp, B, h, w, op + off, s);
+  };
+}
+
+// t = [flow, out], i = [B, h, w, out_iter_stride]
+static Launch make_upsample_bilinear(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor flow = opt(t, 0), out = opt(t, 1);
+  check_f32(flow, "flow"); check_f32(out, "out");
+  const int B = (int)i[0], h = (int)i[1], w = (int)i[2];
+  const int64_t stride = i[3];
+  TORCH_CHECK(out.numel() >= (int64_t)B * 64 * h * w * 2, "upsample: output too small");
+  if (keep) { keep->push_back(flow); keep->push_back(out); }
+  const float* fp = flow.data_ptr<float>();
+  float* op = out.data_ptr<float>();
+  const int64_t cap = out.numel();
+  return [=](hipStream_t s, int it) {
+    const int64_t off = stride * it;
+    if (off + (int64_t)B * 64 * h * w * 2 > cap) return (int)hipErrorInvalidValue;
+    return jr_upsample_bilinear(fp, B, h, w, op + off, s);
+  };
+}
+
+// ---------------------------------------------------------------------- norm
+// t = [x, stats], i = [N, HW, C]
+static Launch make_stats(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor x = opt(t, 0), st = opt(t, 1);
+  check_bf16(x, "x"); check_f32(st, "stats");
+  const int N = (int)i[0], HW = (int)i[1], C = (int)i[2];
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && cs(x) == C && x.numel() >= (int64_t)N * HW * C, "stats: shape");
+  TORCH_CHECK(st.numel() >= (int64_t)N * C * 2, "stats: buffer too small");
+  if (keep) { keep->push_back(x); keep->push_back(st); }
+  const void* xp = x.data_ptr();
+  float* sp = st.data_ptr<float>();
+  const size_t bytes = (size_t)N * C * 2 * sizeof(float);
+  return [=](hipStream_t s, int) {
+    hipError_t e = hipMemsetAsync(sp, 0, bytes, s);
+    if (e != hipSuccess) return (int)e;
+    return jr_channel_stats(xp, N, HW, C, sp, s);
+  };
+}
+
+// t = [x, sx, gx, bx, r, sr, gr, br, y], i = [mode_x, mode_r, N, HW, C, relu]
+static Launch make_norm_act(const TList& t, const IList& i, double eps, std::vector<at::Tensor>* keep) {
+  at::Tensor x = opt(t, 0), sx = opt(t, 1), gx = opt(t, 2), bx = opt(t, 3);
+  at::Tensor r = opt(t, 4), sr = opt(t, 5), gr = opt(t, 6), br = opt(t, 7), y = opt(t, 8);
+  check_bf16(x, "x"); check_bf16(y, "y");
+  const int mx = (int)i[0], mr = (int)i[1], N = (int)i[2], HW = (int)i[3], C = (int)i[4], relu = (int)i[5];
+  TORCH_CHECK(C % 8 == 0 && cs(x) == C && cs(y) == C && x.numel() >= (int64_t)N * HW * C && y.numel() >= (int64_t)N * HW * C,
+              "norm_act: shape");
+  if (mx) check_f32(sx, "sx");
+  if (r.defined()) { check_bf16(r, "res"); TORCH_CHECK(cs(r) == C, "norm_act: residual channels"); if (mr) check_f32(sr, "sr"); }
+  for (auto* v : {&gx, &bx, &gr, &br}) if (v->defined()) check_f32(*v, "affine");
+  if (keep) for (auto& v : {x, sx, gx, bx, r, sr, gr, br, y}) if (v.defined()) keep->push_back(v);
+  auto fp = [](const at::Tensor& v) -> const float* { return v.defined() ? v.data_ptr<float>() : nullptr; };
+  const void* xp = x.data_ptr();
+  const void* rp = ptr(r);
+  void* yp = y.data_ptr();
+  const float *sxp = fp(sx), *gxp = fp(gx), *bxp = fp(bx), *srp = fp(sr), *grp = fp(gr), *brp = fp(br);
+  const float e = (float)eps;
+  return [=](hipStream_t s, int) {
+    return jr_norm_act(xp, sxp, mx, gxp, bxp, rp, srp, mr, grp, brp, yp, N, HW, C, e, relu, s);
+  };
+}
+
+// ---------------------------------------------------------------------- misc
+// t = [img1, img2, out], i = [B, H, W]
+static Launch make_prep(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor a = opt(t, 0), b = opt(t, 1), out = opt(t, 2);
+  check_f32(a, "img1"); check_f32(b, "img2"); check_bf16(out, "out");
+  const int B = (int)i[0], H = (int)i[1], W = (int)i[2];
+  TORCH_CHECK(a.numel() == (int64_t)B * H * W * 3 && b.numel() == a.numel(), "prep: image shape");
+  TORCH_CHECK(out.numel() >= 2LL * B * H * W * 8 && cs(out) == 8, "prep: output");
+  if (keep) { keep->push_back(a); keep->push_back(b); keep->push_back(out); }
+  const float* ap = a.data_ptr<float>();
+  const float* bp = b.data_ptr<float>();
+  void* op = out.data_ptr();
+  return [=](hipStream_t s, int) { return jr_prep_images(ap, bp, B, H, W, op, s); };
+}
+
+// t = [coords], i = [B, h, w]
+static Launch make_init_coords(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor c = opt(t, 0);
+  check_f32(c, "coords");
+  const int B = (int)i[0], h = (int)i[1], w = (int)i[2];
+  TORCH_CHECK(c.numel() >= (int64_t)B * h * w * 2, "init_coords: size");
+  if (keep) keep->push_back(c);
+  float* cp = c.data_ptr<float>();
+  return [=](hipStream_t s, int) { return jr_init_coords(cp, B, h, w, s); };
+}
+
+// t = [x]
+static Launch make_memset(const TList& t, std::vector<at::Tensor>* keep) {
+  at::Tensor x = opt(t, 0);
+  TORCH_CHECK(x.defined() && x.is_cuda() && x.is_contiguous(), "memset: tensor");
+  if (keep) keep->push_back(x);
+  void* p = x.data_ptr();
+  const size_t bytes = x.numel() * x.element_size();
+  return [=](hipStream_t s, int) { return (int)hipMemsetAsync(p, 0, bytes, s); };
+}
+
+// t = [src, dst]
+static Launch make_copy(const TList& t, std::vector<at::Tensor>* keep) {
+  at::Tensor a = opt(t, 0), b = opt(t, 1);
+  TORCH_CHECK(a.defined() && b.defined() && a.is_contiguous() && b.is_contiguous(), "copy: tensors");
+  TORCH_CHECK(a.numel() * a.element_size() == b.numel() * b.element_size(), "copy: byte size mismatch");
+  if (keep) { keep->push_back(a); keep->push_back(b); }
+  const void* ap = a.data_ptr();
+  void* bp = b.data_ptr();
+  const size_t bytes = a.numel() * a.element_size();
+  return [=](hipStream_t s, int) { return (int)hipMemcpyAsync(bp, ap, bytes, hipMemcpyDeviceToDevice, s); };
+}
+
+// t = [src, dst], i = [s_coff, d_coff, M, C]
+static Launch make_copy_channels(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor a = opt(t, 0), b = opt(t, 1);
+  check_bf16(a, "src"); check_bf16(b, "dst");
+  const int so = (int)i[0], dof = (int)i[1], M = (int)i[2], C = (int)i[3];
+  TORCH_CHECK(so + C <= cs(a) && dof + C <= cs(b) && a.numel() >= (int64_t)M * cs(a) && b.numel() >= (int64_t)M * cs(b),
+              "copy_channels: shape");
+  if (keep) { keep->push_back(a); keep->push_back(b); }
+  const void* ap = a.data_ptr();
+  void* bp = b.data_ptr();
+  const int acs = cs(a), bcs = cs(b);
+  return [=](hipStream_t s, int) { return jr_copy_channels(ap, acs, so, bp, bcs, dof, M, C, s); };
+}
+
+static void run_now(const Launch& l) { JR_CHECK_OK(l(cur_stream(), 0)); }
+
+// ---------------------------------------------------------------- eager ops
+void conv_op(const TList& t, IList i, double alpha) { run_now(make_conv(t, i, alpha, nullptr)); }
+void corr_op(const TList& t, IList i, double scale) { run_now(make_corr(t, i, scale, nullptr)); }
+void lookup_op(const TList& t, IList i) { run_now(make_lookup(t, i, nullptr)); }
+void upsample_convex_op(const TList& t, IList i) { run_now(make_upsample_convex(t, i, nullptr)); }
+void upsample_bilinear_op(const TList& t, IList i) { run_now(make_upsample_bilinear(t, i, nullptr)); }
+void stats_op(const TList& t, IList i) { run_now(make_stats(t, i, nullptr)); }
+void norm_act_op(const TList& t, IList i, double eps) { run_now(make_norm_act(t, i, eps, nullptr)); }
+void prep_op(const TList& t, IList i) { run_now(make_prep(t, i, nullptr)); }
+void init_coords_op(const TList& t, IList i) { run_now(make_init_coords(t, i, nullptr)); }
+void copy_channels_op(const TList& t, IList i) { run_now(make_copy_channels(t, i, nullptr)); }
+
+// --------------------------------------------------------------------- Plan
+class Plan : public torch::CustomClassHolder {
+ public:
+  Plan() = default;
+  ~Plan() override { reset_graph(); if (cap_stream_) (void)hipStreamDestroy(cap_stream_); }
+
+  void set_segment(int64_t s) {
+    TORCH_CHECK(s >= 0 && s <= 2, "segment must be 0 (prologue), 1 (loop) or 2 (epilogue)");
+    seg_ = (int)s;
+    reset_graph();
+  }
+  void add_conv(TList t, IList i, double alpha) { push(make_conv(t, i, alpha, &keep_), "conv"); }
+  void add_corr(TList t, IList i, double scale) { push(make_corr(t, i, scale, &keep_), "corr"); }
+  void add_lookup(TList t, IList i) { push(make_lookup(t, i, &keep_), "lookup"); }
+  void add_upsample_convex(TList t, IList i) { push(make_upsample_convex(t, i, &keep_), "upsample_convex"); }
+  void add_upsample_bilinear(TList t, IList i) { push(make_upsample_bilinear(t, i, &keep_), "upsample_bilinear"); }
+  void add_stats(TList t, IList i) { push(make_stats(t, i, &keep_), "stats"); }
+  void add_norm_act(TList t, IList i, double eps) { push(make_norm_act(t, i, eps, &keep_), "norm_act"); }
+  void add_prep(TList t, IList i) { push(make_prep(t, i, &keep_), "prep"); }
+  void add_init_coords(TList t, IList i) { push(make_init_coords(t, i, &keep_), "init_coords"); }
+  void add_memset(TList t) { push(make_memset(t, &keep_), "memset"); }
+  void add_copy(TList t) { push(make_copy(t, &keep_), "copy"); }
+  void add_copy_channels(TList t, IList i) { push(make_copy_channels(t, i, &keep_), "copy_channels"); }
+
+  int64_t num_ops(int64_t seg) const { return (int64_t)segs_[seg].size(); }
+  std::vector<std::string> op_names(int64_t seg) const { return names_[seg]; }
+
+  // Launch prologue, n_iters x loop body, epilogue on the current stream.
+  void run(int64_t n_iters) { JR_CHECK_OK(enqueue(cur_stream(), (int)n_iters)); }
+
+  // Capture the same sequence into one hipGraph (on a private stream: the
+  // legacy default stream cannot be captured) and instantiate it.
+  void capture(int64_t n_iters) {
+    reset_graph();
+    if (!cap_stream_) TORCH_CHECK(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking) == hipSuccess, "stream");
+    hipStream_t s = cap_stream_;
+    // order the capture after work already queued on the current stream
+    TORCH_CHECK(hipStreamSynchronize(cur_stream()) == hipSuccess, "sync");
+    TORCH_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess, "begin capture");
+    int err = enqueue(s, (int)n_iters);
+    hipGraph_t g = nullptr;
+    hipError_t e2 = hipStreamEndCapture(s, &g);
+    TORCH_CHECK(err == 0, "kernel launch failed during capture: ", hipGetErrorString((hipError_t)err));
+    TORCH_CHECK(e2 == hipSuccess && g != nullptr, "end capture failed: ", hipGetErrorString(e2));
+    graph_ = g;
+    hipError_t e3 = hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0);
+    TORCH_CHECK(e3 == hipSuccess, "graph instantiate failed: ", hipGetErrorString(e3));
+    captured_iters_ = n_iters;
+  }
+  int64_t captured_iters() const { return captured_iters_; }
+  void replay() {
+    TORCH_CHECK(exec_ != nullptr, "plan: no captured graph");
+    hipError_t e = hipGraphLaunch(exec_, cur_stream());
+    TORCH_CHECK(e == hipSuccess, "graph launch failed: ", hipGetErrorString(e));
+  }
+  void reset_graph() {
+    if (exec_) { (void)hipGraphExecDestroy(exec_); exec_ = nullptr; }
+    if (graph_) { (void)hipGraphDestroy(graph_); graph_ = nullptr; }
+    captured_iters_ = -1;
+  }
+
+ private:
+  void push(Launch l, const char* name) {
+    segs_[seg_].push_back(std::move(l));
+    names_[seg_].push_back(name);
+    reset_graph();
+  }
+  int enqueue(hipStream_t s, int n_iters) {
+    for (auto& l : segs_[0]) { int e = l(s, 0); if (e) return e; }
+    for (int it = 0; it < n_iters; ++it)
+      for (auto& l : segs_[1]) { int e = l(s, it); if (e) return e; }
+    for (auto& l : segs_[2]) { int e = l(s, n_iters); if (e) return e; }
+    return 0;
+  }
+  std::vector<Launch> segs_[3];
+  std::vector<std::string> names_[3];
+  std::vector<at::Tensor> keep_;
+  int seg_ = 0;
+  hipStream_t cap_stream_ = nullptr;
+  hipGraph_t graph_ = nullptr;
+  hipGraphExec_t exec_ = nullptr;
+  int64_t captured_iters_ = -1;
+};
+
+}  // namespace jr
+
+TORCH_LIBRARY(jax_raft_amd, m) {
+  m.def("conv(Tensor?[] t, int[] i, float alpha) -> ()", &jr::conv_op);
+  m.def("corr(Tensor?[] t, int[] i, float scale) -> ()", &jr::corr_op);
+  m.def("lookup(Tensor?[] t, int[] i) -> ()", &jr::lookup_op);
+  m.def("upsample_convex(Tensor?[] t, int[] i) -> ()", &jr::upsample_convex_op);
+  m.def("upsample_bilinear(Tensor?[] t, int[] i) -> ()", &jr::upsample_bilinear_op);
+  m.def("stats(Tensor?[] t, int[] i) -> ()", &jr::stats_op);
+  m.def("norm_act(Tensor?[] t, int[] i, float eps) -> ()", &jr::norm_act_op);
+  m.def("prep(Tensor?[] t, int[] i) -> ()", &jr::prep_op);
+  m.def("init_coords(Tensor?[] t, int[] i) -> ()", &jr::init_coords_op);
+  m.def("copy_channels(Tensor?[] t, int[] i) -> ()", &jr::copy_channels_op);
+  m.class_<jr::Plan>("Plan")
+      .def(torch::init<>())
+      .def("set_segment", &jr::Plan::set_segment)
+      .def("add_conv", &jr::Plan::add_conv)
+      .def("add_corr", &jr::Plan::add_corr)
+      .def("add_lookup", &jr::Plan::add_lookup)
+      .def("add_upsample_convex", &jr::Plan::add_upsample_convex)
+      .def("add_upsample_bilinear", &jr::Plan::add_upsample_bilinear)
+      .def("add_stats", &jr::Plan::add_stats)
+      .def("add_norm_act", &jr::Plan::add_norm_act)
+      .def("add_prep", &jr::Plan::add_prep)
+      .def("add_init_coords", &jr::Plan::add_init_coords)
+      .def("add_memset", &jr::Plan::add_memset)
+      .def("add_copy", &jr::Plan::add_copy)
+      .def("add_copy_channels", &jr::Plan::add_copy_channels)
+      .def("num_ops", &jr::Plan::num_ops)
+      .def("op_names", &jr::Plan::op_names)
+      .def("run", &jr::Plan::run)
+      .def("capture", &jr::Plan::capture)
+      .def("captured_iters", &jr::Plan::captured_iters)
+      .def("replay", &jr::Plan::replay)
+      .def("reset_graph", &jr::Plan::reset_graph);
+}

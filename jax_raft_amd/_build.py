@@ -1,0 +1,101 @@
+"""In-tree native build: hipcc --offload-arch=gfx950 -> jax_raft_amd/_C.so.
+
+No hipify, no torch JIT cache: every ``.hip`` kernel TU is compiled directly
+for gfx950 and linked with the TORCH_LIBRARY binding / plan runtime into one
+shared object that lives next to this file (so it ships with the repository
+snapshot to the GPU box and is visibly the library the tests load).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO = PKG_DIR.parent
+CSRC = REPO / "csrc"
+BUILD = REPO / "build" / "native"
+SO_PATH = PKG_DIR / "_C.so"
+ARCH = os.environ.get("JR_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CXX = os.environ.get("CXX", "g++")
+
+KERNEL_SOURCES = [
+    CSRC / "kernels" / "conv_igemm.hip",
+    CSRC / "kernels" / "corr.hip",
+    CSRC / "kernels" / "elementwise.hip",
+]
+HOST_SOURCES = [CSRC / "runtime" / "binding.cpp"]
+HEADERS = [CSRC / "kernels" / "common.h", CSRC / "kernels" / "kernels.h"]
+
+
+def _torch_paths():
+    import torch
+    from torch.utils import cpp_extension
+
+    inc = cpp_extension.include_paths(device_type="cuda")
+    lib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, lib, abi
+
+
+def _stale(obj: Path, src: Path) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    deps = [src] + HEADERS
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("native build failed:\n" + " ".join(map(str, cmd)) + "\n" + r.stdout)
+    return r.stdout
+
+
+def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -> Path:
+    """Compile all kernels + runtime for gfx950 and link ``_C.so``."""
+    BUILD.mkdir(parents=True, exist_ok=True)
+    inc, lib, abi = _torch_paths()
+    py_inc = sysconfig.get_paths()["include"]
+    common = ["-O3", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}"]
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    cmds = []
+    objs = []
+    for src in KERNEL_SOURCES:
+        obj = BUILD / (src.stem + ".o")
+        objs.append(obj)
+        if force or _stale(obj, src):
+            cmds.append([HIPCC, f"--offload-arch={ARCH}", *common, "-c", str(src), "-o", str(obj)])
+    for src in HOST_SOURCES:
+        obj = BUILD / (src.stem + ".o")
+        objs.append(obj)
+        if force or _stale(obj, src):
+            incs = [f"-I{p}" for p in inc] + [f"-I{py_inc}"]
+            cmds.append([CXX, *common, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_API_INCLUDE_EXTENSION_H",
+                         *incs, "-c", str(src), "-o", str(obj)])
+    if cmds:
+        with cf.ThreadPoolExecutor(jobs) as ex:
+            for out in ex.map(_run, cmds):
+                if verbose and out.strip():
+                    print(out)
+    need_link = force or not SO_PATH.exists() or any(o.stat().st_mtime > SO_PATH.stat().st_mtime for o in objs)
+    if need_link:
+        tmp = SO_PATH.with_suffix(".so.tmp")
+        link = [
+            HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp),
+            f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+            f"-Wl,-rpath,{lib}",
+        ]
+        _run(link)
+        os.replace(tmp, SO_PATH)
+    return SO_PATH
+
+
+if __name__ == "__main__":
+    p = build(force="--force" in sys.argv, verbose=True)
+    print(p)

@@ -1,0 +1,176 @@
+"""Loader and thin Python front-end for the gfx950 native library (``_C.so``).
+
+The library is built in-tree by :mod:`jax_raft_amd._build`.  On a GPU machine
+the native path is the only GPU implementation: if the library cannot be
+loaded, GPU execution fails loudly instead of silently falling back to
+PyTorch ops.
+"""
+from __future__ import annotations
+
+import math
+import os
+import threading
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from .._build import SO_PATH
+
+_lock = threading.Lock()
+_loaded = False
+_load_error: Optional[BaseException] = None
+
+# activation / epilogue codes (csrc/kernels/common.h, kernels.h)
+ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, ACT_SPLIT_TANH_RELU = 0, 1, 2, 3, 4
+EPI_STD, EPI_GRU_A, EPI_GRU_B, EPI_FLOW = 0, 1, 2, 3
+# tile configs of conv_igemm.hip: (BCO, BP)
+CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (16, 256), 4: (64, 64)}
+NUM_CUS = 256
+
+
+def load(build_if_missing: bool = True) -> None:
+    """Load ``_C.so`` (building it with hipcc first if it is missing)."""
+    global _loaded, _load_error
+    if _loaded:
+        return
+    with _lock:
+        if _loaded:
+            return
+        try:
+            if not SO_PATH.exists() and build_if_missing:
+                from .._build import build
+
+                build()
+            torch.ops.load_library(str(SO_PATH))
+            _loaded = True
+        except BaseException as e:  # pragma: no cover - reported by require()
+            _load_error = e
+            raise
+
+
+def available() -> bool:
+    try:
+        load(build_if_missing=False)
+        return True
+    except BaseException:
+        return False
+
+
+def require() -> None:
+    """Raise if the native library is not usable (GPU path must not fall back)."""
+    try:
+        load()
+    except BaseException as e:
+        raise RuntimeError(f"jax_raft_amd native library unavailable ({SO_PATH}): {e}") from e
+
+
+def ops():
+    require()
+    return torch.ops.jax_raft_amd
+
+
+def new_plan():
+    require()
+    return torch.classes.jax_raft_amd.Plan()
+
+
+def round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+# ------------------------------------------------------------------ conv specs
+
+
+@dataclass
+class ConvSpec:
+    """A packed convolution ready for the implicit-GEMM kernel.
+
+    ``w``: bf16 [cout_pad, kpad], K ordered (kh, kw, cin8) with the input
+    channels zero-padded to ``cin8``; ``b``: fp32 [cout]."""
+
+    w: torch.Tensor
+    b: torch.Tensor
+    kh: int
+    kw: int
+    sh: int
+    sw: int
+    ph: int
+    pw: int
+    cin: int
+    cin8: int
+    cout: int
+
+    def out_hw(self, H: int, W: int) -> Tuple[int, int]:
+        return (H + 2 * self.ph - self.kh) // self.sh + 1, (W + 2 * self.pw - self.kw) // self.sw + 1
+
+
+def pack_weight(kernel: torch.Tensor, cin8: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """HWIO fp32 kernel -> bf16 [cout_pad, kpad] (GEMM A operand)."""
+    kh, kw, cin, cout = kernel.shape
+    cin8 = cin8 or round_up(cin, 8)
+    kraw = kh * kw * cin8
+    kpad = round_up(kraw, 64)
+    cout_pad = round_up(cout, 16)
+    k = torch.zeros(kh, kw, cin8, cout, dtype=torch.float32, device=kernel.device)
+    k[:, :, :cin, :] = kernel.detach().float()
+    w = torch.zeros(cout_pad, kpad, dtype=torch.float32, device=kernel.device)
+    w[:cout, :kraw] = k.permute(3, 0, 1, 2).reshape(cout, kraw)
+    w = w.to(torch.bfloat16)
+    if out is not None:
+        assert out.shape == w.shape and out.dtype == torch.bfloat16
+        out.copy_(w)
+        return out
+    return w
+
+
+def make_spec(kernel: torch.Tensor, bias: torch.Tensor, stride=(1, 1), padding=(0, 0), cin8: Optional[int] = None,
+              device=None) -> ConvSpec:
+    kh, kw, cin, cout = kernel.shape
+    cin8 = cin8 or round_up(cin, 8)
+    w = pack_weight(kernel.to(device) if device is not None else kernel, cin8)
+    b = bias.detach().float().to(w.device).contiguous()
+    return ConvSpec(w, b, kh, kw, stride[0], stride[1], padding[0], padding[1], cin, cin8, cout)
+
+
+def pick_cfg(M: int, cout: int) -> int:
+    """Tile-config heuristic: minimise (waves of blocks) x (tile cost), where a
+    tile's per-FLOP cost rises as it shrinks; keeps >= one wave of blocks over
+    256 CUs whenever the problem allows."""
+    if cout <= 16:
+        return 3
+    best, best_cost = 0, None
+    # (cfg, relative per-FLOP efficiency of the tile); time ~ blocks per CU x tile area / eff
+    for cfg, eff in ((0, 1.0), (2, 0.85), (1, 0.85), (4, 0.65)):
+        bco, bp = CFG_TILES[cfg]
+        nb = math.ceil(M / bp) * math.ceil(cout / bco)
+        cost = math.ceil(nb / NUM_CUS) * (bco * bp) / eff
+        if best_cost is None or cost < best_cost - 1e-9:
+            best, best_cost = cfg, cost
+    return best
+
+
+def conv_args(spec: ConvSpec, x: torch.Tensor, N: int, H: int, W: int, y: torch.Tensor, *, x_coff: int = 0,
+              y_coff: int = 0, act: int = ACT_NONE, split: int = 0, alpha: float = 1.0, y2=None, y2_coff: int = 0,
+              res=None, res_coff: int = 0, res_post: int = 0, h32=None, zbuf=None, hidden: int = 0, coords=None,
+              flow32=None, y3=None, y3_coff: int = 0, epi: int = EPI_STD, cfg: Optional[int] = None):
+    """Build the (tensors, ints, alpha) argument triple of the ``conv`` op."""
+    OH, OW = spec.out_hw(H, W)
+    if cfg is None:
+        cfg = pick_cfg(N * OH * OW, spec.cout)
+    t = [x, spec.w, spec.b, y, y2, res, h32, zbuf, coords, flow32, y3]
+    i = [N, H, W, x_coff, spec.cin8, spec.kh, spec.kw, spec.sh, spec.sw, spec.ph, spec.pw, spec.cout, act, split,
+         y_coff, y2_coff, res_coff, hidden, y3_coff, epi, cfg, res_post]
+    return t, i, float(alpha)
+
+
+def conv2d(spec: ConvSpec, x: torch.Tensor, act: int = ACT_NONE, out_dtype=torch.bfloat16, alpha: float = 1.0,
+           res: Optional[torch.Tensor] = None, res_post: int = 0, cfg: Optional[int] = None) -> torch.Tensor:
+    """Eager NHWC conv of a contiguous bf16 tensor [N, H, W, C] (C == cin8)."""
+    N, H, W, C = x.shape
+    assert C == spec.cin8, f"input channels {C} != packed cin8 {spec.cin8}"
+    OH, OW = spec.out_hw(H, W)
+    y = torch.empty(N, OH, OW, round_up(spec.cout, 8), device=x.device, dtype=out_dtype)
+    t, i, a = conv_args(spec, x, N, H, W, y, act=act, alpha=alpha, res=res, res_post=res_post, cfg=cfg)
+    ops().conv(t, i, a)
+    return y[..., : spec.cout] if y.shape[-1] != spec.cout else y

@@ -1,0 +1,420 @@
+"""Native MI355X inference engine: lowers a :class:`~jax_raft_amd.models.raft.RAFT`
+onto the gfx950 kernels as one :class:`Plan` (prologue = encoders + correlation
+pyramid, loop body = one refinement iteration) and runs it eagerly from C++
+or as a single captured hipGraph.
+
+Mapping to the reference forward (``jax_raft/model.py:557-605``):
+
+=====================================  ==============================================
+reference                              engine
+=====================================  ==============================================
+concat images, feature encoder :562    prep kernel -> implicit-GEMM convs (+IN stats/apply)
+build_pyramid :567, :418-446           ``corr`` (MFMA GEMM, pooling fused, all levels)
+context encoder :569 (BN eval)         convs with BN folded into weights, fused relu/residual
+split/tanh/relu :582-584               final 1x1 conv epilogue writes tanh(h)|relu(ctx)
+                                       straight into the persistent GRU input buffers
+scan body :495-510                     loop segment: lookup, 5 motion convs, 2x GRU (A/B),
+                                       flow head (+mask), coords update, x8 upsample
+=====================================  ==============================================
+
+Persistent buffers replace every concat of the reference:
+``hx = [h | context | motion | flow]`` (GRU z/r input, ``model.py:303,366,290``) and
+``qx = [r*h | context | motion | flow]`` (GRU q input, ``model.py:308``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from ..models.layers import (
+    NORM_BATCH,
+    NORM_INSTANCE,
+    BottleneckBlock,
+    ConvNormActivation,
+    FeatureEncoder,
+    ResidualBlock,
+)
+from ..ops import native as nat
+from ..ops.native import (
+    ACT_NONE,
+    ACT_RELU,
+    ACT_SPLIT_TANH_RELU,
+    EPI_FLOW,
+    EPI_GRU_A,
+    EPI_GRU_B,
+    EPI_STD,
+    ConvSpec,
+    conv_args,
+    round_up,
+)
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def _fold_bn(cna: ConvNormActivation) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Conv kernel/bias with an eval-mode BatchNorm folded in."""
+    k = cna.layers_0.kernel.detach().float()
+    b = cna.layers_0.bias.detach().float()
+    if cna.norm == NORM_BATCH:
+        bn = cna.layers_1
+        s = bn.scale.detach().float() * torch.rsqrt(bn.var.detach().float() + bn.eps)
+        k = k * s  # broadcast over cout (last dim)
+        b = (b - bn.mean.detach().float()) * s + bn.bias.detach().float()
+    return k, b
+
+
+@dataclass
+class _Shape:
+    B: int
+    H: int
+    W: int
+    N: int
+
+
+@dataclass
+class _PlanState:
+    plan: object
+    bufs: Dict[str, torch.Tensor] = field(default_factory=dict)
+    inp1: Optional[torch.Tensor] = None
+    inp2: Optional[torch.Tensor] = None
+    out: Optional[torch.Tensor] = None
+    n_iters: int = 0
+
+
+class RaftEngine:
+    """Inference engine bound to one model and one GPU.
+
+    Args:
+        use_graph: capture the whole forward (prologue + N iterations) into one
+            hipGraph and replay it (default); otherwise launch from C++ eagerly.
+        copy_output: return a fresh tensor (default) instead of the engine's
+            static output buffer (which the next call overwrites).
+    """
+
+    def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True):
+        nat.require()
+        self.model = model
+        self.device = torch.device(device)
+        self.use_graph = use_graph
+        self.copy_output = copy_output
+        self._specs: Dict[str, ConvSpec] = {}
+        self._sources: Dict[str, callable] = {}
+        self._states: Dict[Tuple[int, int, int, int], _PlanState] = {}
+        self._sig = None
+        self._analyse()
+        self._pack()
+
+    # ----------------------------------------------------------- structure
+    def _analyse(self):
+        m = self.model
+        fe, ce = m.feature_encoder, m.context_encoder
+        for enc in (fe, ce):
+            if not isinstance(enc, FeatureEncoder):
+                raise NotImplementedError("native engine supports FeatureEncoder encoders only")
+        ub = m.update_block
+        me, rb, fh = ub.motion_encoder, ub.recurrent_block, ub.flow_head
+        self.hidden = rb.hidden_size
+        self.ctx_ch = ce.out_channels - self.hidden
+        self.num_levels = m.corr_block.num_levels
+        self.radius = m.corr_block.radius
+        S = 2 * self.radius + 1
+        self.corr_ch = self.num_levels * S * S
+        self.corr_cs = round_up(self.corr_ch, 8)
+        self.mot_out = me.out_channels
+        self.hx_real = self.hidden + self.ctx_ch + self.mot_out
+        self.hx_cs = round_up(self.hx_real, 8)
+        self.mot_off = self.hidden + self.ctx_ch
+        self.flow_off = self.mot_off + self.mot_out - 2
+        if self.mot_off % 8 or self.hidden % 16:
+            raise NotImplementedError("native engine needs hidden % 16 == 0 and (hidden + context) % 8 == 0")
+        self.fh_hidden = fh.hidden_size
+        self.has_mask = m.mask_predictor is not None
+        self.fmap_ch = fe.out_channels
+        if self.fmap_ch % 64:
+            raise NotImplementedError("native correlation needs feature channels % 64 == 0")
+
+    def _signature(self):
+        return tuple((id(p), p._version) for p in self.model.parameters()) + tuple(
+            (id(b), b._version) for b in self.model.buffers())
+
+    def _reg(self, name: str, fn):
+        """Register a conv spec source: fn() -> (kernel HWIO, bias, stride, padding, cin8)."""
+        self._sources[name] = fn
+
+    def _pack(self):
+        """(Re)pack every conv into bf16 GEMM layout; BN folded (eval mode).  Packed
+        tensors are updated in place so captured graphs stay valid."""
+        if not self._sources:
+            self._define_specs()
+        for name, fn in self._sources.items():
+            k, b, stride, pad, cin8 = fn()
+            k = k.to(self.device)
+            if name in self._specs:
+                sp = self._specs[name]
+                nat.pack_weight(k, sp.cin8, out=sp.w)
+                sp.b.copy_(b.float().to(self.device))
+            else:
+                self._specs[name] = nat.make_spec(k, b.to(self.device), stride, pad, cin8=cin8, device=self.device)
+        self._sig = self._signature()
+
+    def _define_specs(self):
+        m = self.model
+
+        def cna_src(cna: ConvNormActivation, cin8=None):
+            def f():
+                k, b = _fold_bn(cna)
+                c = cna.layers_0
+                return k, b, c.stride, c.padding, cin8
+            return f
+
+        def conv_src(c, cin8=None):
+            return lambda: (c.kernel.detach().float(), c.bias.detach().float(), c.stride, c.padding, cin8)
+
+        for tag, enc in (("fe", m.feature_encoder), ("ce", m.context_encoder)):
+            self._reg(f"{tag}.stem", cna_src(enc.convnormrelu, 8))
+            for li in (1, 2, 3):
+                layer = getattr(enc, f"layer{li}")
+                for bi in range(layer.n):
+                    blk = getattr(layer, f"layers_{bi}")
+                    names = ["convnormrelu1", "convnormrelu2"] + (["convnormrelu3"] if isinstance(blk, BottleneckBlock) else [])
+                    if blk.stride != (1, 1):
+                        names.append("downsample")
+                    for nm in names:
+                        self._reg(f"{tag}.l{li}.b{bi}.{nm}", cna_src(getattr(blk, nm)))
+            self._reg(f"{tag}.conv", conv_src(enc.conv))
+        ub = m.update_block
+        me, rb, fh = ub.motion_encoder, ub.recurrent_block, ub.flow_head
+        self._reg("me.convcorr1", cna_src(me.convcorr1, self.corr_cs))
+        if len(me.corr_layers) == 2:
+            self._reg("me.convcorr2", cna_src(me.convcorr2))
+        self._reg("me.convflow1", cna_src(me.convflow1, 8))
+        self._reg("me.convflow2", cna_src(me.convflow2))
+        self._reg("me.conv", cna_src(me.conv))
+        for gi in range(len(rb.kernel_size)):
+            gru = getattr(rb, f"convgru{gi + 1}")
+
+            def gru_a(gru=gru):
+                k = torch.cat([gru.convz.kernel.detach(), gru.convr.kernel.detach()], dim=3).float()
+                b = torch.cat([gru.convz.bias.detach(), gru.convr.bias.detach()]).float()
+                return k, b, (1, 1), gru.padding, self.hx_cs
+
+            def gru_b(gru=gru):
+                return gru.convq.kernel.detach().float(), gru.convq.bias.detach().float(), (1, 1), gru.padding, self.hx_cs
+
+            self._reg(f"gru{gi}.a", gru_a)
+            self._reg(f"gru{gi}.b", gru_b)
+        if self.has_mask:
+            mp = m.mask_predictor
+
+            def fh1():
+                k = torch.cat([fh.conv1.kernel.detach(), mp.convrelu.layers_0.kernel.detach()], dim=3).float()
+                b = torch.cat([fh.conv1.bias.detach(), mp.convrelu.layers_0.bias.detach()]).float()
+                return k, b, (1, 1), (1, 1), None
+
+            self._reg("fh1", fh1)
+            self._reg("mask", conv_src(mp.conv))
+        else:
+            self._reg("fh1", conv_src(fh.conv1))
+        self._reg("fh2", conv_src(fh.conv2))
+
+    # ------------------------------------------------------------- lowering
+    def _encoder(self, st: _PlanState, plan, tag: str, enc: FeatureEncoder, x: torch.Tensor, N: int, H: int,
+                 W: int):
+        """Lower a FeatureEncoder up to (not including) its final 1x1 conv."""
+        inorm = enc.norm_kind == NORM_INSTANCE
+        sp = self._specs
+        bufs = st.bufs
+
+        def alloc(name, shape, dtype=BF16):
+            t = torch.empty(shape, dtype=dtype, device=self.device)
+            bufs[name] = t
+            return t
+
+        def conv_raw(name, x, N, H, W, act=ACT_NONE, res=None, res_post=0):
+            s = sp[name]
+            OH, OW = s.out_hw(H, W)
+            y = alloc(name + ".y", (N, OH, OW, s.cout))
+            plan.add_conv(*conv_args(s, x, N, H, W, y, act=act, res=res, res_post=res_post))
+            return y, OH, OW
+
+        def stats(name, y, N, HW, C):
+            t = alloc(name + ".stats", (N, C, 2), F32)
+            plan.add_stats([y, t], [N, HW, C])
+            return t
+
+        def norm_act(name, x, sx, res=None, sr=None, mode_r=0, relu=3):
+            N_, H_, W_, C = x.shape
+            y = alloc(name + ".n", (N_, H_, W_, C))
+            plan.add_norm_act([x, sx, None, None, res, sr, None, None, y],
+                              [1, mode_r, N_, H_ * W_, C, relu], 1e-5)
+            return y
+
+        # stem
+        if inorm:
+            y, H, W = conv_raw(f"{tag}.stem", x, N, H, W)
+            x = norm_act(f"{tag}.stem", y, stats(f"{tag}.stem", y, N, H * W, y.shape[-1]), relu=2)
+        else:
+            x, H, W = conv_raw(f"{tag}.stem", x, N, H, W, act=ACT_RELU)
+        for li in (1, 2, 3):
+            layer = getattr(enc, f"layer{li}")
+            for bi in range(layer.n):
+                blk = getattr(layer, f"layers_{bi}")
+                pre = f"{tag}.l{li}.b{bi}"
+                names = ["convnormrelu1", "convnormrelu2"] + (["convnormrelu3"] if isinstance(blk, BottleneckBlock) else [])
+                has_ds = blk.stride != (1, 1)
+                if inorm:
+                    h_, w_ = H, W
+                    y = x
+                    for j, nm in enumerate(names):
+                        yr, h_, w_ = conv_raw(f"{pre}.{nm}", y, N, h_, w_)
+                        s = stats(f"{pre}.{nm}", yr, N, h_ * w_, yr.shape[-1])
+                        if j + 1 < len(names):
+                            y = norm_act(f"{pre}.{nm}", yr, s, relu=2)
+                        else:
+                            last, last_s = yr, s
+                    if has_ds:
+                        dr, _, _ = conv_raw(f"{pre}.downsample", x, N, H, W)
+                        ds = stats(f"{pre}.downsample", dr, N, h_ * w_, dr.shape[-1])
+                        x = norm_act(f"{pre}.out", last, last_s, res=dr, sr=ds, mode_r=1, relu=3)
+                    else:
+                        x = norm_act(f"{pre}.out", last, last_s, res=x, mode_r=0, relu=3)
+                    H, W = h_, w_
+                else:
+                    res = x
+                    if has_ds:
+                        res, _, _ = conv_raw(f"{pre}.downsample", x, N, H, W)
+                    y = x
+                    h_, w_ = H, W
+                    for j, nm in enumerate(names):
+                        if j + 1 < len(names):
+                            y, h_, w_ = conv_raw(f"{pre}.{nm}", y, N, h_, w_, act=ACT_RELU)
+                        else:
+                            y, h_, w_ = conv_raw(f"{pre}.{nm}", y, N, h_, w_, act=ACT_RELU, res=res, res_post=1)
+                    x, H, W = y, h_, w_
+        return x, H, W
+
+    def _build(self, B: int, H: int, W: int, n_iters: int) -> _PlanState:
+        m = self.model
+        plan = nat.new_plan()
+        st = _PlanState(plan=plan, n_iters=n_iters)
+        dev = self.device
+        bufs = st.bufs
+        sp = self._specs
+        h, w = H // 8, W // 8
+        M = B * h * w
+        L = self.num_levels
+        min_sz = 2 * (2 ** (L - 1))
+        assert h >= min_sz and w >= min_sz, (
+            f"Feature maps are too small to be down-sampled by the correlation pyramid: need >= {min_sz}, got {(h, w)}; "
+            f"input images should be at least {8 * min_sz}.")
+
+        def alloc(name, shape, dtype=BF16, zero=False):
+            t = (torch.zeros if zero else torch.empty)(shape, dtype=dtype, device=dev)
+            bufs[name] = t
+            return t
+
+        st.inp1 = alloc("inp1", (B, H, W, 3), F32)
+        st.inp2 = alloc("inp2", (B, H, W, 3), F32)
+        st.out = alloc("out", (n_iters, B, H, W, 2), F32)
+
+        # ---------------- prologue: encoders + correlation pyramid
+        plan.set_segment(0)
+        x0 = alloc("x0", (2 * B, H, W, 8))
+        plan.add_prep([st.inp1, st.inp2, x0], [B, H, W])
+        feat, fh_, fw_ = self._encoder(st, plan, "fe", m.feature_encoder, x0, 2 * B, H, W)
+        assert (fh_, fw_) == (h, w), "The feature encoder should downsample H and W by 8"
+        fmap = alloc("fmap", (2 * B, h, w, self.fmap_ch))
+        plan.add_conv(*conv_args(sp["fe.conv"], feat, 2 * B, h, w, fmap))
+        levels = []
+        hl, wl = h, w
+        for l in range(L):
+            levels.append(alloc(f"corr.l{l}", (M, hl, wl), F32))
+            hl //= 2
+            wl //= 2
+        plan.add_corr([fmap[:B], fmap[B:]] + levels + [None] * (4 - L), [B, h, w, self.fmap_ch, L],
+                      1.0 / float(self.fmap_ch) ** 0.5)
+
+        hx = alloc("hx", (M, self.hx_cs))
+        qx = alloc("qx", (M, self.hx_cs))
+        h32 = alloc("h32", (M, self.hidden), F32)
+        zb = alloc("z", (M, self.hidden), F32)
+        flow8 = alloc("flow8", (M, 8))
+        coords = alloc("coords", (M, 2), F32)
+        flow32 = alloc("flow32", (M, 2), F32)
+        for t in (hx, qx, flow8, flow32):
+            plan.add_memset([t])
+        ctxf, ch_, cw_ = self._encoder(st, plan, "ce", m.context_encoder, x0[:B], B, H, W)
+        assert (ch_, cw_) == (h, w), "The context encoder should downsample H and W by 8"
+        plan.add_conv(*conv_args(sp["ce.conv"], ctxf, B, h, w, hx, act=ACT_SPLIT_TANH_RELU, split=self.hidden,
+                                 y2=qx, h32=h32, hidden=self.hidden))
+        plan.add_init_coords([coords], [B, h, w])
+
+        # ---------------- loop body: one refinement iteration (model.py:495-510)
+        plan.set_segment(1)
+        corr = alloc("corr", (M, self.corr_cs))
+        plan.add_lookup([coords, corr] + levels + [None] * (4 - L), [L, B, h, w, self.radius])
+        me = m.update_block.motion_encoder
+        cl, fl = me.corr_layers, me.flow_layers
+        cf = alloc("cf", (M, cl[-1] + fl[-1]))
+        if len(cl) == 2:
+            c1 = alloc("c1", (M, cl[0]))
+            plan.add_conv(*conv_args(sp["me.convcorr1"], corr, B, h, w, c1, act=ACT_RELU))
+        else:
+            plan.add_conv(*conv_args(sp["me.convcorr1"], corr, B, h, w, cf, act=ACT_RELU))
+        f1 = alloc("f1", (M, fl[0]))
+        plan.add_conv(*conv_args(sp["me.convflow1"], flow8, B, h, w, f1, act=ACT_RELU))
+        if len(cl) == 2:
+            plan.add_conv(*conv_args(sp["me.convcorr2"], c1, B, h, w, cf, act=ACT_RELU))
+        plan.add_conv(*conv_args(sp["me.convflow2"], f1, B, h, w, cf, y_coff=cl[-1], act=ACT_RELU))
+        plan.add_conv(*conv_args(sp["me.conv"], cf, B, h, w, hx, y_coff=self.mot_off, act=ACT_RELU, y2=qx,
+                                 y2_coff=self.mot_off))
+        for gi in range(len(m.update_block.recurrent_block.kernel_size)):
+            plan.add_conv(*conv_args(sp[f"gru{gi}.a"], hx, B, h, w, qx, h32=h32, zbuf=zb, hidden=self.hidden,
+                                     epi=EPI_GRU_A))
+            plan.add_conv(*conv_args(sp[f"gru{gi}.b"], qx, B, h, w, hx, h32=h32, zbuf=zb, hidden=self.hidden,
+                                     epi=EPI_GRU_B))
+        s1 = sp["fh1"]
+        fm = alloc("fm", (M, round_up(s1.cout, 8)))
+        plan.add_conv(*conv_args(s1, hx, B, h, w, fm, act=ACT_RELU))
+        # flow head conv2 + coordinate update (model.py:505) + flow into hx/qx/flow8
+        plan.add_conv(*conv_args(sp["fh2"], fm, B, h, w, hx, y_coff=self.flow_off, y2=qx, y2_coff=self.flow_off,
+                                 y3=flow8, y3_coff=0, coords=coords, flow32=flow32, epi=EPI_FLOW))
+        stride = B * H * W * 2
+        if self.has_mask:
+            mask = alloc("mask", (M, 576))
+            plan.add_conv(*conv_args(sp["mask"], fm, B, h, w, mask, x_coff=self.fh_hidden,
+                                     alpha=m.mask_predictor.multiplier))
+            plan.add_upsample_convex([mask, flow32, st.out], [B, h, w, stride])
+        else:
+            plan.add_upsample_bilinear([flow32, st.out], [B, h, w, stride])
+        plan.set_segment(2)
+        return st
+
+    # --------------------------------------------------------------- forward
+    @torch.no_grad()
+    def forward(self, image1: torch.Tensor, image2: torch.Tensor, num_flow_updates: int = 12) -> torch.Tensor:
+        if self._signature() != self._sig:
+            self._pack()
+        B, H, W, C = image1.shape
+        assert C == 3, "images must be NHWC with 3 channels"
+        key = (B, H, W, num_flow_updates)
+        st = self._states.get(key)
+        if st is None:
+            st = self._build(B, H, W, num_flow_updates)
+            self._states[key] = st
+        st.inp1.copy_(image1)
+        st.inp2.copy_(image2)
+        if self.use_graph:
+            if st.plan.captured_iters() != num_flow_updates:
+                st.plan.capture(num_flow_updates)
+            st.plan.replay()
+        else:
+            st.plan.run(num_flow_updates)
+        return st.out.clone() if self.copy_output else st.out
+
+    def op_names(self, B: int, H: int, W: int, n_iters: int):
+        st = self._states.get((B, H, W, n_iters)) or self._build(B, H, W, n_iters)
+        return [st.plan.op_names(s) for s in range(3)]

@@ -1,0 +1,266 @@
+"""Numerics of every HIP kernel against the fp32 PyTorch golden ops
+(:mod:`jax_raft_amd.models.reference`).  Inputs are rounded to bf16 first so
+the comparison isolates kernel arithmetic (fp32 accumulate) from the input
+quantisation."""
+import math
+
+import pytest
+import torch
+
+from jax_raft_amd.models import reference as R
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _nat():
+    from jax_raft_amd.ops import native
+
+    native.require()
+    return native
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+def _rel(a, b):
+    return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
+
+
+CONV_CASES = [
+    # N, H, W, cin, cout, kh, kw, stride, pad
+    (2, 17, 23, 64, 64, 3, 3, 1, 1),
+    (2, 20, 24, 64, 96, 3, 3, 2, 1),
+    (2, 20, 24, 64, 96, 1, 1, 2, 0),
+    (1, 40, 48, 3, 64, 7, 7, 2, 3),
+    (2, 13, 16, 384, 256, 1, 5, 1, (0, 2)),
+    (2, 13, 16, 384, 128, 5, 1, 1, (2, 0)),
+    (1, 12, 18, 324, 256, 1, 1, 1, 0),
+    (1, 12, 18, 2, 128, 7, 7, 1, 3),
+    (1, 12, 18, 256, 126, 3, 3, 1, 1),
+    (1, 12, 18, 256, 2, 3, 3, 1, 1),
+    (1, 12, 18, 242, 96, 3, 3, 1, 1),
+    (2, 9, 11, 24, 24, 3, 3, 2, 1),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("cfg", [None, 0, 1, 2, 3, 4])
+def test_conv_matches_reference(case, cfg):
+    nat = _nat()
+    N, H, W, cin, cout, kh, kw, s, p = case
+    pad = p if isinstance(p, tuple) else (p, p)
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, cin)
+    k = torch.randn(kh, kw, cin, cout) / math.sqrt(kh * kw * cin)
+    b = torch.randn(cout) * 0.1
+    ref = R.conv2d_nhwc(_bf(x), _bf(k), b, (s, s), pad)
+    spec = nat.make_spec(k, b, (s, s), pad, device=DEV)
+    cin8 = spec.cin8
+    xg = torch.zeros(N, H, W, cin8, dtype=torch.bfloat16, device=DEV)
+    xg[..., :cin] = x.to(DEV, torch.bfloat16)
+    y = nat.conv2d(spec, xg, out_dtype=torch.float32, cfg=cfg)
+    torch.cuda.synchronize()
+    assert y.shape == ref.shape
+    err = _rel(y.cpu(), ref)
+    assert err < 2e-3, err
+
+
+def test_conv_epilogues():
+    """relu / residual (pre and post) / alpha / bf16 output / channel offsets."""
+    nat = _nat()
+    torch.manual_seed(1)
+    N, H, W, cin, cout = 2, 10, 12, 32, 48
+    x = torch.randn(N, H, W, cin)
+    k = torch.randn(3, 3, cin, cout) / math.sqrt(9 * cin)
+    b = torch.randn(cout) * 0.1
+    res = torch.randn(N, H, W, cout)
+    base = R.conv2d_nhwc(_bf(x), _bf(k), b, (1, 1), (1, 1))
+    spec = nat.make_spec(k, b, (1, 1), (1, 1), device=DEV)
+    xg = x.to(DEV, torch.bfloat16).contiguous()
+    rg = res.to(DEV, torch.bfloat16).contiguous()
+    y = nat.conv2d(spec, xg, act=nat.ACT_RELU, out_dtype=torch.float32, res=rg, res_post=0)
+    assert _rel(y.cpu(), torch.relu(base + _bf(res))) < 3e-3
+    y = nat.conv2d(spec, xg, act=nat.ACT_RELU, out_dtype=torch.float32, res=rg, res_post=1)
+    assert _rel(y.cpu(), torch.relu(torch.relu(base) + _bf(res))) < 3e-3
+    y = nat.conv2d(spec, xg, act=nat.ACT_NONE, out_dtype=torch.float32, alpha=0.25)
+    assert _rel(y.cpu(), 0.25 * base) < 3e-3
+    # write into a channel slice of a wider buffer, plus a second copy
+    big = torch.full((N * H * W, 64), 7.0, dtype=torch.bfloat16, device=DEV)
+    big2 = torch.zeros((N * H * W, 64), dtype=torch.bfloat16, device=DEV)
+    t, i, a = nat.conv_args(spec, xg, N, H, W, big, y_coff=8, act=nat.ACT_TANH, y2=big2, y2_coff=16)
+    nat.ops().conv(t, i, a)
+    torch.cuda.synchronize()
+    exp = torch.tanh(base).reshape(-1, cout)
+    assert _rel(big[:, 8:56].float().cpu(), exp) < 1e-2
+    assert (big[:, :8] == 7).all() and (big[:, 56:] == 7).all()
+    assert _rel(big2[:, 16:64].float().cpu(), exp) < 1e-2
+
+
+def _gru_ref(h, x, kz, bz, kr, br, kq, bq, pad):
+    hx = torch.cat([h, x], -1)
+    z = torch.sigmoid(R.conv2d_nhwc(_bf(hx), _bf(kz), bz, (1, 1), pad))
+    r = torch.sigmoid(R.conv2d_nhwc(_bf(hx), _bf(kr), br, (1, 1), pad))
+    q = torch.tanh(R.conv2d_nhwc(_bf(torch.cat([r * h, x], -1)), _bf(kq), bq, (1, 1), pad))
+    return (1 - z) * h + z * q
+
+
+@pytest.mark.parametrize("hidden,xin,ks,pad", [(128, 256, (1, 5), (0, 2)), (128, 256, (5, 1), (2, 0)),
+                                               (96, 146, (3, 3), (1, 1))])
+def test_gru_fused_epilogues(hidden, xin, ks, pad):
+    nat = _nat()
+    torch.manual_seed(2)
+    B, h, w = 2, 11, 13
+    M = B * h * w
+    cin = hidden + xin
+    cs = nat.round_up(cin, 8)
+    hs = torch.tanh(torch.randn(B, h, w, hidden))
+    xs = torch.randn(B, h, w, xin)
+    ks_ = [torch.randn(*ks, cin, hidden) / math.sqrt(ks[0] * ks[1] * cin) for _ in range(3)]
+    bs_ = [torch.randn(hidden) * 0.1 for _ in range(3)]
+    ref = _gru_ref(hs, xs, ks_[0], bs_[0], ks_[1], bs_[1], ks_[2], bs_[2], pad)
+    hx = torch.zeros(M, cs, dtype=torch.bfloat16, device=DEV)
+    hx[:, :hidden] = hs.reshape(M, hidden).to(DEV, torch.bfloat16)
+    hx[:, hidden:cin] = xs.reshape(M, xin).to(DEV, torch.bfloat16)
+    qx = hx.clone()
+    h32 = hs.reshape(M, hidden).to(DEV).contiguous()
+    zb = torch.empty(M, hidden, device=DEV)
+    sa = nat.make_spec(torch.cat([ks_[0], ks_[1]], 3), torch.cat([bs_[0], bs_[1]]), (1, 1), pad, cin8=cs, device=DEV)
+    sb = nat.make_spec(ks_[2], bs_[2], (1, 1), pad, cin8=cs, device=DEV)
+    nat.ops().conv(*nat.conv_args(sa, hx, B, h, w, qx, h32=h32, zbuf=zb, hidden=hidden, epi=nat.EPI_GRU_A))
+    nat.ops().conv(*nat.conv_args(sb, qx, B, h, w, hx, h32=h32, zbuf=zb, hidden=hidden, epi=nat.EPI_GRU_B))
+    torch.cuda.synchronize()
+    out = h32.cpu().reshape(B, h, w, hidden)
+    # r*h is quantised to bf16 before the q conv in the kernel; reference uses fp32 r*h -> bf16 as well
+    assert (out - ref).abs().max().item() < 2e-2
+    assert (hx[:, :hidden].float().cpu() - ref.reshape(M, hidden)).abs().max().item() < 2.5e-2
+
+
+def test_flow_epilogue():
+    nat = _nat()
+    torch.manual_seed(3)
+    B, h, w, cin = 2, 9, 10, 256
+    M = B * h * w
+    x = torch.randn(B, h, w, cin)
+    k = torch.randn(3, 3, cin, 2) / math.sqrt(9 * cin)
+    b = torch.randn(2) * 0.1
+    delta = R.conv2d_nhwc(_bf(x), _bf(k), b, (1, 1), (1, 1))
+    c0 = R.make_coords_grid(B, h, w)
+    c1 = c0 + torch.randn(B, h, w, 2)
+    spec = nat.make_spec(k, b, (1, 1), (1, 1), device=DEV)
+    coords = c1.reshape(M, 2).to(DEV).contiguous()
+    flow32 = torch.zeros(M, 2, device=DEV)
+    hx = torch.zeros(M, 16, dtype=torch.bfloat16, device=DEV)
+    f8 = torch.zeros(M, 8, dtype=torch.bfloat16, device=DEV)
+    xg = x.to(DEV, torch.bfloat16).contiguous()
+    nat.ops().conv(*nat.conv_args(spec, xg, B, h, w, hx, y_coff=14, y3=f8, coords=coords, flow32=flow32,
+                                  epi=nat.EPI_FLOW))
+    torch.cuda.synchronize()
+    new = c1 + delta
+    assert (coords.cpu().reshape(B, h, w, 2) - new).abs().max() < 2e-3
+    assert (flow32.cpu().reshape(B, h, w, 2) - (new - c0)).abs().max() < 2e-3
+    assert (hx[:, 14:16].float().cpu() - (new - c0).reshape(M, 2)).abs().max() < 5e-2
+    assert (f8[:, :2].float().cpu() - (new - c0).reshape(M, 2)).abs().max() < 5e-2
+
+
+@pytest.mark.parametrize("h,w,C,L", [(16, 16, 64, 4), (23, 37, 128, 4), (55, 128, 256, 4), (17, 20, 64, 2)])
+def test_corr_pyramid(h, w, C, L):
+    nat = _nat()
+    torch.manual_seed(4)
+    B = 2
+    f1 = torch.randn(B, h, w, C)
+    f2 = torch.randn(B, h, w, C)
+    ref = R.build_pyramid(_bf(f1), _bf(f2), L)
+    M = B * h * w
+    lv = []
+    hl, wl = h, w
+    for _ in range(L):
+        lv.append(torch.full((M, hl, wl), float("nan"), device=DEV))
+        hl //= 2
+        wl //= 2
+    g1 = f1.to(DEV, torch.bfloat16).contiguous()
+    g2 = f2.to(DEV, torch.bfloat16).contiguous()
+    nat.ops().corr([g1, g2] + lv + [None] * (4 - L), [B, h, w, C, L], 1.0 / math.sqrt(C))
+    torch.cuda.synchronize()
+    for l in range(L):
+        got = lv[l].cpu()
+        assert not torch.isnan(got).any(), f"level {l} has unwritten cells"
+        assert (got - ref[l]).abs().max().item() < 1e-3 * max(1.0, ref[l].abs().max().item()), l
+
+
+@pytest.mark.parametrize("radius,L", [(4, 4), (3, 4), (2, 2)])
+def test_corr_lookup(radius, L):
+    nat = _nat()
+    torch.manual_seed(5)
+    B, h, w = 2, 17, 19
+    M = B * h * w
+    pyr = []
+    hl, wl = h, w
+    for _ in range(L):
+        pyr.append(torch.randn(M, hl, wl))
+        hl //= 2
+        wl //= 2
+    # coords: in range, fractional, and far outside (zero padding)
+    coords = R.make_coords_grid(B, h, w) + torch.randn(B, h, w, 2) * 4
+    coords[0, 0, 0] = torch.tensor([-30.5, 3.25])
+    coords[1, 2, 3] = torch.tensor([h + 40.0, w + 7.5])
+    ref = R.index_pyramid(pyr, coords, radius)
+    S = 2 * radius + 1
+    ocs = nat.round_up(L * S * S, 8)
+    out = torch.full((M, ocs), 5.0, dtype=torch.bfloat16, device=DEV)
+    nat.ops().lookup([coords.reshape(M, 2).to(DEV).contiguous(), out] + [p.to(DEV) for p in pyr] + [None] * (4 - L),
+                     [L, B, h, w, radius])
+    torch.cuda.synchronize()
+    got = out.float().cpu()
+    assert (got[:, L * S * S:] == 0).all()
+    err = (got[:, : L * S * S] - ref.reshape(M, -1)).abs().max().item()
+    assert err < 3e-2 * ref.abs().max().item(), err
+
+
+def test_upsample_convex_and_bilinear():
+    nat = _nat()
+    torch.manual_seed(6)
+    B, h, w = 2, 7, 9
+    M = B * h * w
+    flow = torch.randn(B, h, w, 2) * 3
+    mask = torch.randn(B, h, w, 576)
+    ref = R.upsample_flow(flow, _bf(mask))
+    out = torch.zeros(2, B, 8 * h, 8 * w, 2, device=DEV)
+    nat.ops().upsample_convex([mask.reshape(M, 576).to(DEV, torch.bfloat16).contiguous(),
+                               flow.reshape(M, 2).to(DEV).contiguous(), out], [B, h, w, B * 64 * h * w * 2])
+    torch.cuda.synchronize()
+    assert (out[1].cpu() - ref).abs().max().item() < 1e-3 * ref.abs().max().item() + 1e-4
+    assert (out[0] == 0).all()
+    refb = R.upsample_flow(flow, None)
+    outb = torch.zeros(1, B, 8 * h, 8 * w, 2, device=DEV)
+    nat.ops().upsample_bilinear([flow.reshape(M, 2).to(DEV).contiguous(), outb], [B, h, w, 0])
+    torch.cuda.synchronize()
+    assert (outb[0].cpu() - refb).abs().max().item() < 1e-4 * refb.abs().max().item() + 1e-5
+
+
+@pytest.mark.parametrize("C", [64, 96, 128, 24])
+def test_instance_norm_stats_apply(C):
+    nat = _nat()
+    torch.manual_seed(7)
+    N, H, W = 3, 37, 29
+    x = _bf(torch.randn(N, H, W, C) * 2 + 0.5)
+    r = _bf(torch.randn(N, H, W, C))
+    xg = x.to(DEV, torch.bfloat16).contiguous()
+    rg = r.to(DEV, torch.bfloat16).contiguous()
+    st = torch.empty(N, C, 2, device=DEV)
+    sr = torch.empty(N, C, 2, device=DEV)
+    nat.ops().stats([xg, st], [N, H * W, C])
+    nat.ops().stats([rg, sr], [N, H * W, C])
+    y = torch.empty_like(xg)
+    # relu(relu(IN(x)) + IN(r))
+    nat.ops().norm_act([xg, st, None, None, rg, sr, None, None, y], [1, 1, N, H * W, C, 3], 1e-5)
+    torch.cuda.synchronize()
+    ref = torch.relu(torch.relu(R.instance_norm_nhwc(x)) + R.instance_norm_nhwc(r))
+    assert (y.float().cpu() - ref).abs().max().item() < 3e-2
+    y2 = torch.empty_like(xg)
+    nat.ops().norm_act([xg, st, None, None, rg, None, None, None, y2], [1, 0, N, H * W, C, 2], 1e-5)
+    torch.cuda.synchronize()
+    ref2 = torch.relu(R.instance_norm_nhwc(x) + r)
+    assert (y2.float().cpu() - ref2).abs().max().item() < 3e-2

@@ -1,0 +1,88 @@
+"""Model API on the CPU golden path (BASELINE config 1: raft_small, 2x128x128x3, 3 iters)."""
+import numpy as np
+import pytest
+import torch
+
+from jax_raft_amd import RAFT, raft_large, raft_small
+from jax_raft_amd.models.layers import CorrBlock
+from jax_raft_amd.utils import checkpoint as C
+
+
+def _pair(B=1, H=128, W=128, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(B, H, W, 3, generator=g) * 2 - 1, torch.rand(B, H, W, 3, generator=g) * 2 - 1
+
+
+def test_config1_raft_small_cpu():
+    model, variables = raft_small()
+    i1, i2 = _pair(2)
+    out = model.apply(variables, i1, i2, train=False, num_flow_updates=3)
+    assert out.shape == (3, 2, 128, 128, 2)
+    assert torch.isfinite(out).all()
+
+
+def test_raft_large_cpu_shapes_default_iters():
+    model, variables = raft_large()
+    i1, i2 = _pair(1, 128, 136)
+    out = model.apply(variables, i1, i2)
+    assert out.shape == (12, 1, 128, 136, 2)
+
+
+def test_apply_accepts_numpy_and_foreign_variables():
+    model, variables = raft_small(seed=0)
+    other, ov = raft_small(seed=7)
+    i1, i2 = _pair()
+    ref = other.apply(ov, i1, i2, num_flow_updates=2)
+    npvars = {"params": {k: v for k, v in ov["params"].items()}}
+    npvars = {"params": C.unflatten_tree({k: v.detach().numpy() for k, v in C.flatten_tree(ov["params"]).items()})}
+    out = model.apply(npvars, i1.numpy(), i2.numpy(), num_flow_updates=2)
+    assert torch.allclose(out, ref, atol=1e-5)
+
+
+def test_input_assertions():
+    model, v = raft_small()
+    a, b = _pair(1, 128, 128)
+    with pytest.raises(AssertionError):
+        model.apply(v, a[:, :124], b[:, :124])
+    with pytest.raises(AssertionError):
+        model.apply(v, a, b[:, :120])
+    small = torch.zeros(1, 64, 64, 3)
+    with pytest.raises(AssertionError):
+        model.apply(v, small, small)
+
+
+def test_train_mode_updates_batch_stats_and_grads():
+    model, v = raft_large()
+    model.train()
+    a, b = _pair(2, 128, 128)
+    before = v["batch_stats"]["context_encoder"]["convnormrelu"]["layers_1"]["mean"].clone()
+    out, new = model.apply(v, a, b, train=True, num_flow_updates=2, mutable=["batch_stats"])
+    after = new["batch_stats"]["context_encoder"]["convnormrelu"]["layers_1"]["mean"]
+    assert not torch.equal(before, after)
+    loss = out.abs().mean()
+    loss.backward()
+    g = model.feature_encoder.convnormrelu.layers_0.kernel.grad
+    assert g is not None and torch.isfinite(g).all() and g.abs().sum() > 0
+
+
+def test_submodule_injection():
+    model, v = raft_small(corr_block=CorrBlock(num_levels=2, radius=2))
+    assert model.corr_block.num_levels == 2
+    assert tuple(v["params"]["update_block"]["motion_encoder"]["convcorr1"]["layers_0"]["kernel"].shape) == (1, 1, 50, 96)
+    out = model.apply(v, *_pair(), num_flow_updates=1)
+    assert out.shape == (1, 1, 128, 128, 2)
+    with pytest.raises(TypeError):
+        raft_small(bogus=1)
+
+
+def test_deterministic_init():
+    _, a = raft_small(seed=0)
+    _, b = raft_small(seed=0)
+    _, c = raft_small(seed=1)
+    fa, fb, fc = (C.flatten_tree(x["params"]) for x in (a, b, c))
+    k = "update_block.flow_head.conv1.kernel"
+    assert torch.equal(fa[k], fb[k]) and not torch.equal(fa[k], fc[k])
+    # truncated-normal init stays within 2 std
+    kern = fa["feature_encoder.convnormrelu.layers_0.kernel"]
+    std = np.sqrt(2.0 / (7 * 7 * 32)) / 0.87962566103423978
+    assert kern.abs().max() <= 2 * std + 1e-6
