@@ -15,11 +15,12 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 JR_DEVICE float bf2f(bf16 v) { return (float)v; }
 JR_DEVICE bf16 f2bf(float v) { return (bf16)v; }
 
-JR_DEVICE float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+JR_DEVICE float rcpf_(float x) { return __builtin_amdgcn_rcpf(x); }
+JR_DEVICE float sigmoidf_(float x) { return rcpf_(1.0f + __expf(-x)); }
 JR_DEVICE float tanhf_(float x) {
   // tanh(x) = 1 - 2 / (exp(2x) + 1); saturates cleanly for large |x|.
   float e = __expf(2.0f * x);
-  return 1.0f - 2.0f / (e + 1.0f);
+  return 1.0f - 2.0f * rcpf_(e + 1.0f);
 }
 
 // Activation codes shared with the host side (jax_raft_amd/ops/native.py).

@@ -92,6 +92,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
   constexpr int WR = BCO >= 32 ? BCO / 32 : 1;
   constexpr int A_ELEMS = BCO * BK;
   constexpr int B_ELEMS = BP * BK;
+  constexpr unsigned OOB = 0x80000000u;   // buffer offset past num_records -> hardware returns 0
   static_assert(TM >= 1 && TN >= 1 && WCO * WP == 4, "tile");
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * (A_ELEMS + B_ELEMS)];
 
@@ -103,14 +104,18 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
   const int p0 = blockIdx.x * BP;
   const int co0 = blockIdx.y * BCO;
   const int ch = tid & 7;
-
-  const bf16* __restrict__ xb = (const bf16*)p.x;
-  const bf16* __restrict__ wb = (const bf16*)p.w;
   const int OHW = p.OH * p.OW;
 
-  // Per-thread im2col row descriptors (fixed across the K loop).
+  // Buffer resources: out-of-range offsets (padding taps, tail rows, K tail)
+  // read as zero with no branch and no exec masking.
+  const __amdgpu_buffer_rsrc_t xsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)p.w_bytes, 0x00020000);
+
+  // Per-thread im2col row descriptors (fixed across the K loop); byte offsets.
   int ih0[XR], iw0[XR];
-  long rbase[XR];
+  unsigned rbase[XR];
 #pragma unroll
   for (int i = 0; i < XR; ++i) {
     const int m = p0 + (tid >> 3) + 32 * i;
@@ -121,68 +126,65 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
       const int ow = rem - oh * p.OW;
       ih0[i] = oh * p.SH - p.PH;
       iw0[i] = ow * p.SW - p.PW;
-      rbase[i] = (long)n * p.H * p.W * p.x_cstride + p.x_coff;
+      rbase[i] = (unsigned)(((long)n * p.H * p.W * p.x_cstride + p.x_coff) * 2);
     } else {
       ih0[i] = -(1 << 28);
       iw0[i] = -(1 << 28);
       rbase[i] = 0;
     }
   }
+  const unsigned wrow_off = (unsigned)((co0 + (tid >> 3)) * p.kpad * 2 + ch * 16);
+  const unsigned wrow_lim = (unsigned)(p.cout_pad - co0 - (tid >> 3));  // rows i*32 < lim are valid
 
-  // K-chunk state of this thread's chunk column: kc = ks*8 + ch.
+  // K-chunk state of the NEXT stage to load: kc = ks*8 + ch.
   const int cpt = p.cin8 >> 3;
   int tap = ch / cpt;
   int cc = ch - tap * cpt;
   int kh = tap / p.KW;
   int kw = tap - kh * p.KW;
+  int ks_next = 0;
+  const unsigned xrow_bytes = (unsigned)p.x_cstride * 2;
 
-  u32x4 xr[XR];
-  u32x4 wr[WR];
+  struct Regs { u32x4 x[XR]; u32x4 w[WR]; };
+  Regs ra, rb;
 
-  auto load_stage = [&](int ks) {
+  auto issue = [&](Regs& r) {
     const bool kvalid = kh < p.KH;
 #pragma unroll
     for (int i = 0; i < XR; ++i) {
       const int ih = ih0[i] + kh;
       const int iw = iw0[i] + kw;
       const bool ok = kvalid && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-      if (ok) {
-        xr[i] = *(const u32x4*)(xb + rbase[i] + (long)(ih * p.W + iw) * p.x_cstride + cc * 8);
-      } else {
-        xr[i] = u32x4{0u, 0u, 0u, 0u};
-      }
+      const unsigned off = rbase[i] + (unsigned)(ih * p.W + iw) * xrow_bytes + (unsigned)cc * 16u;
+      r.x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xsrd, ok ? off : OOB, 0, 0));
     }
+    const unsigned kofs = (unsigned)ks_next * (BK * 2);
 #pragma unroll
     for (int i = 0; i < WR; ++i) {
-      const int row = (tid >> 3) + 32 * i;
-      const int co = co0 + row;
-      const bool act_thread = (BCO >= 32) || (tid < BCO * 8);
-      if (act_thread && co < p.cout_pad) {
-        wr[i] = *(const u32x4*)(wb + (long)co * p.kpad + ks * BK + ch * 8);
-      } else {
-        wr[i] = u32x4{0u, 0u, 0u, 0u};
-      }
+      const bool ok = ((BCO >= 32) || (tid < BCO * 8)) && (unsigned)(32 * i) < wrow_lim && ks_next * BK < p.kpad;
+      const unsigned off = wrow_off + (unsigned)(32 * i) * (unsigned)p.kpad * 2u + kofs;
+      r.w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wsrd, ok ? off : OOB, 0, 0));
     }
-  };
-  auto advance = [&]() {
+    // advance the chunk state to the following stage
+    ++ks_next;
     cc += 8;
     while (cc >= cpt) {
       cc -= cpt;
       if (++kw == p.KW) { kw = 0; ++kh; }
     }
   };
-  auto store_stage = [&](int buf) {
+  auto store = [&](const Regs& r, int buf) {
     bf16* sA = smem + buf * (A_ELEMS + B_ELEMS);
     bf16* sB = sA + A_ELEMS;
 #pragma unroll
     for (int i = 0; i < XR; ++i) {
-      const int r = (tid >> 3) + 32 * i;
-      *(u32x4*)(sB + r * BK + ((ch ^ swzB(r)) << 3)) = xr[i];
+      const int rr = (tid >> 3) + 32 * i;
+      *(u32x4*)(sB + rr * BK + ((ch ^ swzB(rr)) << 3)) = r.x[i];
     }
 #pragma unroll
     for (int i = 0; i < WR; ++i) {
-      const int r = (tid >> 3) + 32 * i;
-      if ((BCO >= 32) || (tid < BCO * 8)) *(u32x4*)(sA + r * BK + ((ch ^ swzA(r)) << 3)) = wr[i];
+      const int rr = (tid >> 3) + 32 * i;
+      if ((BCO >= 32) || (tid < BCO * 8)) *(u32x4*)(sA + rr * BK + ((ch ^ swzA(rr)) << 3)) = r.w[i];
     }
   };
 
@@ -192,21 +194,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
 #pragma unroll
     for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nks = p.kpad / BK;
-  load_stage(0);
-  store_stage(0);
-  __syncthreads();
-
   const int li = lane & 15;
   const int lq = lane >> 4;
-  for (int ks = 0; ks < nks; ++ks) {
-    const int cur = ks & 1;
-    const bool more = ks + 1 < nks;
-    if (more) {
-      advance();
-      load_stage(ks + 1);
-    }
-    const bf16* sA = smem + cur * (A_ELEMS + B_ELEMS);
+  auto compute = [&](int buf) {
+    const bf16* sA = smem + buf * (A_ELEMS + B_ELEMS);
     const bf16* sB = sA + A_ELEMS;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -228,9 +219,29 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
         for (int tn = 0; tn < TN; ++tn)
           acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tm], bfr[tn], acc[tm][tn], 0, 0, 0);
     }
-    if (more) store_stage(cur ^ 1);
+  };
+
+  // Software pipeline: global loads run two K-stages ahead of the MFMAs
+  // (register sets ra/rb alternate, LDS double-buffered, one barrier per
+  // stage).  Loads past the end of K are issued with OOB offsets (zeros),
+  // keeping the loop body branch-free so hipcc emits counted vmcnt waits.
+  const int nks = p.kpad / BK;
+  issue(ra);
+  issue(rb);
+  store(ra, 0);
+  __syncthreads();
+  const int npairs = nks >> 1;
+  for (int it = 0; it < npairs; ++it) {
+    issue(ra);          // stage 2it+2
+    compute(0);         // stage 2it
+    store(rb, 1);       // stage 2it+1 (loaded one stage ago)
+    __syncthreads();
+    issue(rb);          // stage 2it+3
+    compute(1);         // stage 2it+1
+    store(ra, 0);       // stage 2it+2
     __syncthreads();
   }
+  if (nks & 1) compute(0);
 
   // ------------------------------------------------------------------ epilogue
   const int cbase = co0 + wco * WTCO + lq * NV;
@@ -384,6 +395,7 @@ extern "C" int jr_conv_forward(const ConvParams* p, int cfg, int epi, hipStream_
     case 2: return launch_cfg<128, 64, 2>(p, epi, stream);
     case 3: return launch_cfg<16, 256, 1>(p, epi, stream);
     case 4: return launch_cfg<64, 64, 1>(p, epi, stream);
+    case 5: return launch_cfg<16, 64, 1>(p, epi, stream);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -33,10 +33,20 @@ constexpr int CQ = 128;
 constexpr int TY = 8, TX = 16;
 constexpr int CT = TY * TX;
 
+template <typename T>
+JR_DEVICE T cvt_out(float v);
+template <>
+JR_DEVICE float cvt_out<float>(float v) { return v; }
+template <>
+JR_DEVICE bf16 cvt_out<bf16>(float v) { return f2bf(v); }
+JR_DEVICE float to_f(float v) { return v; }
+JR_DEVICE float to_f(bf16 v) { return bf2f(v); }
+
+template <typename T>
 __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restrict__ f1, const bf16* __restrict__ f2,
-                                                           int h, int w, int C, int cs, float* __restrict__ l0,
-                                                           float* __restrict__ l1, float* __restrict__ l2,
-                                                           float* __restrict__ l3, int nlev, float scale) {
+                                                           int h, int w, int C, int cs, T* __restrict__ l0,
+                                                           T* __restrict__ l1, T* __restrict__ l2,
+                                                           T* __restrict__ l3, int nlev, float scale) {
   constexpr int TM = 2, TN = 8;
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * (CQ + CT) * BK];
   const int P = h * w;
@@ -136,10 +146,10 @@ __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restric
       for (int tn = 0; tn < TN; ++tn) v[tn] = acc[tm][tn][r] * scale;
       // level 0
       if (qok && x0 < w) {
-        float* dst = l0 + ((long)b * P + q) * P;
+        T* dst = l0 + ((long)b * P + q) * P;
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn)
-          if (ty0 + tn < h) dst[(ty0 + tn) * w + x0] = v[tn];
+          if (ty0 + tn < h) dst[(ty0 + tn) * w + x0] = cvt_out<T>(v[tn]);
       }
       if (nlev < 2) continue;
       // level 1: pairs of rows (tn, tn+1), lanes (li, li^1)
@@ -152,11 +162,11 @@ __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restric
       {
         const int X1 = x0 >> 1;
         if (qok && (li & 1) == 0 && X1 < w1) {
-          float* dst = l1 + ((long)b * P + q) * (h1 * w1);
+          T* dst = l1 + ((long)b * P + q) * (h1 * w1);
 #pragma unroll
           for (int t = 0; t < TN / 2; ++t) {
             const int Y1 = (ty0 >> 1) + t;
-            if (Y1 < h1) dst[Y1 * w1 + X1] = v1[t];
+            if (Y1 < h1) dst[Y1 * w1 + X1] = cvt_out<T>(v1[t]);
           }
         }
       }
@@ -170,11 +180,11 @@ __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restric
       {
         const int X2 = x0 >> 2;
         if (qok && (li & 3) == 0 && X2 < w2) {
-          float* dst = l2 + ((long)b * P + q) * (h2 * w2);
+          T* dst = l2 + ((long)b * P + q) * (h2 * w2);
 #pragma unroll
           for (int t = 0; t < TN / 4; ++t) {
             const int Y2 = (ty0 >> 2) + t;
-            if (Y2 < h2) dst[Y2 * w2 + X2] = v2[t];
+            if (Y2 < h2) dst[Y2 * w2 + X2] = cvt_out<T>(v2[t]);
           }
         }
       }
@@ -185,7 +195,7 @@ __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restric
         const int X3 = x0 >> 3;
         const int Y3 = ty0 >> 3;
         if (qok && (li & 7) == 0 && X3 < w3 && Y3 < h3) {
-          l3[((long)b * P + q) * (h3 * w3) + Y3 * w3 + X3] = v3;
+          l3[((long)b * P + q) * (h3 * w3) + Y3 * w3 + X3] = cvt_out<T>(v3);
         }
       }
     }
@@ -193,68 +203,60 @@ __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restric
 }
 
 struct LevelPtrs {
-  const float* p[8];
+  const void* p[4];
 };
 
-// blockDim = 256 (4 queries / block); lane = level*16 + i
-__global__ __launch_bounds__(256) void corr_lookup_kernel(LevelPtrs lv, int nlev, int total, int h, int w, int radius,
+// blockDim = 256 (4 queries / block); lane = level*16 + window column i.
+template <int R, typename T>
+__global__ __launch_bounds__(256) void corr_lookup_kernel(LevelPtrs lv, int nlev, int total, int h, int w,
                                                           const float* __restrict__ coords, bf16* __restrict__ out,
                                                           int ocs) {
+  constexpr int S = 2 * R + 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
   bf16* stage = (bf16*)dyn_smem;  // [4][ocs]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = blockIdx.x * 4 + wave;
-  const int S = 2 * radius + 1;
   bf16* st = stage + wave * ocs;
-  // zero the staging row (covers channel padding)
   for (int c = lane; c < ocs; c += 64) st[c] = f2bf(0.f);
-  __syncthreads();
-  if (q < total) {
-    const int P = h * w;
-    const int b = q / P;
-    const int lvl = lane >> 4;
-    const int i = lane & 15;
+  const int lvl = lane >> 4;
+  const int i = lane & 15;
+  float vv[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) vv[j] = 0.f;
+  float fx = 0.f;
+  if (q < total && lvl < nlev && i <= S) {
     const float x = coords[2 * (long)q];
     const float y = coords[2 * (long)q + 1];
-    float vv[16];
+    const float sc = 1.0f / (float)(1 << lvl);
+    const float cx = x * sc, cy = y * sc;
+    const float flx = floorf(cx), fly = floorf(cy);
+    fx = cx - flx;
+    const float fy = cy - fly;
+    const int hl = h >> lvl, wl = w >> lvl;
+    const int col = (int)flx - R + i;
+    const int row0 = (int)fly - R;
+    const T* map = (const T*)lv.p[lvl] + (long)q * (hl * wl);
+    const bool colok = (unsigned)col < (unsigned)wl;
+    float colv[S + 1];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) vv[j] = 0.f;
-    float fx = 0.f;
-    const bool lane_on = lvl < nlev && i <= S;
-    if (lane_on) {
-      const float sc = 1.0f / (float)(1 << lvl);
-      const float cx = x * sc, cy = y * sc;
-      const float flx = floorf(cx), fly = floorf(cy);
-      fx = cx - flx;
-      const float fy = cy - fly;
-      const int hl = h >> lvl, wl = w >> lvl;
-      const int col = (int)flx - radius + i;
-      const int row0 = (int)fly - radius;
-      const float* map = lv.p[lvl] + (long)q * (hl * wl) - (long)b * 0;  // level maps are [B*P][hl][wl]
-      const bool colok = (unsigned)col < (unsigned)wl;
-      float prev = 0.f;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        if (j <= S) {
-          const int rr = row0 + j;
-          const float cur = (colok && (unsigned)rr < (unsigned)hl) ? map[rr * wl + col] : 0.f;
-          if (j > 0) vv[j - 1] = (1.f - fy) * prev + fy * cur;
-          prev = cur;
-        }
-      }
+    for (int j = 0; j <= S; ++j) {
+      const int rr = row0 + j;
+      colv[j] = (colok && (unsigned)rr < (unsigned)hl) ? to_f(map[rr * wl + col]) : 0.f;
     }
-    // horizontal interpolation with the neighbouring column (lane + 1)
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float nb = __shfl_down(vv[j], 1);
-      vv[j] = (1.f - fx) * vv[j] + fx * nb;
-    }
-    if (lvl < nlev && i < S) {
-      const int base = lvl * S * S + i * S;
+    for (int j = 0; j < S; ++j) vv[j] = (1.f - fy) * colv[j] + fy * colv[j + 1];
+  }
+  // horizontal interpolation with the neighbouring column (lane + 1)
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (j < S) st[base + j] = f2bf(vv[j]);
-    }
+  for (int j = 0; j < S; ++j) {
+    const float nb = __shfl_down(vv[j], 1);
+    vv[j] = (1.f - fx) * vv[j] + fx * nb;
+  }
+  __syncthreads();
+  if (q < total && lvl < nlev && i < S) {
+    const int base = lvl * S * S + i * S;
+#pragma unroll
+    for (int j = 0; j < S; ++j) st[base + j] = f2bf(vv[j]);
   }
   __syncthreads();
   if (q < total) {
@@ -263,30 +265,45 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LevelPtrs lv, int nlev
   }
 }
 
+template <typename T>
+int launch_lookup(const LevelPtrs& lv, int L, int total, int h, int w, int r, const float* coords, bf16* out, int ocs,
+                  hipStream_t stream) {
+  dim3 grid((total + 3) / 4);
+  const size_t smem = 4 * ocs * sizeof(bf16);
+  switch (r) {
+#define JR_LK(RR) case RR: hipLaunchKernelGGL((corr_lookup_kernel<RR, T>), grid, dim3(256), smem, stream, lv, L, total, h, w, coords, out, ocs); break;
+    JR_LK(1) JR_LK(2) JR_LK(3) JR_LK(4) JR_LK(5) JR_LK(6)
+#undef JR_LK
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
-extern "C" int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int w, int C, int cs, float* lvl0,
-                               float* lvl1, float* lvl2, float* lvl3, int num_levels, float scale,
+extern "C" int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int w, int C, int cs, void* lvl0,
+                               void* lvl1, void* lvl2, void* lvl3, int num_levels, float scale, int out_bf16,
                                hipStream_t stream) {
   if (C % BK != 0 || cs % 8 != 0 || num_levels < 1 || num_levels > 4) return (int)hipErrorInvalidValue;
   const int P = h * w;
   dim3 grid((P + CQ - 1) / CQ, ((h + TY - 1) / TY) * ((w + TX - 1) / TX), B);
-  hipLaunchKernelGGL(corr_pyramid_kernel, grid, dim3(256), 0, stream, (const bf16*)f1, (const bf16*)f2, h, w, C, cs,
-                     lvl0, lvl1, lvl2, lvl3, num_levels, scale);
+  if (out_bf16)
+    hipLaunchKernelGGL(corr_pyramid_kernel<bf16>, grid, dim3(256), 0, stream, (const bf16*)f1, (const bf16*)f2, h, w, C,
+                       cs, (bf16*)lvl0, (bf16*)lvl1, (bf16*)lvl2, (bf16*)lvl3, num_levels, scale);
+  else
+    hipLaunchKernelGGL(corr_pyramid_kernel<float>, grid, dim3(256), 0, stream, (const bf16*)f1, (const bf16*)f2, h, w,
+                       C, cs, (float*)lvl0, (float*)lvl1, (float*)lvl2, (float*)lvl3, num_levels, scale);
   return (int)hipGetLastError();
 }
 
-extern "C" int jr_corr_lookup(const float* const* levels, int num_levels, int B, int h, int w, int radius,
-                              const float* coords, void* out, int out_cstride, hipStream_t stream) {
+extern "C" int jr_corr_lookup(const void* const* levels, int num_levels, int B, int h, int w, int radius,
+                              const float* coords, void* out, int out_cstride, int lv_bf16, hipStream_t stream) {
   const int S = 2 * radius + 1;
-  if (num_levels > 4 || S + 1 > 16 || out_cstride % 8 != 0 || out_cstride < num_levels * S * S)
+  if (num_levels > 4 || radius < 1 || radius > 6 || out_cstride % 8 != 0 || out_cstride < num_levels * S * S)
     return (int)hipErrorInvalidValue;
   LevelPtrs lv;
-  for (int l = 0; l < 8; ++l) lv.p[l] = l < num_levels ? levels[l] : nullptr;
+  for (int l = 0; l < 4; ++l) lv.p[l] = l < num_levels ? levels[l] : nullptr;
   const int total = B * h * w;
-  dim3 grid((total + 3) / 4);
-  const size_t smem = 4 * out_cstride * sizeof(bf16);
-  hipLaunchKernelGGL(corr_lookup_kernel, grid, dim3(256), smem, stream, lv, num_levels, total, h, w, radius, coords,
-                     (bf16*)out, out_cstride);
-  return (int)hipGetLastError();
+  if (lv_bf16) return launch_lookup<bf16>(lv, num_levels, total, h, w, radius, coords, (bf16*)out, out_cstride, stream);
+  return launch_lookup<float>(lv, num_levels, total, h, w, radius, coords, (bf16*)out, out_cstride, stream);
 }

@@ -75,9 +75,14 @@ __global__ void upsample_bilinear_kernel(const float* __restrict__ flow, int B, 
   ((float2*)out)[idx] = make_float2(8.f * (top_x + wy * (bot_x - top_x)), 8.f * (top_y + wy * (bot_y - top_y)));
 }
 
-// stats[n][c][0..1] += sum / sumsq.  blockDim 256; C/8 threads per row.
-__global__ __launch_bounds__(256) void channel_stats_kernel(const bf16* __restrict__ x, int HW, int C, int rows_per_block,
-                                                            float* __restrict__ stats) {
+// Deterministic per-(n, c) statistics: pass 1 writes one (sum, sumsq) partial
+// per block (fixed row ranges), pass 2 sums the partials in order.  No float
+// atomics, so eager and graph-replayed forwards are bitwise identical.
+// blockDim 256; C/8 threads per row.
+constexpr int STATS_ROWS = 1024;
+
+__global__ __launch_bounds__(256) void channel_stats_partial_kernel(const bf16* __restrict__ x, int HW, int C,
+                                                                    float* __restrict__ part) {
   __shared__ float red[256][17];
   const int n = blockIdx.y;
   const int cg = C >> 3;
@@ -85,8 +90,8 @@ __global__ __launch_bounds__(256) void channel_stats_kernel(const bf16* __restri
   const int g = tid % cg;
   const int rg = tid / cg;
   const int nrg = 256 / cg;
-  const int r0 = blockIdx.x * rows_per_block;
-  const int r1 = min(r0 + rows_per_block, HW);
+  const int r0 = blockIdx.x * STATS_ROWS;
+  const int r1 = min(r0 + STATS_ROWS, HW);
   float s[8], q[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
@@ -105,14 +110,27 @@ __global__ __launch_bounds__(256) void channel_stats_kernel(const bf16* __restri
 #pragma unroll
   for (int j = 0; j < 8; ++j) { red[tid][j] = s[j]; red[tid][8 + j] = q[j]; }
   __syncthreads();
-  // reduce over row-groups: thread t < cg*16 handles (group t%cg, value t/cg)
+  // thread t < cg*16 reduces (channel group t%cg, value t/cg) over the row groups in order
+  const int nb = gridDim.x;
   for (int t = tid; t < cg * 16; t += 256) {
     const int gg = t % cg, vi = t / cg;
     float acc = 0.f;
     for (int k = 0; k < nrg; ++k) acc += red[k * cg + gg][vi];
     const int c = gg * 8 + (vi & 7);
-    atomicAdd(&stats[((long)n * C + c) * 2 + (vi >> 3)], acc);
+    part[(((long)n * nb + blockIdx.x) * C + c) * 2 + (vi >> 3)] = acc;
   }
+}
+
+__global__ void channel_stats_final_kernel(const float* __restrict__ part, int N, int nb, int C,
+                                           float* __restrict__ stats) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * C * 2) return;
+  const int v = idx & 1;
+  const int c = (idx >> 1) % C;
+  const int n = (idx >> 1) / C;
+  float acc = 0.f;
+  for (int b = 0; b < nb; ++b) acc += part[(((long)n * nb + b) * C + c) * 2 + v];
+  stats[idx] = acc;
 }
 
 // y = act(xn + rn): 8 channels per thread
@@ -222,13 +240,17 @@ extern "C" int jr_upsample_bilinear(const float* flow, int B, int h, int w, floa
   return (int)hipGetLastError();
 }
 
-extern "C" int jr_channel_stats(const void* x, int N, int HW, int C, float* stats, hipStream_t stream) {
-  if (C % 8 != 0 || C > 2048 || (C / 8) > 256) return (int)hipErrorInvalidValue;
-  const int rows_per_block = 1024;
-  dim3 grid((HW + rows_per_block - 1) / rows_per_block, N);
-  hipLaunchKernelGGL(channel_stats_kernel, grid, dim3(256), 0, stream, (const bf16*)x, HW, C, rows_per_block, stats);
+extern "C" int jr_channel_stats(const void* x, int N, int HW, int C, float* stats, float* partial,
+                                hipStream_t stream) {
+  if (C % 8 != 0 || (C / 8) > 256) return (int)hipErrorInvalidValue;
+  const int nb = (HW + STATS_ROWS - 1) / STATS_ROWS;
+  hipLaunchKernelGGL(channel_stats_partial_kernel, dim3(nb, N), dim3(256), 0, stream, (const bf16*)x, HW, C, partial);
+  hipLaunchKernelGGL(channel_stats_final_kernel, dim3(nblk((long)N * C * 2, 256)), dim3(256), 0, stream, partial, N,
+                     nb, C, stats);
   return (int)hipGetLastError();
 }
+
+extern "C" int jr_channel_stats_partials(int N, int HW) { return N * ((HW + STATS_ROWS - 1) / STATS_ROWS); }
 
 extern "C" int jr_norm_act(const void* x, const float* sx, int mode_x, const float* gamma, const float* beta,
                            const void* res, const float* sr, int mode_r, const float* gamma_r, const float* beta_r,

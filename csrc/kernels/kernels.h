@@ -28,6 +28,8 @@ struct ConvParams {
   int KH, KW, SH, SW, PH, PW;
   int OH, OW;
   int M;            // N*OH*OW
+  long x_bytes;     // bytes addressable through x (buffer range check, <= 2 GiB)
+  long w_bytes;     // bytes of w
   // packed weights [cout_pad][kpad] bf16 and fp32 bias [cout]
   const void* w;
   int kpad;         // multiple of 64
@@ -54,14 +56,17 @@ struct ConvParams {
   void* y3; int y3_cstride, y3_coff;  // FLOW: third bf16 flow copy
 };
 
-// cfg: 0 = 128co x 128px, 1 = 64co x 128px, 2 = 128co x 64px, 3 = 16co x 256px, 4 = 64co x 64px
+// cfg: 0 = 128co x 128px, 1 = 64co x 128px, 2 = 128co x 64px, 3 = 16co x 256px, 4 = 64co x 64px,
+//      5 = 16co x 64px (narrow outputs, e.g. the 2-channel flow head)
 int jr_conv_forward(const ConvParams* p, int cfg, int epi, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
 // Instance/batch-norm statistics and normalisation.
 // ---------------------------------------------------------------------------
-// stats[n][c][2] += (sum, sumsq) over pixels of x (bf16 NHWC, C channels, contiguous).
-int jr_channel_stats(const void* x, int N, int HW, int C, float* stats, hipStream_t stream);
+// stats[n][c][2] = (sum, sumsq) over pixels of x (bf16 NHWC, C channels, contiguous), deterministic
+// two-pass reduction; `partial` must hold jr_channel_stats_partials(N, HW) * C * 2 floats.
+int jr_channel_stats(const void* x, int N, int HW, int C, float* stats, float* partial, hipStream_t stream);
+int jr_channel_stats_partials(int N, int HW);
 // y = post( pre(xn) + rn ), xn = (x - mean_x) * rstd_x * gamma + beta (mode_x), rn likewise for res.
 // mode: 0 = identity, 1 = instance (stats per n), 2 = batch (stats summed over n).
 // relu bit 0: relu on xn before the residual add; bit 1: relu on the sum.
@@ -72,14 +77,14 @@ int jr_norm_act(const void* x, const float* sx, int mode_x, const float* gamma, 
 // ---------------------------------------------------------------------------
 // Correlation pyramid (MFMA all-pairs GEMM, pooling fused) and lookup.
 // ---------------------------------------------------------------------------
-// f1, f2: bf16 [B][h*w][C] (channel stride cs).  levels[l]: fp32 [B][h*w][h_l][w_l].
+// f1, f2: bf16 [B][h*w][C] (channel stride cs).  levels[l]: fp32 or bf16 [B][h*w][h_l][w_l].
 int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int w, int C, int cs,
-                    float* lvl0, float* lvl1, float* lvl2, float* lvl3, int num_levels, float scale,
+                    void* lvl0, void* lvl1, void* lvl2, void* lvl3, int num_levels, float scale, int out_bf16,
                     hipStream_t stream);
 // coords fp32 [B][h*w][2]; out bf16 [B*h*w][out_cstride] channels l*(2r+1)^2 + i*(2r+1) + j,
-// zero-filled up to out_cstride.
-int jr_corr_lookup(const float* const* levels, int num_levels, int B, int h, int w, int radius,
-                   const float* coords, void* out, int out_cstride, hipStream_t stream);
+// zero-filled up to out_cstride.  radius 1..6.
+int jr_corr_lookup(const void* const* levels, int num_levels, int B, int h, int w, int radius,
+                   const float* coords, void* out, int out_cstride, int lv_bf16, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
 // Flow upsampling x8.

@@ -77,6 +77,9 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   p.OH = (p.H + 2 * p.PH - p.KH) / p.SH + 1;
   p.OW = (p.W + 2 * p.PW - p.KW) / p.SW + 1;
   p.M = p.N * p.OH * p.OW;
+  p.x_bytes = x.numel() * 2;
+  p.w_bytes = w.numel() * 2;
+  TORCH_CHECK(p.x_bytes <= (1LL << 31) && p.w_bytes <= (1LL << 31), "conv: operand larger than 2 GiB");
   p.w = w.data_ptr(); p.kpad = (int)w.size(1); p.cout_pad = (int)w.size(0);
   p.nkc = p.KH * p.KW * p.cin8 / 8;
   p.cout = (int)i[11]; p.bias = bias.data_ptr<float>(); p.alpha = (float)alpha;
@@ -121,13 +124,18 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   } else {
     TORCH_CHECK(false, "conv: unknown epilogue ", epi);
   }
-  TORCH_CHECK(cfg >= 0 && cfg <= 4, "conv: unknown tile config ", cfg);
+  TORCH_CHECK(cfg >= 0 && cfg <= 5, "conv: unknown tile config ", cfg);
   if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3}) if (v.defined()) keep->push_back(v);
   return [p, epi, cfg](hipStream_t s, int) { return jr_conv_forward(&p, cfg, epi, s); };
 }
 
 // --------------------------------------------------------------- correlation
-// t = [f1, f2, l0, l1, l2, l3], i = [B, h, w, C, num_levels]
+// t = [f1, f2, l0, l1, l2, l3], i = [B, h, w, C, num_levels]; levels all fp32 or all bf16
+static void check_level(const at::Tensor& v, at::ScalarType dt) {
+  TORCH_CHECK(v.defined() && v.is_cuda() && v.is_contiguous(), "pyramid level must be a contiguous GPU tensor");
+  TORCH_CHECK(v.scalar_type() == dt && (dt == at::kFloat || dt == at::kBFloat16), "pyramid levels: fp32 or bf16, one dtype");
+}
+
 static Launch make_corr(const TList& t, const IList& i, double scale, std::vector<at::Tensor>* keep) {
   at::Tensor f1 = opt(t, 0), f2 = opt(t, 1);
   check_bf16(f1, "f1"); check_bf16(f2, "f2");
@@ -135,13 +143,16 @@ static Launch make_corr(const TList& t, const IList& i, double scale, std::vecto
   TORCH_CHECK(L >= 1 && L <= 4, "corr: 1..4 levels");
   TORCH_CHECK(C % 64 == 0, "corr: feature channels must be a multiple of 64");
   TORCH_CHECK(f1.numel() >= (int64_t)B * h * w * cs(f1) && f2.numel() == f1.numel() && cs(f1) == cs(f2), "corr: fmap shapes");
-  float* lv[4] = {nullptr, nullptr, nullptr, nullptr};
+  void* lv[4] = {nullptr, nullptr, nullptr, nullptr};
+  at::Tensor l0 = opt(t, 2);
+  TORCH_CHECK(l0.defined(), "corr: level 0 missing");
+  const at::ScalarType dt = l0.scalar_type();
   int hl = h, wl = w;
   for (int l = 0; l < L; ++l) {
     at::Tensor v = opt(t, 2 + l);
-    check_f32(v, "level");
+    check_level(v, dt);
     TORCH_CHECK(v.numel() >= (int64_t)B * h * w * hl * wl, "corr: level ", l, " too small");
-    lv[l] = v.data_ptr<float>();
+    lv[l] = v.data_ptr();
     if (keep) keep->push_back(v);
     hl >>= 1; wl >>= 1;
   }
@@ -150,7 +161,8 @@ static Launch make_corr(const TList& t, const IList& i, double scale, std::vecto
   const void* b = f2.data_ptr();
   const int fcs = cs(f1);
   const float sc = (float)scale;
-  return [=](hipStream_t s, int) { return jr_corr_pyramid(a, b, B, h, w, C, fcs, lv[0], lv[1], lv[2], lv[3], L, sc, s); };
+  const int obf = dt == at::kBFloat16;
+  return [=](hipStream_t s, int) { return jr_corr_pyramid(a, b, B, h, w, C, fcs, lv[0], lv[1], lv[2], lv[3], L, sc, obf, s); };
 }
 
 // t = [coords, out, l0, l1, l2, l3], i = [num_levels, B, h, w, radius]
@@ -159,17 +171,20 @@ static Launch make_lookup(const TList& t, const IList& i, std::vector<at::Tensor
   check_f32(coords, "coords"); check_bf16(out, "out");
   const int L = (int)i[0], B = (int)i[1], h = (int)i[2], w = (int)i[3], r = (int)i[4];
   const int S = 2 * r + 1;
-  TORCH_CHECK(L >= 1 && L <= 4 && S + 1 <= 16, "lookup: levels / radius out of range");
+  TORCH_CHECK(L >= 1 && L <= 4 && r >= 1 && r <= 6, "lookup: levels 1..4, radius 1..6");
   TORCH_CHECK(cs(out) % 8 == 0 && cs(out) >= L * S * S, "lookup: output channel stride");
   TORCH_CHECK(out.numel() >= (int64_t)B * h * w * cs(out) && coords.numel() >= (int64_t)B * h * w * 2, "lookup: sizes");
-  std::vector<const float*> lv(4, nullptr);
+  std::vector<const void*> lv(4, nullptr);
+  at::Tensor l0 = opt(t, 2);
+  TORCH_CHECK(l0.defined(), "lookup: level 0 missing");
+  const at::ScalarType dt = l0.scalar_type();
   int hl = h, wl = w;
   for (int l = 0; l < L; ++l) {
     at::Tensor v = opt(t, 2 + l);
-    check_f32(v, "level");
+    check_level(v, dt);
     TORCH_CHECK(hl >= 2 && wl >= 2, "lookup: pyramid level too small");
     TORCH_CHECK(v.numel() >= (int64_t)B * h * w * hl * wl, "lookup: level size");
-    lv[l] = v.data_ptr<float>();
+    lv[l] = v.data_ptr();
     if (keep) keep->push_back(v);
     hl >>= 1; wl >>= 1;
   }
@@ -177,7 +192,8 @@ static Launch make_lookup(const TList& t, const IList& i, std::vector<at::Tensor
   const float* cp = coords.data_ptr<float>();
   void* op = out.data_ptr();
   const int ocs = cs(out);
-  return [=](hipStream_t s, int) { return jr_corr_lookup(lv.data(), L, B, h, w, r, cp, op, ocs, s); };
+  const int lbf = dt == at::kBFloat16;
+  return [=](hipStream_t s, int) { return jr_corr_lookup(lv.data(), L, B, h, w, r, cp, op, ocs, lbf, s); };
 }
 
 // ------------------------------------------------------------------ upsample
@@ -221,22 +237,23 @@ static Launch make_upsample_bilinear(const TList& t, const IList& i, std::vector
 }
 
 // ---------------------------------------------------------------------- norm
-// t = [x, stats], i = [N, HW, C]
+// t = [x, stats, partial?], i = [N, HW, C]; the partial workspace is allocated
+// here when not given (eager use), never inside a launch (capture safety).
 static Launch make_stats(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
-  at::Tensor x = opt(t, 0), st = opt(t, 1);
+  at::Tensor x = opt(t, 0), st = opt(t, 1), part = opt(t, 2);
   check_bf16(x, "x"); check_f32(st, "stats");
   const int N = (int)i[0], HW = (int)i[1], C = (int)i[2];
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && cs(x) == C && x.numel() >= (int64_t)N * HW * C, "stats: shape");
   TORCH_CHECK(st.numel() >= (int64_t)N * C * 2, "stats: buffer too small");
-  if (keep) { keep->push_back(x); keep->push_back(st); }
+  const int64_t need = (int64_t)jr_channel_stats_partials(N, HW) * C * 2;
+  if (!part.defined()) part = at::empty({need}, st.options());
+  check_f32(part, "partial");
+  TORCH_CHECK(part.numel() >= need, "stats: partial workspace too small");
+  if (keep) { keep->push_back(x); keep->push_back(st); keep->push_back(part); }
   const void* xp = x.data_ptr();
   float* sp = st.data_ptr<float>();
-  const size_t bytes = (size_t)N * C * 2 * sizeof(float);
-  return [=](hipStream_t s, int) {
-    hipError_t e = hipMemsetAsync(sp, 0, bytes, s);
-    if (e != hipSuccess) return (int)e;
-    return jr_channel_stats(xp, N, HW, C, sp, s);
-  };
+  float* pp = part.data_ptr<float>();
+  return [=](hipStream_t s, int) { return jr_channel_stats(xp, N, HW, C, sp, pp, s); };
 }
 
 // t = [x, sx, gx, bx, r, sr, gr, br, y], i = [mode_x, mode_r, N, HW, C, relu]
@@ -332,7 +349,10 @@ void corr_op(const TList& t, IList i, double scale) { run_now(make_corr(t, i, sc
 void lookup_op(const TList& t, IList i) { run_now(make_lookup(t, i, nullptr)); }
 void upsample_convex_op(const TList& t, IList i) { run_now(make_upsample_convex(t, i, nullptr)); }
 void upsample_bilinear_op(const TList& t, IList i) { run_now(make_upsample_bilinear(t, i, nullptr)); }
-void stats_op(const TList& t, IList i) { run_now(make_stats(t, i, nullptr)); }
+void stats_op(const TList& t, IList i) {
+  std::vector<at::Tensor> keep;  // keeps an internally allocated workspace alive until the launch is queued
+  run_now(make_stats(t, i, &keep));
+}
 void norm_act_op(const TList& t, IList i, double eps) { run_now(make_norm_act(t, i, eps, nullptr)); }
 void prep_op(const TList& t, IList i) { run_now(make_prep(t, i, nullptr)); }
 void init_coords_op(const TList& t, IList i) { run_now(make_init_coords(t, i, nullptr)); }

@@ -25,7 +25,7 @@ _load_error: Optional[BaseException] = None
 ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, ACT_SPLIT_TANH_RELU = 0, 1, 2, 3, 4
 EPI_STD, EPI_GRU_A, EPI_GRU_B, EPI_FLOW = 0, 1, 2, 3
 # tile configs of conv_igemm.hip: (BCO, BP)
-CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (16, 256), 4: (64, 64)}
+CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (16, 256), 4: (64, 64), 5: (16, 64)}
 NUM_CUS = 256
 
 
@@ -138,7 +138,7 @@ def pick_cfg(M: int, cout: int) -> int:
     tile's per-FLOP cost rises as it shrinks; keeps >= one wave of blocks over
     256 CUs whenever the problem allows."""
     if cout <= 16:
-        return 3
+        return 5
     best, best_cost = 0, None
     # (cfg, relative per-FLOP efficiency of the tile); time ~ blocks per CU x tile area / eff
     for cfg, eff in ((0, 1.0), (2, 0.85), (1, 0.85), (4, 0.65)):

@@ -53,6 +53,27 @@ from ..ops.native import (
 BF16 = torch.bfloat16
 F32 = torch.float32
 
+_TUNE_CACHE: Dict[tuple, int] = {}
+
+
+def _tune(spec: ConvSpec, x, N, H, W, y, kw, reps: int = 5) -> int:
+    """Time every tile config of one conv problem; return the fastest."""
+    ops = nat.ops()
+    best, best_t = None, None
+    for cfg in sorted(nat.CFG_TILES):
+        args = conv_args(spec, x, N, H, W, y, **dict(kw, cfg=cfg))
+        ops.conv(*args)  # warm (and JIT-free: all configs are precompiled)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            ops.conv(*args)
+        e.record()
+        e.synchronize()
+        t = s.elapsed_time(e)
+        if best_t is None or t < best_t:
+            best, best_t = cfg, t
+    return best
+
 
 def _fold_bn(cna: ConvNormActivation) -> Tuple[torch.Tensor, torch.Tensor]:
     """Conv kernel/bias with an eval-mode BatchNorm folded in."""
@@ -92,14 +113,22 @@ class RaftEngine:
             hipGraph and replay it (default); otherwise launch from C++ eagerly.
         copy_output: return a fresh tensor (default) instead of the engine's
             static output buffer (which the next call overwrites).
+        corr_dtype: storage dtype of the correlation pyramid (bf16 default:
+            the lookup output feeding the bf16 MFMA convs is bf16 anyway;
+            fp32 for bit-closer parity with the fp32 reference).
+        autotune: time every conv tile config on the real buffers when a plan
+            is built and keep the fastest (cached per problem signature).
     """
 
-    def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True):
+    def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True,
+                 corr_dtype: torch.dtype = torch.bfloat16, autotune: bool = True):
         nat.require()
         self.model = model
         self.device = torch.device(device)
         self.use_graph = use_graph
         self.copy_output = copy_output
+        self.corr_dtype = corr_dtype
+        self.autotune = autotune
         self._specs: Dict[str, ConvSpec] = {}
         self._sources: Dict[str, callable] = {}
         self._states: Dict[Tuple[int, int, int, int], _PlanState] = {}
@@ -220,6 +249,20 @@ class RaftEngine:
             self._reg("fh1", conv_src(fh.conv1))
         self._reg("fh2", conv_src(fh.conv2))
 
+    # ------------------------------------------------------------- autotune
+    def _conv(self, plan, spec: ConvSpec, x, N, H, W, y, **kw):
+        """Append one conv to ``plan``, choosing its tile config (autotuned)."""
+        if self.autotune and kw.get("cfg") is None:
+            OH, OW = spec.out_hw(H, W)
+            key = (N * OH * OW, spec.cout, spec.kh, spec.kw, spec.sh, spec.sw, spec.cin8, x.shape[-1],
+                   kw.get("epi", EPI_STD), str(self.device))
+            cfg = _TUNE_CACHE.get(key)
+            if cfg is None:
+                cfg = _tune(spec, x, N, H, W, y, kw)
+                _TUNE_CACHE[key] = cfg
+            kw = dict(kw, cfg=cfg)
+        plan.add_conv(*conv_args(spec, x, N, H, W, y, **kw))
+
     # ------------------------------------------------------------- lowering
     def _encoder(self, st: _PlanState, plan, tag: str, enc: FeatureEncoder, x: torch.Tensor, N: int, H: int,
                  W: int):
@@ -229,7 +272,7 @@ class RaftEngine:
         bufs = st.bufs
 
         def alloc(name, shape, dtype=BF16):
-            t = torch.empty(shape, dtype=dtype, device=self.device)
+            t = torch.zeros(shape, dtype=dtype, device=self.device)
             bufs[name] = t
             return t
 
@@ -237,7 +280,7 @@ class RaftEngine:
             s = sp[name]
             OH, OW = s.out_hw(H, W)
             y = alloc(name + ".y", (N, OH, OW, s.cout))
-            plan.add_conv(*conv_args(s, x, N, H, W, y, act=act, res=res, res_post=res_post))
+            self._conv(plan, s, x, N, H, W, y, act=act, res=res, res_post=res_post)
             return y, OH, OW
 
         def stats(name, y, N, HW, C):
@@ -311,8 +354,8 @@ class RaftEngine:
             f"Feature maps are too small to be down-sampled by the correlation pyramid: need >= {min_sz}, got {(h, w)}; "
             f"input images should be at least {8 * min_sz}.")
 
-        def alloc(name, shape, dtype=BF16, zero=False):
-            t = (torch.zeros if zero else torch.empty)(shape, dtype=dtype, device=dev)
+        def alloc(name, shape, dtype=BF16):
+            t = torch.zeros(shape, dtype=dtype, device=dev)
             bufs[name] = t
             return t
 
@@ -327,11 +370,11 @@ class RaftEngine:
         feat, fh_, fw_ = self._encoder(st, plan, "fe", m.feature_encoder, x0, 2 * B, H, W)
         assert (fh_, fw_) == (h, w), "The feature encoder should downsample H and W by 8"
         fmap = alloc("fmap", (2 * B, h, w, self.fmap_ch))
-        plan.add_conv(*conv_args(sp["fe.conv"], feat, 2 * B, h, w, fmap))
+        self._conv(plan, sp["fe.conv"], feat, 2 * B, h, w, fmap)
         levels = []
         hl, wl = h, w
         for l in range(L):
-            levels.append(alloc(f"corr.l{l}", (M, hl, wl), F32))
+            levels.append(alloc(f"corr.l{l}", (M, hl, wl), self.corr_dtype))
             hl //= 2
             wl //= 2
         plan.add_corr([fmap[:B], fmap[B:]] + levels + [None] * (4 - L), [B, h, w, self.fmap_ch, L],
@@ -348,8 +391,8 @@ class RaftEngine:
             plan.add_memset([t])
         ctxf, ch_, cw_ = self._encoder(st, plan, "ce", m.context_encoder, x0[:B], B, H, W)
         assert (ch_, cw_) == (h, w), "The context encoder should downsample H and W by 8"
-        plan.add_conv(*conv_args(sp["ce.conv"], ctxf, B, h, w, hx, act=ACT_SPLIT_TANH_RELU, split=self.hidden,
-                                 y2=qx, h32=h32, hidden=self.hidden))
+        self._conv(plan, sp["ce.conv"], ctxf, B, h, w, hx, act=ACT_SPLIT_TANH_RELU, split=self.hidden,
+                                 y2=qx, h32=h32, hidden=self.hidden)
         plan.add_init_coords([coords], [B, h, w])
 
         # ---------------- loop body: one refinement iteration (model.py:495-510)
@@ -361,32 +404,32 @@ class RaftEngine:
         cf = alloc("cf", (M, cl[-1] + fl[-1]))
         if len(cl) == 2:
             c1 = alloc("c1", (M, cl[0]))
-            plan.add_conv(*conv_args(sp["me.convcorr1"], corr, B, h, w, c1, act=ACT_RELU))
+            self._conv(plan, sp["me.convcorr1"], corr, B, h, w, c1, act=ACT_RELU)
         else:
-            plan.add_conv(*conv_args(sp["me.convcorr1"], corr, B, h, w, cf, act=ACT_RELU))
+            self._conv(plan, sp["me.convcorr1"], corr, B, h, w, cf, act=ACT_RELU)
         f1 = alloc("f1", (M, fl[0]))
-        plan.add_conv(*conv_args(sp["me.convflow1"], flow8, B, h, w, f1, act=ACT_RELU))
+        self._conv(plan, sp["me.convflow1"], flow8, B, h, w, f1, act=ACT_RELU)
         if len(cl) == 2:
-            plan.add_conv(*conv_args(sp["me.convcorr2"], c1, B, h, w, cf, act=ACT_RELU))
-        plan.add_conv(*conv_args(sp["me.convflow2"], f1, B, h, w, cf, y_coff=cl[-1], act=ACT_RELU))
-        plan.add_conv(*conv_args(sp["me.conv"], cf, B, h, w, hx, y_coff=self.mot_off, act=ACT_RELU, y2=qx,
-                                 y2_coff=self.mot_off))
+            self._conv(plan, sp["me.convcorr2"], c1, B, h, w, cf, act=ACT_RELU)
+        self._conv(plan, sp["me.convflow2"], f1, B, h, w, cf, y_coff=cl[-1], act=ACT_RELU)
+        self._conv(plan, sp["me.conv"], cf, B, h, w, hx, y_coff=self.mot_off, act=ACT_RELU, y2=qx,
+                                 y2_coff=self.mot_off)
         for gi in range(len(m.update_block.recurrent_block.kernel_size)):
-            plan.add_conv(*conv_args(sp[f"gru{gi}.a"], hx, B, h, w, qx, h32=h32, zbuf=zb, hidden=self.hidden,
-                                     epi=EPI_GRU_A))
-            plan.add_conv(*conv_args(sp[f"gru{gi}.b"], qx, B, h, w, hx, h32=h32, zbuf=zb, hidden=self.hidden,
-                                     epi=EPI_GRU_B))
+            self._conv(plan, sp[f"gru{gi}.a"], hx, B, h, w, qx, h32=h32, zbuf=zb, hidden=self.hidden,
+                                     epi=EPI_GRU_A)
+            self._conv(plan, sp[f"gru{gi}.b"], qx, B, h, w, hx, h32=h32, zbuf=zb, hidden=self.hidden,
+                                     epi=EPI_GRU_B)
         s1 = sp["fh1"]
         fm = alloc("fm", (M, round_up(s1.cout, 8)))
-        plan.add_conv(*conv_args(s1, hx, B, h, w, fm, act=ACT_RELU))
+        self._conv(plan, s1, hx, B, h, w, fm, act=ACT_RELU)
         # flow head conv2 + coordinate update (model.py:505) + flow into hx/qx/flow8
-        plan.add_conv(*conv_args(sp["fh2"], fm, B, h, w, hx, y_coff=self.flow_off, y2=qx, y2_coff=self.flow_off,
-                                 y3=flow8, y3_coff=0, coords=coords, flow32=flow32, epi=EPI_FLOW))
+        self._conv(plan, sp["fh2"], fm, B, h, w, hx, y_coff=self.flow_off, y2=qx, y2_coff=self.flow_off,
+                                 y3=flow8, y3_coff=0, coords=coords, flow32=flow32, epi=EPI_FLOW)
         stride = B * H * W * 2
         if self.has_mask:
             mask = alloc("mask", (M, 576))
-            plan.add_conv(*conv_args(sp["mask"], fm, B, h, w, mask, x_coff=self.fh_hidden,
-                                     alpha=m.mask_predictor.multiplier))
+            self._conv(plan, sp["mask"], fm, B, h, w, mask, x_coff=self.fh_hidden,
+                                     alpha=m.mask_predictor.multiplier)
             plan.add_upsample_convex([mask, flow32, st.out], [B, h, w, stride])
         else:
             plan.add_upsample_bilinear([flow32, st.out], [B, h, w, stride])

@@ -65,3 +65,15 @@ def test_weight_update_repacks():
     b = model(i1, i2, num_flow_updates=2)
     torch.cuda.synchronize()
     assert (a - b).abs().max().item() > 1.0
+
+
+def test_engine_fp32_pyramid_closer_to_golden():
+    model, variables = raft_large()
+    i1, i2 = _inputs(1, 128, 128, seed=5)
+    ref = model.apply(variables, i1, i2, num_flow_updates=3)
+    model = model.cuda()
+    out32 = model(i1.cuda(), i2.cuda(), num_flow_updates=3, corr_dtype=torch.float32).cpu()
+    out16 = model(i1.cuda(), i2.cuda(), num_flow_updates=3).cpu()
+    mag = ref.norm(dim=-1).mean().item()
+    assert _epe(out32[-1], ref[-1]) < 0.05 * mag + 0.05
+    assert _epe(out16[-1], ref[-1]) < 0.05 * mag + 0.05

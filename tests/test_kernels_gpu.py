@@ -231,8 +231,9 @@ def test_upsample_convex_and_bilinear():
     nat.ops().upsample_convex([mask.reshape(M, 576).to(DEV, torch.bfloat16).contiguous(),
                                flow.reshape(M, 2).to(DEV).contiguous(), out], [B, h, w, B * 64 * h * w * 2])
     torch.cuda.synchronize()
-    assert (out[1].cpu() - ref).abs().max().item() < 1e-3 * ref.abs().max().item() + 1e-4
-    assert (out[0] == 0).all()
+    # eager ops run as iteration 0 of a plan: the per-iteration stride only applies inside plans
+    assert (out[0].cpu() - ref).abs().max().item() < 1e-3 * ref.abs().max().item() + 1e-4
+    assert (out[1] == 0).all()
     refb = R.upsample_flow(flow, None)
     outb = torch.zeros(1, B, 8 * h, 8 * w, 2, device=DEV)
     nat.ops().upsample_bilinear([flow.reshape(M, 2).to(DEV).contiguous(), outb], [B, h, w, 0])

@@ -1,0 +1,119 @@
+#!/usr/bin/env python3
+"""Per-kernel microbenchmarks at the headline shapes (raft_large, 440x1024,
+batch 4 -> fmap 55x128, M = 28160 query pixels).  Times every loop-body conv
+under each tile config, the lookup, the correlation build and the upsample
+with hip events; prints a table (and JSON with --json)."""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from jax_raft_amd.ops import native as nat  # noqa: E402
+
+
+def timeit(fn, iters=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1000.0  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--h", type=int, default=55)
+    ap.add_argument("--w", type=int, default=128)
+    ap.add_argument("--only", default="")
+    ap.add_argument("--json", default="")
+    args = ap.parse_args()
+    nat.require()
+    dev = "cuda"
+    B, h, w = args.batch, args.h, args.w
+    M = B * h * w
+    torch.manual_seed(0)
+    res = {}
+
+    def rnd(*s, dtype=torch.bfloat16):
+        return torch.randn(*s, device=dev).to(dtype)
+
+    # ------------------------------------------------------------- convs
+    convs = [
+        # name, cin, cin8/x_cs, cout, kh, kw, pad
+        ("convcorr1", 324, 328, 256, 1, 1, (0, 0)),
+        ("convflow1", 2, 8, 128, 7, 7, (3, 3)),
+        ("convcorr2", 256, 256, 192, 3, 3, (1, 1)),
+        ("convflow2", 128, 128, 64, 3, 3, (1, 1)),
+        ("me.conv", 256, 256, 126, 3, 3, (1, 1)),
+        ("gru.a(1x5)", 384, 384, 256, 1, 5, (0, 2)),
+        ("gru.b(1x5)", 384, 384, 128, 1, 5, (0, 2)),
+        ("gru.a(5x1)", 384, 384, 256, 5, 1, (2, 0)),
+        ("fh1+mask1", 128, 128, 512, 3, 3, (1, 1)),
+        ("fh2", 256, 256, 2, 3, 3, (1, 1)),
+        ("mask2", 256, 256, 576, 1, 1, (0, 0)),
+    ]
+    for name, cin, cs, cout, kh, kw, pad in convs:
+        if args.only and args.only not in name:
+            continue
+        k = torch.randn(kh, kw, cin, cout) / math.sqrt(kh * kw * cin)
+        b = torch.randn(cout) * 0.1
+        spec = nat.make_spec(k, b, (1, 1), pad, cin8=cs, device=dev)
+        x = rnd(B, h, w, cs)
+        y = torch.empty(M, nat.round_up(cout, 8), device=dev, dtype=torch.bfloat16)
+        flops = 2.0 * M * cout * kh * kw * cin
+        row = {}
+        for cfg in sorted(nat.CFG_TILES):
+            t, i, a = nat.conv_args(spec, x, B, h, w, y, act=nat.ACT_RELU, cfg=cfg)
+            us = timeit(lambda: nat.ops().conv(t, i, a))
+            row[cfg] = us
+        best = min(row, key=row.get)
+        res[name] = {"us": row, "best_cfg": best, "tflops": flops / row[best] / 1e6, "heuristic": nat.pick_cfg(M, cout)}
+        print(f"{name:12s} " + " ".join(f"c{c}={u:7.1f}" for c, u in row.items()) +
+              f"  best=c{best} {flops / row[best] / 1e6:7.1f} TF/s  heur=c{nat.pick_cfg(M, cout)}", flush=True)
+
+    # ------------------------------------------------------------- correlation
+    if not args.only or "corr" in args.only or "lookup" in args.only:
+        C = 256
+        f = rnd(2 * B, h, w, C)
+        lv = []
+        hl, wl = h, w
+        for _ in range(4):
+            lv.append(torch.empty(M, hl, wl, device=dev))
+            hl //= 2
+            wl //= 2
+        us = timeit(lambda: nat.ops().corr([f[:B], f[B:]] + lv, [B, h, w, C, 4], 1 / 16.0), iters=5)
+        res["corr_pyramid"] = {"us": us, "tflops": 2.0 * B * (h * w) ** 2 * C / us / 1e6}
+        print(f"corr_pyramid {us:8.1f} us  {2.0 * B * (h * w) ** 2 * C / us / 1e6:.1f} TF/s")
+        coords = (torch.stack(torch.meshgrid(torch.arange(w), torch.arange(h), indexing="xy"), -1).float()
+                  .reshape(1, h * w, 2).repeat(B, 1, 1).reshape(M, 2).to(dev))
+        coords += torch.randn_like(coords) * 3
+        out = torch.empty(M, 328, device=dev, dtype=torch.bfloat16)
+        us = timeit(lambda: nat.ops().lookup([coords, out] + lv, [4, B, h, w, 4]))
+        res["lookup"] = {"us": us}
+        print(f"lookup       {us:8.1f} us")
+    if not args.only or "upsample" in args.only:
+        mask = rnd(M, 576)
+        flow = torch.randn(M, 2, device=dev)
+        out = torch.empty(B, 8 * h, 8 * w, 2, device=dev)
+        us = timeit(lambda: nat.ops().upsample_convex([mask, flow, out], [B, h, w, 0]))
+        res["upsample_convex"] = {"us": us}
+        print(f"upsample     {us:8.1f} us")
+    if args.json:
+        with open(args.json, "w") as fh:
+            json.dump(res, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
