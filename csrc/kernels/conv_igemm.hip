@@ -27,7 +27,6 @@ namespace {
 
 constexpr int BK = 64;
 
-JR_DEVICE int swzA(int row) { return ((row >> 1) & 1) | ((row >> 3) & 6); }
 JR_DEVICE int swzB(int row) { return (row >> 1) & 7; }
 
 template <int NV>
@@ -80,172 +79,23 @@ JR_DEVICE void load_f32(const float* src, float* v) {
   }
 }
 
-template <int BCO, int BP, int WCO, int EPI>
-__global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
-  constexpr int WP = 4 / WCO;
-  constexpr int WTCO = BCO / WCO;
-  constexpr int WTP = BP / WP;
-  constexpr int TM = WTCO / 16;
-  constexpr int TN = WTP / 16;
-  constexpr int NV = 4 * TM;              // contiguous channels per lane
-  constexpr int XR = BP / 32;             // X rows loaded per thread
-  constexpr int WR = BCO >= 32 ? BCO / 32 : 1;
-  constexpr int A_ELEMS = BCO * BK;
-  constexpr int B_ELEMS = BP * BK;
-  constexpr unsigned OOB = 0x80000000u;   // buffer offset past num_records -> hardware returns 0
-  static_assert(TM >= 1 && TN >= 1 && WCO * WP == 4, "tile");
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (A_ELEMS + B_ELEMS)];
+// Output channel base of a lane: storage rows are permuted in 64-row groups so
+// that D row (4*lq + r) of 16-row MFMA tile t maps to channel G + lq*16 + t*4 + r.
+template <int TM>
+JR_DEVICE int chan_base(int wrow0, int lq) {
+  const int G = wrow0 & ~63;
+  const int t0 = (wrow0 & 63) >> 4;
+  return G + lq * 16 + t0 * 4;
+}
 
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wco = wave % WCO;
-  const int wp = wave / WCO;
-  const int p0 = blockIdx.x * BP;
-  const int co0 = blockIdx.y * BCO;
-  const int ch = tid & 7;
-  const int OHW = p.OH * p.OW;
-
-  // Buffer resources: out-of-range offsets (padding taps, tail rows, K tail)
-  // read as zero with no branch and no exec masking.
-  const __amdgpu_buffer_rsrc_t xsrd =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wsrd =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)p.w_bytes, 0x00020000);
-
-  // Per-thread im2col row descriptors (fixed across the K loop); byte offsets.
-  int ih0[XR], iw0[XR];
-  unsigned rbase[XR];
-#pragma unroll
-  for (int i = 0; i < XR; ++i) {
-    const int m = p0 + (tid >> 3) + 32 * i;
-    if (m < p.M) {
-      const int n = m / OHW;
-      const int rem = m - n * OHW;
-      const int oh = rem / p.OW;
-      const int ow = rem - oh * p.OW;
-      ih0[i] = oh * p.SH - p.PH;
-      iw0[i] = ow * p.SW - p.PW;
-      rbase[i] = (unsigned)(((long)n * p.H * p.W * p.x_cstride + p.x_coff) * 2);
-    } else {
-      ih0[i] = -(1 << 28);
-      iw0[i] = -(1 << 28);
-      rbase[i] = 0;
-    }
-  }
-  const unsigned wrow_off = (unsigned)((co0 + (tid >> 3)) * p.kpad * 2 + ch * 16);
-  const unsigned wrow_lim = (unsigned)(p.cout_pad - co0 - (tid >> 3));  // rows i*32 < lim are valid
-
-  // K-chunk state of the NEXT stage to load: kc = ks*8 + ch.
-  const int cpt = p.cin8 >> 3;
-  int tap = ch / cpt;
-  int cc = ch - tap * cpt;
-  int kh = tap / p.KW;
-  int kw = tap - kh * p.KW;
-  int ks_next = 0;
-  const unsigned xrow_bytes = (unsigned)p.x_cstride * 2;
-
-  struct Regs { u32x4 x[XR]; u32x4 w[WR]; };
-  Regs ra, rb;
-
-  auto issue = [&](Regs& r) {
-    const bool kvalid = kh < p.KH;
-#pragma unroll
-    for (int i = 0; i < XR; ++i) {
-      const int ih = ih0[i] + kh;
-      const int iw = iw0[i] + kw;
-      const bool ok = kvalid && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-      const unsigned off = rbase[i] + (unsigned)(ih * p.W + iw) * xrow_bytes + (unsigned)cc * 16u;
-      r.x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xsrd, ok ? off : OOB, 0, 0));
-    }
-    const unsigned kofs = (unsigned)ks_next * (BK * 2);
-#pragma unroll
-    for (int i = 0; i < WR; ++i) {
-      const bool ok = ((BCO >= 32) || (tid < BCO * 8)) && (unsigned)(32 * i) < wrow_lim && ks_next * BK < p.kpad;
-      const unsigned off = wrow_off + (unsigned)(32 * i) * (unsigned)p.kpad * 2u + kofs;
-      r.w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wsrd, ok ? off : OOB, 0, 0));
-    }
-    // advance the chunk state to the following stage
-    ++ks_next;
-    cc += 8;
-    while (cc >= cpt) {
-      cc -= cpt;
-      if (++kw == p.KW) { kw = 0; ++kh; }
-    }
-  };
-  auto store = [&](const Regs& r, int buf) {
-    bf16* sA = smem + buf * (A_ELEMS + B_ELEMS);
-    bf16* sB = sA + A_ELEMS;
-#pragma unroll
-    for (int i = 0; i < XR; ++i) {
-      const int rr = (tid >> 3) + 32 * i;
-      *(u32x4*)(sB + rr * BK + ((ch ^ swzB(rr)) << 3)) = r.x[i];
-    }
-#pragma unroll
-    for (int i = 0; i < WR; ++i) {
-      const int rr = (tid >> 3) + 32 * i;
-      if ((BCO >= 32) || (tid < BCO * 8)) *(u32x4*)(sA + rr * BK + ((ch ^ swzA(rr)) << 3)) = r.w[i];
-    }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int li = lane & 15;
-  const int lq = lane >> 4;
-  auto compute = [&](int buf) {
-    const bf16* sA = smem + buf * (A_ELEMS + B_ELEMS);
-    const bf16* sB = sA + A_ELEMS;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = kk * 4 + lq;
-      bf16x8 af[TM], bfr[TN];
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm) {
-        const int row = wco * WTCO + (li >> 2) * NV + tm * 4 + (li & 3);
-        af[tm] = *(const bf16x8*)(sA + row * BK + ((chunk ^ swzA(row)) << 3));
-      }
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn) {
-        const int row = wp * WTP + tn * 16 + li;
-        bfr[tn] = *(const bf16x8*)(sB + row * BK + ((chunk ^ swzB(row)) << 3));
-      }
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tm], bfr[tn], acc[tm][tn], 0, 0, 0);
-    }
-  };
-
-  // Software pipeline: global loads run two K-stages ahead of the MFMAs
-  // (register sets ra/rb alternate, LDS double-buffered, one barrier per
-  // stage).  Loads past the end of K are issued with OOB offsets (zeros),
-  // keeping the loop body branch-free so hipcc emits counted vmcnt waits.
-  const int nks = p.kpad / BK;
-  issue(ra);
-  issue(rb);
-  store(ra, 0);
-  __syncthreads();
-  const int npairs = nks >> 1;
-  for (int it = 0; it < npairs; ++it) {
-    issue(ra);          // stage 2it+2
-    compute(0);         // stage 2it
-    store(rb, 1);       // stage 2it+1 (loaded one stage ago)
-    __syncthreads();
-    issue(rb);          // stage 2it+3
-    compute(1);         // stage 2it+1
-    store(ra, 0);       // stage 2it+2
-    __syncthreads();
-  }
-  if (nks & 1) compute(0);
-
-  // ------------------------------------------------------------------ epilogue
-  const int cbase = co0 + wco * WTCO + lq * NV;
+// Shared epilogue.  Lane (li, lq) of wave (wco, wp) holds, for each pixel tile
+// tn, NV = 4*TM contiguous output channels starting at cbase (see the weight
+// row permutation in jax_raft_amd/ops/native.py:pack_weight).
+template <int TM, int TN, int EPI>
+JR_DEVICE void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM][TN], int mbase, int cbase, int li) {
+  constexpr int NV = 4 * TM;
   if (cbase >= p.cout) return;
+  const int OHW = p.OH * p.OW;
   const bool full = cbase + NV <= p.cout;
   float bias[NV];
 #pragma unroll
@@ -253,7 +103,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
 
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
-    const int m = p0 + wp * WTP + tn * 16 + li;
+    const int m = mbase + tn * 16 + li;
     if (m >= p.M) continue;
     float v[NV];
 #pragma unroll
@@ -371,17 +221,381 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
   }
 }
 
-template <int BCO, int BP, int WCO>
+template <int BCO, int BP, int WCO, int EPI>
+__global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
+  constexpr int WP = 4 / WCO;
+  constexpr int WTCO = BCO / WCO;
+  constexpr int WTP = BP / WP;
+  constexpr int TM = WTCO / 16;
+  constexpr int TN = WTP / 16;
+  constexpr int NV = 4 * TM;              // contiguous channels per lane
+  constexpr int XR = BP / 32;             // X rows loaded per thread
+  constexpr int WR = BCO >= 32 ? BCO / 32 : 1;
+  constexpr int A_ELEMS = BCO * BK;
+  constexpr int B_ELEMS = BP * BK;
+  constexpr unsigned OOB = 0x80000000u;   // buffer offset past num_records -> hardware returns 0
+  static_assert(TM >= 1 && TN >= 1 && WCO * WP == 4, "tile");
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (A_ELEMS + B_ELEMS)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wco = wave % WCO;
+  const int wp = wave / WCO;
+  const int p0 = blockIdx.x * BP;
+  const int co0 = blockIdx.y * BCO;
+  const int ch = tid & 7;
+  const int OHW = p.OH * p.OW;
+
+  // Buffer resources: out-of-range offsets (padding taps, tail rows, K tail)
+  // read as zero with no branch and no exec masking.
+  const __amdgpu_buffer_rsrc_t xsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)p.w_bytes, 0x00020000);
+
+  // Per-thread im2col row descriptors (fixed across the K loop); byte offsets.
+  int ih0[XR], iw0[XR];
+  unsigned rbase[XR];
+#pragma unroll
+  for (int i = 0; i < XR; ++i) {
+    const int m = p0 + (tid >> 3) + 32 * i;
+    if (m < p.M) {
+      const int n = m / OHW;
+      const int rem = m - n * OHW;
+      const int oh = rem / p.OW;
+      const int ow = rem - oh * p.OW;
+      ih0[i] = oh * p.SH - p.PH;
+      iw0[i] = ow * p.SW - p.PW;
+      rbase[i] = (unsigned)(((long)n * p.H * p.W * p.x_cstride + p.x_coff) * 2);
+    } else {
+      ih0[i] = -(1 << 28);
+      iw0[i] = -(1 << 28);
+      rbase[i] = 0;
+    }
+  }
+  const unsigned wrow_off = (unsigned)((co0 + (tid >> 3)) * p.kpad * 2 + ch * 16);
+  const unsigned wrow_lim = (unsigned)(p.cout_pad - co0 - (tid >> 3));  // rows i*32 < lim are valid
+
+  // K-chunk state of the NEXT stage to load: kc = ks*8 + ch.
+  const int cpt = p.cin8 >> 3;
+  int tap = ch / cpt;
+  int cc = ch - tap * cpt;
+  int kh = tap / p.KW;
+  int kw = tap - kh * p.KW;
+  int ks_next = 0;
+  const unsigned xrow_bytes = (unsigned)p.x_cstride * 2;
+
+  struct Regs { u32x4 x[XR]; u32x4 w[WR]; };
+  Regs ra, rb;
+
+  auto issue = [&](Regs& r) {
+    const bool kvalid = kh < p.KH;
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      const int ih = ih0[i] + kh;
+      const int iw = iw0[i] + kw;
+      const bool ok = kvalid && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      const unsigned off = rbase[i] + (unsigned)(ih * p.W + iw) * xrow_bytes + (unsigned)cc * 16u;
+      r.x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xsrd, ok ? off : OOB, 0, 0));
+    }
+    const unsigned kofs = (unsigned)ks_next * (BK * 2);
+#pragma unroll
+    for (int i = 0; i < WR; ++i) {
+      const bool ok = ((BCO >= 32) || (tid < BCO * 8)) && (unsigned)(32 * i) < wrow_lim && ks_next * BK < p.kpad;
+      const unsigned off = wrow_off + (unsigned)(32 * i) * (unsigned)p.kpad * 2u + kofs;
+      r.w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wsrd, ok ? off : OOB, 0, 0));
+    }
+    // advance the chunk state to the following stage
+    ++ks_next;
+    cc += 8;
+    while (cc >= cpt) {
+      cc -= cpt;
+      if (++kw == p.KW) { kw = 0; ++kh; }
+    }
+  };
+  auto store = [&](const Regs& r, int buf) {
+    bf16* sA = smem + buf * (A_ELEMS + B_ELEMS);
+    bf16* sB = sA + A_ELEMS;
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      const int rr = (tid >> 3) + 32 * i;
+      *(u32x4*)(sB + rr * BK + ((ch ^ swzB(rr)) << 3)) = r.x[i];
+    }
+#pragma unroll
+    for (int i = 0; i < WR; ++i) {
+      const int rr = (tid >> 3) + 32 * i;
+      if ((BCO >= 32) || (tid < BCO * 8)) *(u32x4*)(sA + rr * BK + ((ch ^ swzB(rr)) << 3)) = r.w[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int li = lane & 15;
+  const int lq = lane >> 4;
+  auto compute = [&](int buf) {
+    const bf16* sA = smem + buf * (A_ELEMS + B_ELEMS);
+    const bf16* sB = sA + A_ELEMS;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + lq;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int row = wco * WTCO + tm * 16 + li;
+        af[tm] = *(const bf16x8*)(sA + row * BK + ((chunk ^ swzB(row)) << 3));
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int row = wp * WTP + tn * 16 + li;
+        bfr[tn] = *(const bf16x8*)(sB + row * BK + ((chunk ^ swzB(row)) << 3));
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tm], bfr[tn], acc[tm][tn], 0, 0, 0);
+    }
+  };
+
+  // Software pipeline: global loads run two K-stages ahead of the MFMAs
+  // (register sets ra/rb alternate, LDS double-buffered, one barrier per
+  // stage).  Loads past the end of K are issued with OOB offsets (zeros),
+  // keeping the loop body branch-free so hipcc emits counted vmcnt waits.
+  const int nks = p.kpad / BK;
+  issue(ra);
+  issue(rb);
+  store(ra, 0);
+  __syncthreads();
+  const int npairs = nks >> 1;
+  for (int it = 0; it < npairs; ++it) {
+    issue(ra);          // stage 2it+2
+    compute(0);         // stage 2it
+    store(rb, 1);       // stage 2it+1 (loaded one stage ago)
+    __syncthreads();
+    issue(rb);          // stage 2it+3
+    compute(1);         // stage 2it+1
+    store(ra, 0);       // stage 2it+2
+    __syncthreads();
+  }
+  if (nks & 1) compute(0);
+
+  const int wrow0 = co0 + wco * WTCO;
+  conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, chan_base<TM>(wrow0, lq), li);
+}
+
+// ---------------------------------------------------------------------------
+// Kernel D: direct-to-LDS DMA operand staging.
+//
+// Both operand tiles are fetched with `buffer_load_dwordx4 ... lds` (LDS-DMA):
+// no staging VGPRs and no ds_write traffic, and the buffer range check turns
+// padding taps / tail rows into zero fills.  K advances in 32-deep stages
+// through a 4-deep LDS ring with loads issued 3 stages ahead; waits are counted
+// (`s_waitcnt vmcnt(N)`) and barriers raw, so DMA for later stages stays in
+// flight across them (cdna_hip_programming.md §5 "Pipelining across barriers").
+// LDS rows are 64 B (4 x 16-B chunks); chunk c of row r lives at slot
+// c ^ ((r >> 2) & 3): the 16 consecutive rows of a fragment read hit 16
+// distinct 16-B bank slots, and each DMA lane has a FIXED logical chunk
+// ((l & 3) ^ ((l >> 4) & 3)) because a 1-KiB DMA piece covers 16 whole rows.
+// ---------------------------------------------------------------------------
+constexpr int DBK = 32;
+constexpr int DNB = 4;
+
+// One 16-B-per-lane LDS-DMA (buffer_load_dwordx4 ... lds): lane i lands at lds + 16*i.
+JR_DEVICE void dma16(__amdgpu_buffer_rsrc_t r, bf16* lds, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+}
+
+template <int N>
+JR_DEVICE void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+JR_DEVICE void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int BCO, int BP, int WCO, int EPI>
+__global__ __launch_bounds__(256) void conv_dma_kernel(const ConvParams p) {
+  constexpr int WP = 4 / WCO;
+  constexpr int WTCO = BCO / WCO;
+  constexpr int WTP = BP / WP;
+  constexpr int TM = WTCO / 16;
+  constexpr int TN = WTP / 16;
+  constexpr int XPIECES = BP / 16;                 // 1-KiB DMA pieces per stage, X tile
+  constexpr int WPIECES = BCO / 16;                // ... W tile
+  constexpr int XPW = (XPIECES + 3) / 4;           // pieces per wave
+  constexpr int WPW = (WPIECES + 3) / 4;
+  constexpr int DPW = XPW + WPW;                   // DMA instructions per wave per stage (upper bound)
+  constexpr int A_ELEMS = BCO * DBK;
+  constexpr int B_ELEMS = BP * DBK;
+  constexpr int STAGE = A_ELEMS + B_ELEMS;
+  constexpr unsigned OOB = 0x80000000u;
+  static_assert(TM >= 1 && TN >= 1 && WCO * WP == 4, "tile");
+  __shared__ __attribute__((aligned(16))) bf16 smem[DNB * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wco = wave % WCO;
+  const int wp = wave / WCO;
+  const int p0 = blockIdx.x * BP;
+  const int co0 = blockIdx.y * BCO;
+  const int OHW = p.OH * p.OW;
+  const int cl = (lane & 3) ^ ((lane >> 4) & 3);   // this lane's logical 16-B chunk within a stage
+
+  const __amdgpu_buffer_rsrc_t xsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)p.w_bytes, 0x00020000);
+
+  // X rows handled by this lane: piece = wave*XPW + j, row = piece*16 + (lane >> 2)
+  int ih0[XPW], iw0[XPW];
+  unsigned rbase[XPW];
+#pragma unroll
+  for (int j = 0; j < XPW; ++j) {
+    const int piece = wave * XPW + j;
+    const int m = p0 + piece * 16 + (lane >> 2);
+    if (piece < XPIECES && m < p.M) {
+      const int n = m / OHW;
+      const int rem = m - n * OHW;
+      const int oh = rem / p.OW;
+      const int ow = rem - oh * p.OW;
+      ih0[j] = oh * p.SH - p.PH;
+      iw0[j] = ow * p.SW - p.PW;
+      rbase[j] = (unsigned)(((long)n * p.H * p.W * p.x_cstride + p.x_coff) * 2);
+    } else {
+      ih0[j] = -(1 << 28);
+      iw0[j] = -(1 << 28);
+      rbase[j] = 0;
+    }
+  }
+  unsigned wbase[WPW];
+  bool wok[WPW];
+#pragma unroll
+  for (int j = 0; j < WPW; ++j) {
+    const int piece = wave * WPW + j;
+    const int row = co0 + piece * 16 + (lane >> 2);
+    wok[j] = piece < WPIECES && row < p.cout_pad;
+    wbase[j] = (unsigned)(row * p.kpad * 2 + cl * 16);
+  }
+
+  // chunk state of the next stage to issue: kc = ks*4 + cl
+  const int cpt = p.cin8 >> 3;
+  int tap = cl / cpt;
+  int cc = cl - tap * cpt;
+  int kh = tap / p.KW;
+  int kw = tap - kh * p.KW;
+  int ks_next = 0;
+  const unsigned xrow_bytes = (unsigned)p.x_cstride * 2;
+  const int nks = p.kpad / DBK;
+
+  auto issue = [&]() {
+    const int buf = ks_next & (DNB - 1);
+    bf16* sA = smem + buf * STAGE;
+    bf16* sB = sA + A_ELEMS;
+    const bool kvalid = kh < p.KH;
+#pragma unroll
+    for (int j = 0; j < XPW; ++j) {
+      const int piece = wave * XPW + j;
+      if (piece < XPIECES) {
+        const int ih = ih0[j] + kh;
+        const int iw = iw0[j] + kw;
+        const bool ok = kvalid && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        const unsigned off = rbase[j] + (unsigned)(ih * p.W + iw) * xrow_bytes + (unsigned)cc * 16u;
+        dma16(xsrd, sB + piece * 16 * DBK, ok ? off : OOB);
+      }
+    }
+    const unsigned kofs = (unsigned)ks_next * (DBK * 2);
+    const bool kin = ks_next < nks;
+#pragma unroll
+    for (int j = 0; j < WPW; ++j) {
+      const int piece = wave * WPW + j;
+      if (piece < WPIECES) {
+        const bool ok = wok[j] && kin;
+        dma16(wsrd, sA + piece * 16 * DBK, ok ? wbase[j] + kofs : OOB);
+      }
+    }
+    ++ks_next;
+    cc += 4;
+    while (cc >= cpt) {
+      cc -= cpt;
+      if (++kw == p.KW) { kw = 0; ++kh; }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int li = lane & 15;
+  const int lq = lane >> 4;
+  auto compute = [&](int buf) {
+    const bf16* sA = smem + buf * STAGE;
+    const bf16* sB = sA + A_ELEMS;
+    bf16x8 af[TM], bfr[TN];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+      const int row = wco * WTCO + tm * 16 + li;
+      af[tm] = *(const bf16x8*)(sA + row * DBK + ((lq ^ ((row >> 2) & 3)) << 3));
+    }
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int row = wp * WTP + tn * 16 + li;
+      bfr[tn] = *(const bf16x8*)(sB + row * DBK + ((lq ^ ((row >> 2) & 3)) << 3));
+    }
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tm], bfr[tn], acc[tm][tn], 0, 0, 0);
+  };
+
+  // Every wave issues exactly DPW DMA ops per stage (waves without a piece
+  // issue nothing, so their counted waits are conservative and still correct).
+  issue();
+  issue();
+  issue();
+  wait_vmcnt<2 * DPW>();
+  raw_barrier();
+  for (int ks = 0; ks < nks; ++ks) {
+    issue();                       // stage ks+3 into the buffer freed by stage ks-1
+    compute(ks & (DNB - 1));       // stage ks
+    wait_vmcnt<2 * DPW>();         // stage ks+1 has landed (ks+2, ks+3 may still fly)
+    raw_barrier();
+  }
+  wait_vmcnt<0>();
+
+  const int wrow0 = co0 + wco * WTCO;
+  conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, chan_base<TM>(wrow0, lq), li);
+}
+
+template <int BCO, int BP, int WCO, bool DMA>
 int launch_cfg(const ConvParams* p, int epi, hipStream_t s) {
-  dim3 grid((p->M + BP - 1) / BP, (p->cout + BCO - 1) / BCO);
+  // storage rows are permuted inside 64-row groups: cover every group that holds a real channel
+  const int rows = (p->cout + 63) / 64 * 64;
+  dim3 grid((p->M + BP - 1) / BP, (rows + BCO - 1) / BCO);
   dim3 block(256);
+#define JR_LAUNCH(E)                                                                        \
+  if (DMA) hipLaunchKernelGGL((conv_dma_kernel<BCO, BP, WCO, E>), grid, block, 0, s, *p);   \
+  else hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E>), grid, block, 0, s, *p);
   switch (epi) {
-    case EPI_STD: hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, EPI_STD>), grid, block, 0, s, *p); break;
-    case EPI_GRU_A: hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, EPI_GRU_A>), grid, block, 0, s, *p); break;
-    case EPI_GRU_B: hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, EPI_GRU_B>), grid, block, 0, s, *p); break;
-    case EPI_FLOW: hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, EPI_FLOW>), grid, block, 0, s, *p); break;
+    case EPI_STD: JR_LAUNCH(EPI_STD) break;
+    case EPI_GRU_A: JR_LAUNCH(EPI_GRU_A) break;
+    case EPI_GRU_B: JR_LAUNCH(EPI_GRU_B) break;
+    case EPI_FLOW: JR_LAUNCH(EPI_FLOW) break;
     default: return (int)hipErrorInvalidValue;
   }
+#undef JR_LAUNCH
   return (int)hipGetLastError();
 }
 
@@ -390,12 +604,18 @@ int launch_cfg(const ConvParams* p, int epi, hipStream_t s) {
 extern "C" int jr_conv_forward(const ConvParams* p, int cfg, int epi, hipStream_t stream) {
   if (p->M <= 0) return 0;
   switch (cfg) {
-    case 0: return launch_cfg<128, 128, 2>(p, epi, stream);
-    case 1: return launch_cfg<64, 128, 1>(p, epi, stream);
-    case 2: return launch_cfg<128, 64, 2>(p, epi, stream);
-    case 3: return launch_cfg<16, 256, 1>(p, epi, stream);
-    case 4: return launch_cfg<64, 64, 1>(p, epi, stream);
-    case 5: return launch_cfg<16, 64, 1>(p, epi, stream);
+    case 0: return launch_cfg<128, 128, 2, false>(p, epi, stream);
+    case 1: return launch_cfg<64, 128, 1, false>(p, epi, stream);
+    case 2: return launch_cfg<128, 64, 2, false>(p, epi, stream);
+    case 3: return launch_cfg<16, 256, 1, false>(p, epi, stream);
+    case 4: return launch_cfg<64, 64, 1, false>(p, epi, stream);
+    case 5: return launch_cfg<16, 64, 1, false>(p, epi, stream);
+    case 6: return launch_cfg<128, 128, 2, true>(p, epi, stream);
+    case 7: return launch_cfg<64, 128, 1, true>(p, epi, stream);
+    case 8: return launch_cfg<128, 64, 2, true>(p, epi, stream);
+    case 9: return launch_cfg<16, 256, 1, true>(p, epi, stream);
+    case 10: return launch_cfg<64, 64, 1, true>(p, epi, stream);
+    case 11: return launch_cfg<16, 64, 1, true>(p, epi, stream);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -99,7 +99,7 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
               "conv: input channel slice must be 8-aligned and inside the tensor");
   TORCH_CHECK((int64_t)p.N * p.H * p.W * p.x_cstride <= x.numel(), "conv: input tensor too small");
   TORCH_CHECK(p.kpad % 64 == 0 && p.kpad >= p.KH * p.KW * p.cin8, "conv: packed weight K mismatch");
-  TORCH_CHECK(p.cout_pad % 16 == 0 && p.cout_pad >= p.cout && bias.numel() >= p.cout, "conv: packed weight rows");
+  TORCH_CHECK(p.cout_pad % 64 == 0 && p.cout_pad >= p.cout && bias.numel() >= p.cout, "conv: packed weight rows (64-row groups)");
   TORCH_CHECK(p.OH > 0 && p.OW > 0, "conv: empty output");
   TORCH_CHECK(p.y_cstride % 8 == 0, "conv: output channel stride must be a multiple of 8");
   TORCH_CHECK((int64_t)p.M * p.y_cstride <= y.numel(), "conv: output tensor too small");
@@ -124,7 +124,7 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   } else {
     TORCH_CHECK(false, "conv: unknown epilogue ", epi);
   }
-  TORCH_CHECK(cfg >= 0 && cfg <= 5, "conv: unknown tile config ", cfg);
+  TORCH_CHECK(cfg >= 0 && cfg <= 11, "conv: unknown tile config ", cfg);
   if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3}) if (v.defined()) keep->push_back(v);
   return [p, epi, cfg](hipStream_t s, int) { return jr_conv_forward(&p, cfg, epi, s); };
 }

@@ -26,6 +26,8 @@ ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, ACT_SPLIT_TANH_RELU = 0, 1, 2, 3, 4
 EPI_STD, EPI_GRU_A, EPI_GRU_B, EPI_FLOW = 0, 1, 2, 3
 # tile configs of conv_igemm.hip: (BCO, BP)
 CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (16, 256), 4: (64, 64), 5: (16, 64)}
+# configs 6..11: the same tiles on the LDS-DMA kernel (csrc/kernels/conv_igemm.hip, kernel D)
+CFG_TILES.update({c + 6: t for c, t in list(CFG_TILES.items())})
 NUM_CUS = 256
 
 
@@ -105,18 +107,30 @@ class ConvSpec:
         return (H + 2 * self.ph - self.kh) // self.sh + 1, (W + 2 * self.pw - self.kw) // self.sw + 1
 
 
+def _row_perm(cout_pad: int) -> torch.Tensor:
+    """Storage row s -> output channel.  Within each 64-row group the rows are
+    ordered so that D row (4*q + r) of the 16-row MFMA tile t is channel
+    q*16 + t*4 + r: every lane of the conv epilogue then owns contiguous
+    channels and both GEMM operands are read from LDS in natural row order."""
+    s = torch.arange(cout_pad)
+    g, i = s // 64, s % 64
+    t, q, r = i // 16, (i % 16) // 4, i % 4
+    return g * 64 + q * 16 + t * 4 + r
+
+
 def pack_weight(kernel: torch.Tensor, cin8: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """HWIO fp32 kernel -> bf16 [cout_pad, kpad] (GEMM A operand)."""
+    """HWIO fp32 kernel -> bf16 [cout_pad, kpad] (GEMM A operand), K ordered
+    (kh, kw, cin8), rows permuted per :func:`_row_perm`, cout padded to 64."""
     kh, kw, cin, cout = kernel.shape
     cin8 = cin8 or round_up(cin, 8)
     kraw = kh * kw * cin8
     kpad = round_up(kraw, 64)
-    cout_pad = round_up(cout, 16)
+    cout_pad = round_up(cout, 64)
     k = torch.zeros(kh, kw, cin8, cout, dtype=torch.float32, device=kernel.device)
     k[:, :, :cin, :] = kernel.detach().float()
     w = torch.zeros(cout_pad, kpad, dtype=torch.float32, device=kernel.device)
     w[:cout, :kraw] = k.permute(3, 0, 1, 2).reshape(cout, kraw)
-    w = w.to(torch.bfloat16)
+    w = w[_row_perm(cout_pad).to(w.device)].to(torch.bfloat16).contiguous()
     if out is not None:
         assert out.shape == w.shape and out.dtype == torch.bfloat16
         out.copy_(w)
@@ -138,10 +152,10 @@ def pick_cfg(M: int, cout: int) -> int:
     tile's per-FLOP cost rises as it shrinks; keeps >= one wave of blocks over
     256 CUs whenever the problem allows."""
     if cout <= 16:
-        return 5
-    best, best_cost = 0, None
+        return 11
+    best, best_cost = 6, None
     # (cfg, relative per-FLOP efficiency of the tile); time ~ blocks per CU x tile area / eff
-    for cfg, eff in ((0, 1.0), (2, 0.85), (1, 0.85), (4, 0.65)):
+    for cfg, eff in ((6, 1.0), (8, 0.85), (7, 0.85), (10, 0.65)):
         bco, bp = CFG_TILES[cfg]
         nb = math.ceil(M / bp) * math.ceil(cout / bco)
         cost = math.ceil(nb / NUM_CUS) * (bco * bp) / eff

@@ -47,7 +47,7 @@ CONV_CASES = [
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-@pytest.mark.parametrize("cfg", [None, 0, 1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [None] + list(range(12)))
 def test_conv_matches_reference(case, cfg):
     nat = _nat()
     N, H, W, cin, cout, kh, kw, s, p = case
@@ -68,7 +68,8 @@ def test_conv_matches_reference(case, cfg):
     assert err < 2e-3, err
 
 
-def test_conv_epilogues():
+@pytest.mark.parametrize("cfg", [0, 4, 6, 10])
+def test_conv_epilogues(cfg):
     """relu / residual (pre and post) / alpha / bf16 output / channel offsets."""
     nat = _nat()
     torch.manual_seed(1)
@@ -81,16 +82,16 @@ def test_conv_epilogues():
     spec = nat.make_spec(k, b, (1, 1), (1, 1), device=DEV)
     xg = x.to(DEV, torch.bfloat16).contiguous()
     rg = res.to(DEV, torch.bfloat16).contiguous()
-    y = nat.conv2d(spec, xg, act=nat.ACT_RELU, out_dtype=torch.float32, res=rg, res_post=0)
+    y = nat.conv2d(spec, xg, act=nat.ACT_RELU, out_dtype=torch.float32, res=rg, res_post=0, cfg=cfg)
     assert _rel(y.cpu(), torch.relu(base + _bf(res))) < 3e-3
-    y = nat.conv2d(spec, xg, act=nat.ACT_RELU, out_dtype=torch.float32, res=rg, res_post=1)
+    y = nat.conv2d(spec, xg, act=nat.ACT_RELU, out_dtype=torch.float32, res=rg, res_post=1, cfg=cfg)
     assert _rel(y.cpu(), torch.relu(torch.relu(base) + _bf(res))) < 3e-3
-    y = nat.conv2d(spec, xg, act=nat.ACT_NONE, out_dtype=torch.float32, alpha=0.25)
+    y = nat.conv2d(spec, xg, act=nat.ACT_NONE, out_dtype=torch.float32, alpha=0.25, cfg=cfg)
     assert _rel(y.cpu(), 0.25 * base) < 3e-3
     # write into a channel slice of a wider buffer, plus a second copy
     big = torch.full((N * H * W, 64), 7.0, dtype=torch.bfloat16, device=DEV)
     big2 = torch.zeros((N * H * W, 64), dtype=torch.bfloat16, device=DEV)
-    t, i, a = nat.conv_args(spec, xg, N, H, W, big, y_coff=8, act=nat.ACT_TANH, y2=big2, y2_coff=16)
+    t, i, a = nat.conv_args(spec, xg, N, H, W, big, y_coff=8, act=nat.ACT_TANH, y2=big2, y2_coff=16, cfg=cfg)
     nat.ops().conv(t, i, a)
     torch.cuda.synchronize()
     exp = torch.tanh(base).reshape(-1, cout)
@@ -107,9 +108,10 @@ def _gru_ref(h, x, kz, bz, kr, br, kq, bq, pad):
     return (1 - z) * h + z * q
 
 
+@pytest.mark.parametrize("cfg", [None, 0, 6, 10])
 @pytest.mark.parametrize("hidden,xin,ks,pad", [(128, 256, (1, 5), (0, 2)), (128, 256, (5, 1), (2, 0)),
                                                (96, 146, (3, 3), (1, 1))])
-def test_gru_fused_epilogues(hidden, xin, ks, pad):
+def test_gru_fused_epilogues(hidden, xin, ks, pad, cfg):
     nat = _nat()
     torch.manual_seed(2)
     B, h, w = 2, 11, 13
@@ -129,8 +131,8 @@ def test_gru_fused_epilogues(hidden, xin, ks, pad):
     zb = torch.empty(M, hidden, device=DEV)
     sa = nat.make_spec(torch.cat([ks_[0], ks_[1]], 3), torch.cat([bs_[0], bs_[1]]), (1, 1), pad, cin8=cs, device=DEV)
     sb = nat.make_spec(ks_[2], bs_[2], (1, 1), pad, cin8=cs, device=DEV)
-    nat.ops().conv(*nat.conv_args(sa, hx, B, h, w, qx, h32=h32, zbuf=zb, hidden=hidden, epi=nat.EPI_GRU_A))
-    nat.ops().conv(*nat.conv_args(sb, qx, B, h, w, hx, h32=h32, zbuf=zb, hidden=hidden, epi=nat.EPI_GRU_B))
+    nat.ops().conv(*nat.conv_args(sa, hx, B, h, w, qx, h32=h32, zbuf=zb, hidden=hidden, epi=nat.EPI_GRU_A, cfg=cfg))
+    nat.ops().conv(*nat.conv_args(sb, qx, B, h, w, hx, h32=h32, zbuf=zb, hidden=hidden, epi=nat.EPI_GRU_B, cfg=cfg))
     torch.cuda.synchronize()
     out = h32.cpu().reshape(B, h, w, hidden)
     # r*h is quantised to bf16 before the q conv in the kernel; reference uses fp32 r*h -> bf16 as well
@@ -138,7 +140,8 @@ def test_gru_fused_epilogues(hidden, xin, ks, pad):
     assert (hx[:, :hidden].float().cpu() - ref.reshape(M, hidden)).abs().max().item() < 2.5e-2
 
 
-def test_flow_epilogue():
+@pytest.mark.parametrize("cfg", [None, 5, 11, 3, 9])
+def test_flow_epilogue(cfg):
     nat = _nat()
     torch.manual_seed(3)
     B, h, w, cin = 2, 9, 10, 256
@@ -156,7 +159,7 @@ def test_flow_epilogue():
     f8 = torch.zeros(M, 8, dtype=torch.bfloat16, device=DEV)
     xg = x.to(DEV, torch.bfloat16).contiguous()
     nat.ops().conv(*nat.conv_args(spec, xg, B, h, w, hx, y_coff=14, y3=f8, coords=coords, flow32=flow32,
-                                  epi=nat.EPI_FLOW))
+                                  epi=nat.EPI_FLOW, cfg=cfg))
     torch.cuda.synchronize()
     new = c1 + delta
     assert (coords.cpu().reshape(B, h, w, 2) - new).abs().max() < 2e-3
