@@ -1,0 +1,21 @@
+#!/usr/bin/env python3
+"""Convert an official torchvision RAFT checkpoint (.pth state_dict) to the
+jax-raft Flax msgpack format (reference scripts/convert_checkpoint.py).
+
+  python scripts/convert_checkpoint.py raft_large_C_T_SKHT_V2.pth raft_large.msgpack
+
+The .pth is read with torch.load(weights_only=True): tensors only, nothing executed.
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from jax_raft_amd.utils.checkpoint import convert_checkpoint  # noqa: E402
+
+if __name__ == "__main__":
+    if len(sys.argv) != 3:
+        print("Usage: python convert_checkpoint.py <input_file> <output_file>")
+        sys.exit(1)
+    assert sys.argv[2].endswith(".msgpack")
+    convert_checkpoint(sys.argv[1], sys.argv[2])
