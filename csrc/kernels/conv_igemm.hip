@@ -293,9 +293,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
     const bool kvalid = kh < p.KH;
 #pragma unroll
     for (int i = 0; i < XR; ++i) {
-      const int ih = ih0[i] + kh;
-      const int iw = iw0[i] + kw;
-      const bool ok = kvalid && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      const int ihl = ih0[i] + kh, iwl = iw0[i] + kw;  // coordinates in the (dilated) input
+      const int ih = ihl >> p.dsh, iw = iwl >> p.dsw;
+      const bool ok = kvalid && ((ihl & ((1 << p.dsh) - 1)) | (iwl & ((1 << p.dsw) - 1))) == 0 &&
+                  (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
       const unsigned off = rbase[i] + (unsigned)(ih * p.W + iw) * xrow_bytes + (unsigned)cc * 16u;
       r.x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xsrd, ok ? off : OOB, 0, 0));
     }
@@ -506,9 +507,10 @@ __global__ __launch_bounds__(256) void conv_dma_kernel(const ConvParams p) {
     for (int j = 0; j < XPW; ++j) {
       const int piece = wave * XPW + j;
       if (piece < XPIECES) {
-        const int ih = ih0[j] + kh;
-        const int iw = iw0[j] + kw;
-        const bool ok = kvalid && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        const int ihl = ih0[j] + kh, iwl = iw0[j] + kw;  // coordinates in the (dilated) input
+        const int ih = ihl >> p.dsh, iw = iwl >> p.dsw;
+        const bool ok = kvalid && ((ihl & ((1 << p.dsh) - 1)) | (iwl & ((1 << p.dsw) - 1))) == 0 &&
+                        (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
         const unsigned off = rbase[j] + (unsigned)(ih * p.W + iw) * xrow_bytes + (unsigned)cc * 16u;
         dma16(xsrd, sB + piece * 16 * DBK, ok ? off : OOB);
       }

@@ -265,6 +265,66 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LevelPtrs lv, int nlev
   }
 }
 
+// Backward of the lookup w.r.t. the pyramid levels: grad_out [q][ocs]
+// (channel l*S^2 + i*S + j) -> dlevels fp32 [q][hl][wl] (accumulated).
+// Lane (level, i) folds the bilinear weights of its (2r+1) samples into the
+// (2r+2) cells of window columns x0+i (weight 1-fx) and x0+i+1 (weight fx);
+// the x0+i+1 part is handed to lane i+1 by a shuffle, so every cell of the
+// (2r+2)^2 window receives exactly one read-modify-write: no atomics, and
+// each query's level map is private to that query (no cross-query races).
+template <int R, typename G>
+__global__ __launch_bounds__(256) void corr_lookup_bwd_kernel(LevelPtrs dlv, int nlev, int total, int h, int w,
+                                                              const float* __restrict__ coords,
+                                                              const G* __restrict__ gout, int gcs) {
+  constexpr int S = 2 * R + 1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = blockIdx.x * 4 + wave;
+  if (q >= total) return;
+  const int lvl = lane >> 4;
+  const int i = lane & 15;
+  const bool on = lvl < nlev && i <= S;
+  float fx = 0.f, fy = 0.f;
+  int col = 0, row0 = 0, hl = 1, wl = 1;
+  if (on) {
+    const float sc = 1.0f / (float)(1 << lvl);
+    const float cx = coords[2 * (long)q] * sc, cy = coords[2 * (long)q + 1] * sc;
+    const float flx = floorf(cx), fly = floorf(cy);
+    fx = cx - flx;
+    fy = cy - fly;
+    hl = h >> lvl;
+    wl = w >> lvl;
+    col = (int)flx - R + i;
+    row0 = (int)fly - R;
+  }
+  float a[S + 1], b[S + 1];  // contributions to column x0+i (a) and x0+i+1 (b)
+#pragma unroll
+  for (int j = 0; j <= S; ++j) { a[j] = 0.f; b[j] = 0.f; }
+  if (on && i < S) {
+    const G* g = gout + (long)q * gcs + lvl * S * S + i * S;
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const float gv = to_f(g[j]);
+      a[j] += (1.f - fx) * (1.f - fy) * gv;
+      a[j + 1] += (1.f - fx) * fy * gv;
+      b[j] += fx * (1.f - fy) * gv;
+      b[j + 1] += fx * fy * gv;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j <= S; ++j) {
+    const float nb = __shfl_up(b[j], 1);
+    if (i > 0) a[j] += nb;
+  }
+  if (on && (unsigned)col < (unsigned)wl) {
+    float* map = (float*)dlv.p[lvl] + (long)q * (hl * wl);
+#pragma unroll
+    for (int j = 0; j <= S; ++j) {
+      const int rr = row0 + j;
+      if ((unsigned)rr < (unsigned)hl) map[rr * wl + col] += a[j];
+    }
+  }
+}
+
 template <typename T>
 int launch_lookup(const LevelPtrs& lv, int L, int total, int h, int w, int r, const float* coords, bf16* out, int ocs,
                   hipStream_t stream) {
@@ -306,4 +366,29 @@ extern "C" int jr_corr_lookup(const void* const* levels, int num_levels, int B, 
   const int total = B * h * w;
   if (lv_bf16) return launch_lookup<bf16>(lv, num_levels, total, h, w, radius, coords, (bf16*)out, out_cstride, stream);
   return launch_lookup<float>(lv, num_levels, total, h, w, radius, coords, (bf16*)out, out_cstride, stream);
+}
+
+extern "C" int jr_corr_lookup_bwd(void* const* dlevels, int num_levels, int B, int h, int w, int radius,
+                                  const float* coords, const void* gout, int gcs, int g_bf16, hipStream_t stream) {
+  const int S = 2 * radius + 1;
+  if (num_levels > 4 || radius < 1 || radius > 6 || gcs < num_levels * S * S) return (int)hipErrorInvalidValue;
+  LevelPtrs lv;
+  for (int l = 0; l < 4; ++l) lv.p[l] = l < num_levels ? dlevels[l] : nullptr;
+  const int total = B * h * w;
+  dim3 grid((total + 3) / 4);
+  switch (radius) {
+#define JR_LB(RR)                                                                                               \
+  case RR:                                                                                                      \
+    if (g_bf16)                                                                                                 \
+      hipLaunchKernelGGL((corr_lookup_bwd_kernel<RR, bf16>), grid, dim3(256), 0, stream, lv, num_levels, total, h, w, \
+                         coords, (const bf16*)gout, gcs);                                                       \
+    else                                                                                                        \
+      hipLaunchKernelGGL((corr_lookup_bwd_kernel<RR, float>), grid, dim3(256), 0, stream, lv, num_levels, total, h,   \
+                         w, coords, (const float*)gout, gcs);                                                   \
+    break;
+    JR_LB(1) JR_LB(2) JR_LB(3) JR_LB(4) JR_LB(5) JR_LB(6)
+#undef JR_LB
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
 }

@@ -222,6 +222,30 @@ __global__ void copy_channels_kernel(const bf16* __restrict__ src, int scs, int 
   dst[m * dcs + doff + c] = src[m * scs + soff + c];
 }
 
+// im2col in the packed-weight K order (tap-major, cin8 chunks, zero K tail):
+// col[m][k], k = (kh*KW + kw)*cin8 + c.  One thread per 8 channels.
+__global__ void im2col_kernel(const bf16* __restrict__ x, int H, int W, int xcs, int xoff, int cin8, int KH, int KW,
+                              int SH, int SW, int PH, int PW, int OH, int OW, int kpad, long M, bf16* __restrict__ col) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int kc = kpad >> 3;
+  if (idx >= M * kc) return;
+  const long m = idx / kc;
+  const int k = (int)(idx - m * kc) * 8;
+  const int OHW = OH * OW;
+  const int n = (int)(m / OHW);
+  const int rem = (int)(m - (long)n * OHW);
+  const int oh = rem / OW, ow = rem - (rem / OW) * OW;
+  const int tap = k / cin8, c = k - tap * cin8;
+  u32x4 v = {0u, 0u, 0u, 0u};
+  if (tap < KH * KW) {
+    const int kh = tap / KW, kw = tap - (tap / KW) * KW;
+    const int ih = oh * SH - PH + kh, iw = ow * SW - PW + kw;
+    if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+      v = *(const u32x4*)(x + (((long)n * H + ih) * W + iw) * xcs + xoff + c);
+  }
+  *(u32x4*)(col + m * kpad + k) = v;
+}
+
 inline unsigned nblk(long total, int bs) { return (unsigned)((total + bs - 1) / bs); }
 
 }  // namespace
@@ -281,5 +305,14 @@ extern "C" int jr_copy_channels(const void* src, int s_cstride, int s_coff, void
   const long total = (long)M * C;
   hipLaunchKernelGGL(copy_channels_kernel, dim3(nblk(total, 256)), dim3(256), 0, stream, (const bf16*)src, s_cstride,
                      s_coff, (bf16*)dst, d_cstride, d_coff, M, C);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jr_im2col(const void* x, int N, int H, int W, int x_cstride, int x_coff, int cin8, int KH, int KW,
+                         int SH, int SW, int PH, int PW, int OH, int OW, int kpad, void* col, hipStream_t stream) {
+  if (cin8 % 8 || kpad % 8 || x_cstride % 8 || x_coff % 8) return (int)hipErrorInvalidValue;
+  const long M = (long)N * OH * OW;
+  hipLaunchKernelGGL(im2col_kernel, dim3(nblk(M * (kpad / 8), 256)), dim3(256), 0, stream, (const bf16*)x, H, W,
+                     x_cstride, x_coff, cin8, KH, KW, SH, SW, PH, PW, OH, OW, kpad, M, (bf16*)col);
   return (int)hipGetLastError();
 }

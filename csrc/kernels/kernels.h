@@ -26,6 +26,8 @@ struct ConvParams {
   int x_cstride, x_coff;
   int cin8;         // input channels used for K, multiple of 8
   int KH, KW, SH, SW, PH, PW;
+  int dsh, dsw;     // log2 input dilation (transposed-conv / data-gradient mode): tap reads
+                    // dilated coordinate y, valid iff y % 2^dsh == 0, source row y >> dsh
   int OH, OW;
   int M;            // N*OH*OW
   long x_bytes;     // bytes addressable through x (buffer range check, <= 2 GiB)
@@ -86,6 +88,11 @@ int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int w, int C, 
 int jr_corr_lookup(const void* const* levels, int num_levels, int B, int h, int w, int radius,
                    const float* coords, void* out, int out_cstride, int lv_bf16, hipStream_t stream);
 
+// Backward of jr_corr_lookup w.r.t. the levels: accumulates into fp32 dlevels
+// (same shapes as the levels).  gout: bf16 (g_bf16=1) or fp32 [B*h*w][gcs].
+int jr_corr_lookup_bwd(void* const* dlevels, int num_levels, int B, int h, int w, int radius,
+                       const float* coords, const void* gout, int gcs, int g_bf16, hipStream_t stream);
+
 // ---------------------------------------------------------------------------
 // Flow upsampling x8.
 // ---------------------------------------------------------------------------
@@ -101,6 +108,9 @@ int jr_upsample_bilinear(const float* flow, int B, int h, int w, float* out, hip
 int jr_prep_images(const float* img1, const float* img2, int B, int H, int W, void* out, hipStream_t stream);
 // coords[b][y][x] = (x, y); flow32 = 0
 int jr_init_coords(float* coords, int B, int h, int w, hipStream_t stream);
+// im2col of x (bf16 NHWC, channel slice) into col [N*OH*OW][kpad] in the packed-weight K order
+int jr_im2col(const void* x, int N, int H, int W, int x_cstride, int x_coff, int cin8, int KH, int KW,
+              int SH, int SW, int PH, int PW, int OH, int OW, int kpad, void* col, hipStream_t stream);
 // copy bf16 channel slice: dst[m][doff + c] = src[m][soff + c], c < C
 int jr_copy_channels(const void* src, int s_cstride, int s_coff, void* dst, int d_cstride, int d_coff,
                      int M, int C, hipStream_t stream);

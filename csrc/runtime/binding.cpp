@@ -60,9 +60,10 @@ static void check_f32(const at::Tensor& t, const char* name) {
 // ----------------------------------------------------------------------- conv
 // t = [x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3]
 // i = [N, H, W, x_coff, cin8, KH, KW, SH, SW, PH, PW, cout, act, split,
-//      y_coff, y2_coff, res_coff, hidden, y3_coff, epi, cfg, res_post]
+//      y_coff, y2_coff, res_coff, hidden, y3_coff, epi, cfg, res_post
+//      (, OH_override, OW_override, log2 dil_h, log2 dil_w)]
 static Launch make_conv(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep) {
-  TORCH_CHECK(i.size() == 22, "conv: expected 22 ints");
+  TORCH_CHECK(i.size() == 22 || i.size() == 26, "conv: expected 22 or 26 ints");
   at::Tensor x = opt(t, 0), w = opt(t, 1), bias = opt(t, 2), y = opt(t, 3), y2 = opt(t, 4), res = opt(t, 5);
   at::Tensor h32 = opt(t, 6), zbuf = opt(t, 7), coords = opt(t, 8), flow32 = opt(t, 9), y3 = opt(t, 10);
   check_bf16(x, "x");
@@ -74,8 +75,13 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   p.N = (int)i[0]; p.H = (int)i[1]; p.W = (int)i[2];
   p.x_cstride = cs(x); p.x_coff = (int)i[3]; p.cin8 = (int)i[4];
   p.KH = (int)i[5]; p.KW = (int)i[6]; p.SH = (int)i[7]; p.SW = (int)i[8]; p.PH = (int)i[9]; p.PW = (int)i[10];
-  p.OH = (p.H + 2 * p.PH - p.KH) / p.SH + 1;
-  p.OW = (p.W + 2 * p.PW - p.KW) / p.SW + 1;
+  p.dsh = i.size() == 26 ? (int)i[24] : 0;
+  p.dsw = i.size() == 26 ? (int)i[25] : 0;
+  TORCH_CHECK(p.dsh >= 0 && p.dsh <= 3 && p.dsw >= 0 && p.dsw <= 3, "conv: dilation must be 1, 2, 4 or 8");
+  p.OH = ((p.H << p.dsh) - ((1 << p.dsh) - 1) + 2 * p.PH - p.KH) / p.SH + 1;
+  p.OW = ((p.W << p.dsw) - ((1 << p.dsw) - 1) + 2 * p.PW - p.KW) / p.SW + 1;
+  if (i.size() == 26 && i[22] > 0) p.OH = (int)i[22];
+  if (i.size() == 26 && i[23] > 0) p.OW = (int)i[23];
   p.M = p.N * p.OH * p.OW;
   p.x_bytes = x.numel() * 2;
   p.w_bytes = w.numel() * 2;
@@ -341,6 +347,54 @@ static Launch make_copy_channels(const TList& t, const IList& i, std::vector<at:
   return [=](hipStream_t s, int) { return jr_copy_channels(ap, acs, so, bp, bcs, dof, M, C, s); };
 }
 
+// t = [coords, gout, dl0, dl1, dl2, dl3], i = [num_levels, B, h, w, radius]
+static Launch make_lookup_bwd(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor coords = opt(t, 0), g = opt(t, 1);
+  check_f32(coords, "coords");
+  TORCH_CHECK(g.defined() && g.is_cuda() && g.is_contiguous() &&
+              (g.scalar_type() == at::kFloat || g.scalar_type() == at::kBFloat16), "lookup_bwd: grad");
+  const int L = (int)i[0], B = (int)i[1], h = (int)i[2], w = (int)i[3], r = (int)i[4];
+  const int S = 2 * r + 1;
+  TORCH_CHECK(L >= 1 && L <= 4 && r >= 1 && r <= 6 && cs(g) >= L * S * S, "lookup_bwd: shape");
+  TORCH_CHECK(g.numel() >= (int64_t)B * h * w * cs(g), "lookup_bwd: grad size");
+  std::vector<void*> lv(4, nullptr);
+  int hl = h, wl = w;
+  for (int l = 0; l < L; ++l) {
+    at::Tensor v = opt(t, 2 + l);
+    check_f32(v, "dlevel");
+    TORCH_CHECK(v.numel() >= (int64_t)B * h * w * hl * wl, "lookup_bwd: dlevel size");
+    lv[l] = v.data_ptr();
+    if (keep) keep->push_back(v);
+    hl >>= 1; wl >>= 1;
+  }
+  if (keep) { keep->push_back(coords); keep->push_back(g); }
+  const float* cp = coords.data_ptr<float>();
+  const void* gp = g.data_ptr();
+  const int gcs = cs(g);
+  const int gbf = g.scalar_type() == at::kBFloat16;
+  return [=](hipStream_t s, int) { return jr_corr_lookup_bwd(lv.data(), L, B, h, w, r, cp, gp, gcs, gbf, s); };
+}
+
+// t = [x, col], i = [N, H, W, x_coff, cin8, KH, KW, SH, SW, PH, PW]
+static Launch make_im2col(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor x = opt(t, 0), col = opt(t, 1);
+  check_bf16(x, "x"); check_bf16(col, "col");
+  const int N = (int)i[0], H = (int)i[1], W = (int)i[2], xoff = (int)i[3], cin8 = (int)i[4];
+  const int KH = (int)i[5], KW = (int)i[6], SH = (int)i[7], SW = (int)i[8], PH = (int)i[9], PW = (int)i[10];
+  const int OH = (H + 2 * PH - KH) / SH + 1, OW = (W + 2 * PW - KW) / SW + 1;
+  const int kpad = cs(col);
+  TORCH_CHECK(cin8 % 8 == 0 && xoff % 8 == 0 && cs(x) % 8 == 0 && xoff + cin8 <= cs(x), "im2col: input slice");
+  TORCH_CHECK(kpad % 8 == 0 && kpad >= KH * KW * cin8, "im2col: kpad");
+  TORCH_CHECK(x.numel() >= (int64_t)N * H * W * cs(x) && col.numel() >= (int64_t)N * OH * OW * kpad, "im2col: sizes");
+  if (keep) { keep->push_back(x); keep->push_back(col); }
+  const void* xp = x.data_ptr();
+  void* cp = col.data_ptr();
+  const int xcs = cs(x);
+  return [=](hipStream_t s, int) {
+    return jr_im2col(xp, N, H, W, xcs, xoff, cin8, KH, KW, SH, SW, PH, PW, OH, OW, kpad, cp, s);
+  };
+}
+
 static void run_now(const Launch& l) { JR_CHECK_OK(l(cur_stream(), 0)); }
 
 // ---------------------------------------------------------------- eager ops
@@ -357,6 +411,8 @@ void norm_act_op(const TList& t, IList i, double eps) { run_now(make_norm_act(t,
 void prep_op(const TList& t, IList i) { run_now(make_prep(t, i, nullptr)); }
 void init_coords_op(const TList& t, IList i) { run_now(make_init_coords(t, i, nullptr)); }
 void copy_channels_op(const TList& t, IList i) { run_now(make_copy_channels(t, i, nullptr)); }
+void lookup_bwd_op(const TList& t, IList i) { run_now(make_lookup_bwd(t, i, nullptr)); }
+void im2col_op(const TList& t, IList i) { run_now(make_im2col(t, i, nullptr)); }
 
 // --------------------------------------------------------------------- Plan
 class Plan : public torch::CustomClassHolder {
@@ -455,6 +511,8 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("prep(Tensor?[] t, int[] i) -> ()", &jr::prep_op);
   m.def("init_coords(Tensor?[] t, int[] i) -> ()", &jr::init_coords_op);
   m.def("copy_channels(Tensor?[] t, int[] i) -> ()", &jr::copy_channels_op);
+  m.def("lookup_bwd(Tensor?[] t, int[] i) -> ()", &jr::lookup_bwd_op);
+  m.def("im2col(Tensor?[] t, int[] i) -> ()", &jr::im2col_op);
   m.class_<jr::Plan>("Plan")
       .def(torch::init<>())
       .def("set_segment", &jr::Plan::set_segment)

@@ -21,6 +21,7 @@ import torch
 from torch import nn
 
 from . import reference as R
+from ..ops import functional as OF
 
 # --------------------------------------------------------------------------- init
 
@@ -75,7 +76,7 @@ class Conv(nn.Module):
         (kaiming_fan_out_ if init == "kaiming" else lecun_normal_)(self.kernel.data, gen)
 
     def forward(self, x):
-        return R.conv2d_nhwc(x, self.kernel, self.bias, self.stride, self.padding)
+        return OF.conv2d_nhwc(x, self.kernel, self.bias, self.stride, self.padding)
 
 
 class BatchNorm(nn.Module):
@@ -348,9 +349,9 @@ class CorrBlock:
         self.out_channels = num_levels * (2 * radius + 1) ** 2
 
     def build_pyramid(self, fmap1, fmap2):
-        return R.build_pyramid(fmap1, fmap2, self.num_levels)
+        return OF.build_pyramid(fmap1, fmap2, self.num_levels)
 
     def index_pyramid(self, corr_pyramid, centroids_coords):
-        out = R.index_pyramid(corr_pyramid, centroids_coords, self.radius)
+        out = OF.index_pyramid(corr_pyramid, centroids_coords, self.radius)
         assert out.shape[-1] == self.out_channels
         return out

@@ -136,7 +136,8 @@ def upsample_flow(flow: torch.Tensor, up_mask: Optional[torch.Tensor] = None, fa
         up = resize_with_aligned_corners(flow, (B, nh, nw, C), method="bilinear", antialias=False)
         return factor * up
     assert up_mask.shape == (B, h, w, 9 * factor * factor)
-    m = up_mask.reshape(B, h, w, 9, factor, factor)
+    flow = flow.float()
+    m = up_mask.float().reshape(B, h, w, 9, factor, factor)
     m = torch.softmax(m, dim=3)
     fp = F.pad((factor * flow).permute(0, 3, 1, 2), (1, 1, 1, 1))  # (B, C, h+2, w+2)
     neigh = []
@@ -171,11 +172,13 @@ def conv2d_nhwc(
 
 def instance_norm_nhwc(x: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
     """Flax ``nn.InstanceNorm(epsilon=1e-5, use_bias=False, use_scale=False)``
-    (``model.py:706-707``): per (n, c) over H, W, biased variance."""
-    mean = x.mean(dim=(1, 2), keepdim=True)
-    var = (x * x).mean(dim=(1, 2), keepdim=True) - mean * mean
+    (``model.py:706-707``): per (n, c) over H, W, biased variance.  Statistics
+    in fp32 whatever the input dtype."""
+    xf = x.float()
+    mean = xf.mean(dim=(1, 2), keepdim=True)
+    var = (xf * xf).mean(dim=(1, 2), keepdim=True) - mean * mean
     var = var.clamp_min(0.0)
-    return (x - mean) * torch.rsqrt(var + eps)
+    return ((xf - mean) * torch.rsqrt(var + eps)).to(x.dtype)
 
 
 def batch_norm_nhwc(
@@ -194,6 +197,8 @@ def batch_norm_nhwc(
     Returns ``(y, new_mean, new_var)``; in eval mode the running statistics are
     used and returned unchanged.
     """
+    dt = x.dtype
+    x = x.float()
     if train:
         bmean = x.mean(dim=(0, 1, 2))
         bvar = (x * x).mean(dim=(0, 1, 2)) - bmean * bmean
@@ -205,7 +210,7 @@ def batch_norm_nhwc(
         new_mean, new_var = mean, var
         m, v = mean, var
     y = (x - m) * torch.rsqrt(v + eps) * scale + bias
-    return y, new_mean, new_var
+    return y.to(dt), new_mean, new_var
 
 
 def corr_volume(fmap1: torch.Tensor, fmap2: torch.Tensor) -> torch.Tensor:

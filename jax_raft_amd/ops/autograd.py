@@ -1,0 +1,184 @@
+"""Autograd Functions over the native gfx950 kernels (the GPU training path).
+
+=====================  ==========================================  ==========================================
+op                     forward                                     backward
+=====================  ==========================================  ==========================================
+conv2d (NHWC, HWIO)    implicit-GEMM MFMA kernel                   dX: same kernel, flipped/transposed weights,
+                                                                   input-dilation mode for strided convs;
+                                                                   dW: native im2col + library GEMM; db: sum
+corr pyramid           MFMA GEMM with fused 2x2 pooling (fp32)     pooling adjoint + library GEMMs
+pyramid lookup         radius-r bilinear gather kernel             native scatter kernel (no atomics)
+=====================  ==========================================  ==========================================
+
+Everything else in the RAFT graph (norms, gates, concat, upsampling, loss)
+is PyTorch glue on the framework layer.  ``coords`` never receive a gradient
+(``stop_gradient`` at ``jax_raft/model.py:498``).
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Sequence, Tuple
+
+import torch
+
+from . import native as nat
+
+BF16 = torch.bfloat16
+
+
+def _pad_channels(x: torch.Tensor, c8: int) -> torch.Tensor:
+    """bf16 contiguous NHWC with the channel dim zero-padded to ``c8``."""
+    C = x.shape[-1]
+    if C == c8 and x.dtype == BF16 and x.is_contiguous():
+        return x
+    out = torch.zeros(x.shape[:-1] + (c8,), dtype=BF16, device=x.device)
+    out[..., :C] = x
+    return out
+
+
+def _log2_stride(s: int) -> int:
+    if s not in (1, 2, 4, 8):
+        raise NotImplementedError(f"native conv backward supports strides 1/2/4/8, got {s}")
+    return int(math.log2(s))
+
+
+class Conv2dNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, kernel, bias, stride: Tuple[int, int], padding: Tuple[int, int]):
+        kh, kw, cin, cout = kernel.shape
+        N, H, W, C = x.shape
+        assert C == cin, f"conv input has {C} channels, kernel expects {cin}"
+        cin8 = nat.round_up(cin, 8)
+        xb = _pad_channels(x, cin8)
+        spec = nat.make_spec(kernel.detach(), bias.detach(), tuple(stride), tuple(padding), cin8=cin8, device=x.device)
+        y = nat.conv2d(spec, xb, out_dtype=BF16)
+        ctx.save_for_backward(xb, kernel)
+        ctx.meta = (N, H, W, cin, cout, tuple(stride), tuple(padding))
+        ctx.bias_requires_grad = bias.requires_grad
+        return y.contiguous() if not y.is_contiguous() else y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xb, kernel = ctx.saved_tensors
+        N, H, W, cin, cout, (sh, sw), (ph, pw) = ctx.meta
+        kh, kw = kernel.shape[:2]
+        OH, OW = gy.shape[1], gy.shape[2]
+        cout8 = nat.round_up(cout, 8)
+        gyb = _pad_channels(gy, cout8)
+        gx = gk = gb = None
+        if ctx.needs_input_grad[0]:
+            # dX = conv(dilate_s(dY), flip(W)^T), padding k-1-p, output size forced to (H, W)
+            wt = torch.flip(kernel.detach().float(), dims=(0, 1)).permute(0, 1, 3, 2).contiguous()
+            spec = nat.make_spec(wt, torch.zeros(cin, device=gy.device), (1, 1), (kh - 1 - ph, kw - 1 - pw),
+                                 cin8=cout8, device=gy.device)
+            gxp = torch.empty(N, H, W, nat.round_up(cin, 8), dtype=BF16, device=gy.device)
+            t, i, a = nat.conv_args(spec, gyb, N, OH, OW, gxp)
+            i = i + [H, W, _log2_stride(sh), _log2_stride(sw)]
+            nat.ops().conv(t, i, a)
+            gx = gxp[..., :cin]
+        if ctx.needs_input_grad[1]:
+            cin8 = xb.shape[-1]
+            kpad = nat.round_up(kh * kw * cin8, 64)
+            M = N * OH * OW
+            col = torch.empty(M, kpad, dtype=BF16, device=gy.device)
+            nat.ops().im2col([xb, col], [N, H, W, 0, cin8, kh, kw, sh, sw, ph, pw])
+            gw = torch.matmul(gyb.reshape(M, cout8).t()[:cout], col).float()  # (cout, kpad)
+            gw = gw[:, : kh * kw * cin8].reshape(cout, kh, kw, cin8)[..., :cin]
+            gk = gw.permute(1, 2, 3, 0).contiguous()
+        if ctx.bias_requires_grad:
+            gb = gy.float().sum(dim=(0, 1, 2))
+        return gx, gk, gb, None, None
+
+
+def conv2d_nhwc(x, kernel, bias, stride=(1, 1), padding=(0, 0)):
+    return Conv2dNHWC.apply(x, kernel, bias, tuple(stride), tuple(padding))
+
+
+class CorrPyramid(torch.autograd.Function):
+    """fmap1, fmap2 (B, h, w, C) -> L fp32 levels (B*h*w, h_l, w_l)."""
+
+    @staticmethod
+    def forward(ctx, fmap1, fmap2, num_levels: int):
+        B, h, w, C = fmap1.shape
+        f1 = fmap1.to(BF16).contiguous()
+        f2 = fmap2.to(BF16).contiguous()
+        M = B * h * w
+        levels = []
+        hl, wl = h, w
+        for _ in range(num_levels):
+            levels.append(torch.empty(M, hl, wl, device=fmap1.device, dtype=torch.float32))
+            hl //= 2
+            wl //= 2
+        if C % 64 == 0:
+            nat.ops().corr([f1, f2] + levels + [None] * (4 - num_levels), [B, h, w, C, num_levels], 1.0 / math.sqrt(C))
+        else:  # channel count the MFMA kernel does not tile: library GEMM + pooling
+            vol = torch.matmul(f1.float().reshape(B, h * w, C), f2.float().reshape(B, h * w, C).transpose(1, 2))
+            vol = (vol / math.sqrt(C)).reshape(M, h, w)
+            levels[0].copy_(vol)
+            for l in range(1, num_levels):
+                p = levels[l - 1]
+                hh, ww = p.shape[1] // 2, p.shape[2] // 2
+                levels[l].copy_(p[:, : 2 * hh, : 2 * ww].reshape(M, hh, 2, ww, 2).mean(dim=(2, 4)))
+        ctx.save_for_backward(f1, f2)
+        ctx.shape = (B, h, w, C, num_levels)
+        return tuple(levels)
+
+    @staticmethod
+    def backward(ctx, *glevels):
+        f1, f2 = ctx.saved_tensors
+        B, h, w, C, L = ctx.shape
+        M = B * h * w
+        dC = torch.zeros(M, h, w, device=f1.device, dtype=torch.float32)
+        for l, g in enumerate(glevels):
+            if g is None:
+                continue
+            s = 2 ** l
+            hl, wl = g.shape[1], g.shape[2]
+            up = g.float().repeat_interleave(s, dim=1).repeat_interleave(s, dim=2) / float(s * s)
+            dC[:, : hl * s, : wl * s] += up
+        dC = dC.reshape(B, h * w, h * w) / math.sqrt(C)
+        g1 = torch.matmul(dC, f2.float().reshape(B, h * w, C)).reshape(B, h, w, C)
+        g2 = torch.matmul(dC.transpose(1, 2), f1.float().reshape(B, h * w, C)).reshape(B, h, w, C)
+        return g1, g2, None
+
+
+def build_pyramid(fmap1, fmap2, num_levels: int) -> List[torch.Tensor]:
+    return list(CorrPyramid.apply(fmap1, fmap2, num_levels))
+
+
+class PyramidLookup(torch.autograd.Function):
+    """levels (fp32), coords (B, h, w, 2) -> (B, h, w, L*(2r+1)^2) bf16."""
+
+    @staticmethod
+    def forward(ctx, coords, radius: int, *levels):
+        B, h, w, _ = coords.shape
+        L = len(levels)
+        S = 2 * radius + 1
+        ocs = nat.round_up(L * S * S, 8)
+        c = coords.detach().float().reshape(B * h * w, 2).contiguous()
+        out = torch.empty(B * h * w, ocs, dtype=BF16, device=coords.device)
+        lv = [l.contiguous() for l in levels]
+        nat.ops().lookup([c, out] + lv + [None] * (4 - L), [L, B, h, w, radius])
+        ctx.save_for_backward(c)
+        ctx.meta = (B, h, w, radius, L, [tuple(l.shape) for l in levels])
+        return out.reshape(B, h, w, ocs)[..., : L * S * S]
+
+    @staticmethod
+    def backward(ctx, g):
+        (c,) = ctx.saved_tensors
+        B, h, w, radius, L, shapes = ctx.meta
+        g = g.reshape(B * h * w, -1).float().contiguous()
+        dls = [torch.zeros(s, device=g.device, dtype=torch.float32) for s in shapes]
+        nat.ops().lookup_bwd([c, g] + dls + [None] * (4 - L), [L, B, h, w, radius])
+        return (None, None) + tuple(dls)
+
+
+def index_pyramid(pyramid: Sequence[torch.Tensor], coords, radius: int):
+    return PyramidLookup.apply(coords, radius, *pyramid)
+
+
+def raft_forward_autograd(model, image1, image2, train: bool, num_flow_updates: int):
+    """GPU forward with autograd: the module graph of
+    :meth:`RAFT.forward_reference` with its conv / correlation / lookup nodes
+    dispatched to the native Functions above (see :mod:`jax_raft_amd.ops.functional`)."""
+    return model.forward_reference(image1, image2, train, num_flow_updates)
