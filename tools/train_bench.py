@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Training throughput (BASELINE config 5): raft_large on synthetic
+FlyingChairs-shaped 384x512 pairs, 12 refinement iterations, sequence loss,
+AdamW + one-cycle, grad clip 1.0, RCCL gradient all-reduce when launched
+with torchrun.  Prints one JSON line (rank 0): pairs/s over the whole job."""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from jax_raft_amd.parallel import dp  # noqa: E402
+from jax_raft_amd.train.trainer import TrainConfig, Trainer  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--arch", default="raft_large")
+    ap.add_argument("--batch", type=int, default=6)
+    ap.add_argument("--iters", type=int, default=12)
+    ap.add_argument("--size", type=int, nargs=2, default=[384, 512])
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    a = ap.parse_args()
+    cfg = TrainConfig(arch=a.arch, steps=a.steps + a.warmup, batch=a.batch, iters=a.iters, size=tuple(a.size),
+                      log_every=10 ** 9)
+    tr = Trainer(cfg)
+    batches = [tr.batch_for(i) for i in range(2)]
+    for i in range(a.warmup):
+        tr.train_step(batches[i % 2])
+    torch.cuda.synchronize()
+    if dp.is_dist():
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        m = tr.train_step(batches[i % 2])
+    torch.cuda.synchronize()
+    dt = torch.tensor([time.perf_counter() - t0], device=tr.device, dtype=torch.float64)
+    if dp.is_dist():
+        torch.distributed.all_reduce(dt, op=torch.distributed.ReduceOp.MAX)
+    el = dt.item()
+    if tr.rank == 0:
+        print(json.dumps({"metric": "training image-pairs/sec (config 5)", "value": round(tr.world * a.batch * a.steps / el, 3),
+                          "unit": "image-pairs/s", "n_gpus": tr.world, "ms_per_step": round(1000 * el / a.steps, 2),
+                          "loss": float(m["loss"]), "config": {"model": a.arch, "per_gpu_batch": a.batch,
+                          "image_size": list(a.size), "num_flow_updates": a.iters, "parallelism": f"dp{tr.world}",
+                          "dtype": "bf16 (fp32 master weights)"}}), flush=True)
+    if dp.is_dist():
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
