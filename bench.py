@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--iters", type=int, default=32)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-h2d", action="store_true", help="inputs already resident on the GPU")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse >1 rank on fewer GPUs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -48,13 +50,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} != WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    ndev = torch.cuda.device_count()
+    dev_index = local_rank % ndev if args.dist_backend == "gloo" else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     pg = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
         pg = dist
 
     from jax_raft_amd import raft_large, raft_small
@@ -92,7 +99,7 @@ def main():
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     barrier()
-    dt = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    dt = torch.tensor([t1 - t0], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
     if pg is not None:
         pg.all_reduce(dt, op=pg.ReduceOp.MAX)
     elapsed = dt.item()
