@@ -91,16 +91,130 @@ JR_DEVICE int chan_base(int wrow0, int lq) {
 // Shared epilogue.  Lane (li, lq) of wave (wco, wp) holds, for each pixel tile
 // tn, NV = 4*TM contiguous output channels starting at cbase (see the weight
 // row permutation in jax_raft_amd/ops/native.py:pack_weight).
+// Per-pixel epilogue: v[NV] holds the raw accumulators of NV contiguous
+// output channels [cbase, cbase + NV) of output pixel m (bias not yet added).
+template <int NV, int EPI>
+JR_DEVICE void epi_pixel(const ConvParams& p, float (&v)[NV], int m, int cbase) {
+  const bool full = cbase + NV <= p.cout;
+  const int OHW = p.OH * p.OW;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] += (cbase + j < p.cout) ? p.bias[cbase + j] : 0.f;
+  if constexpr (EPI == EPI_STD) {
+    if (p.res) {
+      float rv[NV];
+      const bf16* rp = (const bf16*)p.res + (long)m * p.res_cstride + p.res_coff + cbase;
+      if (full) {
+        load_bf16<NV>(rp, rv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) rv[j] = (cbase + j < p.cout) ? bf2f(rp[j]) : 0.f;
+      }
+      if (p.res_post) {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) v[j] = fmaxf(apply_act(v[j], p.act, cbase + j, p.split) + rv[j], 0.f);
+      } else {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) v[j] = apply_act(v[j] + rv[j], p.act, cbase + j, p.split);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v[j] = apply_act(v[j], p.act, cbase + j, p.split);
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] *= p.alpha;
+    if (p.y_fp32) {
+      float* yp = (float*)p.y + (long)m * p.y_cstride + p.y_coff + cbase;
+      if (full) store_f32<NV>(yp, v);
+      else {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) if (cbase + j < p.cout) yp[j] = v[j];
+      }
+    } else {
+      bf16* yp = (bf16*)p.y + (long)m * p.y_cstride + p.y_coff + cbase;
+      if (full) store_bf16<NV>(yp, v);
+      else {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) if (cbase + j < p.cout) yp[j] = f2bf(v[j]);
+      }
+    }
+    if (p.y2) {
+      bf16* yp = (bf16*)p.y2 + (long)m * p.y2_cstride + p.y2_coff + cbase;
+      if (full) store_bf16<NV>(yp, v);
+      else {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) if (cbase + j < p.cout) yp[j] = f2bf(v[j]);
+      }
+    }
+    if (p.h32) {  // fp32 copy of the channels below `split` (context-encoder hidden state)
+      if (cbase < p.split) {
+        float* hp = p.h32 + (long)m * p.hidden + cbase;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) if (cbase + j < p.split) hp[j] = v[j];
+      }
+    }
+  } else if constexpr (EPI == EPI_GRU_A) {
+    // [z | r] logits -> z (fp32) and r*h (bf16) into the q-input buffer.
+    const int hd = p.hidden;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = sigmoidf_(v[j]);
+    if (cbase < hd) {
+      store_f32<NV>((float*)p.zbuf + (long)m * hd + cbase, v);
+    } else {
+      const int hc = cbase - hd;
+      float h[NV];
+      load_f32<NV>(p.h32 + (long)m * hd + hc, h);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v[j] *= h[j];
+      store_bf16<NV>((bf16*)p.y + (long)m * p.y_cstride + p.y_coff + hc, v);
+    }
+  } else if constexpr (EPI == EPI_GRU_B) {
+    const int hd = p.hidden;
+    float z[NV], h[NV];
+    load_f32<NV>((const float*)p.zbuf + (long)m * hd + cbase, z);
+    float* hp = p.h32 + (long)m * hd + cbase;
+    load_f32<NV>(hp, h);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const float q = tanhf_(v[j]);
+      v[j] = (1.0f - z[j]) * h[j] + z[j] * q;
+    }
+    store_f32<NV>(hp, v);
+    store_bf16<NV>((bf16*)p.y + (long)m * p.y_cstride + p.y_coff + cbase, v);
+    if (p.y2) store_bf16<NV>((bf16*)p.y2 + (long)m * p.y2_cstride + p.y2_coff + cbase, v);
+  } else if constexpr (EPI == EPI_FLOW) {
+    if (cbase == 0) {
+      const int rem = m % OHW;
+      const int py = rem / p.OW;
+      const int px = rem - py * p.OW;
+      const float cx = p.coords[2 * (long)m] + v[0];
+      const float cy = p.coords[2 * (long)m + 1] + v[1];
+      p.coords[2 * (long)m] = cx;
+      p.coords[2 * (long)m + 1] = cy;
+      const float fx = cx - (float)px;
+      const float fy = cy - (float)py;
+      p.flow32[2 * (long)m] = fx;
+      p.flow32[2 * (long)m + 1] = fy;
+      bf16* yp = (bf16*)p.y + (long)m * p.y_cstride + p.y_coff;
+      yp[0] = f2bf(fx); yp[1] = f2bf(fy);
+      if (p.y2) {
+        bf16* y2p = (bf16*)p.y2 + (long)m * p.y2_cstride + p.y2_coff;
+        y2p[0] = f2bf(fx); y2p[1] = f2bf(fy);
+      }
+      if (p.y3) {
+        bf16* y3p = (bf16*)p.y3 + (long)m * p.y3_cstride + p.y3_coff;
+        y3p[0] = f2bf(fx); y3p[1] = f2bf(fy);
+      }
+    }
+  }
+}
+
+// Epilogue of the 16x16x32 kernels.  Lane (li, lq) of wave (wco, wp) holds,
+// for each pixel tile tn, NV = 4*TM contiguous output channels starting at
+// cbase (see the weight row permutation in jax_raft_amd/ops/native.py:pack_weight).
 template <int TM, int TN, int EPI>
 JR_DEVICE void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM][TN], int mbase, int cbase, int li) {
   constexpr int NV = 4 * TM;
   if (cbase >= p.cout) return;
-  const int OHW = p.OH * p.OW;
-  const bool full = cbase + NV <= p.cout;
-  float bias[NV];
-#pragma unroll
-  for (int j = 0; j < NV; ++j) bias[j] = (cbase + j < p.cout) ? p.bias[cbase + j] : 0.f;
-
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
     const int m = mbase + tn * 16 + li;
@@ -109,115 +223,8 @@ JR_DEVICE void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM][TN], int mbas
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[tm * 4 + r] = acc[tm][tn][r] + bias[tm * 4 + r];
-
-    if constexpr (EPI == EPI_STD) {
-      if (p.res) {
-        float rv[NV];
-        const bf16* rp = (const bf16*)p.res + (long)m * p.res_cstride + p.res_coff + cbase;
-        if (full) {
-          load_bf16<NV>(rp, rv);
-        } else {
-#pragma unroll
-          for (int j = 0; j < NV; ++j) rv[j] = (cbase + j < p.cout) ? bf2f(rp[j]) : 0.f;
-        }
-        if (p.res_post) {
-#pragma unroll
-          for (int j = 0; j < NV; ++j) v[j] = fmaxf(apply_act(v[j], p.act, cbase + j, p.split) + rv[j], 0.f);
-        } else {
-#pragma unroll
-          for (int j = 0; j < NV; ++j) v[j] = apply_act(v[j] + rv[j], p.act, cbase + j, p.split);
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < NV; ++j) v[j] = apply_act(v[j], p.act, cbase + j, p.split);
-      }
-#pragma unroll
-      for (int j = 0; j < NV; ++j) v[j] *= p.alpha;
-      if (p.y_fp32) {
-        float* yp = (float*)p.y + (long)m * p.y_cstride + p.y_coff + cbase;
-        if (full) store_f32<NV>(yp, v);
-        else {
-#pragma unroll
-          for (int j = 0; j < NV; ++j) if (cbase + j < p.cout) yp[j] = v[j];
-        }
-      } else {
-        bf16* yp = (bf16*)p.y + (long)m * p.y_cstride + p.y_coff + cbase;
-        if (full) store_bf16<NV>(yp, v);
-        else {
-#pragma unroll
-          for (int j = 0; j < NV; ++j) if (cbase + j < p.cout) yp[j] = f2bf(v[j]);
-        }
-      }
-      if (p.y2) {
-        bf16* yp = (bf16*)p.y2 + (long)m * p.y2_cstride + p.y2_coff + cbase;
-        if (full) store_bf16<NV>(yp, v);
-        else {
-#pragma unroll
-          for (int j = 0; j < NV; ++j) if (cbase + j < p.cout) yp[j] = f2bf(v[j]);
-        }
-      }
-      if (p.h32) {  // fp32 copy of the channels below `split` (context-encoder hidden state)
-        if (cbase < p.split) {
-          float* hp = p.h32 + (long)m * p.hidden + cbase;
-#pragma unroll
-          for (int j = 0; j < NV; ++j) if (cbase + j < p.split) hp[j] = v[j];
-        }
-      }
-    } else if constexpr (EPI == EPI_GRU_A) {
-      // [z | r] logits -> z (fp32) and r*h (bf16) into the q-input buffer.
-      const int hd = p.hidden;
-#pragma unroll
-      for (int j = 0; j < NV; ++j) v[j] = sigmoidf_(v[j]);
-      if (cbase < hd) {
-        store_f32<NV>((float*)p.zbuf + (long)m * hd + cbase, v);
-      } else {
-        const int hc = cbase - hd;
-        float h[NV];
-        load_f32<NV>(p.h32 + (long)m * hd + hc, h);
-#pragma unroll
-        for (int j = 0; j < NV; ++j) v[j] *= h[j];
-        store_bf16<NV>((bf16*)p.y + (long)m * p.y_cstride + p.y_coff + hc, v);
-      }
-    } else if constexpr (EPI == EPI_GRU_B) {
-      const int hd = p.hidden;
-      float z[NV], h[NV];
-      load_f32<NV>((const float*)p.zbuf + (long)m * hd + cbase, z);
-      float* hp = p.h32 + (long)m * hd + cbase;
-      load_f32<NV>(hp, h);
-#pragma unroll
-      for (int j = 0; j < NV; ++j) {
-        const float q = tanhf_(v[j]);
-        v[j] = (1.0f - z[j]) * h[j] + z[j] * q;
-      }
-      store_f32<NV>(hp, v);
-      store_bf16<NV>((bf16*)p.y + (long)m * p.y_cstride + p.y_coff + cbase, v);
-      if (p.y2) store_bf16<NV>((bf16*)p.y2 + (long)m * p.y2_cstride + p.y2_coff + cbase, v);
-    } else if constexpr (EPI == EPI_FLOW) {
-      if (cbase == 0) {
-        const int rem = m % OHW;
-        const int py = rem / p.OW;
-        const int px = rem - py * p.OW;
-        const float cx = p.coords[2 * (long)m] + v[0];
-        const float cy = p.coords[2 * (long)m + 1] + v[1];
-        p.coords[2 * (long)m] = cx;
-        p.coords[2 * (long)m + 1] = cy;
-        const float fx = cx - (float)px;
-        const float fy = cy - (float)py;
-        p.flow32[2 * (long)m] = fx;
-        p.flow32[2 * (long)m + 1] = fy;
-        bf16* yp = (bf16*)p.y + (long)m * p.y_cstride + p.y_coff;
-        yp[0] = f2bf(fx); yp[1] = f2bf(fy);
-        if (p.y2) {
-          bf16* y2p = (bf16*)p.y2 + (long)m * p.y2_cstride + p.y2_coff;
-          y2p[0] = f2bf(fx); y2p[1] = f2bf(fy);
-        }
-        if (p.y3) {
-          bf16* y3p = (bf16*)p.y3 + (long)m * p.y3_cstride + p.y3_coff;
-          y3p[0] = f2bf(fx); y3p[1] = f2bf(fy);
-        }
-      }
-    }
+      for (int r = 0; r < 4; ++r) v[tm * 4 + r] = acc[tm][tn][r];
+    epi_pixel<NV, EPI>(p, v, m, cbase);
   }
 }
 
@@ -387,6 +394,196 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
 
   const int wrow0 = co0 + wco * WTCO;
   conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, chan_base<TM>(wrow0, lq), li);
+}
+
+// ---------------------------------------------------------------------------
+// Kernel M32: as kernel R (register-staged operands, 64-deep K stages,
+// 2-stage prefetch) but on v_mfma_f32_32x32x16_bf16: half the MFMA
+// instructions (and MFMA issue-blocking cycles) per FLOP of the 16x16x32
+// form, the loop being issue-bound.  The 32x32 accumulator gives lane
+// (col = pixel, h = lane>>5) the D rows (r&3) + 8(r>>2) + 4h; the A-operand LDS
+// rows are read in the permuted order below so that those 16 rows are the 16
+// contiguous output channels 32t + 16h + r of the wave's 64-channel group
+// (stored permuted per pack_weight), keeping the epilogue vectorised.
+// ---------------------------------------------------------------------------
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// storage row (within a 64-row group) holding channel 32t + c(rho), c(rho) = 16((rho>>2)&1) + (rho&3) + 4(rho>>3)
+JR_DEVICE int m32_arow(int t, int rho) { return 16 * (rho >> 3) + 4 * (2 * t + ((rho >> 2) & 1)) + (rho & 3); }
+
+template <int BCO, int BP, int WCO, int EPI>
+__global__ __launch_bounds__(256) void conv_m32_kernel(const ConvParams p) {
+  constexpr int WP = 4 / WCO;
+  constexpr int WTCO = BCO / WCO;
+  constexpr int WTP = BP / WP;
+  constexpr int TM = WTCO / 32;
+  constexpr int TN = WTP / 32;
+  constexpr int XR = BP / 32;
+  constexpr int WR = BCO / 32;
+  constexpr int A_ELEMS = BCO * BK;
+  constexpr int B_ELEMS = BP * BK;
+  constexpr unsigned OOB = 0x80000000u;
+  static_assert(TM >= 1 && TN >= 1 && WCO * WP == 4 && BCO >= 32, "tile");
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (A_ELEMS + B_ELEMS)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wco = wave % WCO;
+  const int wp = wave / WCO;
+  const int p0 = blockIdx.x * BP;
+  const int co0 = blockIdx.y * BCO;
+  const int ch = tid & 7;
+  const int OHW = p.OH * p.OW;
+
+  const __amdgpu_buffer_rsrc_t xsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)p.w_bytes, 0x00020000);
+
+  int ih0[XR], iw0[XR];
+  unsigned rbase[XR];
+#pragma unroll
+  for (int i = 0; i < XR; ++i) {
+    const int m = p0 + (tid >> 3) + 32 * i;
+    if (m < p.M) {
+      const int n = m / OHW;
+      const int rem = m - n * OHW;
+      const int oh = rem / p.OW;
+      const int ow = rem - oh * p.OW;
+      ih0[i] = oh * p.SH - p.PH;
+      iw0[i] = ow * p.SW - p.PW;
+      rbase[i] = (unsigned)(((long)n * p.H * p.W * p.x_cstride + p.x_coff) * 2);
+    } else {
+      ih0[i] = -(1 << 28);
+      iw0[i] = -(1 << 28);
+      rbase[i] = 0;
+    }
+  }
+  const unsigned wrow_off = (unsigned)((co0 + (tid >> 3)) * p.kpad * 2 + ch * 16);
+  const unsigned wrow_lim = (unsigned)(p.cout_pad - co0 - (tid >> 3));
+  const int cpt = p.cin8 >> 3;
+  int tap = ch / cpt;
+  int cc = ch - tap * cpt;
+  int kh = tap / p.KW;
+  int kw = tap - kh * p.KW;
+  int ks_next = 0;
+  const unsigned xrow_bytes = (unsigned)p.x_cstride * 2;
+
+  struct Regs { u32x4 x[XR]; u32x4 w[WR]; };
+  Regs ra, rb;
+  auto issue = [&](Regs& r) {
+    const bool kvalid = kh < p.KH;
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      const int ihl = ih0[i] + kh, iwl = iw0[i] + kw;
+      const int ih = ihl >> p.dsh, iw = iwl >> p.dsw;
+      const bool ok = kvalid && ((ihl & ((1 << p.dsh) - 1)) | (iwl & ((1 << p.dsw) - 1))) == 0 &&
+                      (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      const unsigned off = rbase[i] + (unsigned)(ih * p.W + iw) * xrow_bytes + (unsigned)cc * 16u;
+      r.x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xsrd, ok ? off : OOB, 0, 0));
+    }
+    const unsigned kofs = (unsigned)ks_next * (BK * 2);
+#pragma unroll
+    for (int i = 0; i < WR; ++i) {
+      const bool ok = (unsigned)(32 * i) < wrow_lim && ks_next * BK < p.kpad;
+      const unsigned off = wrow_off + (unsigned)(32 * i) * (unsigned)p.kpad * 2u + kofs;
+      r.w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wsrd, ok ? off : OOB, 0, 0));
+    }
+    ++ks_next;
+    cc += 8;
+    while (cc >= cpt) {
+      cc -= cpt;
+      if (++kw == p.KW) { kw = 0; ++kh; }
+    }
+  };
+  auto store = [&](const Regs& r, int buf) {
+    bf16* sA = smem + buf * (A_ELEMS + B_ELEMS);
+    bf16* sB = sA + A_ELEMS;
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      const int rr = (tid >> 3) + 32 * i;
+      *(u32x4*)(sB + rr * BK + ((ch ^ swzB(rr)) << 3)) = r.x[i];
+    }
+#pragma unroll
+    for (int i = 0; i < WR; ++i) {
+      const int rr = (tid >> 3) + 32 * i;
+      *(u32x4*)(sA + rr * BK + ((ch ^ swzB(rr)) << 3)) = r.w[i];
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int rho = lane & 31;
+  const int hh = lane >> 5;
+  const int wbase = wco * WTCO;               // wave's first storage row in the block
+  const int tabs0 = ((co0 + wbase) & 63) >> 5;  // 32-row half of the 64-row group
+  const int gbase = wbase - ((co0 + wbase) & 63);  // block-relative start of that 64-row group
+  auto compute = [&](int buf) {
+    const bf16* sA = smem + buf * (A_ELEMS + B_ELEMS);
+    const bf16* sB = sA + A_ELEMS;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int chunk = kk * 2 + hh;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int row = gbase + m32_arow(tabs0 + tm, rho);
+        af[tm] = *(const bf16x8*)(sA + row * BK + ((chunk ^ swzB(row)) << 3));
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int row = wp * WTP + tn * 32 + rho;
+        bfr[tn] = *(const bf16x8*)(sB + row * BK + ((chunk ^ swzB(row)) << 3));
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm], bfr[tn], acc[tm][tn], 0, 0, 0);
+    }
+  };
+
+  const int nks = p.kpad / BK;
+  issue(ra);
+  issue(rb);
+  store(ra, 0);
+  __syncthreads();
+  const int npairs = nks >> 1;
+  for (int it = 0; it < npairs; ++it) {
+    issue(ra);
+    compute(0);
+    store(rb, 1);
+    __syncthreads();
+    issue(rb);
+    compute(1);
+    store(ra, 0);
+    __syncthreads();
+  }
+  if (nks & 1) compute(0);
+
+  // epilogue: tile tm of lane hh -> channels G + 32*(tabs0+tm) + 16*hh + [0,16)
+  const int G = (co0 + wbase) & ~63;
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int cbase = G + 32 * (tabs0 + tm) + 16 * hh;
+    if (cbase >= p.cout) continue;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int m = p0 + wp * WTP + tn * 32 + rho;
+      if (m >= p.M) continue;
+      float v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = acc[tm][tn][r];
+      epi_pixel<16, EPI>(p, v, m, cbase);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -581,14 +778,15 @@ __global__ __launch_bounds__(256) void conv_dma_kernel(const ConvParams p) {
   conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, chan_base<TM>(wrow0, lq), li);
 }
 
-template <int BCO, int BP, int WCO, bool DMA>
+template <int BCO, int BP, int WCO, int KIND>
 int launch_cfg(const ConvParams* p, int epi, hipStream_t s) {
   // storage rows are permuted inside 64-row groups: cover every group that holds a real channel
   const int rows = (p->cout + 63) / 64 * 64;
   dim3 grid((p->M + BP - 1) / BP, (rows + BCO - 1) / BCO);
   dim3 block(256);
-#define JR_LAUNCH(E)                                                                        \
-  if (DMA) hipLaunchKernelGGL((conv_dma_kernel<BCO, BP, WCO, E>), grid, block, 0, s, *p);   \
+#define JR_LAUNCH(E)                                                                          \
+  if constexpr (KIND == 1) hipLaunchKernelGGL((conv_dma_kernel<BCO, BP, WCO, E>), grid, block, 0, s, *p); \
+  else if constexpr (KIND == 2) hipLaunchKernelGGL((conv_m32_kernel<BCO, BP, WCO, E>), grid, block, 0, s, *p); \
   else hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E>), grid, block, 0, s, *p);
   switch (epi) {
     case EPI_STD: JR_LAUNCH(EPI_STD) break;
@@ -606,18 +804,22 @@ int launch_cfg(const ConvParams* p, int epi, hipStream_t s) {
 extern "C" int jr_conv_forward(const ConvParams* p, int cfg, int epi, hipStream_t stream) {
   if (p->M <= 0) return 0;
   switch (cfg) {
-    case 0: return launch_cfg<128, 128, 2, false>(p, epi, stream);
-    case 1: return launch_cfg<64, 128, 1, false>(p, epi, stream);
-    case 2: return launch_cfg<128, 64, 2, false>(p, epi, stream);
-    case 3: return launch_cfg<16, 256, 1, false>(p, epi, stream);
-    case 4: return launch_cfg<64, 64, 1, false>(p, epi, stream);
-    case 5: return launch_cfg<16, 64, 1, false>(p, epi, stream);
-    case 6: return launch_cfg<128, 128, 2, true>(p, epi, stream);
-    case 7: return launch_cfg<64, 128, 1, true>(p, epi, stream);
-    case 8: return launch_cfg<128, 64, 2, true>(p, epi, stream);
-    case 9: return launch_cfg<16, 256, 1, true>(p, epi, stream);
-    case 10: return launch_cfg<64, 64, 1, true>(p, epi, stream);
-    case 11: return launch_cfg<16, 64, 1, true>(p, epi, stream);
+    case 0: return launch_cfg<128, 128, 2, 0>(p, epi, stream);
+    case 1: return launch_cfg<64, 128, 1, 0>(p, epi, stream);
+    case 2: return launch_cfg<128, 64, 2, 0>(p, epi, stream);
+    case 3: return launch_cfg<16, 256, 1, 0>(p, epi, stream);
+    case 4: return launch_cfg<64, 64, 1, 0>(p, epi, stream);
+    case 5: return launch_cfg<16, 64, 1, 0>(p, epi, stream);
+    case 6: return launch_cfg<128, 128, 2, 1>(p, epi, stream);
+    case 7: return launch_cfg<64, 128, 1, 1>(p, epi, stream);
+    case 8: return launch_cfg<128, 64, 2, 1>(p, epi, stream);
+    case 9: return launch_cfg<16, 256, 1, 1>(p, epi, stream);
+    case 10: return launch_cfg<64, 64, 1, 1>(p, epi, stream);
+    case 11: return launch_cfg<16, 64, 1, 1>(p, epi, stream);
+    case 12: return launch_cfg<128, 128, 2, 2>(p, epi, stream);
+    case 13: return launch_cfg<64, 128, 1, 2>(p, epi, stream);
+    case 14: return launch_cfg<128, 64, 2, 2>(p, epi, stream);
+    case 15: return launch_cfg<64, 64, 2, 2>(p, epi, stream);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -28,6 +28,8 @@ EPI_STD, EPI_GRU_A, EPI_GRU_B, EPI_FLOW = 0, 1, 2, 3
 CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (16, 256), 4: (64, 64), 5: (16, 64)}
 # configs 6..11: the same tiles on the LDS-DMA kernel (csrc/kernels/conv_igemm.hip, kernel D)
 CFG_TILES.update({c + 6: t for c, t in list(CFG_TILES.items())})
+# configs 12..15: 32x32x16-MFMA kernel (kernel M32)
+CFG_TILES.update({12: (128, 128), 13: (64, 128), 14: (128, 64), 15: (64, 64)})
 NUM_CUS = 256
 
 
