@@ -20,6 +20,8 @@
 //  * Fused epilogues: bias, residual, activation (incl. the context-encoder
 //    tanh/relu split), scaling, dual stores into concat buffers, and the
 //    ConvGRU gate/blend and flow-head coordinate update of the RAFT loop.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -208,24 +210,42 @@ JR_DEVICE void epi_pixel(const ConvParams& p, float (&v)[NV], int m, int cbase) 
   }
 }
 
-// Epilogue of the 16x16x32 kernels.  Lane (li, lq) of wave (wco, wp) holds,
-// for each pixel tile tn, NV = 4*TM contiguous output channels starting at
-// cbase (see the weight row permutation in jax_raft_amd/ops/native.py:pack_weight).
-template <int TM, int TN, int EPI>
-JR_DEVICE void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM][TN], int mbase, int cbase, int li) {
-  constexpr int NV = 4 * TM;
-  if (cbase >= p.cout) return;
-#pragma unroll
-  for (int tn = 0; tn < TN; ++tn) {
-    const int m = mbase + tn * 16 + li;
-    if (m >= p.M) continue;
-    float v[NV];
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[tm * 4 + r] = acc[tm][tn][r];
-    epi_pixel<NV, EPI>(p, v, m, cbase);
+// Epilogue of the 16x16x32 kernels.  Lane (li, lq) of a wave whose first
+// storage row is wrow0 holds, for each pixel tile tn and each 64-row group g
+// the wave covers, 4*min(TM,4) contiguous output channels starting at
+// chan_base(wrow0 + 64 g) (see the weight row permutation in
+// jax_raft_amd/ops/native.py:pack_weight).
+template <int I, int N, typename F>
+JR_DEVICE void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
   }
+}
+
+template <int TM, int TN, int EPI>
+JR_DEVICE void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM][TN], int mbase, int wrow0, int lq, int li) {
+  constexpr int TG = TM > 4 ? 4 : TM;   // 16-row tiles per 64-row permutation group
+  static_assert(TM % TG == 0, "TM");
+  constexpr int NV = 4 * TG;
+  // compile-time loops: a large epilogue body defeats `#pragma unroll`, and a
+  // runtime index into acc[][] would move the accumulators to scratch
+  static_for<0, TM / TG>([&](auto gc) {
+    constexpr int g = decltype(gc)::value;
+    const int cbase = chan_base<TG>(wrow0 + 64 * g, lq);
+    if (cbase >= p.cout) return;
+    static_for<0, TN>([&](auto tc) {
+      constexpr int tn = decltype(tc)::value;
+      const int m = mbase + tn * 16 + li;
+      if (m >= p.M) return;
+      float v[NV];
+#pragma unroll
+      for (int tm = 0; tm < TG; ++tm)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[tm * 4 + r] = acc[g * TG + tm][tn][r];
+      epi_pixel<NV, EPI>(p, v, m, cbase);
+    });
+  });
 }
 
 template <int BCO, int BP, int WCO, int EPI>
@@ -393,7 +413,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
   if (nks & 1) compute(0);
 
   const int wrow0 = co0 + wco * WTCO;
-  conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, chan_base<TM>(wrow0, lq), li);
+  conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, wrow0, lq, li);
 }
 
 // ---------------------------------------------------------------------------
@@ -775,7 +795,174 @@ __global__ __launch_bounds__(256) void conv_dma_kernel(const ConvParams p) {
   wait_vmcnt<0>();
 
   const int wrow0 = co0 + wco * WTCO;
-  conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, chan_base<TM>(wrow0, lq), li);
+  conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, wrow0, lq, li);
+}
+
+// ---------------------------------------------------------------------------
+// Kernel D2: LDS-DMA staging at BK = 64 with an NS-deep ring.
+//
+// A stage is (BCO + BP) LDS rows of 128 B (64 bf16 of K): the weight tile then
+// the im2col pixel tile.  It is filled by 1-KiB LDS-DMA pieces
+// (`buffer_load_dwordx4 ... lds`, lane i -> piece base + 16 i) of 8 whole
+// rows, (BCO + BP) / 32 pieces per wave, so every wave issues the same count
+// and the ring waits are exact counted `vmcnt`s with raw barriers: stage
+// ks + NS - 1 is in flight while stage ks feeds the MFMAs.  Row r keeps
+// 16-B chunk c at slot c ^ (r & 6).  That swizzle depends only on the row
+// inside a piece, so each DMA lane fetches one FIXED chunk
+// ((lane & 7) ^ ((lane >> 3) & 6)) for every piece and stage (one im2col K
+// state per lane, as in kernel R), and the ds_read_b128 fragment reads are
+// bank-conflict free under the hardware's lane grouping
+// {0-3,12-15,20-27}, {4-11,16-19,28-31}, ... (rows li and li^4.. of a group
+// land on distinct (row parity, slot) pairs).  No staging VGPRs and no
+// ds_write traffic: the LDS array only serves the fragment reads.
+// ---------------------------------------------------------------------------
+template <int BCO, int BP, int WCO, int NS, int EPI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, (BCO + BP) * NS * 128 > 81920 ? 1 : 2))) void conv_d2_kernel(const ConvParams p) {
+  constexpr int WP = 4 / WCO;
+  constexpr int WTCO = BCO / WCO;
+  constexpr int WTP = BP / WP;
+  constexpr int TM = WTCO / 16;
+  constexpr int TN = WTP / 16;
+  constexpr int ROWS = BCO + BP;
+  constexpr int PPW = ROWS / 32;                   // 8-row pieces per wave per stage
+  constexpr int STAGE = ROWS * BK;                 // bf16 elements
+  constexpr unsigned OOB = 0x80000000u;
+  static_assert(TM >= 1 && TN >= 1 && WCO * WP == 4 && ROWS % 32 == 0, "tile");
+  static_assert(NS >= 2 && NS <= 4, "ring depth");
+  __shared__ __attribute__((aligned(16))) bf16 smem[NS * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wco = wave % WCO;
+  const int wp = wave / WCO;
+  const int p0 = blockIdx.x * BP;
+  const int co0 = blockIdx.y * BCO;
+  const int OHW = p.OH * p.OW;
+  const int cl = (lane & 7) ^ ((lane >> 3) & 6);   // this lane's fixed logical chunk in a stage
+
+  const __amdgpu_buffer_rsrc_t xsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)p.w_bytes, 0x00020000);
+
+  // piece j of this wave covers stage rows q*8 .. q*8+7, q = wave*PPW + j:
+  // rows < BCO are weight rows, the rest pixel rows.  Per-lane row = q*8 + lane/8.
+  int ih0[PPW], iw0[PPW];
+  unsigned rbase[PPW];
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) {
+    const int row = (wave * PPW + j) * 8 + (lane >> 3);
+    if (row < BCO) {
+      // weight row: rbase = byte offset of (row, chunk cl); ih0 flags validity
+      const int wr = co0 + row;
+      rbase[j] = (unsigned)(wr * p.kpad * 2 + cl * 16);
+      ih0[j] = wr < p.cout_pad ? 0 : -1;
+      iw0[j] = 0;
+    } else {
+      const int m = p0 + row - BCO;
+      if (m < p.M) {
+        const int n = m / OHW;
+        const int rem = m - n * OHW;
+        const int oh = rem / p.OW;
+        const int ow = rem - oh * p.OW;
+        ih0[j] = oh * p.SH - p.PH;
+        iw0[j] = ow * p.SW - p.PW;
+        rbase[j] = (unsigned)(((long)n * p.H * p.W * p.x_cstride + p.x_coff) * 2);
+      } else {
+        ih0[j] = -(1 << 28);
+        iw0[j] = -(1 << 28);
+        rbase[j] = 0;
+      }
+    }
+  }
+
+  // im2col K state of the next stage to issue: global chunk kc = ks*8 + cl
+  const int cpt = p.cin8 >> 3;
+  int tap = cl / cpt;
+  int cc = cl - tap * cpt;
+  int kh = tap / p.KW;
+  int kw = tap - kh * p.KW;
+  int ks_next = 0;
+  const unsigned xrow_bytes = (unsigned)p.x_cstride * 2;
+  const int nks = p.kpad / BK;
+
+  auto issue = [&]() {
+    bf16* st = smem + (ks_next % NS) * STAGE;
+    const bool kvalid = kh < p.KH;
+    const bool kin = ks_next < nks;
+    const unsigned kofs = (unsigned)ks_next * (BK * 2);
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int q = wave * PPW + j;               // wave-uniform
+      bf16* dst = st + q * 8 * BK;
+      if (q * 8 < BCO) {
+        dma16(wsrd, dst, (kin && ih0[j] == 0) ? rbase[j] + kofs : OOB);
+      } else {
+        const int ihl = ih0[j] + kh, iwl = iw0[j] + kw;  // coordinates in the (dilated) input
+        const int ih = ihl >> p.dsh, iw = iwl >> p.dsw;
+        const bool ok = kvalid && ((ihl & ((1 << p.dsh) - 1)) | (iwl & ((1 << p.dsw) - 1))) == 0 &&
+                        (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        const unsigned off = rbase[j] + (unsigned)(ih * p.W + iw) * xrow_bytes + (unsigned)cc * 16u;
+        dma16(xsrd, dst, ok ? off : OOB);
+      }
+    }
+    ++ks_next;
+    cc += 8;
+    while (cc >= cpt) {
+      cc -= cpt;
+      if (++kw == p.KW) { kw = 0; ++kh; }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int li = lane & 15;
+  const int lq = lane >> 4;
+  auto compute = [&](int buf) {
+    const bf16* sA = smem + buf * STAGE;
+    const bf16* sB = sA + BCO * BK;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + lq;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int row = wco * WTCO + tm * 16 + li;
+        af[tm] = *(const bf16x8*)(sA + row * BK + ((chunk ^ (row & 6)) << 3));
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int row = wp * WTP + tn * 16 + li;
+        bfr[tn] = *(const bf16x8*)(sB + row * BK + ((chunk ^ (row & 6)) << 3));
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tm], bfr[tn], acc[tm][tn], 0, 0, 0);
+    }
+  };
+
+  // prologue: stages 0 .. NS-2 in flight; wait for stage 0
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) issue();
+  wait_vmcnt<(NS - 2) * PPW>();
+  raw_barrier();
+  for (int ks = 0; ks < nks; ++ks) {
+    issue();                      // stage ks+NS-1 into the buffer stage ks-1 used
+    compute(ks % NS);             // stage ks
+    wait_vmcnt<(NS - 2) * PPW>(); // stage ks+1 has landed (stages ks+2.. may still fly)
+    raw_barrier();
+  }
+  wait_vmcnt<0>();
+
+  const int wrow0 = co0 + wco * WTCO;
+  conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, wrow0, lq, li);
 }
 
 template <int BCO, int BP, int WCO, int KIND>
@@ -786,6 +973,7 @@ int launch_cfg(const ConvParams* p, int epi, hipStream_t s) {
   dim3 block(256);
 #define JR_LAUNCH(E)                                                                          \
   if constexpr (KIND == 1) hipLaunchKernelGGL((conv_dma_kernel<BCO, BP, WCO, E>), grid, block, 0, s, *p); \
+  else if constexpr (KIND >= 3) hipLaunchKernelGGL((conv_d2_kernel<BCO, BP, WCO, KIND - 1, E>), grid, block, 0, s, *p); \
   else if constexpr (KIND == 2) hipLaunchKernelGGL((conv_m32_kernel<BCO, BP, WCO, E>), grid, block, 0, s, *p); \
   else hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E>), grid, block, 0, s, *p);
   switch (epi) {
@@ -810,12 +998,13 @@ extern "C" int jr_conv_forward(const ConvParams* p, int cfg, int epi, hipStream_
     case 3: return launch_cfg<16, 256, 1, 0>(p, epi, stream);
     case 4: return launch_cfg<64, 64, 1, 0>(p, epi, stream);
     case 5: return launch_cfg<16, 64, 1, 0>(p, epi, stream);
-    case 6: return launch_cfg<128, 128, 2, 1>(p, epi, stream);
-    case 7: return launch_cfg<64, 128, 1, 1>(p, epi, stream);
-    case 8: return launch_cfg<128, 64, 2, 1>(p, epi, stream);
-    case 9: return launch_cfg<16, 256, 1, 1>(p, epi, stream);
-    case 10: return launch_cfg<64, 64, 1, 1>(p, epi, stream);
-    case 11: return launch_cfg<16, 64, 1, 1>(p, epi, stream);
+    // kernel D2 (LDS-DMA, BK 64); KIND 3 -> 2-deep ring, 4 -> 3-deep ring
+    case 6: return launch_cfg<128, 128, 2, 3>(p, epi, stream);
+    case 7: return launch_cfg<64, 128, 1, 4>(p, epi, stream);
+    case 8: return launch_cfg<128, 64, 2, 4>(p, epi, stream);
+    case 9: return launch_cfg<128, 256, 2, 3>(p, epi, stream);
+    case 10: return launch_cfg<64, 64, 1, 4>(p, epi, stream);
+    case 11: return launch_cfg<256, 128, 2, 3>(p, epi, stream);
     case 12: return launch_cfg<128, 128, 2, 2>(p, epi, stream);
     case 13: return launch_cfg<64, 128, 1, 2>(p, epi, stream);
     case 14: return launch_cfg<128, 64, 2, 2>(p, epi, stream);

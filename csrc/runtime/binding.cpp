@@ -17,7 +17,9 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <functional>
+#include <string>
 #include <vector>
 
 #include "../kernels/kernels.h"
@@ -98,7 +100,16 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   p.coords = coords.defined() ? coords.data_ptr<float>() : nullptr;
   p.flow32 = flow32.defined() ? flow32.data_ptr<float>() : nullptr;
   p.y3 = ptr(y3); p.y3_cstride = cs(y3); p.y3_coff = (int)i[18];
-  const int epi = (int)i[19], cfg = (int)i[20];
+  const int epi = (int)i[19];
+  int cfg = (int)i[20];
+  // Timing-only ablation (tools/microbench.py --ablate): cfg bits 8/9 give the
+  // X / W buffer descriptors zero records, so every load through them is
+  // dropped by the range check while the instruction stream stays the same.
+  if (cfg >> 8) {
+    if ((cfg >> 8) & 1) p.x_bytes = 0;
+    if ((cfg >> 8) & 2) p.w_bytes = 0;
+    cfg &= 255;
+  }
   // Shape / alignment contract of conv_igemm.hip.
   TORCH_CHECK(p.cin8 % 8 == 0 && p.cin8 > 0, "conv: cin8 must be a positive multiple of 8");
   TORCH_CHECK(p.x_cstride % 8 == 0 && p.x_coff % 8 == 0 && p.x_coff + p.cin8 <= p.x_cstride,
@@ -415,16 +426,45 @@ void lookup_bwd_op(const TList& t, IList i) { run_now(make_lookup_bwd(t, i, null
 void im2col_op(const TList& t, IList i) { run_now(make_im2col(t, i, nullptr)); }
 
 // --------------------------------------------------------------------- Plan
+// A Plan is the lowered RAFT forward: three segments (prologue, loop body run
+// n_iters times with the iteration index, epilogue) of launch closures.  Ops
+// are placed on "lanes": lane 0 is the caller's stream, lanes 1..kMaxLanes-1
+// are private non-blocking streams, and record/wait ops on numbered events
+// express the cross-lane dependencies of the model's DAG (independent
+// branches such as the context encoder vs. the feature encoder + correlation
+// pyramid, or the mask head + upsampling of iteration i vs. iteration i+1).
+// Every side lane is forked from lane 0 at the start of an enqueue and joined
+// back at its end, so run() is ordered like a single-stream launch and
+// capture() records one hipGraph whose parallel branches the runtime may
+// execute concurrently.  A wait on an event not yet recorded during the
+// current enqueue is skipped (e.g. the first iteration's wait on the previous
+// iteration's mask head), which also keeps graph capture self-contained.
 class Plan : public torch::CustomClassHolder {
  public:
+  static constexpr int kMaxLanes = 4;
+  static constexpr int kMaxEvents = 64;
   Plan() = default;
-  ~Plan() override { reset_graph(); if (cap_stream_) (void)hipStreamDestroy(cap_stream_); }
+  ~Plan() override {
+    reset_graph();
+    for (auto e : events_) if (e) (void)hipEventDestroy(e);
+    for (auto e : join_) if (e) (void)hipEventDestroy(e);
+    if (fork_) (void)hipEventDestroy(fork_);
+    for (auto st : lanes_) if (st) (void)hipStreamDestroy(st);
+    if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
+  }
 
   void set_segment(int64_t s) {
     TORCH_CHECK(s >= 0 && s <= 2, "segment must be 0 (prologue), 1 (loop) or 2 (epilogue)");
     seg_ = (int)s;
     reset_graph();
   }
+  void set_lane(int64_t l) {
+    TORCH_CHECK(l >= 0 && l < kMaxLanes, "lane must be in [0, ", kMaxLanes, ")");
+    lane_ = (int)l;
+    used_lanes_ = std::max(used_lanes_, lane_ + 1);
+  }
+  void add_record(int64_t ev) { push_sync(OP_RECORD, ev, "record"); }
+  void add_wait(int64_t ev) { push_sync(OP_WAIT, ev, "wait"); }
   void add_conv(TList t, IList i, double alpha) { push(make_conv(t, i, alpha, &keep_), "conv"); }
   void add_corr(TList t, IList i, double scale) { push(make_corr(t, i, scale, &keep_), "corr"); }
   void add_lookup(TList t, IList i) { push(make_lookup(t, i, &keep_), "lookup"); }
@@ -439,9 +479,14 @@ class Plan : public torch::CustomClassHolder {
   void add_copy_channels(TList t, IList i) { push(make_copy_channels(t, i, &keep_), "copy_channels"); }
 
   int64_t num_ops(int64_t seg) const { return (int64_t)segs_[seg].size(); }
-  std::vector<std::string> op_names(int64_t seg) const { return names_[seg]; }
+  std::vector<std::string> op_names(int64_t seg) const {
+    std::vector<std::string> out;
+    for (const auto& o : segs_[seg]) out.push_back(o.name + (o.lane ? "@" + std::to_string(o.lane) : std::string()));
+    return out;
+  }
+  int64_t num_lanes() const { return used_lanes_; }
 
-  // Launch prologue, n_iters x loop body, epilogue on the current stream.
+  // Launch prologue, n_iters x loop body, epilogue (lane 0 = current stream).
   void run(int64_t n_iters) { JR_CHECK_OK(enqueue(cur_stream(), (int)n_iters)); }
 
   // Capture the same sequence into one hipGraph (on a private stream: the
@@ -456,7 +501,7 @@ class Plan : public torch::CustomClassHolder {
     int err = enqueue(s, (int)n_iters);
     hipGraph_t g = nullptr;
     hipError_t e2 = hipStreamEndCapture(s, &g);
-    TORCH_CHECK(err == 0, "kernel launch failed during capture: ", hipGetErrorString((hipError_t)err));
+    TORCH_CHECK(err == 0, "launch failed during capture: ", hipGetErrorString((hipError_t)err));
     TORCH_CHECK(e2 == hipSuccess && g != nullptr, "end capture failed: ", hipGetErrorString(e2));
     graph_ = g;
     hipError_t e3 = hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0);
@@ -476,22 +521,76 @@ class Plan : public torch::CustomClassHolder {
   }
 
  private:
+  enum OpKind { OP_LAUNCH = 0, OP_RECORD = 1, OP_WAIT = 2 };
+  struct Op {
+    Launch l;
+    int lane;
+    int kind;
+    int ev;
+    std::string name;
+  };
   void push(Launch l, const char* name) {
-    segs_[seg_].push_back(std::move(l));
-    names_[seg_].push_back(name);
+    segs_[seg_].push_back(Op{std::move(l), lane_, OP_LAUNCH, -1, name});
     reset_graph();
   }
-  int enqueue(hipStream_t s, int n_iters) {
-    for (auto& l : segs_[0]) { int e = l(s, 0); if (e) return e; }
-    for (int it = 0; it < n_iters; ++it)
-      for (auto& l : segs_[1]) { int e = l(s, it); if (e) return e; }
-    for (auto& l : segs_[2]) { int e = l(s, n_iters); if (e) return e; }
+  void push_sync(int kind, int64_t ev, const char* name) {
+    TORCH_CHECK(ev >= 0 && ev < kMaxEvents, "event id out of range");
+    segs_[seg_].push_back(Op{Launch(), lane_, kind, (int)ev, std::string(name) + std::to_string(ev)});
+    reset_graph();
+  }
+  static int create_event(hipEvent_t* e) {
+    return (int)hipEventCreateWithFlags(e, hipEventDisableTiming);
+  }
+  int ensure_resources() {
+    if (events_.empty()) {
+      events_.assign(kMaxEvents, nullptr);
+      for (auto& e : events_) if (int r = create_event(&e)) return r;
+    }
+    if (!fork_) if (int r = create_event(&fork_)) return r;
+    for (int l = 1; l < used_lanes_; ++l) {
+      if (!lanes_[l]) if (int r = (int)hipStreamCreateWithFlags(&lanes_[l], hipStreamNonBlocking)) return r;
+      if (!join_[l]) if (int r = create_event(&join_[l])) return r;
+    }
     return 0;
   }
-  std::vector<Launch> segs_[3];
-  std::vector<std::string> names_[3];
+  int exec_op(const Op& o, hipStream_t* st, int it, std::vector<char>& recorded) {
+    hipStream_t s = st[o.lane];
+    switch (o.kind) {
+      case OP_LAUNCH: return o.l(s, it);
+      case OP_RECORD: recorded[o.ev] = 1; return (int)hipEventRecord(events_[o.ev], s);
+      default: return recorded[o.ev] ? (int)hipStreamWaitEvent(s, events_[o.ev], 0) : 0;
+    }
+  }
+  int enqueue(hipStream_t s, int n_iters) {
+    if (int r = ensure_resources()) return r;
+    hipStream_t st[kMaxLanes] = {s, nullptr, nullptr, nullptr};
+    if (used_lanes_ > 1) {
+      if (int r = (int)hipEventRecord(fork_, s)) return r;
+      for (int l = 1; l < used_lanes_; ++l) {
+        st[l] = lanes_[l];
+        if (int r = (int)hipStreamWaitEvent(st[l], fork_, 0)) return r;
+      }
+    }
+    std::vector<char> recorded(kMaxEvents, 0);
+    for (auto& o : segs_[0]) if (int e = exec_op(o, st, 0, recorded)) return e;
+    for (int it = 0; it < n_iters; ++it)
+      for (auto& o : segs_[1]) if (int e = exec_op(o, st, it, recorded)) return e;
+    for (auto& o : segs_[2]) if (int e = exec_op(o, st, n_iters, recorded)) return e;
+    for (int l = 1; l < used_lanes_; ++l) {
+      if (int r = (int)hipEventRecord(join_[l], st[l])) return r;
+      if (int r = (int)hipStreamWaitEvent(s, join_[l], 0)) return r;
+    }
+    return 0;
+  }
+  std::vector<Op> segs_[3];
   std::vector<at::Tensor> keep_;
   int seg_ = 0;
+  int lane_ = 0;
+  int used_lanes_ = 1;
+  std::vector<hipEvent_t> events_;
+  hipEvent_t fork_ = nullptr;
+  hipEvent_t join_[kMaxLanes] = {nullptr, nullptr, nullptr, nullptr};
+  hipStream_t lanes_[kMaxLanes] = {nullptr, nullptr, nullptr, nullptr};
   hipStream_t cap_stream_ = nullptr;
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t exec_ = nullptr;
@@ -516,6 +615,10 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.class_<jr::Plan>("Plan")
       .def(torch::init<>())
       .def("set_segment", &jr::Plan::set_segment)
+      .def("set_lane", &jr::Plan::set_lane)
+      .def("add_record", &jr::Plan::add_record)
+      .def("add_wait", &jr::Plan::add_wait)
+      .def("num_lanes", &jr::Plan::num_lanes)
       .def("add_conv", &jr::Plan::add_conv)
       .def("add_corr", &jr::Plan::add_corr)
       .def("add_lookup", &jr::Plan::add_lookup)

@@ -26,8 +26,8 @@ ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, ACT_SPLIT_TANH_RELU = 0, 1, 2, 3, 4
 EPI_STD, EPI_GRU_A, EPI_GRU_B, EPI_FLOW = 0, 1, 2, 3
 # tile configs of conv_igemm.hip: (BCO, BP)
 CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (16, 256), 4: (64, 64), 5: (16, 64)}
-# configs 6..11: the same tiles on the LDS-DMA kernel (csrc/kernels/conv_igemm.hip, kernel D)
-CFG_TILES.update({c + 6: t for c, t in list(CFG_TILES.items())})
+# configs 6..11: LDS-DMA kernel D2 (csrc/kernels/conv_igemm.hip)
+CFG_TILES.update({6: (128, 128), 7: (64, 128), 8: (128, 64), 9: (128, 256), 10: (64, 64), 11: (256, 128)})
 # configs 12..15: 32x32x16-MFMA kernel (kernel M32)
 CFG_TILES.update({12: (128, 128), 13: (64, 128), 14: (128, 64), 15: (64, 64)})
 NUM_CUS = 256
@@ -154,10 +154,10 @@ def pick_cfg(M: int, cout: int) -> int:
     tile's per-FLOP cost rises as it shrinks; keeps >= one wave of blocks over
     256 CUs whenever the problem allows."""
     if cout <= 16:
-        return 11
-    best, best_cost = 6, None
+        return 5
+    best, best_cost = 0, None
     # (cfg, relative per-FLOP efficiency of the tile); time ~ blocks per CU x tile area / eff
-    for cfg, eff in ((6, 1.0), (8, 0.85), (7, 0.85), (10, 0.65)):
+    for cfg, eff in ((0, 1.0), (2, 0.85), (1, 0.85), (4, 0.65)):
         bco, bp = CFG_TILES[cfg]
         nb = math.ceil(M / bp) * math.ceil(cout / bco)
         cost = math.ceil(nb / NUM_CUS) * (bco * bp) / eff

@@ -118,11 +118,17 @@ class RaftEngine:
             fp32 for bit-closer parity with the fp32 reference).
         autotune: time every conv tile config on the real buffers when a plan
             is built and keep the fastest (cached per problem signature).
+        streams: place the model's independent branches on side lanes of the
+            plan (context encoder || feature encoder + correlation pyramid;
+            flow-feature convs || lookup + correlation convs; mask head +
+            upsampling of iteration i || iteration i+1) so they overlap on
+            the GPU (parallel branches of the captured hipGraph).
     """
 
     def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True,
-                 corr_dtype: torch.dtype = torch.bfloat16, autotune: bool = True):
+                 corr_dtype: torch.dtype = torch.bfloat16, autotune: bool = True, streams: bool = True):
         nat.require()
+        self.streams = streams
         self.model = model
         self.device = torch.device(device)
         self.use_graph = use_graph
@@ -364,9 +370,38 @@ class RaftEngine:
         st.out = alloc("out", (n_iters, B, H, W, 2), F32)
 
         # ---------------- prologue: encoders + correlation pyramid
+        # lanes: 0 = feature encoder + correlation pyramid, 1 = context encoder
+        E_PREP, E_CTX, E_IT, E_FLOW, E_FH, E_MASK = range(6)
+        side = 1 if self.streams else 0
+        side2 = 2 if self.streams else 0
+
+        def lane(l):
+            plan.set_lane(l)
+
         plan.set_segment(0)
+        hx = alloc("hx", (M, self.hx_cs))
+        qx = alloc("qx", (M, self.hx_cs))
+        h32 = alloc("h32", (M, self.hidden), F32)
+        zb = alloc("z", (M, self.hidden), F32)
+        flow8 = alloc("flow8", (M, 8))
+        coords = alloc("coords", (M, 2), F32)
+        flow32 = alloc("flow32", (M, 2), F32)
+        for t in (hx, qx, flow8, flow32):
+            plan.add_memset([t])
         x0 = alloc("x0", (2 * B, H, W, 8))
         plan.add_prep([st.inp1, st.inp2, x0], [B, H, W])
+        plan.add_record(E_PREP)
+
+        lane(side)
+        plan.add_wait(E_PREP)
+        ctxf, ch_, cw_ = self._encoder(st, plan, "ce", m.context_encoder, x0[:B], B, H, W)
+        assert (ch_, cw_) == (h, w), "The context encoder should downsample H and W by 8"
+        self._conv(plan, sp["ce.conv"], ctxf, B, h, w, hx, act=ACT_SPLIT_TANH_RELU, split=self.hidden,
+                   y2=qx, h32=h32, hidden=self.hidden)
+        plan.add_init_coords([coords], [B, h, w])
+        plan.add_record(E_CTX)
+
+        lane(0)
         feat, fh_, fw_ = self._encoder(st, plan, "fe", m.feature_encoder, x0, 2 * B, H, W)
         assert (fh_, fw_) == (h, w), "The feature encoder should downsample H and W by 8"
         fmap = alloc("fmap", (2 * B, h, w, self.fmap_ch))
@@ -379,60 +414,59 @@ class RaftEngine:
             wl //= 2
         plan.add_corr([fmap[:B], fmap[B:]] + levels + [None] * (4 - L), [B, h, w, self.fmap_ch, L],
                       1.0 / float(self.fmap_ch) ** 0.5)
-
-        hx = alloc("hx", (M, self.hx_cs))
-        qx = alloc("qx", (M, self.hx_cs))
-        h32 = alloc("h32", (M, self.hidden), F32)
-        zb = alloc("z", (M, self.hidden), F32)
-        flow8 = alloc("flow8", (M, 8))
-        coords = alloc("coords", (M, 2), F32)
-        flow32 = alloc("flow32", (M, 2), F32)
-        for t in (hx, qx, flow8, flow32):
-            plan.add_memset([t])
-        ctxf, ch_, cw_ = self._encoder(st, plan, "ce", m.context_encoder, x0[:B], B, H, W)
-        assert (ch_, cw_) == (h, w), "The context encoder should downsample H and W by 8"
-        self._conv(plan, sp["ce.conv"], ctxf, B, h, w, hx, act=ACT_SPLIT_TANH_RELU, split=self.hidden,
-                                 y2=qx, h32=h32, hidden=self.hidden)
-        plan.add_init_coords([coords], [B, h, w])
+        plan.add_wait(E_CTX)
 
         # ---------------- loop body: one refinement iteration (model.py:495-510)
+        # lanes: 0 = lookup -> corr convs -> motion conv -> GRU -> flow head,
+        # 1 = flow-feature convs, 2 = mask head + upsampling (off the critical path)
         plan.set_segment(1)
         corr = alloc("corr", (M, self.corr_cs))
-        plan.add_lookup([coords, corr] + levels + [None] * (4 - L), [L, B, h, w, self.radius])
         me = m.update_block.motion_encoder
         cl, fl = me.corr_layers, me.flow_layers
         cf = alloc("cf", (M, cl[-1] + fl[-1]))
+        f1 = alloc("f1", (M, fl[0]))
+        plan.add_record(E_IT)
+        lane(side)
+        plan.add_wait(E_IT)
+        self._conv(plan, sp["me.convflow1"], flow8, B, h, w, f1, act=ACT_RELU)
+        self._conv(plan, sp["me.convflow2"], f1, B, h, w, cf, y_coff=cl[-1], act=ACT_RELU)
+        plan.add_record(E_FLOW)
+        lane(0)
+        plan.add_lookup([coords, corr] + levels + [None] * (4 - L), [L, B, h, w, self.radius])
         if len(cl) == 2:
             c1 = alloc("c1", (M, cl[0]))
             self._conv(plan, sp["me.convcorr1"], corr, B, h, w, c1, act=ACT_RELU)
+            self._conv(plan, sp["me.convcorr2"], c1, B, h, w, cf, act=ACT_RELU)
         else:
             self._conv(plan, sp["me.convcorr1"], corr, B, h, w, cf, act=ACT_RELU)
-        f1 = alloc("f1", (M, fl[0]))
-        self._conv(plan, sp["me.convflow1"], flow8, B, h, w, f1, act=ACT_RELU)
-        if len(cl) == 2:
-            self._conv(plan, sp["me.convcorr2"], c1, B, h, w, cf, act=ACT_RELU)
-        self._conv(plan, sp["me.convflow2"], f1, B, h, w, cf, y_coff=cl[-1], act=ACT_RELU)
+        plan.add_wait(E_FLOW)
         self._conv(plan, sp["me.conv"], cf, B, h, w, hx, y_coff=self.mot_off, act=ACT_RELU, y2=qx,
-                                 y2_coff=self.mot_off)
+                   y2_coff=self.mot_off)
         for gi in range(len(m.update_block.recurrent_block.kernel_size)):
             self._conv(plan, sp[f"gru{gi}.a"], hx, B, h, w, qx, h32=h32, zbuf=zb, hidden=self.hidden,
-                                     epi=EPI_GRU_A)
+                       epi=EPI_GRU_A)
             self._conv(plan, sp[f"gru{gi}.b"], qx, B, h, w, hx, h32=h32, zbuf=zb, hidden=self.hidden,
-                                     epi=EPI_GRU_B)
+                       epi=EPI_GRU_B)
         s1 = sp["fh1"]
         fm = alloc("fm", (M, round_up(s1.cout, 8)))
+        plan.add_wait(E_MASK)  # previous iteration's mask head has consumed fm / flow32
         self._conv(plan, s1, hx, B, h, w, fm, act=ACT_RELU)
         # flow head conv2 + coordinate update (model.py:505) + flow into hx/qx/flow8
         self._conv(plan, sp["fh2"], fm, B, h, w, hx, y_coff=self.flow_off, y2=qx, y2_coff=self.flow_off,
-                                 y3=flow8, y3_coff=0, coords=coords, flow32=flow32, epi=EPI_FLOW)
+                   y3=flow8, y3_coff=0, coords=coords, flow32=flow32, epi=EPI_FLOW)
+        plan.add_record(E_FH)
+        lane(side2)
+        plan.add_wait(E_FH)
         stride = B * H * W * 2
         if self.has_mask:
             mask = alloc("mask", (M, 576))
             self._conv(plan, sp["mask"], fm, B, h, w, mask, x_coff=self.fh_hidden,
-                                     alpha=m.mask_predictor.multiplier)
+                       alpha=m.mask_predictor.multiplier)
             plan.add_upsample_convex([mask, flow32, st.out], [B, h, w, stride])
         else:
             plan.add_upsample_bilinear([flow32, st.out], [B, h, w, stride])
+        plan.add_record(E_MASK)
+        lane(0)
         plan.set_segment(2)
         return st
 

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--w", type=int, default=128)
     ap.add_argument("--only", default="")
     ap.add_argument("--json", default="")
+    ap.add_argument("--gemm", action="store_true", help="also time the equivalent plain GEMM on hipBLASLt")
+    ap.add_argument("--ablate", default="", help="comma list of cfgs: also time them with X / W / both loads dropped")
     args = ap.parse_args()
     nat.require()
     dev = "cuda"
@@ -79,6 +81,20 @@ def main():
             us = timeit(lambda: nat.ops().conv(t, i, a))
             row[cfg] = us
         best = min(row, key=row.get)
+        for cfg in [int(c) for c in args.ablate.split(",") if c]:
+            parts = []
+            for ab, nm in ((1, "noX"), (2, "noW"), (3, "noXW")):
+                t, i, a = nat.conv_args(spec, x, B, h, w, y, act=nat.ACT_RELU, cfg=cfg)
+                i = list(i)
+                i[20] = cfg | (ab << 8)
+                parts.append(f"{nm}={timeit(lambda: nat.ops().conv(t, i, a)):6.1f}")
+            print(f"{'':12s} ablate c{cfg}: full={row[cfg]:6.1f} " + " ".join(parts), flush=True)
+        if args.gemm:  # same M x K x N as a library GEMM (no im2col, no epilogue): a yardstick
+            K = kh * kw * cin
+            a_ = rnd(M, K)
+            b_ = rnd(K, cout)
+            g_us = timeit(lambda: torch.matmul(a_, b_))
+            print(f"{'':12s} hipBLASLt {M}x{K}x{cout}: {g_us:7.1f} us {flops / g_us / 1e6:7.1f} TF/s")
         res[name] = {"us": row, "best_cfg": best, "tflops": flops / row[best] / 1e6, "heuristic": nat.pick_cfg(M, cout)}
         print(f"{name:12s} " + " ".join(f"c{c}={u:7.1f}" for c, u in row.items()) +
               f"  best=c{best} {flops / row[best] / 1e6:7.1f} TF/s  heur=c{nat.pick_cfg(M, cout)}", flush=True)
