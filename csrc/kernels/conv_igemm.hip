@@ -248,7 +248,42 @@ JR_DEVICE void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM][TN], int mbas
   });
 }
 
-template <int BCO, int BP, int WCO, int EPI>
+// Per-row state of the FAST im2col loader (ConvParams::fast): the byte offset
+// of the row's first tap + this lane's 16-B chunk, and a bitmask of the taps
+// (kh * KW + kw) that fall inside the input.  A stage's tap and channel block
+// are wave-uniform, so a stage costs per row one bit test, one add and one
+// select.
+struct FastRow {
+  unsigned off;
+  unsigned mask;
+};
+
+JR_DEVICE FastRow fast_row(const ConvParams& p, int ih0, int iw0, unsigned rbase, bool valid, int ch,
+                           unsigned xrow_bytes) {
+  FastRow r{0u, 0u};
+  if (!valid) return r;
+  r.off = rbase + (unsigned)(ih0 * p.W + iw0) * xrow_bytes + (unsigned)ch * 16u;  // may wrap; only used when a tap is valid
+  for (int kh = 0; kh < p.KH; ++kh) {
+    if ((unsigned)(ih0 + kh) >= (unsigned)p.H) continue;
+    for (int kw = 0; kw < p.KW; ++kw)
+      if ((unsigned)(iw0 + kw) < (unsigned)p.W) r.mask |= 1u << (kh * p.KW + kw);
+  }
+  return r;
+}
+
+// Wave-uniform stage state of the FAST loader.
+struct FastStage {
+  int tap = 0, kh = 0, kw = 0, cb = 0;
+  JR_DEVICE void advance(const ConvParams& p, int cpb) {
+    if (++cb == cpb) {
+      cb = 0;
+      ++tap;
+      if (++kw == p.KW) { kw = 0; ++kh; }
+    }
+  }
+};
+
+template <int BCO, int BP, int WCO, int EPI, bool FAST>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
   constexpr int WP = 4 / WCO;
   constexpr int WTCO = BCO / WCO;
@@ -312,11 +347,29 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
   int kw = tap - kh * p.KW;
   int ks_next = 0;
   const unsigned xrow_bytes = (unsigned)p.x_cstride * 2;
+  [[maybe_unused]] FastRow frow[XR];
+  [[maybe_unused]] FastStage fst;
+  [[maybe_unused]] const int cpb = (p.KH * p.KW == 1) ? (p.kpad / BK) : (p.cin8 >> 6);
+  if constexpr (FAST) {
+#pragma unroll
+    for (int i = 0; i < XR; ++i) frow[i] = fast_row(p, ih0[i], iw0[i], rbase[i], ih0[i] > -(1 << 27), ch, xrow_bytes);
+  }
 
   struct Regs { u32x4 x[XR]; u32x4 w[WR]; };
   Regs ra, rb;
 
   auto issue = [&](Regs& r) {
+    if constexpr (FAST) {
+      const bool kin = ks_next * BK < p.kpad;
+      const bool cv = kin && ch * 8 < p.cin8 - fst.cb * 64;   // channel tail of a 1x1 conv
+      const unsigned soff = (unsigned)(fst.kh * p.W + fst.kw) * xrow_bytes + (unsigned)fst.cb * 128u;
+#pragma unroll
+      for (int i = 0; i < XR; ++i) {
+        const bool ok = cv && ((frow[i].mask >> (fst.tap & 31)) & 1u);
+        r.x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xsrd, ok ? frow[i].off + soff : OOB, 0, 0));
+      }
+      fst.advance(p, cpb);
+    } else {
     const bool kvalid = kh < p.KH;
 #pragma unroll
     for (int i = 0; i < XR; ++i) {
@@ -327,6 +380,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
       const unsigned off = rbase[i] + (unsigned)(ih * p.W + iw) * xrow_bytes + (unsigned)cc * 16u;
       r.x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xsrd, ok ? off : OOB, 0, 0));
     }
+    }
     const unsigned kofs = (unsigned)ks_next * (BK * 2);
 #pragma unroll
     for (int i = 0; i < WR; ++i) {
@@ -336,10 +390,12 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
     }
     // advance the chunk state to the following stage
     ++ks_next;
-    cc += 8;
-    while (cc >= cpt) {
-      cc -= cpt;
-      if (++kw == p.KW) { kw = 0; ++kh; }
+    if constexpr (!FAST) {
+      cc += 8;
+      while (cc >= cpt) {
+        cc -= cpt;
+        if (++kw == p.KW) { kw = 0; ++kh; }
+      }
     }
   };
   auto store = [&](const Regs& r, int buf) {
@@ -431,7 +487,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // storage row (within a 64-row group) holding channel 32t + c(rho), c(rho) = 16((rho>>2)&1) + (rho&3) + 4(rho>>3)
 JR_DEVICE int m32_arow(int t, int rho) { return 16 * (rho >> 3) + 4 * (2 * t + ((rho >> 2) & 1)) + (rho & 3); }
 
-template <int BCO, int BP, int WCO, int EPI>
+template <int BCO, int BP, int WCO, int EPI, bool FAST>
 __global__ __launch_bounds__(256) void conv_m32_kernel(const ConvParams p) {
   constexpr int WP = 4 / WCO;
   constexpr int WTCO = BCO / WCO;
@@ -489,10 +545,29 @@ __global__ __launch_bounds__(256) void conv_m32_kernel(const ConvParams p) {
   int kw = tap - kh * p.KW;
   int ks_next = 0;
   const unsigned xrow_bytes = (unsigned)p.x_cstride * 2;
+  [[maybe_unused]] FastRow frow[XR];
+  [[maybe_unused]] FastStage fst;
+  [[maybe_unused]] const int cpb = (p.KH * p.KW == 1) ? (p.kpad / BK) : (p.cin8 >> 6);
+  if constexpr (FAST) {
+#pragma unroll
+    for (int i = 0; i < XR; ++i) frow[i] = fast_row(p, ih0[i], iw0[i], rbase[i], ih0[i] > -(1 << 27), ch, xrow_bytes);
+  }
 
   struct Regs { u32x4 x[XR]; u32x4 w[WR]; };
   Regs ra, rb;
+
   auto issue = [&](Regs& r) {
+    if constexpr (FAST) {
+      const bool kin = ks_next * BK < p.kpad;
+      const bool cv = kin && ch * 8 < p.cin8 - fst.cb * 64;   // channel tail of a 1x1 conv
+      const unsigned soff = (unsigned)(fst.kh * p.W + fst.kw) * xrow_bytes + (unsigned)fst.cb * 128u;
+#pragma unroll
+      for (int i = 0; i < XR; ++i) {
+        const bool ok = cv && ((frow[i].mask >> (fst.tap & 31)) & 1u);
+        r.x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xsrd, ok ? frow[i].off + soff : OOB, 0, 0));
+      }
+      fst.advance(p, cpb);
+    } else {
     const bool kvalid = kh < p.KH;
 #pragma unroll
     for (int i = 0; i < XR; ++i) {
@@ -503,6 +578,7 @@ __global__ __launch_bounds__(256) void conv_m32_kernel(const ConvParams p) {
       const unsigned off = rbase[i] + (unsigned)(ih * p.W + iw) * xrow_bytes + (unsigned)cc * 16u;
       r.x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xsrd, ok ? off : OOB, 0, 0));
     }
+    }
     const unsigned kofs = (unsigned)ks_next * (BK * 2);
 #pragma unroll
     for (int i = 0; i < WR; ++i) {
@@ -511,10 +587,12 @@ __global__ __launch_bounds__(256) void conv_m32_kernel(const ConvParams p) {
       r.w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wsrd, ok ? off : OOB, 0, 0));
     }
     ++ks_next;
-    cc += 8;
-    while (cc >= cpt) {
-      cc -= cpt;
-      if (++kw == p.KW) { kw = 0; ++kh; }
+    if constexpr (!FAST) {
+      cc += 8;
+      while (cc >= cpt) {
+        cc -= cpt;
+        if (++kw == p.KW) { kw = 0; ++kh; }
+      }
     }
   };
   auto store = [&](const Regs& r, int buf) {
@@ -606,23 +684,7 @@ __global__ __launch_bounds__(256) void conv_m32_kernel(const ConvParams p) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// Kernel D: direct-to-LDS DMA operand staging.
-//
-// Both operand tiles are fetched with `buffer_load_dwordx4 ... lds` (LDS-DMA):
-// no staging VGPRs and no ds_write traffic, and the buffer range check turns
-// padding taps / tail rows into zero fills.  K advances in 32-deep stages
-// through a 4-deep LDS ring with loads issued 3 stages ahead; waits are counted
-// (`s_waitcnt vmcnt(N)`) and barriers raw, so DMA for later stages stays in
-// flight across them (cdna_hip_programming.md §5 "Pipelining across barriers").
-// LDS rows are 64 B (4 x 16-B chunks); chunk c of row r lives at slot
-// c ^ ((r >> 2) & 3): the 16 consecutive rows of a fragment read hit 16
-// distinct 16-B bank slots, and each DMA lane has a FIXED logical chunk
-// ((l & 3) ^ ((l >> 4) & 3)) because a 1-KiB DMA piece covers 16 whole rows.
-// ---------------------------------------------------------------------------
-constexpr int DBK = 32;
-constexpr int DNB = 4;
-
+// LDS-DMA helpers (kernel D2)
 // One 16-B-per-lane LDS-DMA (buffer_load_dwordx4 ... lds): lane i lands at lds + 16*i.
 JR_DEVICE void dma16(__amdgpu_buffer_rsrc_t r, bf16* lds, unsigned voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
@@ -638,164 +700,6 @@ JR_DEVICE void raw_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-}
-
-template <int BCO, int BP, int WCO, int EPI>
-__global__ __launch_bounds__(256) void conv_dma_kernel(const ConvParams p) {
-  constexpr int WP = 4 / WCO;
-  constexpr int WTCO = BCO / WCO;
-  constexpr int WTP = BP / WP;
-  constexpr int TM = WTCO / 16;
-  constexpr int TN = WTP / 16;
-  constexpr int XPIECES = BP / 16;                 // 1-KiB DMA pieces per stage, X tile
-  constexpr int WPIECES = BCO / 16;                // ... W tile
-  constexpr int XPW = (XPIECES + 3) / 4;           // pieces per wave
-  constexpr int WPW = (WPIECES + 3) / 4;
-  constexpr int DPW = XPW + WPW;                   // DMA instructions per wave per stage (upper bound)
-  constexpr int A_ELEMS = BCO * DBK;
-  constexpr int B_ELEMS = BP * DBK;
-  constexpr int STAGE = A_ELEMS + B_ELEMS;
-  constexpr unsigned OOB = 0x80000000u;
-  static_assert(TM >= 1 && TN >= 1 && WCO * WP == 4, "tile");
-  __shared__ __attribute__((aligned(16))) bf16 smem[DNB * STAGE];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wco = wave % WCO;
-  const int wp = wave / WCO;
-  const int p0 = blockIdx.x * BP;
-  const int co0 = blockIdx.y * BCO;
-  const int OHW = p.OH * p.OW;
-  const int cl = (lane & 3) ^ ((lane >> 4) & 3);   // this lane's logical 16-B chunk within a stage
-
-  const __amdgpu_buffer_rsrc_t xsrd =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wsrd =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)p.w_bytes, 0x00020000);
-
-  // X rows handled by this lane: piece = wave*XPW + j, row = piece*16 + (lane >> 2)
-  int ih0[XPW], iw0[XPW];
-  unsigned rbase[XPW];
-#pragma unroll
-  for (int j = 0; j < XPW; ++j) {
-    const int piece = wave * XPW + j;
-    const int m = p0 + piece * 16 + (lane >> 2);
-    if (piece < XPIECES && m < p.M) {
-      const int n = m / OHW;
-      const int rem = m - n * OHW;
-      const int oh = rem / p.OW;
-      const int ow = rem - oh * p.OW;
-      ih0[j] = oh * p.SH - p.PH;
-      iw0[j] = ow * p.SW - p.PW;
-      rbase[j] = (unsigned)(((long)n * p.H * p.W * p.x_cstride + p.x_coff) * 2);
-    } else {
-      ih0[j] = -(1 << 28);
-      iw0[j] = -(1 << 28);
-      rbase[j] = 0;
-    }
-  }
-  unsigned wbase[WPW];
-  bool wok[WPW];
-#pragma unroll
-  for (int j = 0; j < WPW; ++j) {
-    const int piece = wave * WPW + j;
-    const int row = co0 + piece * 16 + (lane >> 2);
-    wok[j] = piece < WPIECES && row < p.cout_pad;
-    wbase[j] = (unsigned)(row * p.kpad * 2 + cl * 16);
-  }
-
-  // chunk state of the next stage to issue: kc = ks*4 + cl
-  const int cpt = p.cin8 >> 3;
-  int tap = cl / cpt;
-  int cc = cl - tap * cpt;
-  int kh = tap / p.KW;
-  int kw = tap - kh * p.KW;
-  int ks_next = 0;
-  const unsigned xrow_bytes = (unsigned)p.x_cstride * 2;
-  const int nks = p.kpad / DBK;
-
-  auto issue = [&]() {
-    const int buf = ks_next & (DNB - 1);
-    bf16* sA = smem + buf * STAGE;
-    bf16* sB = sA + A_ELEMS;
-    const bool kvalid = kh < p.KH;
-#pragma unroll
-    for (int j = 0; j < XPW; ++j) {
-      const int piece = wave * XPW + j;
-      if (piece < XPIECES) {
-        const int ihl = ih0[j] + kh, iwl = iw0[j] + kw;  // coordinates in the (dilated) input
-        const int ih = ihl >> p.dsh, iw = iwl >> p.dsw;
-        const bool ok = kvalid && ((ihl & ((1 << p.dsh) - 1)) | (iwl & ((1 << p.dsw) - 1))) == 0 &&
-                        (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-        const unsigned off = rbase[j] + (unsigned)(ih * p.W + iw) * xrow_bytes + (unsigned)cc * 16u;
-        dma16(xsrd, sB + piece * 16 * DBK, ok ? off : OOB);
-      }
-    }
-    const unsigned kofs = (unsigned)ks_next * (DBK * 2);
-    const bool kin = ks_next < nks;
-#pragma unroll
-    for (int j = 0; j < WPW; ++j) {
-      const int piece = wave * WPW + j;
-      if (piece < WPIECES) {
-        const bool ok = wok[j] && kin;
-        dma16(wsrd, sA + piece * 16 * DBK, ok ? wbase[j] + kofs : OOB);
-      }
-    }
-    ++ks_next;
-    cc += 4;
-    while (cc >= cpt) {
-      cc -= cpt;
-      if (++kw == p.KW) { kw = 0; ++kh; }
-    }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int li = lane & 15;
-  const int lq = lane >> 4;
-  auto compute = [&](int buf) {
-    const bf16* sA = smem + buf * STAGE;
-    const bf16* sB = sA + A_ELEMS;
-    bf16x8 af[TM], bfr[TN];
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm) {
-      const int row = wco * WTCO + tm * 16 + li;
-      af[tm] = *(const bf16x8*)(sA + row * DBK + ((lq ^ ((row >> 2) & 3)) << 3));
-    }
-#pragma unroll
-    for (int tn = 0; tn < TN; ++tn) {
-      const int row = wp * WTP + tn * 16 + li;
-      bfr[tn] = *(const bf16x8*)(sB + row * DBK + ((lq ^ ((row >> 2) & 3)) << 3));
-    }
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn)
-        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tm], bfr[tn], acc[tm][tn], 0, 0, 0);
-  };
-
-  // Every wave issues exactly DPW DMA ops per stage (waves without a piece
-  // issue nothing, so their counted waits are conservative and still correct).
-  issue();
-  issue();
-  issue();
-  wait_vmcnt<2 * DPW>();
-  raw_barrier();
-  for (int ks = 0; ks < nks; ++ks) {
-    issue();                       // stage ks+3 into the buffer freed by stage ks-1
-    compute(ks & (DNB - 1));       // stage ks
-    wait_vmcnt<2 * DPW>();         // stage ks+1 has landed (ks+2, ks+3 may still fly)
-    raw_barrier();
-  }
-  wait_vmcnt<0>();
-
-  const int wrow0 = co0 + wco * WTCO;
-  conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, wrow0, lq, li);
 }
 
 // ---------------------------------------------------------------------------
@@ -972,10 +876,14 @@ int launch_cfg(const ConvParams* p, int epi, hipStream_t s) {
   dim3 grid((p->M + BP - 1) / BP, (rows + BCO - 1) / BCO);
   dim3 block(256);
 #define JR_LAUNCH(E)                                                                          \
-  if constexpr (KIND == 1) hipLaunchKernelGGL((conv_dma_kernel<BCO, BP, WCO, E>), grid, block, 0, s, *p); \
-  else if constexpr (KIND >= 3) hipLaunchKernelGGL((conv_d2_kernel<BCO, BP, WCO, KIND - 1, E>), grid, block, 0, s, *p); \
-  else if constexpr (KIND == 2) hipLaunchKernelGGL((conv_m32_kernel<BCO, BP, WCO, E>), grid, block, 0, s, *p); \
-  else hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E>), grid, block, 0, s, *p);
+  if constexpr (KIND >= 3) hipLaunchKernelGGL((conv_d2_kernel<BCO, BP, WCO, KIND - 1, E>), grid, block, 0, s, *p); \
+  else if constexpr (KIND == 2) {                                                              \
+    if (p->fast) hipLaunchKernelGGL((conv_m32_kernel<BCO, BP, WCO, E, true>), grid, block, 0, s, *p); \
+    else hipLaunchKernelGGL((conv_m32_kernel<BCO, BP, WCO, E, false>), grid, block, 0, s, *p);         \
+  } else {                                                                                     \
+    if (p->fast) hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, true>), grid, block, 0, s, *p); \
+    else hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, false>), grid, block, 0, s, *p);         \
+  }
   switch (epi) {
     case EPI_STD: JR_LAUNCH(EPI_STD) break;
     case EPI_GRU_A: JR_LAUNCH(EPI_GRU_A) break;
@@ -1009,6 +917,9 @@ extern "C" int jr_conv_forward(const ConvParams* p, int cfg, int epi, hipStream_
     case 13: return launch_cfg<64, 128, 1, 2>(p, epi, stream);
     case 14: return launch_cfg<128, 64, 2, 2>(p, epi, stream);
     case 15: return launch_cfg<64, 64, 2, 2>(p, epi, stream);
+    // hipBLASLt-like shapes: 256-wide block, 128x64 / 64x128 wave tiles, one block per CU
+    case 16: return launch_cfg<256, 128, 2, 0>(p, epi, stream);
+    case 17: return launch_cfg<128, 256, 2, 0>(p, epi, stream);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -56,10 +56,17 @@ struct ConvParams {
   float* coords;    // FLOW: fp32 [M][2]
   float* flow32;    // FLOW: fp32 [M][2]
   void* y3; int y3_cstride, y3_coff;  // FLOW: third bf16 flow copy
+  // 1 when every 64-deep K stage lies inside one tap (a 1x1 conv, or cin8 % 64 == 0 with at most
+  // 32 taps) and there is no input dilation: the register-staged kernels then use wave-uniform
+  // tap state and per-row tap bitmasks instead of per-lane im2col arithmetic
+  int fast;
 };
 
-// cfg: 0 = 128co x 128px, 1 = 64co x 128px, 2 = 128co x 64px, 3 = 16co x 256px, 4 = 64co x 64px,
-//      5 = 16co x 64px (narrow outputs, e.g. the 2-channel flow head)
+// cfg (co x px block tile): kernel R (register-staged, 16x16x32 MFMA) 0 = 128x128, 1 = 64x128,
+// 2 = 128x64, 3 = 16x256, 4 = 64x64, 5 = 16x64 (narrow outputs, e.g. the 2-channel flow head),
+// 16 = 256x128, 17 = 128x256; kernel D2 (LDS-DMA) 6 = 128x128, 7 = 64x128, 8 = 128x64,
+// 9 = 128x256, 10 = 64x64, 11 = 256x128; kernel M32 (32x32x16 MFMA) 12 = 128x128,
+// 13 = 64x128, 14 = 128x64, 15 = 64x64.  The engine autotunes the choice per conv.
 int jr_conv_forward(const ConvParams* p, int cfg, int epi, hipStream_t stream);
 
 // ---------------------------------------------------------------------------

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <functional>
 #include <string>
 #include <vector>
@@ -100,6 +101,10 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   p.coords = coords.defined() ? coords.data_ptr<float>() : nullptr;
   p.flow32 = flow32.defined() ? flow32.data_ptr<float>() : nullptr;
   p.y3 = ptr(y3); p.y3_cstride = cs(y3); p.y3_coff = (int)i[18];
+  {
+    const int taps = p.KH * p.KW;
+    p.fast = p.dsh == 0 && p.dsw == 0 && taps <= 32 && (taps == 1 || p.cin8 % 64 == 0) && !std::getenv("JR_CONV_NO_FAST");
+  }
   const int epi = (int)i[19];
   int cfg = (int)i[20];
   // Timing-only ablation (tools/microbench.py --ablate): cfg bits 8/9 give the
@@ -141,7 +146,7 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   } else {
     TORCH_CHECK(false, "conv: unknown epilogue ", epi);
   }
-  TORCH_CHECK(cfg >= 0 && cfg <= 15, "conv: unknown tile config ", cfg);
+  TORCH_CHECK(cfg >= 0 && cfg <= 17, "conv: unknown tile config ", cfg);
   if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3}) if (v.defined()) keep->push_back(v);
   return [p, epi, cfg](hipStream_t s, int) { return jr_conv_forward(&p, cfg, epi, s); };
 }

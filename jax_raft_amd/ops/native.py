@@ -30,6 +30,8 @@ CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (16, 256), 4: (64, 64
 CFG_TILES.update({6: (128, 128), 7: (64, 128), 8: (128, 64), 9: (128, 256), 10: (64, 64), 11: (256, 128)})
 # configs 12..15: 32x32x16-MFMA kernel (kernel M32)
 CFG_TILES.update({12: (128, 128), 13: (64, 128), 14: (128, 64), 15: (64, 64)})
+# configs 16/17: kernel R at 256-wide block tiles (128x64 / 64x128 wave tiles, one block per CU)
+CFG_TILES.update({16: (256, 128), 17: (128, 256)})
 NUM_CUS = 256
 
 
