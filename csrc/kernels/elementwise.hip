@@ -316,3 +316,23 @@ extern "C" int jr_im2col(const void* x, int N, int H, int W, int x_cstride, int 
                      x_cstride, x_coff, cin8, KH, KW, SH, SW, PH, PW, OH, OW, kpad, M, (bf16*)col);
   return (int)hipGetLastError();
 }
+
+// Zero fill (plan memsets are kernels, not hipMemsetAsync nodes, so a captured
+// plan is a pure kernel + event graph on every lane).
+__global__ __launch_bounds__(256) void zero_fill_kernel(u32x4* __restrict__ p16, long n16, unsigned* __restrict__ p4,
+                                                          long n4) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n16) p16[i] = u32x4{0u, 0u, 0u, 0u};
+  if (i < n4) p4[i] = 0u;
+}
+
+extern "C" int jr_zero_fill(void* p, long bytes, hipStream_t stream) {
+  if (((uintptr_t)p & 15) || (bytes & 3)) return (int)hipErrorInvalidValue;
+  const long n16 = bytes / 16;
+  const long n4 = (bytes - n16 * 16) / 4;
+  const long n = n16 > n4 ? n16 : n4;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(zero_fill_kernel, dim3(nblk(n, 256)), dim3(256), 0, stream, (u32x4*)p, n16,
+                     (unsigned*)((char*)p + n16 * 16), n4);
+  return (int)hipGetLastError();
+}

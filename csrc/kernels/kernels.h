@@ -119,6 +119,7 @@ int jr_init_coords(float* coords, int B, int h, int w, hipStream_t stream);
 int jr_im2col(const void* x, int N, int H, int W, int x_cstride, int x_coff, int cin8, int KH, int KW,
               int SH, int SW, int PH, int PW, int OH, int OW, int kpad, void* col, hipStream_t stream);
 // copy bf16 channel slice: dst[m][doff + c] = src[m][soff + c], c < C
+int jr_zero_fill(void* p, long bytes, hipStream_t stream);
 int jr_copy_channels(const void* src, int s_cstride, int s_coff, void* dst, int d_cstride, int d_coff,
                      int M, int C, hipStream_t stream);
 

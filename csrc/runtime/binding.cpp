@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <functional>
 #include <string>
@@ -219,19 +220,31 @@ static Launch make_lookup(const TList& t, const IList& i, std::vector<at::Tensor
 }
 
 // ------------------------------------------------------------------ upsample
+// Upsampled-flow output: a view whose trailing (B, 8h, 8w, 2) block is dense
+// (the engine passes out[:, b0:b1] of the (iters, B_total, H, W, 2) buffer).
+// Returns the float capacity from the view's first element to the end of its
+// storage, which bounds every per-iteration write.
+static int64_t check_flow_out(const at::Tensor& out, int B, int h, int w) {
+  TORCH_CHECK(out.defined() && out.is_cuda() && out.scalar_type() == at::kFloat, "out must be a CUDA float32 tensor");
+  TORCH_CHECK(out.dim() >= 4 && out.size(-1) == 2 && out.size(-2) == 8 * w && out.size(-3) == 8 * h &&
+                  out.size(-4) == B && out.stride(-1) == 1 && out.stride(-2) == 2 && out.stride(-3) == 16 * w &&
+                  out.stride(-4) == 128 * (int64_t)h * w,
+              "out: trailing (B, 8h, 8w, 2) block must be dense");
+  return (int64_t)(out.storage().nbytes() / sizeof(float)) - out.storage_offset();
+}
+
 // t = [mask, flow, out], i = [B, h, w, out_iter_stride]
 static Launch make_upsample_convex(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
   at::Tensor mask = opt(t, 0), flow = opt(t, 1), out = opt(t, 2);
-  check_bf16(mask, "mask"); check_f32(flow, "flow"); check_f32(out, "out");
+  check_bf16(mask, "mask"); check_f32(flow, "flow");
   const int B = (int)i[0], h = (int)i[1], w = (int)i[2];
   const int64_t stride = i[3];
   TORCH_CHECK(cs(mask) >= 576, "upsample: mask needs 576 channels");
-  TORCH_CHECK(out.numel() >= (int64_t)B * 64 * h * w * 2, "upsample: output too small");
+  const int64_t cap = check_flow_out(out, B, h, w);
   if (keep) { keep->push_back(mask); keep->push_back(flow); keep->push_back(out); }
   const void* mp = mask.data_ptr();
   const float* fp = flow.data_ptr<float>();
   float* op = out.data_ptr<float>();
-  const int64_t cap = out.numel();
   const int mcs = cs(mask);
   return [=](hipStream_t s, int it) {
     const int64_t off = stride * it;
@@ -243,14 +256,13 @@ static Launch make_upsample_convex(const TList& t, const IList& i, std::vector<a
 // t = [flow, out], i = [B, h, w, out_iter_stride]
 static Launch make_upsample_bilinear(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
   at::Tensor flow = opt(t, 0), out = opt(t, 1);
-  check_f32(flow, "flow"); check_f32(out, "out");
+  check_f32(flow, "flow");
   const int B = (int)i[0], h = (int)i[1], w = (int)i[2];
   const int64_t stride = i[3];
-  TORCH_CHECK(out.numel() >= (int64_t)B * 64 * h * w * 2, "upsample: output too small");
+  const int64_t cap = check_flow_out(out, B, h, w);
   if (keep) { keep->push_back(flow); keep->push_back(out); }
   const float* fp = flow.data_ptr<float>();
   float* op = out.data_ptr<float>();
-  const int64_t cap = out.numel();
   return [=](hipStream_t s, int it) {
     const int64_t off = stride * it;
     if (off + (int64_t)B * 64 * h * w * 2 > cap) return (int)hipErrorInvalidValue;
@@ -334,7 +346,8 @@ static Launch make_memset(const TList& t, std::vector<at::Tensor>* keep) {
   if (keep) keep->push_back(x);
   void* p = x.data_ptr();
   const size_t bytes = x.numel() * x.element_size();
-  return [=](hipStream_t s, int) { return (int)hipMemsetAsync(p, 0, bytes, s); };
+  TORCH_CHECK(((uintptr_t)p & 15) == 0 && bytes % 4 == 0, "memset: 16-B aligned, 4-B multiple tensors only");
+  return [=](hipStream_t s, int) { return jr_zero_fill(p, (long)bytes, s); };
 }
 
 // t = [src, dst]
@@ -446,7 +459,7 @@ void im2col_op(const TList& t, IList i) { run_now(make_im2col(t, i, nullptr)); }
 // iteration's mask head), which also keeps graph capture self-contained.
 class Plan : public torch::CustomClassHolder {
  public:
-  static constexpr int kMaxLanes = 4;
+  static constexpr int kMaxLanes = 8;
   static constexpr int kMaxEvents = 64;
   Plan() = default;
   ~Plan() override {
@@ -500,16 +513,20 @@ class Plan : public torch::CustomClassHolder {
     reset_graph();
     if (!cap_stream_) TORCH_CHECK(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking) == hipSuccess, "stream");
     hipStream_t s = cap_stream_;
+    debug_ = std::getenv("JR_PLAN_DEBUG") != nullptr;
     // order the capture after work already queued on the current stream
     TORCH_CHECK(hipStreamSynchronize(cur_stream()) == hipSuccess, "sync");
     TORCH_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess, "begin capture");
     int err = enqueue(s, (int)n_iters);
+    if (debug_) fprintf(stderr, "[plan] enqueue done err=%d\n", err);
     hipGraph_t g = nullptr;
     hipError_t e2 = hipStreamEndCapture(s, &g);
+    if (debug_) fprintf(stderr, "[plan] end capture %d\n", (int)e2);
     TORCH_CHECK(err == 0, "launch failed during capture: ", hipGetErrorString((hipError_t)err));
     TORCH_CHECK(e2 == hipSuccess && g != nullptr, "end capture failed: ", hipGetErrorString(e2));
     graph_ = g;
     hipError_t e3 = hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0);
+    if (debug_) fprintf(stderr, "[plan] instantiate %d\n", (int)e3);
     TORCH_CHECK(e3 == hipSuccess, "graph instantiate failed: ", hipGetErrorString(e3));
     captured_iters_ = n_iters;
   }
@@ -558,17 +575,25 @@ class Plan : public torch::CustomClassHolder {
     }
     return 0;
   }
+  // recorded[ev] = 1 + lane of the event's latest record in this enqueue (0: not recorded).
+  // A wait on an event last recorded on the same lane is already satisfied by stream
+  // order and is skipped (a same-stream record/wait pair on a forked capture stream
+  // also crashes hipStreamEndCapture on this ROCm).
   int exec_op(const Op& o, hipStream_t* st, int it, std::vector<char>& recorded) {
     hipStream_t s = st[o.lane];
+    if (debug_) fprintf(stderr, "[plan] it=%d lane=%d %s stream=%p\n", it, o.lane, o.name.c_str(), (void*)s);
     switch (o.kind) {
       case OP_LAUNCH: return o.l(s, it);
-      case OP_RECORD: recorded[o.ev] = 1; return (int)hipEventRecord(events_[o.ev], s);
-      default: return recorded[o.ev] ? (int)hipStreamWaitEvent(s, events_[o.ev], 0) : 0;
+      case OP_RECORD: recorded[o.ev] = (char)(1 + o.lane); return (int)hipEventRecord(events_[o.ev], s);
+      default:
+        if (!recorded[o.ev] || recorded[o.ev] == 1 + o.lane) return 0;
+        return (int)hipStreamWaitEvent(s, events_[o.ev], 0);
     }
   }
   int enqueue(hipStream_t s, int n_iters) {
     if (int r = ensure_resources()) return r;
-    hipStream_t st[kMaxLanes] = {s, nullptr, nullptr, nullptr};
+    hipStream_t st[kMaxLanes] = {};
+    st[0] = s;
     if (used_lanes_ > 1) {
       if (int r = (int)hipEventRecord(fork_, s)) return r;
       for (int l = 1; l < used_lanes_; ++l) {
@@ -594,12 +619,13 @@ class Plan : public torch::CustomClassHolder {
   int used_lanes_ = 1;
   std::vector<hipEvent_t> events_;
   hipEvent_t fork_ = nullptr;
-  hipEvent_t join_[kMaxLanes] = {nullptr, nullptr, nullptr, nullptr};
-  hipStream_t lanes_[kMaxLanes] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t join_[kMaxLanes] = {};
+  hipStream_t lanes_[kMaxLanes] = {};
   hipStream_t cap_stream_ = nullptr;
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t exec_ = nullptr;
   int64_t captured_iters_ = -1;
+  bool debug_ = false;
 };
 
 }  // namespace jr

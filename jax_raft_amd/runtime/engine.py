@@ -23,6 +23,7 @@ Persistent buffers replace every concat of the reference:
 """
 from __future__ import annotations
 
+
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -97,7 +98,8 @@ class _Shape:
 
 @dataclass
 class _PlanState:
-    plan: object
+    plan: object                      # plans[0]
+    plans: List[object] = field(default_factory=list)   # one native Plan (one hipGraph) per batch part
     bufs: Dict[str, torch.Tensor] = field(default_factory=dict)
     inp1: Optional[torch.Tensor] = None
     inp2: Optional[torch.Tensor] = None
@@ -123,12 +125,18 @@ class RaftEngine:
             flow-feature convs || lookup + correlation convs; mask head +
             upsampling of iteration i || iteration i+1) so they overlap on
             the GPU (parallel branches of the captured hipGraph).
+        split: run the batch as this many independent half-forwards on
+            separate lanes (when the batch divides evenly), so that one
+            part's kernels fill the CUs another part's leave idle.
     """
 
     def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True,
-                 corr_dtype: torch.dtype = torch.bfloat16, autotune: bool = True, streams: bool = True):
+                 corr_dtype: torch.dtype = torch.bfloat16, autotune: bool = True, streams: bool = True,
+                 split: int = 1):
         nat.require()
         self.streams = streams
+        self.split = split
+        self._part_streams: List[torch.cuda.Stream] = []
         self.model = model
         self.device = torch.device(device)
         self.use_graph = use_graph
@@ -271,15 +279,16 @@ class RaftEngine:
 
     # ------------------------------------------------------------- lowering
     def _encoder(self, st: _PlanState, plan, tag: str, enc: FeatureEncoder, x: torch.Tensor, N: int, H: int,
-                 W: int):
-        """Lower a FeatureEncoder up to (not including) its final 1x1 conv."""
+                 W: int, bt: str = ""):
+        """Lower a FeatureEncoder up to (not including) its final 1x1 conv.  ``tag``
+        names the conv specs ("fe"/"ce"), ``bt`` prefixes the buffers (batch part)."""
         inorm = enc.norm_kind == NORM_INSTANCE
         sp = self._specs
         bufs = st.bufs
 
         def alloc(name, shape, dtype=BF16):
             t = torch.zeros(shape, dtype=dtype, device=self.device)
-            bufs[name] = t
+            bufs[bt + name] = t
             return t
 
         def conv_raw(name, x, N, H, W, act=ACT_NONE, res=None, res_post=0):
@@ -346,39 +355,63 @@ class RaftEngine:
         return x, H, W
 
     def _build(self, B: int, H: int, W: int, n_iters: int) -> _PlanState:
+        h, w = H // 8, W // 8
+        L = self.num_levels
+        min_sz = 2 * (2 ** (L - 1))
+        assert h >= min_sz and w >= min_sz, (
+            f"Feature maps are too small to be down-sampled by the correlation pyramid: need >= {min_sz}, got {(h, w)}; "
+            f"input images should be at least {8 * min_sz}.")
+        dev = self.device
+        parts = self.split if (self.split > 1 and B % self.split == 0) else 1
+        nb = B // parts
+        # Each part is an independent forward with its own Plan, captured as its
+        # own hipGraph and replayed on its own stream, so the parts' kernels fill
+        # each other's idle CUs (kernel tails, launch gaps, small kernels).
+        plans = [nat.new_plan() for _ in range(parts)]
+        st = _PlanState(plan=plans[0], plans=plans, n_iters=n_iters)
+        st.inp1 = torch.zeros((B, H, W, 3), dtype=F32, device=dev)
+        st.inp2 = torch.zeros((B, H, W, 3), dtype=F32, device=dev)
+        st.out = torch.zeros((n_iters, B, H, W, 2), dtype=F32, device=dev)
+        lanes = (0, 1, 2) if self.streams else (0, 0, 0)
+        for part, plan in enumerate(plans):
+            self._build_part(st, plan, part * nb, nb, H, W, n_iters, f"p{part}.", lanes, 0)
+            plan.set_lane(0)
+            plan.set_segment(2)
+        if parts > 1 and len(self._part_streams) < parts:
+            self._part_streams = [torch.cuda.Stream(device=dev) for _ in range(parts)]
+        return st
+
+    def _build_part(self, st: _PlanState, plan, b0: int, B: int, H: int, W: int, n_iters: int, pt: str,
+                    lanes: Tuple[int, int, int], ev0: int):
+        """Lower one forward over images [b0, b0 + B) onto ``plan`` using lanes
+        (main, side, side2) and events ev0 .. ev0 + 5."""
         m = self.model
-        plan = nat.new_plan()
-        st = _PlanState(plan=plan, n_iters=n_iters)
         dev = self.device
         bufs = st.bufs
         sp = self._specs
         h, w = H // 8, W // 8
         M = B * h * w
         L = self.num_levels
-        min_sz = 2 * (2 ** (L - 1))
-        assert h >= min_sz and w >= min_sz, (
-            f"Feature maps are too small to be down-sampled by the correlation pyramid: need >= {min_sz}, got {(h, w)}; "
-            f"input images should be at least {8 * min_sz}.")
 
         def alloc(name, shape, dtype=BF16):
             t = torch.zeros(shape, dtype=dtype, device=dev)
-            bufs[name] = t
+            bufs[pt + name] = t
             return t
 
-        st.inp1 = alloc("inp1", (B, H, W, 3), F32)
-        st.inp2 = alloc("inp2", (B, H, W, 3), F32)
-        st.out = alloc("out", (n_iters, B, H, W, 2), F32)
+        inp1 = st.inp1[b0:b0 + B]
+        inp2 = st.inp2[b0:b0 + B]
+        out = st.out[:, b0:b0 + B]
 
         # ---------------- prologue: encoders + correlation pyramid
         # lanes: 0 = feature encoder + correlation pyramid, 1 = context encoder
-        E_PREP, E_CTX, E_IT, E_FLOW, E_FH, E_MASK = range(6)
-        side = 1 if self.streams else 0
-        side2 = 2 if self.streams else 0
+        E_PREP, E_CTX, E_IT, E_FLOW, E_FH, E_MASK = range(ev0, ev0 + 6)
+        main, side, side2 = lanes
 
         def lane(l):
             plan.set_lane(l)
 
         plan.set_segment(0)
+        lane(main)
         hx = alloc("hx", (M, self.hx_cs))
         qx = alloc("qx", (M, self.hx_cs))
         h32 = alloc("h32", (M, self.hidden), F32)
@@ -389,20 +422,20 @@ class RaftEngine:
         for t in (hx, qx, flow8, flow32):
             plan.add_memset([t])
         x0 = alloc("x0", (2 * B, H, W, 8))
-        plan.add_prep([st.inp1, st.inp2, x0], [B, H, W])
+        plan.add_prep([inp1, inp2, x0], [B, H, W])
         plan.add_record(E_PREP)
 
         lane(side)
         plan.add_wait(E_PREP)
-        ctxf, ch_, cw_ = self._encoder(st, plan, "ce", m.context_encoder, x0[:B], B, H, W)
+        ctxf, ch_, cw_ = self._encoder(st, plan, "ce", m.context_encoder, x0[:B], B, H, W, bt=pt)
         assert (ch_, cw_) == (h, w), "The context encoder should downsample H and W by 8"
         self._conv(plan, sp["ce.conv"], ctxf, B, h, w, hx, act=ACT_SPLIT_TANH_RELU, split=self.hidden,
                    y2=qx, h32=h32, hidden=self.hidden)
         plan.add_init_coords([coords], [B, h, w])
         plan.add_record(E_CTX)
 
-        lane(0)
-        feat, fh_, fw_ = self._encoder(st, plan, "fe", m.feature_encoder, x0, 2 * B, H, W)
+        lane(main)
+        feat, fh_, fw_ = self._encoder(st, plan, "fe", m.feature_encoder, x0, 2 * B, H, W, bt=pt)
         assert (fh_, fw_) == (h, w), "The feature encoder should downsample H and W by 8"
         fmap = alloc("fmap", (2 * B, h, w, self.fmap_ch))
         self._conv(plan, sp["fe.conv"], feat, 2 * B, h, w, fmap)
@@ -420,6 +453,7 @@ class RaftEngine:
         # lanes: 0 = lookup -> corr convs -> motion conv -> GRU -> flow head,
         # 1 = flow-feature convs, 2 = mask head + upsampling (off the critical path)
         plan.set_segment(1)
+        lane(main)
         corr = alloc("corr", (M, self.corr_cs))
         me = m.update_block.motion_encoder
         cl, fl = me.corr_layers, me.flow_layers
@@ -431,7 +465,7 @@ class RaftEngine:
         self._conv(plan, sp["me.convflow1"], flow8, B, h, w, f1, act=ACT_RELU)
         self._conv(plan, sp["me.convflow2"], f1, B, h, w, cf, y_coff=cl[-1], act=ACT_RELU)
         plan.add_record(E_FLOW)
-        lane(0)
+        lane(main)
         plan.add_lookup([coords, corr] + levels + [None] * (4 - L), [L, B, h, w, self.radius])
         if len(cl) == 2:
             c1 = alloc("c1", (M, cl[0]))
@@ -457,18 +491,16 @@ class RaftEngine:
         plan.add_record(E_FH)
         lane(side2)
         plan.add_wait(E_FH)
-        stride = B * H * W * 2
+        stride = st.out.shape[1] * H * W * 2  # one iteration of the full-batch output
         if self.has_mask:
             mask = alloc("mask", (M, 576))
             self._conv(plan, sp["mask"], fm, B, h, w, mask, x_coff=self.fh_hidden,
                        alpha=m.mask_predictor.multiplier)
-            plan.add_upsample_convex([mask, flow32, st.out], [B, h, w, stride])
+            plan.add_upsample_convex([mask, flow32, out], [B, h, w, stride])
         else:
-            plan.add_upsample_bilinear([flow32, st.out], [B, h, w, stride])
+            plan.add_upsample_bilinear([flow32, out], [B, h, w, stride])
         plan.add_record(E_MASK)
-        lane(0)
-        plan.set_segment(2)
-        return st
+        lane(main)
 
     # --------------------------------------------------------------- forward
     @torch.no_grad()
@@ -484,13 +516,27 @@ class RaftEngine:
             self._states[key] = st
         st.inp1.copy_(image1)
         st.inp2.copy_(image2)
-        if self.use_graph:
-            if st.plan.captured_iters() != num_flow_updates:
-                st.plan.capture(num_flow_updates)
-            st.plan.replay()
+        if len(st.plans) == 1:
+            self._launch(st.plan, num_flow_updates)
         else:
-            st.plan.run(num_flow_updates)
+            cur = torch.cuda.current_stream(self.device)
+            fork = torch.cuda.Event()
+            fork.record(cur)
+            for plan, strm in zip(st.plans, self._part_streams):
+                strm.wait_event(fork)
+                with torch.cuda.stream(strm):
+                    self._launch(plan, num_flow_updates)
+            for strm in self._part_streams[:len(st.plans)]:
+                cur.wait_stream(strm)
         return st.out.clone() if self.copy_output else st.out
+
+    def _launch(self, plan, n_iters: int) -> None:
+        if self.use_graph:
+            if plan.captured_iters() != n_iters:
+                plan.capture(n_iters)
+            plan.replay()
+        else:
+            plan.run(n_iters)
 
     def op_names(self, B: int, H: int, W: int, n_iters: int):
         st = self._states.get((B, H, W, n_iters)) or self._build(B, H, W, n_iters)
