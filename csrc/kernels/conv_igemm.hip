@@ -283,20 +283,21 @@ struct FastStage {
   }
 };
 
-template <int BCO, int BP, int WCO, int EPI, bool FAST>
-__global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
-  constexpr int WP = 4 / WCO;
+template <int BCO, int BP, int WCO, int EPI, bool FAST, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(const ConvParams p) {
+  constexpr int WP = NW / WCO;
+  constexpr int RP = NW * 8;              // staging rows covered by one pass of the block (8 lanes per row)
   constexpr int WTCO = BCO / WCO;
   constexpr int WTP = BP / WP;
   constexpr int TM = WTCO / 16;
   constexpr int TN = WTP / 16;
   constexpr int NV = 4 * TM;              // contiguous channels per lane
-  constexpr int XR = BP / 32;             // X rows loaded per thread
-  constexpr int WR = BCO >= 32 ? BCO / 32 : 1;
+  constexpr int XR = BP / RP;             // X rows loaded per thread
+  constexpr int WR = BCO >= RP ? BCO / RP : 1;
   constexpr int A_ELEMS = BCO * BK;
   constexpr int B_ELEMS = BP * BK;
   constexpr unsigned OOB = 0x80000000u;   // buffer offset past num_records -> hardware returns 0
-  static_assert(TM >= 1 && TN >= 1 && WCO * WP == 4, "tile");
+  static_assert(TM >= 1 && TN >= 1 && WCO * WP == NW && XR >= 1, "tile");
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * (A_ELEMS + B_ELEMS)];
 
   const int tid = threadIdx.x;
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
   unsigned rbase[XR];
 #pragma unroll
   for (int i = 0; i < XR; ++i) {
-    const int m = p0 + (tid >> 3) + 32 * i;
+    const int m = p0 + (tid >> 3) + RP * i;
     if (m < p.M) {
       const int n = m / OHW;
       const int rem = m - n * OHW;
@@ -337,7 +338,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
     }
   }
   const unsigned wrow_off = (unsigned)((co0 + (tid >> 3)) * p.kpad * 2 + ch * 16);
-  const unsigned wrow_lim = (unsigned)(p.cout_pad - co0 - (tid >> 3));  // rows i*32 < lim are valid
+  const unsigned wrow_lim = (unsigned)(p.cout_pad - co0 - (tid >> 3));  // rows i*RP < lim are valid
 
   // K-chunk state of the NEXT stage to load: kc = ks*8 + ch.
   const int cpt = p.cin8 >> 3;
@@ -384,8 +385,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
     const unsigned kofs = (unsigned)ks_next * (BK * 2);
 #pragma unroll
     for (int i = 0; i < WR; ++i) {
-      const bool ok = ((BCO >= 32) || (tid < BCO * 8)) && (unsigned)(32 * i) < wrow_lim && ks_next * BK < p.kpad;
-      const unsigned off = wrow_off + (unsigned)(32 * i) * (unsigned)p.kpad * 2u + kofs;
+      const bool ok = ((BCO >= RP) || (tid < BCO * 8)) && (unsigned)(RP * i) < wrow_lim && ks_next * BK < p.kpad;
+      const unsigned off = wrow_off + (unsigned)(RP * i) * (unsigned)p.kpad * 2u + kofs;
       r.w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wsrd, ok ? off : OOB, 0, 0));
     }
     // advance the chunk state to the following stage
@@ -403,13 +404,13 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
     bf16* sB = sA + A_ELEMS;
 #pragma unroll
     for (int i = 0; i < XR; ++i) {
-      const int rr = (tid >> 3) + 32 * i;
+      const int rr = (tid >> 3) + RP * i;
       *(u32x4*)(sB + rr * BK + ((ch ^ swzB(rr)) << 3)) = r.x[i];
     }
 #pragma unroll
     for (int i = 0; i < WR; ++i) {
-      const int rr = (tid >> 3) + 32 * i;
-      if ((BCO >= 32) || (tid < BCO * 8)) *(u32x4*)(sA + rr * BK + ((ch ^ swzB(rr)) << 3)) = r.w[i];
+      const int rr = (tid >> 3) + RP * i;
+      if ((BCO >= RP) || (tid < BCO * 8)) *(u32x4*)(sA + rr * BK + ((ch ^ swzB(rr)) << 3)) = r.w[i];
     }
   };
 
@@ -876,7 +877,11 @@ int launch_cfg(const ConvParams* p, int epi, hipStream_t s) {
   dim3 grid((p->M + BP - 1) / BP, (rows + BCO - 1) / BCO);
   dim3 block(256);
 #define JR_LAUNCH(E)                                                                          \
-  if constexpr (KIND >= 3) hipLaunchKernelGGL((conv_d2_kernel<BCO, BP, WCO, KIND - 1, E>), grid, block, 0, s, *p); \
+  if constexpr (KIND == 6 || KIND == 7) {                                                     \
+    constexpr int NW_ = KIND == 6 ? 8 : 16;                                                    \
+    if (p->fast) hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, true, NW_>), grid, dim3(NW_ * 64), 0, s, *p); \
+    else hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, false, NW_>), grid, dim3(NW_ * 64), 0, s, *p);         \
+  } else if constexpr (KIND >= 3) hipLaunchKernelGGL((conv_d2_kernel<BCO, BP, WCO, KIND - 1, E>), grid, block, 0, s, *p); \
   else if constexpr (KIND == 2) {                                                              \
     if (p->fast) hipLaunchKernelGGL((conv_m32_kernel<BCO, BP, WCO, E, true>), grid, block, 0, s, *p); \
     else hipLaunchKernelGGL((conv_m32_kernel<BCO, BP, WCO, E, false>), grid, block, 0, s, *p);         \
@@ -920,6 +925,14 @@ extern "C" int jr_conv_forward(const ConvParams* p, int cfg, int epi, hipStream_
     // hipBLASLt-like shapes: 256-wide block, 128x64 / 64x128 wave tiles, one block per CU
     case 16: return launch_cfg<256, 128, 2, 0>(p, epi, stream);
     case 17: return launch_cfg<128, 256, 2, 0>(p, epi, stream);
+    // kernel R with 8 waves per block (64x32 / 32x64 wave tiles): twice the waves per SIMD
+    case 18: return launch_cfg<128, 128, 2, 6>(p, epi, stream);
+    case 19: return launch_cfg<128, 128, 4, 6>(p, epi, stream);
+    case 20: return launch_cfg<256, 128, 4, 6>(p, epi, stream);
+    case 21: return launch_cfg<128, 128, 4, 7>(p, epi, stream);   // 16 waves, 32x32 wave tiles
+    case 22: return launch_cfg<256, 128, 4, 7>(p, epi, stream);   // 16 waves, 64x32
+    case 23: return launch_cfg<128, 64, 2, 6>(p, epi, stream);    // 8 waves, 64x16
+    case 24: return launch_cfg<64, 128, 1, 6>(p, epi, stream);    // 8 waves, 64x16
     default: return (int)hipErrorInvalidValue;
   }
 }

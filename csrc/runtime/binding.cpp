@@ -147,7 +147,7 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   } else {
     TORCH_CHECK(false, "conv: unknown epilogue ", epi);
   }
-  TORCH_CHECK(cfg >= 0 && cfg <= 17, "conv: unknown tile config ", cfg);
+  TORCH_CHECK(cfg >= 0 && cfg <= 24, "conv: unknown tile config ", cfg);
   if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3}) if (v.defined()) keep->push_back(v);
   return [p, epi, cfg](hipStream_t s, int) { return jr_conv_forward(&p, cfg, epi, s); };
 }

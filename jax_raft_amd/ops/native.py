@@ -32,6 +32,10 @@ CFG_TILES.update({6: (128, 128), 7: (64, 128), 8: (128, 64), 9: (128, 256), 10: 
 CFG_TILES.update({12: (128, 128), 13: (64, 128), 14: (128, 64), 15: (64, 64)})
 # configs 16/17: kernel R at 256-wide block tiles (128x64 / 64x128 wave tiles, one block per CU)
 CFG_TILES.update({16: (256, 128), 17: (128, 256)})
+# configs 18..20: kernel R with 8 waves per block (64x32, 32x64, 64x64 wave tiles)
+CFG_TILES.update({18: (128, 128), 19: (128, 128), 20: (256, 128)})
+# configs 21/22: 16 waves per block (32x32 / 64x32 wave tiles); 23/24: 8 waves at 128x64 / 64x128
+CFG_TILES.update({21: (128, 128), 22: (256, 128), 23: (128, 64), 24: (64, 128)})
 NUM_CUS = 256
 
 

@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""Per-kernel time breakdown of the timed bench steps from a rocprofv3
+kernel-trace CSV (run bench.py with --no-graph so every launch is traced).
+Only dispatches after the autotune/warm-up phase are kept: the last
+``--steps`` forwards are located by their prep_images launches."""
+import argparse
+import collections
+import csv
+import re
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--top", type=int, default=30)
+    a = ap.parse_args()
+    rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
+    starts = [i for i, r in enumerate(rows) if "prep_images" in r["Kernel_Name"]]
+    first = starts[-a.steps]
+    rows = rows[first:]
+    agg = collections.defaultdict(lambda: [0, 0.0])
+    for r in rows:
+        n = re.sub(r"\(anonymous namespace\)::", "", r["Kernel_Name"])
+        n = re.sub(r"\(.*", "", n)
+        if n.startswith("void "):
+            n = n[5:]
+        key = f"{n} grid=({r['Grid_Size_X']},{r['Grid_Size_Y']})" if "conv" in n else n
+        agg[key][0] += 1
+        agg[key][1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    tot = sum(v[1] for v in agg.values())
+    wall = (int(rows[-1]["End_Timestamp"]) - int(rows[0]["Start_Timestamp"])) / 1e3
+    print(f"steps={a.steps} kernel-sum={tot / 1e3 / a.steps:.3f} ms/step  wall={wall / 1e3 / a.steps:.3f} ms/step")
+    for n, (c, d) in sorted(agg.items(), key=lambda x: -x[1][1])[:a.top]:
+        print(f"{d / 1e3 / a.steps:8.3f} ms/step {100 * d / tot:5.1f}% {c // a.steps:5d}/step  {d / c:8.1f} us  {n[:110]}")
+
+
+if __name__ == "__main__":
+    main()
