@@ -488,19 +488,20 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // storage row (within a 64-row group) holding channel 32t + c(rho), c(rho) = 16((rho>>2)&1) + (rho&3) + 4(rho>>3)
 JR_DEVICE int m32_arow(int t, int rho) { return 16 * (rho >> 3) + 4 * (2 * t + ((rho >> 2) & 1)) + (rho & 3); }
 
-template <int BCO, int BP, int WCO, int EPI, bool FAST>
-__global__ __launch_bounds__(256) void conv_m32_kernel(const ConvParams p) {
-  constexpr int WP = 4 / WCO;
+template <int BCO, int BP, int WCO, int EPI, bool FAST, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void conv_m32_kernel(const ConvParams p) {
+  constexpr int WP = NW / WCO;
+  constexpr int RP = NW * 8;   // staging rows per block pass
   constexpr int WTCO = BCO / WCO;
   constexpr int WTP = BP / WP;
   constexpr int TM = WTCO / 32;
   constexpr int TN = WTP / 32;
-  constexpr int XR = BP / 32;
-  constexpr int WR = BCO / 32;
+  constexpr int XR = BP / RP;
+  constexpr int WR = BCO >= RP ? BCO / RP : 1;
   constexpr int A_ELEMS = BCO * BK;
   constexpr int B_ELEMS = BP * BK;
   constexpr unsigned OOB = 0x80000000u;
-  static_assert(TM >= 1 && TN >= 1 && WCO * WP == 4 && BCO >= 32, "tile");
+  static_assert(TM >= 1 && TN >= 1 && WCO * WP == NW && BCO >= RP && XR >= 1, "tile");
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * (A_ELEMS + B_ELEMS)];
 
   const int tid = threadIdx.x;
@@ -522,7 +523,7 @@ __global__ __launch_bounds__(256) void conv_m32_kernel(const ConvParams p) {
   unsigned rbase[XR];
 #pragma unroll
   for (int i = 0; i < XR; ++i) {
-    const int m = p0 + (tid >> 3) + 32 * i;
+    const int m = p0 + (tid >> 3) + RP * i;
     if (m < p.M) {
       const int n = m / OHW;
       const int rem = m - n * OHW;
@@ -583,8 +584,8 @@ __global__ __launch_bounds__(256) void conv_m32_kernel(const ConvParams p) {
     const unsigned kofs = (unsigned)ks_next * (BK * 2);
 #pragma unroll
     for (int i = 0; i < WR; ++i) {
-      const bool ok = (unsigned)(32 * i) < wrow_lim && ks_next * BK < p.kpad;
-      const unsigned off = wrow_off + (unsigned)(32 * i) * (unsigned)p.kpad * 2u + kofs;
+      const bool ok = (unsigned)(RP * i) < wrow_lim && ks_next * BK < p.kpad;
+      const unsigned off = wrow_off + (unsigned)(RP * i) * (unsigned)p.kpad * 2u + kofs;
       r.w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wsrd, ok ? off : OOB, 0, 0));
     }
     ++ks_next;
@@ -601,12 +602,12 @@ __global__ __launch_bounds__(256) void conv_m32_kernel(const ConvParams p) {
     bf16* sB = sA + A_ELEMS;
 #pragma unroll
     for (int i = 0; i < XR; ++i) {
-      const int rr = (tid >> 3) + 32 * i;
+      const int rr = (tid >> 3) + RP * i;
       *(u32x4*)(sB + rr * BK + ((ch ^ swzB(rr)) << 3)) = r.x[i];
     }
 #pragma unroll
     for (int i = 0; i < WR; ++i) {
-      const int rr = (tid >> 3) + 32 * i;
+      const int rr = (tid >> 3) + RP * i;
       *(u32x4*)(sA + rr * BK + ((ch ^ swzB(rr)) << 3)) = r.w[i];
     }
   };
@@ -633,7 +634,7 @@ __global__ __launch_bounds__(256) void conv_m32_kernel(const ConvParams p) {
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
-        const int row = gbase + m32_arow(tabs0 + tm, rho);
+        const int row = gbase + 64 * ((tabs0 + tm) >> 1) + m32_arow((tabs0 + tm) & 1, rho);  // 128-row wave tiles span two groups
         af[tm] = *(const bf16x8*)(sA + row * BK + ((chunk ^ swzB(row)) << 3));
       }
 #pragma unroll
@@ -881,7 +882,7 @@ int launch_cfg(const ConvParams* p, int epi, hipStream_t s) {
     constexpr int NW_ = KIND == 6 ? 8 : 16;                                                    \
     if (p->fast) hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, true, NW_>), grid, dim3(NW_ * 64), 0, s, *p); \
     else hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, false, NW_>), grid, dim3(NW_ * 64), 0, s, *p);         \
-  } else if constexpr (KIND >= 3) hipLaunchKernelGGL((conv_d2_kernel<BCO, BP, WCO, KIND - 1, E>), grid, block, 0, s, *p); \
+  } else if constexpr (KIND == 3 || KIND == 4) hipLaunchKernelGGL((conv_d2_kernel<BCO, BP, WCO, KIND - 1, E>), grid, block, 0, s, *p); \
   else if constexpr (KIND == 2) {                                                              \
     if (p->fast) hipLaunchKernelGGL((conv_m32_kernel<BCO, BP, WCO, E, true>), grid, block, 0, s, *p); \
     else hipLaunchKernelGGL((conv_m32_kernel<BCO, BP, WCO, E, false>), grid, block, 0, s, *p);         \

@@ -64,9 +64,10 @@ struct ConvParams {
 
 // cfg (co x px block tile): kernel R (register-staged, 16x16x32 MFMA) 0 = 128x128, 1 = 64x128,
 // 2 = 128x64, 3 = 16x256, 4 = 64x64, 5 = 16x64 (narrow outputs, e.g. the 2-channel flow head),
-// 16 = 256x128, 17 = 128x256; kernel D2 (LDS-DMA) 6 = 128x128, 7 = 64x128, 8 = 128x64,
-// 9 = 128x256, 10 = 64x64, 11 = 256x128; kernel M32 (32x32x16 MFMA) 12 = 128x128,
-// 13 = 64x128, 14 = 128x64, 15 = 64x64.  The engine autotunes the choice per conv.
+// 16 = 256x128, 17 = 128x256 (4 waves); 18 = 128x128, 19 = 128x128, 20 = 256x128, 23 = 128x64,
+// 24 = 64x128 (8 waves); 21 = 128x128, 22 = 256x128 (16 waves); kernel D2 (LDS-DMA) 6 = 128x128,
+// 7 = 64x128, 8 = 128x64, 9 = 128x256, 10 = 64x64, 11 = 256x128; kernel M32 (32x32x16 MFMA)
+// 12 = 128x128, 13 = 64x128, 14 = 128x64, 15 = 64x64.  The engine autotunes the choice per conv.
 int jr_conv_forward(const ConvParams* p, int cfg, int epi, hipStream_t stream);
 
 // ---------------------------------------------------------------------------

@@ -36,6 +36,10 @@ CFG_TILES.update({16: (256, 128), 17: (128, 256)})
 CFG_TILES.update({18: (128, 128), 19: (128, 128), 20: (256, 128)})
 # configs 21/22: 16 waves per block (32x32 / 64x32 wave tiles); 23/24: 8 waves at 128x64 / 64x128
 CFG_TILES.update({21: (128, 128), 22: (256, 128), 23: (128, 64), 24: (64, 128)})
+# Autotune candidates: configs that win at least one RAFT conv on MI355X
+# (tools/microbench.py, profiles/r1_microbench_conv_cfgs.txt); the others stay
+# compiled and tested but are not timed at plan build.
+TUNE_CFGS = (0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24)
 NUM_CUS = 256
 
 

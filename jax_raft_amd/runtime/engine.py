@@ -61,7 +61,7 @@ def _tune(spec: ConvSpec, x, N, H, W, y, kw, reps: int = 5) -> int:
     """Time every tile config of one conv problem; return the fastest."""
     ops = nat.ops()
     best, best_t = None, None
-    for cfg in sorted(nat.CFG_TILES):
+    for cfg in nat.TUNE_CFGS:
         args = conv_args(spec, x, N, H, W, y, **dict(kw, cfg=cfg))
         ops.conv(*args)  # warm (and JIT-free: all configs are precompiled)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
