@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-h2d", action="store_true", help="inputs already resident on the GPU")
     ap.add_argument("--no-streams", action="store_true", help="single-lane plan (no concurrent branches)")
+    ap.add_argument("--fused-flow-head", action="store_true", help="dedicated flow_head kernel for the flow head output")
     ap.add_argument("--split", type=int, default=1, help="independent batch parts (one hipGraph each) run concurrently per GPU")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse >1 rank on fewer GPUs")
@@ -83,7 +84,7 @@ def main():
         a = img1.to(dev, non_blocking=True)
         b = img2.to(dev, non_blocking=True)
         return model(a, b, num_flow_updates=args.iters, use_graph=not args.no_graph, streams=not args.no_streams,
-                     split=args.split)
+                     split=args.split, fused_flow_head=args.fused_flow_head)
 
     def barrier():
         if pg is not None:

@@ -121,6 +121,12 @@ int jr_im2col(const void* x, int N, int H, int W, int x_cstride, int x_coff, int
               int SH, int SW, int PH, int PW, int OH, int OW, int kpad, void* col, hipStream_t stream);
 // copy bf16 channel slice: dst[m][doff + c] = src[m][soff + c], c < C
 int jr_zero_fill(void* p, long bytes, hipStream_t stream);
+// Flow-head conv2 (3x3, cin -> 2, cin in {128, 256}) fused with the coordinate update
+// (flowhead.hip): fm bf16 [N*h*w][fcs] (channels [0, cin) used), wt bf16 [2][9][cin]
+// (output, tap kh*3+kw, channel).
+int jr_flow_head(const void* fm, int fcs, const void* wt, const float* bias, int N, int h, int w, int cin,
+                 float* coords, float* flow32, void* hx, int hx_cs, int hx_off, void* qx, int qx_cs, int qx_off,
+                 void* f8, int f8_cs, hipStream_t stream);
 int jr_copy_channels(const void* src, int s_cstride, int s_coff, void* dst, int d_cstride, int d_coff,
                      int M, int C, hipStream_t stream);
 

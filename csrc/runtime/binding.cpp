@@ -152,6 +152,41 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   return [p, epi, cfg](hipStream_t s, int) { return jr_conv_forward(&p, cfg, epi, s); };
 }
 
+
+// ------------------------------------------------------------------ flow head
+// t = [fm, wt (bf16 [2][9][cin]), bias (fp32 [2]), coords, flow32, hx, qx?, flow8?]
+// i = [N, h, w, cin, fm_coff, hx_off, qx_off]
+static Launch make_flow_head(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor fm = opt(t, 0), wt = opt(t, 1), bias = opt(t, 2), coords = opt(t, 3), flow32 = opt(t, 4), hx = opt(t, 5),
+             qx = opt(t, 6), f8 = opt(t, 7);
+  TORCH_CHECK(i.size() == 7, "flow_head: expected 7 ints");
+  check_bf16(fm, "fm"); check_bf16(wt, "wt"); check_f32(bias, "bias"); check_f32(coords, "coords");
+  check_f32(flow32, "flow32"); check_bf16(hx, "hx");
+  const int N = (int)i[0], h = (int)i[1], w = (int)i[2], cin = (int)i[3], coff = (int)i[4];
+  const int hx_off = (int)i[5], qx_off = (int)i[6];
+  const int64_t M = (int64_t)N * h * w;
+  TORCH_CHECK(cin == 128 || cin == 256, "flow_head: cin must be 128 or 256");
+  TORCH_CHECK(wt.numel() == 9 * cin * 2 && bias.numel() >= 2, "flow_head: weight shape");
+  TORCH_CHECK(cs(fm) % 8 == 0 && coff % 8 == 0 && coff + cin <= cs(fm) && fm.numel() >= M * cs(fm), "flow_head: fm");
+  TORCH_CHECK(coords.numel() >= 2 * M && flow32.numel() >= 2 * M, "flow_head: coords / flow32");
+  TORCH_CHECK(hx.numel() >= M * cs(hx) && hx_off + 2 <= cs(hx), "flow_head: hx");
+  if (qx.defined()) { check_bf16(qx, "qx"); TORCH_CHECK(qx.numel() >= M * cs(qx) && qx_off + 2 <= cs(qx), "flow_head: qx"); }
+  if (f8.defined()) { check_bf16(f8, "flow8"); TORCH_CHECK(f8.numel() >= M * cs(f8) && cs(f8) >= 2, "flow_head: flow8"); }
+  if (keep) for (auto& v : {fm, wt, bias, coords, flow32, hx, qx, f8}) if (v.defined()) keep->push_back(v);
+  const void* fp = (const char*)fm.data_ptr() + 2 * (int64_t)coff;
+  const void* wp = wt.data_ptr();
+  const float* bp = bias.data_ptr<float>();
+  float* cp = coords.data_ptr<float>();
+  float* f32p = flow32.data_ptr<float>();
+  void* hp = hx.data_ptr();
+  void* qp = ptr(qx);
+  void* f8p = ptr(f8);
+  const int fcs = cs(fm), hcs = cs(hx), qcs = qx.defined() ? cs(qx) : 0, f8cs = f8.defined() ? cs(f8) : 0;
+  return [=](hipStream_t s, int) {
+    return jr_flow_head(fp, fcs, wp, bp, N, h, w, cin, cp, f32p, hp, hcs, hx_off, qp, qcs, qx_off, f8p, f8cs, s);
+  };
+}
+
 // --------------------------------------------------------------- correlation
 // t = [f1, f2, l0, l1, l2, l3], i = [B, h, w, C, num_levels]; levels all fp32 or all bf16
 static void check_level(const at::Tensor& v, at::ScalarType dt) {
@@ -442,6 +477,7 @@ void init_coords_op(const TList& t, IList i) { run_now(make_init_coords(t, i, nu
 void copy_channels_op(const TList& t, IList i) { run_now(make_copy_channels(t, i, nullptr)); }
 void lookup_bwd_op(const TList& t, IList i) { run_now(make_lookup_bwd(t, i, nullptr)); }
 void im2col_op(const TList& t, IList i) { run_now(make_im2col(t, i, nullptr)); }
+void flow_head_op(const TList& t, IList i) { run_now(make_flow_head(t, i, nullptr)); }
 
 // --------------------------------------------------------------------- Plan
 // A Plan is the lowered RAFT forward: three segments (prologue, loop body run
@@ -495,6 +531,7 @@ class Plan : public torch::CustomClassHolder {
   void add_memset(TList t) { push(make_memset(t, &keep_), "memset"); }
   void add_copy(TList t) { push(make_copy(t, &keep_), "copy"); }
   void add_copy_channels(TList t, IList i) { push(make_copy_channels(t, i, &keep_), "copy_channels"); }
+  void add_flow_head(TList t, IList i) { push(make_flow_head(t, i, &keep_), "flow_head"); }
 
   int64_t num_ops(int64_t seg) const { return (int64_t)segs_[seg].size(); }
   std::vector<std::string> op_names(int64_t seg) const {
@@ -643,6 +680,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("copy_channels(Tensor?[] t, int[] i) -> ()", &jr::copy_channels_op);
   m.def("lookup_bwd(Tensor?[] t, int[] i) -> ()", &jr::lookup_bwd_op);
   m.def("im2col(Tensor?[] t, int[] i) -> ()", &jr::im2col_op);
+  m.def("flow_head(Tensor?[] t, int[] i) -> ()", &jr::flow_head_op);
   m.class_<jr::Plan>("Plan")
       .def(torch::init<>())
       .def("set_segment", &jr::Plan::set_segment)
@@ -662,6 +700,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_memset", &jr::Plan::add_memset)
       .def("add_copy", &jr::Plan::add_copy)
       .def("add_copy_channels", &jr::Plan::add_copy_channels)
+      .def("add_flow_head", &jr::Plan::add_flow_head)
       .def("num_ops", &jr::Plan::num_ops)
       .def("op_names", &jr::Plan::op_names)
       .def("run", &jr::Plan::run)

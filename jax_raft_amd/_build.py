@@ -27,6 +27,7 @@ KERNEL_SOURCES = [
     CSRC / "kernels" / "conv_igemm.hip",
     CSRC / "kernels" / "corr.hip",
     CSRC / "kernels" / "elementwise.hip",
+    CSRC / "kernels" / "flowhead.hip",
 ]
 HOST_SOURCES = [CSRC / "runtime" / "binding.cpp"]
 HEADERS = [CSRC / "kernels" / "common.h", CSRC / "kernels" / "kernels.h"]

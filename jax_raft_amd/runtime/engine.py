@@ -125,6 +125,9 @@ class RaftEngine:
             flow-feature convs || lookup + correlation convs; mask head +
             upsampling of iteration i || iteration i+1) so they overlap on
             the GPU (parallel branches of the captured hipGraph).
+        fused_flow_head: run the flow head's output conv + coordinate update as
+            the dedicated flow_head kernel (flowhead.hip) instead of the
+            implicit-GEMM conv with the EPI_FLOW epilogue (measured equal).
         split: run the batch as this many independent half-forwards on
             separate lanes (when the batch divides evenly), so that one
             part's kernels fill the CUs another part's leave idle.
@@ -132,11 +135,13 @@ class RaftEngine:
 
     def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True,
                  corr_dtype: torch.dtype = torch.bfloat16, autotune: bool = True, streams: bool = True,
-                 split: int = 1):
+                 split: int = 1, fused_flow_head: bool = False):
         nat.require()
+        self.fused_flow_head = fused_flow_head
         self.streams = streams
         self.split = split
         self._part_streams: List[torch.cuda.Stream] = []
+        self._fh2_w = self._fh2_b = None
         self.model = model
         self.device = torch.device(device)
         self.use_graph = use_graph
@@ -201,6 +206,16 @@ class RaftEngine:
                 sp.b.copy_(b.float().to(self.device))
             else:
                 self._specs[name] = nat.make_spec(k, b.to(self.device), stride, pad, cin8=cin8, device=self.device)
+        # flow head output conv for the fused flow_head kernel: bf16 [2][9][cin]
+        fh2 = self.model.update_block.flow_head.conv2
+        k = fh2.kernel.detach().float()
+        wf = k.permute(3, 0, 1, 2).reshape(2, 9, k.shape[2]).to(self.device, torch.bfloat16).contiguous()
+        bf = fh2.bias.detach().float().to(self.device).contiguous()
+        if getattr(self, "_fh2_w", None) is None:
+            self._fh2_w, self._fh2_b = wf, bf
+        else:
+            self._fh2_w.copy_(wf)
+            self._fh2_b.copy_(bf)
         self._sig = self._signature()
 
     def _define_specs(self):
@@ -486,8 +501,12 @@ class RaftEngine:
         plan.add_wait(E_MASK)  # previous iteration's mask head has consumed fm / flow32
         self._conv(plan, s1, hx, B, h, w, fm, act=ACT_RELU)
         # flow head conv2 + coordinate update (model.py:505) + flow into hx/qx/flow8
-        self._conv(plan, sp["fh2"], fm, B, h, w, hx, y_coff=self.flow_off, y2=qx, y2_coff=self.flow_off,
-                   y3=flow8, y3_coff=0, coords=coords, flow32=flow32, epi=EPI_FLOW)
+        if self.fused_flow_head and self.fh_hidden in (128, 256):
+            plan.add_flow_head([fm, self._fh2_w, self._fh2_b, coords, flow32, hx, qx, flow8],
+                               [B, h, w, self.fh_hidden, 0, self.flow_off, self.flow_off])
+        else:
+            self._conv(plan, sp["fh2"], fm, B, h, w, hx, y_coff=self.flow_off, y2=qx, y2_coff=self.flow_off,
+                       y3=flow8, y3_coff=0, coords=coords, flow32=flow32, epi=EPI_FLOW)
         plan.add_record(E_FH)
         lane(side2)
         plan.add_wait(E_FH)

@@ -269,3 +269,36 @@ def test_instance_norm_stats_apply(C):
     torch.cuda.synchronize()
     ref2 = torch.relu(R.instance_norm_nhwc(x) + r)
     assert (y2.float().cpu() - ref2).abs().max().item() < 3e-2
+
+
+@pytest.mark.parametrize("cin", [256, 128])
+def test_flow_head_fused(cin):
+    """flow_head (flowhead.hip) = FlowHead.conv2 (3x3, cin -> 2) + coords update + flow copies."""
+    nat = _nat()
+    torch.manual_seed(7)
+    B, h, w = 2, 9, 70          # w not a multiple of the 32-pixel wave segment
+    M = B * h * w
+    fcs, coff = cin + 64, 32    # channel slice of a wider buffer, like the fused fh1+mask1 output
+    fm = torch.randn(B, h, w, fcs) * 0.5
+    k = torch.randn(3, 3, cin, 2) / math.sqrt(9 * cin)
+    b = torch.randn(2) * 0.1
+    coords = torch.randn(M, 2) * 5
+    delta = R.conv2d_nhwc(_bf(fm[..., coff:coff + cin]), _bf(k), b, (1, 1), (1, 1)).reshape(M, 2)
+    new = coords + delta
+    grid = torch.stack(torch.meshgrid(torch.arange(w).float(), torch.arange(h).float(), indexing="xy"), -1)
+    flow_ref = new - grid[None].expand(B, h, w, 2).reshape(M, 2)
+    fmg = fm.reshape(M, fcs).to(DEV, torch.bfloat16).contiguous()
+    cg = coords.to(DEV).contiguous()
+    f32 = torch.zeros(M, 2, device=DEV)
+    hx = torch.zeros(M, 24, device=DEV, dtype=torch.bfloat16)
+    qx = torch.zeros(M, 24, device=DEV, dtype=torch.bfloat16)
+    f8 = torch.zeros(M, 8, device=DEV, dtype=torch.bfloat16)
+    wt = k.permute(3, 0, 1, 2).reshape(2, 9, cin).to(DEV, torch.bfloat16).contiguous()
+    nat.ops().flow_head([fmg, wt, b.to(DEV), cg, f32, hx, qx, f8], [B, h, w, cin, coff, 16, 8])
+    torch.cuda.synchronize()
+    tol = 1e-3 * flow_ref.abs().max().item() + 1e-3
+    assert (cg.cpu() - new).abs().max().item() < tol
+    assert (f32.cpu() - flow_ref).abs().max().item() < tol
+    assert (hx[:, 16:18].float().cpu() - flow_ref).abs().max().item() < 0.02 * flow_ref.abs().max().item() + 1e-2
+    assert torch.equal(hx[:, 16:18], qx[:, 8:10]) and torch.equal(hx[:, 16:18], f8[:, :2])
+    assert (hx[:, :16] == 0).all() and (hx[:, 18:] == 0).all()
