@@ -77,3 +77,27 @@ def test_engine_fp32_pyramid_closer_to_golden():
     mag = ref.norm(dim=-1).mean().item()
     assert _epe(out32[-1], ref[-1]) < 0.05 * mag + 0.05
     assert _epe(out16[-1], ref[-1]) < 0.05 * mag + 0.05
+
+
+def test_input_prefetcher_pipeline_matches_direct():
+    """Overlapped H2D (runtime/pipeline.py) feeds the engine the same inputs as a direct copy."""
+    from jax_raft_amd.runtime.pipeline import InputPrefetcher
+
+    model, _ = raft_small(seed=0)
+    model = model.cuda()
+    g = torch.Generator().manual_seed(3)
+    batches = [((torch.rand(2, 128, 160, 3, generator=g) * 2 - 1).pin_memory(),
+                (torch.rand(2, 128, 160, 3, generator=g) * 2 - 1).pin_memory()) for _ in range(3)]
+    pf = InputPrefetcher([(2, 128, 160, 3), (2, 128, 160, 3)], "cuda")
+    outs = []
+    pf.put(0, batches[0])
+    for i in range(3):
+        a, b = pf.get(i)
+        outs.append(model(a, b, num_flow_updates=3).clone())
+        pf.release(i)
+        if i + 1 < 3:
+            pf.put(i + 1, batches[i + 1])
+    torch.cuda.synchronize()
+    for (x1, x2), o in zip(batches, outs):
+        ref = model(x1.cuda(), x2.cuda(), num_flow_updates=3)
+        assert torch.equal(o, ref)
