@@ -121,16 +121,29 @@ __global__ __launch_bounds__(256) void channel_stats_partial_kernel(const bf16* 
   }
 }
 
-__global__ void channel_stats_final_kernel(const float* __restrict__ part, int N, int nb, int C,
-                                           float* __restrict__ stats) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= N * C * 2) return;
-  const int v = idx & 1;
-  const int c = (idx >> 1) % C;
-  const int n = (idx >> 1) / C;
+// Deterministic final reduction of the per-block partials: block (n, value
+// chunk) = 64 consecutive (channel, sum|sumsq) values x 4 partial-block lanes;
+// each thread sums every 4th partial block (unrolled so several loads are in
+// flight), then the 4 lanes combine through LDS in a fixed order.
+__global__ __launch_bounds__(256) void channel_stats_final_kernel(const float* __restrict__ part, int N, int nb, int C,
+                                                                   float* __restrict__ stats) {
+  __shared__ float red[4][64];
+  const int n = blockIdx.y;
+  const int vi = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lb = threadIdx.x >> 6;
+  const int nv = 2 * C;
   float acc = 0.f;
-  for (int b = 0; b < nb; ++b) acc += part[(((long)n * nb + b) * C + c) * 2 + v];
-  stats[idx] = acc;
+  if (vi < nv) {
+    const float* p = part + (long)n * nb * nv + vi;
+#pragma unroll 8
+    for (int b = lb; b < nb; b += 4) acc += p[(long)b * nv];
+  }
+  red[lb][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (lb == 0 && vi < nv) {
+    const int t = threadIdx.x;
+    stats[(long)n * nv + vi] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+  }
 }
 
 // y = act(xn + rn): 8 channels per thread
@@ -269,8 +282,8 @@ extern "C" int jr_channel_stats(const void* x, int N, int HW, int C, float* stat
   if (C % 8 != 0 || (C / 8) > 256) return (int)hipErrorInvalidValue;
   const int nb = (HW + STATS_ROWS - 1) / STATS_ROWS;
   hipLaunchKernelGGL(channel_stats_partial_kernel, dim3(nb, N), dim3(256), 0, stream, (const bf16*)x, HW, C, partial);
-  hipLaunchKernelGGL(channel_stats_final_kernel, dim3(nblk((long)N * C * 2, 256)), dim3(256), 0, stream, partial, N,
-                     nb, C, stats);
+  hipLaunchKernelGGL(channel_stats_final_kernel, dim3((2 * C + 63) / 64, N), dim3(256), 0, stream, partial, N, nb, C,
+                     stats);
   return (int)hipGetLastError();
 }
 
