@@ -42,8 +42,8 @@ __global__ __launch_bounds__(256) void flow_head_kernel(const bf16* __restrict__
   __shared__ __attribute__((aligned(16))) bf16 tile[3 * TW * RS];
   __shared__ float2 part[3][SEG];
   __shared__ __attribute__((aligned(16))) unsigned wl[2 * 9 * CIN / 2];
-  for (int e = tid; e < 2 * 9 * CIN / 8; e += 256) ((u32x4*)wl)[e] = ((const u32x4*)wt)[e];
   const int tid = threadIdx.x;
+  for (int e = tid; e < 2 * 9 * CIN / 8; e += 256) ((u32x4*)wl)[e] = ((const u32x4*)wt)[e];
   const int lane = tid & 63;
   const int segs = (w + SEG - 1) / SEG;
   const int seg = blockIdx.x % segs;
