@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--sync-h2d", action="store_true", help="copy each step's inputs synchronously (no prefetch overlap)")
     ap.add_argument("--no-streams", action="store_true", help="single-lane plan (no concurrent branches)")
     ap.add_argument("--fused-flow-head", action="store_true", help="dedicated flow_head kernel for the flow head output")
+    ap.add_argument("--final-only", action="store_true",
+                    help="serving mode: upsample/return only the final flow (not the reference's output)")
     ap.add_argument("--split", type=int, default=1, help="independent batch parts (one hipGraph each) run concurrently per GPU")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse >1 rank on fewer GPUs")
@@ -90,17 +92,21 @@ def main():
 
     def forward(a, b):
         return model(a, b, num_flow_updates=args.iters, use_graph=not args.no_graph, streams=not args.no_streams,
-                     split=args.split, fused_flow_head=args.fused_flow_head)
+                     split=args.split, fused_flow_head=args.fused_flow_head, return_all_iters=not args.final_only)
 
-    def run(n):
+    def run(n, events=None):
         if pf is None:
-            for _ in range(n):
+            for i in range(n):
                 out = forward(img1.to(dev, non_blocking=True), img2.to(dev, non_blocking=True))
+                if events is not None:
+                    events[i + 1].record()
             return out
         pf.put(0, [img1, img2])
         for i in range(n):
             a, b = pf.get(i)
             out = forward(a, b)
+            if events is not None:
+                events[i + 1].record()
             pf.release(i)
             if i + 1 < n:
                 pf.put(i + 1, [img1, img2])
@@ -113,14 +119,20 @@ def main():
 
     out = run(args.warmup)
     torch.cuda.synchronize(dev)
-    assert out.shape == (args.iters, B, H, W, 2) and bool(torch.isfinite(out[-1]).all())
+    assert out.shape == (1 if args.final_only else args.iters, B, H, W, 2) and bool(torch.isfinite(out[-1]).all())
 
+    # per-step device timestamps (hipEvents on the compute stream) for the
+    # step-time distribution; the headline uses the host clock around all K steps
+    events = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     barrier()
     t0 = time.perf_counter()
-    out = run(args.steps)
+    events[0].record()
+    out = run(args.steps, events)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     barrier()
+    step_ms = sorted(events[i].elapsed_time(events[i + 1]) for i in range(args.steps))
+    pct = lambda q: round(step_ms[min(len(step_ms) - 1, int(q * len(step_ms)))], 3)
     dt = torch.tensor([t1 - t0], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
     if pg is not None:
         pg.all_reduce(dt, op=pg.ReduceOp.MAX)
@@ -136,9 +148,11 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
+            "step_ms_p50": pct(0.5),
+            "step_ms_p99": pct(0.99),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(pairs_per_s / BASELINE_FPS, 3) if args.arch == "raft_large" and args.iters == 32 else None,
+            "vs_baseline": round(pairs_per_s / BASELINE_FPS, 3) if args.arch == "raft_large" and args.iters == 32 and not args.final_only else None,
             "dtype": "bf16",
             "data": "synthetic (random Sintel-shaped 440x1024 frames, random-init weights; EPE not measurable)",
             "epe_sintel_clean": None,
@@ -149,7 +163,7 @@ def main():
                 "image_size": [H, W],
                 "seq_len": None,
                 "num_flow_updates": args.iters,
-                "outputs": "all iterations upsampled (reference semantics)",
+                "outputs": "final iteration only (serving mode)" if args.final_only else "all iterations upsampled (reference semantics)",
                 "hipgraph": not args.no_graph,
                 "concurrent_branches": not args.no_streams,
                 "batch_parts": args.split,

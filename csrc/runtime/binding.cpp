@@ -16,6 +16,7 @@
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -493,6 +494,11 @@ void flow_head_op(const TList& t, IList i) { run_now(make_flow_head(t, i, nullpt
 // execute concurrently.  A wait on an event not yet recorded during the
 // current enqueue is skipped (e.g. the first iteration's wait on the previous
 // iteration's mask head), which also keeps graph capture self-contained.
+struct RangeGuard {
+  explicit RangeGuard(const char* name) { roctxRangePushA(name); }
+  ~RangeGuard() { roctxRangePop(); }
+};
+
 class Plan : public torch::CustomClassHolder {
  public:
   static constexpr int kMaxLanes = 8;
@@ -639,10 +645,22 @@ class Plan : public torch::CustomClassHolder {
       }
     }
     std::vector<char> recorded(kMaxEvents, 0);
-    for (auto& o : segs_[0]) if (int e = exec_op(o, st, 0, recorded)) return e;
-    for (int it = 0; it < n_iters; ++it)
+    // roctx ranges (visible in rocprofv3 --marker-trace) bracket the host-side
+    // enqueue of each phase: encoders + correlation pyramid, every refinement
+    // iteration, the epilogue.
+    RangeGuard all("raft.plan");
+    {
+      RangeGuard r("raft.prologue");
+      for (auto& o : segs_[0]) if (int e = exec_op(o, st, 0, recorded)) return e;
+    }
+    for (int it = 0; it < n_iters; ++it) {
+      RangeGuard r("raft.iteration");
       for (auto& o : segs_[1]) if (int e = exec_op(o, st, it, recorded)) return e;
-    for (auto& o : segs_[2]) if (int e = exec_op(o, st, n_iters, recorded)) return e;
+    }
+    {
+      RangeGuard r("raft.epilogue");
+      for (auto& o : segs_[2]) if (int e = exec_op(o, st, n_iters, recorded)) return e;
+    }
     for (int l = 1; l < used_lanes_; ++l) {
       if (int r = (int)hipEventRecord(join_[l], st[l])) return r;
       if (int r = (int)hipStreamWaitEvent(s, join_[l], 0)) return r;

@@ -78,7 +78,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
         if force or _stale(obj, src):
             incs = [f"-I{p}" for p in inc] + [f"-I{py_inc}"]
             cmds.append([CXX, *common, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_API_INCLUDE_EXTENSION_H",
-                         *incs, "-c", str(src), "-o", str(obj)])
+                         *incs, "-I/opt/rocm/include", "-c", str(src), "-o", str(obj)])
     if cmds:
         with cf.ThreadPoolExecutor(jobs) as ex:
             for out in ex.map(_run, cmds):
@@ -90,7 +90,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
         link = [
             HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp),
             f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-            f"-Wl,-rpath,{lib}",
+            f"-Wl,-rpath,{lib}", "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib",
         ]
         _run(link)
         os.replace(tmp, SO_PATH)

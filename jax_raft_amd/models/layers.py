@@ -81,18 +81,22 @@ class Conv(nn.Module):
 
 class BatchNorm(nn.Module):
     """Flax ``nn.BatchNorm`` (momentum 0.99, eps 1e-5): params scale/bias,
-    batch_stats mean/var."""
+    batch_stats mean/var.  ``sync_group`` (set by
+    :func:`jax_raft_amd.parallel.dp.convert_sync_batchnorm`) synchronises the
+    training-mode batch statistics across data-parallel ranks."""
 
     def __init__(self, c: int, momentum: float = 0.99, eps: float = 1e-5):
         super().__init__()
         self.momentum, self.eps = momentum, eps
+        self.sync_group = None
         self.scale = nn.Parameter(torch.ones(c))
         self.bias = nn.Parameter(torch.zeros(c))
         self.register_buffer("mean", torch.zeros(c))
         self.register_buffer("var", torch.ones(c))
 
     def forward(self, x, train: bool):
-        y, nm, nv = R.batch_norm_nhwc(x, self.scale, self.bias, self.mean, self.var, train, self.eps, self.momentum)
+        y, nm, nv = R.batch_norm_nhwc(x, self.scale, self.bias, self.mean, self.var, train, self.eps, self.momentum,
+                                      sync_group=self.sync_group)
         if train:
             with torch.no_grad():
                 self.mean.copy_(nm)

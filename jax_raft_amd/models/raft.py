@@ -72,7 +72,11 @@ class RAFT(nn.Module):
     def variables(self) -> Dict[str, Dict[str, Any]]:
         return ckpt.variables_from_module(self)
 
-    def forward(self, image1, image2, train: bool = False, num_flow_updates: int = 12, **engine_kw):
+    def forward(self, image1, image2, train: bool = False, num_flow_updates: int = 12, return_all_iters: bool = True,
+                **engine_kw):
+        """Upsampled flows of every refinement iteration, (num_flow_updates, B, H, W, 2)
+        (reference semantics, ``model.py:605``).  ``return_all_iters=False`` (inference
+        serving mode) upsamples and returns only the final flow, shape (1, B, H, W, 2)."""
         image1, image2 = _as_tensor(image1), _as_tensor(image2)
         B, H, W, _ = image1.shape
         assert (H, W) == tuple(image2.shape[-3:-1]), "input images should have the same shape"
@@ -82,9 +86,11 @@ class RAFT(nn.Module):
             if train or autograd:
                 from ..ops.autograd import raft_forward_autograd
 
-                return raft_forward_autograd(self, image1, image2, train, num_flow_updates)
-            return self.engine(image1.device, **engine_kw).forward(image1, image2, num_flow_updates)
-        return self.forward_reference(image1, image2, train, num_flow_updates)
+                out = raft_forward_autograd(self, image1, image2, train, num_flow_updates)
+                return out if return_all_iters else out[-1:]
+            return self.engine(image1.device, **engine_kw).forward(image1, image2, num_flow_updates,
+                                                                   return_all_iters=return_all_iters)
+        return self.forward_reference(image1, image2, train, num_flow_updates, return_all_iters)
 
     def apply(self, variables: Mapping[str, Any], image1, image2, train: bool = False, num_flow_updates: int = 12,
               mutable=False, **kw):
@@ -103,7 +109,7 @@ class RAFT(nn.Module):
         return out
 
     # ------------------------------------------------------- golden execution
-    def forward_reference(self, image1, image2, train: bool, num_flow_updates: int):
+    def forward_reference(self, image1, image2, train: bool, num_flow_updates: int, return_all_iters: bool = True):
         """Reference-semantics forward (``model.py:557-605`` with the scan body
         ``UpdateCell.__call__``, ``model.py:495-510``)."""
         B, H, W, _ = image1.shape
@@ -123,12 +129,14 @@ class RAFT(nn.Module):
         coords0 = R.make_coords_grid(B, H // 8, W // 8, device=image1.device)
         coords1 = coords0.clone()
         preds = []
-        for _ in range(num_flow_updates):
+        for it in range(num_flow_updates):
             coords1 = coords1.detach()  # stop_gradient, model.py:498
             corr = self.corr_block.index_pyramid(pyramid, coords1)
             flow = coords1 - coords0
             hidden, delta = self.update_block(hidden, context, corr, flow, train)
             coords1 = coords1 + delta
+            if not return_all_iters and it + 1 < num_flow_updates:
+                continue
             up_mask = None if self.mask_predictor is None else self.mask_predictor(hidden, train)
             preds.append(R.upsample_flow(coords1 - coords0, up_mask))
         return torch.stack(preds, dim=0)

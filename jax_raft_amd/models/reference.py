@@ -190,18 +190,35 @@ def batch_norm_nhwc(
     train: bool,
     eps: float = 1e-5,
     momentum: float = 0.99,
+    sync_group=None,
 ):
     """Flax ``nn.BatchNorm`` (defaults: momentum 0.99, eps 1e-5) as used by the
     raft_large context encoder (``model.py:147,157,711``).
 
     Returns ``(y, new_mean, new_var)``; in eval mode the running statistics are
-    used and returned unchanged.
+    used and returned unchanged.  ``sync_group`` (a torch.distributed group, or
+    ``True`` for the default group) makes it a synchronised BatchNorm over the
+    data-parallel ranks (Flax ``axis_name=`` semantics): the batch statistics
+    come from one differentiable all-reduce of (sum x, sum x^2, count) per
+    layer, so every rank normalises with -- and back-propagates through -- the
+    global-batch mean/variance.
     """
     dt = x.dtype
     x = x.float()
     if train:
-        bmean = x.mean(dim=(0, 1, 2))
-        bvar = (x * x).mean(dim=(0, 1, 2)) - bmean * bmean
+        if sync_group is not None and torch.distributed.is_available() and torch.distributed.is_initialized():
+            from torch.distributed.nn.functional import all_reduce as _ar
+
+            n = torch.full((1,), float(x.numel() // x.shape[-1]), device=x.device)
+            packed = torch.cat([x.sum(dim=(0, 1, 2)), (x * x).sum(dim=(0, 1, 2)), n])
+            packed = _ar(packed) if sync_group is True else _ar(packed, group=sync_group)
+            C = x.shape[-1]
+            tot = packed[2 * C]
+            bmean = packed[:C] / tot
+            bvar = packed[C:2 * C] / tot - bmean * bmean
+        else:
+            bmean = x.mean(dim=(0, 1, 2))
+            bvar = (x * x).mean(dim=(0, 1, 2)) - bmean * bmean
         bvar = bvar.clamp_min(0.0)
         new_mean = momentum * mean + (1.0 - momentum) * bmean.detach()
         new_var = momentum * var + (1.0 - momentum) * bvar.detach()

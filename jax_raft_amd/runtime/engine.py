@@ -273,6 +273,7 @@ class RaftEngine:
                 return k, b, (1, 1), (1, 1), None
 
             self._reg("fh1", fh1)
+            self._reg("fh1.flow", conv_src(fh.conv1))  # final-only mode: flow head alone in the loop
             self._reg("mask", conv_src(mp.conv))
         else:
             self._reg("fh1", conv_src(fh.conv1))
@@ -369,7 +370,7 @@ class RaftEngine:
                     x, H, W = y, h_, w_
         return x, H, W
 
-    def _build(self, B: int, H: int, W: int, n_iters: int) -> _PlanState:
+    def _build(self, B: int, H: int, W: int, n_iters: int, all_iters: bool = True) -> _PlanState:
         h, w = H // 8, W // 8
         L = self.num_levels
         min_sz = 2 * (2 ** (L - 1))
@@ -386,10 +387,10 @@ class RaftEngine:
         st = _PlanState(plan=plans[0], plans=plans, n_iters=n_iters)
         st.inp1 = torch.zeros((B, H, W, 3), dtype=F32, device=dev)
         st.inp2 = torch.zeros((B, H, W, 3), dtype=F32, device=dev)
-        st.out = torch.zeros((n_iters, B, H, W, 2), dtype=F32, device=dev)
+        st.out = torch.zeros((n_iters if all_iters else 1, B, H, W, 2), dtype=F32, device=dev)
         lanes = (0, 1, 2) if self.streams else (0, 0, 0)
         for part, plan in enumerate(plans):
-            self._build_part(st, plan, part * nb, nb, H, W, n_iters, f"p{part}.", lanes, 0)
+            self._build_part(st, plan, part * nb, nb, H, W, n_iters, f"p{part}.", lanes, 0, all_iters)
             plan.set_lane(0)
             plan.set_segment(2)
         if parts > 1 and len(self._part_streams) < parts:
@@ -397,9 +398,12 @@ class RaftEngine:
         return st
 
     def _build_part(self, st: _PlanState, plan, b0: int, B: int, H: int, W: int, n_iters: int, pt: str,
-                    lanes: Tuple[int, int, int], ev0: int):
+                    lanes: Tuple[int, int, int], ev0: int, all_iters: bool = True):
         """Lower one forward over images [b0, b0 + B) onto ``plan`` using lanes
-        (main, side, side2) and events ev0 .. ev0 + 5."""
+        (main, side, side2) and events ev0 .. ev0 + 5.  ``all_iters=False`` is the
+        final-only serving mode: the loop runs the flow head alone (no mask head)
+        and the mask head + x8 upsampling run once, in the epilogue segment, on
+        the final hidden state and flow."""
         m = self.model
         dev = self.device
         bufs = st.bufs
@@ -496,9 +500,10 @@ class RaftEngine:
                        epi=EPI_GRU_A)
             self._conv(plan, sp[f"gru{gi}.b"], qx, B, h, w, hx, h32=h32, zbuf=zb, hidden=self.hidden,
                        epi=EPI_GRU_B)
-        s1 = sp["fh1"]
-        fm = alloc("fm", (M, round_up(s1.cout, 8)))
-        plan.add_wait(E_MASK)  # previous iteration's mask head has consumed fm / flow32
+        s1 = sp["fh1"] if (all_iters or not self.has_mask) else sp["fh1.flow"]
+        fm = alloc("fm", (M, round_up(sp["fh1"].cout, 8)))
+        if all_iters:
+            plan.add_wait(E_MASK)  # previous iteration's mask head has consumed fm / flow32
         self._conv(plan, s1, hx, B, h, w, fm, act=ACT_RELU)
         # flow head conv2 + coordinate update (model.py:505) + flow into hx/qx/flow8
         if self.fused_flow_head and self.fh_hidden in (128, 256):
@@ -507,10 +512,16 @@ class RaftEngine:
         else:
             self._conv(plan, sp["fh2"], fm, B, h, w, hx, y_coff=self.flow_off, y2=qx, y2_coff=self.flow_off,
                        y3=flow8, y3_coff=0, coords=coords, flow32=flow32, epi=EPI_FLOW)
-        plan.add_record(E_FH)
-        lane(side2)
-        plan.add_wait(E_FH)
-        stride = st.out.shape[1] * H * W * 2  # one iteration of the full-batch output
+        if all_iters:
+            plan.add_record(E_FH)
+            lane(side2)
+            plan.add_wait(E_FH)
+            stride = st.out.shape[1] * H * W * 2  # one iteration of the full-batch output
+        else:
+            plan.set_segment(2)  # epilogue: upsample the final flow once (out has one iteration)
+            stride = 0
+            if self.has_mask:
+                self._conv(plan, sp["fh1"], hx, B, h, w, fm, act=ACT_RELU)  # mask head input on the final h
         if self.has_mask:
             mask = alloc("mask", (M, 576))
             self._conv(plan, sp["mask"], fm, B, h, w, mask, x_coff=self.fh_hidden,
@@ -518,20 +529,24 @@ class RaftEngine:
             plan.add_upsample_convex([mask, flow32, out], [B, h, w, stride])
         else:
             plan.add_upsample_bilinear([flow32, out], [B, h, w, stride])
-        plan.add_record(E_MASK)
+        if all_iters:
+            plan.add_record(E_MASK)
         lane(main)
 
     # --------------------------------------------------------------- forward
     @torch.no_grad()
-    def forward(self, image1: torch.Tensor, image2: torch.Tensor, num_flow_updates: int = 12) -> torch.Tensor:
+    def forward(self, image1: torch.Tensor, image2: torch.Tensor, num_flow_updates: int = 12,
+                return_all_iters: bool = True) -> torch.Tensor:
+        """All ``num_flow_updates`` upsampled flows (N, B, H, W, 2), as the reference
+        returns; ``return_all_iters=False`` returns only the final one, (1, B, H, W, 2)."""
         if self._signature() != self._sig:
             self._pack()
         B, H, W, C = image1.shape
         assert C == 3, "images must be NHWC with 3 channels"
-        key = (B, H, W, num_flow_updates)
+        key = (B, H, W, num_flow_updates, bool(return_all_iters))
         st = self._states.get(key)
         if st is None:
-            st = self._build(B, H, W, num_flow_updates)
+            st = self._build(B, H, W, num_flow_updates, bool(return_all_iters))
             self._states[key] = st
         st.inp1.copy_(image1)
         st.inp2.copy_(image2)
@@ -557,6 +572,6 @@ class RaftEngine:
         else:
             plan.run(n_iters)
 
-    def op_names(self, B: int, H: int, W: int, n_iters: int):
-        st = self._states.get((B, H, W, n_iters)) or self._build(B, H, W, n_iters)
+    def op_names(self, B: int, H: int, W: int, n_iters: int, return_all_iters: bool = True):
+        st = self._states.get((B, H, W, n_iters, return_all_iters)) or self._build(B, H, W, n_iters, return_all_iters)
         return [st.plan.op_names(s) for s in range(3)]

@@ -51,6 +51,7 @@ class TrainConfig:
     ckpt_every: int = 0
     resume: bool = False
     freeze_bn: bool = False
+    sync_bn: bool = False          # synchronised BatchNorm statistics across DP ranks
     bucket_mb: float = 32.0
 
 
@@ -64,6 +65,8 @@ class Trainer:
         self.model, _ = factory(seed=cfg.seed)
         self.model = self.model.to(self.device).train()
         dp.broadcast_module(self.model)
+        if cfg.sync_bn and self.world > 1:
+            dp.convert_sync_batchnorm(self.model)
         self.sync = dp.GradAllReducer(self.model, bucket_mb=cfg.bucket_mb)
         self.opt = torch.optim.AdamW(self.model.parameters(), lr=cfg.lr, weight_decay=cfg.weight_decay, eps=cfg.eps)
         self.sched = torch.optim.lr_scheduler.OneCycleLR(

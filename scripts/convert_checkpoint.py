@@ -11,11 +11,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from jax_raft_amd.utils.checkpoint import convert_checkpoint  # noqa: E402
+from jax_raft_amd.cli import convert_main  # noqa: E402
 
 if __name__ == "__main__":
-    if len(sys.argv) != 3:
-        print("Usage: python convert_checkpoint.py <input_file> <output_file>")
-        sys.exit(1)
-    assert sys.argv[2].endswith(".msgpack")
-    convert_checkpoint(sys.argv[1], sys.argv[2])
+    sys.exit(convert_main())

@@ -101,3 +101,19 @@ def test_input_prefetcher_pipeline_matches_direct():
     for (x1, x2), o in zip(batches, outs):
         ref = model(x1.cuda(), x2.cuda(), num_flow_updates=3)
         assert torch.equal(o, ref)
+
+
+@pytest.mark.parametrize("factory", [raft_small, raft_large])
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_final_only_mode_equals_last_iteration(factory, use_graph):
+    """return_all_iters=False upsamples once in the plan epilogue: equal to the
+    last of the all-iterations output (same kernels, same order up to the mask head)."""
+    model, _ = factory()
+    model = model.cuda()
+    i1, i2 = _inputs(2, 128, 128, seed=6)
+    i1, i2 = i1.cuda(), i2.cuda()
+    full = model(i1, i2, num_flow_updates=4, use_graph=use_graph)
+    last = model(i1, i2, num_flow_updates=4, use_graph=use_graph, return_all_iters=False)
+    torch.cuda.synchronize()
+    assert last.shape == (1,) + tuple(full.shape[1:])
+    assert (last[0] - full[-1]).abs().max().item() < 1e-4

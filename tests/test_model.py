@@ -86,3 +86,14 @@ def test_deterministic_init():
     kern = fa["feature_encoder.convnormrelu.layers_0.kernel"]
     std = np.sqrt(2.0 / (7 * 7 * 32)) / 0.87962566103423978
     assert kern.abs().max() <= 2 * std + 1e-6
+
+
+def test_final_only_output_cpu():
+    model, variables = raft_small()
+    g = torch.Generator().manual_seed(0)
+    i1 = torch.rand(1, 128, 128, 3, generator=g) * 2 - 1
+    i2 = torch.rand(1, 128, 128, 3, generator=g) * 2 - 1
+    full = model.apply(variables, i1, i2, num_flow_updates=3)
+    last = model.apply(variables, i1, i2, num_flow_updates=3, return_all_iters=False)
+    assert last.shape == (1, 1, 128, 128, 2)
+    assert torch.allclose(last[0], full[-1])

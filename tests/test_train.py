@@ -9,7 +9,7 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from jax_raft_amd import raft_small
+from jax_raft_amd import raft_large, raft_small
 from jax_raft_amd.train.data import SyntheticFlow
 from jax_raft_amd.train.loss import sequence_loss
 from jax_raft_amd.train.trainer import TrainConfig, Trainer
@@ -125,3 +125,46 @@ def test_shard_and_gather_single_process():
     x = torch.arange(8).reshape(4, 2)
     assert torch.equal(dp.shard(x, 1, 2), x[2:])
     assert torch.equal(dp.gather(x), x)
+
+
+def _syncbn_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    from jax_raft_amd.parallel import dp
+
+    r, w, dev = dp.init_distributed(backend="gloo")
+    model, _ = raft_large(seed=0)
+    enc = model.context_encoder.train()
+    assert dp.convert_sync_batchnorm(enc) == 15
+    sync = dp.GradAllReducer(enc, bucket_mb=4.0)
+    x = _batch()[0]
+    y = enc(x[r * 2:(r + 1) * 2], train=True)
+    y.square().mean().backward()
+    sync.finish()
+    if r == 0:
+        state = {"y0": y.detach(), "mean": enc.layer1.layers_0.convnormrelu1.layers_1.mean.clone()}
+        state.update({n: p.grad for n, p in enc.named_parameters()})
+        torch.save(state, out)
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_sync_batchnorm_matches_full_batch_gloo(tmp_path):
+    """SyncBN over 2 gloo ranks (half batch each) == one process on the full
+    batch: same normalised outputs, running stats and averaged gradients."""
+    out = str(tmp_path / "s.pt")
+    mp.spawn(_syncbn_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    st = torch.load(out, weights_only=True)
+    model, _ = raft_large(seed=0)
+    enc = model.context_encoder.train()
+    y = enc(_batch()[0], train=True)
+    y.square().mean().backward()
+    assert torch.allclose(st["y0"], y[:2].detach(), atol=1e-4, rtol=1e-4)
+    assert torch.allclose(st["mean"], enc.layer1.layers_0.convnormrelu1.layers_1.mean, atol=1e-6)
+    # BN amplifies fp32 summation-order noise (sum-of-squares statistics): 1% of
+    # the tensor's max; conv biases feeding a BN have a structurally ~0 gradient
+    gmax = max(p.grad.abs().max().item() for p in enc.parameters())
+    for n, p in enc.named_parameters():
+        a, b = st[n], p.grad
+        assert torch.allclose(a, b, rtol=1e-2, atol=1e-4 * gmax + 1e-2 * b.abs().max().item()), n

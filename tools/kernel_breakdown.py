@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel time breakdown of the timed bench steps from a rocprofv3
-kernel-trace CSV (run bench.py with --no-graph so every launch is traced).
+kernel trace: the ``*_kernel_trace.csv`` or the rocpd SQLite database
+(``*_results.db``, rocprofv3's default output format on ROCm 7).
 Only dispatches after the autotune/warm-up phase are kept: the last
 ``--steps`` forwards are located by their prep_images launches."""
 import argparse
@@ -9,13 +10,24 @@ import csv
 import re
 
 
+def _load(path):
+    if path.endswith(".db"):
+        import sqlite3
+
+        con = sqlite3.connect(path)
+        cur = con.execute("select name, start, end, grid_x, grid_y from kernels")
+        return [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e, "Grid_Size_X": gx, "Grid_Size_Y": gy}
+                for n, s, e, gx, gy in cur]
+    return list(csv.DictReader(open(path)))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--top", type=int, default=30)
     a = ap.parse_args()
-    rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
+    rows = sorted(_load(a.trace), key=lambda r: int(r["Start_Timestamp"]))
     starts = [i for i, r in enumerate(rows) if "prep_images" in r["Kernel_Name"]]
     first = starts[-a.steps]
     rows = rows[first:]
