@@ -44,9 +44,11 @@ def main():
     ap.add_argument("--no-h2d", action="store_true", help="inputs already resident on the GPU")
     ap.add_argument("--sync-h2d", action="store_true", help="copy each step's inputs synchronously (no prefetch overlap)")
     ap.add_argument("--no-streams", action="store_true", help="single-lane plan (no concurrent branches)")
-    ap.add_argument("--fused-flow-head", action="store_true", help="dedicated flow_head kernel for the flow head output")
+    ap.add_argument("--flow-head", default="taps", choices=["taps", "conv", "fused"],
+                    help="flow head output conv: 1x1 GEMM + tap sum (default), 3x3 conv, or the halo-tiled kernel")
     ap.add_argument("--final-only", action="store_true",
                     help="serving mode: upsample/return only the final flow (not the reference's output)")
+    ap.add_argument("--double-buffer", action="store_true", help="parity double-buffering of the flow head outputs")
     ap.add_argument("--split", type=int, default=1, help="independent batch parts (one hipGraph each) run concurrently per GPU")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse >1 rank on fewer GPUs")
@@ -92,7 +94,8 @@ def main():
 
     def forward(a, b):
         return model(a, b, num_flow_updates=args.iters, use_graph=not args.no_graph, streams=not args.no_streams,
-                     split=args.split, fused_flow_head=args.fused_flow_head, return_all_iters=not args.final_only)
+                     split=args.split, flow_head=args.flow_head, return_all_iters=not args.final_only,
+                     double_buffer=args.double_buffer)
 
     def run(n, events=None):
         if pf is None:
@@ -166,6 +169,7 @@ def main():
                 "outputs": "final iteration only (serving mode)" if args.final_only else "all iterations upsampled (reference semantics)",
                 "hipgraph": not args.no_graph,
                 "concurrent_branches": not args.no_streams,
+                "flow_head": args.flow_head,
                 "batch_parts": args.split,
                 "h2d_in_timed_region": not args.no_h2d,
                 "h2d_overlapped": not (args.no_h2d or args.sync_h2d),

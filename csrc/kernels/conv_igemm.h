@@ -1,0 +1,922 @@
+// NHWC implicit-GEMM convolution on gfx950 MFMA (bf16 in, fp32 accumulate):
+// kernel templates shared by the per-family translation units conv_fam_*.hip
+// (split so the tile-config instantiations compile in parallel).
+//
+// Replaces every convolution of the reference RAFT (flax.linen.Conv sites in
+// jax_raft/model.py:101-159 (ConvNormActivation), :238-255 (encoders),
+// :275-290 (MotionEncoder), :304-310 (ConvGRU), :347-349 (FlowHead),
+// :389-394 (MaskPredictor)).  Design (MI355X-first, not a translation):
+//
+//  * "Swapped" GEMM orientation: the MFMA A operand is the packed weight
+//    matrix W[co][k] and the B operand the implicit im2col X[pixel][k].  The
+//    16x16x32 accumulator then holds, per lane, 4 consecutive output channels
+//    of ONE pixel; with the A-row permutation below each lane owns 4*TM
+//    contiguous channels, so the epilogue is pixel-local and vectorised
+//    (16-32 B stores, residual/GRU-state loads as whole vectors).
+//  * K = (kh, kw, cin8) flattened in 8-channel (16 B) chunks, so any kernel
+//    shape (1x1, 3x3, 7x7, 1x5, 5x1, strided) runs through one loader.
+//  * 64-deep K stages, double-buffered LDS, register-staged global loads
+//    issued before the MFMA block of the previous stage (one barrier per
+//    stage).  LDS rows are 128 B with XOR swizzles chosen so that the
+//    ds_read_b128 fragment reads of both operands are bank-conflict free.
+//  * Fused epilogues: bias, residual, activation (incl. the context-encoder
+//    tanh/relu split), scaling, dual stores into concat buffers, and the
+//    ConvGRU gate/blend and flow-head coordinate update of the RAFT loop.
+#pragma once
+#include <type_traits>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int BK = 64;
+
+JR_DEVICE int swzB(int row) { return (row >> 1) & 7; }
+
+template <int NV>
+JR_DEVICE void store_bf16(bf16* dst, const float* v) {
+  if constexpr (NV % 8 == 0) {
+#pragma unroll
+    for (int c = 0; c < NV / 8; ++c) {
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[c * 8 + j]);
+      *(bf16x8*)(dst + c * 8) = o;
+    }
+  } else {
+    static_assert(NV == 4, "NV");
+    bf16x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
+    *(bf16x4*)dst = o;
+  }
+}
+
+template <int NV>
+JR_DEVICE void load_bf16(const bf16* src, float* v) {
+  if constexpr (NV % 8 == 0) {
+#pragma unroll
+    for (int c = 0; c < NV / 8; ++c) {
+      bf16x8 o = *(const bf16x8*)(src + c * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c * 8 + j] = bf2f(o[j]);
+    }
+  } else {
+    bf16x4 o = *(const bf16x4*)src;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = bf2f(o[j]);
+  }
+}
+
+template <int NV>
+JR_DEVICE void store_f32(float* dst, const float* v) {
+#pragma unroll
+  for (int c = 0; c < NV / 4; ++c) *(f32x4*)(dst + 4 * c) = f32x4{v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]};
+}
+
+template <int NV>
+JR_DEVICE void load_f32(const float* src, float* v) {
+#pragma unroll
+  for (int c = 0; c < NV / 4; ++c) {
+    f32x4 o = *(const f32x4*)(src + 4 * c);
+    v[4 * c] = o[0]; v[4 * c + 1] = o[1]; v[4 * c + 2] = o[2]; v[4 * c + 3] = o[3];
+  }
+}
+
+// Output channel base of a lane: storage rows are permuted in 64-row groups so
+// that D row (4*lq + r) of 16-row MFMA tile t maps to channel G + lq*16 + t*4 + r.
+template <int TM>
+JR_DEVICE int chan_base(int wrow0, int lq) {
+  const int G = wrow0 & ~63;
+  const int t0 = (wrow0 & 63) >> 4;
+  return G + lq * 16 + t0 * 4;
+}
+
+// Shared epilogue.  Lane (li, lq) of wave (wco, wp) holds, for each pixel tile
+// tn, NV = 4*TM contiguous output channels starting at cbase (see the weight
+// row permutation in jax_raft_amd/ops/native.py:pack_weight).
+// Per-pixel epilogue: v[NV] holds the raw accumulators of NV contiguous
+// output channels [cbase, cbase + NV) of output pixel m (bias not yet added).
+template <int NV, int EPI>
+JR_DEVICE void epi_pixel(const ConvParams& p, float (&v)[NV], int m, int cbase) {
+  const bool full = cbase + NV <= p.cout;
+  const int OHW = p.OH * p.OW;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] += (cbase + j < p.cout) ? p.bias[cbase + j] : 0.f;
+  if (p.bmap) {
+    const float* bp = p.bmap + (long)m * p.bmap_cstride + p.bmap_coff + cbase;
+    if (full) {
+      float bv[NV];
+      load_f32<NV>(bp, bv);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v[j] += bv[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v[j] += (cbase + j < p.cout) ? bp[j] : 0.f;
+    }
+  }
+  if constexpr (EPI == EPI_STD) {
+    if (p.res) {
+      float rv[NV];
+      const bf16* rp = (const bf16*)p.res + (long)m * p.res_cstride + p.res_coff + cbase;
+      if (full) {
+        load_bf16<NV>(rp, rv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) rv[j] = (cbase + j < p.cout) ? bf2f(rp[j]) : 0.f;
+      }
+      if (p.res_post) {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) v[j] = fmaxf(apply_act(v[j], p.act, cbase + j, p.split) + rv[j], 0.f);
+      } else {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) v[j] = apply_act(v[j] + rv[j], p.act, cbase + j, p.split);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v[j] = apply_act(v[j], p.act, cbase + j, p.split);
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] *= p.alpha;
+    if (p.y_fp32) {
+      float* yp = (float*)p.y + (long)m * p.y_cstride + p.y_coff + cbase;
+      if (full) store_f32<NV>(yp, v);
+      else {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) if (cbase + j < p.cout) yp[j] = v[j];
+      }
+    } else {
+      bf16* yp = (bf16*)p.y + (long)m * p.y_cstride + p.y_coff + cbase;
+      if (full) store_bf16<NV>(yp, v);
+      else {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) if (cbase + j < p.cout) yp[j] = f2bf(v[j]);
+      }
+    }
+    if (p.y2) {
+      bf16* yp = (bf16*)p.y2 + (long)m * p.y2_cstride + p.y2_coff + cbase;
+      if (full) store_bf16<NV>(yp, v);
+      else {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) if (cbase + j < p.cout) yp[j] = f2bf(v[j]);
+      }
+    }
+    if (p.h32) {  // fp32 copy of the channels below `split` (context-encoder hidden state)
+      if (cbase < p.split) {
+        float* hp = p.h32 + (long)m * p.hidden + cbase;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) if (cbase + j < p.split) hp[j] = v[j];
+      }
+    }
+  } else if constexpr (EPI == EPI_GRU_A) {
+    // [z | r] logits -> z (fp32) and r*h (bf16) into the q-input buffer.
+    const int hd = p.hidden;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = sigmoidf_(v[j]);
+    if (cbase < hd) {
+      store_f32<NV>((float*)p.zbuf + (long)m * hd + cbase, v);
+    } else {
+      const int hc = cbase - hd;
+      float h[NV];
+      load_f32<NV>(p.h32 + (long)m * hd + hc, h);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v[j] *= h[j];
+      store_bf16<NV>((bf16*)p.y + (long)m * p.y_cstride + p.y_coff + hc, v);
+    }
+  } else if constexpr (EPI == EPI_GRU_B) {
+    const int hd = p.hidden;
+    float z[NV], h[NV];
+    load_f32<NV>((const float*)p.zbuf + (long)m * hd + cbase, z);
+    float* hp = p.h32 + (long)m * hd + cbase;
+    load_f32<NV>(hp, h);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const float q = tanhf_(v[j]);
+      v[j] = (1.0f - z[j]) * h[j] + z[j] * q;
+    }
+    store_f32<NV>(hp, v);
+    store_bf16<NV>((bf16*)p.y + (long)m * p.y_cstride + p.y_coff + cbase, v);
+    if (p.y2) store_bf16<NV>((bf16*)p.y2 + (long)m * p.y2_cstride + p.y2_coff + cbase, v);
+  } else if constexpr (EPI == EPI_FLOW) {
+    if (cbase == 0) {
+      const int rem = m % OHW;
+      const int py = rem / p.OW;
+      const int px = rem - py * p.OW;
+      const float cx = p.coords[2 * (long)m] + v[0];
+      const float cy = p.coords[2 * (long)m + 1] + v[1];
+      p.coords[2 * (long)m] = cx;
+      p.coords[2 * (long)m + 1] = cy;
+      const float fx = cx - (float)px;
+      const float fy = cy - (float)py;
+      p.flow32[2 * (long)m] = fx;
+      p.flow32[2 * (long)m + 1] = fy;
+      bf16* yp = (bf16*)p.y + (long)m * p.y_cstride + p.y_coff;
+      yp[0] = f2bf(fx); yp[1] = f2bf(fy);
+      if (p.y2) {
+        bf16* y2p = (bf16*)p.y2 + (long)m * p.y2_cstride + p.y2_coff;
+        y2p[0] = f2bf(fx); y2p[1] = f2bf(fy);
+      }
+      if (p.y3) {
+        bf16* y3p = (bf16*)p.y3 + (long)m * p.y3_cstride + p.y3_coff;
+        y3p[0] = f2bf(fx); y3p[1] = f2bf(fy);
+      }
+    }
+  }
+}
+
+// Epilogue of the 16x16x32 kernels.  Lane (li, lq) of a wave whose first
+// storage row is wrow0 holds, for each pixel tile tn and each 64-row group g
+// the wave covers, 4*min(TM,4) contiguous output channels starting at
+// chan_base(wrow0 + 64 g) (see the weight row permutation in
+// jax_raft_amd/ops/native.py:pack_weight).
+template <int I, int N, typename F>
+JR_DEVICE void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+template <int TM, int TN, int EPI>
+JR_DEVICE void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM][TN], int mbase, int wrow0, int lq, int li) {
+  constexpr int TG = TM > 4 ? 4 : TM;   // 16-row tiles per 64-row permutation group
+  static_assert(TM % TG == 0, "TM");
+  constexpr int NV = 4 * TG;
+  // compile-time loops: a large epilogue body defeats `#pragma unroll`, and a
+  // runtime index into acc[][] would move the accumulators to scratch
+  static_for<0, TM / TG>([&](auto gc) {
+    constexpr int g = decltype(gc)::value;
+    const int cbase = chan_base<TG>(wrow0 + 64 * g, lq);
+    if (cbase >= p.cout) return;
+    static_for<0, TN>([&](auto tc) {
+      constexpr int tn = decltype(tc)::value;
+      const int m = mbase + tn * 16 + li;
+      if (m >= p.M) return;
+      float v[NV];
+#pragma unroll
+      for (int tm = 0; tm < TG; ++tm)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[tm * 4 + r] = acc[g * TG + tm][tn][r];
+      epi_pixel<NV, EPI>(p, v, m, cbase);
+    });
+  });
+}
+
+// Per-row state of the FAST im2col loader (ConvParams::fast): the byte offset
+// of the row's first tap + this lane's 16-B chunk, and a bitmask of the taps
+// (kh * KW + kw) that fall inside the input.  A stage's tap and channel block
+// are wave-uniform, so a stage costs per row one bit test, one add and one
+// select.
+struct FastRow {
+  unsigned off;
+  unsigned mask;
+};
+
+JR_DEVICE FastRow fast_row(const ConvParams& p, int ih0, int iw0, unsigned rbase, bool valid, int ch,
+                           unsigned xrow_bytes) {
+  FastRow r{0u, 0u};
+  if (!valid) return r;
+  r.off = rbase + (unsigned)(ih0 * p.W + iw0) * xrow_bytes + (unsigned)ch * 16u;  // may wrap; only used when a tap is valid
+  for (int kh = 0; kh < p.KH; ++kh) {
+    if ((unsigned)(ih0 + kh) >= (unsigned)p.H) continue;
+    for (int kw = 0; kw < p.KW; ++kw)
+      if ((unsigned)(iw0 + kw) < (unsigned)p.W) r.mask |= 1u << (kh * p.KW + kw);
+  }
+  return r;
+}
+
+// Wave-uniform stage state of the FAST loader.
+struct FastStage {
+  int tap = 0, kh = 0, kw = 0, cb = 0;
+  JR_DEVICE void advance(const ConvParams& p, int cpb) {
+    if (++cb == cpb) {
+      cb = 0;
+      ++tap;
+      if (++kw == p.KW) { kw = 0; ++kh; }
+    }
+  }
+};
+
+template <int BCO, int BP, int WCO, int EPI, bool FAST, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(const ConvParams p) {
+  constexpr int WP = NW / WCO;
+  constexpr int RP = NW * 8;              // staging rows covered by one pass of the block (8 lanes per row)
+  constexpr int WTCO = BCO / WCO;
+  constexpr int WTP = BP / WP;
+  constexpr int TM = WTCO / 16;
+  constexpr int TN = WTP / 16;
+  constexpr int NV = 4 * TM;              // contiguous channels per lane
+  constexpr int XR = BP / RP;             // X rows loaded per thread
+  constexpr int WR = BCO >= RP ? BCO / RP : 1;
+  constexpr int A_ELEMS = BCO * BK;
+  constexpr int B_ELEMS = BP * BK;
+  constexpr unsigned OOB = 0x80000000u;   // buffer offset past num_records -> hardware returns 0
+  static_assert(TM >= 1 && TN >= 1 && WCO * WP == NW && XR >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (A_ELEMS + B_ELEMS)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wco = wave % WCO;
+  const int wp = wave / WCO;
+  const int p0 = blockIdx.x * BP;
+  const int co0 = blockIdx.y * BCO;
+  const int ch = tid & 7;
+  const int OHW = p.OH * p.OW;
+
+  // Buffer resources: out-of-range offsets (padding taps, tail rows, K tail)
+  // read as zero with no branch and no exec masking.
+  const __amdgpu_buffer_rsrc_t xsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)p.w_bytes, 0x00020000);
+
+  // Per-thread im2col row descriptors (fixed across the K loop); byte offsets.
+  int ih0[XR], iw0[XR];
+  unsigned rbase[XR];
+#pragma unroll
+  for (int i = 0; i < XR; ++i) {
+    const int m = p0 + (tid >> 3) + RP * i;
+    if (m < p.M) {
+      const int n = m / OHW;
+      const int rem = m - n * OHW;
+      const int oh = rem / p.OW;
+      const int ow = rem - oh * p.OW;
+      ih0[i] = oh * p.SH - p.PH;
+      iw0[i] = ow * p.SW - p.PW;
+      rbase[i] = (unsigned)(((long)n * p.H * p.W * p.x_cstride + p.x_coff) * 2);
+    } else {
+      ih0[i] = -(1 << 28);
+      iw0[i] = -(1 << 28);
+      rbase[i] = 0;
+    }
+  }
+  const unsigned wrow_off = (unsigned)((co0 + (tid >> 3)) * p.kpad * 2 + ch * 16);
+  const unsigned wrow_lim = (unsigned)(p.cout_pad - co0 - (tid >> 3));  // rows i*RP < lim are valid
+
+  // K-chunk state of the NEXT stage to load: kc = ks*8 + ch.
+  const int cpt = p.cin8 >> 3;
+  int tap = ch / cpt;
+  int cc = ch - tap * cpt;
+  int kh = tap / p.KW;
+  int kw = tap - kh * p.KW;
+  int ks_next = 0;
+  const unsigned xrow_bytes = (unsigned)p.x_cstride * 2;
+  [[maybe_unused]] FastRow frow[XR];
+  [[maybe_unused]] FastStage fst;
+  [[maybe_unused]] const int cpb = (p.KH * p.KW == 1) ? (p.kpad / BK) : (p.cin8 >> 6);
+  if constexpr (FAST) {
+#pragma unroll
+    for (int i = 0; i < XR; ++i) frow[i] = fast_row(p, ih0[i], iw0[i], rbase[i], ih0[i] > -(1 << 27), ch, xrow_bytes);
+  }
+
+  struct Regs { u32x4 x[XR]; u32x4 w[WR]; };
+  Regs ra, rb;
+
+  auto issue = [&](Regs& r) {
+    if constexpr (FAST) {
+      const bool kin = ks_next * BK < p.kpad;
+      const bool cv = kin && ch * 8 < p.cin8 - fst.cb * 64;   // channel tail of a 1x1 conv
+      const unsigned soff = (unsigned)(fst.kh * p.W + fst.kw) * xrow_bytes + (unsigned)fst.cb * 128u;
+#pragma unroll
+      for (int i = 0; i < XR; ++i) {
+        const bool ok = cv && ((frow[i].mask >> (fst.tap & 31)) & 1u);
+        r.x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xsrd, ok ? frow[i].off + soff : OOB, 0, 0));
+      }
+      fst.advance(p, cpb);
+    } else {
+    const bool kvalid = kh < p.KH;
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      const int ihl = ih0[i] + kh, iwl = iw0[i] + kw;  // coordinates in the (dilated) input
+      const int ih = ihl >> p.dsh, iw = iwl >> p.dsw;
+      const bool ok = kvalid && ((ihl & ((1 << p.dsh) - 1)) | (iwl & ((1 << p.dsw) - 1))) == 0 &&
+                  (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      const unsigned off = rbase[i] + (unsigned)(ih * p.W + iw) * xrow_bytes + (unsigned)cc * 16u;
+      r.x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xsrd, ok ? off : OOB, 0, 0));
+    }
+    }
+    const unsigned kofs = (unsigned)ks_next * (BK * 2);
+#pragma unroll
+    for (int i = 0; i < WR; ++i) {
+      const bool ok = ((BCO >= RP) || (tid < BCO * 8)) && (unsigned)(RP * i) < wrow_lim && ks_next * BK < p.kpad;
+      const unsigned off = wrow_off + (unsigned)(RP * i) * (unsigned)p.kpad * 2u + kofs;
+      r.w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wsrd, ok ? off : OOB, 0, 0));
+    }
+    // advance the chunk state to the following stage
+    ++ks_next;
+    if constexpr (!FAST) {
+      cc += 8;
+      while (cc >= cpt) {
+        cc -= cpt;
+        if (++kw == p.KW) { kw = 0; ++kh; }
+      }
+    }
+  };
+  auto store = [&](const Regs& r, int buf) {
+    bf16* sA = smem + buf * (A_ELEMS + B_ELEMS);
+    bf16* sB = sA + A_ELEMS;
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      const int rr = (tid >> 3) + RP * i;
+      *(u32x4*)(sB + rr * BK + ((ch ^ swzB(rr)) << 3)) = r.x[i];
+    }
+#pragma unroll
+    for (int i = 0; i < WR; ++i) {
+      const int rr = (tid >> 3) + RP * i;
+      if ((BCO >= RP) || (tid < BCO * 8)) *(u32x4*)(sA + rr * BK + ((ch ^ swzB(rr)) << 3)) = r.w[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int li = lane & 15;
+  const int lq = lane >> 4;
+  auto compute = [&](int buf) {
+    const bf16* sA = smem + buf * (A_ELEMS + B_ELEMS);
+    const bf16* sB = sA + A_ELEMS;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + lq;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int row = wco * WTCO + tm * 16 + li;
+        af[tm] = *(const bf16x8*)(sA + row * BK + ((chunk ^ swzB(row)) << 3));
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int row = wp * WTP + tn * 16 + li;
+        bfr[tn] = *(const bf16x8*)(sB + row * BK + ((chunk ^ swzB(row)) << 3));
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tm], bfr[tn], acc[tm][tn], 0, 0, 0);
+    }
+  };
+
+  // Software pipeline: global loads run two K-stages ahead of the MFMAs
+  // (register sets ra/rb alternate, LDS double-buffered, one barrier per
+  // stage).  Loads past the end of K are issued with OOB offsets (zeros),
+  // keeping the loop body branch-free so hipcc emits counted vmcnt waits.
+  const int nks = p.kpad / BK;
+  issue(ra);
+  issue(rb);
+  store(ra, 0);
+  __syncthreads();
+  const int npairs = nks >> 1;
+  for (int it = 0; it < npairs; ++it) {
+    issue(ra);          // stage 2it+2
+    compute(0);         // stage 2it
+    store(rb, 1);       // stage 2it+1 (loaded one stage ago)
+    __syncthreads();
+    issue(rb);          // stage 2it+3
+    compute(1);         // stage 2it+1
+    store(ra, 0);       // stage 2it+2
+    __syncthreads();
+  }
+  if (nks & 1) compute(0);
+
+  const int wrow0 = co0 + wco * WTCO;
+  conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, wrow0, lq, li);
+}
+
+// ---------------------------------------------------------------------------
+// Kernel M32: as kernel R (register-staged operands, 64-deep K stages,
+// 2-stage prefetch) but on v_mfma_f32_32x32x16_bf16: half the MFMA
+// instructions (and MFMA issue-blocking cycles) per FLOP of the 16x16x32
+// form, the loop being issue-bound.  The 32x32 accumulator gives lane
+// (col = pixel, h = lane>>5) the D rows (r&3) + 8(r>>2) + 4h; the A-operand LDS
+// rows are read in the permuted order below so that those 16 rows are the 16
+// contiguous output channels 32t + 16h + r of the wave's 64-channel group
+// (stored permuted per pack_weight), keeping the epilogue vectorised.
+// ---------------------------------------------------------------------------
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// storage row (within a 64-row group) holding channel 32t + c(rho), c(rho) = 16((rho>>2)&1) + (rho&3) + 4(rho>>3)
+JR_DEVICE int m32_arow(int t, int rho) { return 16 * (rho >> 3) + 4 * (2 * t + ((rho >> 2) & 1)) + (rho & 3); }
+
+template <int BCO, int BP, int WCO, int EPI, bool FAST, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void conv_m32_kernel(const ConvParams p) {
+  constexpr int WP = NW / WCO;
+  constexpr int RP = NW * 8;   // staging rows per block pass
+  constexpr int WTCO = BCO / WCO;
+  constexpr int WTP = BP / WP;
+  constexpr int TM = WTCO / 32;
+  constexpr int TN = WTP / 32;
+  constexpr int XR = BP / RP;
+  constexpr int WR = BCO >= RP ? BCO / RP : 1;
+  constexpr int A_ELEMS = BCO * BK;
+  constexpr int B_ELEMS = BP * BK;
+  constexpr unsigned OOB = 0x80000000u;
+  static_assert(TM >= 1 && TN >= 1 && WCO * WP == NW && BCO >= RP && XR >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (A_ELEMS + B_ELEMS)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wco = wave % WCO;
+  const int wp = wave / WCO;
+  const int p0 = blockIdx.x * BP;
+  const int co0 = blockIdx.y * BCO;
+  const int ch = tid & 7;
+  const int OHW = p.OH * p.OW;
+
+  const __amdgpu_buffer_rsrc_t xsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)p.w_bytes, 0x00020000);
+
+  int ih0[XR], iw0[XR];
+  unsigned rbase[XR];
+#pragma unroll
+  for (int i = 0; i < XR; ++i) {
+    const int m = p0 + (tid >> 3) + RP * i;
+    if (m < p.M) {
+      const int n = m / OHW;
+      const int rem = m - n * OHW;
+      const int oh = rem / p.OW;
+      const int ow = rem - oh * p.OW;
+      ih0[i] = oh * p.SH - p.PH;
+      iw0[i] = ow * p.SW - p.PW;
+      rbase[i] = (unsigned)(((long)n * p.H * p.W * p.x_cstride + p.x_coff) * 2);
+    } else {
+      ih0[i] = -(1 << 28);
+      iw0[i] = -(1 << 28);
+      rbase[i] = 0;
+    }
+  }
+  const unsigned wrow_off = (unsigned)((co0 + (tid >> 3)) * p.kpad * 2 + ch * 16);
+  const unsigned wrow_lim = (unsigned)(p.cout_pad - co0 - (tid >> 3));
+  const int cpt = p.cin8 >> 3;
+  int tap = ch / cpt;
+  int cc = ch - tap * cpt;
+  int kh = tap / p.KW;
+  int kw = tap - kh * p.KW;
+  int ks_next = 0;
+  const unsigned xrow_bytes = (unsigned)p.x_cstride * 2;
+  [[maybe_unused]] FastRow frow[XR];
+  [[maybe_unused]] FastStage fst;
+  [[maybe_unused]] const int cpb = (p.KH * p.KW == 1) ? (p.kpad / BK) : (p.cin8 >> 6);
+  if constexpr (FAST) {
+#pragma unroll
+    for (int i = 0; i < XR; ++i) frow[i] = fast_row(p, ih0[i], iw0[i], rbase[i], ih0[i] > -(1 << 27), ch, xrow_bytes);
+  }
+
+  struct Regs { u32x4 x[XR]; u32x4 w[WR]; };
+  Regs ra, rb;
+
+  auto issue = [&](Regs& r) {
+    if constexpr (FAST) {
+      const bool kin = ks_next * BK < p.kpad;
+      const bool cv = kin && ch * 8 < p.cin8 - fst.cb * 64;   // channel tail of a 1x1 conv
+      const unsigned soff = (unsigned)(fst.kh * p.W + fst.kw) * xrow_bytes + (unsigned)fst.cb * 128u;
+#pragma unroll
+      for (int i = 0; i < XR; ++i) {
+        const bool ok = cv && ((frow[i].mask >> (fst.tap & 31)) & 1u);
+        r.x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xsrd, ok ? frow[i].off + soff : OOB, 0, 0));
+      }
+      fst.advance(p, cpb);
+    } else {
+    const bool kvalid = kh < p.KH;
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      const int ihl = ih0[i] + kh, iwl = iw0[i] + kw;
+      const int ih = ihl >> p.dsh, iw = iwl >> p.dsw;
+      const bool ok = kvalid && ((ihl & ((1 << p.dsh) - 1)) | (iwl & ((1 << p.dsw) - 1))) == 0 &&
+                      (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      const unsigned off = rbase[i] + (unsigned)(ih * p.W + iw) * xrow_bytes + (unsigned)cc * 16u;
+      r.x[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xsrd, ok ? off : OOB, 0, 0));
+    }
+    }
+    const unsigned kofs = (unsigned)ks_next * (BK * 2);
+#pragma unroll
+    for (int i = 0; i < WR; ++i) {
+      const bool ok = (unsigned)(RP * i) < wrow_lim && ks_next * BK < p.kpad;
+      const unsigned off = wrow_off + (unsigned)(RP * i) * (unsigned)p.kpad * 2u + kofs;
+      r.w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wsrd, ok ? off : OOB, 0, 0));
+    }
+    ++ks_next;
+    if constexpr (!FAST) {
+      cc += 8;
+      while (cc >= cpt) {
+        cc -= cpt;
+        if (++kw == p.KW) { kw = 0; ++kh; }
+      }
+    }
+  };
+  auto store = [&](const Regs& r, int buf) {
+    bf16* sA = smem + buf * (A_ELEMS + B_ELEMS);
+    bf16* sB = sA + A_ELEMS;
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      const int rr = (tid >> 3) + RP * i;
+      *(u32x4*)(sB + rr * BK + ((ch ^ swzB(rr)) << 3)) = r.x[i];
+    }
+#pragma unroll
+    for (int i = 0; i < WR; ++i) {
+      const int rr = (tid >> 3) + RP * i;
+      *(u32x4*)(sA + rr * BK + ((ch ^ swzB(rr)) << 3)) = r.w[i];
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int rho = lane & 31;
+  const int hh = lane >> 5;
+  const int wbase = wco * WTCO;               // wave's first storage row in the block
+  const int tabs0 = ((co0 + wbase) & 63) >> 5;  // 32-row half of the 64-row group
+  const int gbase = wbase - ((co0 + wbase) & 63);  // block-relative start of that 64-row group
+  auto compute = [&](int buf) {
+    const bf16* sA = smem + buf * (A_ELEMS + B_ELEMS);
+    const bf16* sB = sA + A_ELEMS;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int chunk = kk * 2 + hh;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int row = gbase + 64 * ((tabs0 + tm) >> 1) + m32_arow((tabs0 + tm) & 1, rho);  // 128-row wave tiles span two groups
+        af[tm] = *(const bf16x8*)(sA + row * BK + ((chunk ^ swzB(row)) << 3));
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int row = wp * WTP + tn * 32 + rho;
+        bfr[tn] = *(const bf16x8*)(sB + row * BK + ((chunk ^ swzB(row)) << 3));
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm], bfr[tn], acc[tm][tn], 0, 0, 0);
+    }
+  };
+
+  const int nks = p.kpad / BK;
+  issue(ra);
+  issue(rb);
+  store(ra, 0);
+  __syncthreads();
+  const int npairs = nks >> 1;
+  for (int it = 0; it < npairs; ++it) {
+    issue(ra);
+    compute(0);
+    store(rb, 1);
+    __syncthreads();
+    issue(rb);
+    compute(1);
+    store(ra, 0);
+    __syncthreads();
+  }
+  if (nks & 1) compute(0);
+
+  // epilogue: tile tm of lane hh -> channels G + 32*(tabs0+tm) + 16*hh + [0,16)
+  const int G = (co0 + wbase) & ~63;
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int cbase = G + 32 * (tabs0 + tm) + 16 * hh;
+    if (cbase >= p.cout) continue;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int m = p0 + wp * WTP + tn * 32 + rho;
+      if (m >= p.M) continue;
+      float v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = acc[tm][tn][r];
+      epi_pixel<16, EPI>(p, v, m, cbase);
+    }
+  }
+}
+
+// LDS-DMA helpers (kernel D2)
+// One 16-B-per-lane LDS-DMA (buffer_load_dwordx4 ... lds): lane i lands at lds + 16*i.
+JR_DEVICE void dma16(__amdgpu_buffer_rsrc_t r, bf16* lds, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+}
+
+template <int N>
+JR_DEVICE void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+JR_DEVICE void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
+// Kernel D2: LDS-DMA staging at BK = 64 with an NS-deep ring.
+//
+// A stage is (BCO + BP) LDS rows of 128 B (64 bf16 of K): the weight tile then
+// the im2col pixel tile.  It is filled by 1-KiB LDS-DMA pieces
+// (`buffer_load_dwordx4 ... lds`, lane i -> piece base + 16 i) of 8 whole
+// rows, (BCO + BP) / 32 pieces per wave, so every wave issues the same count
+// and the ring waits are exact counted `vmcnt`s with raw barriers: stage
+// ks + NS - 1 is in flight while stage ks feeds the MFMAs.  Row r keeps
+// 16-B chunk c at slot c ^ (r & 6).  That swizzle depends only on the row
+// inside a piece, so each DMA lane fetches one FIXED chunk
+// ((lane & 7) ^ ((lane >> 3) & 6)) for every piece and stage (one im2col K
+// state per lane, as in kernel R), and the ds_read_b128 fragment reads are
+// bank-conflict free under the hardware's lane grouping
+// {0-3,12-15,20-27}, {4-11,16-19,28-31}, ... (rows li and li^4.. of a group
+// land on distinct (row parity, slot) pairs).  No staging VGPRs and no
+// ds_write traffic: the LDS array only serves the fragment reads.
+// ---------------------------------------------------------------------------
+template <int BCO, int BP, int WCO, int NS, int EPI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, (BCO + BP) * NS * 128 > 81920 ? 1 : 2))) void conv_d2_kernel(const ConvParams p) {
+  constexpr int WP = 4 / WCO;
+  constexpr int WTCO = BCO / WCO;
+  constexpr int WTP = BP / WP;
+  constexpr int TM = WTCO / 16;
+  constexpr int TN = WTP / 16;
+  constexpr int ROWS = BCO + BP;
+  constexpr int PPW = ROWS / 32;                   // 8-row pieces per wave per stage
+  constexpr int STAGE = ROWS * BK;                 // bf16 elements
+  constexpr unsigned OOB = 0x80000000u;
+  static_assert(TM >= 1 && TN >= 1 && WCO * WP == 4 && ROWS % 32 == 0, "tile");
+  static_assert(NS >= 2 && NS <= 4, "ring depth");
+  __shared__ __attribute__((aligned(16))) bf16 smem[NS * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wco = wave % WCO;
+  const int wp = wave / WCO;
+  const int p0 = blockIdx.x * BP;
+  const int co0 = blockIdx.y * BCO;
+  const int OHW = p.OH * p.OW;
+  const int cl = (lane & 7) ^ ((lane >> 3) & 6);   // this lane's fixed logical chunk in a stage
+
+  const __amdgpu_buffer_rsrc_t xsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)p.w_bytes, 0x00020000);
+
+  // piece j of this wave covers stage rows q*8 .. q*8+7, q = wave*PPW + j:
+  // rows < BCO are weight rows, the rest pixel rows.  Per-lane row = q*8 + lane/8.
+  int ih0[PPW], iw0[PPW];
+  unsigned rbase[PPW];
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) {
+    const int row = (wave * PPW + j) * 8 + (lane >> 3);
+    if (row < BCO) {
+      // weight row: rbase = byte offset of (row, chunk cl); ih0 flags validity
+      const int wr = co0 + row;
+      rbase[j] = (unsigned)(wr * p.kpad * 2 + cl * 16);
+      ih0[j] = wr < p.cout_pad ? 0 : -1;
+      iw0[j] = 0;
+    } else {
+      const int m = p0 + row - BCO;
+      if (m < p.M) {
+        const int n = m / OHW;
+        const int rem = m - n * OHW;
+        const int oh = rem / p.OW;
+        const int ow = rem - oh * p.OW;
+        ih0[j] = oh * p.SH - p.PH;
+        iw0[j] = ow * p.SW - p.PW;
+        rbase[j] = (unsigned)(((long)n * p.H * p.W * p.x_cstride + p.x_coff) * 2);
+      } else {
+        ih0[j] = -(1 << 28);
+        iw0[j] = -(1 << 28);
+        rbase[j] = 0;
+      }
+    }
+  }
+
+  // im2col K state of the next stage to issue: global chunk kc = ks*8 + cl
+  const int cpt = p.cin8 >> 3;
+  int tap = cl / cpt;
+  int cc = cl - tap * cpt;
+  int kh = tap / p.KW;
+  int kw = tap - kh * p.KW;
+  int ks_next = 0;
+  const unsigned xrow_bytes = (unsigned)p.x_cstride * 2;
+  const int nks = p.kpad / BK;
+
+  auto issue = [&]() {
+    bf16* st = smem + (ks_next % NS) * STAGE;
+    const bool kvalid = kh < p.KH;
+    const bool kin = ks_next < nks;
+    const unsigned kofs = (unsigned)ks_next * (BK * 2);
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int q = wave * PPW + j;               // wave-uniform
+      bf16* dst = st + q * 8 * BK;
+      if (q * 8 < BCO) {
+        dma16(wsrd, dst, (kin && ih0[j] == 0) ? rbase[j] + kofs : OOB);
+      } else {
+        const int ihl = ih0[j] + kh, iwl = iw0[j] + kw;  // coordinates in the (dilated) input
+        const int ih = ihl >> p.dsh, iw = iwl >> p.dsw;
+        const bool ok = kvalid && ((ihl & ((1 << p.dsh) - 1)) | (iwl & ((1 << p.dsw) - 1))) == 0 &&
+                        (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        const unsigned off = rbase[j] + (unsigned)(ih * p.W + iw) * xrow_bytes + (unsigned)cc * 16u;
+        dma16(xsrd, dst, ok ? off : OOB);
+      }
+    }
+    ++ks_next;
+    cc += 8;
+    while (cc >= cpt) {
+      cc -= cpt;
+      if (++kw == p.KW) { kw = 0; ++kh; }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int li = lane & 15;
+  const int lq = lane >> 4;
+  auto compute = [&](int buf) {
+    const bf16* sA = smem + buf * STAGE;
+    const bf16* sB = sA + BCO * BK;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + lq;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int row = wco * WTCO + tm * 16 + li;
+        af[tm] = *(const bf16x8*)(sA + row * BK + ((chunk ^ (row & 6)) << 3));
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int row = wp * WTP + tn * 16 + li;
+        bfr[tn] = *(const bf16x8*)(sB + row * BK + ((chunk ^ (row & 6)) << 3));
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tm], bfr[tn], acc[tm][tn], 0, 0, 0);
+    }
+  };
+
+  // prologue: stages 0 .. NS-2 in flight; wait for stage 0
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) issue();
+  wait_vmcnt<(NS - 2) * PPW>();
+  raw_barrier();
+  for (int ks = 0; ks < nks; ++ks) {
+    issue();                      // stage ks+NS-1 into the buffer stage ks-1 used
+    compute(ks % NS);             // stage ks
+    wait_vmcnt<(NS - 2) * PPW>(); // stage ks+1 has landed (stages ks+2.. may still fly)
+    raw_barrier();
+  }
+  wait_vmcnt<0>();
+
+  const int wrow0 = co0 + wco * WTCO;
+  conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, wrow0, lq, li);
+}
+
+template <int BCO, int BP, int WCO, int KIND>
+int launch_cfg(const ConvParams* p, int epi, hipStream_t s) {
+  // storage rows are permuted inside 64-row groups: cover every group that holds a real channel
+  const int rows = (p->cout + 63) / 64 * 64;
+  dim3 grid((p->M + BP - 1) / BP, (rows + BCO - 1) / BCO);
+  dim3 block(256);
+#define JR_LAUNCH(E)                                                                          \
+  if constexpr (KIND == 6 || KIND == 7) {                                                     \
+    constexpr int NW_ = KIND == 6 ? 8 : 16;                                                    \
+    if (p->fast) hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, true, NW_>), grid, dim3(NW_ * 64), 0, s, *p); \
+    else hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, false, NW_>), grid, dim3(NW_ * 64), 0, s, *p);         \
+  } else if constexpr (KIND == 3 || KIND == 4) hipLaunchKernelGGL((conv_d2_kernel<BCO, BP, WCO, KIND - 1, E>), grid, block, 0, s, *p); \
+  else if constexpr (KIND == 2) {                                                              \
+    if (p->fast) hipLaunchKernelGGL((conv_m32_kernel<BCO, BP, WCO, E, true>), grid, block, 0, s, *p); \
+    else hipLaunchKernelGGL((conv_m32_kernel<BCO, BP, WCO, E, false>), grid, block, 0, s, *p);         \
+  } else if constexpr (KIND == 8) {                                                            \
+    if (p->fast) hipLaunchKernelGGL((conv_m32_kernel<BCO, BP, WCO, E, true, 8>), grid, dim3(512), 0, s, *p); \
+    else hipLaunchKernelGGL((conv_m32_kernel<BCO, BP, WCO, E, false, 8>), grid, dim3(512), 0, s, *p);         \
+  } else {                                                                                     \
+    if (p->fast) hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, true>), grid, block, 0, s, *p); \
+    else hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, false>), grid, block, 0, s, *p);         \
+  }
+  switch (epi) {
+    case EPI_STD: JR_LAUNCH(EPI_STD) break;
+    case EPI_GRU_A: JR_LAUNCH(EPI_GRU_A) break;
+    case EPI_GRU_B: JR_LAUNCH(EPI_GRU_B) break;
+    case EPI_FLOW: JR_LAUNCH(EPI_FLOW) break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef JR_LAUNCH
+  return (int)hipGetLastError();
+}
+
+}  // namespace

@@ -153,3 +153,71 @@ extern "C" int jr_flow_head(const void* fm, int fcs, const void* wt, const float
 #undef JR_FH
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Flow-head output conv as "1x1 GEMM + tap sum" (the default engine path).
+// A 3x3 conv with 2 outputs is linear in its input, so
+//   delta(p) = b + sum_{kh,kw} W[kh][kw]^T fm(p + (kh-1, kw-1))
+//            = b + sum_tap t[p + d_tap][tap],   t[q][tap] = W[tap]^T fm(q)
+// t (9 taps x 2 outputs per pixel) is ONE 1x1 implicit-GEMM conv over fm
+// (K = cin, N = 18: fm is read once instead of 9 times), and this kernel adds
+// the 9 shifted partials (zero padding = skipping out-of-map neighbours)
+// and applies the fused epilogue of EPI_FLOW: coords += delta, flow =
+// coords - grid as fp32 and as bf16 into hx / qx / flow8 (model.py:347-350,505).
+// One thread per pixel; t is [M][tcs] fp32 (tcs >= 18), 2.7 MB at batch 4 and
+// L2-resident right after the GEMM that wrote it.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void flow_taps_kernel(const float* __restrict__ t, int tcs, const float* __restrict__ bias,
+                                                       int N, int h, int w, float* __restrict__ coords,
+                                                       float* __restrict__ flow32, bf16* __restrict__ hx, int hx_cs,
+                                                       int hx_off, bf16* __restrict__ qx, int qx_cs, int qx_off,
+                                                       bf16* __restrict__ f8, int f8_cs) {
+  const long m = (long)blockIdx.x * 256 + threadIdx.x;
+  const long M = (long)N * h * w;
+  if (m >= M) return;
+  const int hw = h * w;
+  const int rem = (int)(m % hw);
+  const int y = rem / w, x = rem - (rem / w) * w;
+  const long img0 = m - rem;
+  float dx = bias[0], dy = bias[1];
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int yy = y + kh - 1;
+    if ((unsigned)yy >= (unsigned)h) continue;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int xx = x + kw - 1;
+      if ((unsigned)xx >= (unsigned)w) continue;
+      const float2 v = *(const float2*)(t + (img0 + (long)yy * w + xx) * tcs + 2 * (kh * 3 + kw));
+      dx += v.x;
+      dy += v.y;
+    }
+  }
+  const float cx = coords[2 * m] + dx;
+  const float cy = coords[2 * m + 1] + dy;
+  coords[2 * m] = cx;
+  coords[2 * m + 1] = cy;
+  const float fx = cx - (float)x, fy = cy - (float)y;
+  flow32[2 * m] = fx;
+  flow32[2 * m + 1] = fy;
+  hx[m * hx_cs + hx_off] = f2bf(fx);
+  hx[m * hx_cs + hx_off + 1] = f2bf(fy);
+  if (qx) {
+    qx[m * qx_cs + qx_off] = f2bf(fx);
+    qx[m * qx_cs + qx_off + 1] = f2bf(fy);
+  }
+  if (f8) {
+    f8[m * f8_cs] = f2bf(fx);
+    f8[m * f8_cs + 1] = f2bf(fy);
+  }
+}
+
+extern "C" int jr_flow_taps(const float* t, int tcs, const float* bias, int N, int h, int w, float* coords,
+                            float* flow32, void* hx, int hx_cs, int hx_off, void* qx, int qx_cs, int qx_off, void* f8,
+                            int f8_cs, hipStream_t stream) {
+  const long M = (long)N * h * w;
+  if (tcs < 18 || (tcs & 1)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(flow_taps_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, stream, t, tcs, bias, N, h, w,
+                     coords, flow32, (bf16*)hx, hx_cs, hx_off, (bf16*)qx, qx_cs, qx_off, (bf16*)f8, f8_cs);
+  return (int)hipGetLastError();
+}

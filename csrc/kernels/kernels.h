@@ -56,6 +56,9 @@ struct ConvParams {
   float* coords;    // FLOW: fp32 [M][2]
   float* flow32;    // FLOW: fp32 [M][2]
   void* y3; int y3_cstride, y3_coff;  // FLOW: third bf16 flow copy
+  // optional fp32 per-pixel bias map [M][bmap_cstride], channels [bmap_coff, bmap_coff + cout),
+  // added with the bias (e.g. the loop-invariant context-feature part of the ConvGRU gates)
+  const float* bmap; int bmap_cstride, bmap_coff;
   // 1 when every 64-deep K stage lies inside one tap (a 1x1 conv, or cin8 % 64 == 0 with at most
   // 32 taps) and there is no input dilation: the register-staged kernels then use wave-uniform
   // tap state and per-row tap bitmasks instead of per-lane im2col arithmetic
@@ -127,6 +130,11 @@ int jr_zero_fill(void* p, long bytes, hipStream_t stream);
 int jr_flow_head(const void* fm, int fcs, const void* wt, const float* bias, int N, int h, int w, int cin,
                  float* coords, float* flow32, void* hx, int hx_cs, int hx_off, void* qx, int qx_cs, int qx_off,
                  void* f8, int f8_cs, hipStream_t stream);
+// delta(p) = bias + sum of the 9 shifted per-tap partials t[p + d][tap] ([M][tcs] fp32,
+// tap-major pairs), then the EPI_FLOW coordinate / flow update (flowhead.hip)
+int jr_flow_taps(const float* t, int tcs, const float* bias, int N, int h, int w, float* coords, float* flow32,
+                 void* hx, int hx_cs, int hx_off, void* qx, int qx_cs, int qx_off, void* f8, int f8_cs,
+                 hipStream_t stream);
 int jr_copy_channels(const void* src, int s_cstride, int s_coff, void* dst, int d_cstride, int d_coff,
                      int M, int C, hipStream_t stream);
 

@@ -63,14 +63,15 @@ static void check_f32(const at::Tensor& t, const char* name) {
 }
 
 // ----------------------------------------------------------------------- conv
-// t = [x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3]
+// t = [x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3, bmap]
 // i = [N, H, W, x_coff, cin8, KH, KW, SH, SW, PH, PW, cout, act, split,
 //      y_coff, y2_coff, res_coff, hidden, y3_coff, epi, cfg, res_post
-//      (, OH_override, OW_override, log2 dil_h, log2 dil_w)]
+//      (, OH_override, OW_override, log2 dil_h, log2 dil_w (, bmap_coff))]
 static Launch make_conv(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep) {
-  TORCH_CHECK(i.size() == 22 || i.size() == 26, "conv: expected 22 or 26 ints");
+  TORCH_CHECK(i.size() == 22 || i.size() == 26 || i.size() == 27, "conv: expected 22, 26 or 27 ints");
   at::Tensor x = opt(t, 0), w = opt(t, 1), bias = opt(t, 2), y = opt(t, 3), y2 = opt(t, 4), res = opt(t, 5);
   at::Tensor h32 = opt(t, 6), zbuf = opt(t, 7), coords = opt(t, 8), flow32 = opt(t, 9), y3 = opt(t, 10);
+  at::Tensor bmap = opt(t, 11);
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_f32(bias, "bias");
@@ -80,13 +81,13 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   p.N = (int)i[0]; p.H = (int)i[1]; p.W = (int)i[2];
   p.x_cstride = cs(x); p.x_coff = (int)i[3]; p.cin8 = (int)i[4];
   p.KH = (int)i[5]; p.KW = (int)i[6]; p.SH = (int)i[7]; p.SW = (int)i[8]; p.PH = (int)i[9]; p.PW = (int)i[10];
-  p.dsh = i.size() == 26 ? (int)i[24] : 0;
-  p.dsw = i.size() == 26 ? (int)i[25] : 0;
+  p.dsh = i.size() >= 26 ? (int)i[24] : 0;
+  p.dsw = i.size() >= 26 ? (int)i[25] : 0;
   TORCH_CHECK(p.dsh >= 0 && p.dsh <= 3 && p.dsw >= 0 && p.dsw <= 3, "conv: dilation must be 1, 2, 4 or 8");
   p.OH = ((p.H << p.dsh) - ((1 << p.dsh) - 1) + 2 * p.PH - p.KH) / p.SH + 1;
   p.OW = ((p.W << p.dsw) - ((1 << p.dsw) - 1) + 2 * p.PW - p.KW) / p.SW + 1;
-  if (i.size() == 26 && i[22] > 0) p.OH = (int)i[22];
-  if (i.size() == 26 && i[23] > 0) p.OW = (int)i[23];
+  if (i.size() >= 26 && i[22] > 0) p.OH = (int)i[22];
+  if (i.size() >= 26 && i[23] > 0) p.OW = (int)i[23];
   p.M = p.N * p.OH * p.OW;
   p.x_bytes = x.numel() * 2;
   p.w_bytes = w.numel() * 2;
@@ -103,6 +104,15 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   p.coords = coords.defined() ? coords.data_ptr<float>() : nullptr;
   p.flow32 = flow32.defined() ? flow32.data_ptr<float>() : nullptr;
   p.y3 = ptr(y3); p.y3_cstride = cs(y3); p.y3_coff = (int)i[18];
+  p.bmap = bmap.defined() ? bmap.data_ptr<float>() : nullptr;
+  p.bmap_cstride = bmap.defined() ? cs(bmap) : 0;
+  p.bmap_coff = i.size() == 27 ? (int)i[26] : 0;
+  if (bmap.defined()) {
+    check_f32(bmap, "bmap");
+    TORCH_CHECK(p.bmap_cstride % 4 == 0 && p.bmap_coff % 4 == 0 && p.bmap_coff + p.cout <= p.bmap_cstride,
+                "conv: bias map channel slice must be 4-aligned and inside the tensor");
+    TORCH_CHECK(bmap.numel() >= (int64_t)p.M * p.bmap_cstride, "conv: bias map too small");
+  }
   {
     const int taps = p.KH * p.KW;
     p.fast = p.dsh == 0 && p.dsw == 0 && taps <= 32 && (taps == 1 || p.cin8 % 64 == 0) && !std::getenv("JR_CONV_NO_FAST");
@@ -148,11 +158,41 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   } else {
     TORCH_CHECK(false, "conv: unknown epilogue ", epi);
   }
-  TORCH_CHECK(cfg >= 0 && cfg <= 24, "conv: unknown tile config ", cfg);
-  if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3}) if (v.defined()) keep->push_back(v);
+  TORCH_CHECK(cfg >= 0 && cfg <= 28, "conv: unknown tile config ", cfg);
+  if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3, bmap}) if (v.defined()) keep->push_back(v);
   return [p, epi, cfg](hipStream_t s, int) { return jr_conv_forward(&p, cfg, epi, s); };
 }
 
+
+// ------------------------------------------------------------------ flow taps
+// t = [taps (fp32 [M][tcs]), bias (fp32 [2]), coords, flow32, hx, qx?, flow8?]
+// i = [N, h, w, hx_off, qx_off]
+static Launch make_flow_taps(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor tp = opt(t, 0), bias = opt(t, 1), coords = opt(t, 2), flow32 = opt(t, 3), hx = opt(t, 4), qx = opt(t, 5),
+             f8 = opt(t, 6);
+  TORCH_CHECK(i.size() == 5, "flow_taps: expected 5 ints");
+  check_f32(tp, "taps"); check_f32(bias, "bias"); check_f32(coords, "coords"); check_f32(flow32, "flow32");
+  check_bf16(hx, "hx");
+  const int N = (int)i[0], h = (int)i[1], w = (int)i[2], hx_off = (int)i[3], qx_off = (int)i[4];
+  const int64_t M = (int64_t)N * h * w;
+  TORCH_CHECK(cs(tp) >= 18 && cs(tp) % 2 == 0 && tp.numel() >= M * cs(tp), "flow_taps: taps [M][>=18]");
+  TORCH_CHECK(bias.numel() >= 2 && coords.numel() >= 2 * M && flow32.numel() >= 2 * M, "flow_taps: bias / coords / flow32");
+  TORCH_CHECK(hx.numel() >= M * cs(hx) && hx_off + 2 <= cs(hx), "flow_taps: hx");
+  if (qx.defined()) { check_bf16(qx, "qx"); TORCH_CHECK(qx.numel() >= M * cs(qx) && qx_off + 2 <= cs(qx), "flow_taps: qx"); }
+  if (f8.defined()) { check_bf16(f8, "flow8"); TORCH_CHECK(f8.numel() >= M * cs(f8) && cs(f8) >= 2, "flow_taps: flow8"); }
+  if (keep) for (auto& v : {tp, bias, coords, flow32, hx, qx, f8}) if (v.defined()) keep->push_back(v);
+  const float* tpp = tp.data_ptr<float>();
+  const float* bp = bias.data_ptr<float>();
+  float* cp = coords.data_ptr<float>();
+  float* f32p = flow32.data_ptr<float>();
+  void* hp = hx.data_ptr();
+  void* qp = ptr(qx);
+  void* f8p = ptr(f8);
+  const int tcs = cs(tp), hcs = cs(hx), qcs = qx.defined() ? cs(qx) : 0, f8cs = f8.defined() ? cs(f8) : 0;
+  return [=](hipStream_t s, int) {
+    return jr_flow_taps(tpp, tcs, bp, N, h, w, cp, f32p, hp, hcs, hx_off, qp, qcs, qx_off, f8p, f8cs, s);
+  };
+}
 
 // ------------------------------------------------------------------ flow head
 // t = [fm, wt (bf16 [2][9][cin]), bias (fp32 [2]), coords, flow32, hx, qx?, flow8?]
@@ -479,6 +519,7 @@ void copy_channels_op(const TList& t, IList i) { run_now(make_copy_channels(t, i
 void lookup_bwd_op(const TList& t, IList i) { run_now(make_lookup_bwd(t, i, nullptr)); }
 void im2col_op(const TList& t, IList i) { run_now(make_im2col(t, i, nullptr)); }
 void flow_head_op(const TList& t, IList i) { run_now(make_flow_head(t, i, nullptr)); }
+void flow_taps_op(const TList& t, IList i) { run_now(make_flow_taps(t, i, nullptr)); }
 
 // --------------------------------------------------------------------- Plan
 // A Plan is the lowered RAFT forward: three segments (prologue, loop body run
@@ -494,6 +535,14 @@ void flow_head_op(const TList& t, IList i) { run_now(make_flow_head(t, i, nullpt
 // execute concurrently.  A wait on an event not yet recorded during the
 // current enqueue is skipped (e.g. the first iteration's wait on the previous
 // iteration's mask head), which also keeps graph capture self-contained.
+// Loop-body ops can carry a parity (set_parity 0/1): they are enqueued only in
+// even / odd iterations, which double-buffers a tensor that a side lane still
+// reads while the next iteration rewrites it (the flow head's features and
+// flow vs. the mask head + upsampling of the previous iteration).
+// Lane 0 runs on a private stream of the device's greatest priority (forked
+// from / joined to the caller's stream): the model's critical path (lookup ->
+// motion encoder -> GRU -> flow head) wins the dispatcher over the side lanes'
+// work, which only fills the CUs the critical path leaves idle.
 struct RangeGuard {
   explicit RangeGuard(const char* name) { roctxRangePushA(name); }
   ~RangeGuard() { roctxRangePop(); }
@@ -516,7 +565,13 @@ class Plan : public torch::CustomClassHolder {
   void set_segment(int64_t s) {
     TORCH_CHECK(s >= 0 && s <= 2, "segment must be 0 (prologue), 1 (loop) or 2 (epilogue)");
     seg_ = (int)s;
+    parity_ = -1;
     reset_graph();
+  }
+  void set_parity(int64_t p) {
+    TORCH_CHECK(p >= -1 && p <= 1, "parity must be -1 (every iteration), 0 (even) or 1 (odd)");
+    TORCH_CHECK(p == -1 || seg_ == 1, "parity applies to loop-body ops only");
+    parity_ = (int)p;
   }
   void set_lane(int64_t l) {
     TORCH_CHECK(l >= 0 && l < kMaxLanes, "lane must be in [0, ", kMaxLanes, ")");
@@ -538,6 +593,7 @@ class Plan : public torch::CustomClassHolder {
   void add_copy(TList t) { push(make_copy(t, &keep_), "copy"); }
   void add_copy_channels(TList t, IList i) { push(make_copy_channels(t, i, &keep_), "copy_channels"); }
   void add_flow_head(TList t, IList i) { push(make_flow_head(t, i, &keep_), "flow_head"); }
+  void add_flow_taps(TList t, IList i) { push(make_flow_taps(t, i, &keep_), "flow_taps"); }
 
   int64_t num_ops(int64_t seg) const { return (int64_t)segs_[seg].size(); }
   std::vector<std::string> op_names(int64_t seg) const {
@@ -554,13 +610,18 @@ class Plan : public torch::CustomClassHolder {
   // legacy default stream cannot be captured) and instantiate it.
   void capture(int64_t n_iters) {
     reset_graph();
-    if (!cap_stream_) TORCH_CHECK(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking) == hipSuccess, "stream");
+    if (!cap_stream_) {
+      int least = 0, greatest = 0;
+      TORCH_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess, "priority range");
+      if (!use_priority()) greatest = 0;
+      TORCH_CHECK(hipStreamCreateWithPriority(&cap_stream_, hipStreamNonBlocking, greatest) == hipSuccess, "stream");
+    }
     hipStream_t s = cap_stream_;
     debug_ = std::getenv("JR_PLAN_DEBUG") != nullptr;
     // order the capture after work already queued on the current stream
     TORCH_CHECK(hipStreamSynchronize(cur_stream()) == hipSuccess, "sync");
     TORCH_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess, "begin capture");
-    int err = enqueue(s, (int)n_iters);
+    int err = enqueue(s, (int)n_iters, true);
     if (debug_) fprintf(stderr, "[plan] enqueue done err=%d\n", err);
     hipGraph_t g = nullptr;
     hipError_t e2 = hipStreamEndCapture(s, &g);
@@ -593,15 +654,21 @@ class Plan : public torch::CustomClassHolder {
     int kind;
     int ev;
     std::string name;
+    int parity;  // -1: every iteration; 0 / 1: even / odd loop iterations only
   };
   void push(Launch l, const char* name) {
-    segs_[seg_].push_back(Op{std::move(l), lane_, OP_LAUNCH, -1, name});
+    segs_[seg_].push_back(Op{std::move(l), lane_, OP_LAUNCH, -1, name, parity_});
     reset_graph();
   }
   void push_sync(int kind, int64_t ev, const char* name) {
     TORCH_CHECK(ev >= 0 && ev < kMaxEvents, "event id out of range");
-    segs_[seg_].push_back(Op{Launch(), lane_, kind, (int)ev, std::string(name) + std::to_string(ev)});
+    segs_[seg_].push_back(Op{Launch(), lane_, kind, (int)ev, std::string(name) + std::to_string(ev), parity_});
     reset_graph();
+  }
+  // JR_LANE_PRIORITY=0 disables the lane priorities (A/B measurements)
+  static bool use_priority() {
+    const char* v = std::getenv("JR_LANE_PRIORITY");
+    return !(v && v[0] == '0');
   }
   static int create_event(hipEvent_t* e) {
     return (int)hipEventCreateWithFlags(e, hipEventDisableTiming);
@@ -612,8 +679,13 @@ class Plan : public torch::CustomClassHolder {
       for (auto& e : events_) if (int r = create_event(&e)) return r;
     }
     if (!fork_) if (int r = create_event(&fork_)) return r;
+    int least = 0, greatest = 0;
+    if (int r = (int)hipDeviceGetStreamPriorityRange(&least, &greatest)) return r;
+    if (!use_priority()) least = greatest = 0;
+    if (!lanes_[0]) if (int r = (int)hipStreamCreateWithPriority(&lanes_[0], hipStreamNonBlocking, greatest)) return r;
+    if (!join_[0]) if (int r = create_event(&join_[0])) return r;
     for (int l = 1; l < used_lanes_; ++l) {
-      if (!lanes_[l]) if (int r = (int)hipStreamCreateWithFlags(&lanes_[l], hipStreamNonBlocking)) return r;
+      if (!lanes_[l]) if (int r = (int)hipStreamCreateWithPriority(&lanes_[l], hipStreamNonBlocking, least)) return r;
       if (!join_[l]) if (int r = create_event(&join_[l])) return r;
     }
     return 0;
@@ -623,6 +695,7 @@ class Plan : public torch::CustomClassHolder {
   // order and is skipped (a same-stream record/wait pair on a forked capture stream
   // also crashes hipStreamEndCapture on this ROCm).
   int exec_op(const Op& o, hipStream_t* st, int it, std::vector<char>& recorded) {
+    if (o.parity >= 0 && (it & 1) != o.parity) return 0;
     hipStream_t s = st[o.lane];
     if (debug_) fprintf(stderr, "[plan] it=%d lane=%d %s stream=%p\n", it, o.lane, o.name.c_str(), (void*)s);
     switch (o.kind) {
@@ -633,16 +706,19 @@ class Plan : public torch::CustomClassHolder {
         return (int)hipStreamWaitEvent(s, events_[o.ev], 0);
     }
   }
-  int enqueue(hipStream_t s, int n_iters) {
+  int enqueue(hipStream_t s, int n_iters, bool capturing = false) {
     if (int r = ensure_resources()) return r;
+    // Eager: lane 0 is the private high-priority stream, forked from the caller's.
+    // Capture: lane 0 is the capture stream itself (created with the greatest
+    // priority); a capture whose origin stream holds only the fork/join event
+    // nodes crashes hipStreamEndCapture on this ROCm.
+    const int l0 = capturing ? 1 : 0;
     hipStream_t st[kMaxLanes] = {};
     st[0] = s;
-    if (used_lanes_ > 1) {
-      if (int r = (int)hipEventRecord(fork_, s)) return r;
-      for (int l = 1; l < used_lanes_; ++l) {
-        st[l] = lanes_[l];
-        if (int r = (int)hipStreamWaitEvent(st[l], fork_, 0)) return r;
-      }
+    if (int r = (int)hipEventRecord(fork_, s)) return r;
+    for (int l = l0; l < used_lanes_; ++l) {
+      st[l] = lanes_[l];
+      if (int r = (int)hipStreamWaitEvent(st[l], fork_, 0)) return r;
     }
     std::vector<char> recorded(kMaxEvents, 0);
     // roctx ranges (visible in rocprofv3 --marker-trace) bracket the host-side
@@ -661,7 +737,7 @@ class Plan : public torch::CustomClassHolder {
       RangeGuard r("raft.epilogue");
       for (auto& o : segs_[2]) if (int e = exec_op(o, st, n_iters, recorded)) return e;
     }
-    for (int l = 1; l < used_lanes_; ++l) {
+    for (int l = l0; l < used_lanes_; ++l) {
       if (int r = (int)hipEventRecord(join_[l], st[l])) return r;
       if (int r = (int)hipStreamWaitEvent(s, join_[l], 0)) return r;
     }
@@ -671,6 +747,7 @@ class Plan : public torch::CustomClassHolder {
   std::vector<at::Tensor> keep_;
   int seg_ = 0;
   int lane_ = 0;
+  int parity_ = -1;
   int used_lanes_ = 1;
   std::vector<hipEvent_t> events_;
   hipEvent_t fork_ = nullptr;
@@ -699,10 +776,12 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("lookup_bwd(Tensor?[] t, int[] i) -> ()", &jr::lookup_bwd_op);
   m.def("im2col(Tensor?[] t, int[] i) -> ()", &jr::im2col_op);
   m.def("flow_head(Tensor?[] t, int[] i) -> ()", &jr::flow_head_op);
+  m.def("flow_taps(Tensor?[] t, int[] i) -> ()", &jr::flow_taps_op);
   m.class_<jr::Plan>("Plan")
       .def(torch::init<>())
       .def("set_segment", &jr::Plan::set_segment)
       .def("set_lane", &jr::Plan::set_lane)
+      .def("set_parity", &jr::Plan::set_parity)
       .def("add_record", &jr::Plan::add_record)
       .def("add_wait", &jr::Plan::add_wait)
       .def("num_lanes", &jr::Plan::num_lanes)
@@ -719,6 +798,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_copy", &jr::Plan::add_copy)
       .def("add_copy_channels", &jr::Plan::add_copy_channels)
       .def("add_flow_head", &jr::Plan::add_flow_head)
+      .def("add_flow_taps", &jr::Plan::add_flow_taps)
       .def("num_ops", &jr::Plan::num_ops)
       .def("op_names", &jr::Plan::op_names)
       .def("run", &jr::Plan::run)

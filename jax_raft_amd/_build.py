@@ -25,12 +25,16 @@ CXX = os.environ.get("CXX", "g++")
 
 KERNEL_SOURCES = [
     CSRC / "kernels" / "conv_igemm.hip",
+    CSRC / "kernels" / "conv_fam_r.hip",
+    CSRC / "kernels" / "conv_fam_rw.hip",
+    CSRC / "kernels" / "conv_fam_m32.hip",
+    CSRC / "kernels" / "conv_fam_d2.hip",
     CSRC / "kernels" / "corr.hip",
     CSRC / "kernels" / "elementwise.hip",
     CSRC / "kernels" / "flowhead.hip",
 ]
 HOST_SOURCES = [CSRC / "runtime" / "binding.cpp"]
-HEADERS = [CSRC / "kernels" / "common.h", CSRC / "kernels" / "kernels.h"]
+HEADERS = [CSRC / "kernels" / "common.h", CSRC / "kernels" / "kernels.h", CSRC / "kernels" / "conv_igemm.h"]
 
 
 def _torch_paths():

@@ -36,10 +36,12 @@ CFG_TILES.update({16: (256, 128), 17: (128, 256)})
 CFG_TILES.update({18: (128, 128), 19: (128, 128), 20: (256, 128)})
 # configs 21/22: 16 waves per block (32x32 / 64x32 wave tiles); 23/24: 8 waves at 128x64 / 64x128
 CFG_TILES.update({21: (128, 128), 22: (256, 128), 23: (128, 64), 24: (64, 128)})
+# configs 25..28: kernel M32 with 8 waves (64x64 / 64x64 / 64x32 / 64x32 wave tiles)
+CFG_TILES.update({25: (256, 128), 26: (128, 256), 27: (128, 128), 28: (64, 256)})
 # Autotune candidates: configs that win at least one RAFT conv on MI355X
 # (tools/microbench.py, profiles/r1_microbench_conv_cfgs.txt); the others stay
 # compiled and tested but are not timed at plan build.
-TUNE_CFGS = (0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24)
+TUNE_CFGS = (0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28)
 NUM_CUS = 256
 
 
@@ -179,14 +181,18 @@ def pick_cfg(M: int, cout: int) -> int:
 def conv_args(spec: ConvSpec, x: torch.Tensor, N: int, H: int, W: int, y: torch.Tensor, *, x_coff: int = 0,
               y_coff: int = 0, act: int = ACT_NONE, split: int = 0, alpha: float = 1.0, y2=None, y2_coff: int = 0,
               res=None, res_coff: int = 0, res_post: int = 0, h32=None, zbuf=None, hidden: int = 0, coords=None,
-              flow32=None, y3=None, y3_coff: int = 0, epi: int = EPI_STD, cfg: Optional[int] = None):
-    """Build the (tensors, ints, alpha) argument triple of the ``conv`` op."""
+              flow32=None, y3=None, y3_coff: int = 0, epi: int = EPI_STD, cfg: Optional[int] = None,
+              bmap=None, bmap_coff: int = 0):
+    """Build the (tensors, ints, alpha) argument triple of the ``conv`` op.
+    ``bmap``: optional fp32 per-pixel bias map [M, C], channels from ``bmap_coff``."""
     OH, OW = spec.out_hw(H, W)
     if cfg is None:
         cfg = pick_cfg(N * OH * OW, spec.cout)
-    t = [x, spec.w, spec.b, y, y2, res, h32, zbuf, coords, flow32, y3]
+    t = [x, spec.w, spec.b, y, y2, res, h32, zbuf, coords, flow32, y3, bmap]
     i = [N, H, W, x_coff, spec.cin8, spec.kh, spec.kw, spec.sh, spec.sw, spec.ph, spec.pw, spec.cout, act, split,
          y_coff, y2_coff, res_coff, hidden, y3_coff, epi, cfg, res_post]
+    if bmap is not None:
+        i += [0, 0, 0, 0, bmap_coff]
     return t, i, float(alpha)
 
 

@@ -18,8 +18,14 @@ scan body :495-510                     loop segment: lookup, 5 motion convs, 2x 
 =====================================  ==============================================
 
 Persistent buffers replace every concat of the reference:
-``hx = [h | context | motion | flow]`` (GRU z/r input, ``model.py:303,366,290``) and
-``qx = [r*h | context | motion | flow]`` (GRU q input, ``model.py:308``).
+``hx = [h | motion | flow]`` (GRU z/r input, ``model.py:303,366,290``) and
+``qx = [r*h | motion | flow]`` (GRU q input, ``model.py:308``).  The context
+features -- the third part of the GRU input ``[h | context | motion]`` -- are
+loop-invariant, so their share of every ConvGRU gate (z, r and q, plus the
+gate biases) is computed ONCE in the prologue (one conv per GRU over the
+context, fp32 output) and added per pixel in the loop convs' epilogues (the
+``bmap`` bias map).  That removes a third of the GRU GEMMs' K from every
+iteration: K = 5 x 256 instead of 5 x 384 for raft_large.
 """
 from __future__ import annotations
 
@@ -125,19 +131,30 @@ class RaftEngine:
             flow-feature convs || lookup + correlation convs; mask head +
             upsampling of iteration i || iteration i+1) so they overlap on
             the GPU (parallel branches of the captured hipGraph).
-        fused_flow_head: run the flow head's output conv + coordinate update as
-            the dedicated flow_head kernel (flowhead.hip) instead of the
-            implicit-GEMM conv with the EPI_FLOW epilogue (measured equal).
+        flow_head: how the flow head's output conv (3x3, 256 -> 2) + the
+            coordinate update run: "taps" (default) = a 1x1 implicit-GEMM conv
+            to the 9 x 2 per-tap partials + the flow_taps kernel that sums the
+            shifted partials (fm read once instead of 9 times); "conv" = the
+            3x3 implicit-GEMM conv with the EPI_FLOW epilogue; "fused" = the
+            dedicated halo-tiled flow_head kernel (flowhead.hip).
         split: run the batch as this many independent half-forwards on
             separate lanes (when the batch divides evenly), so that one
             part's kernels fill the CUs another part's leave idle.
+        double_buffer: ("lanes" schedule) double-buffer the flow head outputs by iteration
+            parity, so iteration i+1's flow head need not wait for iteration
+            i's mask head (otherwise one buffer and a WAR wait).  Off by
+            default: the extra overlap measured slower (233 vs 244 pairs/s),
+            the mask head then contends with the next iteration's critical path.
     """
 
     def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True,
                  corr_dtype: torch.dtype = torch.bfloat16, autotune: bool = True, streams: bool = True,
-                 split: int = 1, fused_flow_head: bool = False):
+                 split: int = 1, flow_head: str = "taps", double_buffer: bool = False,
+                 fused_flow_head: bool = False):
         nat.require()
-        self.fused_flow_head = fused_flow_head
+        self.double_buffer = double_buffer
+        self.flow_head = "fused" if fused_flow_head else flow_head
+        assert self.flow_head in ("taps", "conv", "fused"), self.flow_head
         self.streams = streams
         self.split = split
         self._part_streams: List[torch.cuda.Stream] = []
@@ -172,12 +189,14 @@ class RaftEngine:
         self.corr_ch = self.num_levels * S * S
         self.corr_cs = round_up(self.corr_ch, 8)
         self.mot_out = me.out_channels
-        self.hx_real = self.hidden + self.ctx_ch + self.mot_out
+        # loop buffers hold [h | motion | flow]; the context part of the GRU input is folded (see module doc)
+        self.hx_real = self.hidden + self.mot_out
         self.hx_cs = round_up(self.hx_real, 8)
-        self.mot_off = self.hidden + self.ctx_ch
+        self.mot_off = self.hidden
         self.flow_off = self.mot_off + self.mot_out - 2
-        if self.mot_off % 8 or self.hidden % 16:
-            raise NotImplementedError("native engine needs hidden % 16 == 0 and (hidden + context) % 8 == 0")
+        self.gate_cs = round_up(3 * self.hidden, 8)   # fp32 context bias map: [z | r | q] per GRU
+        if self.hidden % 16:
+            raise NotImplementedError("native engine needs hidden % 16 == 0")
         self.fh_hidden = fh.hidden_size
         self.has_mask = m.mask_predictor is not None
         self.fmap_ch = fe.out_channels
@@ -254,16 +273,27 @@ class RaftEngine:
         for gi in range(len(rb.kernel_size)):
             gru = getattr(rb, f"convgru{gi + 1}")
 
+            H_, C_ = self.hidden, self.ctx_ch
+
+            def loop_part(k):  # input channels [h | context | motion] -> [h | motion]
+                k = k.detach().float()
+                return torch.cat([k[:, :, :H_], k[:, :, H_ + C_:]], dim=2)
+
             def gru_a(gru=gru):
-                k = torch.cat([gru.convz.kernel.detach(), gru.convr.kernel.detach()], dim=3).float()
-                b = torch.cat([gru.convz.bias.detach(), gru.convr.bias.detach()]).float()
-                return k, b, (1, 1), gru.padding, self.hx_cs
+                k = torch.cat([loop_part(gru.convz.kernel), loop_part(gru.convr.kernel)], dim=3)
+                return k, torch.zeros(2 * H_), (1, 1), gru.padding, self.hx_cs
 
             def gru_b(gru=gru):
-                return gru.convq.kernel.detach().float(), gru.convq.bias.detach().float(), (1, 1), gru.padding, self.hx_cs
+                return loop_part(gru.convq.kernel), torch.zeros(H_), (1, 1), gru.padding, self.hx_cs
+
+            def gru_ctx(gru=gru):  # context share of [z | r | q] + the gate biases (prologue, once)
+                k = torch.cat([c.kernel.detach()[:, :, H_:H_ + C_] for c in (gru.convz, gru.convr, gru.convq)], dim=3)
+                b = torch.cat([c.bias.detach() for c in (gru.convz, gru.convr, gru.convq)])
+                return k.float(), b.float(), (1, 1), gru.padding, None
 
             self._reg(f"gru{gi}.a", gru_a)
             self._reg(f"gru{gi}.b", gru_b)
+            self._reg(f"gru{gi}.ctx", gru_ctx)
         if self.has_mask:
             mp = m.mask_predictor
 
@@ -279,13 +309,21 @@ class RaftEngine:
             self._reg("fh1", conv_src(fh.conv1))
         self._reg("fh2", conv_src(fh.conv2))
 
+        def fh2_taps():  # (3,3,cin,2) -> (1,1,cin,18): out channel tap*2 + o
+            k = fh.conv2.kernel.detach().float()
+            cin = k.shape[2]
+            k = k.reshape(9, cin, 2).permute(1, 0, 2).reshape(1, 1, cin, 18)
+            return k, torch.zeros(18), (1, 1), (0, 0), None
+
+        self._reg("fh2.taps", fh2_taps)
+
     # ------------------------------------------------------------- autotune
     def _conv(self, plan, spec: ConvSpec, x, N, H, W, y, **kw):
         """Append one conv to ``plan``, choosing its tile config (autotuned)."""
         if self.autotune and kw.get("cfg") is None:
             OH, OW = spec.out_hw(H, W)
             key = (N * OH * OW, spec.cout, spec.kh, spec.kw, spec.sh, spec.sw, spec.cin8, x.shape[-1],
-                   kw.get("epi", EPI_STD), str(self.device))
+                   kw.get("epi", EPI_STD), kw.get("bmap") is not None, str(self.device))
             cfg = _TUNE_CACHE.get(key)
             if cfg is None:
                 cfg = _tune(spec, x, N, H, W, y, kw)
@@ -400,7 +438,7 @@ class RaftEngine:
     def _build_part(self, st: _PlanState, plan, b0: int, B: int, H: int, W: int, n_iters: int, pt: str,
                     lanes: Tuple[int, int, int], ev0: int, all_iters: bool = True):
         """Lower one forward over images [b0, b0 + B) onto ``plan`` using lanes
-        (main, side, side2) and events ev0 .. ev0 + 5.  ``all_iters=False`` is the
+        (main, side, side2) and events ev0 .. ev0 + 6.  ``all_iters=False`` is the
         final-only serving mode: the loop runs the flow head alone (no mask head)
         and the mask head + x8 upsampling run once, in the epilogue segment, on
         the final hidden state and flow."""
@@ -423,7 +461,7 @@ class RaftEngine:
 
         # ---------------- prologue: encoders + correlation pyramid
         # lanes: 0 = feature encoder + correlation pyramid, 1 = context encoder
-        E_PREP, E_CTX, E_IT, E_FLOW, E_FH, E_MASK = range(ev0, ev0 + 6)
+        E_PREP, E_CTX, E_IT, E_FLOW, E_FH, E_MASK = range(ev0, ev0 + 6)  # E_MASK + 1: odd-iteration mask head
         main, side, side2 = lanes
 
         def lane(l):
@@ -448,8 +486,17 @@ class RaftEngine:
         plan.add_wait(E_PREP)
         ctxf, ch_, cw_ = self._encoder(st, plan, "ce", m.context_encoder, x0[:B], B, H, W, bt=pt)
         assert (ch_, cw_) == (h, w), "The context encoder should downsample H and W by 8"
-        self._conv(plan, sp["ce.conv"], ctxf, B, h, w, hx, act=ACT_SPLIT_TANH_RELU, split=self.hidden,
-                   y2=qx, h32=h32, hidden=self.hidden)
+        # [tanh(h) | relu(context)] (model.py:582-584); h also as fp32 state
+        ce_out = alloc("ce_out", (M, round_up(self.hidden + self.ctx_ch, 8)))
+        self._conv(plan, sp["ce.conv"], ctxf, B, h, w, ce_out, act=ACT_SPLIT_TANH_RELU, split=self.hidden,
+                   h32=h32, hidden=self.hidden)
+        plan.add_copy_channels([ce_out, hx], [0, 0, M, self.hidden])
+        # loop-invariant context share of every GRU gate (+ gate biases), fp32
+        gbias = []
+        for gi in range(len(m.update_block.recurrent_block.kernel_size)):
+            gb = alloc(f"gru{gi}.cbias", (M, self.gate_cs), F32)
+            self._conv(plan, sp[f"gru{gi}.ctx"], ce_out, B, h, w, gb, x_coff=self.hidden)
+            gbias.append(gb)
         plan.add_init_coords([coords], [B, h, w])
         plan.add_record(E_CTX)
 
@@ -478,11 +525,42 @@ class RaftEngine:
         cl, fl = me.corr_layers, me.flow_layers
         cf = alloc("cf", (M, cl[-1] + fl[-1]))
         f1 = alloc("f1", (M, fl[0]))
+
+        def flow_features():
+            self._conv(plan, sp["me.convflow1"], flow8, B, h, w, f1, act=ACT_RELU)
+            self._conv(plan, sp["me.convflow2"], f1, B, h, w, cf, y_coff=cl[-1], act=ACT_RELU)
+
+        s1 = sp["fh1"] if (all_iters or not self.has_mask) else sp["fh1.flow"]
+        fm_ch = round_up(sp["fh1"].cout, 8)
+        mask = alloc("mask", (M, 576)) if self.has_mask else None
+        stride = st.out.shape[1] * H * W * 2  # one iteration of the full-batch output
+        taps = alloc("fh2.taps", (M, 24), F32) if self.flow_head == "taps" else None
+
+        def flow_head(fm, f32):
+            self._conv(plan, s1, hx, B, h, w, fm, act=ACT_RELU)
+            # flow head conv2 + coordinate update (model.py:505) + flow into hx/qx/flow8
+            if self.flow_head == "taps":
+                self._conv(plan, sp["fh2.taps"], fm, B, h, w, taps)
+                plan.add_flow_taps([taps, self._fh2_b, coords, f32, hx, qx, flow8], [B, h, w, self.flow_off, self.flow_off])
+            elif self.flow_head == "fused" and self.fh_hidden in (128, 256):
+                plan.add_flow_head([fm, self._fh2_w, self._fh2_b, coords, f32, hx, qx, flow8],
+                                   [B, h, w, self.fh_hidden, 0, self.flow_off, self.flow_off])
+            else:
+                self._conv(plan, sp["fh2"], fm, B, h, w, hx, y_coff=self.flow_off, y2=qx, y2_coff=self.flow_off,
+                           y3=flow8, y3_coff=0, coords=coords, flow32=f32, epi=EPI_FLOW)
+
+        def upsample(fm, f32, stride):
+            if self.has_mask:
+                self._conv(plan, sp["mask"], fm, B, h, w, mask, x_coff=self.fh_hidden,
+                           alpha=m.mask_predictor.multiplier)
+                plan.add_upsample_convex([mask, f32, out], [B, h, w, stride])
+            else:
+                plan.add_upsample_bilinear([f32, out], [B, h, w, stride])
+
         plan.add_record(E_IT)
         lane(side)
         plan.add_wait(E_IT)
-        self._conv(plan, sp["me.convflow1"], flow8, B, h, w, f1, act=ACT_RELU)
-        self._conv(plan, sp["me.convflow2"], f1, B, h, w, cf, y_coff=cl[-1], act=ACT_RELU)
+        flow_features()
         plan.add_record(E_FLOW)
         lane(main)
         plan.add_lookup([coords, corr] + levels + [None] * (4 - L), [L, B, h, w, self.radius])
@@ -497,40 +575,38 @@ class RaftEngine:
                    y2_coff=self.mot_off)
         for gi in range(len(m.update_block.recurrent_block.kernel_size)):
             self._conv(plan, sp[f"gru{gi}.a"], hx, B, h, w, qx, h32=h32, zbuf=zb, hidden=self.hidden,
-                       epi=EPI_GRU_A)
+                       epi=EPI_GRU_A, bmap=gbias[gi], bmap_coff=0)
             self._conv(plan, sp[f"gru{gi}.b"], qx, B, h, w, hx, h32=h32, zbuf=zb, hidden=self.hidden,
-                       epi=EPI_GRU_B)
-        s1 = sp["fh1"] if (all_iters or not self.has_mask) else sp["fh1.flow"]
-        fm = alloc("fm", (M, round_up(sp["fh1"].cout, 8)))
+                       epi=EPI_GRU_B, bmap=gbias[gi], bmap_coff=2 * self.hidden)
         if all_iters:
-            plan.add_wait(E_MASK)  # previous iteration's mask head has consumed fm / flow32
-        self._conv(plan, s1, hx, B, h, w, fm, act=ACT_RELU)
-        # flow head conv2 + coordinate update (model.py:505) + flow into hx/qx/flow8
-        if self.fused_flow_head and self.fh_hidden in (128, 256):
-            plan.add_flow_head([fm, self._fh2_w, self._fh2_b, coords, flow32, hx, qx, flow8],
-                               [B, h, w, self.fh_hidden, 0, self.flow_off, self.flow_off])
+            # The mask head + upsampling of iteration i run on a side lane while
+            # iteration i+1 proceeds; the flow head's features / flow they read
+            # are double-buffered by iteration parity, so the next flow head
+            # only waits for the mask head of iteration i-1 (same buffers).
+            fms = [alloc("fm", (M, fm_ch))]
+            f32s = [flow32]
+            if self.double_buffer:
+                fms.append(alloc("fm.odd", (M, fm_ch)))
+                f32s.append(alloc("flow32.odd", (M, 2), F32))
+            for par in range(len(fms)):
+                if len(fms) > 1:
+                    plan.set_parity(par)
+                lane(main)
+                plan.add_wait(E_MASK + par)
+                flow_head(fms[par], f32s[par])
+                plan.add_record(E_FH)
+                lane(side2)
+                plan.add_wait(E_FH)
+                upsample(fms[par], f32s[par], stride)
+                plan.add_record(E_MASK + par)
+            plan.set_parity(-1)
         else:
-            self._conv(plan, sp["fh2"], fm, B, h, w, hx, y_coff=self.flow_off, y2=qx, y2_coff=self.flow_off,
-                       y3=flow8, y3_coff=0, coords=coords, flow32=flow32, epi=EPI_FLOW)
-        if all_iters:
-            plan.add_record(E_FH)
-            lane(side2)
-            plan.add_wait(E_FH)
-            stride = st.out.shape[1] * H * W * 2  # one iteration of the full-batch output
-        else:
+            fm = alloc("fm", (M, fm_ch))
+            flow_head(fm, flow32)
             plan.set_segment(2)  # epilogue: upsample the final flow once (out has one iteration)
-            stride = 0
             if self.has_mask:
                 self._conv(plan, sp["fh1"], hx, B, h, w, fm, act=ACT_RELU)  # mask head input on the final h
-        if self.has_mask:
-            mask = alloc("mask", (M, 576))
-            self._conv(plan, sp["mask"], fm, B, h, w, mask, x_coff=self.fh_hidden,
-                       alpha=m.mask_predictor.multiplier)
-            plan.add_upsample_convex([mask, flow32, out], [B, h, w, stride])
-        else:
-            plan.add_upsample_bilinear([flow32, out], [B, h, w, stride])
-        if all_iters:
-            plan.add_record(E_MASK)
+            upsample(fm, flow32, 0)
         lane(main)
 
     # --------------------------------------------------------------- forward

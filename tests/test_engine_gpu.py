@@ -117,3 +117,18 @@ def test_final_only_mode_equals_last_iteration(factory, use_graph):
     torch.cuda.synchronize()
     assert last.shape == (1,) + tuple(full.shape[1:])
     assert (last[0] - full[-1]).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("flow_head", ["conv", "fused"])
+def test_flow_head_modes_agree(flow_head):
+    """The three lowerings of FlowHead.conv2 + coords update give the same flows."""
+    model, _ = raft_large()
+    model = model.cuda()
+    i1, i2 = _inputs(1, 128, 128, seed=9)
+    i1, i2 = i1.cuda(), i2.cuda()
+    a = model(i1, i2, num_flow_updates=4)
+    b = model(i1, i2, num_flow_updates=4, flow_head=flow_head)
+    torch.cuda.synchronize()
+    mag = a.norm(dim=-1).mean().item()
+    assert _epe(a[-1], b[-1]) < 0.01 * mag + 0.01
+

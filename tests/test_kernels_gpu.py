@@ -69,7 +69,7 @@ def test_conv_matches_reference(case, cfg):
     assert err < 2e-3, err
 
 
-@pytest.mark.parametrize("cfg", [0, 4, 6, 7, 9, 10, 11, 12, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24])
+@pytest.mark.parametrize("cfg", [0, 4, 6, 7, 9, 10, 11, 12, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28])
 def test_conv_epilogues(cfg):
     """relu / residual (pre and post) / alpha / bf16 output / channel offsets."""
     nat = _nat()
@@ -109,7 +109,7 @@ def _gru_ref(h, x, kz, bz, kr, br, kq, bq, pad):
     return (1 - z) * h + z * q
 
 
-@pytest.mark.parametrize("cfg", [None, 0, 6, 8, 9, 10, 11, 12, 13, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24])
+@pytest.mark.parametrize("cfg", [None, 0, 6, 8, 9, 10, 11, 12, 13, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28])
 @pytest.mark.parametrize("hidden,xin,ks,pad", [(128, 256, (1, 5), (0, 2)), (128, 256, (5, 1), (2, 0)),
                                                (96, 146, (3, 3), (1, 1))])
 def test_gru_fused_epilogues(hidden, xin, ks, pad, cfg):
@@ -141,7 +141,7 @@ def test_gru_fused_epilogues(hidden, xin, ks, pad, cfg):
     assert (hx[:, :hidden].float().cpu() - ref.reshape(M, hidden)).abs().max().item() < 2.5e-2
 
 
-@pytest.mark.parametrize("cfg", [None, 5, 11, 3, 9, 15])
+@pytest.mark.parametrize("cfg", [None, 5, 11, 3, 9, 15, 25, 28])
 def test_flow_epilogue(cfg):
     nat = _nat()
     torch.manual_seed(3)
@@ -300,5 +300,61 @@ def test_flow_head_fused(cin):
     assert (cg.cpu() - new).abs().max().item() < tol
     assert (f32.cpu() - flow_ref).abs().max().item() < tol
     assert (hx[:, 16:18].float().cpu() - flow_ref).abs().max().item() < 0.02 * flow_ref.abs().max().item() + 1e-2
+    assert torch.equal(hx[:, 16:18], qx[:, 8:10]) and torch.equal(hx[:, 16:18], f8[:, :2])
+    assert (hx[:, :16] == 0).all() and (hx[:, 18:] == 0).all()
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28])
+def test_conv_bias_map(cfg):
+    """Per-pixel fp32 bias map (the folded context share of the GRU gates):
+    conv(x) + bias + bmap[:, coff:coff+cout] before the activation."""
+    nat = _nat()
+    torch.manual_seed(7)
+    N, H, W, cin, cout = 2, 9, 21, 64, 96
+    x = torch.randn(N, H, W, cin)
+    k = torch.randn(1, 5, cin, cout) * 0.05
+    b = torch.randn(cout) * 0.1
+    bm = torch.randn(N * H * W, 136)
+    base = R.conv2d_nhwc(_bf(x), _bf(k), b, (1, 1), (0, 2)).reshape(-1, cout)
+    spec = nat.make_spec(k, b, (1, 1), (0, 2), device=DEV)
+    xg = x.to(DEV, torch.bfloat16).contiguous()
+    y = torch.zeros(N * H * W, cout, dtype=torch.float32, device=DEV)
+    t, i, a = nat.conv_args(spec, xg, N, H, W, y, act=nat.ACT_SIGMOID, cfg=cfg, bmap=bm.to(DEV), bmap_coff=40)
+    nat.ops().conv(t, i, a)
+    torch.cuda.synchronize()
+    assert _rel(y.cpu(), torch.sigmoid(base + bm[:, 40:40 + cout])) < 3e-3
+
+
+@pytest.mark.parametrize("cfg", [None, 4, 5, 24])
+def test_flow_taps(cfg):
+    """FlowHead.conv2 as a 1x1 conv to 9 x 2 per-tap partials (tap-major
+    output channels) + flow_taps (shifted-partial sum, coords update, flow copies)."""
+    nat = _nat()
+    torch.manual_seed(8)
+    B, h, w, cin = 2, 9, 70, 256
+    M = B * h * w
+    fm = torch.randn(B, h, w, cin) * 0.5
+    k = torch.randn(3, 3, cin, 2) / math.sqrt(9 * cin)
+    b = torch.randn(2) * 0.1
+    coords = torch.randn(M, 2) * 5
+    delta = R.conv2d_nhwc(_bf(fm), _bf(k), b, (1, 1), (1, 1)).reshape(M, 2)
+    new = coords + delta
+    grid = torch.stack(torch.meshgrid(torch.arange(w).float(), torch.arange(h).float(), indexing="xy"), -1)
+    flow_ref = new - grid[None].expand(B, h, w, 2).reshape(M, 2)
+    k18 = k.reshape(9, cin, 2).permute(1, 0, 2).reshape(1, 1, cin, 18)
+    spec = nat.make_spec(k18, torch.zeros(18), device=DEV)
+    taps = torch.zeros(M, 24, device=DEV)
+    fmg = fm.to(DEV, torch.bfloat16).contiguous()
+    nat.ops().conv(*nat.conv_args(spec, fmg, B, h, w, taps, cfg=cfg))
+    cg = coords.to(DEV).contiguous()
+    f32 = torch.zeros(M, 2, device=DEV)
+    hx = torch.zeros(M, 24, device=DEV, dtype=torch.bfloat16)
+    qx = torch.zeros(M, 24, device=DEV, dtype=torch.bfloat16)
+    f8 = torch.zeros(M, 8, device=DEV, dtype=torch.bfloat16)
+    nat.ops().flow_taps([taps, b.to(DEV), cg, f32, hx, qx, f8], [B, h, w, 16, 8])
+    torch.cuda.synchronize()
+    tol = 1e-3 * flow_ref.abs().max().item() + 1e-3
+    assert (cg.cpu() - new).abs().max().item() < tol
+    assert (f32.cpu() - flow_ref).abs().max().item() < tol
     assert torch.equal(hx[:, 16:18], qx[:, 8:10]) and torch.equal(hx[:, 16:18], f8[:, :2])
     assert (hx[:, :16] == 0).all() and (hx[:, 18:] == 0).all()

@@ -59,9 +59,10 @@ def main():
         ("convcorr2", 256, 256, 192, 3, 3, (1, 1)),
         ("convflow2", 128, 128, 64, 3, 3, (1, 1)),
         ("me.conv", 256, 256, 126, 3, 3, (1, 1)),
-        ("gru.a(1x5)", 384, 384, 256, 1, 5, (0, 2)),
-        ("gru.b(1x5)", 384, 384, 128, 1, 5, (0, 2)),
-        ("gru.a(5x1)", 384, 384, 256, 5, 1, (2, 0)),
+        # GRU convs over [h | motion | flow] (the context share is a prologue bias map)
+        ("gru.a(1x5)", 256, 256, 256, 1, 5, (0, 2)),
+        ("gru.b(1x5)", 256, 256, 128, 1, 5, (0, 2)),
+        ("gru.a(5x1)", 256, 256, 256, 5, 1, (2, 0)),
         ("fh1+mask1", 128, 128, 512, 3, 3, (1, 1)),
         ("fh2", 256, 256, 2, 3, 3, (1, 1)),
         ("mask2", 256, 256, 576, 1, 1, (0, 0)),
@@ -76,8 +77,9 @@ def main():
         y = torch.empty(M, nat.round_up(cout, 8), device=dev, dtype=torch.bfloat16)
         flops = 2.0 * M * cout * kh * kw * cin
         row = {}
-        for cfg in sorted(nat.CFG_TILES):
-            t, i, a = nat.conv_args(spec, x, B, h, w, y, act=nat.ACT_RELU, cfg=cfg)
+        bm = torch.randn(M, 384, device=dev) if name.startswith("gru") else None
+        for cfg in nat.TUNE_CFGS:
+            t, i, a = nat.conv_args(spec, x, B, h, w, y, act=nat.ACT_RELU, cfg=cfg, bmap=bm)
             us = timeit(lambda: nat.ops().conv(t, i, a))
             row[cfg] = us
         best = min(row, key=row.get)
