@@ -48,6 +48,9 @@ def main():
                     help="flow head output conv: 1x1 GEMM + tap sum (default), 3x3 conv, or the halo-tiled kernel")
     ap.add_argument("--final-only", action="store_true",
                     help="serving mode: upsample/return only the final flow (not the reference's output)")
+    ap.add_argument("--gate-dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="storage of the GRU z gate / folded context bias map (the hidden state is fp32 either way)")
+    ap.add_argument("--flow-lane", default="side", choices=["side", "main"])
     ap.add_argument("--double-buffer", action="store_true", help="parity double-buffering of the flow head outputs")
     ap.add_argument("--split", type=int, default=1, help="independent batch parts (one hipGraph each) run concurrently per GPU")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -95,7 +98,8 @@ def main():
     def forward(a, b):
         return model(a, b, num_flow_updates=args.iters, use_graph=not args.no_graph, streams=not args.no_streams,
                      split=args.split, flow_head=args.flow_head, return_all_iters=not args.final_only,
-                     double_buffer=args.double_buffer)
+                     double_buffer=args.double_buffer,
+                     gate_dtype=torch.bfloat16 if args.gate_dtype == "bf16" else torch.float32, flow_lane=args.flow_lane)
 
     def run(n, events=None):
         if pf is None:
@@ -170,6 +174,8 @@ def main():
                 "hipgraph": not args.no_graph,
                 "concurrent_branches": not args.no_streams,
                 "flow_head": args.flow_head,
+                "gate_dtype": args.gate_dtype,
+                "flow_lane": args.flow_lane,
                 "batch_parts": args.split,
                 "h2d_in_timed_region": not args.no_h2d,
                 "h2d_overlapped": not (args.no_h2d or args.sync_h2d),

@@ -105,16 +105,25 @@ JR_DEVICE void epi_pixel(const ConvParams& p, float (&v)[NV], int m, int cbase) 
 #pragma unroll
   for (int j = 0; j < NV; ++j) v[j] += (cbase + j < p.cout) ? p.bias[cbase + j] : 0.f;
   if (p.bmap) {
-    const float* bp = p.bmap + (long)m * p.bmap_cstride + p.bmap_coff + cbase;
-    if (full) {
-      float bv[NV];
-      load_f32<NV>(bp, bv);
+    const long bo = (long)m * p.bmap_cstride + p.bmap_coff + cbase;
+    float bv[NV];
+    if (p.bmap_bf16) {
+      const bf16* bp = (const bf16*)p.bmap + bo;
+      if (full) load_bf16<NV>(bp, bv);
+      else {
 #pragma unroll
-      for (int j = 0; j < NV; ++j) v[j] += bv[j];
+        for (int j = 0; j < NV; ++j) bv[j] = (cbase + j < p.cout) ? bf2f(bp[j]) : 0.f;
+      }
     } else {
+      const float* bp = (const float*)p.bmap + bo;
+      if (full) load_f32<NV>(bp, bv);
+      else {
 #pragma unroll
-      for (int j = 0; j < NV; ++j) v[j] += (cbase + j < p.cout) ? bp[j] : 0.f;
+        for (int j = 0; j < NV; ++j) bv[j] = (cbase + j < p.cout) ? bp[j] : 0.f;
+      }
     }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] += bv[j];
   }
   if constexpr (EPI == EPI_STD) {
     if (p.res) {
@@ -175,7 +184,8 @@ JR_DEVICE void epi_pixel(const ConvParams& p, float (&v)[NV], int m, int cbase) 
 #pragma unroll
     for (int j = 0; j < NV; ++j) v[j] = sigmoidf_(v[j]);
     if (cbase < hd) {
-      store_f32<NV>((float*)p.zbuf + (long)m * hd + cbase, v);
+      if (p.z_bf16) store_bf16<NV>((bf16*)p.zbuf + (long)m * hd + cbase, v);
+      else store_f32<NV>((float*)p.zbuf + (long)m * hd + cbase, v);
     } else {
       const int hc = cbase - hd;
       float h[NV];
@@ -187,7 +197,8 @@ JR_DEVICE void epi_pixel(const ConvParams& p, float (&v)[NV], int m, int cbase) 
   } else if constexpr (EPI == EPI_GRU_B) {
     const int hd = p.hidden;
     float z[NV], h[NV];
-    load_f32<NV>((const float*)p.zbuf + (long)m * hd + cbase, z);
+    if (p.z_bf16) load_bf16<NV>((const bf16*)p.zbuf + (long)m * hd + cbase, z);
+    else load_f32<NV>((const float*)p.zbuf + (long)m * hd + cbase, z);
     float* hp = p.h32 + (long)m * hd + cbase;
     load_f32<NV>(hp, h);
 #pragma unroll
@@ -298,7 +309,7 @@ struct FastStage {
   }
 };
 
-template <int BCO, int BP, int WCO, int EPI, bool FAST, int NW = 4>
+template <int BCO, int BP, int WCO, int EPI, bool FAST, int NW = 4, int PIPE = 0>  // PIPE 1: kernel P
 __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(const ConvParams p) {
   constexpr int WP = NW / WCO;
   constexpr int RP = NW * 8;              // staging rows covered by one pass of the block (8 lanes per row)
@@ -461,6 +472,76 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(const ConvParams p)
           acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tm], bfr[tn], acc[tm][tn], 0, 0, 0);
     }
   };
+
+  if constexpr (PIPE == 1) {
+    // Kernel P main loop: the same staging (global loads two stages ahead in
+    // register sets ra/rb, LDS double-buffered, one barrier per stage), but the
+    // MFMA fragments are double-buffered in registers at half-stage (32-deep K)
+    // granularity, so every LDS read burst overlaps MFMAs already issued:
+    //   read F_b (this stage, k 32..63) || MFMAs on F_a (k 0..31)
+    //   stage the next stage into the other LDS buffer, issue its successor's loads
+    //   MFMAs on F_b, barrier, read F_a of the next stage || the F_b MFMAs drain.
+    // In kernel R every wave reads a whole stage right after the barrier and
+    // then multiplies: the LDS burst (~768 array cycles per CU for 16 waves) and
+    // the MFMAs serialise.
+    auto rdfrag = [&](int buf, int kk, bf16x8 (&af)[TM], bf16x8 (&bfr)[TN]) {
+      const bf16* sA = smem + buf * (A_ELEMS + B_ELEMS);
+      const bf16* sB = sA + A_ELEMS;
+      const int chunk = kk * 4 + lq;
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int row = wco * WTCO + tm * 16 + li;
+        af[tm] = *(const bf16x8*)(sA + row * BK + ((chunk ^ swzB(row)) << 3));
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int row = wp * WTP + tn * 16 + li;
+        bfr[tn] = *(const bf16x8*)(sB + row * BK + ((chunk ^ swzB(row)) << 3));
+      }
+    };
+    auto mma = [&](const bf16x8 (&af)[TM], const bf16x8 (&bfr)[TN]) {
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tm], bfr[tn], acc[tm][tn], 0, 0, 0);
+    };
+    bf16x8 fa[TM], fb[TN], ga[TM], gb[TN];   // F_a = (fa, fb), F_b = (ga, gb)
+    const int nks = p.kpad / BK;
+    issue(ra);          // stage 0
+    issue(rb);          // stage 1
+    store(ra, 0);
+    __syncthreads();
+    issue(ra);          // stage 2
+    rdfrag(0, 0, fa, fb);
+    const int npairs = nks >> 1;
+    for (int it = 0; it < npairs; ++it) {
+      // stage 2it (LDS buffer 0)
+      rdfrag(0, 1, ga, gb);
+      mma(fa, fb);
+      store(rb, 1);     // stage 2it+1
+      issue(rb);        // stage 2it+3
+      mma(ga, gb);
+      __syncthreads();
+      rdfrag(1, 0, fa, fb);
+      // stage 2it+1 (LDS buffer 1)
+      rdfrag(1, 1, ga, gb);
+      mma(fa, fb);
+      store(ra, 0);     // stage 2it+2
+      issue(ra);        // stage 2it+4
+      mma(ga, gb);
+      __syncthreads();
+      rdfrag(0, 0, fa, fb);
+    }
+    if (nks & 1) {      // stage nks-1 (buffer 0, F_a already read)
+      rdfrag(0, 1, ga, gb);
+      mma(fa, fb);
+      mma(ga, gb);
+    }
+    const int wrow0 = co0 + wco * WTCO;
+    conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, wrow0, lq, li);
+    return;
+  }
 
   // Software pipeline: global loads run two K-stages ahead of the MFMAs
   // (register sets ra/rb alternate, LDS double-buffered, one barrier per
@@ -893,7 +974,11 @@ int launch_cfg(const ConvParams* p, int epi, hipStream_t s) {
   dim3 grid((p->M + BP - 1) / BP, (rows + BCO - 1) / BCO);
   dim3 block(256);
 #define JR_LAUNCH(E)                                                                          \
-  if constexpr (KIND == 6 || KIND == 7) {                                                     \
+  if constexpr (KIND == 9 || KIND == 11) {                                                     \
+    constexpr int NW_ = KIND == 9 ? 8 : 16;                                                      \
+    if (p->fast) hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, true, NW_, 1>), grid, dim3(NW_ * 64), 0, s, *p); \
+    else hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, false, NW_, 1>), grid, dim3(NW_ * 64), 0, s, *p);         \
+  } else if constexpr (KIND == 6 || KIND == 7) {                                                     \
     constexpr int NW_ = KIND == 6 ? 8 : 16;                                                    \
     if (p->fast) hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, true, NW_>), grid, dim3(NW_ * 64), 0, s, *p); \
     else hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, false, NW_>), grid, dim3(NW_ * 64), 0, s, *p);         \

@@ -56,9 +56,11 @@ struct ConvParams {
   float* coords;    // FLOW: fp32 [M][2]
   float* flow32;    // FLOW: fp32 [M][2]
   void* y3; int y3_cstride, y3_coff;  // FLOW: third bf16 flow copy
-  // optional fp32 per-pixel bias map [M][bmap_cstride], channels [bmap_coff, bmap_coff + cout),
+  // optional fp32 / bf16 per-pixel bias map [M][bmap_cstride], channels [bmap_coff, bmap_coff + cout),
   // added with the bias (e.g. the loop-invariant context-feature part of the ConvGRU gates)
-  const float* bmap; int bmap_cstride, bmap_coff;
+  const void* bmap; int bmap_cstride, bmap_coff;
+  int bmap_bf16;    // bias map stored as bf16 (else fp32)
+  int z_bf16;       // GRU: z gate buffer stored as bf16 (else fp32)
   // 1 when every 64-deep K stage lies inside one tap (a 1x1 conv, or cin8 % 64 == 0 with at most
   // 32 taps) and there is no input dilation: the register-staged kernels then use wave-uniform
   // tap state and per-row tap bitmasks instead of per-lane im2col arithmetic

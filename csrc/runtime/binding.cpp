@@ -104,13 +104,17 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   p.coords = coords.defined() ? coords.data_ptr<float>() : nullptr;
   p.flow32 = flow32.defined() ? flow32.data_ptr<float>() : nullptr;
   p.y3 = ptr(y3); p.y3_cstride = cs(y3); p.y3_coff = (int)i[18];
-  p.bmap = bmap.defined() ? bmap.data_ptr<float>() : nullptr;
+  p.bmap = ptr(bmap);
   p.bmap_cstride = bmap.defined() ? cs(bmap) : 0;
   p.bmap_coff = i.size() == 27 ? (int)i[26] : 0;
+  p.bmap_bf16 = bmap.defined() && bmap.scalar_type() == at::kBFloat16;
+  p.z_bf16 = zbuf.defined() && zbuf.scalar_type() == at::kBFloat16;
   if (bmap.defined()) {
-    check_f32(bmap, "bmap");
-    TORCH_CHECK(p.bmap_cstride % 4 == 0 && p.bmap_coff % 4 == 0 && p.bmap_coff + p.cout <= p.bmap_cstride,
-                "conv: bias map channel slice must be 4-aligned and inside the tensor");
+    TORCH_CHECK(bmap.is_cuda() && bmap.is_contiguous() &&
+                    (bmap.scalar_type() == at::kFloat || bmap.scalar_type() == at::kBFloat16),
+                "conv: bias map must be a contiguous fp32 / bf16 GPU tensor");
+    TORCH_CHECK(p.bmap_cstride % 8 == 0 && p.bmap_coff % 8 == 0 && p.bmap_coff + p.cout <= p.bmap_cstride,
+                "conv: bias map channel slice must be 8-aligned and inside the tensor");
     TORCH_CHECK(bmap.numel() >= (int64_t)p.M * p.bmap_cstride, "conv: bias map too small");
   }
   {
@@ -144,11 +148,17 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
     if (res.defined()) { check_bf16(res, "res"); TORCH_CHECK(p.res_cstride % 8 == 0 && p.res_coff % 8 == 0, "res align"); }
     if (h32.defined()) { check_f32(h32, "h32"); TORCH_CHECK(h32.numel() >= (int64_t)p.M * p.hidden, "h32 size"); }
   } else if (epi == EPI_GRU_A) {
-    check_f32(h32, "h32"); check_f32(zbuf, "zbuf"); check_bf16(y, "y");
+    check_f32(h32, "h32"); check_bf16(y, "y");
+    TORCH_CHECK(zbuf.defined() && zbuf.is_cuda() && zbuf.is_contiguous() &&
+                    (zbuf.scalar_type() == at::kFloat || zbuf.scalar_type() == at::kBFloat16) &&
+                    zbuf.numel() >= (int64_t)p.M * p.hidden, "GRU: zbuf must be an fp32 / bf16 [M][hidden] GPU tensor");
     TORCH_CHECK(p.cout == 2 * p.hidden && p.hidden % 16 == 0, "GRU-A: cout must be 2*hidden, hidden % 16 == 0");
     TORCH_CHECK(p.y_coff % 8 == 0, "GRU-A align");
   } else if (epi == EPI_GRU_B) {
-    check_f32(h32, "h32"); check_f32(zbuf, "zbuf"); check_bf16(y, "y");
+    check_f32(h32, "h32"); check_bf16(y, "y");
+    TORCH_CHECK(zbuf.defined() && zbuf.is_cuda() && zbuf.is_contiguous() &&
+                    (zbuf.scalar_type() == at::kFloat || zbuf.scalar_type() == at::kBFloat16) &&
+                    zbuf.numel() >= (int64_t)p.M * p.hidden, "GRU: zbuf must be an fp32 / bf16 [M][hidden] GPU tensor");
     TORCH_CHECK(p.cout == p.hidden && p.hidden % 16 == 0, "GRU-B: cout must be hidden");
     TORCH_CHECK(p.y_coff % 8 == 0, "GRU-B align");
     if (y2.defined()) { check_bf16(y2, "y2"); TORCH_CHECK(p.y2_coff % 8 == 0, "y2 align"); }
@@ -158,7 +168,7 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   } else {
     TORCH_CHECK(false, "conv: unknown epilogue ", epi);
   }
-  TORCH_CHECK(cfg >= 0 && cfg <= 28, "conv: unknown tile config ", cfg);
+  TORCH_CHECK(cfg >= 0 && cfg <= 34 && !(cfg >= 29 && cfg <= 32), "conv: unknown tile config ", cfg);
   if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3, bmap}) if (v.defined()) keep->push_back(v);
   return [p, epi, cfg](hipStream_t s, int) { return jr_conv_forward(&p, cfg, epi, s); };
 }

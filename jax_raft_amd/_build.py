@@ -27,6 +27,7 @@ KERNEL_SOURCES = [
     CSRC / "kernels" / "conv_igemm.hip",
     CSRC / "kernels" / "conv_fam_r.hip",
     CSRC / "kernels" / "conv_fam_rw.hip",
+    CSRC / "kernels" / "conv_fam_p.hip",
     CSRC / "kernels" / "conv_fam_m32.hip",
     CSRC / "kernels" / "conv_fam_d2.hip",
     CSRC / "kernels" / "corr.hip",

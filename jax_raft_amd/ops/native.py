@@ -38,10 +38,12 @@ CFG_TILES.update({18: (128, 128), 19: (128, 128), 20: (256, 128)})
 CFG_TILES.update({21: (128, 128), 22: (256, 128), 23: (128, 64), 24: (64, 128)})
 # configs 25..28: kernel M32 with 8 waves (64x64 / 64x64 / 64x32 / 64x32 wave tiles)
 CFG_TILES.update({25: (256, 128), 26: (128, 256), 27: (128, 128), 28: (64, 256)})
+# configs 33/34: kernel P (register double-buffered fragments), 8 / 16 waves
+CFG_TILES.update({33: (128, 128), 34: (256, 128)})
 # Autotune candidates: configs that win at least one RAFT conv on MI355X
 # (tools/microbench.py, profiles/r1_microbench_conv_cfgs.txt); the others stay
 # compiled and tested but are not timed at plan build.
-TUNE_CFGS = (0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28)
+TUNE_CFGS = (0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34)
 NUM_CUS = 256
 
 

@@ -140,6 +140,12 @@ class RaftEngine:
         split: run the batch as this many independent half-forwards on
             separate lanes (when the batch divides evenly), so that one
             part's kernels fill the CUs another part's leave idle.
+        gate_dtype: storage dtype of the ConvGRU z gate and of the folded
+            context bias map (bf16 default, fp32 for bit-closer parity); the
+            hidden state itself is always carried in fp32.
+        flow_lane: "side" runs the motion encoder's flow-feature convs on a side
+            lane concurrently with the lookup + correlation convs; "main" runs
+            them on the critical-path lane before the lookup.
         double_buffer: ("lanes" schedule) double-buffer the flow head outputs by iteration
             parity, so iteration i+1's flow head need not wait for iteration
             i's mask head (otherwise one buffer and a WAR wait).  Off by
@@ -150,8 +156,12 @@ class RaftEngine:
     def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True,
                  corr_dtype: torch.dtype = torch.bfloat16, autotune: bool = True, streams: bool = True,
                  split: int = 1, flow_head: str = "taps", double_buffer: bool = False,
-                 fused_flow_head: bool = False):
+                 fused_flow_head: bool = False, gate_dtype: torch.dtype = torch.bfloat16,
+                 flow_lane: str = "side"):
         nat.require()
+        self.gate_dtype = gate_dtype
+        assert flow_lane in ("side", "main"), flow_lane
+        self.flow_lane = flow_lane if streams else "main"
         self.double_buffer = double_buffer
         self.flow_head = "fused" if fused_flow_head else flow_head
         assert self.flow_head in ("taps", "conv", "fused"), self.flow_head
@@ -472,7 +482,7 @@ class RaftEngine:
         hx = alloc("hx", (M, self.hx_cs))
         qx = alloc("qx", (M, self.hx_cs))
         h32 = alloc("h32", (M, self.hidden), F32)
-        zb = alloc("z", (M, self.hidden), F32)
+        zb = alloc("z", (M, self.hidden), self.gate_dtype)
         flow8 = alloc("flow8", (M, 8))
         coords = alloc("coords", (M, 2), F32)
         flow32 = alloc("flow32", (M, 2), F32)
@@ -494,7 +504,7 @@ class RaftEngine:
         # loop-invariant context share of every GRU gate (+ gate biases), fp32
         gbias = []
         for gi in range(len(m.update_block.recurrent_block.kernel_size)):
-            gb = alloc(f"gru{gi}.cbias", (M, self.gate_cs), F32)
+            gb = alloc(f"gru{gi}.cbias", (M, self.gate_cs), self.gate_dtype)
             self._conv(plan, sp[f"gru{gi}.ctx"], ce_out, B, h, w, gb, x_coff=self.hidden)
             gbias.append(gb)
         plan.add_init_coords([coords], [B, h, w])
@@ -557,12 +567,15 @@ class RaftEngine:
             else:
                 plan.add_upsample_bilinear([f32, out], [B, h, w, stride])
 
-        plan.add_record(E_IT)
-        lane(side)
-        plan.add_wait(E_IT)
-        flow_features()
-        plan.add_record(E_FLOW)
-        lane(main)
+        if self.flow_lane == "side":
+            plan.add_record(E_IT)
+            lane(side)
+            plan.add_wait(E_IT)
+            flow_features()
+            plan.add_record(E_FLOW)
+            lane(main)
+        else:
+            flow_features()
         plan.add_lookup([coords, corr] + levels + [None] * (4 - L), [L, B, h, w, self.radius])
         if len(cl) == 2:
             c1 = alloc("c1", (M, cl[0]))
@@ -570,7 +583,8 @@ class RaftEngine:
             self._conv(plan, sp["me.convcorr2"], c1, B, h, w, cf, act=ACT_RELU)
         else:
             self._conv(plan, sp["me.convcorr1"], corr, B, h, w, cf, act=ACT_RELU)
-        plan.add_wait(E_FLOW)
+        if self.flow_lane == "side":
+            plan.add_wait(E_FLOW)
         self._conv(plan, sp["me.conv"], cf, B, h, w, hx, y_coff=self.mot_off, act=ACT_RELU, y2=qx,
                    y2_coff=self.mot_off)
         for gi in range(len(m.update_block.recurrent_block.kernel_size)):

@@ -69,7 +69,7 @@ def test_conv_matches_reference(case, cfg):
     assert err < 2e-3, err
 
 
-@pytest.mark.parametrize("cfg", [0, 4, 6, 7, 9, 10, 11, 12, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28])
+@pytest.mark.parametrize("cfg", [0, 4, 6, 7, 9, 10, 11, 12, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34])
 def test_conv_epilogues(cfg):
     """relu / residual (pre and post) / alpha / bf16 output / channel offsets."""
     nat = _nat()
@@ -109,7 +109,7 @@ def _gru_ref(h, x, kz, bz, kr, br, kq, bq, pad):
     return (1 - z) * h + z * q
 
 
-@pytest.mark.parametrize("cfg", [None, 0, 6, 8, 9, 10, 11, 12, 13, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28])
+@pytest.mark.parametrize("cfg", [None, 0, 6, 8, 9, 10, 11, 12, 13, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34])
 @pytest.mark.parametrize("hidden,xin,ks,pad", [(128, 256, (1, 5), (0, 2)), (128, 256, (5, 1), (2, 0)),
                                                (96, 146, (3, 3), (1, 1))])
 def test_gru_fused_epilogues(hidden, xin, ks, pad, cfg):
@@ -304,7 +304,7 @@ def test_flow_head_fused(cin):
     assert (hx[:, :16] == 0).all() and (hx[:, 18:] == 0).all()
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34])
 def test_conv_bias_map(cfg):
     """Per-pixel fp32 bias map (the folded context share of the GRU gates):
     conv(x) + bias + bmap[:, coff:coff+cout] before the activation."""
@@ -323,6 +323,12 @@ def test_conv_bias_map(cfg):
     nat.ops().conv(t, i, a)
     torch.cuda.synchronize()
     assert _rel(y.cpu(), torch.sigmoid(base + bm[:, 40:40 + cout])) < 3e-3
+    # bf16 bias map
+    t, i, a = nat.conv_args(spec, xg, N, H, W, y, act=nat.ACT_SIGMOID, cfg=cfg, bmap=bm.to(DEV, torch.bfloat16),
+                            bmap_coff=40)
+    nat.ops().conv(t, i, a)
+    torch.cuda.synchronize()
+    assert _rel(y.cpu(), torch.sigmoid(base + _bf(bm[:, 40:40 + cout]))) < 3e-3
 
 
 @pytest.mark.parametrize("cfg", [None, 4, 5, 24])
