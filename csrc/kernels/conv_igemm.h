@@ -179,7 +179,10 @@ JR_DEVICE void epi_pixel(const ConvParams& p, float (&v)[NV], int m, int cbase) 
       }
     }
   } else if constexpr (EPI == EPI_GRU_A) {
-    // [z | r] logits -> z (fp32) and r*h (bf16) into the q-input buffer.
+    // [z | r] logits -> z (fp32 / bf16) and r*h (bf16) into the q-input buffer.
+    // h comes from the fp32 state when given, else from the conv's own bf16
+    // input (channels [x_coff, x_coff + hidden) of the same pixel: the GRU
+    // input [h | ...] at stride 1): half the bytes, usually still L2-resident.
     const int hd = p.hidden;
 #pragma unroll
     for (int j = 0; j < NV; ++j) v[j] = sigmoidf_(v[j]);
@@ -189,7 +192,8 @@ JR_DEVICE void epi_pixel(const ConvParams& p, float (&v)[NV], int m, int cbase) 
     } else {
       const int hc = cbase - hd;
       float h[NV];
-      load_f32<NV>(p.h32 + (long)m * hd + hc, h);
+      if (p.h32) load_f32<NV>(p.h32 + (long)m * hd + hc, h);
+      else load_bf16<NV>((const bf16*)p.x + (long)m * p.x_cstride + p.x_coff + hc, h);
 #pragma unroll
       for (int j = 0; j < NV; ++j) v[j] *= h[j];
       store_bf16<NV>((bf16*)p.y + (long)m * p.y_cstride + p.y_coff + hc, v);

@@ -148,7 +148,10 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
     if (res.defined()) { check_bf16(res, "res"); TORCH_CHECK(p.res_cstride % 8 == 0 && p.res_coff % 8 == 0, "res align"); }
     if (h32.defined()) { check_f32(h32, "h32"); TORCH_CHECK(h32.numel() >= (int64_t)p.M * p.hidden, "h32 size"); }
   } else if (epi == EPI_GRU_A) {
-    check_f32(h32, "h32"); check_bf16(y, "y");
+    if (h32.defined()) check_f32(h32, "h32");
+    else TORCH_CHECK(p.OH == p.H && p.OW == p.W && p.dsh == 0 && p.dsw == 0 && p.x_coff + p.hidden <= p.x_cstride,
+                     "GRU-A without h32 reads h from its stride-1 input [h | ...]");
+    check_bf16(y, "y");
     TORCH_CHECK(zbuf.defined() && zbuf.is_cuda() && zbuf.is_contiguous() &&
                     (zbuf.scalar_type() == at::kFloat || zbuf.scalar_type() == at::kBFloat16) &&
                     zbuf.numel() >= (int64_t)p.M * p.hidden, "GRU: zbuf must be an fp32 / bf16 [M][hidden] GPU tensor");

@@ -588,7 +588,8 @@ class RaftEngine:
         self._conv(plan, sp["me.conv"], cf, B, h, w, hx, y_coff=self.mot_off, act=ACT_RELU, y2=qx,
                    y2_coff=self.mot_off)
         for gi in range(len(m.update_block.recurrent_block.kernel_size)):
-            self._conv(plan, sp[f"gru{gi}.a"], hx, B, h, w, qx, h32=h32, zbuf=zb, hidden=self.hidden,
+            # r*h from the bf16 h of the conv's own input hx (no fp32 state read)
+            self._conv(plan, sp[f"gru{gi}.a"], hx, B, h, w, qx, zbuf=zb, hidden=self.hidden,
                        epi=EPI_GRU_A, bmap=gbias[gi], bmap_coff=0)
             self._conv(plan, sp[f"gru{gi}.b"], qx, B, h, w, hx, h32=h32, zbuf=zb, hidden=self.hidden,
                        epi=EPI_GRU_B, bmap=gbias[gi], bmap_coff=2 * self.hidden)
