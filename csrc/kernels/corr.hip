@@ -44,7 +44,7 @@ JR_DEVICE float to_f(bf16 v) { return bf2f(v); }
 
 template <typename T>
 __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restrict__ f1, const bf16* __restrict__ f2,
-                                                           int h, int w, int C, int cs, T* __restrict__ l0,
+                                                           int h, int w, int nq, int C, int cs, T* __restrict__ l0,
                                                            T* __restrict__ l1, T* __restrict__ l2,
                                                            T* __restrict__ l3, int nlev, float scale) {
   constexpr int TM = 2, TN = 8;
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restric
   const int tx0 = (blockIdx.y % ntx) * TX;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ch = tid & 7;
-  const bf16* A = f1 + (long)b * P * cs;
+  const bf16* A = f1 + (long)b * nq * cs;
   const bf16* Bm = f2 + (long)b * P * cs;
 
   // each thread loads 4 query rows and 4 target rows (chunk ch of 8)
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restric
   for (int i = 0; i < 4; ++i) {
     const int r = (tid >> 3) + 32 * i;
     const int q = q0 + r;
-    aok[i] = q < P;
+    aok[i] = q < nq;
     aoff[i] = (long)(aok[i] ? q : 0) * cs;
     const int ty = ty0 + (r >> 4), tx = tx0 + (r & 15);
     bok[i] = ty < h && tx < w;
@@ -140,13 +140,13 @@ __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restric
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int q = q0 + wave * (TM * 16) + tm * 16 + 4 * lq + r;
-      const bool qok = q < P;
+      const bool qok = q < nq;
       float v[TN];
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) v[tn] = acc[tm][tn][r] * scale;
       // level 0
       if (qok && x0 < w) {
-        T* dst = l0 + ((long)b * P + q) * P;
+        T* dst = l0 + ((long)b * nq + q) * P;
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn)
           if (ty0 + tn < h) dst[(ty0 + tn) * w + x0] = cvt_out<T>(v[tn]);
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restric
       {
         const int X1 = x0 >> 1;
         if (qok && (li & 1) == 0 && X1 < w1) {
-          T* dst = l1 + ((long)b * P + q) * (h1 * w1);
+          T* dst = l1 + ((long)b * nq + q) * (h1 * w1);
 #pragma unroll
           for (int t = 0; t < TN / 2; ++t) {
             const int Y1 = (ty0 >> 1) + t;
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restric
       {
         const int X2 = x0 >> 2;
         if (qok && (li & 3) == 0 && X2 < w2) {
-          T* dst = l2 + ((long)b * P + q) * (h2 * w2);
+          T* dst = l2 + ((long)b * nq + q) * (h2 * w2);
 #pragma unroll
           for (int t = 0; t < TN / 4; ++t) {
             const int Y2 = (ty0 >> 2) + t;
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restric
         const int X3 = x0 >> 3;
         const int Y3 = ty0 >> 3;
         if (qok && (li & 7) == 0 && X3 < w3 && Y3 < h3) {
-          l3[((long)b * P + q) * (h3 * w3) + Y3 * w3 + X3] = cvt_out<T>(v3);
+          l3[((long)b * nq + q) * (h3 * w3) + Y3 * w3 + X3] = cvt_out<T>(v3);
         }
       }
     }
@@ -341,40 +341,41 @@ int launch_lookup(const LevelPtrs& lv, int L, int total, int h, int w, int r, co
 
 }  // namespace
 
-extern "C" int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int w, int C, int cs, void* lvl0,
+extern "C" int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int w, int nq, int C, int cs, void* lvl0,
                                void* lvl1, void* lvl2, void* lvl3, int num_levels, float scale, int out_bf16,
                                hipStream_t stream) {
-  if (C % BK != 0 || cs % 8 != 0 || num_levels < 1 || num_levels > 4) return (int)hipErrorInvalidValue;
-  const int P = h * w;
-  dim3 grid((P + CQ - 1) / CQ, ((h + TY - 1) / TY) * ((w + TX - 1) / TX), B);
+  if (C % BK != 0 || cs % 8 != 0 || num_levels < 1 || num_levels > 4 || nq < 1) return (int)hipErrorInvalidValue;
+  dim3 grid((nq + CQ - 1) / CQ, ((h + TY - 1) / TY) * ((w + TX - 1) / TX), B);
   if (out_bf16)
-    hipLaunchKernelGGL(corr_pyramid_kernel<bf16>, grid, dim3(256), 0, stream, (const bf16*)f1, (const bf16*)f2, h, w, C,
-                       cs, (bf16*)lvl0, (bf16*)lvl1, (bf16*)lvl2, (bf16*)lvl3, num_levels, scale);
+    hipLaunchKernelGGL(corr_pyramid_kernel<bf16>, grid, dim3(256), 0, stream, (const bf16*)f1, (const bf16*)f2, h, w,
+                       nq, C, cs, (bf16*)lvl0, (bf16*)lvl1, (bf16*)lvl2, (bf16*)lvl3, num_levels, scale);
   else
     hipLaunchKernelGGL(corr_pyramid_kernel<float>, grid, dim3(256), 0, stream, (const bf16*)f1, (const bf16*)f2, h, w,
-                       C, cs, (float*)lvl0, (float*)lvl1, (float*)lvl2, (float*)lvl3, num_levels, scale);
+                       nq, C, cs, (float*)lvl0, (float*)lvl1, (float*)lvl2, (float*)lvl3, num_levels, scale);
   return (int)hipGetLastError();
 }
 
-extern "C" int jr_corr_lookup(const void* const* levels, int num_levels, int B, int h, int w, int radius,
+// h, w: the (target) level-0 map size; nq: query pixels per image (h * w
+// unless the queries are a slab of rows, cp.py).
+extern "C" int jr_corr_lookup(const void* const* levels, int num_levels, int B, int h, int w, int nq, int radius,
                               const float* coords, void* out, int out_cstride, int lv_bf16, hipStream_t stream) {
   const int S = 2 * radius + 1;
   if (num_levels > 4 || radius < 1 || radius > 6 || out_cstride % 8 != 0 || out_cstride < num_levels * S * S)
     return (int)hipErrorInvalidValue;
   LevelPtrs lv;
   for (int l = 0; l < 4; ++l) lv.p[l] = l < num_levels ? levels[l] : nullptr;
-  const int total = B * h * w;
+  const int total = B * nq;
   if (lv_bf16) return launch_lookup<bf16>(lv, num_levels, total, h, w, radius, coords, (bf16*)out, out_cstride, stream);
   return launch_lookup<float>(lv, num_levels, total, h, w, radius, coords, (bf16*)out, out_cstride, stream);
 }
 
-extern "C" int jr_corr_lookup_bwd(void* const* dlevels, int num_levels, int B, int h, int w, int radius,
+extern "C" int jr_corr_lookup_bwd(void* const* dlevels, int num_levels, int B, int h, int w, int nq, int radius,
                                   const float* coords, const void* gout, int gcs, int g_bf16, hipStream_t stream) {
   const int S = 2 * radius + 1;
   if (num_levels > 4 || radius < 1 || radius > 6 || gcs < num_levels * S * S) return (int)hipErrorInvalidValue;
   LevelPtrs lv;
   for (int l = 0; l < 4; ++l) lv.p[l] = l < num_levels ? dlevels[l] : nullptr;
-  const int total = B * h * w;
+  const int total = B * nq;
   dim3 grid((total + 3) / 4);
   switch (radius) {
 #define JR_LB(RR)                                                                                               \

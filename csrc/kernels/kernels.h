@@ -92,18 +92,20 @@ int jr_norm_act(const void* x, const float* sx, int mode_x, const float* gamma, 
 // ---------------------------------------------------------------------------
 // Correlation pyramid (MFMA all-pairs GEMM, pooling fused) and lookup.
 // ---------------------------------------------------------------------------
-// f1, f2: bf16 [B][h*w][C] (channel stride cs).  levels[l]: fp32 or bf16 [B][h*w][h_l][w_l].
-int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int w, int C, int cs,
+// f1: bf16 [B][nq][C] query pixels (nq = h*w, or a slab of query rows for
+// context parallelism), f2: bf16 [B][h*w][C] (channel stride cs of both).
+// levels[l]: fp32 or bf16 [B][nq][h_l][w_l].
+int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int w, int nq, int C, int cs,
                     void* lvl0, void* lvl1, void* lvl2, void* lvl3, int num_levels, float scale, int out_bf16,
                     hipStream_t stream);
-// coords fp32 [B][h*w][2]; out bf16 [B*h*w][out_cstride] channels l*(2r+1)^2 + i*(2r+1) + j,
-// zero-filled up to out_cstride.  radius 1..6.
-int jr_corr_lookup(const void* const* levels, int num_levels, int B, int h, int w, int radius,
+// coords fp32 [B][nq][2]; out bf16 [B*nq][out_cstride] channels l*(2r+1)^2 + i*(2r+1) + j,
+// zero-filled up to out_cstride.  h, w: level-0 map size.  radius 1..6.
+int jr_corr_lookup(const void* const* levels, int num_levels, int B, int h, int w, int nq, int radius,
                    const float* coords, void* out, int out_cstride, int lv_bf16, hipStream_t stream);
 
 // Backward of jr_corr_lookup w.r.t. the levels: accumulates into fp32 dlevels
-// (same shapes as the levels).  gout: bf16 (g_bf16=1) or fp32 [B*h*w][gcs].
-int jr_corr_lookup_bwd(void* const* dlevels, int num_levels, int B, int h, int w, int radius,
+// (same shapes as the levels).  gout: bf16 (g_bf16=1) or fp32 [B*nq][gcs].
+int jr_corr_lookup_bwd(void* const* dlevels, int num_levels, int B, int h, int w, int nq, int radius,
                        const float* coords, const void* gout, int gcs, int g_bf16, hipStream_t stream);
 
 // ---------------------------------------------------------------------------

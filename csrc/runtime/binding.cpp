@@ -252,9 +252,12 @@ static Launch make_corr(const TList& t, const IList& i, double scale, std::vecto
   at::Tensor f1 = opt(t, 0), f2 = opt(t, 1);
   check_bf16(f1, "f1"); check_bf16(f2, "f2");
   const int B = (int)i[0], h = (int)i[1], w = (int)i[2], C = (int)i[3], L = (int)i[4];
+  // optional i[5]: query pixels per image in f1 (a slab of query rows; default all h*w)
+  const int nq = i.size() > 5 ? (int)i[5] : h * w;
   TORCH_CHECK(L >= 1 && L <= 4, "corr: 1..4 levels");
   TORCH_CHECK(C % 64 == 0, "corr: feature channels must be a multiple of 64");
-  TORCH_CHECK(f1.numel() >= (int64_t)B * h * w * cs(f1) && f2.numel() == f1.numel() && cs(f1) == cs(f2), "corr: fmap shapes");
+  TORCH_CHECK(nq >= 1 && f1.numel() >= (int64_t)B * nq * cs(f1) && f2.numel() >= (int64_t)B * h * w * cs(f2) &&
+              cs(f1) == cs(f2), "corr: fmap shapes");
   void* lv[4] = {nullptr, nullptr, nullptr, nullptr};
   at::Tensor l0 = opt(t, 2);
   TORCH_CHECK(l0.defined(), "corr: level 0 missing");
@@ -263,7 +266,7 @@ static Launch make_corr(const TList& t, const IList& i, double scale, std::vecto
   for (int l = 0; l < L; ++l) {
     at::Tensor v = opt(t, 2 + l);
     check_level(v, dt);
-    TORCH_CHECK(v.numel() >= (int64_t)B * h * w * hl * wl, "corr: level ", l, " too small");
+    TORCH_CHECK(v.numel() >= (int64_t)B * nq * hl * wl, "corr: level ", l, " too small");
     lv[l] = v.data_ptr();
     if (keep) keep->push_back(v);
     hl >>= 1; wl >>= 1;
@@ -274,7 +277,7 @@ static Launch make_corr(const TList& t, const IList& i, double scale, std::vecto
   const int fcs = cs(f1);
   const float sc = (float)scale;
   const int obf = dt == at::kBFloat16;
-  return [=](hipStream_t s, int) { return jr_corr_pyramid(a, b, B, h, w, C, fcs, lv[0], lv[1], lv[2], lv[3], L, sc, obf, s); };
+  return [=](hipStream_t s, int) { return jr_corr_pyramid(a, b, B, h, w, nq, C, fcs, lv[0], lv[1], lv[2], lv[3], L, sc, obf, s); };
 }
 
 // t = [coords, out, l0, l1, l2, l3], i = [num_levels, B, h, w, radius]
@@ -282,10 +285,11 @@ static Launch make_lookup(const TList& t, const IList& i, std::vector<at::Tensor
   at::Tensor coords = opt(t, 0), out = opt(t, 1);
   check_f32(coords, "coords"); check_bf16(out, "out");
   const int L = (int)i[0], B = (int)i[1], h = (int)i[2], w = (int)i[3], r = (int)i[4];
+  const int nq = i.size() > 5 ? (int)i[5] : h * w;  // queries per image (slab of rows) vs level-0 map h x w
   const int S = 2 * r + 1;
-  TORCH_CHECK(L >= 1 && L <= 4 && r >= 1 && r <= 6, "lookup: levels 1..4, radius 1..6");
+  TORCH_CHECK(L >= 1 && L <= 4 && r >= 1 && r <= 6 && nq >= 1, "lookup: levels 1..4, radius 1..6");
   TORCH_CHECK(cs(out) % 8 == 0 && cs(out) >= L * S * S, "lookup: output channel stride");
-  TORCH_CHECK(out.numel() >= (int64_t)B * h * w * cs(out) && coords.numel() >= (int64_t)B * h * w * 2, "lookup: sizes");
+  TORCH_CHECK(out.numel() >= (int64_t)B * nq * cs(out) && coords.numel() >= (int64_t)B * nq * 2, "lookup: sizes");
   std::vector<const void*> lv(4, nullptr);
   at::Tensor l0 = opt(t, 2);
   TORCH_CHECK(l0.defined(), "lookup: level 0 missing");
@@ -295,7 +299,7 @@ static Launch make_lookup(const TList& t, const IList& i, std::vector<at::Tensor
     at::Tensor v = opt(t, 2 + l);
     check_level(v, dt);
     TORCH_CHECK(hl >= 2 && wl >= 2, "lookup: pyramid level too small");
-    TORCH_CHECK(v.numel() >= (int64_t)B * h * w * hl * wl, "lookup: level size");
+    TORCH_CHECK(v.numel() >= (int64_t)B * nq * hl * wl, "lookup: level size");
     lv[l] = v.data_ptr();
     if (keep) keep->push_back(v);
     hl >>= 1; wl >>= 1;
@@ -305,7 +309,7 @@ static Launch make_lookup(const TList& t, const IList& i, std::vector<at::Tensor
   void* op = out.data_ptr();
   const int ocs = cs(out);
   const int lbf = dt == at::kBFloat16;
-  return [=](hipStream_t s, int) { return jr_corr_lookup(lv.data(), L, B, h, w, r, cp, op, ocs, lbf, s); };
+  return [=](hipStream_t s, int) { return jr_corr_lookup(lv.data(), L, B, h, w, nq, r, cp, op, ocs, lbf, s); };
 }
 
 // ------------------------------------------------------------------ upsample
@@ -472,15 +476,16 @@ static Launch make_lookup_bwd(const TList& t, const IList& i, std::vector<at::Te
   TORCH_CHECK(g.defined() && g.is_cuda() && g.is_contiguous() &&
               (g.scalar_type() == at::kFloat || g.scalar_type() == at::kBFloat16), "lookup_bwd: grad");
   const int L = (int)i[0], B = (int)i[1], h = (int)i[2], w = (int)i[3], r = (int)i[4];
+  const int nq = i.size() > 5 ? (int)i[5] : h * w;
   const int S = 2 * r + 1;
-  TORCH_CHECK(L >= 1 && L <= 4 && r >= 1 && r <= 6 && cs(g) >= L * S * S, "lookup_bwd: shape");
-  TORCH_CHECK(g.numel() >= (int64_t)B * h * w * cs(g), "lookup_bwd: grad size");
+  TORCH_CHECK(L >= 1 && L <= 4 && r >= 1 && r <= 6 && nq >= 1 && cs(g) >= L * S * S, "lookup_bwd: shape");
+  TORCH_CHECK(g.numel() >= (int64_t)B * nq * cs(g) && coords.numel() >= (int64_t)B * nq * 2, "lookup_bwd: grad size");
   std::vector<void*> lv(4, nullptr);
   int hl = h, wl = w;
   for (int l = 0; l < L; ++l) {
     at::Tensor v = opt(t, 2 + l);
     check_f32(v, "dlevel");
-    TORCH_CHECK(v.numel() >= (int64_t)B * h * w * hl * wl, "lookup_bwd: dlevel size");
+    TORCH_CHECK(v.numel() >= (int64_t)B * nq * hl * wl, "lookup_bwd: dlevel size");
     lv[l] = v.data_ptr();
     if (keep) keep->push_back(v);
     hl >>= 1; wl >>= 1;
@@ -490,7 +495,7 @@ static Launch make_lookup_bwd(const TList& t, const IList& i, std::vector<at::Te
   const void* gp = g.data_ptr();
   const int gcs = cs(g);
   const int gbf = g.scalar_type() == at::kBFloat16;
-  return [=](hipStream_t s, int) { return jr_corr_lookup_bwd(lv.data(), L, B, h, w, r, cp, gp, gcs, gbf, s); };
+  return [=](hipStream_t s, int) { return jr_corr_lookup_bwd(lv.data(), L, B, h, w, nq, r, cp, gp, gcs, gbf, s); };
 }
 
 // t = [x, col], i = [N, H, W, x_coff, cin8, KH, KW, SH, SW, PH, PW]

@@ -254,8 +254,19 @@ def build_pyramid(fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int) -> 
         f"H and W of feature maps should be at least {min_fmap_size}; got: {tuple(fmap1.shape[-3:-1])}. "
         f"Input image dimensions should be at least 8 * {min_fmap_size} = {8 * min_fmap_size}."
     )
-    B, h, w, _ = fmap1.shape
-    vol = corr_volume(fmap1, fmap2).reshape(B * h * w, h, w)
+    return build_pyramid_queries(fmap1, fmap2, num_levels)
+
+
+def build_pyramid_queries(fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int) -> List[torch.Tensor]:
+    """:func:`build_pyramid` for a subset of query pixels: ``fmap1`` (B, hq, wq, C)
+    holds the queries (e.g. a slab of query rows, context parallelism), ``fmap2``
+    (B, h, w, C) every target pixel.  Levels are (B*hq*wq, h_l, w_l); each query's
+    maps are exactly its rows of the full pyramid (pooling acts on target dims only)."""
+    B, hq, wq, C = fmap1.shape
+    _, h, w, _ = fmap2.shape
+    f1 = fmap1.reshape(B, hq * wq, C)
+    f2 = fmap2.reshape(B, h * w, C)
+    vol = (torch.matmul(f1, f2.transpose(1, 2)) / math.sqrt(C)).reshape(B * hq * wq, h, w)
     pyr = [vol]
     for _ in range(num_levels - 1):
         hh, ww = vol.shape[-2] // 2, vol.shape[-1] // 2

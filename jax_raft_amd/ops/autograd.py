@@ -95,14 +95,18 @@ def conv2d_nhwc(x, kernel, bias, stride=(1, 1), padding=(0, 0)):
 
 
 class CorrPyramid(torch.autograd.Function):
-    """fmap1, fmap2 (B, h, w, C) -> L fp32 levels (B*h*w, h_l, w_l)."""
+    """fmap1 (B, hq, wq, C) query pixels, fmap2 (B, h, w, C) -> L fp32 levels
+    (B*hq*wq, h_l, w_l).  The queries are normally the whole map (hq, wq = h, w);
+    context parallelism (:mod:`jax_raft_amd.parallel.cp`) passes a slab of rows."""
 
     @staticmethod
     def forward(ctx, fmap1, fmap2, num_levels: int):
-        B, h, w, C = fmap1.shape
+        B, hq, wq, C = fmap1.shape
+        _, h, w, _ = fmap2.shape
+        nq = hq * wq
         f1 = fmap1.to(BF16).contiguous()
         f2 = fmap2.to(BF16).contiguous()
-        M = B * h * w
+        M = B * nq
         levels = []
         hl, wl = h, w
         for _ in range(num_levels):
@@ -110,9 +114,10 @@ class CorrPyramid(torch.autograd.Function):
             hl //= 2
             wl //= 2
         if C % 64 == 0:
-            nat.ops().corr([f1, f2] + levels + [None] * (4 - num_levels), [B, h, w, C, num_levels], 1.0 / math.sqrt(C))
+            nat.ops().corr([f1, f2] + levels + [None] * (4 - num_levels), [B, h, w, C, num_levels, nq],
+                           1.0 / math.sqrt(C))
         else:  # channel count the MFMA kernel does not tile: library GEMM + pooling
-            vol = torch.matmul(f1.float().reshape(B, h * w, C), f2.float().reshape(B, h * w, C).transpose(1, 2))
+            vol = torch.matmul(f1.float().reshape(B, nq, C), f2.float().reshape(B, h * w, C).transpose(1, 2))
             vol = (vol / math.sqrt(C)).reshape(M, h, w)
             levels[0].copy_(vol)
             for l in range(1, num_levels):
@@ -120,15 +125,15 @@ class CorrPyramid(torch.autograd.Function):
                 hh, ww = p.shape[1] // 2, p.shape[2] // 2
                 levels[l].copy_(p[:, : 2 * hh, : 2 * ww].reshape(M, hh, 2, ww, 2).mean(dim=(2, 4)))
         ctx.save_for_backward(f1, f2)
-        ctx.shape = (B, h, w, C, num_levels)
+        ctx.shape = (B, hq, wq, h, w, C, num_levels)
         return tuple(levels)
 
     @staticmethod
     def backward(ctx, *glevels):
         f1, f2 = ctx.saved_tensors
-        B, h, w, C, L = ctx.shape
-        M = B * h * w
-        dC = torch.zeros(M, h, w, device=f1.device, dtype=torch.float32)
+        B, hq, wq, h, w, C, L = ctx.shape
+        nq = hq * wq
+        dC = torch.zeros(B * nq, h, w, device=f1.device, dtype=torch.float32)
         for l, g in enumerate(glevels):
             if g is None:
                 continue
@@ -136,9 +141,9 @@ class CorrPyramid(torch.autograd.Function):
             hl, wl = g.shape[1], g.shape[2]
             up = g.float().repeat_interleave(s, dim=1).repeat_interleave(s, dim=2) / float(s * s)
             dC[:, : hl * s, : wl * s] += up
-        dC = dC.reshape(B, h * w, h * w) / math.sqrt(C)
-        g1 = torch.matmul(dC, f2.float().reshape(B, h * w, C)).reshape(B, h, w, C)
-        g2 = torch.matmul(dC.transpose(1, 2), f1.float().reshape(B, h * w, C)).reshape(B, h, w, C)
+        dC = dC.reshape(B, nq, h * w) / math.sqrt(C)
+        g1 = torch.matmul(dC, f2.float().reshape(B, h * w, C)).reshape(B, hq, wq, C)
+        g2 = torch.matmul(dC.transpose(1, 2), f1.float().reshape(B, nq, C)).reshape(B, h, w, C)
         return g1, g2, None
 
 
@@ -151,25 +156,28 @@ class PyramidLookup(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, coords, radius: int, *levels):
-        B, h, w, _ = coords.shape
+        # queries: coords (B, hq, wq); level-0 maps: (h, w) (hq, wq = h, w unless a row slab)
+        B, hq, wq, _ = coords.shape
+        h, w = levels[0].shape[1], levels[0].shape[2]
+        nq = hq * wq
         L = len(levels)
         S = 2 * radius + 1
         ocs = nat.round_up(L * S * S, 8)
-        c = coords.detach().float().reshape(B * h * w, 2).contiguous()
-        out = torch.empty(B * h * w, ocs, dtype=BF16, device=coords.device)
+        c = coords.detach().float().reshape(B * nq, 2).contiguous()
+        out = torch.empty(B * nq, ocs, dtype=BF16, device=coords.device)
         lv = [l.contiguous() for l in levels]
-        nat.ops().lookup([c, out] + lv + [None] * (4 - L), [L, B, h, w, radius])
+        nat.ops().lookup([c, out] + lv + [None] * (4 - L), [L, B, h, w, radius, nq])
         ctx.save_for_backward(c)
-        ctx.meta = (B, h, w, radius, L, [tuple(l.shape) for l in levels])
-        return out.reshape(B, h, w, ocs)[..., : L * S * S]
+        ctx.meta = (B, h, w, nq, radius, L, [tuple(l.shape) for l in levels])
+        return out.reshape(B, hq, wq, ocs)[..., : L * S * S]
 
     @staticmethod
     def backward(ctx, g):
         (c,) = ctx.saved_tensors
-        B, h, w, radius, L, shapes = ctx.meta
-        g = g.reshape(B * h * w, -1).float().contiguous()
+        B, h, w, nq, radius, L, shapes = ctx.meta
+        g = g.reshape(B * nq, -1).float().contiguous()
         dls = [torch.zeros(s, device=g.device, dtype=torch.float32) for s in shapes]
-        nat.ops().lookup_bwd([c, g] + dls + [None] * (4 - L), [L, B, h, w, radius])
+        nat.ops().lookup_bwd([c, g] + dls + [None] * (4 - L), [L, B, h, w, radius, nq])
         return (None, None) + tuple(dls)
 
 

@@ -35,6 +35,16 @@ def build_pyramid(fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int) -> 
     return R.build_pyramid(fmap1, fmap2, num_levels)
 
 
+def build_pyramid_queries(fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int) -> List[torch.Tensor]:
+    """Pyramid of a subset of query pixels ``fmap1`` (B, hq, wq, C) against all of
+    ``fmap2`` (B, h, w, C): levels (B*hq*wq, h_l, w_l) (context parallelism)."""
+    if fmap1.is_cuda:
+        from .autograd import build_pyramid as native_pyr
+
+        return native_pyr(fmap1, fmap2, num_levels)
+    return R.build_pyramid_queries(fmap1, fmap2, num_levels)
+
+
 def index_pyramid(pyramid: Sequence[torch.Tensor], coords: torch.Tensor, radius: int) -> torch.Tensor:
     if coords.is_cuda:
         from .autograd import index_pyramid as native_lookup

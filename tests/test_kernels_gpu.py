@@ -364,3 +364,73 @@ def test_flow_taps(cfg):
     assert (f32.cpu() - flow_ref).abs().max().item() < tol
     assert torch.equal(hx[:, 16:18], qx[:, 8:10]) and torch.equal(hx[:, 16:18], f8[:, :2])
     assert (hx[:, :16] == 0).all() and (hx[:, 18:] == 0).all()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_corr_query_slab_and_lookup(dtype):
+    """Context-parallel query slabs (parallel/cp.py): the corr kernel on rows
+    [r0, r1) of fmap1 (nq = slab pixels) reproduces those rows of the full
+    pyramid, and the lookup of the slab's coords against slab-sized level
+    buffers reproduces those rows of the full lookup."""
+    nat = _nat()
+    torch.manual_seed(9)
+    B, h, w, C, L, radius = 2, 23, 37, 128, 4, 4
+    r0, r1 = 7, 16
+    nq = (r1 - r0) * w
+    f1 = torch.randn(B, h, w, C).to(DEV, torch.bfloat16)
+    f2 = torch.randn(B, h, w, C).to(DEV, torch.bfloat16)
+
+    def levels(M):
+        out, hl, wl = [], h, w
+        for _ in range(L):
+            out.append(torch.full((M, hl, wl), float("nan"), device=DEV, dtype=dtype))
+            hl //= 2
+            wl //= 2
+        return out
+
+    full = levels(B * h * w)
+    nat.ops().corr([f1, f2] + full, [B, h, w, C, L], 1.0 / math.sqrt(C))
+    part = levels(B * nq)
+    nat.ops().corr([f1[:, r0:r1].contiguous(), f2] + part, [B, h, w, C, L, nq], 1.0 / math.sqrt(C))
+    torch.cuda.synchronize()
+    for a, b in zip(full, part):
+        rows = a.reshape(B, h, w, *a.shape[1:])[:, r0:r1].reshape(B * nq, *a.shape[1:])
+        assert not torch.isnan(b).any()
+        assert torch.equal(b, rows)
+    S = 2 * radius + 1
+    ocs = nat.round_up(L * S * S, 8)
+    coords = (R.make_coords_grid(B, h, w) + torch.randn(B, h, w, 2) * 3).to(DEV)
+    out_full = torch.empty(B * h * w, ocs, dtype=torch.bfloat16, device=DEV)
+    nat.ops().lookup([coords.reshape(-1, 2).contiguous(), out_full] + full, [L, B, h, w, radius])
+    cs = coords[:, r0:r1].reshape(-1, 2).contiguous()
+    out_part = torch.empty(B * nq, ocs, dtype=torch.bfloat16, device=DEV)
+    nat.ops().lookup([cs, out_part] + part, [L, B, h, w, radius, nq])
+    torch.cuda.synchronize()
+    ref = out_full.reshape(B, h, w, ocs)[:, r0:r1].reshape(B * nq, ocs)
+    assert torch.equal(out_part, ref)
+    if dtype == torch.float32:  # backward of the slab lookup == rows of the full backward
+        g = torch.randn(B * h * w, ocs, device=DEV)
+        dfull = [torch.zeros_like(l) for l in full]
+        nat.ops().lookup_bwd([coords.reshape(-1, 2).contiguous(), g] + dfull, [L, B, h, w, radius])
+        dpart = [torch.zeros_like(l) for l in part]
+        gp = g.reshape(B, h, w, ocs)[:, r0:r1].reshape(B * nq, ocs).contiguous()
+        nat.ops().lookup_bwd([cs, gp] + dpart, [L, B, h, w, radius, nq])
+        torch.cuda.synchronize()
+        for a, b in zip(dfull, dpart):
+            assert torch.equal(b, a.reshape(B, h, w, *a.shape[1:])[:, r0:r1].reshape(B * nq, *a.shape[1:]))
+
+
+def test_context_parallel_single_gpu_matches_engine():
+    """ContextParallelRAFT (one slab: the native slab kernels + module path)
+    against the golden fp32 forward on the same weights."""
+    from jax_raft_amd import raft_small
+    from jax_raft_amd.parallel.cp import ContextParallelRAFT
+
+    model, variables = raft_small(seed=0)
+    g = torch.Generator().manual_seed(4)
+    i1 = torch.rand(1, 128, 160, 3, generator=g) * 2 - 1
+    i2 = torch.rand(1, 128, 160, 3, generator=g) * 2 - 1
+    ref = model.apply(variables, i1, i2, num_flow_updates=3)
+    out = ContextParallelRAFT(model.cuda())(i1.cuda(), i2.cuda(), num_flow_updates=3).cpu()
+    epe = (out[-1] - ref[-1]).norm(dim=-1).mean().item()
+    assert epe < 0.05 * ref[-1].norm(dim=-1).mean().item() + 0.05, epe
