@@ -52,6 +52,7 @@ def main():
                     help="storage of the GRU z gate / folded context bias map (the hidden state is fp32 either way)")
     ap.add_argument("--flow-lane", default="side", choices=["side", "main"])
     ap.add_argument("--double-buffer", action="store_true", help="parity double-buffering of the flow head outputs")
+    ap.add_argument("--no-direct-flow", action="store_true", help="flow branch 7x7 conv on the implicit GEMM instead of the direct VALU kernel")
     ap.add_argument("--split", type=int, default=1, help="independent batch parts (one hipGraph each) run concurrently per GPU")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse >1 rank on fewer GPUs")
@@ -98,7 +99,7 @@ def main():
     def forward(a, b):
         return model(a, b, num_flow_updates=args.iters, use_graph=not args.no_graph, streams=not args.no_streams,
                      split=args.split, flow_head=args.flow_head, return_all_iters=not args.final_only,
-                     double_buffer=args.double_buffer,
+                     double_buffer=args.double_buffer, direct_flow=not args.no_direct_flow,
                      gate_dtype=torch.bfloat16 if args.gate_dtype == "bf16" else torch.float32, flow_lane=args.flow_lane)
 
     def run(n, events=None):
@@ -176,6 +177,7 @@ def main():
                 "flow_head": args.flow_head,
                 "gate_dtype": args.gate_dtype,
                 "flow_lane": args.flow_lane,
+                "direct_flow_conv": not args.no_direct_flow,
                 "batch_parts": args.split,
                 "h2d_in_timed_region": not args.no_h2d,
                 "h2d_overlapped": not (args.no_h2d or args.sync_h2d),

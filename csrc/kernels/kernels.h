@@ -139,6 +139,14 @@ int jr_flow_head(const void* fm, int fcs, const void* wt, const float* bias, int
 int jr_flow_taps(const float* t, int tcs, const float* bias, int N, int h, int w, float* coords, float* flow32,
                  void* hx, int hx_cs, int hx_off, void* qx, int qx_cs, int qx_off, void* f8, int f8_cs,
                  hipStream_t stream);
+// Conv of a 2-channel input (the flow branch's 7x7 / 3x3): x bf16 NHWC
+// [N][H][W][x_cstride] (channels 0, 1 used), stride 1, output H x W; w bf16
+// MFMA A fragments [cout/16][NKC][64 lanes][8] (jax_raft_amd/ops/native.py:
+// pack_direct_weight); bias fp32 [cout]; y bf16 channels [y_coff, y_coff +
+// cout) of [N*H*W][y_cstride].  (KH, KW) in {(7, 7), (3, 3)}, cout % 32 == 0.
+int jr_conv_direct(const void* x, int x_cstride, int N, int H, int W, int cin, int KH, int KW, int PH, int PW,
+                   const void* w, const float* bias, int cout, int relu, void* y, int y_cstride, int y_coff,
+                   hipStream_t stream);
 int jr_copy_channels(const void* src, int s_cstride, int s_coff, void* dst, int d_cstride, int d_coff,
                      int M, int C, hipStream_t stream);
 

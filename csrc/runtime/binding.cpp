@@ -207,6 +207,31 @@ static Launch make_flow_taps(const TList& t, const IList& i, std::vector<at::Ten
   };
 }
 
+// ---------------------------------------------------------------- direct conv
+// t = [x (bf16 NHWC, 2 channels used), w (bf16 A fragments [cout/16][NKC][64][8]), bias (fp32 [cout]), y (bf16)]
+// i = [N, H, W, cin, KH, KW, PH, PW, cout, relu, y_coff]   (stride 1, output H x W)
+static Launch make_conv_direct(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor x = opt(t, 0), w = opt(t, 1), bias = opt(t, 2), y = opt(t, 3);
+  TORCH_CHECK(i.size() == 11, "conv_direct: expected 11 ints");
+  check_bf16(x, "x"); check_bf16(w, "w"); check_f32(bias, "bias"); check_bf16(y, "y");
+  const int N = (int)i[0], H = (int)i[1], W = (int)i[2], cin = (int)i[3], KH = (int)i[4], KW = (int)i[5];
+  const int PH = (int)i[6], PW = (int)i[7], cout = (int)i[8], relu = (int)i[9], y_coff = (int)i[10];
+  const int64_t M = (int64_t)N * H * W;
+  TORCH_CHECK(cs(x) >= cin && x.numel() >= M * cs(x), "conv_direct: x [N*H*W][>=cin]");
+  const int kwp = KW <= 4 ? 4 : 8, nkc = (KH * kwp * 2 + 31) / 32;
+  TORCH_CHECK(cin == 2 && w.numel() == (int64_t)cout * nkc * 32 && bias.numel() >= cout, "conv_direct: w / bias");
+  TORCH_CHECK(y.numel() >= M * cs(y) && y_coff + cout <= cs(y), "conv_direct: y");
+  if (keep) for (auto& v : {x, w, bias, y}) keep->push_back(v);
+  const void* xp = x.data_ptr();
+  const void* wp = w.data_ptr();
+  const float* bp = bias.data_ptr<float>();
+  void* yp = y.data_ptr();
+  const int xcs = cs(x), ycs = cs(y);
+  return [=](hipStream_t s, int) {
+    return jr_conv_direct(xp, xcs, N, H, W, cin, KH, KW, PH, PW, wp, bp, cout, relu, yp, ycs, y_coff, s);
+  };
+}
+
 // ------------------------------------------------------------------ flow head
 // t = [fm, wt (bf16 [2][9][cin]), bias (fp32 [2]), coords, flow32, hx, qx?, flow8?]
 // i = [N, h, w, cin, fm_coff, hx_off, qx_off]
@@ -538,6 +563,7 @@ void lookup_bwd_op(const TList& t, IList i) { run_now(make_lookup_bwd(t, i, null
 void im2col_op(const TList& t, IList i) { run_now(make_im2col(t, i, nullptr)); }
 void flow_head_op(const TList& t, IList i) { run_now(make_flow_head(t, i, nullptr)); }
 void flow_taps_op(const TList& t, IList i) { run_now(make_flow_taps(t, i, nullptr)); }
+void conv_direct_op(const TList& t, IList i) { run_now(make_conv_direct(t, i, nullptr)); }
 
 // --------------------------------------------------------------------- Plan
 // A Plan is the lowered RAFT forward: three segments (prologue, loop body run
@@ -612,6 +638,7 @@ class Plan : public torch::CustomClassHolder {
   void add_copy_channels(TList t, IList i) { push(make_copy_channels(t, i, &keep_), "copy_channels"); }
   void add_flow_head(TList t, IList i) { push(make_flow_head(t, i, &keep_), "flow_head"); }
   void add_flow_taps(TList t, IList i) { push(make_flow_taps(t, i, &keep_), "flow_taps"); }
+  void add_conv_direct(TList t, IList i) { push(make_conv_direct(t, i, &keep_), "conv_direct"); }
 
   int64_t num_ops(int64_t seg) const { return (int64_t)segs_[seg].size(); }
   std::vector<std::string> op_names(int64_t seg) const {
@@ -795,6 +822,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("im2col(Tensor?[] t, int[] i) -> ()", &jr::im2col_op);
   m.def("flow_head(Tensor?[] t, int[] i) -> ()", &jr::flow_head_op);
   m.def("flow_taps(Tensor?[] t, int[] i) -> ()", &jr::flow_taps_op);
+  m.def("conv_direct(Tensor?[] t, int[] i) -> ()", &jr::conv_direct_op);
   m.class_<jr::Plan>("Plan")
       .def(torch::init<>())
       .def("set_segment", &jr::Plan::set_segment)
@@ -817,6 +845,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_copy_channels", &jr::Plan::add_copy_channels)
       .def("add_flow_head", &jr::Plan::add_flow_head)
       .def("add_flow_taps", &jr::Plan::add_flow_taps)
+      .def("add_conv_direct", &jr::Plan::add_conv_direct)
       .def("num_ops", &jr::Plan::num_ops)
       .def("op_names", &jr::Plan::op_names)
       .def("run", &jr::Plan::run)

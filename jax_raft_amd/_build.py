@@ -33,6 +33,7 @@ KERNEL_SOURCES = [
     CSRC / "kernels" / "corr.hip",
     CSRC / "kernels" / "elementwise.hip",
     CSRC / "kernels" / "flowhead.hip",
+    CSRC / "kernels" / "conv_direct.hip",
 ]
 HOST_SOURCES = [CSRC / "runtime" / "binding.cpp"]
 HEADERS = [CSRC / "kernels" / "common.h", CSRC / "kernels" / "kernels.h", CSRC / "kernels" / "conv_igemm.h"]

@@ -154,6 +154,29 @@ def pack_weight(kernel: torch.Tensor, cin8: Optional[int] = None, out: Optional[
     return w
 
 
+def pack_direct_weight(kernel: torch.Tensor) -> torch.Tensor:
+    """HWIO kernel (kh, kw, 2, cout) -> bf16 MFMA A fragments [cout/16][NKC][64][8]
+    for the 2-channel conv (conv_direct.hip).  K is ordered (kh, kw padded to
+    KWP = 4 | 8, c): fragment (t, kc), lane l, element e holds
+    W[co = 16t + l % 16][k = 32 kc + 8 (l // 16) + e]."""
+    kh, kw, cin, cout = kernel.shape
+    assert cin == 2 and cout % 32 == 0, "2-channel conv with cout % 32 == 0"
+    kwp = 4 if kw <= 4 else 8
+    nkc = (kh * kwp * 2 + 31) // 32
+    k = torch.zeros(kh, kwp, 2, cout, dtype=torch.float32, device=kernel.device)
+    k[:, :kw] = kernel.detach().float()
+    wk = torch.zeros(cout, nkc * 32, dtype=torch.float32, device=kernel.device)
+    wk[:, : kh * kwp * 2] = k.reshape(kh * kwp * 2, cout).t()
+    wk = wk.reshape(cout // 16, 16, nkc, 4, 8).permute(0, 2, 3, 1, 4)  # [t][kc][kg][i][e]
+    return wk.reshape(cout // 16, nkc, 64, 8).to(torch.bfloat16).contiguous()
+
+
+def direct_conv_ok(kernel: torch.Tensor, stride=(1, 1)) -> bool:
+    """Shapes the direct VALU conv kernel supports (the flow branch's 7x7 / 3x3 on 2 channels)."""
+    kh, kw, cin, cout = kernel.shape
+    return cin == 2 and (kh, kw) in ((7, 7), (3, 3)) and tuple(stride) == (1, 1) and cout % 32 == 0
+
+
 def make_spec(kernel: torch.Tensor, bias: torch.Tensor, stride=(1, 1), padding=(0, 0), cin8: Optional[int] = None,
               device=None) -> ConvSpec:
     kh, kw, cin, cout = kernel.shape

@@ -151,14 +151,20 @@ class RaftEngine:
             i's mask head (otherwise one buffer and a WAR wait).  Off by
             default: the extra overlap measured slower (233 vs 244 pairs/s),
             the mask head then contends with the next iteration's critical path.
+        direct_flow: run the flow branch's first conv (7x7 on the 2-channel
+            flow, ``model.py:282-283``) on the direct VALU kernel
+            (conv_direct.hip) instead of the implicit GEMM, whose 49 gathered
+            taps of 2 real channels starve the MFMA loader.
     """
 
     def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True,
                  corr_dtype: torch.dtype = torch.bfloat16, autotune: bool = True, streams: bool = True,
                  split: int = 1, flow_head: str = "taps", double_buffer: bool = False,
                  fused_flow_head: bool = False, gate_dtype: torch.dtype = torch.bfloat16,
-                 flow_lane: str = "side"):
+                 flow_lane: str = "side", direct_flow: bool = True):
         nat.require()
+        self.direct_flow = direct_flow
+        self._cf1_w = self._cf1_b = None
         self.gate_dtype = gate_dtype
         assert flow_lane in ("side", "main"), flow_lane
         self.flow_lane = flow_lane if streams else "main"
@@ -245,6 +251,15 @@ class RaftEngine:
         else:
             self._fh2_w.copy_(wf)
             self._fh2_b.copy_(bf)
+        cf1 = self.model.update_block.motion_encoder.convflow1.layers_0
+        if self.direct_flow and nat.direct_conv_ok(cf1.kernel, cf1.stride):
+            wd = nat.pack_direct_weight(cf1.kernel).to(self.device)
+            bd = cf1.bias.detach().float().to(self.device).contiguous()
+            if self._cf1_w is None:
+                self._cf1_w, self._cf1_b = wd, bd
+            else:
+                self._cf1_w.copy_(wd)
+                self._cf1_b.copy_(bd)
         self._sig = self._signature()
 
     def _define_specs(self):
@@ -483,7 +498,9 @@ class RaftEngine:
         qx = alloc("qx", (M, self.hx_cs))
         h32 = alloc("h32", (M, self.hidden), F32)
         zb = alloc("z", (M, self.hidden), self.gate_dtype)
-        flow8 = alloc("flow8", (M, 8))
+        # bf16 flow for the flow branch: compact 2 channels for the 2-channel conv
+        # kernel (4 taps = one 16-B load), 8-channel rows for the implicit GEMM
+        flow8 = alloc("flow8", (M, 2 if self._cf1_w is not None else 8))
         coords = alloc("coords", (M, 2), F32)
         flow32 = alloc("flow32", (M, 2), F32)
         for t in (hx, qx, flow8, flow32):
@@ -537,7 +554,13 @@ class RaftEngine:
         f1 = alloc("f1", (M, fl[0]))
 
         def flow_features():
-            self._conv(plan, sp["me.convflow1"], flow8, B, h, w, f1, act=ACT_RELU)
+            if self._cf1_w is not None:
+                c = me.convflow1.layers_0
+                kh, kw_, _, co = c.kernel.shape
+                plan.add_conv_direct([flow8, self._cf1_w, self._cf1_b, f1],
+                                     [B, h, w, 2, kh, kw_, c.padding[0], c.padding[1], co, 1, 0])
+            else:
+                self._conv(plan, sp["me.convflow1"], flow8, B, h, w, f1, act=ACT_RELU)
             self._conv(plan, sp["me.convflow2"], f1, B, h, w, cf, y_coff=cl[-1], act=ACT_RELU)
 
         s1 = sp["fh1"] if (all_iters or not self.has_mask) else sp["fh1.flow"]

@@ -434,3 +434,26 @@ def test_context_parallel_single_gpu_matches_engine():
     out = ContextParallelRAFT(model.cuda())(i1.cuda(), i2.cuda(), num_flow_updates=3).cpu()
     epe = (out[-1] - ref[-1]).norm(dim=-1).mean().item()
     assert epe < 0.05 * ref[-1].norm(dim=-1).mean().item() + 0.05, epe
+
+
+@pytest.mark.parametrize("kh,cout,xcs,ycs,ycoff", [(7, 128, 8, 128, 0), (7, 128, 2, 128, 0), (7, 64, 8, 96, 32),
+                                                   (7, 64, 2, 64, 0), (3, 32, 2, 32, 0)])
+def test_conv_direct(kh, cout, xcs, ycs, ycoff):
+    """Direct VALU conv (conv_direct.hip: the flow branch's 7x7 on 2 channels) vs fp32 conv."""
+    nat = _nat()
+    torch.manual_seed(12)
+    N, H, W = 2, 19, 27
+    x = torch.randn(N, H, W, 2) * 3
+    k = torch.randn(kh, kh, 2, cout) * 0.2
+    b = torch.randn(cout)
+    p = kh // 2
+    ref = torch.relu(R.conv2d_nhwc(_bf(x), k, b, (1, 1), (p, p)))
+    xb = torch.zeros(N, H, W, xcs, dtype=torch.bfloat16)
+    xb[..., :2] = x.to(torch.bfloat16)
+    y = torch.full((N * H * W, ycs), 7.0, dtype=torch.bfloat16, device=DEV)
+    nat.ops().conv_direct([xb.to(DEV), nat.pack_direct_weight(k).to(DEV), b.to(DEV), y],
+                          [N, H, W, 2, kh, kh, p, p, cout, 1, ycoff])
+    torch.cuda.synchronize()
+    got = y.float().cpu()
+    assert (got[:, :ycoff] == 7.0).all() and (got[:, ycoff + cout:] == 7.0).all()
+    assert _rel(got[:, ycoff:ycoff + cout], ref.reshape(-1, cout)) < 1e-2
