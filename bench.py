@@ -54,6 +54,9 @@ def main():
     ap.add_argument("--double-buffer", action="store_true", help="parity double-buffering of the flow head outputs")
     ap.add_argument("--no-direct-flow", action="store_true", help="flow branch 7x7 conv on the implicit GEMM instead of the direct VALU kernel")
     ap.add_argument("--split", type=int, default=1, help="independent batch parts (one hipGraph each) run concurrently per GPU")
+    ap.add_argument("--pipeline", action=argparse.BooleanOptionalAction, default=False,
+                    help="cross-batch pipelining: batch i+1's encoders + correlation pyramid run concurrently "
+                         "with batch i's refinement loop (two plan slots, prologue / loop graphs on two streams)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse >1 rank on fewer GPUs")
     args = ap.parse_args()
@@ -96,25 +99,35 @@ def main():
     # (InputPrefetcher), so only the first copy of a run is exposed.
     pf = None if (args.no_h2d or args.sync_h2d) else InputPrefetcher([(B, H, W, 3), (B, H, W, 3)], dev)
 
+    engine_kw = dict(use_graph=not args.no_graph, streams=not args.no_streams, split=args.split,
+                     flow_head=args.flow_head, double_buffer=args.double_buffer, direct_flow=not args.no_direct_flow,
+                     gate_dtype=torch.bfloat16 if args.gate_dtype == "bf16" else torch.float32,
+                     flow_lane=args.flow_lane)
+    pipelined = args.pipeline and not args.no_graph
+    eng = model.engine(dev, **engine_kw) if pipelined else None
+
     def forward(a, b):
-        return model(a, b, num_flow_updates=args.iters, use_graph=not args.no_graph, streams=not args.no_streams,
-                     split=args.split, flow_head=args.flow_head, return_all_iters=not args.final_only,
-                     double_buffer=args.double_buffer, direct_flow=not args.no_direct_flow,
-                     gate_dtype=torch.bfloat16 if args.gate_dtype == "bf16" else torch.float32, flow_lane=args.flow_lane)
+        """One step; returns (flows, stream the step's work ends on)."""
+        if pipelined:
+            # batch i's encoders + correlation pyramid overlap batch i-1's refinement loop
+            h = eng.submit(a, b, args.iters, return_all_iters=not args.final_only)
+            return h.out, eng.loop_stream
+        return (model(a, b, num_flow_updates=args.iters, return_all_iters=not args.final_only, **engine_kw),
+                torch.cuda.current_stream(dev))
 
     def run(n, events=None):
         if pf is None:
             for i in range(n):
-                out = forward(img1.to(dev, non_blocking=True), img2.to(dev, non_blocking=True))
+                out, s = forward(img1.to(dev, non_blocking=True), img2.to(dev, non_blocking=True))
                 if events is not None:
-                    events[i + 1].record()
+                    events[i + 1].record(s)
             return out
         pf.put(0, [img1, img2])
         for i in range(n):
             a, b = pf.get(i)
-            out = forward(a, b)
+            out, s = forward(a, b)
             if events is not None:
-                events[i + 1].record()
+                events[i + 1].record(s)
             pf.release(i)
             if i + 1 < n:
                 pf.put(i + 1, [img1, img2])
@@ -179,6 +192,7 @@ def main():
                 "flow_lane": args.flow_lane,
                 "direct_flow_conv": not args.no_direct_flow,
                 "batch_parts": args.split,
+                "cross_batch_pipeline": bool(pipelined),
                 "h2d_in_timed_region": not args.no_h2d,
                 "h2d_overlapped": not (args.no_h2d or args.sync_h2d),
                 "parallelism": f"dp{world}",

@@ -97,6 +97,7 @@ __global__ __launch_bounds__(256) void channel_stats_partial_kernel(const bf16* 
   for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
   if (rg < nrg) {
     const bf16* base = x + (long)n * HW * C + g * 8;
+#pragma unroll 4
     for (int r = r0 + rg; r < r1; r += nrg) {
       const bf16x8 v = *(const bf16x8*)(base + (long)r * C);
 #pragma unroll
@@ -146,60 +147,83 @@ __global__ __launch_bounds__(256) void channel_stats_final_kernel(const float* _
   }
 }
 
-// y = act(xn + rn): 8 channels per thread
-__global__ void norm_act_kernel(const bf16* __restrict__ x, const float* __restrict__ sx, int mode_x,
-                                const float* __restrict__ gx, const float* __restrict__ bx,
-                                const bf16* __restrict__ r, const float* __restrict__ sr, int mode_r,
-                                const float* __restrict__ gr, const float* __restrict__ br, bf16* __restrict__ y,
-                                int N, int HW, int C, float eps, int relu) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+// y = act(xn + rn).  Block = (row chunk, image n); thread = (8-channel group g,
+// row lane): the per-channel scale/shift of x (and of the residual) are derived
+// from the statistics once per thread and reused for every row it visits, and
+// all indexing is 32-bit within one image (no 64-bit divisions per element).
+struct NormSide {
+  float a[8], b[8];
+};
+
+JR_DEVICE void norm_coeffs(NormSide& o, const float* st, int mode, const float* gam, const float* bet, int n, int N,
+                           int HW, int C, int c0, float eps) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    float a = 1.f, b = 0.f;
+    if (mode == 1) {
+      const float inv = 1.0f / (float)HW;
+      const float m = st[((long)n * C + c) * 2] * inv;
+      const float var = fmaxf(st[((long)n * C + c) * 2 + 1] * inv - m * m, 0.f);
+      a = rsqrtf(var + eps);
+      b = -m * a;
+    } else if (mode == 2) {
+      float s0 = 0.f, s1 = 0.f;
+      for (int k = 0; k < N; ++k) { s0 += st[((long)k * C + c) * 2]; s1 += st[((long)k * C + c) * 2 + 1]; }
+      const float inv = 1.0f / ((float)HW * (float)N);
+      const float m = s0 * inv;
+      const float var = fmaxf(s1 * inv - m * m, 0.f);
+      a = rsqrtf(var + eps);
+      b = -m * a;
+    }
+    if (gam) { a *= gam[c]; b *= gam[c]; }
+    if (bet) b += bet[c];
+    o.a[j] = a;
+    o.b[j] = b;
+  }
+}
+
+__global__ __launch_bounds__(256) void norm_act_kernel(const bf16* __restrict__ x, const float* __restrict__ sx,
+                                                       int mode_x, const float* __restrict__ gx,
+                                                       const float* __restrict__ bx, const bf16* __restrict__ r,
+                                                       const float* __restrict__ sr, int mode_r,
+                                                       const float* __restrict__ gr, const float* __restrict__ br,
+                                                       bf16* __restrict__ y, int N, int HW, int C, float eps, int relu,
+                                                       int rows) {
+  const int n = blockIdx.y;
   const int cg = C >> 3;
-  const long total = (long)N * HW * cg;
-  if (idx >= total) return;
-  const int g = idx % cg;
-  const long pix = idx / cg;
-  const int n = pix / HW;
+  const int tid = threadIdx.x;
+  const int g = tid % cg, rg = tid / cg, nrg = 256 / cg;
+  if (rg >= nrg) return;
   const int c0 = g * 8;
-  auto norm8 = [&](const bf16* src, const float* st, int mode, const float* gam, const float* bet, float* o) {
-    const bf16x8 v = *(const bf16x8*)(src + pix * C + c0);
+  NormSide nx, nr;
+  norm_coeffs(nx, sx, mode_x, gx, bx, n, N, HW, C, c0, eps);
+  if (r) norm_coeffs(nr, sr, mode_r, gr, br, n, N, HW, C, c0, eps);
+  const long base = (long)n * HW * C + c0;
+  const bf16* xb = x + base;
+  const bf16* rb = r ? r + base : nullptr;
+  bf16* yb = y + base;
+  const int r0 = blockIdx.x * rows;
+  const int r1 = min(r0 + rows, HW);
+#pragma unroll 2
+  for (int row = r0 + rg; row < r1; row += nrg) {
+    const int off = row * C;
+    const bf16x8 v = *(const bf16x8*)(xb + off);
+    bf16x8 w;
+    if (rb) w = *(const bf16x8*)(rb + off);
+    float a[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float f = bf2f(v[j]);
-      const int c = c0 + j;
-      if (mode == 1) {
-        const float inv = 1.0f / (float)HW;
-        const float m = st[((long)n * C + c) * 2] * inv;
-        const float var = fmaxf(st[((long)n * C + c) * 2 + 1] * inv - m * m, 0.f);
-        f = (f - m) * rsqrtf(var + eps);
-      } else if (mode == 2) {
-        float s0 = 0.f, s1 = 0.f;
-        for (int k = 0; k < N; ++k) { s0 += st[((long)k * C + c) * 2]; s1 += st[((long)k * C + c) * 2 + 1]; }
-        const float inv = 1.0f / ((float)HW * (float)N);
-        const float m = s0 * inv;
-        const float var = fmaxf(s1 * inv - m * m, 0.f);
-        f = (f - m) * rsqrtf(var + eps);
-      }
-      if (gam) f *= gam[c];
-      if (bet) f += bet[c];
-      o[j] = f;
+      a[j] = fmaf(bf2f(v[j]), nx.a[j], nx.b[j]);
+      if (relu & 1) a[j] = fmaxf(a[j], 0.f);
+      if (rb) a[j] += fmaf(bf2f(w[j]), nr.a[j], nr.b[j]);
+      if (relu & 2) a[j] = fmaxf(a[j], 0.f);
     }
-  };
-  float a[8];
-  norm8(x, sx, mode_x, gx, bx, a);
-  if (relu & 1) {
+    bf16x8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) a[j] = fmaxf(a[j], 0.f);
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(a[j]);
+    *(bf16x8*)(yb + off) = o;
   }
-  if (r) {
-    float b[8];
-    norm8(r, sr, mode_r, gr, br, b);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) a[j] += b[j];
-  }
-  bf16x8 o;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = f2bf((relu & 2) ? fmaxf(a[j], 0.f) : a[j]);
-  *(bf16x8*)(y + pix * C + c0) = o;
 }
 
 __global__ void prep_images_kernel(const float* __restrict__ i1, const float* __restrict__ i2, int B, long HW,
@@ -293,9 +317,14 @@ extern "C" int jr_norm_act(const void* x, const float* sx, int mode_x, const flo
                            const void* res, const float* sr, int mode_r, const float* gamma_r, const float* beta_r,
                            void* y, int N, int HW, int C, float eps, int relu, hipStream_t stream) {
   if (C % 8 != 0) return (int)hipErrorInvalidValue;
-  const long total = (long)N * HW * (C / 8);
-  hipLaunchKernelGGL(norm_act_kernel, dim3(nblk(total, 256)), dim3(256), 0, stream, (const bf16*)x, sx, mode_x, gamma,
-                     beta, (const bf16*)res, sr, mode_r, gamma_r, beta_r, (bf16*)y, N, HW, C, eps, relu);
+  if (C / 8 > 256) return (int)hipErrorInvalidValue;
+  // rows per block: a multiple of the block's row lanes, sized for ~2048 blocks
+  const int nrg = 256 / (C / 8);
+  const long want = ((long)N * HW + 2047) / 2048;
+  const int rows = (int)std::max<long>(nrg, (want + nrg - 1) / nrg * nrg);
+  const unsigned nb = (unsigned)((HW + rows - 1) / rows);
+  hipLaunchKernelGGL(norm_act_kernel, dim3(nb, N), dim3(256), 0, stream, (const bf16*)x, sx, mode_x, gamma, beta,
+                     (const bf16*)res, sr, mode_r, gamma_r, beta_r, (bf16*)y, N, HW, C, eps, relu, rows);
   return (int)hipGetLastError();
 }
 

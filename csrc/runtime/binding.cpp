@@ -655,6 +655,33 @@ class Plan : public torch::CustomClassHolder {
   // legacy default stream cannot be captured) and instantiate it.
   void capture(int64_t n_iters) {
     reset_graph();
+    capture_into(n_iters, -1, &graph_, &exec_);
+    captured_iters_ = n_iters;
+  }
+  // Capture one phase as its own hipGraph: part 0 = the prologue (encoders +
+  // correlation pyramid), part 1 = n_iters loop iterations + the epilogue.
+  // Replayed on different streams, the prologue of batch i+1 overlaps the
+  // refinement loop of batch i (cross-batch pipelining, runtime/engine.py).
+  void capture_part(int64_t part, int64_t n_iters) {
+    TORCH_CHECK(part == 0 || part == 1, "part must be 0 (prologue) or 1 (loop + epilogue)");
+    reset_part(part);
+    capture_into(n_iters, (int)part, &pgraph_[part], &pexec_[part]);
+    pcaptured_[part] = n_iters;
+  }
+  int64_t captured_part_iters(int64_t part) const { return pcaptured_[part & 1]; }
+  void replay_part(int64_t part) {
+    TORCH_CHECK((part == 0 || part == 1) && pexec_[part] != nullptr, "plan: part ", part, " not captured");
+    hipError_t e = hipGraphLaunch(pexec_[part], cur_stream());
+    TORCH_CHECK(e == hipSuccess, "graph launch failed: ", hipGetErrorString(e));
+  }
+
+ private:
+  void reset_part(int64_t part) {
+    if (pexec_[part]) { (void)hipGraphExecDestroy(pexec_[part]); pexec_[part] = nullptr; }
+    if (pgraph_[part]) { (void)hipGraphDestroy(pgraph_[part]); pgraph_[part] = nullptr; }
+    pcaptured_[part] = -1;
+  }
+  void capture_into(int64_t n_iters, int part, hipGraph_t* graph_out, hipGraphExec_t* exec_out) {
     if (!cap_stream_) {
       int least = 0, greatest = 0;
       TORCH_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess, "priority range");
@@ -666,19 +693,20 @@ class Plan : public torch::CustomClassHolder {
     // order the capture after work already queued on the current stream
     TORCH_CHECK(hipStreamSynchronize(cur_stream()) == hipSuccess, "sync");
     TORCH_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess, "begin capture");
-    int err = enqueue(s, (int)n_iters, true);
+    int err = enqueue(s, (int)n_iters, true, part);
     if (debug_) fprintf(stderr, "[plan] enqueue done err=%d\n", err);
     hipGraph_t g = nullptr;
     hipError_t e2 = hipStreamEndCapture(s, &g);
     if (debug_) fprintf(stderr, "[plan] end capture %d\n", (int)e2);
     TORCH_CHECK(err == 0, "launch failed during capture: ", hipGetErrorString((hipError_t)err));
     TORCH_CHECK(e2 == hipSuccess && g != nullptr, "end capture failed: ", hipGetErrorString(e2));
-    graph_ = g;
-    hipError_t e3 = hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0);
+    *graph_out = g;
+    hipError_t e3 = hipGraphInstantiate(exec_out, g, nullptr, nullptr, 0);
     if (debug_) fprintf(stderr, "[plan] instantiate %d\n", (int)e3);
     TORCH_CHECK(e3 == hipSuccess, "graph instantiate failed: ", hipGetErrorString(e3));
-    captured_iters_ = n_iters;
   }
+
+ public:
   int64_t captured_iters() const { return captured_iters_; }
   void replay() {
     TORCH_CHECK(exec_ != nullptr, "plan: no captured graph");
@@ -689,6 +717,8 @@ class Plan : public torch::CustomClassHolder {
     if (exec_) { (void)hipGraphExecDestroy(exec_); exec_ = nullptr; }
     if (graph_) { (void)hipGraphDestroy(graph_); graph_ = nullptr; }
     captured_iters_ = -1;
+    reset_part(0);
+    reset_part(1);
   }
 
  private:
@@ -751,7 +781,8 @@ class Plan : public torch::CustomClassHolder {
         return (int)hipStreamWaitEvent(s, events_[o.ev], 0);
     }
   }
-  int enqueue(hipStream_t s, int n_iters, bool capturing = false) {
+  // part: -1 = the whole forward, 0 = prologue only, 1 = loop + epilogue only.
+  int enqueue(hipStream_t s, int n_iters, bool capturing = false, int part = -1) {
     if (int r = ensure_resources()) return r;
     // Eager: lane 0 is the private high-priority stream, forked from the caller's.
     // Capture: lane 0 is the capture stream itself (created with the greatest
@@ -770,15 +801,15 @@ class Plan : public torch::CustomClassHolder {
     // enqueue of each phase: encoders + correlation pyramid, every refinement
     // iteration, the epilogue.
     RangeGuard all("raft.plan");
-    {
+    if (part != 1) {
       RangeGuard r("raft.prologue");
       for (auto& o : segs_[0]) if (int e = exec_op(o, st, 0, recorded)) return e;
     }
-    for (int it = 0; it < n_iters; ++it) {
+    for (int it = 0; part != 0 && it < n_iters; ++it) {
       RangeGuard r("raft.iteration");
       for (auto& o : segs_[1]) if (int e = exec_op(o, st, it, recorded)) return e;
     }
-    {
+    if (part != 0) {
       RangeGuard r("raft.epilogue");
       for (auto& o : segs_[2]) if (int e = exec_op(o, st, n_iters, recorded)) return e;
     }
@@ -802,6 +833,9 @@ class Plan : public torch::CustomClassHolder {
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t exec_ = nullptr;
   int64_t captured_iters_ = -1;
+  hipGraph_t pgraph_[2] = {};
+  hipGraphExec_t pexec_[2] = {};
+  int64_t pcaptured_[2] = {-1, -1};
   bool debug_ = false;
 };
 
@@ -852,5 +886,8 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("capture", &jr::Plan::capture)
       .def("captured_iters", &jr::Plan::captured_iters)
       .def("replay", &jr::Plan::replay)
+      .def("capture_part", &jr::Plan::capture_part)
+      .def("captured_part_iters", &jr::Plan::captured_part_iters)
+      .def("replay_part", &jr::Plan::replay_part)
       .def("reset_graph", &jr::Plan::reset_graph);
 }

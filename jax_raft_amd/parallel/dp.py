@@ -52,6 +52,9 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> Tup
         torch.cuda.set_device(device)
     if world > 1 and not is_dist():
         backend = backend or ("nccl" if use_gpu else "gloo")
+        # fail fast: a rank that dies or hangs in a collective tears the job
+        # down after ``timeout_s`` instead of blocking every other rank forever
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":

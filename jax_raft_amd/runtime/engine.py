@@ -113,6 +113,24 @@ class _PlanState:
     n_iters: int = 0
 
 
+class PendingFlow:
+    """Result of :meth:`RaftEngine.submit`: the flows tensor plus the event
+    that marks it complete (recorded on the engine's loop stream)."""
+
+    def __init__(self, out: torch.Tensor, done: torch.cuda.Event, device):
+        self.out, self.done, self.device = out, done, device
+
+    def wait(self, stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+        """Order ``stream`` (default: current) after the result; returns it."""
+        (stream or torch.cuda.current_stream(self.device)).wait_event(self.done)
+        return self.out
+
+    def result(self) -> torch.Tensor:
+        """Block the host until the result is ready; returns it."""
+        self.done.synchronize()
+        return self.out
+
+
 class RaftEngine:
     """Inference engine bound to one model and one GPU.
 
@@ -185,6 +203,7 @@ class RaftEngine:
         self._sources: Dict[str, callable] = {}
         self._states: Dict[Tuple[int, int, int, int], _PlanState] = {}
         self._sig = None
+        self._pipe = None
         self._analyse()
         self._pack()
 
@@ -677,6 +696,78 @@ class RaftEngine:
             for strm in self._part_streams[:len(st.plans)]:
                 cur.wait_stream(strm)
         return st.out.clone() if self.copy_output else st.out
+
+    # ------------------------------------------------- pipelined (serving)
+    @torch.no_grad()
+    def submit(self, image1: torch.Tensor, image2: torch.Tensor, num_flow_updates: int = 12,
+               return_all_iters: bool = True, depth: int = 2) -> "PendingFlow":
+        """Asynchronous forward for serving loops: batch i's encoders +
+        correlation pyramid (the prologue graph, on a low-priority stream) run
+        concurrently with batch i-1's refinement loop (the loop graph, on a
+        high-priority stream), filling the CUs the latency-bound loop leaves
+        idle.  ``depth`` plan slots (own buffers + graphs) rotate; a slot's
+        prologue waits until the loop that last used it is done.
+
+        The inputs are read on the current stream (copied into the slot); the
+        current stream is never made to wait on the GPU work, so the next
+        submit can be issued at once.  Returns a :class:`PendingFlow`; call
+        ``.wait()`` (orders the current stream after the result) or
+        ``.result()``."""
+        if self._signature() != self._sig:
+            self._pack()
+        B, H, W, C = image1.shape
+        assert C == 3, "images must be NHWC with 3 channels"
+        assert self.use_graph, "submit() replays captured graphs (use_graph=True)"
+        pipe = self._pipe
+        if pipe is None or pipe["depth"] != depth:
+            pipe = self._pipe = dict(
+                depth=depth, n=0,
+                sp=torch.cuda.Stream(device=self.device, priority=0),
+                sl=torch.cuda.Stream(device=self.device, priority=-1),
+                e_in=[torch.cuda.Event() for _ in range(depth)],
+                e_pro=[torch.cuda.Event() for _ in range(depth)],
+                e_loop=[torch.cuda.Event() for _ in range(depth)])
+        slot = pipe["n"] % depth
+        pipe["n"] += 1
+        key = (B, H, W, num_flow_updates, bool(return_all_iters), "slot", slot)
+        st = self._states.get(key)
+        if st is None:
+            saved, self.split = self.split, 1
+            try:
+                st = self._build(B, H, W, num_flow_updates, bool(return_all_iters))
+            finally:
+                self.split = saved
+            self._states[key] = st
+        plan = st.plan
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(pipe["e_pro"][slot])      # the slot's last prologue has read its inputs
+        st.inp1.copy_(image1)
+        st.inp2.copy_(image2)
+        pipe["e_in"][slot].record(cur)
+        sp, sl = pipe["sp"], pipe["sl"]
+        with torch.cuda.stream(sp):
+            sp.wait_event(pipe["e_in"][slot])
+            sp.wait_event(pipe["e_loop"][slot])  # the slot's last loop is done with its buffers
+            if plan.captured_part_iters(0) != num_flow_updates:
+                plan.capture_part(0, num_flow_updates)
+            plan.replay_part(0)
+            pipe["e_pro"][slot].record(sp)
+        with torch.cuda.stream(sl):
+            sl.wait_event(pipe["e_pro"][slot])
+            if plan.captured_part_iters(1) != num_flow_updates:
+                plan.capture_part(1, num_flow_updates)
+            plan.replay_part(1)
+            out = st.out.clone()
+            pipe["e_loop"][slot].record(sl)
+            done = torch.cuda.Event()
+            done.record(sl)
+        out.record_stream(cur)
+        return PendingFlow(out, done, self.device)
+
+    @property
+    def loop_stream(self) -> Optional[torch.cuda.Stream]:
+        """The stream :meth:`submit` replays loop graphs on (None before the first submit)."""
+        return None if self._pipe is None else self._pipe["sl"]
 
     def _launch(self, plan, n_iters: int) -> None:
         if self.use_graph:

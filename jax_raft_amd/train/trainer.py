@@ -53,6 +53,9 @@ class TrainConfig:
     freeze_bn: bool = False
     sync_bn: bool = False          # synchronised BatchNorm statistics across DP ranks
     bucket_mb: float = 32.0
+    skip_nonfinite: bool = True    # drop a step whose (all-reduced) gradient is NaN/Inf
+    max_skipped: int = 10          # ... but abort after this many consecutive drops
+    fault_nan_step: int = -1       # fault injection: poison the loss of this step (tests)
 
 
 class Trainer:
@@ -74,6 +77,8 @@ class Trainer:
             anneal_strategy="linear")
         self.data = SyntheticFlow(size=tuple(cfg.size), seed=cfg.seed, device=self.device)
         self.step = 0
+        self.skipped = 0           # total dropped steps
+        self._skip_run = 0         # consecutive dropped steps
         if cfg.resume and cfg.ckpt_dir and os.path.exists(os.path.join(cfg.ckpt_dir, "latest.json")):
             self.load(cfg.ckpt_dir)
 
@@ -85,10 +90,22 @@ class Trainer:
         train_bn = not cfg.freeze_bn
         preds = self.model(img1, img2, train=train_bn, num_flow_updates=cfg.iters, autograd=True)
         loss, metrics = sequence_loss(preds, flow, valid, cfg.gamma, cfg.max_flow)
+        if self.step + 1 == cfg.fault_nan_step:
+            loss = loss * float("nan")
         loss.backward()
         self.sync.finish()
         gnorm = torch.nn.utils.clip_grad_norm_(self.model.parameters(), cfg.clip)
-        self.opt.step()
+        # Failure detection: the gradient is all-reduced, so every rank sees the
+        # same norm and takes the same decision (no extra collective needed).
+        if cfg.skip_nonfinite and not bool(torch.isfinite(gnorm)):
+            self.opt.zero_grad(set_to_none=True)
+            self.skipped += 1
+            self._skip_run += 1
+            if self._skip_run > cfg.max_skipped:
+                raise FloatingPointError(f"{self._skip_run} consecutive non-finite gradients at step {self.step + 1}")
+        else:
+            self._skip_run = 0
+            self.opt.step()
         self.sched.step()
         self.step += 1
         out = {"loss": loss.detach(), "grad_norm": gnorm.detach(), **{k: v.detach() for k, v in metrics.items()}}
@@ -99,11 +116,13 @@ class Trainer:
         base = (step * self.world + self.rank) * cfg.batch
         return self.data.batch(list(range(base, base + cfg.batch)))
 
-    def fit(self, log=print) -> Dict[str, float]:
+    def fit(self, log=print, stop_at: Optional[int] = None) -> Dict[str, float]:
+        """Train to ``cfg.steps`` (or stop early after step ``stop_at``)."""
         cfg = self.cfg
+        end = cfg.steps if stop_at is None else min(stop_at, cfg.steps)
         t0 = time.perf_counter()
         last = {}
-        while self.step < cfg.steps:
+        while self.step < end:
             batch = self.batch_for(self.step)
             m = self.train_step(batch)
             if self.step % cfg.log_every == 0 or self.step == cfg.steps:
@@ -111,7 +130,7 @@ class Trainer:
                 if self.device.type == "cuda":
                     torch.cuda.synchronize(self.device)
                 dt = time.perf_counter() - t0
-                vals.update(step=self.step, lr=self.sched.get_last_lr()[0], elapsed_s=dt,
+                vals.update(step=self.step, skipped=self.skipped, lr=self.sched.get_last_lr()[0], elapsed_s=dt,
                             pairs_per_s=self.step * cfg.batch * self.world / dt)
                 last = vals
                 if self.rank == 0:
@@ -131,7 +150,8 @@ class Trainer:
         os.makedirs(d, exist_ok=True)
         name = f"step_{self.step}"
         ckpt.save_msgpack(self.model, os.path.join(d, name + ".msgpack"))
-        torch.save({"opt": self.opt.state_dict(), "sched": self.sched.state_dict(), "step": self.step},
+        torch.save({"opt": self.opt.state_dict(), "sched": self.sched.state_dict(), "step": self.step,
+                    "skipped": self.skipped},
                    os.path.join(d, name + ".opt.pt"))
         with open(os.path.join(d, "latest.json"), "w") as f:
             json.dump({"step": self.step, "weights": name + ".msgpack", "opt": name + ".opt.pt",
@@ -147,6 +167,7 @@ class Trainer:
         self.opt.load_state_dict(st["opt"])
         self.sched.load_state_dict(st["sched"])
         self.step = int(st["step"])
+        self.skipped = int(st.get("skipped", 0))
 
 
 def main(argv=None):
@@ -155,7 +176,8 @@ def main(argv=None):
         if f_.name == "size":
             ap.add_argument("--size", type=int, nargs=2, default=list(f_.default))
         elif f_.type in ("bool", bool):
-            ap.add_argument(f"--{f_.name.replace('_', '-')}", action="store_true")
+            ap.add_argument(f"--{f_.name.replace('_', '-')}", action=argparse.BooleanOptionalAction,
+                            default=f_.default)
         else:
             typ = {"int": int, "float": float, "str": str}.get(str(f_.type).replace("Optional[str]", "str"), str)
             ap.add_argument(f"--{f_.name.replace('_', '-')}", type=typ if f_.default is not None else str,

@@ -132,3 +132,21 @@ def test_flow_head_modes_agree(flow_head):
     mag = a.norm(dim=-1).mean().item()
     assert _epe(a[-1], b[-1]) < 0.01 * mag + 0.01
 
+
+
+@pytest.mark.parametrize("final_only", [False, True])
+def test_pipelined_submit_matches_forward(final_only):
+    """Cross-batch pipelining (prologue graph of batch i+1 || loop graph of
+    batch i, two plan slots): every result equals the synchronous forward of
+    the same batch, bitwise (same kernels and tile configs, own buffers)."""
+    model, _ = raft_large()
+    model = model.cuda()
+    eng = model.engine(torch.device("cuda", 0))
+    batches = [tuple(t.cuda() for t in _inputs(2, 128, 160, seed=10 + k)) for k in range(4)]
+    refs = [eng.forward(a, b, 3, return_all_iters=not final_only) for a, b in batches]
+    torch.cuda.synchronize()
+    pend = [eng.submit(a, b, 3, return_all_iters=not final_only) for a, b in batches]
+    outs = [p.result() for p in pend]
+    for r, o in zip(refs, outs):
+        assert o.shape == r.shape
+        assert torch.equal(o, r)

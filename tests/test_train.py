@@ -65,6 +65,42 @@ def test_trainer_cpu_and_resume(tmp_path):
     assert tr2.step == 3
 
 
+def test_trainer_skips_injected_nonfinite_step():
+    """Failure detection: a poisoned step (fault injection) is dropped on every
+    rank, leaves the weights finite and untouched, and training carries on."""
+    cfg = TrainConfig(arch="raft_small", steps=3, batch=1, iters=2, size=(128, 128), log_every=1,
+                      lr=1e-4, fault_nan_step=2)
+    tr = Trainer(cfg, device=torch.device("cpu"))
+    tr.train_step(tr.batch_for(0))
+    w1 = {n: p.detach().clone() for n, p in tr.model.named_parameters()}
+    m = tr.train_step(tr.batch_for(1))  # step 2: NaN loss -> dropped
+    assert tr.skipped == 1 and not torch.isfinite(m["grad_norm"])
+    assert all(torch.equal(w1[n], p) for n, p in tr.model.named_parameters())
+    tr.train_step(tr.batch_for(2))
+    assert tr.step == 3 and tr.skipped == 1
+    assert all(torch.isfinite(p).all() for p in tr.model.parameters())
+    cfg.max_skipped, cfg.fault_nan_step = 0, 4
+    with pytest.raises(FloatingPointError):
+        tr.train_step(tr.batch_for(3))
+
+
+def test_trainer_crash_resume_matches_uninterrupted(tmp_path):
+    """Checkpoint/resume: stopping after step 2 and resuming to step 3 gives the
+    same weights as an uninterrupted 3-step run (optimizer + LR schedule state
+    and the step-indexed data stream are all restored)."""
+    kw = dict(arch="raft_small", batch=1, iters=2, size=(128, 128), log_every=1, lr=1e-4)
+    full = Trainer(TrainConfig(steps=3, **kw), device=torch.device("cpu"))
+    full.fit(log=lambda s: None)
+    a = Trainer(TrainConfig(steps=3, ckpt_dir=str(tmp_path), **kw), device=torch.device("cpu"))
+    a.fit(log=lambda s: None, stop_at=2)
+    del a  # "crash"
+    b = Trainer(TrainConfig(steps=3, ckpt_dir=str(tmp_path), resume=True, **kw), device=torch.device("cpu"))
+    assert b.step == 2
+    b.fit(log=lambda s: None)
+    for (n, p), q in zip(full.model.named_parameters(), b.model.parameters()):
+        assert torch.allclose(p, q, rtol=1e-5, atol=1e-6), n
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
