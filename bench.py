@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--gate-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="storage of the GRU z gate / folded context bias map (the hidden state is fp32 either way)")
     ap.add_argument("--flow-lane", default="side", choices=["side", "main"])
+    ap.add_argument("--mask-head", default="split", choices=["split", "fused"],
+                    help="mask predictor 3x3 conv on the mask lane (split) or batched with the flow head's (fused)")
     ap.add_argument("--double-buffer", action="store_true", help="parity double-buffering of the flow head outputs")
     ap.add_argument("--no-direct-flow", action="store_true", help="flow branch 7x7 conv on the implicit GEMM instead of the direct VALU kernel")
     ap.add_argument("--split", type=int, default=1, help="independent batch parts (one hipGraph each) run concurrently per GPU")
@@ -102,7 +104,7 @@ def main():
     engine_kw = dict(use_graph=not args.no_graph, streams=not args.no_streams, split=args.split,
                      flow_head=args.flow_head, double_buffer=args.double_buffer, direct_flow=not args.no_direct_flow,
                      gate_dtype=torch.bfloat16 if args.gate_dtype == "bf16" else torch.float32,
-                     flow_lane=args.flow_lane)
+                     flow_lane=args.flow_lane, mask_head=args.mask_head)
     pipelined = args.pipeline and not args.no_graph
     eng = model.engine(dev, **engine_kw) if pipelined else None
 
@@ -190,6 +192,7 @@ def main():
                 "flow_head": args.flow_head,
                 "gate_dtype": args.gate_dtype,
                 "flow_lane": args.flow_lane,
+                "mask_head": args.mask_head,
                 "direct_flow_conv": not args.no_direct_flow,
                 "batch_parts": args.split,
                 "cross_batch_pipeline": bool(pipelined),

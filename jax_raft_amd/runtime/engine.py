@@ -173,14 +173,22 @@ class RaftEngine:
             flow, ``model.py:282-283``) on the direct VALU kernel
             (conv_direct.hip) instead of the implicit GEMM, whose 49 gathered
             taps of 2 real channels starve the MFMA loader.
+        mask_head: (raft_large, all-iterations output) "split" (default) runs
+            only the flow head's 3x3 conv (128 -> 256) on the critical path and
+            the mask predictor's 3x3 conv (128 -> 256, ``model.py:389-390``) on
+            the mask lane, reading h before the next iteration's first GRU
+            overwrites it (event-ordered); "fused" runs both 3x3 convs as one
+            128 -> 512 GEMM on the critical path.
     """
 
     def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True,
                  corr_dtype: torch.dtype = torch.bfloat16, autotune: bool = True, streams: bool = True,
                  split: int = 1, flow_head: str = "taps", double_buffer: bool = False,
                  fused_flow_head: bool = False, gate_dtype: torch.dtype = torch.bfloat16,
-                 flow_lane: str = "side", direct_flow: bool = True):
+                 flow_lane: str = "side", direct_flow: bool = True, mask_head: str = "split"):
         nat.require()
+        assert mask_head in ("split", "fused"), mask_head
+        self.mask_head = mask_head if streams else "fused"
         self.direct_flow = direct_flow
         self._cf1_w = self._cf1_b = None
         self.gate_dtype = gate_dtype
@@ -347,7 +355,8 @@ class RaftEngine:
                 return k, b, (1, 1), (1, 1), None
 
             self._reg("fh1", fh1)
-            self._reg("fh1.flow", conv_src(fh.conv1))  # final-only mode: flow head alone in the loop
+            self._reg("fh1.flow", conv_src(fh.conv1))  # final-only mode / split mask head: flow head alone
+            self._reg("mask.convrelu", cna_src(mp.convrelu))
             self._reg("mask", conv_src(mp.conv))
         else:
             self._reg("fh1", conv_src(fh.conv1))
@@ -506,6 +515,7 @@ class RaftEngine:
         # ---------------- prologue: encoders + correlation pyramid
         # lanes: 0 = feature encoder + correlation pyramid, 1 = context encoder
         E_PREP, E_CTX, E_IT, E_FLOW, E_FH, E_MASK = range(ev0, ev0 + 6)  # E_MASK + 1: odd-iteration mask head
+        E_MR = ev0 + 7  # split mask head: the mask lane has read h (the next GRU may overwrite it)
         main, side, side2 = lanes
 
         def lane(l):
@@ -582,17 +592,21 @@ class RaftEngine:
                 self._conv(plan, sp["me.convflow1"], flow8, B, h, w, f1, act=ACT_RELU)
             self._conv(plan, sp["me.convflow2"], f1, B, h, w, cf, y_coff=cl[-1], act=ACT_RELU)
 
-        s1 = sp["fh1"] if (all_iters or not self.has_mask) else sp["fh1.flow"]
-        fm_ch = round_up(sp["fh1"].cout, 8)
+        split_mask = self.has_mask and all_iters and self.mask_head == "split" and not self.double_buffer
+        s1 = sp["fh1"] if (all_iters and not split_mask or not self.has_mask) else sp["fh1.flow"]
+        fm_ch = round_up((s1 if split_mask else sp["fh1"]).cout, 8)
+        mfeat = alloc("mfeat", (M, round_up(sp["mask.convrelu"].cout, 8))) if split_mask else None
         mask = alloc("mask", (M, 576)) if self.has_mask else None
         stride = st.out.shape[1] * H * W * 2  # one iteration of the full-batch output
         taps = alloc("fh2.taps", (M, 24), F32) if self.flow_head == "taps" else None
 
-        def flow_head(fm, f32):
+        def flow_head(fm, f32, before_update=None):
             self._conv(plan, s1, hx, B, h, w, fm, act=ACT_RELU)
             # flow head conv2 + coordinate update (model.py:505) + flow into hx/qx/flow8
             if self.flow_head == "taps":
                 self._conv(plan, sp["fh2.taps"], fm, B, h, w, taps)
+                if before_update is not None:
+                    before_update()
                 plan.add_flow_taps([taps, self._fh2_b, coords, f32, hx, qx, flow8], [B, h, w, self.flow_off, self.flow_off])
             elif self.flow_head == "fused" and self.fh_hidden in (128, 256):
                 plan.add_flow_head([fm, self._fh2_w, self._fh2_b, coords, f32, hx, qx, flow8],
@@ -603,7 +617,13 @@ class RaftEngine:
 
         def upsample(fm, f32, stride):
             if self.has_mask:
-                self._conv(plan, sp["mask"], fm, B, h, w, mask, x_coff=self.fh_hidden,
+                if split_mask:
+                    self._conv(plan, sp["mask.convrelu"], hx, B, h, w, mfeat, act=ACT_RELU)
+                    plan.add_record(E_MR)
+                    fm, coff = mfeat, 0
+                else:
+                    coff = self.fh_hidden
+                self._conv(plan, sp["mask"], fm, B, h, w, mask, x_coff=coff,
                            alpha=m.mask_predictor.multiplier)
                 plan.add_upsample_convex([mask, f32, out], [B, h, w, stride])
             else:
@@ -633,6 +653,8 @@ class RaftEngine:
             # r*h from the bf16 h of the conv's own input hx (no fp32 state read)
             self._conv(plan, sp[f"gru{gi}.a"], hx, B, h, w, qx, zbuf=zb, hidden=self.hidden,
                        epi=EPI_GRU_A, bmap=gbias[gi], bmap_coff=0)
+            if gi == 0 and split_mask:
+                plan.add_wait(E_MR)  # the previous iteration's mask head has read h
             self._conv(plan, sp[f"gru{gi}.b"], qx, B, h, w, hx, h32=h32, zbuf=zb, hidden=self.hidden,
                        epi=EPI_GRU_B, bmap=gbias[gi], bmap_coff=2 * self.hidden)
         if all_iters:
@@ -649,8 +671,13 @@ class RaftEngine:
                 if len(fms) > 1:
                     plan.set_parity(par)
                 lane(main)
-                plan.add_wait(E_MASK + par)
-                flow_head(fms[par], f32s[par])
+                if split_mask and self.flow_head == "taps":
+                    # the flow head's features are not read by the mask lane: only
+                    # the flow update (flow32) must wait for the last upsampling
+                    flow_head(fms[par], f32s[par], before_update=lambda p=par: plan.add_wait(E_MASK + p))
+                else:
+                    plan.add_wait(E_MASK + par)
+                    flow_head(fms[par], f32s[par])
                 plan.add_record(E_FH)
                 lane(side2)
                 plan.add_wait(E_FH)

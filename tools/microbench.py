@@ -105,15 +105,17 @@ def main():
     if not args.only or "corr" in args.only or "lookup" in args.only:
         C = 256
         f = rnd(2 * B, h, w, C)
-        lv = []
-        hl, wl = h, w
-        for _ in range(4):
-            lv.append(torch.empty(M, hl, wl, device=dev))
-            hl //= 2
-            wl //= 2
-        us = timeit(lambda: nat.ops().corr([f[:B], f[B:]] + lv, [B, h, w, C, 4], 1 / 16.0), iters=5)
-        res["corr_pyramid"] = {"us": us, "tflops": 2.0 * B * (h * w) ** 2 * C / us / 1e6}
-        print(f"corr_pyramid {us:8.1f} us  {2.0 * B * (h * w) ** 2 * C / us / 1e6:.1f} TF/s")
+        for dt in (torch.float32, torch.bfloat16):  # bf16 = the engine's default pyramid storage
+            lv = []
+            hl, wl = h, w
+            for _ in range(4):
+                lv.append(torch.empty(M, hl, wl, device=dev, dtype=dt))
+                hl //= 2
+                wl //= 2
+            us = timeit(lambda: nat.ops().corr([f[:B], f[B:]] + lv, [B, h, w, C, 4], 1 / 16.0), iters=5)
+            tag = "corr_pyramid" + ("" if dt == torch.bfloat16 else "_fp32")
+            res[tag] = {"us": us, "tflops": 2.0 * B * (h * w) ** 2 * C / us / 1e6}
+            print(f"{tag:12s} {us:8.1f} us  {2.0 * B * (h * w) ** 2 * C / us / 1e6:.1f} TF/s", flush=True)
         coords = (torch.stack(torch.meshgrid(torch.arange(w), torch.arange(h), indexing="xy"), -1).float()
                   .reshape(1, h * w, 2).repeat(B, 1, 1).reshape(M, 2).to(dev))
         coords += torch.randn_like(coords) * 3
