@@ -178,6 +178,38 @@ JR_DEVICE void epi_pixel(const ConvParams& p, float (&v)[NV], int m, int cbase) 
         for (int j = 0; j < NV; ++j) if (cbase + j < p.split) hp[j] = v[j];
       }
     }
+  } else if constexpr (EPI == EPI_CONVEX) {
+    // Fused MaskPredictor 1x1 conv + convex x8 upsampling (model.py:85-98, :394-400):
+    // this lane holds the 9 neighbour logits of sub-pixel s = cbase / 16 of pixel m.
+    if constexpr (NV == 16) {
+      const int OHW = p.OH * p.OW;
+      const int b = m / OHW, rem = m - b * OHW;
+      const int y = rem / p.OW, x = rem - y * p.OW;
+      const int s = cbase >> 4;
+      float mx = -3.0e38f;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        v[k] *= p.alpha;
+        mx = fmaxf(mx, v[k]);
+      }
+      float sum = 0.f, ux = 0.f, uy = 0.f;
+      const float* fb = p.flow32 + 2L * b * OHW;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int yy = y + k / 3 - 1, xx = x + k % 3 - 1;
+        const float e = __expf(v[k] - mx);
+        sum += e;
+        if ((unsigned)yy < (unsigned)p.OH && (unsigned)xx < (unsigned)p.OW) {
+          const float2 f = *(const float2*)(fb + 2 * (yy * p.OW + xx));
+          ux += e * f.x;
+          uy += e * f.y;
+        }
+      }
+      const float inv = 8.0f / sum;
+      const long W8 = 8L * p.OW;
+      float* op = (float*)p.y + 2 * (((long)b * 8 * p.OH + 8 * y + (s >> 3)) * W8 + 8 * x + (s & 7));
+      *(float2*)op = make_float2(ux * inv, uy * inv);
+    }
   } else if constexpr (EPI == EPI_GRU_A) {
     // [z | r] logits -> z (fp32 / bf16) and r*h (bf16) into the q-input buffer.
     // h comes from the fp32 state when given, else from the conv's own bf16
@@ -1002,6 +1034,7 @@ int launch_cfg(const ConvParams* p, int epi, hipStream_t s) {
     case EPI_GRU_A: JR_LAUNCH(EPI_GRU_A) break;
     case EPI_GRU_B: JR_LAUNCH(EPI_GRU_B) break;
     case EPI_FLOW: JR_LAUNCH(EPI_FLOW) break;
+    case EPI_CONVEX: JR_LAUNCH(EPI_CONVEX) break;
     default: return (int)hipErrorInvalidValue;
   }
 #undef JR_LAUNCH

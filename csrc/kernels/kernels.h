@@ -17,6 +17,9 @@ enum ConvEpi : int {
   EPI_GRU_A = 1,  // channels [0,Hd): z = sigmoid -> zbuf ; [Hd,2Hd): r = sigmoid -> rh = r*h32 -> y
   EPI_GRU_B = 2,  // q = tanh ; h = (1-z) h + z q -> h32, y (bf16 copy of h), y2 (second copy)
   EPI_FLOW = 3,   // delta = acc+bias (2 ch): coords += delta ; flow = coords - coords0 -> flow32, y/y2 (bf16)
+  EPI_CONVEX = 4, // mask logits in subpixel-major order (channel s*16 + k, k < 9 real): *alpha -> softmax
+                  // over the 9 neighbours -> convex combination of 8*flow32 at the 3x3 neighbours ->
+                  // fp32 upsampled flow written straight into y = out[B][8 OH][8 OW][2]
 };
 
 struct ConvParams {

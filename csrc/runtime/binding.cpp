@@ -67,8 +67,11 @@ static void check_f32(const at::Tensor& t, const char* name) {
 // i = [N, H, W, x_coff, cin8, KH, KW, SH, SW, PH, PW, cout, act, split,
 //      y_coff, y2_coff, res_coff, hidden, y3_coff, epi, cfg, res_post
 //      (, OH_override, OW_override, log2 dil_h, log2 dil_w (, bmap_coff))]
+static int64_t check_flow_out(const at::Tensor& out, int B, int h, int w);
+
 static Launch make_conv(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep) {
-  TORCH_CHECK(i.size() == 22 || i.size() == 26 || i.size() == 27, "conv: expected 22, 26 or 27 ints");
+  TORCH_CHECK(i.size() == 22 || i.size() == 26 || i.size() == 27 || i.size() == 28,
+              "conv: expected 22, 26, 27 or 28 ints");
   at::Tensor x = opt(t, 0), w = opt(t, 1), bias = opt(t, 2), y = opt(t, 3), y2 = opt(t, 4), res = opt(t, 5);
   at::Tensor h32 = opt(t, 6), zbuf = opt(t, 7), coords = opt(t, 8), flow32 = opt(t, 9), y3 = opt(t, 10);
   at::Tensor bmap = opt(t, 11);
@@ -106,7 +109,8 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   p.y3 = ptr(y3); p.y3_cstride = cs(y3); p.y3_coff = (int)i[18];
   p.bmap = ptr(bmap);
   p.bmap_cstride = bmap.defined() ? cs(bmap) : 0;
-  p.bmap_coff = i.size() == 27 ? (int)i[26] : 0;
+  p.bmap_coff = i.size() >= 27 ? (int)i[26] : 0;
+  const int64_t it_stride = i.size() >= 28 ? i[27] : 0;  // EPI_CONVEX: output floats per loop iteration
   p.bmap_bf16 = bmap.defined() && bmap.scalar_type() == at::kBFloat16;
   p.z_bf16 = zbuf.defined() && zbuf.scalar_type() == at::kBFloat16;
   if (bmap.defined()) {
@@ -117,11 +121,11 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
                 "conv: bias map channel slice must be 8-aligned and inside the tensor");
     TORCH_CHECK(bmap.numel() >= (int64_t)p.M * p.bmap_cstride, "conv: bias map too small");
   }
+  const int epi = (int)i[19];
   {
     const int taps = p.KH * p.KW;
     p.fast = p.dsh == 0 && p.dsw == 0 && taps <= 32 && (taps == 1 || p.cin8 % 64 == 0) && !std::getenv("JR_CONV_NO_FAST");
   }
-  const int epi = (int)i[19];
   int cfg = (int)i[20];
   // Timing-only ablation (tools/microbench.py --ablate): cfg bits 8/9 give the
   // X / W buffer descriptors zero records, so every load through them is
@@ -139,8 +143,13 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   TORCH_CHECK(p.kpad % 64 == 0 && p.kpad >= p.KH * p.KW * p.cin8, "conv: packed weight K mismatch");
   TORCH_CHECK(p.cout_pad % 64 == 0 && p.cout_pad >= p.cout && bias.numel() >= p.cout, "conv: packed weight rows (64-row groups)");
   TORCH_CHECK(p.OH > 0 && p.OW > 0, "conv: empty output");
-  TORCH_CHECK(p.y_cstride % 8 == 0, "conv: output channel stride must be a multiple of 8");
-  TORCH_CHECK((int64_t)p.M * p.y_cstride <= y.numel(), "conv: output tensor too small");
+  int64_t out_cap = 0;
+  if (epi == EPI_CONVEX) {
+    out_cap = check_flow_out(y, p.N, p.OH, p.OW);
+  } else {
+    TORCH_CHECK(p.y_cstride % 8 == 0, "conv: output channel stride must be a multiple of 8");
+    TORCH_CHECK((int64_t)p.M * p.y_cstride <= y.numel(), "conv: output tensor too small");
+  }
   if (epi == EPI_STD) {
     TORCH_CHECK(p.y_coff % 8 == 0 && p.y_coff + p.cout <= p.y_cstride, "conv: output slice");
     TORCH_CHECK(y.scalar_type() == at::kBFloat16 || y.scalar_type() == at::kFloat, "conv: output dtype");
@@ -168,11 +177,30 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   } else if (epi == EPI_FLOW) {
     check_f32(coords, "coords"); check_f32(flow32, "flow32"); check_bf16(y, "y");
     TORCH_CHECK(p.cout == 2, "FLOW: cout must be 2");
+  } else if (epi == EPI_CONVEX) {
+    check_f32(flow32, "flow32");
+    TORCH_CHECK(flow32.numel() >= (int64_t)p.M * 2, "CONVEX: flow32 must be [M][2]");
+    TORCH_CHECK(p.cout % 16 == 0 && p.cout >= 16 && p.act == 0 /* ACT_NONE */ && !bmap.defined(),
+                "CONVEX: logits in 16-channel sub-pixel groups, no activation / bias map");
+    // the epilogue needs 16 contiguous channels per lane: every config but the 16- / 32-row wave tiles
+    TORCH_CHECK(cfg != 3 && cfg != 5 && cfg != 19 && cfg != 21, "CONVEX: tile config ", cfg,
+                " has < 16 channels per lane");
+    TORCH_CHECK(it_stride >= 0, "CONVEX: iteration stride");
   } else {
     TORCH_CHECK(false, "conv: unknown epilogue ", epi);
   }
   TORCH_CHECK(cfg >= 0 && cfg <= 34 && !(cfg >= 29 && cfg <= 32), "conv: unknown tile config ", cfg);
   if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3, bmap}) if (v.defined()) keep->push_back(v);
+  if (epi == EPI_CONVEX) {
+    const int64_t need = (int64_t)p.N * 64 * p.OH * p.OW * 2;
+    return [p, epi, cfg, it_stride, out_cap, need](hipStream_t s, int it) {
+      const int64_t off = it_stride * it;
+      if (off + need > out_cap) return (int)hipErrorInvalidValue;
+      ConvParams q = p;
+      q.y = (float*)p.y + off;
+      return jr_conv_forward(&q, cfg, epi, s);
+    };
+  }
   return [p, epi, cfg](hipStream_t s, int) { return jr_conv_forward(&p, cfg, epi, s); };
 }
 

@@ -48,6 +48,7 @@ from ..ops.native import (
     ACT_NONE,
     ACT_RELU,
     ACT_SPLIT_TANH_RELU,
+    EPI_CONVEX,
     EPI_FLOW,
     EPI_GRU_A,
     EPI_GRU_B,
@@ -68,6 +69,8 @@ def _tune(spec: ConvSpec, x, N, H, W, y, kw, reps: int = 5) -> int:
     ops = nat.ops()
     best, best_t = None, None
     for cfg in nat.TUNE_CFGS:
+        if kw.get("epi") == nat.EPI_CONVEX and cfg in nat.NARROW_CFGS:
+            continue
         args = conv_args(spec, x, N, H, W, y, **dict(kw, cfg=cfg))
         ops.conv(*args)  # warm (and JIT-free: all configs are precompiled)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -179,14 +182,25 @@ class RaftEngine:
             the mask lane, reading h before the next iteration's first GRU
             overwrites it (event-ordered); "fused" runs both 3x3 convs as one
             128 -> 512 GEMM on the critical path.
+        convex: (raft_large) "fused" (default) computes the mask predictor's
+            1x1 conv (256 -> 576, ``model.py:394-400``) with the EPI_CONVEX
+            epilogue: output channels reordered sub-pixel-major (9 logits of a
+            sub-pixel in one lane), softmax + convex combination of the 3x3
+            flow neighbourhood and the x8 pixel shuffle (``model.py:85-98``) in
+            registers, the upsampled flow written straight to the output (no
+            576-channel mask round trip, one launch less per iteration);
+            "separate" = mask conv + upsample_convex kernel.
     """
 
     def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True,
                  corr_dtype: torch.dtype = torch.bfloat16, autotune: bool = True, streams: bool = True,
                  split: int = 1, flow_head: str = "taps", double_buffer: bool = False,
                  fused_flow_head: bool = False, gate_dtype: torch.dtype = torch.bfloat16,
-                 flow_lane: str = "side", direct_flow: bool = True, mask_head: str = "split"):
+                 flow_lane: str = "side", direct_flow: bool = True, mask_head: str = "split",
+                 convex: str = "fused"):
         nat.require()
+        assert convex in ("fused", "separate"), convex
+        self.convex = convex
         assert mask_head in ("split", "fused"), mask_head
         self.mask_head = mask_head if streams else "fused"
         self.direct_flow = direct_flow
@@ -358,6 +372,8 @@ class RaftEngine:
             self._reg("fh1.flow", conv_src(fh.conv1))  # final-only mode / split mask head: flow head alone
             self._reg("mask.convrelu", cna_src(mp.convrelu))
             self._reg("mask", conv_src(mp.conv))
+            self._reg("mask.convex", lambda: (*nat.convex_mask_kernel(mp.conv.kernel, mp.conv.bias), (1, 1), (0, 0),
+                                              None))
         else:
             self._reg("fh1", conv_src(fh.conv1))
         self._reg("fh2", conv_src(fh.conv2))
@@ -596,7 +612,7 @@ class RaftEngine:
         s1 = sp["fh1"] if (all_iters and not split_mask or not self.has_mask) else sp["fh1.flow"]
         fm_ch = round_up((s1 if split_mask else sp["fh1"]).cout, 8)
         mfeat = alloc("mfeat", (M, round_up(sp["mask.convrelu"].cout, 8))) if split_mask else None
-        mask = alloc("mask", (M, 576)) if self.has_mask else None
+        mask = alloc("mask", (M, 576)) if self.has_mask and self.convex != "fused" else None
         stride = st.out.shape[1] * H * W * 2  # one iteration of the full-batch output
         taps = alloc("fh2.taps", (M, 24), F32) if self.flow_head == "taps" else None
 
@@ -623,9 +639,14 @@ class RaftEngine:
                     fm, coff = mfeat, 0
                 else:
                     coff = self.fh_hidden
-                self._conv(plan, sp["mask"], fm, B, h, w, mask, x_coff=coff,
-                           alpha=m.mask_predictor.multiplier)
-                plan.add_upsample_convex([mask, f32, out], [B, h, w, stride])
+                if self.convex == "fused":
+                    # mask logits never leave the CU: softmax + convex combination in the epilogue
+                    self._conv(plan, sp["mask.convex"], fm, B, h, w, out, x_coff=coff, epi=EPI_CONVEX,
+                               flow32=f32, alpha=m.mask_predictor.multiplier, it_stride=stride)
+                else:
+                    self._conv(plan, sp["mask"], fm, B, h, w, mask, x_coff=coff,
+                               alpha=m.mask_predictor.multiplier)
+                    plan.add_upsample_convex([mask, f32, out], [B, h, w, stride])
             else:
                 plan.add_upsample_bilinear([f32, out], [B, h, w, stride])
 

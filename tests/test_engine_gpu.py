@@ -167,3 +167,22 @@ def test_split_mask_head_matches_fused():
     for it in range(6):
         assert _epe(a[it], b[it]) < 0.02 * mag + 0.02, it
     assert (a - c).abs().max().item() < 1e-3
+
+
+@pytest.mark.parametrize("final_only", [False, True])
+def test_fused_convex_upsample_matches_separate(final_only):
+    """The EPI_CONVEX conv (MaskPredictor 1x1 conv with softmax + convex x8
+    upsampling in its epilogue, sub-pixel-major logits) equals the mask conv +
+    upsample_convex kernel pair, and both track the fp32 golden forward."""
+    model, variables = raft_large()
+    i1, i2 = _inputs(2, 128, 160, seed=31)
+    ref = model.apply(variables, i1, i2, num_flow_updates=3)
+    model = model.cuda()
+    a = model(i1.cuda(), i2.cuda(), num_flow_updates=3, convex="fused", return_all_iters=not final_only)
+    b = model(i1.cuda(), i2.cuda(), num_flow_updates=3, convex="separate", return_all_iters=not final_only)
+    torch.cuda.synchronize()
+    assert a.shape == b.shape
+    mag = ref.norm(dim=-1).mean().item()
+    for it in range(a.shape[0]):
+        assert _epe(a[it], b[it]) < 0.01 * mag + 0.01, it
+    assert _epe(a[-1].cpu(), ref[-1]) < 0.05 * mag + 0.05
