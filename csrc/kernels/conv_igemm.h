@@ -310,6 +310,23 @@ JR_DEVICE void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM][TN], int mbas
   });
 }
 
+// XCD-aware tile order.  MI355X dispatches workgroups round-robin over its 8
+// XCDs (private L2 each), so consecutive linear ids -- neighbouring pixel
+// tiles, which share the input rows of a 3x3 / 1x5 / 5x1 window -- land on
+// different L2s.  Remap the linear id so every XCD walks a contiguous run of
+// tiles (bijective for any grid size; dispatch placement only changes speed).
+JR_DEVICE void tile_of_block(const ConvParams& p, int& bx, int& by) {
+  bx = blockIdx.x;
+  by = blockIdx.y;
+  const int nx = gridDim.x, nwg = nx * gridDim.y;
+  if (!p.xcd_remap || nwg <= 8) return;
+  const int bid = by * nx + bx;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  bx = t % nx;
+  by = t / nx;
+}
+
 // Per-row state of the FAST im2col loader (ConvParams::fast): the byte offset
 // of the row's first tap + this lane's 16-B chunk, and a bitmask of the taps
 // (kh * KW + kw) that fall inside the input.  A stage's tap and channel block
@@ -367,8 +384,10 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(const ConvParams p)
   const int wave = tid >> 6;
   const int wco = wave % WCO;
   const int wp = wave / WCO;
-  const int p0 = blockIdx.x * BP;
-  const int co0 = blockIdx.y * BCO;
+  int bx_, by_;
+  tile_of_block(p, bx_, by_);
+  const int p0 = bx_ * BP;
+  const int co0 = by_ * BCO;
   const int ch = tid & 7;
   const int OHW = p.OH * p.OW;
 
@@ -641,8 +660,10 @@ __global__ __launch_bounds__(NW * 64) void conv_m32_kernel(const ConvParams p) {
   const int wave = tid >> 6;
   const int wco = wave % WCO;
   const int wp = wave / WCO;
-  const int p0 = blockIdx.x * BP;
-  const int co0 = blockIdx.y * BCO;
+  int bx_, by_;
+  tile_of_block(p, bx_, by_);
+  const int p0 = bx_ * BP;
+  const int co0 = by_ * BCO;
   const int ch = tid & 7;
   const int OHW = p.OH * p.OW;
 
@@ -874,8 +895,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, (BCO + B
   const int wave = tid >> 6;
   const int wco = wave % WCO;
   const int wp = wave / WCO;
-  const int p0 = blockIdx.x * BP;
-  const int co0 = blockIdx.y * BCO;
+  int bx_, by_;
+  tile_of_block(p, bx_, by_);
+  const int p0 = bx_ * BP;
+  const int co0 = by_ * BCO;
   const int OHW = p.OH * p.OW;
   const int cl = (lane & 7) ^ ((lane >> 3) & 6);   // this lane's fixed logical chunk in a stage
 

@@ -68,6 +68,8 @@ struct ConvParams {
   // 32 taps) and there is no input dilation: the register-staged kernels then use wave-uniform
   // tap state and per-row tap bitmasks instead of per-lane im2col arithmetic
   int fast;
+  // 1: XCD-aware workgroup -> tile order (conv_igemm.h:xcd_tile); 0: dispatch order
+  int xcd_remap;
 };
 
 // cfg (co x px block tile): kernel R (register-staged, 16x16x32 MFMA) 0 = 128x128, 1 = 64x128,

@@ -125,6 +125,7 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   {
     const int taps = p.KH * p.KW;
     p.fast = p.dsh == 0 && p.dsw == 0 && taps <= 32 && (taps == 1 || p.cin8 % 64 == 0) && !std::getenv("JR_CONV_NO_FAST");
+    p.xcd_remap = std::getenv("JR_CONV_XCD") ? 1 : 0;  // measured: -0.5..1.4 % on the RAFT convs (inputs MALL-resident)
   }
   int cfg = (int)i[20];
   // Timing-only ablation (tools/microbench.py --ablate): cfg bits 8/9 give the
