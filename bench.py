@@ -43,7 +43,9 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-h2d", action="store_true", help="inputs already resident on the GPU")
     ap.add_argument("--sync-h2d", action="store_true", help="copy each step's inputs synchronously (no prefetch overlap)")
-    ap.add_argument("--no-streams", action="store_true", help="single-lane plan (no concurrent branches)")
+    ap.add_argument("--streams", default="auto", choices=["auto", "on", "off"],
+                    help="concurrent model branches on plan lanes: auto = at batch >= 4 per GPU (measured break-even)")
+    ap.add_argument("--no-streams", action="store_true", help="same as --streams off")
     ap.add_argument("--flow-head", default="taps", choices=["taps", "conv", "fused"],
                     help="flow head output conv: 1x1 GEMM + tap sum (default), 3x3 conv, or the halo-tiled kernel")
     ap.add_argument("--final-only", action="store_true",
@@ -101,7 +103,8 @@ def main():
     # (InputPrefetcher), so only the first copy of a run is exposed.
     pf = None if (args.no_h2d or args.sync_h2d) else InputPrefetcher([(B, H, W, 3), (B, H, W, 3)], dev)
 
-    engine_kw = dict(use_graph=not args.no_graph, streams=not args.no_streams, split=args.split,
+    streams = False if args.no_streams else {"auto": "auto", "on": True, "off": False}[args.streams]
+    engine_kw = dict(use_graph=not args.no_graph, streams=streams, split=args.split,
                      flow_head=args.flow_head, double_buffer=args.double_buffer, direct_flow=not args.no_direct_flow,
                      gate_dtype=torch.bfloat16 if args.gate_dtype == "bf16" else torch.float32,
                      flow_lane=args.flow_lane, mask_head=args.mask_head)
@@ -188,7 +191,7 @@ def main():
                 "num_flow_updates": args.iters,
                 "outputs": "final iteration only (serving mode)" if args.final_only else "all iterations upsampled (reference semantics)",
                 "hipgraph": not args.no_graph,
-                "concurrent_branches": not args.no_streams,
+                "concurrent_branches": (streams if streams != "auto" else f"auto (on: batch >= 4)"),
                 "flow_head": args.flow_head,
                 "gate_dtype": args.gate_dtype,
                 "flow_lane": args.flow_lane,

@@ -147,7 +147,8 @@ class RaftEngine:
             fp32 for bit-closer parity with the fp32 reference).
         autotune: time every conv tile config on the real buffers when a plan
             is built and keep the fastest (cached per problem signature).
-        streams: place the model's independent branches on side lanes of the
+        streams: (True / False / "auto" = True at batch >= 4 per plan, where
+            it measured faster) place the model's independent branches on side lanes of the
             plan (context encoder || feature encoder + correlation pyramid;
             flow-feature convs || lookup + correlation convs; mask head +
             upsampling of iteration i || iteration i+1) so they overlap on
@@ -193,7 +194,7 @@ class RaftEngine:
     """
 
     def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True,
-                 corr_dtype: torch.dtype = torch.bfloat16, autotune: bool = True, streams: bool = True,
+                 corr_dtype: torch.dtype = torch.bfloat16, autotune: bool = True, streams="auto",
                  split: int = 1, flow_head: str = "taps", double_buffer: bool = False,
                  fused_flow_head: bool = False, gate_dtype: torch.dtype = torch.bfloat16,
                  flow_lane: str = "side", direct_flow: bool = True, mask_head: str = "split",
@@ -202,6 +203,9 @@ class RaftEngine:
         assert convex in ("fused", "separate"), convex
         self.convex = convex
         assert mask_head in ("split", "fused"), mask_head
+        assert streams in (True, False, "auto"), streams
+        self.streams_mode = streams
+        self._mask_head_opt, self._flow_lane_opt = mask_head, flow_lane
         self.mask_head = mask_head if streams else "fused"
         self.direct_flow = direct_flow
         self._cf1_w = self._cf1_b = None
@@ -477,7 +481,27 @@ class RaftEngine:
                     x, H, W = y, h_, w_
         return x, H, W
 
+    # lanes pay off once the per-iteration kernels fill the chip: measured on
+    # MI355X (raft_large, 440x1024, 32 iters; tools/probe_launch.py) the lane
+    # schedule is 17-21 % slower at batch 1, equal at batch 2 and 2 % faster
+    # at batch 4 than one in-order lane
+    AUTO_STREAMS_MIN_BATCH = 4
+
     def _build(self, B: int, H: int, W: int, n_iters: int, all_iters: bool = True) -> _PlanState:
+        if self.streams_mode != "auto":
+            return self._build_impl(B, H, W, n_iters, all_iters)
+        nb = B // self.split if (self.split > 1 and B % self.split == 0) else B
+        on = nb >= self.AUTO_STREAMS_MIN_BATCH
+        saved = (self.streams, self.flow_lane, self.mask_head)
+        self.streams = on
+        self.flow_lane = self._flow_lane_opt if on else "main"
+        self.mask_head = self._mask_head_opt if on else "fused"
+        try:
+            return self._build_impl(B, H, W, n_iters, all_iters)
+        finally:
+            self.streams, self.flow_lane, self.mask_head = saved
+
+    def _build_impl(self, B: int, H: int, W: int, n_iters: int, all_iters: bool = True) -> _PlanState:
         h, w = H // 8, W // 8
         L = self.num_levels
         min_sz = 2 * (2 ** (L - 1))

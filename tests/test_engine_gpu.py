@@ -159,9 +159,9 @@ def test_split_mask_head_matches_fused():
     model, _ = raft_large()
     model = model.cuda()
     i1, i2 = (t.cuda() for t in _inputs(2, 128, 160, seed=21))
-    a = model(i1, i2, num_flow_updates=6, mask_head="split")
-    b = model(i1, i2, num_flow_updates=6, mask_head="fused")
-    c = model(i1, i2, num_flow_updates=6, mask_head="split", use_graph=False)
+    a = model(i1, i2, num_flow_updates=6, mask_head="split", streams=True)
+    b = model(i1, i2, num_flow_updates=6, mask_head="fused", streams=True)
+    c = model(i1, i2, num_flow_updates=6, mask_head="split", streams=True, use_graph=False)
     torch.cuda.synchronize()
     mag = b.norm(dim=-1).mean().item()
     for it in range(6):
@@ -186,3 +186,20 @@ def test_fused_convex_upsample_matches_separate(final_only):
     for it in range(a.shape[0]):
         assert _epe(a[it], b[it]) < 0.01 * mag + 0.01, it
     assert _epe(a[-1].cpu(), ref[-1]) < 0.05 * mag + 0.05
+
+
+def test_streams_auto_matches_lanes_and_single_lane():
+    """streams="auto" picks the single in-order lane below batch 4 and the lane
+    schedule from batch 4; all three schedules give the same flows."""
+    model, _ = raft_small()
+    model = model.cuda()
+    for B in (1, 4):
+        i1, i2 = (t.cuda() for t in _inputs(B, 128, 128, seed=40 + B))
+        a = model(i1, i2, num_flow_updates=3, streams="auto")
+        b = model(i1, i2, num_flow_updates=3, streams=True)
+        c = model(i1, i2, num_flow_updates=3, streams=False)
+        torch.cuda.synchronize()
+        assert (a - b).abs().max().item() < 1e-3 and (a - c).abs().max().item() < 1e-3
+        eng = model.engine(torch.device("cuda", 0), streams="auto")
+        st = eng._states[(B, 128, 128, 3, True)]
+        assert (st.plan.num_lanes() > 1) == (B >= eng.AUTO_STREAMS_MIN_BATCH)
