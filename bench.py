@@ -44,7 +44,7 @@ def main():
     ap.add_argument("--no-h2d", action="store_true", help="inputs already resident on the GPU")
     ap.add_argument("--sync-h2d", action="store_true", help="copy each step's inputs synchronously (no prefetch overlap)")
     ap.add_argument("--streams", default="auto", choices=["auto", "on", "off"],
-                    help="concurrent model branches on plan lanes: auto = at batch >= 4 per GPU (measured break-even)")
+                    help="concurrent model branches on plan lanes: auto = at batch >= 4 per GPU with all iterations upsampled (measured break-even)")
     ap.add_argument("--no-streams", action="store_true", help="same as --streams off")
     ap.add_argument("--flow-head", default="taps", choices=["taps", "conv", "fused"],
                     help="flow head output conv: 1x1 GEMM + tap sum (default), 3x3 conv, or the halo-tiled kernel")
@@ -191,7 +191,7 @@ def main():
                 "num_flow_updates": args.iters,
                 "outputs": "final iteration only (serving mode)" if args.final_only else "all iterations upsampled (reference semantics)",
                 "hipgraph": not args.no_graph,
-                "concurrent_branches": (streams if streams != "auto" else f"auto (on: batch >= 4)"),
+                "concurrent_branches": (streams if streams != "auto" else ("auto (on: batch >= 4)" if not args.final_only else "auto (off in final-only mode)")),
                 "flow_head": args.flow_head,
                 "gate_dtype": args.gate_dtype,
                 "flow_lane": args.flow_lane,

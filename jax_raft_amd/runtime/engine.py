@@ -147,8 +147,8 @@ class RaftEngine:
             fp32 for bit-closer parity with the fp32 reference).
         autotune: time every conv tile config on the real buffers when a plan
             is built and keep the fastest (cached per problem signature).
-        streams: (True / False / "auto" = True at batch >= 4 per plan, where
-            it measured faster) place the model's independent branches on side lanes of the
+        streams: (True / False / "auto" = True at batch >= 4 per plan with all
+            iterations upsampled, where it measured faster) place the model's independent branches on side lanes of the
             plan (context encoder || feature encoder + correlation pyramid;
             flow-feature convs || lookup + correlation convs; mask head +
             upsampling of iteration i || iteration i+1) so they overlap on
@@ -484,14 +484,17 @@ class RaftEngine:
     # lanes pay off once the per-iteration kernels fill the chip: measured on
     # MI355X (raft_large, 440x1024, 32 iters; tools/probe_launch.py) the lane
     # schedule is 17-21 % slower at batch 1, equal at batch 2 and 2 % faster
-    # at batch 4 than one in-order lane
+    # at batch 4 than one in-order lane.  In final-only mode the loop has no
+    # mask head to overlap, only the flow-feature convs: there lanes measured
+    # 13.1 (one lane) vs 12.7-24.9 ms (lanes, schedule-dependent run to run)
+    # at batch 4, so "auto" keeps one lane.
     AUTO_STREAMS_MIN_BATCH = 4
 
     def _build(self, B: int, H: int, W: int, n_iters: int, all_iters: bool = True) -> _PlanState:
         if self.streams_mode != "auto":
             return self._build_impl(B, H, W, n_iters, all_iters)
         nb = B // self.split if (self.split > 1 and B % self.split == 0) else B
-        on = nb >= self.AUTO_STREAMS_MIN_BATCH
+        on = nb >= self.AUTO_STREAMS_MIN_BATCH and all_iters
         saved = (self.streams, self.flow_lane, self.mask_head)
         self.streams = on
         self.flow_lane = self._flow_lane_opt if on else "main"

@@ -203,3 +203,8 @@ def test_streams_auto_matches_lanes_and_single_lane():
         eng = model.engine(torch.device("cuda", 0), streams="auto")
         st = eng._states[(B, 128, 128, 3, True)]
         assert (st.plan.num_lanes() > 1) == (B >= eng.AUTO_STREAMS_MIN_BATCH)
+        # final-only (serving) mode: "auto" keeps one lane at every batch
+        d = model(i1, i2, num_flow_updates=3, streams="auto", return_all_iters=False)
+        torch.cuda.synchronize()
+        assert (d[-1] - c[-1]).abs().max().item() < 1e-3
+        assert eng._states[(B, 128, 128, 3, False)].plan.num_lanes() == 1

@@ -18,6 +18,10 @@ for mode in sys.argv[2:]:
         _e._TUNE_CACHE.clear()
         m._engines = {}
         continue
+    if mode == "drop":  # drop the built plans, keep engines + autotune cache (plans rebuilt from the cache)
+        for e in m._engines.values():
+            e._states.clear()
+        continue
     if mode == "dumptune":
         from jax_raft_amd.runtime import engine as _e
         for k, v in sorted(_e._TUNE_CACHE.items(), key=str):
