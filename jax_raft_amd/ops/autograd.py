@@ -17,6 +17,7 @@ is PyTorch glue on the framework layer.  ``coords`` never receive a gradient
 from __future__ import annotations
 
 import math
+import weakref
 from typing import List, Sequence, Tuple
 
 import torch
@@ -42,6 +43,38 @@ def _log2_stride(s: int) -> int:
     return int(math.log2(s))
 
 
+_SPEC_CACHE: dict = {}
+_SPEC_CACHE_MAX = 512
+
+
+def _cached_spec(kernel: torch.Tensor, bias, stride, padding, cin8: int, transposed: bool):
+    """Packed-weight ConvSpec, reused while the parameter is unchanged.
+
+    The update block's weights are shared by every refinement iteration, so a
+    12-iteration training step would otherwise re-pack each of them 12x in the
+    forward and 12x (flipped) in the backward.  The key is the parameter's
+    identity (weakref-checked) and its in-place ``_version`` counter, which
+    every optimizer step bumps, so a stale pack is never reused."""
+    key = (id(kernel), kernel._version, None if bias is None else (id(bias), bias._version),
+           tuple(stride), tuple(padding), cin8, transposed, kernel.device)
+    hit = _SPEC_CACHE.get(key)
+    if hit is not None and hit[0]() is kernel and (bias is None or hit[1]() is bias):
+        return hit[2]
+    kh, kw, cin, cout = kernel.shape
+    if transposed:
+        # dX = conv(dilate_s(dY), flip(W)^T), padding k-1-p
+        wt = torch.flip(kernel.detach().float(), dims=(0, 1)).permute(0, 1, 3, 2).contiguous()
+        spec = nat.make_spec(wt, torch.zeros(cin, device=kernel.device), (1, 1),
+                             (kh - 1 - padding[0], kw - 1 - padding[1]), cin8=cin8, device=kernel.device)
+    else:
+        spec = nat.make_spec(kernel.detach(), bias.detach(), tuple(stride), tuple(padding), cin8=cin8,
+                             device=kernel.device)
+    if len(_SPEC_CACHE) >= _SPEC_CACHE_MAX:
+        _SPEC_CACHE.clear()
+    _SPEC_CACHE[key] = (weakref.ref(kernel), None if bias is None else weakref.ref(bias), spec)
+    return spec
+
+
 class Conv2dNHWC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, kernel, bias, stride: Tuple[int, int], padding: Tuple[int, int]):
@@ -50,7 +83,7 @@ class Conv2dNHWC(torch.autograd.Function):
         assert C == cin, f"conv input has {C} channels, kernel expects {cin}"
         cin8 = nat.round_up(cin, 8)
         xb = _pad_channels(x, cin8)
-        spec = nat.make_spec(kernel.detach(), bias.detach(), tuple(stride), tuple(padding), cin8=cin8, device=x.device)
+        spec = _cached_spec(kernel, bias, stride, padding, cin8, transposed=False)
         y = nat.conv2d(spec, xb, out_dtype=BF16)
         ctx.save_for_backward(xb, kernel)
         ctx.meta = (N, H, W, cin, cout, tuple(stride), tuple(padding))
@@ -68,9 +101,7 @@ class Conv2dNHWC(torch.autograd.Function):
         gx = gk = gb = None
         if ctx.needs_input_grad[0]:
             # dX = conv(dilate_s(dY), flip(W)^T), padding k-1-p, output size forced to (H, W)
-            wt = torch.flip(kernel.detach().float(), dims=(0, 1)).permute(0, 1, 3, 2).contiguous()
-            spec = nat.make_spec(wt, torch.zeros(cin, device=gy.device), (1, 1), (kh - 1 - ph, kw - 1 - pw),
-                                 cin8=cout8, device=gy.device)
+            spec = _cached_spec(kernel, None, (1, 1), (ph, pw), cout8, transposed=True)
             gxp = torch.empty(N, H, W, nat.round_up(cin, 8), dtype=BF16, device=gy.device)
             t, i, a = nat.conv_args(spec, gyb, N, OH, OW, gxp)
             i = i + [H, W, _log2_stride(sh), _log2_stride(sw)]
@@ -151,6 +182,32 @@ def build_pyramid(fmap1, fmap2, num_levels: int) -> List[torch.Tensor]:
     return list(CorrPyramid.apply(fmap1, fmap2, num_levels))
 
 
+class _LookupGradAcc:
+    """One fp32 gradient accumulator per pyramid, shared by all of its lookups.
+
+    Every refinement iteration looks up the same pyramid, so per-call level
+    gradients would cost a full zero-filled fp32 pyramid per iteration plus
+    an autograd add of it (hundreds of MB each at training resolution).  The
+    backward kernel accumulates (read-modify-write) instead: every lookup's
+    backward adds into this one buffer and returns no level gradient, except
+    the last one to run, which hands the finished sum to the pyramid's
+    backward.  ``n`` counts the graph's lookups; the countdown re-arms after
+    completion so ``retain_graph`` backward passes also work."""
+
+    def __init__(self):
+        self.n = 0
+        self.left = 0
+        self.bufs = None
+
+
+def _lookup_acc(levels) -> _LookupGradAcc:
+    acc = getattr(levels[0], "_jr_lookup_acc", None)
+    if acc is None:
+        acc = _LookupGradAcc()
+        levels[0]._jr_lookup_acc = acc
+    return acc
+
+
 class PyramidLookup(torch.autograd.Function):
     """levels (fp32), coords (B, h, w, 2) -> (B, h, w, L*(2r+1)^2) bf16."""
 
@@ -169,15 +226,31 @@ class PyramidLookup(torch.autograd.Function):
         nat.ops().lookup([c, out] + lv + [None] * (4 - L), [L, B, h, w, radius, nq])
         ctx.save_for_backward(c)
         ctx.meta = (B, h, w, nq, radius, L, [tuple(l.shape) for l in levels])
+        ctx.acc = None
+        if torch.is_grad_enabled() and any(l.requires_grad for l in levels):
+            ctx.acc = _lookup_acc(levels)
+            ctx.acc.n += 1
+            ctx.acc.left += 1
         return out.reshape(B, hq, wq, ocs)[..., : L * S * S]
 
     @staticmethod
     def backward(ctx, g):
         (c,) = ctx.saved_tensors
         B, h, w, nq, radius, L, shapes = ctx.meta
-        g = g.reshape(B * nq, -1).float().contiguous()
-        dls = [torch.zeros(s, device=g.device, dtype=torch.float32) for s in shapes]
-        nat.ops().lookup_bwd([c, g] + dls + [None] * (4 - L), [L, B, h, w, radius, nq])
+        g = g.reshape(B * nq, -1)
+        g = g.contiguous() if g.dtype in (BF16, torch.float32) else g.float().contiguous()
+        acc = ctx.acc
+        if acc is None:
+            dls = [torch.zeros(s, device=g.device, dtype=torch.float32) for s in shapes]
+            nat.ops().lookup_bwd([c, g] + dls + [None] * (4 - L), [L, B, h, w, radius, nq])
+            return (None, None) + tuple(dls)
+        if acc.bufs is None:
+            acc.bufs = [torch.zeros(s, device=g.device, dtype=torch.float32) for s in shapes]
+        nat.ops().lookup_bwd([c, g] + acc.bufs + [None] * (4 - L), [L, B, h, w, radius, nq])
+        acc.left -= 1
+        if acc.left > 0:
+            return (None, None) + (None,) * L
+        dls, acc.bufs, acc.left = acc.bufs, None, acc.n
         return (None, None) + tuple(dls)
 
 

@@ -89,6 +89,7 @@ def broadcast_module(module: torch.nn.Module, src: int = 0) -> None:
     with torch.no_grad():
         for t in list(module.parameters()) + list(module.buffers()):
             dist.broadcast(t.data, src)
+            t.add_(0)  # bump the version counter (.data writes do not): invalidates cached weight packs
 
 
 class GradAllReducer:

@@ -104,6 +104,54 @@ def test_lookup_backward(radius):
         assert _rel(a.grad, b.grad) < 1e-5
 
 
+def test_lookup_backward_shared_accumulator():
+    """Several lookups of one pyramid (the refinement loop's pattern) sum their
+    level gradients in one shared buffer; a retain_graph second pass repeats."""
+    from jax_raft_amd.ops.autograd import index_pyramid
+
+    torch.manual_seed(5)
+    B, h, w, radius = 2, 16, 20, 4
+    M = B * h * w
+    pyr = []
+    hl, wl = h, w
+    for _ in range(4):
+        pyr.append(torch.randn(M, hl, wl))
+        hl //= 2
+        wl //= 2
+    cs = [R.make_coords_grid(B, h, w) + torch.randn(B, h, w, 2) * 3 for _ in range(3)]
+    pr = [p.clone().requires_grad_(True) for p in pyr]
+    ref = sum((k + 1) * R.index_pyramid(pr, c, radius).sum() for k, c in enumerate(cs))
+    ref.backward()
+    pg = [p.cuda().requires_grad_(True) for p in pyr]
+    out = sum((k + 1) * index_pyramid(pg, c.cuda(), radius).float().sum() for k, c in enumerate(cs))
+    out.backward(retain_graph=True)
+    torch.cuda.synchronize()
+    for a, b in zip(pg, pr):
+        assert _rel(a.grad, b.grad) < 1e-4
+    first = [a.grad.clone() for a in pg]
+    out.backward()
+    torch.cuda.synchronize()
+    for a, f in zip(pg, first):
+        assert _rel(a.grad, 2 * f) < 1e-6
+
+
+def test_conv_spec_cache_tracks_inplace_updates():
+    from jax_raft_amd.ops.autograd import conv2d_nhwc
+
+    torch.manual_seed(6)
+    x = torch.randn(1, 12, 12, 16, device="cuda")
+    k = torch.randn(3, 3, 16, 32, device="cuda", requires_grad=True)
+    b = torch.randn(32, device="cuda", requires_grad=True)
+    y0 = conv2d_nhwc(x, k, b, (1, 1), (1, 1)).float()
+    y0b = conv2d_nhwc(x, k, b, (1, 1), (1, 1)).float()
+    assert torch.equal(y0, y0b)
+    with torch.no_grad():
+        k.mul_(2.0)
+        b.mul_(2.0)
+    y1 = conv2d_nhwc(x, k, b, (1, 1), (1, 1)).float()
+    assert _rel(y1, 2 * y0) < 1e-2
+
+
 @pytest.mark.parametrize("factory", [raft_small, raft_large])
 def test_model_gradients_match_cpu(factory):
     torch.manual_seed(3)

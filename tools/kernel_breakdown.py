@@ -26,10 +26,11 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--marker", default="prep_images", help="kernel that starts a step ('' = whole trace / steps)")
     a = ap.parse_args()
     rows = sorted(_load(a.trace), key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if "prep_images" in r["Kernel_Name"]]
-    first = starts[-a.steps]
+    starts = [i for i, r in enumerate(rows) if a.marker and a.marker in r["Kernel_Name"]]
+    first = starts[-a.steps] if len(starts) >= a.steps else 0
     rows = rows[first:]
     agg = collections.defaultdict(lambda: [0, 0.0])
     for r in rows:
