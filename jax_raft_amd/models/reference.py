@@ -147,8 +147,12 @@ def upsample_flow(flow: torch.Tensor, up_mask: Optional[torch.Tensor] = None, fa
     neigh = torch.stack(neigh, dim=2)  # (B, C, 9, h, w)
     neigh = neigh.permute(0, 3, 4, 1, 2)  # (B, h, w, C, 9)
     # out[n,y,x,c,a,b] = sum_k m[n,y,x,k,a,b] * neigh[n,y,x,c,k]
-    up = torch.einsum("nyxkab,nyxck->nyxcab", m, neigh)
-    up = up.permute(0, 1, 4, 2, 5, 3).reshape(B, nh, nw, C)
+    # as broadcast multiply + reduction: the einsum lowers to B*h*w tiny
+    # (C x 9) @ (9 x 64) batched GEMMs, which the GPU library runs ~5x slower
+    # than this memory-bound form (training profile, profiles/r1_train_kernel_breakdown_v1.txt)
+    mm = m.reshape(B, h, w, 1, 9, factor * factor)
+    up = (neigh.unsqueeze(-1) * mm).sum(dim=4)  # (B, h, w, C, 64)
+    up = up.reshape(B, h, w, C, factor, factor).permute(0, 1, 4, 2, 5, 3).reshape(B, nh, nw, C)
     return up
 
 

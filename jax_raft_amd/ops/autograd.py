@@ -117,7 +117,7 @@ class Conv2dNHWC(torch.autograd.Function):
             gw = gw[:, : kh * kw * cin8].reshape(cout, kh, kw, cin8)[..., :cin]
             gk = gw.permute(1, 2, 3, 0).contiguous()
         if ctx.bias_requires_grad:
-            gb = gy.float().sum(dim=(0, 1, 2))
+            gb = gy.sum(dim=(0, 1, 2), dtype=torch.float32)
         return gx, gk, gb, None, None
 
 
