@@ -75,6 +75,29 @@ def _cached_spec(kernel: torch.Tensor, bias, stride, padding, cin8: int, transpo
     return spec
 
 
+def _wgrad_gemm(gy2: torch.Tensor, col: torch.Tensor, cout: int) -> torch.Tensor:
+    """dW = dY^T @ im2col(X): a long-K GEMM (K = batch pixels) with a small
+    (cout x kh*kw*cin) output, i.e. only a handful of output tiles for 256 CUs
+    (the encoder's 64 x 576 weight grads ran as 9 library tiles, ~550 us each).
+    Split K into S batches so there are ~2 tiles per CU, bf16 MFMA with fp32
+    partials, then reduce the partials in fp32."""
+    M, cout8 = gy2.shape
+    kpad = col.shape[1]
+    tiles = -(-cout // 64) * -(-kpad // 64)
+    S = 1
+    while S < 64 and tiles * S * 2 <= 2 * nat.NUM_CUS and M % (2 * S) == 0 and M // (2 * S) >= 1024:
+        S *= 2
+    if S == 1 or not gy2.is_cuda:
+        return torch.matmul(gy2.t()[:cout], col).float()
+    a = gy2.reshape(S, M // S, cout8).transpose(1, 2)[:, :cout]
+    b = col.reshape(S, M // S, kpad)
+    try:
+        part = torch.bmm(a, b, out_dtype=torch.float32)
+    except (RuntimeError, TypeError):
+        part = torch.bmm(a, b).float()
+    return part.sum(0)
+
+
 class Conv2dNHWC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, kernel, bias, stride: Tuple[int, int], padding: Tuple[int, int]):
@@ -113,7 +136,7 @@ class Conv2dNHWC(torch.autograd.Function):
             M = N * OH * OW
             col = torch.empty(M, kpad, dtype=BF16, device=gy.device)
             nat.ops().im2col([xb, col], [N, H, W, 0, cin8, kh, kw, sh, sw, ph, pw])
-            gw = torch.matmul(gyb.reshape(M, cout8).t()[:cout], col).float()  # (cout, kpad)
+            gw = _wgrad_gemm(gyb.reshape(M, cout8), col, cout)  # (cout, kpad) fp32
             gw = gw[:, : kh * kw * cin8].reshape(cout, kh, kw, cin8)[..., :cin]
             gk = gw.permute(1, 2, 3, 0).contiguous()
         if ctx.bias_requires_grad:

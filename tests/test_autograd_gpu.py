@@ -182,3 +182,16 @@ def test_model_gradients_match_cpu(factory):
     cos = torch.tensor(cos)
     assert cos.median() > 0.97, cos
     assert cos.min() > 0.7, cos
+
+
+@pytest.mark.parametrize("M,cout,kpad", [(65536, 64, 576), (18432, 128, 1152), (3000, 32, 64)])
+def test_wgrad_split_k(M, cout, kpad):
+    from jax_raft_amd.ops.autograd import _wgrad_gemm
+
+    torch.manual_seed(7)
+    gy = torch.randn(M, cout, device="cuda").to(torch.bfloat16)
+    col = torch.randn(M, kpad, device="cuda").to(torch.bfloat16)
+    got = _wgrad_gemm(gy, col, cout)
+    ref = gy.float().t() @ col.float()
+    assert got.dtype == torch.float32 and got.shape == (cout, kpad)
+    assert _rel(got, ref) < 1e-2
