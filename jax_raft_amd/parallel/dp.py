@@ -46,7 +46,14 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> Tup
     WORLD_SIZE) return ``(0, 1, device)`` without creating a group."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    backend = backend or os.environ.get("JR_DIST_BACKEND") or None
+    # JR_SHARE_GPU=1: ranks share the visible GPUs round-robin over gloo (a
+    # rehearsal of >1 rank on a 1-GPU box; RCCL refuses two ranks per GPU)
+    share = os.environ.get("JR_SHARE_GPU") == "1" and torch.cuda.is_available()
+    use_gpu = torch.cuda.is_available() and (backend != "gloo" or share)
+    if share:
+        backend = "gloo"
+        local = local % torch.cuda.device_count()
     device = torch.device("cuda", local) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(device)
