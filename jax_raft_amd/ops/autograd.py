@@ -76,10 +76,11 @@ def _cached_spec(kernel: torch.Tensor, bias, stride, padding, cin8: int, transpo
 
 
 def _wgrad_gemm(gy2: torch.Tensor, col: torch.Tensor, cout: int) -> torch.Tensor:
-    """dW = dY^T @ im2col(X): a long-K GEMM (K = batch pixels) with a small
-    (cout x kh*kw*cin) output, i.e. only a handful of output tiles for 256 CUs
-    (the encoder's 64 x 576 weight grads ran as 9 library tiles, ~550 us each).
-    Split K into S batches so there are ~2 tiles per CU, bf16 MFMA with fp32
+    """dW = im2col(X)^T @ dY as (kpad, cout) fp32, i.e. already the HWIO
+    kernel layout (no transpose copy).  A long-K GEMM (K = batch pixels) with
+    a small output, i.e. only a handful of output tiles for 256 CUs (the
+    encoder's 576 x 64 weight grads ran as 9 library tiles, ~550 us each):
+    split K into S batches so there are ~2 tiles per CU, bf16 MFMA with fp32
     partials, then reduce the partials in fp32."""
     M, cout8 = gy2.shape
     kpad = col.shape[1]
@@ -88,9 +89,9 @@ def _wgrad_gemm(gy2: torch.Tensor, col: torch.Tensor, cout: int) -> torch.Tensor
     while S < 64 and tiles * S * 2 <= 2 * nat.NUM_CUS and M % (2 * S) == 0 and M // (2 * S) >= 1024:
         S *= 2
     if S == 1 or not gy2.is_cuda:
-        return torch.matmul(gy2.t()[:cout], col).float()
-    a = gy2.reshape(S, M // S, cout8).transpose(1, 2)[:, :cout]
-    b = col.reshape(S, M // S, kpad)
+        return torch.matmul(col.t(), gy2[:, :cout]).float()
+    a = col.reshape(S, M // S, kpad).transpose(1, 2)
+    b = gy2.reshape(S, M // S, cout8)[:, :, :cout]
     try:
         part = torch.bmm(a, b, out_dtype=torch.float32)
     except (RuntimeError, TypeError):
@@ -136,9 +137,10 @@ class Conv2dNHWC(torch.autograd.Function):
             M = N * OH * OW
             col = torch.empty(M, kpad, dtype=BF16, device=gy.device)
             nat.ops().im2col([xb, col], [N, H, W, 0, cin8, kh, kw, sh, sw, ph, pw])
-            gw = _wgrad_gemm(gyb.reshape(M, cout8), col, cout)  # (cout, kpad) fp32
-            gw = gw[:, : kh * kw * cin8].reshape(cout, kh, kw, cin8)[..., :cin]
-            gk = gw.permute(1, 2, 3, 0).contiguous()
+            gw = _wgrad_gemm(gyb.reshape(M, cout8), col, cout)  # (kpad, cout) fp32
+            gk = gw[: kh * kw * cin8].reshape(kh, kw, cin8, cout)
+            if cin8 != cin:
+                gk = gk[:, :, :cin].contiguous()
         if ctx.bias_requires_grad:
             gb = gy.sum(dim=(0, 1, 2), dtype=torch.float32)
         return gx, gk, gb, None, None

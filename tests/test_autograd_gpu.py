@@ -192,6 +192,6 @@ def test_wgrad_split_k(M, cout, kpad):
     gy = torch.randn(M, cout, device="cuda").to(torch.bfloat16)
     col = torch.randn(M, kpad, device="cuda").to(torch.bfloat16)
     got = _wgrad_gemm(gy, col, cout)
-    ref = gy.float().t() @ col.float()
-    assert got.dtype == torch.float32 and got.shape == (cout, kpad)
+    ref = col.float().t() @ gy.float()
+    assert got.dtype == torch.float32 and got.shape == (kpad, cout)
     assert _rel(got, ref) < 1e-2
