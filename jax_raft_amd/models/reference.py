@@ -178,11 +178,36 @@ def instance_norm_nhwc(x: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
     """Flax ``nn.InstanceNorm(epsilon=1e-5, use_bias=False, use_scale=False)``
     (``model.py:706-707``): per (n, c) over H, W, biased variance.  Statistics
     in fp32 whatever the input dtype."""
-    xf = x.float()
-    mean = xf.mean(dim=(1, 2), keepdim=True)
-    var = (xf * xf).mean(dim=(1, 2), keepdim=True) - mean * mean
-    var = var.clamp_min(0.0)
+    if torch.is_grad_enabled() and x.requires_grad:
+        return _InstanceNormNHWC.apply(x, eps)
+    xf = x.to(torch.promote_types(x.dtype, torch.float32))
+    var, mean = torch.var_mean(xf, dim=(1, 2), unbiased=False, keepdim=True)
     return ((xf - mean) * torch.rsqrt(var + eps)).to(x.dtype)
+
+
+class _InstanceNormNHWC(torch.autograd.Function):
+    """Instance norm with a closed-form backward: saves only the input and the
+    per-(n, c) statistics (no fp32 copies of the activation), and computes
+    dx = rstd * (g - mean(g) - xhat * mean(g * xhat)) in one expression chain
+    instead of autograd's trace through the mean / square / rsqrt graph."""
+
+    @staticmethod
+    def forward(ctx, x, eps: float):
+        xf = x.to(torch.promote_types(x.dtype, torch.float32))
+        var, mean = torch.var_mean(xf, dim=(1, 2), unbiased=False, keepdim=True)
+        rstd = torch.rsqrt(var + eps)
+        ctx.save_for_backward(x, mean, rstd)
+        return ((xf - mean) * rstd).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, mean, rstd = ctx.saved_tensors
+        ft = torch.promote_types(x.dtype, torch.float32)
+        g = gy.to(ft)
+        xhat = (x.to(ft) - mean) * rstd
+        gm = g.mean(dim=(1, 2), keepdim=True)
+        gxm = (g * xhat).mean(dim=(1, 2), keepdim=True)
+        return (rstd * (g - gm - xhat * gxm)).to(x.dtype), None
 
 
 def batch_norm_nhwc(

@@ -118,3 +118,24 @@ def test_conv2d_nhwc_matches_conv2d():
     ours = R.conv2d_nhwc(x, k, b, (1, 1), (0, 2))
     theirs = F.conv2d(x.permute(0, 3, 1, 2), k.permute(3, 2, 0, 1), b, padding=(0, 2)).permute(0, 2, 3, 1)
     assert torch.allclose(ours, theirs, atol=1e-5)
+
+
+def test_instance_norm_closed_form_backward():
+    """The instance norm's custom backward matches finite differences (float64)
+    and autograd through the plain E[x^2]-E[x]^2 formula."""
+    import torch
+
+    from jax_raft_amd.models import reference as R
+
+    torch.manual_seed(0)
+    x = torch.randn(2, 5, 6, 3, dtype=torch.float64, requires_grad=True)
+    assert torch.autograd.gradcheck(lambda t: R.instance_norm_nhwc(t), (x,))
+    x2 = torch.randn(2, 9, 7, 4, requires_grad=True)
+    g = torch.randn(2, 9, 7, 4)
+    (R.instance_norm_nhwc(x2) * g).sum().backward()
+    ga = x2.grad.clone()
+    x2.grad = None
+    m = x2.mean(dim=(1, 2), keepdim=True)
+    v = (x2 * x2).mean(dim=(1, 2), keepdim=True) - m * m
+    ((x2 - m) * torch.rsqrt(v + 1e-5) * g).sum().backward()
+    assert (ga - x2.grad).abs().max() < 1e-5
