@@ -17,6 +17,7 @@ is PyTorch glue on the framework layer.  ``coords`` never receive a gradient
 from __future__ import annotations
 
 import math
+import os
 import weakref
 from typing import List, Sequence, Tuple
 
@@ -75,6 +76,9 @@ def _cached_spec(kernel: torch.Tensor, bias, stride, padding, cin8: int, transpo
     return spec
 
 
+_WGRAD_TILES_PER_CU = int(os.environ.get("JR_WGRAD_TILES_PER_CU", "2"))
+
+
 def _wgrad_gemm(gy2: torch.Tensor, col: torch.Tensor, cout: int) -> torch.Tensor:
     """dW = im2col(X)^T @ dY as (kpad, cout) fp32, i.e. already the HWIO
     kernel layout (no transpose copy).  A long-K GEMM (K = batch pixels) with
@@ -86,7 +90,7 @@ def _wgrad_gemm(gy2: torch.Tensor, col: torch.Tensor, cout: int) -> torch.Tensor
     kpad = col.shape[1]
     tiles = -(-cout // 64) * -(-kpad // 64)
     S = 1
-    while S < 64 and tiles * S * 2 <= 2 * nat.NUM_CUS and M % (2 * S) == 0 and M // (2 * S) >= 1024:
+    while S < 64 and tiles * S * 2 <= _WGRAD_TILES_PER_CU * nat.NUM_CUS and M % (2 * S) == 0 and M // (2 * S) >= 1024:
         S *= 2
     if S == 1 or not gy2.is_cuda:
         return torch.matmul(col.t(), gy2[:, :cout]).float()
