@@ -30,6 +30,23 @@ BASELINE_FPS = 11.8  # README.md:9 of the reference (RTX 3090 Ti, raft_large, 32
 METRIC = "image-pairs/sec + Sintel-clean EPE, raft_large 32 iters at 1/2/4/8 MI355X"
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _relaunch(n: int) -> int:
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    print("bench.py: --gpus {} without a launcher, running: {}".format(n, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -64,6 +81,12 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse >1 rank on fewer GPUs")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `bench.py --gpus N` without a launcher: start torch.distributed.run as a
+        # child (nothing has touched the GPU yet) and exit with its return code,
+        # rather than silently benchmarking one GPU.
+        sys.exit(_relaunch(args.gpus))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -99,13 +99,25 @@ class RAFT(nn.Module):
         With ``mutable=['batch_stats']`` (and ``train=True``) returns
         ``(flows, {'batch_stats': updated})`` like Flax."""
         own = self.variables()
-        same = _same_leaves(own, variables)
-        if not same:
-            # load foreign variables (numpy / torch leaves) into this module's tensors
-            ckpt.load_variables_into(self, variables, strict=False)
-        out = self(image1, image2, train=train, num_flow_updates=num_flow_updates, **kw)
+        if _same_leaves(own, variables):
+            out = self(image1, image2, train=train, num_flow_updates=num_flow_updates, **kw)
+            if mutable:
+                return out, {"batch_stats": ckpt.variables_from_module(self)["batch_stats"]}
+            return out
+        # Foreign variables (numpy / torch leaves): validated like Flax's apply
+        # (every param present, no unexpected leaf, shapes equal; an absent
+        # 'batch_stats' collection keeps the module's own statistics) and bound
+        # functionally for this call only -- the module's tensors are untouched.
+        # Leaves are copied, so a train-mode BatchNorm update never writes into
+        # the caller's arrays; it is returned through ``mutable`` like Flax.
+        bound = ckpt.variables_as_tensors(self, variables)
+        out = torch.func.functional_call(
+            self, bound, (image1, image2), dict(train=train, num_flow_updates=num_flow_updates, **kw))
         if mutable:
-            return out, {"batch_stats": ckpt.variables_from_module(self)["batch_stats"]}
+            stats = {k: v for k, v in bound.items() if k.endswith(".mean") or k.endswith(".var")}
+            if not stats:
+                stats = {k: v for k, v in ckpt.flatten_tree(own["batch_stats"]).items()}
+            return out, {"batch_stats": ckpt.unflatten_tree(stats)}
         return out
 
     # ------------------------------------------------------- golden execution

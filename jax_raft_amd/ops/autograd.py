@@ -76,7 +76,26 @@ def _cached_spec(kernel: torch.Tensor, bias, stride, padding, cin8: int, transpo
     return spec
 
 
-_WGRAD_TILES_PER_CU = int(os.environ.get("JR_WGRAD_TILES_PER_CU", "2"))
+def _env_pos_int(name: str, default: int) -> int:
+    raw = os.environ.get(name, str(default))
+    try:
+        v = int(raw)
+    except ValueError:
+        raise ValueError(f"{name} must be a positive integer, got {raw!r}") from None
+    if v < 1:
+        raise ValueError(f"{name} must be >= 1, got {v}")
+    return v
+
+
+_WGRAD_TILES_PER_CU = _env_pos_int("JR_WGRAD_TILES_PER_CU", 2)
+
+
+def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a @ b (bf16 operands) with the product kept in fp32 (no bf16 rounding of dW)."""
+    try:
+        return torch.mm(a, b, out_dtype=torch.float32)
+    except (RuntimeError, TypeError):
+        return torch.mm(a.float(), b.float())
 
 
 def _wgrad_gemm(gy2: torch.Tensor, col: torch.Tensor, cout: int) -> torch.Tensor:
@@ -93,7 +112,7 @@ def _wgrad_gemm(gy2: torch.Tensor, col: torch.Tensor, cout: int) -> torch.Tensor
     while S < 64 and tiles * S * 2 <= _WGRAD_TILES_PER_CU * nat.NUM_CUS and M % (2 * S) == 0 and M // (2 * S) >= 1024:
         S *= 2
     if S == 1 or not gy2.is_cuda:
-        return torch.matmul(col.t(), gy2[:, :cout]).float()
+        return _mm_f32(col.t(), gy2[:, :cout])
     a = col.reshape(S, M // S, kpad).transpose(1, 2)
     b = gy2.reshape(S, M // S, cout8)[:, :, :cout]
     try:
@@ -186,6 +205,11 @@ class CorrPyramid(torch.autograd.Function):
                 levels[l].copy_(p[:, : 2 * hh, : 2 * ww].reshape(M, hh, 2, ww, 2).mean(dim=(2, 4)))
         ctx.save_for_backward(f1, f2)
         ctx.shape = (B, hq, wq, h, w, C, num_levels)
+        # lookups of these levels accumulate their gradient into one shared buffer
+        # (see _LookupGradAcc) and hand it over here instead of through autograd
+        ctx.acc = _LookupGradAcc()
+        levels[0]._jr_lookup_acc = ctx.acc
+        ctx.set_materialize_grads(False)
         return tuple(levels)
 
     @staticmethod
@@ -193,6 +217,9 @@ class CorrPyramid(torch.autograd.Function):
         f1, f2 = ctx.saved_tensors
         B, hq, wq, h, w, C, L = ctx.shape
         nq = hq * wq
+        shared = ctx.acc.take()
+        if shared is not None:
+            glevels = tuple(s if g is None else s + g for s, g in zip(shared, glevels))
         dC = torch.zeros(B * nq, h, w, device=f1.device, dtype=torch.float32)
         for l, g in enumerate(glevels):
             if g is None:
@@ -218,23 +245,36 @@ class _LookupGradAcc:
     gradients would cost a full zero-filled fp32 pyramid per iteration plus
     an autograd add of it (hundreds of MB each at training resolution).  The
     backward kernel accumulates (read-modify-write) instead: every lookup's
-    backward adds into this one buffer and returns no level gradient, except
-    the last one to run, which hands the finished sum to the pyramid's
-    backward.  ``n`` counts the graph's lookups; the countdown re-arms after
-    completion so ``retain_graph`` backward passes also work."""
+    backward adds into this one buffer and returns no level gradient; the
+    pyramid's own backward (:class:`CorrPyramid`) takes the sum.
+
+    The buffer is tagged with the autograd graph task (one ``backward`` /
+    ``autograd.grad`` call) that filled it, so a sum left behind by a pass in
+    which the pyramid's backward did not run (gradients requested w.r.t. the
+    levels themselves, or a pass that never reached the pyramid) is discarded
+    instead of leaking into a later pass."""
 
     def __init__(self):
-        self.n = 0
-        self.left = 0
         self.bufs = None
+        self.task = None
+
+    def buffers(self, shapes, device) -> List[torch.Tensor]:
+        task = torch._C._current_graph_task_id()
+        if self.bufs is None or self.task != task:
+            self.bufs = [torch.zeros(s, device=device, dtype=torch.float32) for s in shapes]
+            self.task = task
+        return self.bufs
+
+    def take(self):
+        bufs = self.bufs if self.task == torch._C._current_graph_task_id() else None
+        self.bufs, self.task = None, None
+        return bufs
 
 
-def _lookup_acc(levels) -> _LookupGradAcc:
-    acc = getattr(levels[0], "_jr_lookup_acc", None)
-    if acc is None:
-        acc = _LookupGradAcc()
-        levels[0]._jr_lookup_acc = acc
-    return acc
+def _lookup_acc(levels):
+    """The shared accumulator of a pyramid built by :class:`CorrPyramid` (None
+    for levels from elsewhere, whose lookups return their own gradients)."""
+    return getattr(levels[0], "_jr_lookup_acc", None)
 
 
 class PyramidLookup(torch.autograd.Function):
@@ -255,11 +295,7 @@ class PyramidLookup(torch.autograd.Function):
         nat.ops().lookup([c, out] + lv + [None] * (4 - L), [L, B, h, w, radius, nq])
         ctx.save_for_backward(c)
         ctx.meta = (B, h, w, nq, radius, L, [tuple(l.shape) for l in levels])
-        ctx.acc = None
-        if torch.is_grad_enabled() and any(l.requires_grad for l in levels):
-            ctx.acc = _lookup_acc(levels)
-            ctx.acc.n += 1
-            ctx.acc.left += 1
+        ctx.acc = _lookup_acc(levels)
         return out.reshape(B, hq, wq, ocs)[..., : L * S * S]
 
     @staticmethod
@@ -273,14 +309,8 @@ class PyramidLookup(torch.autograd.Function):
             dls = [torch.zeros(s, device=g.device, dtype=torch.float32) for s in shapes]
             nat.ops().lookup_bwd([c, g] + dls + [None] * (4 - L), [L, B, h, w, radius, nq])
             return (None, None) + tuple(dls)
-        if acc.bufs is None:
-            acc.bufs = [torch.zeros(s, device=g.device, dtype=torch.float32) for s in shapes]
-        nat.ops().lookup_bwd([c, g] + acc.bufs + [None] * (4 - L), [L, B, h, w, radius, nq])
-        acc.left -= 1
-        if acc.left > 0:
-            return (None, None) + (None,) * L
-        dls, acc.bufs, acc.left = acc.bufs, None, acc.n
-        return (None, None) + tuple(dls)
+        nat.ops().lookup_bwd([c, g] + acc.buffers(shapes, g.device) + [None] * (4 - L), [L, B, h, w, radius, nq])
+        return (None, None) + (None,) * L
 
 
 def index_pyramid(pyramid: Sequence[torch.Tensor], coords, radius: int):

@@ -72,7 +72,9 @@ def _ext_hook(code: int, data: bytes):
 def _unchunk(tree):
     if isinstance(tree, dict):
         if tree.get(_CHUNK_KEY):
-            shape = tuple(tree["shape"])
+            # Flax stores the shape and the chunk list via _tuple_to_dict: {'0': .., '1': ..}
+            shp = tree["shape"]
+            shape = tuple(int(shp[str(i)]) for i in range(len(shp))) if isinstance(shp, Mapping) else tuple(shp)
             chunks = tree["chunks"]
             flat = np.concatenate([chunks[str(i)].reshape(-1) for i in range(len(chunks))])
             return flat.reshape(shape)
@@ -108,7 +110,7 @@ def _chunk(tree):
         flat = tree.reshape(-1)
         per = max(1, _MAX_CHUNK // tree.itemsize)
         chunks = {str(i): flat[j:j + per] for i, j in enumerate(range(0, flat.size, per))}
-        return {_CHUNK_KEY: True, "shape": list(tree.shape), "chunks": chunks}
+        return {_CHUNK_KEY: True, "shape": {str(i): int(d) for i, d in enumerate(tree.shape)}, "chunks": chunks}
     return tree
 
 
@@ -182,6 +184,43 @@ def load_variables_into(model: torch.nn.Module, variables: Mapping[str, Any], st
             if tuple(v.shape) != tuple(t.shape):
                 raise ValueError(f"shape mismatch for {k}: checkpoint {tuple(v.shape)} vs model {tuple(t.shape)}")
             t.copy_(v.to(t.dtype))
+
+
+def variables_as_tensors(model: torch.nn.Module, variables: Mapping[str, Any]) -> Dict[str, torch.Tensor]:
+    """Validate a foreign variable tree against ``model`` and return its leaves
+    as fresh tensors (the module's device and dtypes), keyed by the module's
+    parameter / buffer names, for ``torch.func.functional_call``.
+
+    Strict like Flax's ``apply``: a missing or unexpected ``params`` leaf or a
+    shape mismatch raises.  The ``batch_stats`` collection may be absent as a
+    whole (the module's own statistics are used); when it is given it must be
+    complete."""
+    if not isinstance(variables, Mapping) or "params" not in variables:
+        raise KeyError("variables must be a mapping with a 'params' collection")
+    params = {k: v for k, v in model.named_parameters()}
+    stats = {k: v for k, v in model.named_buffers() if k.endswith(".mean") or k.endswith(".var")}
+    out: Dict[str, torch.Tensor] = {}
+    for coll, target in (("params", params), ("batch_stats", stats)):
+        given = variables.get(coll)
+        if coll == "batch_stats" and not given:
+            continue
+        src = flatten_tree(given or {})
+        missing = sorted(set(target) - set(src))
+        extra = sorted(set(src) - set(target))
+        if missing or extra:
+            raise KeyError(f"variable tree mismatch in '{coll}': missing={missing[:8]}"
+                           f"{'...' if len(missing) > 8 else ''} unexpected={extra[:8]}"
+                           f"{'...' if len(extra) > 8 else ''}")
+        for k, t in target.items():
+            v = src[k]
+            v = v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))
+            if tuple(v.shape) != tuple(t.shape):
+                raise ValueError(f"shape mismatch for {coll}/{k}: given {tuple(v.shape)} vs model {tuple(t.shape)}")
+            if v.requires_grad and v.device == t.device and v.dtype == t.dtype:
+                out[k] = v   # differentiable w.r.t. the given leaf (jax.grad over variables)
+            else:
+                out[k] = v.detach().to(device=t.device, dtype=t.dtype, copy=True)
+    return out
 
 
 def save_msgpack(model_or_vars, path: str) -> None:

@@ -134,3 +134,21 @@ def test_torchvision_conversion_roundtrip(tmp_path):
         assert set(a) == set(b)
         for k in a:
             assert torch.equal(a[k], b[k]), k
+
+
+def test_chunked_array_flax_encoding(monkeypatch):
+    """Arrays above the chunk limit use Flax's {'0': .., '1': ..} encoding for
+    both 'shape' and 'chunks' (flax.serialization._tuple_to_dict)."""
+    monkeypatch.setattr(C, "_MAX_CHUNK", 64)
+    big = np.arange(3 * 7 * 5, dtype=np.float32).reshape(3, 7, 5)
+    raw = C.msgpack_serialize({"params": {"w": big, "b": np.ones(2, np.float32)}})
+    tree = msgpack.unpackb(raw, ext_hook=C._ext_hook, raw=False, strict_map_key=False)
+    enc = tree["params"]["w"]
+    assert enc[C._CHUNK_KEY] is True
+    assert enc["shape"] == {"0": 3, "1": 7, "2": 5}
+    assert set(enc["chunks"]) == {str(i) for i in range(len(enc["chunks"]))} and len(enc["chunks"]) > 1
+    back = C.msgpack_restore(raw)
+    assert np.array_equal(back["params"]["w"], big)
+    # a file written by Flax itself (shape dict) and a legacy list shape both decode
+    legacy = dict(enc, shape=[3, 7, 5])
+    assert np.array_equal(C._unchunk(legacy), big)

@@ -97,3 +97,59 @@ def test_final_only_output_cpu():
     last = model.apply(variables, i1, i2, num_flow_updates=3, return_all_iters=False)
     assert last.shape == (1, 1, 128, 128, 2)
     assert torch.allclose(last[0], full[-1])
+
+
+def test_apply_rejects_mismatched_variable_tree():
+    model, v = raft_small(seed=0)
+    i1, i2 = _pair()
+    flat = {k: t.detach().clone() for k, t in C.flatten_tree(v["params"]).items()}
+    renamed = dict(flat)
+    k0 = "update_block.flow_head.conv2.bias"
+    renamed["update_block.flow_head.conv2.bias_typo"] = renamed.pop(k0)
+    with pytest.raises(KeyError):
+        model.apply({"params": C.unflatten_tree(renamed)}, i1, i2, num_flow_updates=1)
+    missing = dict(flat)
+    missing.pop(k0)
+    with pytest.raises(KeyError):
+        model.apply({"params": C.unflatten_tree(missing)}, i1, i2, num_flow_updates=1)
+    with pytest.raises(KeyError):
+        model.apply({"params": {"typo_encoder": flat[k0]}}, i1, i2, num_flow_updates=1)
+    bad = dict(flat)
+    bad[k0] = torch.zeros(3)
+    with pytest.raises(ValueError):
+        model.apply({"params": C.unflatten_tree(bad)}, i1, i2, num_flow_updates=1)
+
+
+def test_apply_foreign_variables_leave_module_untouched():
+    model, v = raft_small(seed=0)
+    _, ov = raft_small(seed=3)
+    before = {k: t.detach().clone() for k, t in C.flatten_tree(v["params"]).items()}
+    i1, i2 = _pair()
+    foreign = {"params": C.unflatten_tree({k: t.detach().numpy().copy()
+                                           for k, t in C.flatten_tree(ov["params"]).items()})}
+    out_f = model.apply(foreign, i1, i2, num_flow_updates=2)
+    for k, t in C.flatten_tree(model.variables()["params"]).items():
+        assert torch.equal(t, before[k]), k
+    out_own = model.apply(v, i1, i2, num_flow_updates=2)
+    assert not torch.allclose(out_f, out_own)
+
+
+def test_apply_foreign_batch_stats_returned_not_written():
+    model, v = raft_large(seed=0)
+    model.train()
+    i1, i2 = _pair(2)
+    foreign = {c: C.unflatten_tree({k: t.detach().numpy().copy() for k, t in C.flatten_tree(v[c]).items()})
+               for c in ("params", "batch_stats")}
+    key = ("context_encoder", "convnormrelu", "layers_1", "mean")
+    arr = foreign["batch_stats"]
+    for p in key:
+        arr = arr[p]
+    snapshot = arr.copy()
+    own_before = model.context_encoder.convnormrelu.layers_1.mean.detach().clone()
+    _, new = model.apply(foreign, i1, i2, train=True, num_flow_updates=1, mutable=["batch_stats"])
+    upd = new["batch_stats"]
+    for p in key:
+        upd = upd[p]
+    assert np.array_equal(arr, snapshot)            # caller's arrays not written
+    assert torch.equal(model.context_encoder.convnormrelu.layers_1.mean, own_before)
+    assert not torch.allclose(upd.cpu(), torch.as_tensor(snapshot))
