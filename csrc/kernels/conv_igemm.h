@@ -84,6 +84,93 @@ JR_DEVICE void load_f32(const float* src, float* v) {
   }
 }
 
+// EPI_BWD epilogue (training backward, see BwdSeg in kernels.h): v[NV] holds the
+// data gradient of NV contiguous input channels [cbase, cbase + NV) of pixel m.
+// Modes 1 / 2 need whole groups inside [0, hidden) (hidden % 16 == 0, checked
+// on the host); mode 0 handles a partial last group (cbase + NV > cout).
+template <int NV>
+JR_DEVICE void epi_bwd(const ConvParams& p, float (&v)[NV], int m, int cbase) {
+  const int s = cbase < p.hidden ? 0 : 1;
+  const BwdSeg& g = p.seg[s];
+  const int lc = cbase - (s ? p.hidden : 0);
+  const int n = min(NV, p.cout - cbase);  // valid channels of this group
+  const bool full = n == NV;
+  if (g.gin) {
+    const float* gp = g.gin + (long)m * g.gin_cs + g.gin_coff + lc;
+    if (full) {
+      float gi[NV];
+      load_f32<NV>(gp, gi);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v[j] += gi[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) if (j < n) v[j] += gp[j];
+    }
+  }
+  if (g.mode == 0) {
+    if (g.mask) {
+      const bf16* mp = (const bf16*)g.mask + (long)m * g.mask_cs + g.mask_coff + lc;
+      float mv[NV];
+      if (full) load_bf16<NV>(mp, mv);
+      else {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) mv[j] = j < n ? bf2f(mp[j]) : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v[j] = mv[j] > 0.f ? v[j] : 0.f;
+    }
+    if (g.valid > 0) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) if (lc + j >= g.valid) v[j] = 0.f;
+    }
+    if (g.out_f32) {
+      float* op = (float*)g.out + (long)m * g.out_cs + g.out_coff + lc;
+      if (full) store_f32<NV>(op, v);
+      else {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) if (j < n) op[j] = v[j];
+      }
+    } else {
+      bf16* op = (bf16*)g.out + (long)m * g.out_cs + g.out_coff + lc;
+      if (full) store_bf16<NV>(op, v);
+      else {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) if (j < n) op[j] = f2bf(v[j]);
+      }
+    }
+    return;
+  }
+  const int hd = p.hidden;
+  float hp[NV];
+  load_f32<NV>(p.ghp + (long)m * hd + lc, hp);
+  float* dh = (float*)g.out + (long)m * g.out_cs + g.out_coff + lc;
+  if (g.mode == 1) {
+    float z[NV], q[NV], a[NV], b[NV];
+    load_bf16<NV>((const bf16*)p.gz + (long)m * hd + lc, z);
+    load_bf16<NV>((const bf16*)p.gq + (long)m * hd + lc, q);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      a[j] = v[j] * z[j] * (1.f - q[j] * q[j]);                  // dL/d(q pre-activation)
+      b[j] = v[j] * (q[j] - hp[j]) * z[j] * (1.f - z[j]);        // dL/d(z pre-activation)
+      v[j] *= 1.f - z[j];                                        // dL/dh (blend path)
+    }
+    store_bf16<NV>((bf16*)p.gdq + (long)m * hd + lc, a);
+    store_bf16<NV>((bf16*)p.gdzr + (long)m * 2 * hd + lc, b);
+    store_f32<NV>(dh, v);
+  } else {
+    float r[NV], d[NV], a[NV];
+    load_bf16<NV>((const bf16*)p.gr + (long)m * hd + lc, r);
+    load_f32<NV>(dh, d);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      a[j] = v[j] * hp[j] * r[j] * (1.f - r[j]);                 // dL/d(r pre-activation)
+      d[j] += v[j] * r[j];                                       // dL/dh (reset path)
+    }
+    store_bf16<NV>((bf16*)p.gdzr + (long)m * 2 * hd + hd + lc, a);
+    store_f32<NV>(dh, d);
+  }
+}
+
 // Output channel base of a lane: storage rows are permuted in 64-row groups so
 // that D row (4*lq + r) of 16-row MFMA tile t maps to channel G + lq*16 + t*4 + r.
 template <int TM>
@@ -223,6 +310,7 @@ JR_DEVICE void epi_pixel(const ConvParams& p, float (&v)[NV], int m, int cbase) 
       else store_f32<NV>((float*)p.zbuf + (long)m * hd + cbase, v);
     } else {
       const int hc = cbase - hd;
+      if (p.rbuf) store_bf16<NV>((bf16*)p.rbuf + (long)m * hd + hc, v);  // training: r for the backward
       float h[NV];
       if (p.h32) load_f32<NV>(p.h32 + (long)m * hd + hc, h);
       else load_bf16<NV>((const bf16*)p.x + (long)m * p.x_cstride + p.x_coff + hc, h);
@@ -237,11 +325,15 @@ JR_DEVICE void epi_pixel(const ConvParams& p, float (&v)[NV], int m, int cbase) 
     else load_f32<NV>((const float*)p.zbuf + (long)m * hd + cbase, z);
     float* hp = p.h32 + (long)m * hd + cbase;
     load_f32<NV>(hp, h);
+    float qv[NV];
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
       const float q = tanhf_(v[j]);
+      qv[j] = q;
       v[j] = (1.0f - z[j]) * h[j] + z[j] * q;
     }
+    if (p.qbuf) store_bf16<NV>((bf16*)p.qbuf + (long)m * hd + cbase, qv);  // training: q for the backward
+    if (p.h32o) hp = p.h32o + (long)m * hd + cbase;
     store_f32<NV>(hp, v);
     store_bf16<NV>((bf16*)p.y + (long)m * p.y_cstride + p.y_coff + cbase, v);
     if (p.y2) store_bf16<NV>((bf16*)p.y2 + (long)m * p.y2_cstride + p.y2_coff + cbase, v);
@@ -269,6 +361,8 @@ JR_DEVICE void epi_pixel(const ConvParams& p, float (&v)[NV], int m, int cbase) 
         y3p[0] = f2bf(fx); y3p[1] = f2bf(fy);
       }
     }
+  } else if constexpr (EPI == EPI_BWD) {
+    epi_bwd<NV>(p, v, m, cbase);
   }
 }
 
@@ -1058,6 +1152,7 @@ int launch_cfg(const ConvParams* p, int epi, hipStream_t s) {
     case EPI_GRU_B: JR_LAUNCH(EPI_GRU_B) break;
     case EPI_FLOW: JR_LAUNCH(EPI_FLOW) break;
     case EPI_CONVEX: JR_LAUNCH(EPI_CONVEX) break;
+    case EPI_BWD: JR_LAUNCH(EPI_BWD) break;
     default: return (int)hipErrorInvalidValue;
   }
 #undef JR_LAUNCH

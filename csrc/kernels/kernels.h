@@ -20,6 +20,22 @@ enum ConvEpi : int {
   EPI_CONVEX = 4, // mask logits in subpixel-major order (channel s*16 + k, k < 9 real): *alpha -> softmax
                   // over the 9 neighbours -> convex combination of 8*flow32 at the 3x3 neighbours ->
                   // fp32 upsampled flow written straight into y = out[B][8 OH][8 OW][2]
+  EPI_BWD = 5,    // data-gradient conv of the training loop's backward (no bias): channels
+                  // [0, hidden) -> seg[0], [hidden, cout) -> seg[1] (see BwdSeg)
+};
+
+// One channel segment of the EPI_BWD epilogue.  Local channel lc = c - base.
+//   mode 0: g = acc (+ gin) ; g = 0 where mask <= 0 or lc >= valid ; out = g (bf16 | fp32)
+//   mode 1: ConvGRU blend backward (h' = (1-z) h + z q, model.py:311): g = acc (+ gin) = dL/dh'
+//           gdq[lc] = g z (1-q^2) ; gdzr[lc] = g (q-h) z (1-z) ; out (fp32) = g (1-z)   (dL/dh partial)
+//   mode 2: ConvGRU reset-gate backward (acc = dL/d(r h), model.py:308):
+//           gdzr[hidden + lc] = acc h r (1-r) ; out (fp32) += acc r
+struct BwdSeg {
+  int mode;
+  const float* gin; int gin_cs, gin_coff;
+  const void* mask; int mask_cs, mask_coff;
+  int valid;
+  void* out; int out_cs, out_coff, out_f32;
 };
 
 struct ConvParams {
@@ -70,6 +86,15 @@ struct ConvParams {
   int fast;
   // 1: XCD-aware workgroup -> tile order (conv_igemm.h:xcd_tile); 0: dispatch order
   int xcd_remap;
+  // training forward extras: GRU-A also stores r (bf16 [M][hidden]); GRU-B stores q (bf16) and
+  // writes the new fp32 state to h32o (else in place into h32)
+  void* rbuf;
+  void* qbuf;
+  float* h32o;
+  // EPI_BWD: channel segments and the ConvGRU backward operands ([M][hidden]; gdzr [M][2 hidden])
+  BwdSeg seg[2];
+  const void* gz; const void* gr; const void* gq; const float* ghp;
+  void* gdq; void* gdzr;
 };
 
 // cfg (co x px block tile): kernel R (register-staged, 16x16x32 MFMA) 0 = 128x128, 1 = 64x128,
@@ -120,6 +145,18 @@ int jr_corr_lookup_bwd(void* const* dlevels, int num_levels, int B, int h, int w
 int jr_upsample_convex(const void* mask, int mask_cstride, const float* flow, int B, int h, int w,
                        float* out, hipStream_t stream);
 int jr_upsample_bilinear(const float* flow, int B, int h, int w, float* out, hipStream_t stream);
+// Backward of jr_upsample_convex (training): mask bf16 [M][mask_cs] (the 576 logits, already
+// scaled by alpha), flow fp32 [M][2], gout fp32 [B][8h][8w][2] ->
+//   dmask bf16 [M][dmask_cs]: alpha * dL/dlogit (the gradient of the un-scaled mask conv output)
+//   taps fp32 [M][18]: taps[q][2k + c] = dL/d flow_c at the k-th 3x3 neighbour of q
+int jr_upsample_convex_bwd(const void* mask, int mask_cs, const float* flow, const float* gout, int B, int h, int w,
+                           float alpha, void* dmask, int dmask_cs, float* taps, hipStream_t stream);
+// Backward of jr_upsample_bilinear w.r.t. the low-res flow (deterministic gather):
+// gout fp32 [B][8h][8w][2] -> dflow bf16 [M][dcs] (channels 0, 1; 2..dcs-1 zeroed)
+int jr_upsample_bilinear_bwd(const float* gout, int B, int h, int w, void* dflow, int dcs, hipStream_t stream);
+// dflow(p) = sum_k taps[p - d_k][2k + c] over the in-map 3x3 neighbours (d_k = (k/3-1, k%3-1)),
+// written as bf16 [M][dcs] (channels 0, 1; 2..dcs-1 zeroed)
+int jr_flow_gather_bwd(const float* taps, int tcs, int N, int h, int w, void* dflow, int dcs, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
 // Misc.

@@ -69,7 +69,10 @@ static void check_f32(const at::Tensor& t, const char* name) {
 //      (, OH_override, OW_override, log2 dil_h, log2 dil_w (, bmap_coff))]
 static int64_t check_flow_out(const at::Tensor& out, int B, int h, int w);
 
-static Launch make_conv(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep) {
+static void conv_train_extras(ConvParams& p, int epi, const TList& tx, const IList& ix, std::vector<at::Tensor>* keep);
+
+static Launch make_conv(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep,
+                        const TList* tx = nullptr, const IList* ix = nullptr) {
   TORCH_CHECK(i.size() == 22 || i.size() == 26 || i.size() == 27 || i.size() == 28,
               "conv: expected 22, 26, 27 or 28 ints");
   at::Tensor x = opt(t, 0), w = opt(t, 1), bias = opt(t, 2), y = opt(t, 3), y2 = opt(t, 4), res = opt(t, 5);
@@ -178,6 +181,10 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   } else if (epi == EPI_FLOW) {
     check_f32(coords, "coords"); check_f32(flow32, "flow32"); check_bf16(y, "y");
     TORCH_CHECK(p.cout == 2, "FLOW: cout must be 2");
+  } else if (epi == EPI_BWD) {
+    TORCH_CHECK(tx != nullptr, "EPI_BWD needs the training operands (conv_train)");
+    TORCH_CHECK(!bmap.defined() && !res.defined(), "EPI_BWD: no bias map / residual");
+    TORCH_CHECK(p.hidden >= 0 && p.hidden % 16 == 0 && p.hidden <= p.cout, "EPI_BWD: split must be a multiple of 16 <= cout");
   } else if (epi == EPI_CONVEX) {
     check_f32(flow32, "flow32");
     TORCH_CHECK(flow32.numel() >= (int64_t)p.M * 2, "CONVEX: flow32 must be [M][2]");
@@ -191,6 +198,7 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
     TORCH_CHECK(false, "conv: unknown epilogue ", epi);
   }
   TORCH_CHECK(cfg >= 0 && cfg <= 34 && !(cfg >= 29 && cfg <= 32), "conv: unknown tile config ", cfg);
+  if (tx) conv_train_extras(p, epi, *tx, *ix, keep);
   if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3, bmap}) if (v.defined()) keep->push_back(v);
   if (epi == EPI_CONVEX) {
     const int64_t need = (int64_t)p.N * 64 * p.OH * p.OW * 2;
@@ -203,6 +211,135 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
     };
   }
   return [p, epi, cfg](hipStream_t s, int) { return jr_conv_forward(&p, cfg, epi, s); };
+}
+
+// Training operands of a conv (op conv_train / Plan.add_conv_train):
+// tx = [rbuf, qbuf, h32o, gz, gr, gq, ghp, gdq, gdzr,
+//       seg0.gin, seg0.mask, seg0.out, seg1.gin, seg1.mask, seg1.out]
+// ix = [seg0.mode, seg0.gin_coff, seg0.mask_coff, seg0.valid, seg0.out_coff,  (same for seg1)]
+// Channel strides are the tensors' last dims.  GRU operands are [M][hidden]
+// (gdzr [M][2 hidden]); see BwdSeg (kernels.h) for the segment semantics.
+static void conv_train_extras(ConvParams& p, int epi, const TList& tx, const IList& ix, std::vector<at::Tensor>* keep) {
+  TORCH_CHECK(tx.size() == 15 && ix.size() == 10, "conv_train: expected 15 tensors and 10 ints");
+  std::vector<at::Tensor> ts;
+  for (size_t k = 0; k < 15; ++k) ts.push_back(opt(tx, k));
+  const int64_t M = p.M;
+  auto need_bf16 = [&](const at::Tensor& v, int64_t n, const char* nm) {
+    check_bf16(v, nm);
+    TORCH_CHECK(v.numel() >= n, "conv_train: ", nm, " too small");
+  };
+  auto need_f32 = [&](const at::Tensor& v, int64_t n, const char* nm) {
+    check_f32(v, nm);
+    TORCH_CHECK(v.numel() >= n, "conv_train: ", nm, " too small");
+  };
+  const int hd = p.hidden;
+  if (ts[0].defined()) { TORCH_CHECK(epi == EPI_GRU_A, "rbuf: GRU-A only"); need_bf16(ts[0], M * hd, "rbuf"); p.rbuf = ts[0].data_ptr(); }
+  if (ts[1].defined()) { TORCH_CHECK(epi == EPI_GRU_B, "qbuf: GRU-B only"); need_bf16(ts[1], M * hd, "qbuf"); p.qbuf = ts[1].data_ptr(); }
+  if (ts[2].defined()) { TORCH_CHECK(epi == EPI_GRU_B, "h32o: GRU-B only"); need_f32(ts[2], M * hd, "h32o"); p.h32o = ts[2].data_ptr<float>(); }
+  if (epi == EPI_BWD) {
+    bool gru = false;
+    for (int s = 0; s < 2; ++s) {
+      BwdSeg& g = p.seg[s];
+      const int b = 5 * s;
+      const int lo = s ? hd : 0, hi = s ? p.cout : hd;
+      const int width = hi - lo;
+      g.mode = (int)ix[b];
+      TORCH_CHECK(g.mode >= 0 && g.mode <= 2, "conv_train: segment mode 0..2");
+      TORCH_CHECK(!(s == 1 && g.mode != 0), "conv_train: segment 1 is mode 0");
+      if (width <= 0) continue;
+      const at::Tensor &gin = ts[9 + 3 * s], &mask = ts[10 + 3 * s], &out = ts[11 + 3 * s];
+      TORCH_CHECK(out.defined() && out.is_cuda() && out.is_contiguous() &&
+                      (out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16),
+                  "conv_train: segment output must be a contiguous fp32 / bf16 GPU tensor");
+      g.out = out.data_ptr(); g.out_cs = cs(out); g.out_coff = (int)ix[b + 4];
+      g.out_f32 = out.scalar_type() == at::kFloat;
+      TORCH_CHECK(g.out_cs % 8 == 0 && g.out_coff % 8 == 0 && g.out_coff + width <= g.out_cs &&
+                      out.numel() >= M * g.out_cs, "conv_train: segment output slice");
+      if (gin.defined()) {
+        need_f32(gin, 0, "gin");
+        g.gin = gin.data_ptr<float>(); g.gin_cs = cs(gin); g.gin_coff = (int)ix[b + 1];
+        TORCH_CHECK(g.gin_cs % 4 == 0 && g.gin_coff % 4 == 0 && g.gin_coff + width <= g.gin_cs &&
+                        gin.numel() >= M * g.gin_cs, "conv_train: segment gradient-input slice");
+      }
+      if (mask.defined()) {
+        TORCH_CHECK(g.mode == 0, "conv_train: ReLU mask in mode 0 only");
+        need_bf16(mask, 0, "mask");
+        g.mask = mask.data_ptr(); g.mask_cs = cs(mask); g.mask_coff = (int)ix[b + 2];
+        TORCH_CHECK(g.mask_cs % 8 == 0 && g.mask_coff % 8 == 0 && g.mask_coff + width <= g.mask_cs &&
+                        mask.numel() >= M * g.mask_cs, "conv_train: segment mask slice");
+      }
+      g.valid = (int)ix[b + 3];
+      if (g.mode != 0) {
+        gru = true;
+        TORCH_CHECK(g.out_f32 && g.out_cs == hd && g.out_coff == 0, "conv_train: GRU segment output is fp32 [M][hidden]");
+        if (g.mode == 2) TORCH_CHECK(!gin.defined(), "conv_train: reset-gate segment takes no gradient input");
+      }
+      if (keep) for (auto* v : {&gin, &mask, &out}) if (v->defined()) keep->push_back(*v);
+    }
+    if (gru) {
+      TORCH_CHECK(hd > 0, "conv_train: GRU segment needs hidden > 0");
+      const bool m1 = p.seg[0].mode == 1;
+      if (m1) { need_bf16(ts[3], M * hd, "gz"); need_bf16(ts[5], M * hd, "gq"); need_bf16(ts[7], M * hd, "gdq"); }
+      else need_bf16(ts[4], M * hd, "gr");
+      need_f32(ts[6], M * hd, "ghp");
+      need_bf16(ts[8], M * 2 * hd, "gdzr");
+      p.gz = ptr(ts[3]); p.gr = ptr(ts[4]); p.gq = ptr(ts[5]);
+      p.ghp = ts[6].data_ptr<float>(); p.gdq = ptr(ts[7]); p.gdzr = ts[8].data_ptr();
+    }
+  }
+  if (keep) for (auto& v : ts) if (v.defined()) keep->push_back(v);
+}
+
+// t = [mask, flow, gout, dmask, taps], i = [B, h, w], alpha
+static Launch make_upsample_convex_bwd(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep) {
+  at::Tensor mask = opt(t, 0), flow = opt(t, 1), g = opt(t, 2), dm = opt(t, 3), taps = opt(t, 4);
+  TORCH_CHECK(i.size() == 3, "upsample_convex_bwd: expected 3 ints");
+  check_bf16(mask, "mask"); check_f32(flow, "flow"); check_f32(g, "gout"); check_bf16(dm, "dmask"); check_f32(taps, "taps");
+  const int B = (int)i[0], h = (int)i[1], w = (int)i[2];
+  const int64_t M = (int64_t)B * h * w;
+  TORCH_CHECK(cs(mask) >= 576 && mask.numel() >= M * cs(mask), "upsample_convex_bwd: mask [M][>=576]");
+  TORCH_CHECK(cs(dm) >= 576 && dm.numel() >= M * cs(dm), "upsample_convex_bwd: dmask [M][>=576]");
+  TORCH_CHECK(flow.numel() >= 2 * M && g.numel() >= 128 * M && taps.numel() >= 18 * M, "upsample_convex_bwd: sizes");
+  if (keep) for (auto& v : {mask, flow, g, dm, taps}) keep->push_back(v);
+  const void* mp = mask.data_ptr();
+  const float* fp = flow.data_ptr<float>();
+  const float* gp = g.data_ptr<float>();
+  void* dp = dm.data_ptr();
+  float* tp = taps.data_ptr<float>();
+  const int mcs = cs(mask), dcs = cs(dm);
+  const float a = (float)alpha;
+  return [=](hipStream_t s, int) { return jr_upsample_convex_bwd(mp, mcs, fp, gp, B, h, w, a, dp, dcs, tp, s); };
+}
+
+// t = [taps, dflow], i = [N, h, w]
+static Launch make_flow_gather_bwd(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor taps = opt(t, 0), df = opt(t, 1);
+  TORCH_CHECK(i.size() == 3, "flow_gather_bwd: expected 3 ints");
+  check_f32(taps, "taps"); check_bf16(df, "dflow");
+  const int N = (int)i[0], h = (int)i[1], w = (int)i[2];
+  const int64_t M = (int64_t)N * h * w;
+  TORCH_CHECK(cs(taps) >= 18 && cs(taps) % 2 == 0 && taps.numel() >= M * cs(taps), "flow_gather_bwd: taps");
+  TORCH_CHECK(cs(df) >= 2 && df.numel() >= M * cs(df), "flow_gather_bwd: dflow");
+  if (keep) { keep->push_back(taps); keep->push_back(df); }
+  const float* tp = taps.data_ptr<float>();
+  void* dp = df.data_ptr();
+  const int tcs = cs(taps), dcs = cs(df);
+  return [=](hipStream_t s, int) { return jr_flow_gather_bwd(tp, tcs, N, h, w, dp, dcs, s); };
+}
+
+// t = [gout, dflow], i = [B, h, w]
+static Launch make_upsample_bilinear_bwd(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor g = opt(t, 0), df = opt(t, 1);
+  TORCH_CHECK(i.size() == 3, "upsample_bilinear_bwd: expected 3 ints");
+  check_f32(g, "gout"); check_bf16(df, "dflow");
+  const int B = (int)i[0], h = (int)i[1], w = (int)i[2];
+  const int64_t M = (int64_t)B * h * w;
+  TORCH_CHECK(g.numel() >= 128 * M && cs(df) >= 2 && df.numel() >= M * cs(df), "upsample_bilinear_bwd: sizes");
+  if (keep) { keep->push_back(g); keep->push_back(df); }
+  const float* gp = g.data_ptr<float>();
+  void* dp = df.data_ptr();
+  const int dcs = cs(df);
+  return [=](hipStream_t s, int) { return jr_upsample_bilinear_bwd(gp, B, h, w, dp, dcs, s); };
 }
 
 
@@ -593,6 +730,12 @@ void im2col_op(const TList& t, IList i) { run_now(make_im2col(t, i, nullptr)); }
 void flow_head_op(const TList& t, IList i) { run_now(make_flow_head(t, i, nullptr)); }
 void flow_taps_op(const TList& t, IList i) { run_now(make_flow_taps(t, i, nullptr)); }
 void conv_direct_op(const TList& t, IList i) { run_now(make_conv_direct(t, i, nullptr)); }
+void conv_train_op(const TList& t, IList i, double alpha, const TList& tx, IList ix) {
+  run_now(make_conv(t, i, alpha, nullptr, &tx, &ix));
+}
+void upsample_convex_bwd_op(const TList& t, IList i, double alpha) { run_now(make_upsample_convex_bwd(t, i, alpha, nullptr)); }
+void flow_gather_bwd_op(const TList& t, IList i) { run_now(make_flow_gather_bwd(t, i, nullptr)); }
+void upsample_bilinear_bwd_op(const TList& t, IList i) { run_now(make_upsample_bilinear_bwd(t, i, nullptr)); }
 
 // --------------------------------------------------------------------- Plan
 // A Plan is the lowered RAFT forward: three segments (prologue, loop body run
@@ -668,6 +811,16 @@ class Plan : public torch::CustomClassHolder {
   void add_flow_head(TList t, IList i) { push(make_flow_head(t, i, &keep_), "flow_head"); }
   void add_flow_taps(TList t, IList i) { push(make_flow_taps(t, i, &keep_), "flow_taps"); }
   void add_conv_direct(TList t, IList i) { push(make_conv_direct(t, i, &keep_), "conv_direct"); }
+  void add_conv_train(TList t, IList i, double alpha, TList tx, IList ix) {
+    push(make_conv(t, i, alpha, &keep_, &tx, &ix), "conv_train");
+  }
+  void add_upsample_convex_bwd(TList t, IList i, double alpha) {
+    push(make_upsample_convex_bwd(t, i, alpha, &keep_), "upsample_convex_bwd");
+  }
+  void add_flow_gather_bwd(TList t, IList i) { push(make_flow_gather_bwd(t, i, &keep_), "flow_gather_bwd"); }
+  void add_upsample_bilinear_bwd(TList t, IList i) { push(make_upsample_bilinear_bwd(t, i, &keep_), "upsample_bilinear_bwd"); }
+  void add_lookup_bwd(TList t, IList i) { push(make_lookup_bwd(t, i, &keep_), "lookup_bwd"); }
+  void add_im2col(TList t, IList i) { push(make_im2col(t, i, &keep_), "im2col"); }
 
   int64_t num_ops(int64_t seg) const { return (int64_t)segs_[seg].size(); }
   std::vector<std::string> op_names(int64_t seg) const {
@@ -886,6 +1039,10 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("flow_head(Tensor?[] t, int[] i) -> ()", &jr::flow_head_op);
   m.def("flow_taps(Tensor?[] t, int[] i) -> ()", &jr::flow_taps_op);
   m.def("conv_direct(Tensor?[] t, int[] i) -> ()", &jr::conv_direct_op);
+  m.def("conv_train(Tensor?[] t, int[] i, float alpha, Tensor?[] tx, int[] ix) -> ()", &jr::conv_train_op);
+  m.def("upsample_convex_bwd(Tensor?[] t, int[] i, float alpha) -> ()", &jr::upsample_convex_bwd_op);
+  m.def("flow_gather_bwd(Tensor?[] t, int[] i) -> ()", &jr::flow_gather_bwd_op);
+  m.def("upsample_bilinear_bwd(Tensor?[] t, int[] i) -> ()", &jr::upsample_bilinear_bwd_op);
   m.class_<jr::Plan>("Plan")
       .def(torch::init<>())
       .def("set_segment", &jr::Plan::set_segment)
@@ -909,6 +1066,12 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_flow_head", &jr::Plan::add_flow_head)
       .def("add_flow_taps", &jr::Plan::add_flow_taps)
       .def("add_conv_direct", &jr::Plan::add_conv_direct)
+      .def("add_conv_train", &jr::Plan::add_conv_train)
+      .def("add_upsample_convex_bwd", &jr::Plan::add_upsample_convex_bwd)
+      .def("add_flow_gather_bwd", &jr::Plan::add_flow_gather_bwd)
+      .def("add_upsample_bilinear_bwd", &jr::Plan::add_upsample_bilinear_bwd)
+      .def("add_lookup_bwd", &jr::Plan::add_lookup_bwd)
+      .def("add_im2col", &jr::Plan::add_im2col)
       .def("num_ops", &jr::Plan::num_ops)
       .def("op_names", &jr::Plan::op_names)
       .def("run", &jr::Plan::run)

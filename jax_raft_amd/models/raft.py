@@ -82,11 +82,12 @@ class RAFT(nn.Module):
         assert (H, W) == tuple(image2.shape[-3:-1]), "input images should have the same shape"
         assert (H % 8 == 0) and (W % 8 == 0), "input image H and W should be divisible by 8"
         autograd = engine_kw.pop("autograd", False)
+        fused = engine_kw.pop("fused", None)
         if image1.is_cuda:
             if train or autograd:
                 from ..ops.autograd import raft_forward_autograd
 
-                out = raft_forward_autograd(self, image1, image2, train, num_flow_updates)
+                out = raft_forward_autograd(self, image1, image2, train, num_flow_updates, fused=fused)
                 return out if return_all_iters else out[-1:]
             return self.engine(image1.device, **engine_kw).forward(image1, image2, num_flow_updates,
                                                                    return_all_iters=return_all_iters)

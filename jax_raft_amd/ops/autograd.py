@@ -215,23 +215,31 @@ class CorrPyramid(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *glevels):
         f1, f2 = ctx.saved_tensors
-        B, hq, wq, h, w, C, L = ctx.shape
-        nq = hq * wq
         shared = ctx.acc.take()
         if shared is not None:
             glevels = tuple(s if g is None else s + g for s, g in zip(shared, glevels))
-        dC = torch.zeros(B * nq, h, w, device=f1.device, dtype=torch.float32)
-        for l, g in enumerate(glevels):
-            if g is None:
-                continue
-            s = 2 ** l
-            hl, wl = g.shape[1], g.shape[2]
-            up = g.float().repeat_interleave(s, dim=1).repeat_interleave(s, dim=2) / float(s * s)
-            dC[:, : hl * s, : wl * s] += up
-        dC = dC.reshape(B, nq, h * w) / math.sqrt(C)
-        g1 = torch.matmul(dC, f2.float().reshape(B, h * w, C)).reshape(B, hq, wq, C)
-        g2 = torch.matmul(dC.transpose(1, 2), f1.float().reshape(B, nq, C)).reshape(B, h, w, C)
+        g1, g2 = pyramid_backward(f1, f2, ctx.shape, glevels)
         return g1, g2, None
+
+
+def pyramid_backward(f1, f2, shape, glevels):
+    """Gradients of the correlation pyramid w.r.t. the query / target feature
+    maps: the 2x2 average-pooling adjoints summed into the full-resolution
+    volume gradient dC, then the two GEMMs of ``C = f1 f2^T / sqrt(C)``."""
+    B, hq, wq, h, w, C, L = shape
+    nq = hq * wq
+    dC = torch.zeros(B * nq, h, w, device=f1.device, dtype=torch.float32)
+    for l, g in enumerate(glevels):
+        if g is None:
+            continue
+        s = 2 ** l
+        hl, wl = g.shape[1], g.shape[2]
+        up = g.float().repeat_interleave(s, dim=1).repeat_interleave(s, dim=2) / float(s * s)
+        dC[:, : hl * s, : wl * s] += up
+    dC = dC.reshape(B, nq, h * w) / math.sqrt(C)
+    g1 = torch.matmul(dC, f2.float().reshape(B, h * w, C)).reshape(B, hq, wq, C)
+    g2 = torch.matmul(dC.transpose(1, 2), f1.float().reshape(B, nq, C)).reshape(B, h, w, C)
+    return g1, g2
 
 
 def build_pyramid(fmap1, fmap2, num_levels: int) -> List[torch.Tensor]:
@@ -317,8 +325,17 @@ def index_pyramid(pyramid: Sequence[torch.Tensor], coords, radius: int):
     return PyramidLookup.apply(coords, radius, *pyramid)
 
 
-def raft_forward_autograd(model, image1, image2, train: bool, num_flow_updates: int):
-    """GPU forward with autograd: the module graph of
-    :meth:`RAFT.forward_reference` with its conv / correlation / lookup nodes
-    dispatched to the native Functions above (see :mod:`jax_raft_amd.ops.functional`)."""
+def raft_forward_autograd(model, image1, image2, train: bool, num_flow_updates: int, fused=None):
+    """GPU forward with autograd.  Default: the correlation pyramid + refinement
+    loop as one fused native node (:mod:`jax_raft_amd.train.fused`; encoders on
+    the Functions above).  ``fused=False`` (or ``JR_FUSED_TRAIN=0``): the module
+    graph of :meth:`RAFT.forward_reference` with its conv / correlation / lookup
+    nodes dispatched to the native Functions above (see
+    :mod:`jax_raft_amd.ops.functional`)."""
+    from ..train import fused as F
+
+    if fused is None:
+        fused = F.enabled()
+    if fused and F.supported(model):
+        return F.forward_train(model, image1, image2, train, num_flow_updates)
     return model.forward_reference(image1, image2, train, num_flow_updates)

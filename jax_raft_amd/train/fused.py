@@ -1,0 +1,653 @@
+"""Fused native training path of the RAFT refinement loop (forward + backward).
+
+The unfused training path (:mod:`jax_raft_amd.ops.autograd`) runs the update
+block as PyTorch autograd glue around native convolutions: every concat,
+gate, activation, residual and gradient accumulation is its own framework
+kernel, and each of the ``N`` iterations re-derives its weight gradients.
+This module replaces the whole loop (``jax_raft/model.py:484-510`` scanned
+``num_flow_updates`` times, ``model.py:589-603``) by ONE autograd node whose
+forward and backward are native plans:
+
+* **forward** -- the inference engine's fused kernels (lookup, implicit-GEMM
+  convs writing straight into the persistent ``[h | motion | flow]`` GRU input
+  buffers, the ConvGRU gate epilogues with the loop-invariant context share
+  folded into a per-pixel bias map, the flow-head coordinate update, the mask
+  conv + convex x8 upsampling), with every activation the backward needs
+  written to per-iteration buffers (one ``[T, M, C]`` tensor per site);
+* **backward** -- hand-written BPTT: per iteration (last to first) the
+  upsampling adjoints (``train.hip``), then each conv's data gradient as the
+  same implicit-GEMM kernel over flipped / transposed weights with the
+  ``EPI_BWD`` epilogue, which applies the ReLU masks, accumulates the motion
+  and hidden-state gradients in fp32 and performs the ConvGRU gate backward
+  (``h' = (1-z) h + z q``, ``model.py:301-312``) in registers, and the
+  pyramid-lookup scatter (``corr.hip``);
+* **weight gradients** -- deferred to the end of the backward and computed
+  ONCE per weight over all iterations stacked along K (``T * M`` rows): the
+  update block's weights are shared by every iteration, so ``dW = sum_t
+  X_t^T dY_t`` is one long-K GEMM instead of ``T`` small ones plus ``T - 1``
+  fp32 adds.  The context share of the ConvGRU gates is linear in the
+  (loop-invariant) context, so its weight and data gradients need only the
+  iteration sum of the gate gradients: one conv each per step.
+
+Both plans are recorded once per (shape, iterations) with every pointer,
+shape and tile config resolved, and replayed as captured hipGraphs.  The
+saved activations live in persistent buffers owned by :class:`FusedLoop`
+(~3 GB for raft_large at 6 x 384 x 512, 12 iterations): a forward must be
+followed by its backward before the next forward of the same loop (checked).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+
+from ..models.layers import FeatureEncoder
+from ..ops import native as nat
+from ..ops.native import ACT_NONE, ACT_RELU, EPI_GRU_A, EPI_GRU_B, EPI_STD, round_up
+
+BF16, F32 = torch.bfloat16, torch.float32
+EPI_BWD = 5
+
+
+@dataclass
+class Seg:
+    """One channel segment of an EPI_BWD conv (csrc/kernels/kernels.h:BwdSeg)."""
+    mode: int = 0
+    gin: Optional[torch.Tensor] = None
+    gin_coff: int = 0
+    mask: Optional[torch.Tensor] = None
+    mask_coff: int = 0
+    valid: int = 0
+    out: Optional[torch.Tensor] = None
+    out_coff: int = 0
+
+
+def _tx(rbuf=None, qbuf=None, h32o=None, gz=None, gr=None, gq=None, ghp=None, gdq=None, gdzr=None,
+        s0: Optional[Seg] = None, s1: Optional[Seg] = None):
+    s0, s1 = s0 or Seg(), s1 or Seg()
+    tx = [rbuf, qbuf, h32o, gz, gr, gq, ghp, gdq, gdzr, s0.gin, s0.mask, s0.out, s1.gin, s1.mask, s1.out]
+    ix = [s0.mode, s0.gin_coff, s0.mask_coff, s0.valid, s0.out_coff,
+          s1.mode, s1.gin_coff, s1.mask_coff, s1.valid, s1.out_coff]
+    return tx, ix
+
+
+def _flip_t(k: torch.Tensor) -> torch.Tensor:
+    """HWIO kernel -> the kernel of its data gradient (flipped taps, in/out swapped)."""
+    return torch.flip(k, dims=(0, 1)).permute(0, 1, 3, 2)
+
+
+def _pad_last(k: torch.Tensor, n: int) -> torch.Tensor:
+    if k.shape[-1] == n:
+        return k
+    out = k.new_zeros(k.shape[:-1] + (n,))
+    out[..., : k.shape[-1]] = k
+    return out
+
+
+_CFG_CACHE: Dict[tuple, int] = {}
+
+
+def supported(model) -> bool:
+    """Whether :class:`FusedLoop` can lower ``model``'s refinement loop."""
+    ub = model.update_block
+    me, rb = ub.motion_encoder, ub.recurrent_block
+    if not isinstance(model.feature_encoder, FeatureEncoder) or not isinstance(model.context_encoder, FeatureEncoder):
+        return False
+    hd = rb.hidden_size
+    ctx = model.context_encoder.out_channels - hd
+    if hd % 16 or ctx <= 0 or me.out_channels < 3 or model.feature_encoder.out_channels % 64:
+        return False
+    if model.mask_predictor is not None and (model.mask_predictor.conv.cout != 576 or
+                                             model.mask_predictor.convrelu.layers_0.cout % 8):
+        return False
+    if any(s != (1, 1) for s in (me.convflow1.layers_0.stride, me.conv.layers_0.stride)):
+        return False
+    return True
+
+
+class FusedLoop:
+    """Native forward/backward of ``num_flow_updates`` refinement iterations for
+    one model at one (batch, image size); see the module docstring."""
+
+    def __init__(self, model, B: int, H: int, W: int, T: int, device, use_graph: bool = True):
+        nat.require()
+        self.model = model
+        self.B, self.H, self.W, self.T = B, H, W, T
+        self.h, self.w = H // 8, W // 8
+        self.M = B * self.h * self.w
+        self.device = torch.device(device)
+        self.use_graph = use_graph
+        self.gen = 0            # forward generation (a backward must match the latest forward)
+        self.done_gen = -1
+        self._analyse()
+        self._params()
+        self._alloc()
+        self._specs: Dict[str, nat.ConvSpec] = {}
+        self._pack()
+        self.plan_f = self._build_fwd()
+        self.plan_b = self._build_bwd()
+
+    # ------------------------------------------------------------ structure
+    def _analyse(self):
+        m = self.model
+        ub = m.update_block
+        me, rb, fh = ub.motion_encoder, ub.recurrent_block, ub.flow_head
+        self.me, self.rb, self.fh, self.mp = me, rb, fh, m.mask_predictor
+        self.hd = rb.hidden_size
+        self.ctx_ch = m.context_encoder.out_channels - self.hd
+        self.ctx_cs = round_up(self.ctx_ch, 8)
+        self.G = len(rb.kernel_size)
+        self.grus = [getattr(rb, f"convgru{g + 1}") for g in range(self.G)]
+        self.L = m.corr_block.num_levels
+        self.radius = m.corr_block.radius
+        S = 2 * self.radius + 1
+        self.corr_ch = self.L * S * S
+        self.corr_cs = round_up(self.corr_ch, 8)
+        self.cl, self.fl = me.corr_layers, me.flow_layers
+        self.mot_out = me.out_channels
+        self.hx_real = self.hd + self.mot_out
+        self.hx_cs = round_up(self.hx_real, 8)
+        self.mot_cs = self.hx_cs - self.hd
+        self.flow_off = self.hd + self.mot_out - 2
+        self.cf_ch = self.cl[-1] + self.fl[-1]
+        self.cf_cs = round_up(self.cf_ch, 8)
+        self.fh_hidden = fh.hidden_size
+        self.has_mask = self.mp is not None
+        self.mask_hidden = self.mp.hidden_size if self.has_mask else 0
+        self.fm_cs = round_up(self.fh_hidden + self.mask_hidden, 8)
+        self.gate_cs = round_up(3 * self.hd, 8)
+        self.fmap_ch = m.feature_encoder.out_channels
+
+    def _params(self):
+        me, fh, mp = self.me, self.fh, self.mp
+        convs = [me.convcorr1.layers_0]
+        if len(self.cl) == 2:
+            convs.append(me.convcorr2.layers_0)
+        convs += [me.convflow1.layers_0, me.convflow2.layers_0, me.conv.layers_0]
+        for gru in self.grus:
+            convs += [gru.convz, gru.convr, gru.convq]
+        convs += [fh.conv1, fh.conv2]
+        if self.has_mask:
+            convs += [mp.convrelu.layers_0, mp.conv]
+        self.convs = convs
+        self.params: List[torch.nn.Parameter] = []
+        for c in convs:
+            self.params += [c.kernel, c.bias]
+
+    def _alloc(self):
+        T, G, M, hd, dev = self.T, self.G, self.M, self.hd, self.device
+        h, w = self.h, self.w
+
+        def z(*shape, dtype=BF16):
+            return torch.zeros(shape, dtype=dtype, device=dev)
+
+        self.ctx_in = z(M, self.ctx_cs)
+        self.fm1 = z(self.B, h, w, self.fmap_ch)
+        self.fm2 = z(self.B, h, w, self.fmap_ch)
+        self.gbias = [z(M, self.gate_cs, dtype=F32) for _ in range(G)]
+        # [g][t]: GRU g's inputs at iteration t; hx[0][t + 1] / hf[0][t + 1] = output of the last GRU
+        self.hx = z(G, T + 1, M, self.hx_cs)
+        self.qx = z(G, T + 1, M, self.hx_cs)
+        self.hf = z(G, T + 1, M, hd, dtype=F32)
+        self.zg = z(G, T, M, hd)
+        self.rg = z(G, T, M, hd)
+        self.qg = z(G, T, M, hd)
+        self.corr = z(T, M, self.corr_cs)
+        self.c1 = z(T, M, self.cl[0]) if len(self.cl) == 2 else None
+        self.cf = z(T, M, self.cf_cs)
+        self.f1 = z(T, M, self.fl[0])
+        self.flow8 = z(T + 1, M, 8)
+        self.coords = z(T + 1, M, 2, dtype=F32)
+        nat.ops().init_coords([self.coords[0]], [self.B, h, w])
+        self.flow32 = z(T, M, 2, dtype=F32)
+        self.fmm = z(T, M, self.fm_cs)
+        self.taps = z(M, 24, dtype=F32)
+        self.mask = z(T, M, 576) if self.has_mask else None
+        self.out = z(T, self.B, self.H, self.W, 2, dtype=F32)
+        levels = []
+        hl, wl = h, w
+        for _ in range(self.L):
+            levels.append(z(M, hl, wl, dtype=F32))
+            hl //= 2
+            wl //= 2
+        self.levels = levels
+        self.lv_grads = [torch.zeros_like(l) for l in levels]
+        # backward
+        self.gout = z(T, self.B, self.H, self.W, 2, dtype=F32)
+        self.dmask = z(T, M, 576) if self.has_mask else None
+        self.utaps = z(M, 18, dtype=F32)
+        self.ddelta = z(T, M, 8)
+        self.dfmm = z(T, M, self.fm_cs)
+        self.dq = z(G, T, M, hd)
+        self.dzr = z(G, T, M, 2 * hd)
+        self.dh = [z(M, hd, dtype=F32) for _ in range(G)]
+        self.dh_next = z(M, hd, dtype=F32)
+        self.dmot = z(M, self.mot_cs, dtype=F32)
+        self.dm = z(T, M, self.mot_cs)
+        self.dcf = z(T, M, self.cf_cs)
+        self.dc1 = z(T, M, self.cl[0]) if len(self.cl) == 2 else None
+        self.dcorr = z(M, self.corr_cs)
+        self.df1 = z(T, M, self.fl[0])
+        self.dctx = z(M, self.ctx_cs, dtype=F32)
+
+    # --------------------------------------------------------------- weights
+    def _sources(self):
+        """name -> () -> (HWIO fp32 kernel, fp32 bias, padding, cin8).  Forward
+        specs mirror runtime/engine.py; names ending in T are data-gradient specs
+        (flipped, in/out-swapped kernels, padding k-1-p, zero bias, output
+        channels padded to the buffer they are written into)."""
+        me, fh, mp, hd, C = self.me, self.fh, self.mp, self.hd, self.ctx_ch
+        src = {}
+
+        def kb(c):
+            return c.kernel.detach().float(), c.bias.detach().float()
+
+        def fwd(c, cin8=None):
+            return lambda: (*kb(c), c.padding, cin8)
+
+        def bwd(k_fn, pad, cin8, cout_pad):
+            def f():
+                k = k_fn()
+                kh, kw = k.shape[:2]
+                kt = _pad_last(_flip_t(k), cout_pad)
+                return kt, torch.zeros(cout_pad, device=k.device), (kh - 1 - pad[0], kw - 1 - pad[1]), cin8
+            return f
+
+        c1, cf1, cf2, mc = me.convcorr1.layers_0, me.convflow1.layers_0, me.convflow2.layers_0, me.conv.layers_0
+        src["cc1"] = fwd(c1, self.corr_cs)
+        src["cc1T"] = bwd(lambda: c1.kernel.detach().float(), c1.padding, round_up(c1.cout, 8), self.corr_cs)
+        if len(self.cl) == 2:
+            c2 = me.convcorr2.layers_0
+            src["cc2"] = fwd(c2)
+            src["cc2T"] = bwd(lambda: c2.kernel.detach().float(), c2.padding, round_up(c2.cout, 8), round_up(c2.cin, 8))
+        src["cf1"] = fwd(cf1, 8)
+        src["cf2"] = fwd(cf2)
+        src["cf2T"] = bwd(lambda: cf2.kernel.detach().float(), cf2.padding, round_up(cf2.cout, 8), round_up(cf2.cin, 8))
+        src["mc"] = fwd(mc)
+        src["mcT"] = bwd(lambda: mc.kernel.detach().float(), mc.padding, round_up(mc.cout, 8), self.cf_cs)
+
+        def loop_part(k):  # input channels [h | context | motion] -> [h | motion] (hx layout, padded)
+            k = k.detach().float()
+            kk = torch.cat([k[:, :, :hd], k[:, :, hd + C:]], dim=2)
+            out = k.new_zeros(k.shape[:2] + (self.hx_cs, k.shape[3]))
+            out[:, :, : kk.shape[2]] = kk
+            return out
+
+        for g, gru in enumerate(self.grus):
+            pad = gru.padding
+
+            def ga(gru=gru):
+                return torch.cat([loop_part(gru.convz.kernel), loop_part(gru.convr.kernel)], dim=3)
+
+            def gb(gru=gru):
+                return loop_part(gru.convq.kernel)
+
+            def gc(gru=gru):
+                return torch.cat([c.kernel.detach()[:, :, hd:hd + C] for c in (gru.convz, gru.convr, gru.convq)],
+                                 dim=3).float()
+
+            def gcb(gru=gru):
+                return torch.cat([c.bias.detach() for c in (gru.convz, gru.convr, gru.convq)]).float()
+
+            src[f"gA{g}"] = (lambda ga=ga, pad=pad: (ga(), torch.zeros(2 * hd, device=self.device), pad, self.hx_cs))
+            src[f"gB{g}"] = (lambda gb=gb, pad=pad: (gb(), torch.zeros(hd, device=self.device), pad, self.hx_cs))
+            src[f"gC{g}"] = (lambda gc=gc, gcb=gcb, pad=pad: (gc(), gcb(), pad, self.ctx_cs))
+            src[f"gAT{g}"] = bwd(ga, pad, 2 * hd, self.hx_cs)
+            src[f"gBT{g}"] = bwd(gb, pad, hd, self.hx_cs)
+            src[f"gCT{g}"] = bwd(gc, pad, 3 * hd, self.ctx_cs)
+        if self.has_mask:
+            mr = mp.convrelu.layers_0
+
+            def fh1():
+                return torch.cat([fh.conv1.kernel.detach(), mr.kernel.detach()], dim=3).float()
+
+            src["fh1"] = lambda: (fh1(), torch.cat([fh.conv1.bias.detach(), mr.bias.detach()]).float(), (1, 1), None)
+            src["fh1T"] = bwd(fh1, (1, 1), self.fm_cs, hd)
+            src["mask"] = fwd(mp.conv)
+            src["maskT"] = bwd(lambda: mp.conv.kernel.detach().float(), (0, 0), 576, self.mask_hidden)
+        else:
+            src["fh1"] = fwd(fh.conv1)
+            src["fh1T"] = bwd(lambda: fh.conv1.kernel.detach().float(), (1, 1), self.fm_cs, hd)
+
+        def taps():  # (3,3,cin,2) -> (1,1,cin,18): out channel tap*2 + o
+            k = fh.conv2.kernel.detach().float()
+            cin = k.shape[2]
+            return k.reshape(9, cin, 2).permute(1, 0, 2).reshape(1, 1, cin, 18)
+
+        src["fh2t"] = lambda: (taps(), torch.zeros(18, device=self.device), (0, 0), None)
+        src["fh2T"] = bwd(lambda: fh.conv2.kernel.detach().float(), (1, 1), 8, self.fh_hidden)
+        return src
+
+    def _pack(self):
+        """(Re)pack every spec in place (pointers stay valid for the recorded plans)."""
+        if not hasattr(self, "_src"):
+            self._src = self._sources()
+        for name, fn in self._src.items():
+            k, b, pad, cin8 = fn()
+            k = k.to(self.device)
+            sp = self._specs.get(name)
+            if sp is None:
+                self._specs[name] = nat.make_spec(k, b.to(self.device), (1, 1), tuple(pad), cin8=cin8, device=self.device)
+            else:
+                nat.pack_weight(k, sp.cin8, out=sp.w)
+                sp.b.copy_(b)
+        fb = self.fh.conv2.bias.detach().float().to(self.device)
+        if not hasattr(self, "_fh2_bias"):
+            self._fh2_bias = fb.contiguous()
+        else:
+            self._fh2_bias.copy_(fb)
+
+    # ----------------------------------------------------------- recording
+    def _cfg(self, spec, x, x_coff) -> int:
+        B, h, w = self.B, self.h, self.w
+        key = ("train", self.M, spec.cout, spec.kh, spec.kw, spec.cin8, x.shape[-1], str(self.device))
+        cfg = _CFG_CACHE.get(key)
+        if cfg is None:
+            from ..runtime.engine import _tune
+
+            y = torch.empty(self.M, round_up(spec.cout, 8), dtype=BF16, device=self.device)
+            cfg = _tune(spec, x, B, h, w, y, dict(x_coff=x_coff))
+            _CFG_CACHE[key] = cfg
+        return cfg
+
+    def _conv(self, plan, name, x, y, *, x_coff=0, tx=None, ix=None, **kw):
+        spec = self._specs[name]
+        cfg = self._cfg(spec, x, x_coff)
+        t, i, a = nat.conv_args(spec, x, self.B, self.h, self.w, y, x_coff=x_coff, cfg=cfg, **kw)
+        if tx is None:
+            plan.add_conv(t, i, a)
+        else:
+            plan.add_conv_train(t, i, a, tx, ix)
+
+    def _bconv(self, plan, name, x, *, x_coff=0, split=0, s0=None, s1=None, **gru):
+        """Data-gradient conv with the EPI_BWD epilogue."""
+        tx, ix = _tx(s0=s0, s1=s1, **gru)
+        y = (s1.out if s1 is not None and s1.out is not None else s0.out)
+        self._conv(plan, name, x, y, x_coff=x_coff, tx=tx, ix=ix, epi=EPI_BWD, hidden=split)
+
+    def _build_fwd(self):
+        P = nat.new_plan()
+        P.set_segment(0)
+        P.set_lane(0)
+        T, G, hd, B, h, w = self.T, self.G, self.hd, self.B, self.h, self.w
+        cl, fl = self.cl, self.fl
+        P.add_corr([self.fm1, self.fm2] + self.levels + [None] * (4 - self.L), [B, h, w, self.fmap_ch, self.L],
+                   1.0 / float(self.fmap_ch) ** 0.5)
+        for g in range(G):  # loop-invariant context share of every gate (+ biases), fp32
+            self._conv(P, f"gC{g}", self.ctx_in, self.gbias[g])
+        for t in range(T):
+            hx0, qx0 = self.hx[0, t], self.qx[0, t]
+            P.add_lookup([self.coords[t], self.corr[t]] + self.levels + [None] * (4 - self.L),
+                         [self.L, B, h, w, self.radius])
+            if len(cl) == 2:
+                self._conv(P, "cc1", self.corr[t], self.c1[t], act=ACT_RELU)
+                self._conv(P, "cc2", self.c1[t], self.cf[t], act=ACT_RELU)
+            else:
+                self._conv(P, "cc1", self.corr[t], self.cf[t], act=ACT_RELU)
+            self._conv(P, "cf1", self.flow8[t], self.f1[t], act=ACT_RELU)
+            self._conv(P, "cf2", self.f1[t], self.cf[t], y_coff=cl[-1], act=ACT_RELU)
+            self._conv(P, "mc", self.cf[t], hx0, y_coff=hd, act=ACT_RELU, y2=qx0, y2_coff=hd)
+            for g in range(1, G):  # [motion | flow] into the other GRUs' inputs
+                P.add_copy_channels([hx0, self.hx[g, t]], [hd, hd, self.M, self.mot_cs])
+                P.add_copy_channels([hx0, self.qx[g, t]], [hd, hd, self.M, self.mot_cs])
+            for g in range(G):
+                tx, ix = _tx(rbuf=self.rg[g, t])
+                self._conv(P, f"gA{g}", self.hx[g, t], self.qx[g, t], zbuf=self.zg[g, t], h32=self.hf[g, t],
+                           hidden=hd, epi=EPI_GRU_A, bmap=self.gbias[g], bmap_coff=0, tx=tx, ix=ix)
+                last = g + 1 == G
+                nh = self.hx[0, t + 1] if last else self.hx[g + 1, t]
+                nhf = self.hf[0, t + 1] if last else self.hf[g + 1, t]
+                tx, ix = _tx(qbuf=self.qg[g, t], h32o=nhf)
+                self._conv(P, f"gB{g}", self.qx[g, t], nh, zbuf=self.zg[g, t], h32=self.hf[g, t], hidden=hd,
+                           epi=EPI_GRU_B, bmap=self.gbias[g], bmap_coff=2 * hd, tx=tx, ix=ix)
+            hn = self.hx[0, t + 1]
+            self._conv(P, "fh1", hn, self.fmm[t], act=ACT_RELU)
+            self._conv(P, "fh2t", self.fmm[t], self.taps)
+            P.add_copy([self.coords[t], self.coords[t + 1]])
+            P.add_flow_taps([self.taps, self._fh2_bias, self.coords[t + 1], self.flow32[t], hn, self.qx[0, t + 1],
+                             self.flow8[t + 1]], [B, h, w, self.flow_off, self.flow_off])
+            if self.has_mask:
+                self._conv(P, "mask", self.fmm[t], self.mask[t], x_coff=self.fh_hidden,
+                           alpha=self.mp.multiplier)
+                P.add_upsample_convex([self.mask[t], self.flow32[t], self.out[t]], [B, h, w, 0])
+            else:
+                P.add_upsample_bilinear([self.flow32[t], self.out[t]], [B, h, w, 0])
+        return P
+
+    def _build_bwd(self):
+        P = nat.new_plan()
+        P.set_segment(0)
+        P.set_lane(0)
+        T, G, hd, B, h, w = self.T, self.G, self.hd, self.B, self.h, self.w
+        cl = self.cl
+        for g_ in self.lv_grads:
+            P.add_memset([g_])
+        for t in reversed(range(T)):
+            fm = self.fmm[t]
+            if self.has_mask:
+                P.add_upsample_convex_bwd([self.mask[t], self.flow32[t], self.gout[t], self.dmask[t], self.utaps],
+                                          [B, h, w], self.mp.multiplier)
+                P.add_flow_gather_bwd([self.utaps, self.ddelta[t]], [B, h, w])
+                self._bconv(P, "maskT", self.dmask[t],
+                            s1=Seg(mask=fm, mask_coff=self.fh_hidden, out=self.dfmm[t], out_coff=self.fh_hidden))
+            else:
+                P.add_upsample_bilinear_bwd([self.gout[t], self.ddelta[t]], [B, h, w])
+            self._bconv(P, "fh2T", self.ddelta[t], s1=Seg(mask=fm, out=self.dfmm[t]))
+            # flow head (+ mask) conv1 data gradient -> blend backward of the last GRU
+            gl = G - 1
+            self._bconv(P, "fh1T", self.dfmm[t], split=hd,
+                        s0=Seg(mode=1, gin=self.dh_next if t + 1 < T else None, out=self.dh[gl]),
+                        gz=self.zg[gl, t], gq=self.qg[gl, t], ghp=self.hf[gl, t], gdq=self.dq[gl, t],
+                        gdzr=self.dzr[gl, t])
+            for g in reversed(range(G)):
+                self._bconv(P, f"gBT{g}", self.dq[g, t], split=hd, s0=Seg(mode=2, out=self.dh[g]),
+                            s1=Seg(gin=None if g == gl else self.dmot, out=self.dmot),
+                            gr=self.rg[g, t], ghp=self.hf[g, t], gdzr=self.dzr[g, t])
+                if g > 0:
+                    self._bconv(P, f"gAT{g}", self.dzr[g, t], split=hd,
+                                s0=Seg(mode=1, gin=self.dh[g], out=self.dh[g - 1]),
+                                s1=Seg(gin=self.dmot, out=self.dmot),
+                                gz=self.zg[g - 1, t], gq=self.qg[g - 1, t], ghp=self.hf[g - 1, t],
+                                gdq=self.dq[g - 1, t], gdzr=self.dzr[g - 1, t])
+                else:
+                    self._bconv(P, "gAT0", self.dzr[0, t], split=hd, s0=Seg(gin=self.dh[0], out=self.dh_next),
+                                s1=Seg(gin=self.dmot, mask=self.hx[0, t], mask_coff=hd, valid=self.mot_out - 2,
+                                       out=self.dm[t]))
+            self._bconv(P, "mcT", self.dm[t], s1=Seg(mask=self.cf[t], out=self.dcf[t]))
+            if len(cl) == 2:
+                self._bconv(P, "cc2T", self.dcf[t], s1=Seg(mask=self.c1[t], out=self.dc1[t]))
+                self._bconv(P, "cc1T", self.dc1[t], s1=Seg(out=self.dcorr, valid=self.corr_ch))
+            else:
+                self._bconv(P, "cc1T", self.dcf[t], s1=Seg(out=self.dcorr, valid=self.corr_ch))
+            P.add_lookup_bwd([self.coords[t], self.dcorr] + self.lv_grads + [None] * (4 - self.L),
+                             [self.L, B, h, w, self.radius])
+            self._bconv(P, "cf2T", self.dcf[t], x_coff=cl[-1], s1=Seg(mask=self.f1[t], out=self.df1[t]))
+        return P
+
+    def _run(self, plan):
+        if self.use_graph:
+            if plan.captured_iters() != 0:
+                plan.capture(0)
+            plan.replay()
+        else:
+            plan.run(0)
+
+    # --------------------------------------------------------------- steps
+    def forward(self, fmap1: torch.Tensor, fmap2: torch.Tensor, ctx_raw: torch.Tensor) -> torch.Tensor:
+        """fmap1 / fmap2: feature-encoder outputs (B, h, w, C); ctx_raw:
+        context-encoder output (B, h, w, hidden + ctx).  Returns the
+        (T, B, H, W, 2) upsampled flows of every iteration."""
+        hd = self.hd
+        self._pack()
+        self.fm1.copy_(fmap1.detach())
+        self.fm2.copy_(fmap2.detach())
+        c = ctx_raw.detach().reshape(self.M, -1).float()
+        h0 = torch.tanh(c[:, :hd])
+        self.hf[0, 0].copy_(h0)
+        self.hx[0, 0, :, :hd].copy_(h0)
+        self.ctx_in[:, : self.ctx_ch].copy_(torch.relu(c[:, hd:]))
+        self._run(self.plan_f)
+        self.gen += 1
+        return self.out.clone()
+
+    def backward(self, gout: torch.Tensor, gen: int):
+        if gen != self.gen or self.done_gen == gen:
+            raise RuntimeError("fused refinement loop: this backward's saved activations were overwritten by a "
+                               "later forward of the same loop (run backward before the next forward) or it "
+                               "already ran (retain_graph is not supported by the fused loop)")
+        self.done_gen = gen
+        self.gout.copy_(gout)
+        self._run(self.plan_b)
+        return self._finish()
+
+    # ---------------------------------------------------- weight gradients
+    def _wgrad(self, x, n_img, x_coff, cin8, kh, kw, pad, dy, cin, cout):
+        """dW (kh, kw, cin, cout) fp32 = im2col(x)^T dy over the stacked images."""
+        from ..ops.autograd import _wgrad_gemm
+
+        kpad = round_up(kh * kw * cin8, 64)
+        Mt = n_img * self.h * self.w
+        col = torch.empty(Mt, kpad, dtype=BF16, device=self.device)
+        nat.ops().im2col([x, col], [n_img, self.h, self.w, x_coff, cin8, kh, kw, 1, 1, pad[0], pad[1]])
+        gw = _wgrad_gemm(dy, col, cout)
+        return gw[: kh * kw * cin8].reshape(kh, kw, cin8, cout)[:, :, :cin]
+
+    def _finish(self):
+        T, G, M, hd, C = self.T, self.G, self.M, self.hd, self.ctx_ch
+        nT = T * self.B
+        me, fh, mp = self.me, self.fh, self.mp
+        grads: Dict[int, torch.Tensor] = {}
+
+        def put(p, g):
+            grads[id(p)] = g.to(p.dtype)
+
+        def wb(conv, x, n_img, x_coff, cin8, dy2, pad=None):
+            kh, kw, cin, cout = conv.kernel.shape
+            pad = conv.padding if pad is None else pad
+            put(conv.kernel, self._wgrad(x, n_img, x_coff, cin8, kh, kw, pad, dy2, cin, cout))
+            put(conv.bias, dy2.sum(0, dtype=F32))
+
+        c1 = me.convcorr1.layers_0
+        if len(self.cl) == 2:
+            wb(c1, self.corr, nT, 0, self.corr_cs, self.dc1.reshape(-1, self.cl[0]))
+            wb(me.convcorr2.layers_0, self.c1, nT, 0, self.cl[0], self.dcf.reshape(-1, self.cf_cs)[:, : self.cl[1]])
+        else:
+            wb(c1, self.corr, nT, 0, self.corr_cs, self.dcf.reshape(-1, self.cf_cs)[:, : self.cl[0]])
+        wb(me.convflow1.layers_0, self.flow8[:T], nT, 0, 8, self.df1.reshape(-1, self.fl[0]))
+        wb(me.convflow2.layers_0, self.f1, nT, 0, self.fl[0],
+           self.dcf.reshape(-1, self.cf_cs)[:, self.cl[-1]: self.cl[-1] + self.fl[1]])
+        wb(me.conv.layers_0, self.cf, nT, 0, self.cf_cs, self.dm.reshape(-1, self.mot_cs)[:, : self.mot_out - 2])
+        # ConvGRUs: loop part (h | motion) per iteration stacked; context part once over the iteration sum
+        dctx = self.dctx
+        for g, gru in enumerate(self.grus):
+            kh, kw = gru.convz.kernel.shape[:2]
+            pad = gru.padding
+            gA = self._wgrad(self.hx[g, :T], nT, 0, self.hx_cs, kh, kw, pad, self.dzr[g].reshape(-1, 2 * hd),
+                             self.hx_cs, 2 * hd)
+            gB = self._wgrad(self.qx[g, :T], nT, 0, self.hx_cs, kh, kw, pad, self.dq[g].reshape(-1, hd),
+                             self.hx_cs, hd)
+            S = torch.cat([self.dzr[g].sum(0, dtype=F32), self.dq[g].sum(0, dtype=F32)], dim=1)  # (M, 3 hd)
+            Sb = S.to(BF16)
+            gC = self._wgrad(self.ctx_in, self.B, 0, self.ctx_cs, kh, kw, pad, Sb, C, 3 * hd)
+            db = S.sum(0)
+            loop_in = gru.convz.kernel.shape[2]  # hd + C + mot
+            for j, conv in enumerate((gru.convz, gru.convr, gru.convq)):
+                full = torch.zeros(kh, kw, loop_in, hd, device=self.device, dtype=F32)
+                src = gA[..., j * hd:(j + 1) * hd] if j < 2 else gB
+                full[:, :, :hd] = src[:, :, :hd]
+                full[:, :, hd + C:] = src[:, :, hd: hd + loop_in - hd - C]
+                full[:, :, hd:hd + C] = gC[..., j * hd:(j + 1) * hd]
+                put(conv.kernel, full)
+                put(conv.bias, db[j * hd:(j + 1) * hd])
+            # context data gradient of this GRU's gates (accumulated over the GRUs)
+            tx, ix = _tx(s1=Seg(gin=dctx if g > 0 else None, out=dctx))
+            spec = self._specs[f"gCT{g}"]
+            t_, i_, a_ = nat.conv_args(spec, Sb, self.B, self.h, self.w, dctx, epi=EPI_BWD, hidden=0,
+                                       cfg=self._cfg(spec, Sb, 0))
+            nat.ops().conv_train(t_, i_, a_, tx, ix)
+        # flow head / mask predictor
+        dfm = self.dfmm.reshape(-1, self.fm_cs)
+        hx_next = self.hx[0, 1:T + 1]
+        if self.has_mask:
+            mr = mp.convrelu.layers_0
+            k = self._wgrad(hx_next, nT, 0, hd, 3, 3, (1, 1), dfm, hd, self.fh_hidden + self.mask_hidden)
+            put(fh.conv1.kernel, k[..., : self.fh_hidden])
+            put(mr.kernel, k[..., self.fh_hidden:])
+            db = dfm.sum(0, dtype=F32)
+            put(fh.conv1.bias, db[: self.fh_hidden])
+            put(mr.bias, db[self.fh_hidden: self.fh_hidden + self.mask_hidden])
+            wb(mp.conv, self.fmm, nT, self.fh_hidden, self.mask_hidden, self.dmask.reshape(-1, 576))
+        else:
+            wb(fh.conv1, hx_next, nT, 0, hd, dfm[:, : self.fh_hidden])
+        wb(fh.conv2, self.fmm, nT, 0, self.fh_hidden, self.ddelta.reshape(-1, 8)[:, :2])
+        # correlation pyramid: pooling adjoints + the two GEMMs of fmap1 fmap2^T / sqrt(C)
+        from ..ops.autograd import pyramid_backward
+
+        g1, g2 = pyramid_backward(self.fm1, self.fm2, (self.B, self.h, self.w, self.h, self.w, self.fmap_ch, self.L),
+                                  self.lv_grads)
+        # context-encoder output gradient: [tanh'(h0) dh | relu'(ctx) dctx]
+        h0 = self.hf[0, 0]
+        dc = torch.empty(M, hd + C, device=self.device, dtype=F32)
+        dc[:, :hd] = self.dh_next * (1 - h0 * h0)
+        dc[:, hd:] = dctx[:, :C] * (self.ctx_in[:, :C] > 0)
+        return g1, g2, dc.reshape(self.B, self.h, self.w, hd + C), [grads.get(id(p)) for p in self.params]
+
+
+class FusedRefine(torch.autograd.Function):
+    """Autograd node of the correlation pyramid + the whole refinement loop
+    (see :class:`FusedLoop`): inputs fmap1, fmap2, the context-encoder output
+    and the loop's parameters; output the stacked upsampled flows."""
+
+    @staticmethod
+    def forward(ctx, loop: FusedLoop, fmap1, fmap2, ctx_raw, *params):
+        out = loop.forward(fmap1, fmap2, ctx_raw)
+        ctx.loop, ctx.gen = loop, loop.gen
+        ctx.dtypes = (fmap1.dtype, fmap2.dtype, ctx_raw.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        loop: FusedLoop = ctx.loop
+        g1, g2, dctx, pgrads = loop.backward(gout.contiguous(), ctx.gen)
+        d1, d2, d3 = ctx.dtypes
+        return (None, g1.to(d1), g2.to(d2), dctx.to(d3)) + tuple(pgrads)
+
+
+_LOOPS: Dict[tuple, FusedLoop] = {}
+
+
+def enabled() -> bool:
+    return os.environ.get("JR_FUSED_TRAIN", "1") != "0"
+
+
+def get_loop(model, B, H, W, T, device) -> FusedLoop:
+    key = (id(model), B, H, W, T, str(device))
+    lp = _LOOPS.get(key)
+    if lp is None or lp.model is not model:
+        # one loop per model and shape: drop stale entries of other shapes of this model
+        for k in [k for k, v in _LOOPS.items() if k[0] == id(model)]:
+            del _LOOPS[k]
+        lp = FusedLoop(model, B, H, W, T, device, use_graph=os.environ.get("JR_FUSED_GRAPH", "1") != "0")
+        _LOOPS[key] = lp
+    return lp
+
+
+def forward_train(model, image1, image2, train: bool, num_flow_updates: int):
+    """Training forward with the fused loop: the encoders run on the native
+    autograd path, the correlation pyramid + refinement loop is one
+    :class:`FusedRefine` node."""
+    B, H, W, _ = image1.shape
+    fmaps = model.feature_encoder(torch.cat([image1, image2], dim=0), train)
+    fmap1, fmap2 = torch.chunk(fmaps, 2, dim=0)
+    assert tuple(fmap1.shape[1:3]) == (H // 8, W // 8), "The feature encoder should downsample H and W by 8"
+    h, w = H // 8, W // 8
+    min_sz = 2 * (2 ** (model.corr_block.num_levels - 1))
+    assert h >= min_sz and w >= min_sz, (
+        "Feature maps are too small to be down-sampled by the correlation pyramid. "
+        f"H and W of feature maps should be at least {min_sz}; got: {(h, w)}.")
+    ctx_out = model.context_encoder(image1, train)
+    assert tuple(ctx_out.shape[1:3]) == (h, w), "The context encoder should downsample H and W by 8"
+    loop = get_loop(model, B, H, W, num_flow_updates, image1.device)
+    return FusedRefine.apply(loop, fmap1, fmap2, ctx_out, *loop.params)

@@ -1,0 +1,160 @@
+"""Fused native training path of the refinement loop (jax_raft_amd/train/fused.py)
+against the unfused native autograd path and fp32 CPU autograd of the golden
+model, plus the training-only kernels (upsampling adjoints) against torch
+autograd of the reference ops."""
+import pytest
+import torch
+
+from jax_raft_amd import raft_large, raft_small
+from jax_raft_amd.models import reference as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float().cpu() - b.float().cpu()).norm() / (b.float().cpu().norm() + 1e-8)).item()
+
+
+def _cos(a, b):
+    a, b = a.float().cpu().flatten(), b.float().cpu().flatten()
+    return (torch.dot(a, b) / (a.norm() * b.norm() + 1e-12)).item()
+
+
+def test_upsample_convex_bwd_kernel():
+    from jax_raft_amd.ops import native as nat
+
+    torch.manual_seed(0)
+    B, h, w = 2, 5, 7
+    M = B * h * w
+    mask = (torch.randn(B, h, w, 576) * 2).to(torch.bfloat16).float()
+    flow = torch.randn(B, h, w, 2) * 3
+    g = torch.randn(B, 8 * h, 8 * w, 2)
+    a = 0.25
+    m_ = (mask / a).requires_grad_(True)   # conv output before the multiplier
+    f_ = flow.clone().requires_grad_(True)
+    up = R.upsample_flow(f_, m_ * a)
+    (up * g).sum().backward()
+    dm = torch.empty(M, 576, dtype=torch.bfloat16, device="cuda")
+    taps = torch.empty(M, 18, device="cuda")
+    nat.ops().upsample_convex_bwd([mask.reshape(M, 576).to(torch.bfloat16).cuda(), flow.reshape(M, 2).cuda(),
+                                   g.cuda(), dm, taps], [B, h, w], a)
+    dflow = torch.empty(M, 8, dtype=torch.bfloat16, device="cuda")
+    nat.ops().flow_gather_bwd([taps, dflow], [B, h, w])
+    torch.cuda.synchronize()
+    assert _rel(dm, m_.grad.reshape(M, 576)) < 1e-2
+    assert _rel(dflow[:, :2], f_.grad.reshape(M, 2)) < 1e-2
+    assert dflow[:, 2:].abs().max().item() == 0
+
+
+def test_upsample_bilinear_bwd_kernel():
+    from jax_raft_amd.ops import native as nat
+
+    torch.manual_seed(1)
+    B, h, w = 2, 16, 20
+    M = B * h * w
+    flow = torch.randn(B, h, w, 2).requires_grad_(True)
+    g = torch.randn(B, 8 * h, 8 * w, 2)
+    (R.upsample_flow(flow, None) * g).sum().backward()
+    d = torch.empty(M, 8, dtype=torch.bfloat16, device="cuda")
+    nat.ops().upsample_bilinear_bwd([g.cuda(), d], [B, h, w])
+    torch.cuda.synchronize()
+    assert _rel(d[:, :2], flow.grad.reshape(M, 2)) < 1e-2
+
+
+def _setup(factory, B=2, H=128, W=160, seed=3):
+    torch.manual_seed(seed)
+    model, _ = factory()
+    model = model.cuda().train()
+    g = torch.Generator().manual_seed(seed)
+    i1 = torch.rand(B, H, W, 3, generator=g) * 2 - 1
+    i2 = torch.rand(B, H, W, 3, generator=g) * 2 - 1
+    target = torch.randn(B, H, W, 2, generator=g) * 4
+    return model, i1, i2, target
+
+
+def _run(model, i1, i2, target, iters, fused):
+    model.zero_grad(set_to_none=True)
+    out = model(i1.cuda(), i2.cuda(), train=True, num_flow_updates=iters, fused=fused)
+    w = torch.tensor([0.8 ** (iters - k - 1) for k in range(iters)], device="cuda").view(-1, 1, 1, 1, 1)
+    (w * (out.float() - target.cuda()).abs()).mean().backward()
+    torch.cuda.synchronize()
+    return out.detach(), {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
+
+
+@pytest.mark.parametrize("factory", [raft_large, raft_small])
+def test_fused_matches_unfused(factory):
+    model, i1, i2, target = _setup(factory)
+    state = {k: v.clone() for k, v in model.state_dict().items()}
+    out_u, g_u = _run(model, i1, i2, target, 3, fused=False)
+    model.load_state_dict(state)
+    out_f, g_f = _run(model, i1, i2, target, 3, fused=True)
+    assert out_f.shape == out_u.shape
+    assert _rel(out_f, out_u) < 2e-2, _rel(out_f, out_u)
+    assert set(g_f) == set(g_u)
+    scale = max(v.norm().item() for v in g_u.values())
+    bad = []
+    for n in g_u:
+        if g_u[n].norm().item() < 1e-4 * scale:
+            continue  # e.g. biases feeding an InstanceNorm: exactly-zero true gradient, rounding noise
+        c = _cos(g_f[n], g_u[n])
+        r = g_f[n].norm().item() / g_u[n].norm().item()
+        if c < 0.98 or not (0.9 < r < 1.1):
+            bad.append((n, round(c, 4), round(r, 4)))
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("factory", [raft_large, raft_small])
+def test_fused_matches_cpu_fp32(factory):
+    model, i1, i2, target = _setup(factory, seed=5)
+    mc = factory()[0]
+    mc.load_state_dict(model.state_dict())
+    mc.train()
+    out = mc(i1, i2, train=True, num_flow_updates=2)
+    w = torch.tensor([0.8, 1.0]).view(-1, 1, 1, 1, 1)
+    (w * (out - target).abs()).mean().backward()
+    ref = {n: p.grad for n, p in mc.named_parameters() if p.grad is not None}
+    outg, gg = _run(model, i1, i2, target, 2, fused=True)
+    assert _rel(outg, out) < 5e-2  # bf16 convs vs the fp32 golden model (random-init raft_small: ~3 %)
+    scale = max(v.norm().item() for v in ref.values())
+    cos = torch.tensor([_cos(gg[n], ref[n]) for n in ref if ref[n].norm().item() > 1e-4 * scale])
+    assert cos.median() > 0.97, cos
+    assert cos.min() > 0.7, cos
+
+
+def test_fused_graph_equals_eager(monkeypatch):
+    from jax_raft_amd.train import fused as F
+
+    model, i1, i2, target = _setup(raft_large, seed=7)
+    state = {k: v.clone() for k, v in model.state_dict().items()}
+    monkeypatch.setenv("JR_FUSED_GRAPH", "0")
+    F._LOOPS.clear()
+    out_e, g_e = _run(model, i1, i2, target, 2, fused=True)
+    monkeypatch.setenv("JR_FUSED_GRAPH", "1")
+    F._LOOPS.clear()
+    model.load_state_dict(state)
+    out_g, g_g = _run(model, i1, i2, target, 2, fused=True)
+    assert torch.equal(out_e, out_g)
+    for n in g_e:
+        assert torch.equal(g_e[n], g_g[n]), n
+
+
+def test_fused_repeated_steps_and_guard():
+    """Weights repacked per step (an optimizer step changes the result), and a
+    second forward before the first backward is refused."""
+    model, i1, i2, target = _setup(raft_large, seed=9)
+    opt = torch.optim.SGD(model.parameters(), lr=1e-2)
+    losses = []
+    for _ in range(3):
+        opt.zero_grad()
+        out = model(i1.cuda(), i2.cuda(), train=True, num_flow_updates=2, fused=True)
+        loss = (out - target.cuda()).abs().mean()
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert all(torch.isfinite(torch.tensor(losses)))
+    assert losses[0] != losses[1] != losses[2]
+    a = model(i1.cuda(), i2.cuda(), train=True, num_flow_updates=2, fused=True)
+    b = model(i1.cuda(), i2.cuda(), train=True, num_flow_updates=2, fused=True)
+    b.sum().backward()
+    with pytest.raises(RuntimeError, match="overwritten"):
+        a.sum().backward()
