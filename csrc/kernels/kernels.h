@@ -157,6 +157,25 @@ int jr_upsample_bilinear_bwd(const float* gout, int B, int h, int w, void* dflow
 // dflow(p) = sum_k taps[p - d_k][2k + c] over the in-map 3x3 neighbours (d_k = (k/3-1, k%3-1)),
 // written as bf16 [M][dcs] (channels 0, 1; 2..dcs-1 zeroed)
 int jr_flow_gather_bwd(const float* taps, int tcs, int N, int h, int w, void* dflow, int dcs, hipStream_t stream);
+// Backward of an encoder unit "y -> norm (mode 0 none / 1 instance / 2 batch, gamma/beta
+// optional) -> relu (relu & 1)" whose output gradient is gout * [om > 0] (om optional: the
+// ReLU'd residual-block output): dy bf16, gres fp32 (optional) = gout * [om > 0]; red fp32
+// [N][C][2] = per-(n, c) (sum g, sum g*xhat) (the BN affine gradients), partial: workspace of
+// jr_norm_bwd_partials(N, HW) * C * 2 floats.  y / gout / om / dy / gres are [N][HW][C] dense.
+int jr_norm_bwd_partials(int N, int HW);
+int jr_norm_bwd(const void* gout, const void* om, const void* y, const float* stats, int mode, const float* gamma,
+                const float* beta, int relu, int N, int HW, int C, float eps, float* red, float* partial, void* dy,
+                float* gres, hipStream_t stream);
+// Sequence loss over N <= 32 predictions pred fp32 [N][P][2] vs gt fp32 [P][2]
+// (valid: optional fp32 [P]): part fp32 [jr_seq_loss_blocks(P)][37] per-block
+// partial sums (0..N-1: sum over valid pixels of |pred_i - gt|_1; 32: EPE sum of
+// the last prediction, 33..35: its <1/<3/<5 px counts, 36: valid count).
+int jr_seq_loss_blocks(long P);
+int jr_seq_loss(const float* pred, const float* gt, const float* valid, long P, int N, float max_flow, float* part,
+                hipStream_t stream);
+// grad fp32 [N][P][2] = scale[i] * valid * sign(pred_i - gt)
+int jr_seq_loss_bwd(const float* pred, const float* gt, const float* valid, long P, int N, float max_flow,
+                    const float* scale, float* grad, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
 // Misc.

@@ -4,6 +4,8 @@
 // atomics): the convex upsampling's flow gradient is split into per-neighbour
 // partials (one wave per low-res pixel) and a shifted-partials sum, the same
 // "taps" decomposition the forward flow head uses (flowhead.hip).
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -162,9 +164,291 @@ __global__ __launch_bounds__(256) void upsample_bilinear_bwd_kernel(const float*
   for (int c = 2; c < dcs; ++c) o[c] = f2bf(0.f);
 }
 
+// RAFT sequence loss (original RAFT recipe; the reference returns every
+// iteration's prediction for it, model.py:510,605): one pass over the N
+// predictions.  Per block, partial sums of |pred_i - gt| over the valid pixels
+// (valid = (|gt| < max_flow) & (valid_in >= 0.5)) for every iteration, and on
+// the final prediction the EPE sum, the <1/<3/<5 px counts and the valid
+// count: part[block][N + 5], reduced on the host side in fixed order.
+constexpr int LOSS_MAX_N = 32;
+
+JR_DEVICE bool loss_valid(const float* gt, const float* vin, long p, float max_flow) {
+  const float2 g = *(const float2*)(gt + 2 * p);
+  return sqrtf(g.x * g.x + g.y * g.y) < max_flow && (vin == nullptr || vin[p] >= 0.5f);
+}
+
+__global__ __launch_bounds__(256) void seq_loss_kernel(const float* __restrict__ pred, const float* __restrict__ gt,
+                                                       const float* __restrict__ vin, long P, int N, float max_flow,
+                                                       float* __restrict__ part) {
+  __shared__ float red[LOSS_MAX_N + 5][8];
+  float acc[LOSS_MAX_N + 5];
+#pragma unroll
+  for (int k = 0; k < LOSS_MAX_N + 5; ++k) acc[k] = 0.f;
+  const long stride = (long)gridDim.x * 256;
+  for (long p = (long)blockIdx.x * 256 + threadIdx.x; p < P; p += stride) {
+    if (!loss_valid(gt, vin, p, max_flow)) continue;
+    const float2 g = *(const float2*)(gt + 2 * p);
+#pragma unroll
+    for (int i = 0; i < LOSS_MAX_N; ++i) {
+      if (i < N) {
+        const float2 f = *(const float2*)(pred + 2 * ((long)i * P + p));
+        acc[i] += fabsf(f.x - g.x) + fabsf(f.y - g.y);
+        if (i == N - 1) {
+          const float e = sqrtf((f.x - g.x) * (f.x - g.x) + (f.y - g.y) * (f.y - g.y));
+          acc[LOSS_MAX_N] += e;
+          acc[LOSS_MAX_N + 1] += e < 1.f ? 1.f : 0.f;
+          acc[LOSS_MAX_N + 2] += e < 3.f ? 1.f : 0.f;
+          acc[LOSS_MAX_N + 3] += e < 5.f ? 1.f : 0.f;
+          acc[LOSS_MAX_N + 4] += 1.f;
+        }
+      }
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < LOSS_MAX_N + 5; ++k) {
+    float v = acc[k];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (lane == 0) red[k][wave] = v;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < LOSS_MAX_N + 5; k += 256)
+    part[(long)blockIdx.x * (LOSS_MAX_N + 5) + k] = ((red[k][0] + red[k][1]) + red[k][2]) + red[k][3];
+}
+
+// grad[i][p] = scale_i * valid(p) * sign(pred_i(p) - gt(p))   (scale_i = g_out * gamma^(N-1-i) / (2P))
+__global__ __launch_bounds__(256) void seq_loss_bwd_kernel(const float* __restrict__ pred, const float* __restrict__ gt,
+                                                           const float* __restrict__ vin, long P, int N,
+                                                           float max_flow, const float* __restrict__ scale,
+                                                           float* __restrict__ grad) {
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  const bool v = loss_valid(gt, vin, p, max_flow);
+  const float2 g = *(const float2*)(gt + 2 * p);
+  for (int i = 0; i < N; ++i) {
+    const long o = 2 * ((long)i * P + p);
+    const float2 f = *(const float2*)(pred + o);
+    const float s = v ? scale[i] : 0.f;
+    const float dx = f.x > g.x ? s : (f.x < g.x ? -s : 0.f);
+    const float dy = f.y > g.y ? s : (f.y < g.y ? -s : 0.f);
+    *(float2*)(grad + o) = make_float2(dx, dy);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Normalisation backward of the encoders' "conv -> norm -> (relu) [+ residual]"
+// units (InstanceNorm model.py:706-707, BatchNorm :147,157 in train mode, or
+// identity), given the forward's raw conv output y and its per-(n, c)
+// (sum, sumsq) statistics (elementwise.hip:jr_channel_stats):
+//   g   = gout * [om > 0] * [relu: z > 0],  z = gamma * xhat + beta
+//   dy  = rstd * gamma * (g - mean(g) - xhat * mean(g * xhat))     (means over the norm set)
+//   gres = gout * [om > 0]                                          (residual-branch gradient)
+// mode 0 (no norm): dy = g.  Reductions are deterministic two-pass (no atomics).
+// ---------------------------------------------------------------------------
+constexpr int NB_ROWS = 1024;
+
+struct NormCo {
+  float mean[8], rstd[8], gam[8], bet[8];
+};
+
+JR_DEVICE void norm_co(NormCo& o, const float* st, int mode, const float* gam, const float* bet, int n, int N, int HW,
+                       int C, int c0, float eps) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    float m = 0.f, r = 1.f;
+    if (mode == 1) {
+      const float inv = 1.0f / (float)HW;
+      m = st[((long)n * C + c) * 2] * inv;
+      r = rsqrtf(fmaxf(st[((long)n * C + c) * 2 + 1] * inv - m * m, 0.f) + eps);
+    } else if (mode == 2) {
+      float s0 = 0.f, s1 = 0.f;
+      for (int k = 0; k < N; ++k) { s0 += st[((long)k * C + c) * 2]; s1 += st[((long)k * C + c) * 2 + 1]; }
+      const float inv = 1.0f / ((float)HW * (float)N);
+      m = s0 * inv;
+      r = rsqrtf(fmaxf(s1 * inv - m * m, 0.f) + eps);
+    }
+    o.mean[j] = m;
+    o.rstd[j] = r;
+    o.gam[j] = gam ? gam[c] : 1.f;
+    o.bet[j] = bet ? bet[c] : 0.f;
+  }
+}
+
+// g and xhat of 8 channels of one row
+JR_DEVICE void norm_g(const NormCo& co, const bf16* gp, const bf16* op, const bf16* yp, int relu, float (&g)[8],
+                      float (&xh)[8]) {
+  const bf16x8 gv = *(const bf16x8*)gp;
+  const bf16x8 yv = *(const bf16x8*)yp;
+  bf16x8 ov;
+  if (op) ov = *(const bf16x8*)op;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    xh[j] = (bf2f(yv[j]) - co.mean[j]) * co.rstd[j];
+    float v = bf2f(gv[j]);
+    if (op && !(bf2f(ov[j]) > 0.f)) v = 0.f;
+    if ((relu & 1) && !(co.gam[j] * xh[j] + co.bet[j] > 0.f)) v = 0.f;
+    g[j] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void norm_bwd_partial_kernel(const bf16* __restrict__ gout, const bf16* __restrict__ om,
+                                                               const bf16* __restrict__ y, const float* __restrict__ st,
+                                                               int mode, const float* __restrict__ gam,
+                                                               const float* __restrict__ bet, int relu, int N, int HW,
+                                                               int C, float eps, float* __restrict__ part) {
+  __shared__ float red[256][17];
+  const int n = blockIdx.y;
+  const int cg = C >> 3;
+  const int tid = threadIdx.x;
+  const int g8 = tid % cg, rg = tid / cg, nrg = 256 / cg;
+  const int r0 = blockIdx.x * NB_ROWS;
+  const int r1 = min(r0 + NB_ROWS, HW);
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
+  if (rg < nrg) {
+    NormCo co;
+    norm_co(co, st, mode, gam, bet, n, N, HW, C, g8 * 8, eps);
+    const long base = (long)n * HW * C + g8 * 8;
+    for (int r = r0 + rg; r < r1; r += nrg) {
+      const long off = base + (long)r * C;
+      float g[8], xh[8];
+      norm_g(co, gout + off, om ? om + off : nullptr, y + off, relu, g, xh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s[j] += g[j]; q[j] += g[j] * xh[j]; }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[tid][j] = s[j]; red[tid][8 + j] = q[j]; }
+  __syncthreads();
+  const int nb = gridDim.x;
+  for (int t = tid; t < cg * 16; t += 256) {
+    const int gg = t % cg, vi = t / cg;
+    float acc = 0.f;
+    for (int k = 0; k < nrg; ++k) acc += red[k * cg + gg][vi];
+    const int c = gg * 8 + (vi & 7);
+    part[(((long)n * nb + blockIdx.x) * C + c) * 2 + (vi >> 3)] = acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void norm_bwd_final_kernel(const float* __restrict__ part, int nb, int C,
+                                                             float* __restrict__ red) {
+  __shared__ float sm[4][64];
+  const int n = blockIdx.y;
+  const int vi = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lb = threadIdx.x >> 6;
+  const int nv = 2 * C;
+  float acc = 0.f;
+  if (vi < nv) {
+    const float* p = part + (long)n * nb * nv + vi;
+    for (int b = lb; b < nb; b += 4) acc += p[(long)b * nv];
+  }
+  sm[lb][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (lb == 0 && vi < nv) {
+    const int t = threadIdx.x;
+    red[(long)n * nv + vi] = ((sm[0][t] + sm[1][t]) + sm[2][t]) + sm[3][t];
+  }
+}
+
+__global__ __launch_bounds__(256) void norm_bwd_apply_kernel(const bf16* __restrict__ gout, const bf16* __restrict__ om,
+                                                             const bf16* __restrict__ y, const float* __restrict__ st,
+                                                             int mode, const float* __restrict__ gam,
+                                                             const float* __restrict__ bet, int relu,
+                                                             const float* __restrict__ red, int N, int HW, int C,
+                                                             float eps, bf16* __restrict__ dy, float* __restrict__ gres,
+                                                             int rows) {
+  const int n = blockIdx.y;
+  const int cg = C >> 3;
+  const int tid = threadIdx.x;
+  const int g8 = tid % cg, rg = tid / cg, nrg = 256 / cg;
+  if (rg >= nrg) return;
+  const int c0 = g8 * 8;
+  NormCo co;
+  norm_co(co, st, mode, gam, bet, n, N, HW, C, c0, eps);
+  float a[8], m1[8], m2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    float S1 = 0.f, S2 = 0.f, cnt = (float)HW;
+    if (mode == 1) {
+      S1 = red[((long)n * C + c) * 2];
+      S2 = red[((long)n * C + c) * 2 + 1];
+    } else if (mode == 2) {
+      for (int k = 0; k < N; ++k) { S1 += red[((long)k * C + c) * 2]; S2 += red[((long)k * C + c) * 2 + 1]; }
+      cnt *= (float)N;
+    }
+    a[j] = co.rstd[j] * co.gam[j];
+    m1[j] = S1 / cnt;
+    m2[j] = S2 / cnt;
+  }
+  const long base = (long)n * HW * C + c0;
+  const int r0 = blockIdx.x * rows;
+  const int r1 = min(r0 + rows, HW);
+  for (int row = r0 + rg; row < r1; row += nrg) {
+    const long off = base + (long)row * C;
+    float g[8], xh[8];
+    norm_g(co, gout + off, om ? om + off : nullptr, y + off, relu, g, xh);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(mode == 0 ? g[j] : a[j] * (g[j] - m1[j] - xh[j] * m2[j]));
+    *(bf16x8*)(dy + off) = o;
+    if (gres) {
+      const bf16x8 gv = *(const bf16x8*)(gout + off);
+      bf16x8 ov;
+      if (om) ov = *(const bf16x8*)(om + off);
+      float r[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = (om && !(bf2f(ov[j]) > 0.f)) ? 0.f : bf2f(gv[j]);
+      *(f32x4*)(gres + off) = f32x4{r[0], r[1], r[2], r[3]};
+      *(f32x4*)(gres + off + 4) = f32x4{r[4], r[5], r[6], r[7]};
+    }
+  }
+}
+
 inline unsigned nblk(long total, int bs) { return (unsigned)((total + bs - 1) / bs); }
 
 }  // namespace
+
+extern "C" int jr_norm_bwd_partials(int N, int HW) { return N * ((HW + NB_ROWS - 1) / NB_ROWS); }
+
+extern "C" int jr_norm_bwd(const void* gout, const void* om, const void* y, const float* stats, int mode,
+                           const float* gamma, const float* beta, int relu, int N, int HW, int C, float eps,
+                           float* red, float* partial, void* dy, float* gres, hipStream_t stream) {
+  if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
+  if (mode != 0) {
+    const int nb = (HW + NB_ROWS - 1) / NB_ROWS;
+    hipLaunchKernelGGL(norm_bwd_partial_kernel, dim3(nb, N), dim3(256), 0, stream, (const bf16*)gout,
+                       (const bf16*)om, (const bf16*)y, stats, mode, gamma, beta, relu, N, HW, C, eps, partial);
+    hipLaunchKernelGGL(norm_bwd_final_kernel, dim3((2 * C + 63) / 64, N), dim3(256), 0, stream, partial, nb, C, red);
+  }
+  const int nrg = 256 / (C / 8);
+  const long want = ((long)N * HW + 2047) / 2048;
+  const int rows = (int)std::max<long>(nrg, (want + nrg - 1) / nrg * nrg);
+  const unsigned nbk = (unsigned)((HW + rows - 1) / rows);
+  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(nbk, N), dim3(256), 0, stream, (const bf16*)gout, (const bf16*)om,
+                     (const bf16*)y, stats, mode, gamma, beta, relu, red, N, HW, C, eps, (bf16*)dy, gres, rows);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jr_seq_loss_blocks(long P) { return (int)std::min<long>(1024, (P + 255) / 256); }
+
+extern "C" int jr_seq_loss(const float* pred, const float* gt, const float* valid, long P, int N, float max_flow,
+                           float* part, hipStream_t stream) {
+  if (N < 1 || N > LOSS_MAX_N) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(seq_loss_kernel, dim3(jr_seq_loss_blocks(P)), dim3(256), 0, stream, pred, gt, valid, P, N,
+                     max_flow, part);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jr_seq_loss_bwd(const float* pred, const float* gt, const float* valid, long P, int N, float max_flow,
+                               const float* scale, float* grad, hipStream_t stream) {
+  hipLaunchKernelGGL(seq_loss_bwd_kernel, dim3(nblk(P, 256)), dim3(256), 0, stream, pred, gt, valid, P, N, max_flow,
+                     scale, grad);
+  return (int)hipGetLastError();
+}
 
 extern "C" int jr_upsample_convex_bwd(const void* mask, int mask_cs, const float* flow, const float* gout, int B,
                                       int h, int w, float alpha, void* dmask, int dmask_cs, float* taps,

@@ -311,6 +311,42 @@ static Launch make_upsample_convex_bwd(const TList& t, const IList& i, double al
   return [=](hipStream_t s, int) { return jr_upsample_convex_bwd(mp, mcs, fp, gp, B, h, w, a, dp, dcs, tp, s); };
 }
 
+// t = [gout, om?, y, stats?, gamma?, beta?, red?, partial?, dy, gres?], i = [mode, relu, N, HW, C]
+static Launch make_norm_bwd(const TList& t, const IList& i, double eps, std::vector<at::Tensor>* keep) {
+  at::Tensor g = opt(t, 0), om = opt(t, 1), y = opt(t, 2), st = opt(t, 3), gam = opt(t, 4), bet = opt(t, 5);
+  at::Tensor red = opt(t, 6), part = opt(t, 7), dy = opt(t, 8), gres = opt(t, 9);
+  TORCH_CHECK(i.size() == 5, "norm_bwd: expected [mode, relu, N, HW, C]");
+  const int mode = (int)i[0], relu = (int)i[1], N = (int)i[2], HW = (int)i[3], C = (int)i[4];
+  const int64_t n = (int64_t)N * HW * C;
+  TORCH_CHECK(mode >= 0 && mode <= 2 && C % 8 == 0 && C <= 2048, "norm_bwd: mode 0..2, C % 8 == 0");
+  check_bf16(g, "gout"); check_bf16(y, "y"); check_bf16(dy, "dy");
+  TORCH_CHECK(g.numel() >= n && y.numel() >= n && dy.numel() >= n && cs(g) == C && cs(y) == C && cs(dy) == C,
+              "norm_bwd: [N][HW][C] tensors");
+  if (om.defined()) { check_bf16(om, "om"); TORCH_CHECK(om.numel() >= n && cs(om) == C, "norm_bwd: om"); }
+  if (gres.defined()) { check_f32(gres, "gres"); TORCH_CHECK(gres.numel() >= n && cs(gres) == C, "norm_bwd: gres"); }
+  if (mode) {
+    check_f32(st, "stats");
+    TORCH_CHECK(st.numel() >= (int64_t)N * C * 2, "norm_bwd: stats");
+    check_f32(red, "red");
+    TORCH_CHECK(red.numel() >= (int64_t)N * C * 2, "norm_bwd: red");
+    const int64_t need = (int64_t)jr_norm_bwd_partials(N, HW) * C * 2;
+    if (!part.defined()) part = at::empty({need}, st.options());
+    check_f32(part, "partial");
+    TORCH_CHECK(part.numel() >= need, "norm_bwd: partial workspace too small");
+  }
+  for (auto* v : {&gam, &bet}) if (v->defined()) { check_f32(*v, "affine"); TORCH_CHECK(v->numel() >= C, "norm_bwd: affine"); }
+  if (keep) for (auto& v : {g, om, y, st, gam, bet, red, part, dy, gres}) if (v.defined()) keep->push_back(v);
+  auto fp = [](const at::Tensor& v) -> float* { return v.defined() ? v.data_ptr<float>() : nullptr; };
+  const void *gp = g.data_ptr(), *op = ptr(om), *yp = y.data_ptr();
+  const float *sp = fp(st), *gmp = fp(gam), *btp = fp(bet);
+  float *rp = fp(red), *pp = fp(part), *grp = fp(gres);
+  void* dp = dy.data_ptr();
+  const float e = (float)eps;
+  return [=](hipStream_t s, int) {
+    return jr_norm_bwd(gp, op, yp, sp, mode, gmp, btp, relu, N, HW, C, e, rp, pp, dp, grp, s);
+  };
+}
+
 // t = [taps, dflow], i = [N, h, w]
 static Launch make_flow_gather_bwd(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
   at::Tensor taps = opt(t, 0), df = opt(t, 1);
@@ -711,6 +747,38 @@ static Launch make_im2col(const TList& t, const IList& i, std::vector<at::Tensor
 
 static void run_now(const Launch& l) { JR_CHECK_OK(l(cur_stream(), 0)); }
 
+// ------------------------------------------------------------- sequence loss
+// t = [pred (fp32 [N][P][2]), gt (fp32 [P][2]), valid? (fp32 [P]), part (fp32 [blocks][37])], i = [P, N]
+void seq_loss_op(const TList& t, IList i, double max_flow) {
+  at::Tensor pred = opt(t, 0), gt = opt(t, 1), valid = opt(t, 2), part = opt(t, 3);
+  TORCH_CHECK(i.size() == 2, "seq_loss: expected [P, N]");
+  check_f32(pred, "pred"); check_f32(gt, "gt"); check_f32(part, "part");
+  const int64_t P = i[0];
+  const int N = (int)i[1];
+  TORCH_CHECK(N >= 1 && N <= 32, "seq_loss: 1..32 predictions");
+  TORCH_CHECK(pred.numel() == (int64_t)N * P * 2 && gt.numel() == P * 2, "seq_loss: shapes");
+  TORCH_CHECK(part.numel() >= (int64_t)jr_seq_loss_blocks(P) * 37, "seq_loss: partials");
+  if (valid.defined()) { check_f32(valid, "valid"); TORCH_CHECK(valid.numel() == P, "seq_loss: valid"); }
+  JR_CHECK_OK(jr_seq_loss(pred.data_ptr<float>(), gt.data_ptr<float>(),
+                          valid.defined() ? valid.data_ptr<float>() : nullptr, P, N, (float)max_flow,
+                          part.data_ptr<float>(), cur_stream()));
+}
+int64_t seq_loss_blocks_op(int64_t P) { return jr_seq_loss_blocks(P); }
+// t = [pred, gt, valid?, scale (fp32 [N]), grad (fp32 [N][P][2])], i = [P, N]
+void seq_loss_bwd_op(const TList& t, IList i, double max_flow) {
+  at::Tensor pred = opt(t, 0), gt = opt(t, 1), valid = opt(t, 2), scale = opt(t, 3), grad = opt(t, 4);
+  TORCH_CHECK(i.size() == 2, "seq_loss_bwd: expected [P, N]");
+  check_f32(pred, "pred"); check_f32(gt, "gt"); check_f32(scale, "scale"); check_f32(grad, "grad");
+  const int64_t P = i[0];
+  const int N = (int)i[1];
+  TORCH_CHECK(pred.numel() == (int64_t)N * P * 2 && gt.numel() == P * 2 && grad.numel() == pred.numel() &&
+              scale.numel() >= N, "seq_loss_bwd: shapes");
+  if (valid.defined()) { check_f32(valid, "valid"); TORCH_CHECK(valid.numel() == P, "seq_loss_bwd: valid"); }
+  JR_CHECK_OK(jr_seq_loss_bwd(pred.data_ptr<float>(), gt.data_ptr<float>(),
+                              valid.defined() ? valid.data_ptr<float>() : nullptr, P, N, (float)max_flow,
+                              scale.data_ptr<float>(), grad.data_ptr<float>(), cur_stream()));
+}
+
 // ---------------------------------------------------------------- eager ops
 void conv_op(const TList& t, IList i, double alpha) { run_now(make_conv(t, i, alpha, nullptr)); }
 void corr_op(const TList& t, IList i, double scale) { run_now(make_corr(t, i, scale, nullptr)); }
@@ -734,6 +802,10 @@ void conv_train_op(const TList& t, IList i, double alpha, const TList& tx, IList
   run_now(make_conv(t, i, alpha, nullptr, &tx, &ix));
 }
 void upsample_convex_bwd_op(const TList& t, IList i, double alpha) { run_now(make_upsample_convex_bwd(t, i, alpha, nullptr)); }
+void norm_bwd_op(const TList& t, IList i, double eps) {
+  std::vector<at::Tensor> keep;
+  run_now(make_norm_bwd(t, i, eps, &keep));
+}
 void flow_gather_bwd_op(const TList& t, IList i) { run_now(make_flow_gather_bwd(t, i, nullptr)); }
 void upsample_bilinear_bwd_op(const TList& t, IList i) { run_now(make_upsample_bilinear_bwd(t, i, nullptr)); }
 
@@ -817,6 +889,7 @@ class Plan : public torch::CustomClassHolder {
   void add_upsample_convex_bwd(TList t, IList i, double alpha) {
     push(make_upsample_convex_bwd(t, i, alpha, &keep_), "upsample_convex_bwd");
   }
+  void add_norm_bwd(TList t, IList i, double eps) { push(make_norm_bwd(t, i, eps, &keep_), "norm_bwd"); }
   void add_flow_gather_bwd(TList t, IList i) { push(make_flow_gather_bwd(t, i, &keep_), "flow_gather_bwd"); }
   void add_upsample_bilinear_bwd(TList t, IList i) { push(make_upsample_bilinear_bwd(t, i, &keep_), "upsample_bilinear_bwd"); }
   void add_lookup_bwd(TList t, IList i) { push(make_lookup_bwd(t, i, &keep_), "lookup_bwd"); }
@@ -1042,7 +1115,11 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("conv_train(Tensor?[] t, int[] i, float alpha, Tensor?[] tx, int[] ix) -> ()", &jr::conv_train_op);
   m.def("upsample_convex_bwd(Tensor?[] t, int[] i, float alpha) -> ()", &jr::upsample_convex_bwd_op);
   m.def("flow_gather_bwd(Tensor?[] t, int[] i) -> ()", &jr::flow_gather_bwd_op);
+  m.def("norm_bwd(Tensor?[] t, int[] i, float eps) -> ()", &jr::norm_bwd_op);
   m.def("upsample_bilinear_bwd(Tensor?[] t, int[] i) -> ()", &jr::upsample_bilinear_bwd_op);
+  m.def("seq_loss(Tensor?[] t, int[] i, float max_flow) -> ()", &jr::seq_loss_op);
+  m.def("seq_loss_blocks(int P) -> int", &jr::seq_loss_blocks_op);
+  m.def("seq_loss_bwd(Tensor?[] t, int[] i, float max_flow) -> ()", &jr::seq_loss_bwd_op);
   m.class_<jr::Plan>("Plan")
       .def(torch::init<>())
       .def("set_segment", &jr::Plan::set_segment)
@@ -1069,6 +1146,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_conv_train", &jr::Plan::add_conv_train)
       .def("add_upsample_convex_bwd", &jr::Plan::add_upsample_convex_bwd)
       .def("add_flow_gather_bwd", &jr::Plan::add_flow_gather_bwd)
+      .def("add_norm_bwd", &jr::Plan::add_norm_bwd)
       .def("add_upsample_bilinear_bwd", &jr::Plan::add_upsample_bilinear_bwd)
       .def("add_lookup_bwd", &jr::Plan::add_lookup_bwd)
       .def("add_im2col", &jr::Plan::add_im2col)

@@ -89,6 +89,48 @@ def _pad_last(k: torch.Tensor, n: int) -> torch.Tensor:
 _CFG_CACHE: Dict[tuple, int] = {}
 
 
+def record_conv(plan, spec, x, N, H, W, y, *, tx=None, ix=None, extra=None, **kw):
+    """Append one conv to ``plan`` (``plan=None``: launch it now) with its tile
+    config autotuned once per problem signature.  ``extra`` = [OH, OW, log2
+    dil_h, log2 dil_w] selects the input-dilation (strided data-gradient) mode.
+    Timing runs the same problem with the plain epilogue into a scratch
+    output, so epilogues that accumulate into their buffers are never re-run."""
+    x_coff = kw.get("x_coff", 0)
+    OH, OW = (extra[0], extra[1]) if extra else spec.out_hw(H, W)
+    key = ("train", N, H, W, OH, OW, spec.kh, spec.kw, spec.sh, spec.sw, spec.ph, spec.pw, spec.cin8, spec.cout,
+           x.shape[-1], tuple(extra) if extra else None, str(x.device))
+    cfg = _CFG_CACHE.get(key)
+    ops = nat.ops()
+    if cfg is None:
+        scratch = torch.empty(N * OH * OW, round_up(spec.cout, 8), dtype=BF16, device=x.device)
+        best = None
+        for c in nat.TUNE_CFGS:
+            t, i, a = nat.conv_args(spec, x, N, H, W, scratch, x_coff=x_coff, cfg=c)
+            if extra:
+                i = i + list(extra)
+            ops.conv(t, i, a)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(3):
+                ops.conv(t, i, a)
+            e1.record()
+            e1.synchronize()
+            el = e0.elapsed_time(e1)
+            if best is None or el < best[0]:
+                best = (el, c)
+        cfg = best[1]
+        _CFG_CACHE[key] = cfg
+    t, i, a = nat.conv_args(spec, x, N, H, W, y, cfg=cfg, **kw)
+    if extra:
+        if len(i) > 22:
+            raise ValueError("input dilation with a bias map / iteration stride is not supported")
+        i = i + list(extra)
+    if tx is None:
+        (plan.add_conv if plan is not None else ops.conv)(t, i, a)
+    else:
+        (plan.add_conv_train if plan is not None else ops.conv_train)(t, i, a, tx, ix)
+
+
 def supported(model) -> bool:
     """Whether :class:`FusedLoop` can lower ``model``'s refinement loop."""
     ub = model.update_block
@@ -184,8 +226,9 @@ class FusedLoop:
             return torch.zeros(shape, dtype=dtype, device=dev)
 
         self.ctx_in = z(M, self.ctx_cs)
-        self.fm1 = z(self.B, h, w, self.fmap_ch)
-        self.fm2 = z(self.B, h, w, self.fmap_ch)
+        self.fm = z(2 * self.B, h, w, self.fmap_ch)   # feature-encoder output [img1 batch | img2 batch]
+        self.fm1, self.fm2 = self.fm[: self.B], self.fm[self.B:]
+        self.ctx_raw = z(self.B, h, w, self.hd + self.ctx_ch)  # context-encoder output (full-model path)
         self.gbias = [z(M, self.gate_cs, dtype=F32) for _ in range(G)]
         # [g][t]: GRU g's inputs at iteration t; hx[0][t + 1] / hf[0][t + 1] = output of the last GRU
         self.hx = z(G, T + 1, M, self.hx_cs)
@@ -340,26 +383,8 @@ class FusedLoop:
             self._fh2_bias.copy_(fb)
 
     # ----------------------------------------------------------- recording
-    def _cfg(self, spec, x, x_coff) -> int:
-        B, h, w = self.B, self.h, self.w
-        key = ("train", self.M, spec.cout, spec.kh, spec.kw, spec.cin8, x.shape[-1], str(self.device))
-        cfg = _CFG_CACHE.get(key)
-        if cfg is None:
-            from ..runtime.engine import _tune
-
-            y = torch.empty(self.M, round_up(spec.cout, 8), dtype=BF16, device=self.device)
-            cfg = _tune(spec, x, B, h, w, y, dict(x_coff=x_coff))
-            _CFG_CACHE[key] = cfg
-        return cfg
-
     def _conv(self, plan, name, x, y, *, x_coff=0, tx=None, ix=None, **kw):
-        spec = self._specs[name]
-        cfg = self._cfg(spec, x, x_coff)
-        t, i, a = nat.conv_args(spec, x, self.B, self.h, self.w, y, x_coff=x_coff, cfg=cfg, **kw)
-        if tx is None:
-            plan.add_conv(t, i, a)
-        else:
-            plan.add_conv_train(t, i, a, tx, ix)
+        record_conv(plan, self._specs[name], x, self.B, self.h, self.w, y, x_coff=x_coff, tx=tx, ix=ix, **kw)
 
     def _bconv(self, plan, name, x, *, x_coff=0, split=0, s0=None, s1=None, **gru):
         """Data-gradient conv with the EPI_BWD epilogue."""
@@ -479,10 +504,14 @@ class FusedLoop:
         """fmap1 / fmap2: feature-encoder outputs (B, h, w, C); ctx_raw:
         context-encoder output (B, h, w, hidden + ctx).  Returns the
         (T, B, H, W, 2) upsampled flows of every iteration."""
-        hd = self.hd
-        self._pack()
         self.fm1.copy_(fmap1.detach())
         self.fm2.copy_(fmap2.detach())
+        return self.forward_prepared(ctx_raw)
+
+    def forward_prepared(self, ctx_raw: torch.Tensor) -> torch.Tensor:
+        """As :meth:`forward` with the feature maps already in :attr:`fm`."""
+        hd = self.hd
+        self._pack()
         c = ctx_raw.detach().reshape(self.M, -1).float()
         h0 = torch.tanh(c[:, :hd])
         self.hf[0, 0].copy_(h0)
@@ -563,10 +592,7 @@ class FusedLoop:
                 put(conv.bias, db[j * hd:(j + 1) * hd])
             # context data gradient of this GRU's gates (accumulated over the GRUs)
             tx, ix = _tx(s1=Seg(gin=dctx if g > 0 else None, out=dctx))
-            spec = self._specs[f"gCT{g}"]
-            t_, i_, a_ = nat.conv_args(spec, Sb, self.B, self.h, self.w, dctx, epi=EPI_BWD, hidden=0,
-                                       cfg=self._cfg(spec, Sb, 0))
-            nat.ops().conv_train(t_, i_, a_, tx, ix)
+            self._conv(None, f"gCT{g}", Sb, dctx, tx=tx, ix=ix, epi=EPI_BWD, hidden=0)
         # flow head / mask predictor
         dfm = self.dfmm.reshape(-1, self.fm_cs)
         hx_next = self.hx[0, 1:T + 1]
@@ -615,38 +641,114 @@ class FusedRefine(torch.autograd.Function):
         return (None, g1.to(d1), g2.to(d2), dctx.to(d3)) + tuple(pgrads)
 
 
-_LOOPS: Dict[tuple, FusedLoop] = {}
+class FusedModel:
+    """The whole RAFT training forward / backward as native plans: the
+    feature and context encoders (:class:`~jax_raft_amd.train.fused_encoder.EncoderTrain`)
+    write straight into the loop's feature-map / context buffers, and the
+    loop's input gradients are handed back to the encoders' backward plans
+    without leaving the device or the persistent buffers."""
+
+    def __init__(self, model, B: int, H: int, W: int, T: int, device, use_graph: bool = True):
+        from .fused_encoder import EncoderTrain
+
+        self.model = model
+        self.B, self.H, self.W = B, H, W
+        self.loop = FusedLoop(model, B, H, W, T, device, use_graph)
+        dev = self.loop.device
+        self.img1 = torch.zeros(B, H, W, 3, device=dev)
+        self.img2 = torch.zeros(B, H, W, 3, device=dev)
+        self.x0 = torch.zeros(2 * B, H, W, 8, dtype=BF16, device=dev)
+        self.fe = EncoderTrain(model.feature_encoder, self.x0, self.loop.fm, record_conv, use_graph)
+        self.ce = EncoderTrain(model.context_encoder, self.x0[:B], self.loop.ctx_raw, record_conv, use_graph)
+        self.params = [p for p in model.parameters()]
+
+    def forward(self, image1, image2, train: bool) -> torch.Tensor:
+        self.img1.copy_(image1)
+        self.img2.copy_(image2)
+        nat.ops().prep([self.img1, self.img2, self.x0], [self.B, self.H, self.W])
+        self.fe.forward(update_stats=train)
+        self.ce.forward(update_stats=train)
+        return self.loop.forward_prepared(self.loop.ctx_raw)
+
+    def backward(self, gout, gen: int):
+        B = self.B
+        g1, g2, dctx, pgrads = self.loop.backward(gout, gen)
+        self.fe.dy_out[:B].copy_(g1)
+        self.fe.dy_out[B:].copy_(g2)
+        self.ce.dy_out.copy_(dctx)
+        grads = {id(p): g for p, g in zip(self.loop.params, pgrads)}
+        grads.update(self.fe.backward())
+        grads.update(self.ce.backward())
+        return [grads.get(id(p)) for p in self.params]
+
+
+class FusedRAFT(torch.autograd.Function):
+    """Autograd node of the whole model (encoders + pyramid + loop); inputs
+    the images (no gradient) and every model parameter."""
+
+    @staticmethod
+    def forward(ctx, fm: FusedModel, image1, image2, train: bool, *params):
+        out = fm.forward(image1, image2, train)
+        ctx.fm, ctx.gen = fm, fm.loop.gen
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        grads = ctx.fm.backward(gout.contiguous(), ctx.gen)
+        return (None, None, None, None) + tuple(grads)
+
+
+_LOOPS: Dict[tuple, object] = {}
 
 
 def enabled() -> bool:
     return os.environ.get("JR_FUSED_TRAIN", "1") != "0"
 
 
+def full_model_ok(model, train: bool) -> bool:
+    """The whole-model node needs train-mode (batch-statistics) BatchNorm without
+    cross-rank synchronisation; otherwise only the loop is fused."""
+    from ..models.layers import BatchNorm
+
+    bns = [m for m in model.modules() if isinstance(m, BatchNorm)]
+    if bns and (not train or any(b.sync_group is not None for b in bns)):
+        return False
+    return os.environ.get("JR_FUSED_ENCODERS", "1") != "0"
+
+
+def _cached(kind, model, B, H, W, T, device):
+    key = (kind, id(model), B, H, W, T, str(device))
+    obj = _LOOPS.get(key)
+    if obj is None or obj.model is not model:
+        for k in [k for k, v in _LOOPS.items() if k[1] == id(model)]:
+            del _LOOPS[k]   # one plan set per model: drop other shapes / kinds
+        g = os.environ.get("JR_FUSED_GRAPH", "1") != "0"
+        obj = (FusedModel if kind == "model" else FusedLoop)(model, B, H, W, T, device, use_graph=g)
+        _LOOPS[key] = obj
+    return obj
+
+
 def get_loop(model, B, H, W, T, device) -> FusedLoop:
-    key = (id(model), B, H, W, T, str(device))
-    lp = _LOOPS.get(key)
-    if lp is None or lp.model is not model:
-        # one loop per model and shape: drop stale entries of other shapes of this model
-        for k in [k for k, v in _LOOPS.items() if k[0] == id(model)]:
-            del _LOOPS[k]
-        lp = FusedLoop(model, B, H, W, T, device, use_graph=os.environ.get("JR_FUSED_GRAPH", "1") != "0")
-        _LOOPS[key] = lp
-    return lp
+    return _cached("loop", model, B, H, W, T, device)
 
 
 def forward_train(model, image1, image2, train: bool, num_flow_updates: int):
-    """Training forward with the fused loop: the encoders run on the native
-    autograd path, the correlation pyramid + refinement loop is one
-    :class:`FusedRefine` node."""
+    """Training forward on the fused native path: the whole model as one
+    :class:`FusedRAFT` node when :func:`full_model_ok`, else the encoders on
+    the native autograd Functions and the correlation pyramid + refinement
+    loop as one :class:`FusedRefine` node."""
     B, H, W, _ = image1.shape
-    fmaps = model.feature_encoder(torch.cat([image1, image2], dim=0), train)
-    fmap1, fmap2 = torch.chunk(fmaps, 2, dim=0)
-    assert tuple(fmap1.shape[1:3]) == (H // 8, W // 8), "The feature encoder should downsample H and W by 8"
     h, w = H // 8, W // 8
     min_sz = 2 * (2 ** (model.corr_block.num_levels - 1))
     assert h >= min_sz and w >= min_sz, (
         "Feature maps are too small to be down-sampled by the correlation pyramid. "
         f"H and W of feature maps should be at least {min_sz}; got: {(h, w)}.")
+    if full_model_ok(model, train):
+        fm = _cached("model", model, B, H, W, num_flow_updates, image1.device)
+        return FusedRAFT.apply(fm, image1.float().contiguous(), image2.float().contiguous(), bool(train), *fm.params)
+    fmaps = model.feature_encoder(torch.cat([image1, image2], dim=0), train)
+    fmap1, fmap2 = torch.chunk(fmaps, 2, dim=0)
+    assert tuple(fmap1.shape[1:3]) == (h, w), "The feature encoder should downsample H and W by 8"
     ctx_out = model.context_encoder(image1, train)
     assert tuple(ctx_out.shape[1:3]) == (h, w), "The context encoder should downsample H and W by 8"
     loop = get_loop(model, B, H, W, num_flow_updates, image1.device)

@@ -1,0 +1,315 @@
+"""Native training forward / backward of a RAFT feature or context encoder
+(``FeatureEncoder``, reference ``jax_raft/model.py:219-257`` with the
+Residual / Bottleneck blocks of ``model.py:162-216``).
+
+Every conv unit is lowered as ``conv (implicit-GEMM MFMA, bias) -> per-(n, c)
+statistics -> normalise (+ relu) [+ residual (+ its norm)] -> relu`` -- the
+inference engine's encoder lowering (runtime/engine.py:_encoder) with
+InstanceNorm (``model.py:706-707``), train-mode BatchNorm with batch
+statistics and affine parameters (``model.py:147,157``) or no norm -- and
+every raw conv output, statistic and activation is kept for the backward.
+
+The backward walks the blocks in reverse: the norm backward
+(``train.hip:jr_norm_bwd``: ReLU / residual-output masks, the closed-form
+instance / batch-norm adjoint, the residual-branch gradient) and each conv's
+data gradient as the implicit-GEMM kernel over flipped weights (input
+dilation for the strided convs, the residual gradient added in the fp32
+epilogue of the block's first conv).  Weight gradients are one im2col GEMM
+per conv after the plan; BatchNorm's scale / bias gradients are the norm
+backward's per-channel reductions.
+
+Forward and backward are native :class:`Plan` s recorded once per shape and
+replayed (as hipGraphs by default).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+
+from ..models.layers import NORM_BATCH, NORM_INSTANCE, BottleneckBlock, FeatureEncoder
+from ..ops import native as nat
+from ..ops.native import ACT_NONE, round_up
+
+BF16, F32 = torch.bfloat16, torch.float32
+EPI_BWD = 5
+EPS = 1e-5
+
+
+def _log2(s: int) -> int:
+    if s not in (1, 2, 4, 8):
+        raise NotImplementedError(f"stride {s}")
+    return int(math.log2(s))
+
+
+class _Unit:
+    """One conv -> norm (-> relu) unit and its training buffers."""
+
+    def __init__(self, conv, norm_mod, mode: int, x: torch.Tensor, N: int, H: int, W: int):
+        self.conv, self.norm_mod, self.mode = conv, norm_mod, mode
+        self.x, self.N, self.H, self.W = x, N, H, W
+        kh, kw = conv.kernel_size
+        self.OH = (H + 2 * conv.padding[0] - kh) // conv.stride[0] + 1
+        self.OW = (W + 2 * conv.padding[1] - kw) // conv.stride[1] + 1
+        self.cout = conv.cout
+        self.cin8 = x.shape[-1]
+
+
+class EncoderTrain:
+    """Training plans of one :class:`FeatureEncoder` over ``N`` images.
+
+    ``x``: persistent bf16 input [N, H, W, cin8]; ``y_out``: bf16 [N, h, w, C]
+    the final 1x1 conv writes; ``dy_out``: bf16 gradient of ``y_out`` (filled by
+    the caller before :meth:`backward`)."""
+
+    def __init__(self, enc: FeatureEncoder, x: torch.Tensor, y_out: torch.Tensor, tuner, use_graph: bool = True):
+        self.enc = enc
+        self.x = x
+        self.y_out = y_out
+        self.dy_out = torch.zeros_like(y_out)
+        self.device = x.device
+        self.tuner = tuner
+        self.use_graph = use_graph
+        self.mode = {NORM_INSTANCE: 1, NORM_BATCH: 2, None: 0}[enc.norm_kind]
+        self._specs: Dict[int, nat.ConvSpec] = {}
+        self._tspecs: Dict[int, nat.ConvSpec] = {}
+        self.units: List[_Unit] = []
+        self.blocks = []
+        self.bufs: List[torch.Tensor] = []
+        self.plan_f = nat.new_plan()
+        self.plan_b = nat.new_plan()
+        for P in (self.plan_f, self.plan_b):
+            P.set_segment(0)
+            P.set_lane(0)
+        self._pack()
+        self._record_fwd()
+        self._record_bwd()
+
+    # ------------------------------------------------------------ helpers
+    def _z(self, *shape, dtype=BF16):
+        t = torch.zeros(shape, dtype=dtype, device=self.device)
+        self.bufs.append(t)
+        return t
+
+    def _convs(self):
+        enc = self.enc
+        out = [enc.convnormrelu.layers_0]
+        for li in (1, 2, 3):
+            layer = getattr(enc, f"layer{li}")
+            for bi in range(layer.n):
+                blk = getattr(layer, f"layers_{bi}")
+                names = ["convnormrelu1", "convnormrelu2"] + (["convnormrelu3"] if isinstance(blk, BottleneckBlock) else [])
+                if blk.stride != (1, 1):
+                    names.append("downsample")
+                out += [getattr(blk, n).layers_0 for n in names]
+        out.append(enc.conv)
+        return out
+
+    def _pack(self):
+        """(Re)pack forward and data-gradient weights in place."""
+        for c in self._convs():
+            k, b = c.kernel.detach().float(), c.bias.detach().float()
+            kh, kw, cin, cout = k.shape
+            cin8 = 8 if c is self.enc.convnormrelu.layers_0 else round_up(cin, 8)
+            kt = torch.flip(k, dims=(0, 1)).permute(0, 1, 3, 2)
+            if cin8 != cin:
+                kt = torch.cat([kt, kt.new_zeros(kh, kw, cout, cin8 - cin)], dim=3)
+            sp = self._specs.get(id(c))
+            if sp is None:
+                self._specs[id(c)] = nat.make_spec(k, b, c.stride, c.padding, cin8=cin8, device=self.device)
+                self._tspecs[id(c)] = nat.make_spec(kt, torch.zeros(cin8, device=self.device), (1, 1),
+                                                    (kh - 1 - c.padding[0], kw - 1 - c.padding[1]),
+                                                    cin8=round_up(cout, 8), device=self.device)
+            else:
+                nat.pack_weight(k, sp.cin8, out=sp.w)
+                sp.b.copy_(b)
+                tp = self._tspecs[id(c)]
+                nat.pack_weight(kt, tp.cin8, out=tp.w)
+
+    def _affine(self, unit):
+        if self.mode == 2:
+            bn = unit.norm_mod
+            return bn.scale.data, bn.bias.data
+        return None, None
+
+    # ------------------------------------------------------------ forward
+    def _conv_unit(self, conv, norm_mod, x, N, H, W) -> _Unit:
+        u = _Unit(conv, norm_mod, self.mode, x, N, H, W)
+        u.y = self._z(N, u.OH, u.OW, u.cout)
+        sp = self._specs[id(conv)]
+        self.tuner(self.plan_f, sp, x, N, H, W, u.y, act=ACT_NONE)
+        if self.mode:
+            u.st = self._z(N, u.cout, 2, dtype=F32)
+            self.plan_f.add_stats([u.y, u.st], [N, u.OH * u.OW, u.cout])
+        else:
+            u.st = None
+        self.units.append(u)
+        return u
+
+    def _norm_act(self, u: _Unit, relu: int, res=None, ru: Optional[_Unit] = None) -> torch.Tensor:
+        a = self._z(u.N, u.OH, u.OW, u.cout)
+        g, b = self._affine(u)
+        if ru is not None:
+            gr, br = self._affine(ru)
+            self.plan_f.add_norm_act([u.y, u.st, g, b, ru.y, ru.st, gr, br, a],
+                                     [self.mode, self.mode, u.N, u.OH * u.OW, u.cout, relu], EPS)
+        else:
+            self.plan_f.add_norm_act([u.y, u.st, g, b, res, None, None, None, a],
+                                     [self.mode, 0, u.N, u.OH * u.OW, u.cout, relu], EPS)
+        return a
+
+    def _record_fwd(self):
+        enc = self.enc
+        N, H, W = self.x.shape[:3]
+        stem = self._conv_unit(enc.convnormrelu.layers_0, getattr(enc.convnormrelu, "layers_1", None), self.x, N, H, W)
+        x = self._norm_act(stem, relu=1)
+        stem.a = x
+        self.stem = stem
+        H, W = stem.OH, stem.OW
+        for li in (1, 2, 3):
+            layer = getattr(enc, f"layer{li}")
+            for bi in range(layer.n):
+                blk = getattr(layer, f"layers_{bi}")
+                names = ["convnormrelu1", "convnormrelu2"] + (["convnormrelu3"] if isinstance(blk, BottleneckBlock) else [])
+                units = []
+                h_in, w_in, xin = H, W, x
+                y = x
+                hh, ww = H, W
+                for j, nm in enumerate(names):
+                    cna = getattr(blk, nm)
+                    u = self._conv_unit(cna.layers_0, getattr(cna, "layers_1", None), y, N, hh, ww)
+                    units.append(u)
+                    hh, ww = u.OH, u.OW
+                    if j + 1 < len(names):
+                        y = self._norm_act(u, relu=1)
+                        u.a = y
+                ds = None
+                if blk.stride != (1, 1):
+                    cna = blk.downsample
+                    ds = self._conv_unit(cna.layers_0, getattr(cna, "layers_1", None), xin, N, h_in, w_in)
+                last = units[-1]
+                if ds is not None:
+                    out = self._norm_act(last, relu=3, ru=ds)
+                else:
+                    out = self._norm_act(last, relu=3, res=xin)
+                last.a = out
+                self.blocks.append(dict(units=units, ds=ds, x=xin, out=out, H=h_in, W=w_in))
+                x, H, W = out, hh, ww
+        self.tuner(self.plan_f, self._specs[id(enc.conv)], x, N, H, W, self.y_out, act=ACT_NONE)
+        self.final_x = x
+
+    # ----------------------------------------------------------- backward
+    def _dgrad(self, u: _Unit, dy: torch.Tensor, out: torch.Tensor, gin: Optional[torch.Tensor] = None):
+        """Data gradient of unit u's conv: dy [N, OH, OW, cout] -> out [N, H, W, cin8] (bf16 or
+        fp32), gin fp32 [N, H, W, cin8] added in the epilogue."""
+        from .fused import Seg, _tx
+
+        tp = self._tspecs[id(u.conv)]
+        s = u.conv.stride
+        tx, ix = _tx(s1=Seg(gin=gin, out=out))
+        extra = None if s == (1, 1) else [u.H, u.W, _log2(s[0]), _log2(s[1])]
+        self.tuner(self.plan_b, tp, dy, u.N, u.OH, u.OW, out, tx=tx, ix=ix, epi=EPI_BWD, hidden=0, extra=extra)
+
+    def _norm_bwd(self, u: _Unit, gout, dy, om=None, relu=1, gres=None, norm_mod=None):
+        g, b = self._affine(u)
+        if self.mode:
+            u.red = self._z(u.N, u.cout, 2, dtype=F32)
+        else:
+            u.red = None
+        part = None  # the plan op allocates (and keeps) its reduction workspace
+        self.plan_b.add_norm_bwd([gout, om, u.y, u.st, g, b, u.red, part, dy, gres],
+                                 [self.mode, relu, u.N, u.OH * u.OW, u.cout], EPS)
+
+    def _record_bwd(self):
+        enc = self.enc
+        N = self.x.shape[0]
+        last_blk = self.blocks[-1]
+        # final 1x1 conv: dL/d(last block output)
+        fin = _Unit(enc.conv, None, 0, self.final_x, N, self.final_x.shape[1], self.final_x.shape[2])
+        self.fin = fin
+        fin.dy = self.dy_out
+        dout = self._z(*last_blk["out"].shape)
+        self._dgrad(fin, self.dy_out, dout)
+        for bi in reversed(range(len(self.blocks))):
+            blk = self.blocks[bi]
+            units, ds = blk["units"], blk["ds"]
+            last = units[-1]
+            last.dy = self._z(*last.y.shape)
+            res_g = None
+            if ds is None:
+                res_g = self._z(*blk["x"].shape, dtype=F32)  # dL/dx through the identity shortcut
+                self._norm_bwd(last, dout, last.dy, om=blk["out"], relu=1, gres=res_g)
+            else:
+                self._norm_bwd(last, dout, last.dy, om=blk["out"], relu=1)
+                ds.dy = self._z(*ds.y.shape)
+                self._norm_bwd(ds, dout, ds.dy, om=blk["out"], relu=0)
+                res_g = self._z(*blk["x"].shape, dtype=F32)
+                self._dgrad(ds, ds.dy, res_g)
+            # chain back through the block's units
+            g = last.dy
+            for j in reversed(range(len(units))):
+                u = units[j]
+                if j > 0:
+                    da = self._z(*units[j - 1].a.shape)
+                    self._dgrad(u, g, da)
+                    p = units[j - 1]
+                    p.dy = self._z(*p.y.shape)
+                    self._norm_bwd(p, da, p.dy, relu=1)
+                    g = p.dy
+                else:
+                    dx = self._z(*blk["x"].shape)
+                    self._dgrad(u, g, dx, gin=res_g)
+                    dout = dx
+        # stem: dL/d(stem activation) = dout of the first block's input
+        self.stem.dy = self._z(*self.stem.y.shape)
+        self._norm_bwd(self.stem, dout, self.stem.dy, relu=1)
+
+    # ---------------------------------------------------------------- run
+    def _run(self, plan):
+        if self.use_graph:
+            if plan.captured_iters() != 0:
+                plan.capture(0)
+            plan.replay()
+        else:
+            plan.run(0)
+
+    def forward(self, update_stats: bool, momentum: float = 0.99):
+        self._pack()
+        self._run(self.plan_f)
+        if update_stats and self.mode == 2:
+            with torch.no_grad():
+                for u in self.units:
+                    bn = u.norm_mod
+                    s = u.st.sum(0)  # (C, 2)
+                    cnt = float(u.N * u.OH * u.OW)
+                    m = s[:, 0] / cnt
+                    v = (s[:, 1] / cnt - m * m).clamp_min(0.0)
+                    bn.mean.mul_(bn.momentum).add_((1.0 - bn.momentum) * m)
+                    bn.var.mul_(bn.momentum).add_((1.0 - bn.momentum) * v)
+
+    def backward(self) -> Dict[int, torch.Tensor]:
+        """Runs the backward plan (``dy_out`` must be filled); returns
+        {id(param): grad} for every encoder parameter."""
+        from ..ops.autograd import _wgrad_gemm
+
+        self._run(self.plan_b)
+        grads: Dict[int, torch.Tensor] = {}
+        for u in self.units + [self.fin]:
+            c = u.conv
+            kh, kw, cin, cout = c.kernel.shape
+            sh, sw = c.stride
+            ph, pw = c.padding
+            kpad = round_up(kh * kw * u.cin8, 64)
+            Mt = u.N * u.OH * u.OW
+            col = torch.empty(Mt, kpad, dtype=BF16, device=self.device)
+            nat.ops().im2col([u.x, col], [u.N, u.H, u.W, 0, u.cin8, kh, kw, sh, sw, ph, pw])
+            dy2 = u.dy.reshape(Mt, -1)
+            gw = _wgrad_gemm(dy2, col, cout)
+            grads[id(c.kernel)] = gw[: kh * kw * u.cin8].reshape(kh, kw, u.cin8, cout)[:, :, :cin].contiguous()
+            grads[id(c.bias)] = dy2.sum(0, dtype=F32)
+            if self.mode == 2 and u.norm_mod is not None:
+                r = u.red.sum(0)
+                grads[id(u.norm_mod.scale)] = r[:, 1].contiguous()
+                grads[id(u.norm_mod.bias)] = r[:, 0].contiguous()
+        return grads

@@ -81,26 +81,49 @@ def _run(model, i1, i2, target, iters, fused):
     return out.detach(), {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
 
 
+@pytest.mark.parametrize("encoders", [True, False], ids=["whole-model", "loop-only"])
 @pytest.mark.parametrize("factory", [raft_large, raft_small])
-def test_fused_matches_unfused(factory):
+def test_fused_matches_unfused(factory, encoders, monkeypatch):
+    """Both GPU paths against fp32 CPU autograd of the golden model: the fused
+    gradients are at least as close to the fp32 reference as the unfused
+    path's (two bf16 paths differ from each other by ~the bf16 noise of the
+    early encoder layers, cos ~0.97, so they are not compared directly)."""
+    from jax_raft_amd.train import fused as F
+
+    monkeypatch.setenv("JR_FUSED_ENCODERS", "1" if encoders else "0")
+    F._LOOPS.clear()
     model, i1, i2, target = _setup(factory)
     state = {k: v.clone() for k, v in model.state_dict().items()}
-    out_u, g_u = _run(model, i1, i2, target, 3, fused=False)
+    mc = factory()[0]
+    mc.load_state_dict({k: v.cpu() for k, v in state.items()})
+    mc.train()
+    iters = 3
+    out_r = mc(i1, i2, train=True, num_flow_updates=iters)
+    w = torch.tensor([0.8 ** (iters - k - 1) for k in range(iters)]).view(-1, 1, 1, 1, 1)
+    (w * (out_r - target).abs()).mean().backward()
+    g_r = {n: p.grad for n, p in mc.named_parameters() if p.grad is not None}
+    out_u, g_u = _run(model, i1, i2, target, iters, fused=False)
     model.load_state_dict(state)
-    out_f, g_f = _run(model, i1, i2, target, 3, fused=True)
+    out_f, g_f = _run(model, i1, i2, target, iters, fused=True)
     assert out_f.shape == out_u.shape
-    assert _rel(out_f, out_u) < 2e-2, _rel(out_f, out_u)
-    assert set(g_f) == set(g_u)
-    scale = max(v.norm().item() for v in g_u.values())
-    bad = []
-    for n in g_u:
-        if g_u[n].norm().item() < 1e-4 * scale:
+    ef, eu = _rel(out_f, out_r), _rel(out_u, out_r)
+    assert ef < max(2e-2, 1.5 * eu), (ef, eu)
+    assert set(g_f) == set(g_u) == set(g_r)
+    scale = max(v.norm().item() for v in g_r.values())
+    bad, cfs, cus = [], [], []
+    for n in g_r:
+        if g_r[n].norm().item() < 1e-4 * scale:
             continue  # e.g. biases feeding an InstanceNorm: exactly-zero true gradient, rounding noise
-        c = _cos(g_f[n], g_u[n])
-        r = g_f[n].norm().item() / g_u[n].norm().item()
-        if c < 0.98 or not (0.9 < r < 1.1):
-            bad.append((n, round(c, 4), round(r, 4)))
+        cf, cu = _cos(g_f[n], g_r[n]), _cos(g_u[n], g_r[n])
+        cfs.append(cf)
+        cus.append(cu)
+        r = g_f[n].norm().item() / g_r[n].norm().item()
+        # per parameter within bf16 noise of the unfused path (raft_small's 8-channel
+        # bottleneck convs sit at cos ~0.9 for both paths), and no worse on the median
+        if cf < cu - 0.03 or not (0.85 < r < 1.15):
+            bad.append((n, round(cf, 4), round(cu, 4), round(r, 4)))
     assert not bad, bad
+    assert torch.tensor(cfs).median() >= torch.tensor(cus).median() - 0.005
 
 
 @pytest.mark.parametrize("factory", [raft_large, raft_small])
@@ -158,3 +181,26 @@ def test_fused_repeated_steps_and_guard():
     b.sum().backward()
     with pytest.raises(RuntimeError, match="overwritten"):
         a.sum().backward()
+
+
+@pytest.mark.parametrize("with_valid", [False, True])
+def test_native_sequence_loss(with_valid):
+    from jax_raft_amd.train.loss import sequence_loss, sequence_loss_reference
+
+    torch.manual_seed(11)
+    N, B, H, W = 5, 2, 24, 40
+    preds = torch.randn(N, B, H, W, 2) * 3
+    gt = torch.randn(B, H, W, 2) * 3
+    gt[0, 0, :4] = 500.0  # beyond max_flow: excluded
+    valid = (torch.rand(B, H, W) > 0.3).float() if with_valid else None
+    pr = preds.clone().requires_grad_(True)
+    lr, mr = sequence_loss_reference(pr, gt, valid)
+    lr.backward()
+    pg = preds.cuda().requires_grad_(True)
+    lg, mg = sequence_loss(pg, gt.cuda(), None if valid is None else valid.cuda())
+    lg.backward()
+    torch.cuda.synchronize()
+    assert abs(lg.item() - lr.item()) < 1e-4 * abs(lr.item())
+    for k in mr:
+        assert abs(mg[k].item() - mr[k].item()) < 1e-4, k
+    assert _rel(pg.grad, pr.grad) < 1e-5
