@@ -166,6 +166,19 @@ int jr_norm_bwd_partials(int N, int HW);
 int jr_norm_bwd(const void* gout, const void* om, const void* y, const float* stats, int mode, const float* gamma,
                 const float* beta, int relu, int N, int HW, int C, float eps, float* red, float* partial, void* dy,
                 float* gres, hipStream_t stream);
+// Batched weight packing (training): one rectangular piece of one packed conv weight
+// (bf16 [cout_pad][kpad], rows permuted, ops/native.py:pack_weight) from an fp32 HWIO source
+// [kh][kw][cin_s][cout_s].  For dst output channel co in [co0, co1), tap, input channel ci
+// in [ci0, ci1) (source indices co - co0 + so_co, ci - ci0 + so_ci):
+//   mode 0 forward:       src[tap][ci'][co']
+//   mode 1 data gradient: src[flip(tap)][co'][ci']   (the dst conv's in/out are the source's out/in)
+//   mode 2 flow-head taps: dst (1,1,cin,18), co = 2*tap' + c: src[tap'][ci'][c]
+//   mode 3 bias:          fp32 dst[co] = src[co']
+// All fields 64-bit (the table is built by the host as an int64 array).
+struct PackPiece {
+  int64_t src, dst, kh, kw, cin_s, cout_s, cin8, kpad, co0, co1, ci0, ci1, so_co, so_ci, mode, pad;
+};
+int jr_pack_pieces(const void* table, int n, long max_elems, hipStream_t stream);
 // Sequence loss over N <= 32 predictions pred fp32 [N][P][2] vs gt fp32 [P][2]
 // (valid: optional fp32 [P]): part fp32 [jr_seq_loss_blocks(P)][37] per-block
 // partial sums (0..N-1: sum over valid pixels of |pred_i - gt|_1; 32: EPE sum of

@@ -408,9 +408,60 @@ __global__ __launch_bounds__(256) void norm_bwd_apply_kernel(const bf16* __restr
   }
 }
 
+// ---------------------------------------------------------------------------
+// Weight packing for training: every step the optimizer changes the fp32 HWIO
+// parameters, and every conv of the fused training plans needs its bf16 GEMM
+// A operand ([cout_pad][kpad], K = (tap, cin8), rows permuted in 64-row groups,
+// ops/native.py:pack_weight) -- forward, flipped / transposed data-gradient
+// and flow-head tap layouts.  One launch repacks all of them from a table of
+// rectangular pieces (blockIdx.y = piece), as the first op of the captured
+// forward plan (no per-parameter framework ops).
+// ---------------------------------------------------------------------------
+JR_DEVICE long packed_row(long co) {   // storage row of output channel co (inverse of _row_perm)
+  const long g = co >> 6, j = co & 63;
+  return g * 64 + ((j & 15) >> 2) * 16 + (j >> 4) * 4 + (j & 3);
+}
+
+__global__ __launch_bounds__(256) void pack_pieces_kernel(const PackPiece* __restrict__ pieces) {
+  const PackPiece pc = pieces[blockIdx.y];
+  const float* src = (const float*)pc.src;
+  const long nco = pc.co1 - pc.co0, nci = pc.ci1 - pc.ci0;
+  const long taps = pc.mode == 3 ? 1 : pc.kh * pc.kw;
+  const long total = nco * taps * (pc.mode == 3 ? 1 : nci);
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    if (pc.mode == 3) {  // bias: fp32 dst[co] = src[co - co0 + so_co]
+      ((float*)pc.dst)[pc.co0 + e] = src[e + pc.so_co];
+      continue;
+    }
+    const long ci = pc.ci0 + e % nci;
+    const long r = e / nci;
+    const long tap = r % taps;
+    const long co = pc.co0 + r / taps;
+    const long sco = co - pc.co0 + pc.so_co, sci = ci - pc.ci0 + pc.so_ci;
+    float v;
+    if (pc.mode == 0) {          // forward: W[tap][ci][co]
+      v = src[(tap * pc.cin_s + sci) * pc.cout_s + sco];
+    } else if (pc.mode == 1) {   // data gradient: W[flipped tap][src in = co][src out = ci]
+      const long th = tap / pc.kw, tw = tap % pc.kw;
+      const long ft = (pc.kh - 1 - th) * pc.kw + (pc.kw - 1 - tw);
+      v = src[(ft * pc.cin_s + sco) * pc.cout_s + sci];
+    } else {                     // flow-head taps: dst (1,1,cin,18), co = 2 * src tap + c
+      v = src[((co >> 1) * pc.cin_s + sci) * pc.cout_s + (co & 1)];
+    }
+    ((bf16*)pc.dst)[packed_row(co) * pc.kpad + tap * pc.cin8 + ci] = f2bf(v);
+  }
+}
+
 inline unsigned nblk(long total, int bs) { return (unsigned)((total + bs - 1) / bs); }
 
 }  // namespace
+
+extern "C" int jr_pack_pieces(const void* table, int n, long max_elems, hipStream_t stream) {
+  if (n <= 0) return 0;
+  const unsigned bx = (unsigned)std::min<long>(256, std::max<long>(1, (max_elems + 255) / 256));
+  hipLaunchKernelGGL(pack_pieces_kernel, dim3(bx, n), dim3(256), 0, stream, (const PackPiece*)table);
+  return (int)hipGetLastError();
+}
 
 extern "C" int jr_norm_bwd_partials(int N, int HW) { return N * ((HW + NB_ROWS - 1) / NB_ROWS); }
 

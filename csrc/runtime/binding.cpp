@@ -347,6 +347,19 @@ static Launch make_norm_bwd(const TList& t, const IList& i, double eps, std::vec
   };
 }
 
+// t = [table (int64 [n][16] device), *sources, *destinations (kept alive)], i = [n, max_elems]
+static Launch make_pack(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor tab = opt(t, 0);
+  TORCH_CHECK(i.size() == 2, "pack: expected [n, max_elems]");
+  TORCH_CHECK(tab.defined() && tab.is_cuda() && tab.is_contiguous() && tab.scalar_type() == at::kLong &&
+                  tab.numel() == i[0] * 16, "pack: table must be a contiguous int64 [n][16] GPU tensor");
+  if (keep) for (size_t k = 0; k < t.size(); ++k) { at::Tensor v = opt(t, k); if (v.defined()) keep->push_back(v); }
+  const void* tp = tab.data_ptr();
+  const int n = (int)i[0];
+  const long me = (long)i[1];
+  return [=](hipStream_t s, int) { return jr_pack_pieces(tp, n, me, s); };
+}
+
 // t = [taps, dflow], i = [N, h, w]
 static Launch make_flow_gather_bwd(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
   at::Tensor taps = opt(t, 0), df = opt(t, 1);
@@ -802,6 +815,10 @@ void conv_train_op(const TList& t, IList i, double alpha, const TList& tx, IList
   run_now(make_conv(t, i, alpha, nullptr, &tx, &ix));
 }
 void upsample_convex_bwd_op(const TList& t, IList i, double alpha) { run_now(make_upsample_convex_bwd(t, i, alpha, nullptr)); }
+void pack_op(const TList& t, IList i) {
+  std::vector<at::Tensor> keep;
+  run_now(make_pack(t, i, &keep));
+}
 void norm_bwd_op(const TList& t, IList i, double eps) {
   std::vector<at::Tensor> keep;
   run_now(make_norm_bwd(t, i, eps, &keep));
@@ -889,6 +906,7 @@ class Plan : public torch::CustomClassHolder {
   void add_upsample_convex_bwd(TList t, IList i, double alpha) {
     push(make_upsample_convex_bwd(t, i, alpha, &keep_), "upsample_convex_bwd");
   }
+  void add_pack(TList t, IList i) { push(make_pack(t, i, &keep_), "pack"); }
   void add_norm_bwd(TList t, IList i, double eps) { push(make_norm_bwd(t, i, eps, &keep_), "norm_bwd"); }
   void add_flow_gather_bwd(TList t, IList i) { push(make_flow_gather_bwd(t, i, &keep_), "flow_gather_bwd"); }
   void add_upsample_bilinear_bwd(TList t, IList i) { push(make_upsample_bilinear_bwd(t, i, &keep_), "upsample_bilinear_bwd"); }
@@ -1116,6 +1134,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("upsample_convex_bwd(Tensor?[] t, int[] i, float alpha) -> ()", &jr::upsample_convex_bwd_op);
   m.def("flow_gather_bwd(Tensor?[] t, int[] i) -> ()", &jr::flow_gather_bwd_op);
   m.def("norm_bwd(Tensor?[] t, int[] i, float eps) -> ()", &jr::norm_bwd_op);
+  m.def("pack(Tensor?[] t, int[] i) -> ()", &jr::pack_op);
   m.def("upsample_bilinear_bwd(Tensor?[] t, int[] i) -> ()", &jr::upsample_bilinear_bwd_op);
   m.def("seq_loss(Tensor?[] t, int[] i, float max_flow) -> ()", &jr::seq_loss_op);
   m.def("seq_loss_blocks(int P) -> int", &jr::seq_loss_blocks_op);
@@ -1147,6 +1166,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_upsample_convex_bwd", &jr::Plan::add_upsample_convex_bwd)
       .def("add_flow_gather_bwd", &jr::Plan::add_flow_gather_bwd)
       .def("add_norm_bwd", &jr::Plan::add_norm_bwd)
+      .def("add_pack", &jr::Plan::add_pack)
       .def("add_upsample_bilinear_bwd", &jr::Plan::add_upsample_bilinear_bwd)
       .def("add_lookup_bwd", &jr::Plan::add_lookup_bwd)
       .def("add_im2col", &jr::Plan::add_im2col)

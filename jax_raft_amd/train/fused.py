@@ -89,6 +89,52 @@ def _pad_last(k: torch.Tensor, n: int) -> torch.Tensor:
 _CFG_CACHE: Dict[tuple, int] = {}
 
 
+class Packer:
+    """Table of rectangular weight pieces repacked by ONE native launch
+    (csrc/kernels/train.hip:pack_pieces_kernel) from the fp32 HWIO parameters
+    into the bf16 GEMM layouts of the training plans' conv specs -- recorded as
+    the first op of a forward plan, so a training step repacks every weight the
+    optimizer changed without any per-parameter framework op."""
+
+    def __init__(self):
+        self.rows: List[List[int]] = []
+        self.srcs: List[torch.Tensor] = []
+        self.dsts: List[torch.Tensor] = []
+
+    def _src(self, t: torch.Tensor) -> torch.Tensor:
+        assert t.dtype == F32 and t.is_contiguous() and t.is_cuda, "pack source: contiguous fp32 GPU parameter"
+        self.srcs.append(t)
+        return t
+
+    def piece(self, src, spec, mode: int, co, ci, so_co: int = 0, so_ci: int = 0):
+        """dst output channels co = (co0, co1), input channels ci = (ci0, ci1) of
+        ``spec`` from ``src`` (mode 0 forward, 1 data gradient, 2 flow-head taps)."""
+        src = self._src(src.data)
+        kh, kw = spec.kh, spec.kw
+        self.dsts.append(spec.w)
+        self.rows.append([src.data_ptr(), spec.w.data_ptr(), kh, kw, src.shape[2], src.shape[3], spec.cin8,
+                          spec.w.shape[1], co[0], co[1], ci[0], ci[1], so_co, so_ci, mode, 0])
+
+    def bias(self, src, dst: torch.Tensor, co, so: int = 0):
+        src = self._src(src.data)
+        assert dst.dtype == F32 and dst.is_contiguous()
+        self.dsts.append(dst)
+        self.rows.append([src.data_ptr(), dst.data_ptr(), 1, 1, 1, 1, 1, 1, co[0], co[1], 0, 1, so, 0, 3, 0])
+
+    def stale(self) -> bool:
+        return any(s.data_ptr() != r[0] for s, r in zip(self.srcs, self.rows))
+
+    def record(self, plan):
+        dev = self.dsts[0].device
+        self.table = torch.tensor(self.rows, dtype=torch.int64).to(dev).contiguous()
+        max_el = max(max(1, (r[9] - r[8]) * r[2] * r[3] * (r[11] - r[10])) for r in self.rows)
+        args = ([self.table] + self.srcs + self.dsts, [len(self.rows), max_el])
+        if plan is None:
+            nat.ops().pack(*args)
+        else:
+            plan.add_pack(*args)
+
+
 def record_conv(plan, spec, x, N, H, W, y, *, tx=None, ix=None, extra=None, **kw):
     """Append one conv to ``plan`` (``plan=None``: launch it now) with its tile
     config autotuned once per problem signature.  ``extra`` = [OH, OW, log2
@@ -168,6 +214,7 @@ class FusedLoop:
         self._alloc()
         self._specs: Dict[str, nat.ConvSpec] = {}
         self._pack()
+        self.packer = self._pieces()
         self.plan_f = self._build_fwd()
         self.plan_b = self._build_bwd()
 
@@ -382,6 +429,71 @@ class FusedLoop:
         else:
             self._fh2_bias.copy_(fb)
 
+    def _pieces(self) -> "Packer":
+        """The pack table of every spec (mirrors :meth:`_sources`)."""
+        pk, sp, hd, C = Packer(), self._specs, self.hd, self.ctx_ch
+        me, fh, mp = self.me, self.fh, self.mp
+
+        def fwd(name, c, co=None, ci=None):
+            kh, kw, cin, cout = c.kernel.shape
+            pk.piece(c.kernel, sp[name], 0, co or (0, cout), ci or (0, cin))
+            pk.bias(c.bias, sp[name].b, (0, cout))
+
+        def bwd(name, c):
+            kh, kw, cin, cout = c.kernel.shape
+            pk.piece(c.kernel, sp[name + "T"], 1, (0, cin), (0, cout))
+
+        c1 = me.convcorr1.layers_0
+        fwd("cc1", c1)
+        bwd("cc1", c1)
+        if len(self.cl) == 2:
+            fwd("cc2", me.convcorr2.layers_0)
+            bwd("cc2", me.convcorr2.layers_0)
+        fwd("cf1", me.convflow1.layers_0)
+        fwd("cf2", me.convflow2.layers_0)
+        bwd("cf2", me.convflow2.layers_0)
+        fwd("mc", me.conv.layers_0)
+        bwd("mc", me.conv.layers_0)
+        mot = self.mot_out
+        for g, gru in enumerate(self.grus):
+            for j, c in enumerate((gru.convz, gru.convr)):   # loop part [h | motion] of the z / r gates
+                co = (j * hd, (j + 1) * hd)
+                pk.piece(c.kernel, sp[f"gA{g}"], 0, co, (0, hd))
+                pk.piece(c.kernel, sp[f"gA{g}"], 0, co, (hd, hd + mot), so_ci=hd + C)
+                pk.piece(c.kernel, sp[f"gAT{g}"], 1, (0, hd), co)
+                pk.piece(c.kernel, sp[f"gAT{g}"], 1, (hd, hd + mot), co, so_co=hd + C)
+            q = gru.convq
+            pk.piece(q.kernel, sp[f"gB{g}"], 0, (0, hd), (0, hd))
+            pk.piece(q.kernel, sp[f"gB{g}"], 0, (0, hd), (hd, hd + mot), so_ci=hd + C)
+            pk.piece(q.kernel, sp[f"gBT{g}"], 1, (0, hd), (0, hd))
+            pk.piece(q.kernel, sp[f"gBT{g}"], 1, (hd, hd + mot), (0, hd), so_co=hd + C)
+            for j, c in enumerate((gru.convz, gru.convr, gru.convq)):   # context share + gate biases
+                co = (j * hd, (j + 1) * hd)
+                pk.piece(c.kernel, sp[f"gC{g}"], 0, co, (0, C), so_ci=hd)
+                pk.bias(c.bias, sp[f"gC{g}"].b, co)
+                pk.piece(c.kernel, sp[f"gCT{g}"], 1, (0, C), co, so_co=hd)
+        if self.has_mask:
+            mr = mp.convrelu.layers_0
+            fh_, mh = self.fh_hidden, self.mask_hidden
+            pk.piece(fh.conv1.kernel, sp["fh1"], 0, (0, fh_), (0, hd))
+            pk.piece(mr.kernel, sp["fh1"], 0, (fh_, fh_ + mh), (0, hd))
+            pk.bias(fh.conv1.bias, sp["fh1"].b, (0, fh_))
+            pk.bias(mr.bias, sp["fh1"].b, (fh_, fh_ + mh))
+            pk.piece(fh.conv1.kernel, sp["fh1T"], 1, (0, hd), (0, fh_))
+            pk.piece(mr.kernel, sp["fh1T"], 1, (0, hd), (fh_, fh_ + mh))
+            fwd("mask", mp.conv)
+            pk.piece(mp.conv.kernel, sp["maskT"], 1, (0, mh), (0, 576))
+        else:
+            fwd("fh1", fh.conv1)
+            pk.piece(fh.conv1.kernel, sp["fh1T"], 1, (0, hd), (0, self.fh_hidden))
+        pk.piece(fh.conv2.kernel, sp["fh2t"], 2, (0, 18), (0, self.fh_hidden))
+        pk.piece(fh.conv2.kernel, sp["fh2T"], 1, (0, self.fh_hidden), (0, 2))
+        pk.bias(fh.conv2.bias, self._fh2_bias, (0, 2))
+        return pk
+
+    def stale(self) -> bool:
+        return self.packer.stale()
+
     # ----------------------------------------------------------- recording
     def _conv(self, plan, name, x, y, *, x_coff=0, tx=None, ix=None, **kw):
         record_conv(plan, self._specs[name], x, self.B, self.h, self.w, y, x_coff=x_coff, tx=tx, ix=ix, **kw)
@@ -398,6 +510,7 @@ class FusedLoop:
         P.set_lane(0)
         T, G, hd, B, h, w = self.T, self.G, self.hd, self.B, self.h, self.w
         cl, fl = self.cl, self.fl
+        self.packer.record(P)   # this step's weights -> every spec (forward and data-gradient layouts)
         P.add_corr([self.fm1, self.fm2] + self.levels + [None] * (4 - self.L), [B, h, w, self.fmap_ch, self.L],
                    1.0 / float(self.fmap_ch) ** 0.5)
         for g in range(G):  # loop-invariant context share of every gate (+ biases), fp32
@@ -511,7 +624,6 @@ class FusedLoop:
     def forward_prepared(self, ctx_raw: torch.Tensor) -> torch.Tensor:
         """As :meth:`forward` with the feature maps already in :attr:`fm`."""
         hd = self.hd
-        self._pack()
         c = ctx_raw.detach().reshape(self.M, -1).float()
         h0 = torch.tanh(c[:, :hd])
         self.hf[0, 0].copy_(h0)
@@ -662,6 +774,10 @@ class FusedModel:
         self.ce = EncoderTrain(model.context_encoder, self.x0[:B], self.loop.ctx_raw, record_conv, use_graph)
         self.params = [p for p in model.parameters()]
 
+    def stale(self) -> bool:
+        """Parameters re-allocated (e.g. moved) since the plans were recorded."""
+        return self.loop.stale() or self.fe.packer.stale() or self.ce.packer.stale()
+
     def forward(self, image1, image2, train: bool) -> torch.Tensor:
         self.img1.copy_(image1)
         self.img2.copy_(image2)
@@ -719,7 +835,7 @@ def full_model_ok(model, train: bool) -> bool:
 def _cached(kind, model, B, H, W, T, device):
     key = (kind, id(model), B, H, W, T, str(device))
     obj = _LOOPS.get(key)
-    if obj is None or obj.model is not model:
+    if obj is None or obj.model is not model or obj.stale():
         for k in [k for k, v in _LOOPS.items() if k[1] == id(model)]:
             del _LOOPS[k]   # one plan set per model: drop other shapes / kinds
         g = os.environ.get("JR_FUSED_GRAPH", "1") != "0"

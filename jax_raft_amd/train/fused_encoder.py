@@ -83,6 +83,8 @@ class EncoderTrain:
             P.set_segment(0)
             P.set_lane(0)
         self._pack()
+        self.packer = self._pieces()
+        self.packer.record(self.plan_f)   # first op of the forward plan: repack this step's weights
         self._record_fwd()
         self._record_bwd()
 
@@ -126,6 +128,17 @@ class EncoderTrain:
                 sp.b.copy_(b)
                 tp = self._tspecs[id(c)]
                 nat.pack_weight(kt, tp.cin8, out=tp.w)
+
+    def _pieces(self):
+        from .fused import Packer
+
+        pk = Packer()
+        for c in self._convs():
+            kh, kw, cin, cout = c.kernel.shape
+            pk.piece(c.kernel, self._specs[id(c)], 0, (0, cout), (0, cin))
+            pk.bias(c.bias, self._specs[id(c)].b, (0, cout))
+            pk.piece(c.kernel, self._tspecs[id(c)], 1, (0, cin), (0, cout))
+        return pk
 
     def _affine(self, unit):
         if self.mode == 2:
@@ -275,7 +288,6 @@ class EncoderTrain:
             plan.run(0)
 
     def forward(self, update_stats: bool, momentum: float = 0.99):
-        self._pack()
         self._run(self.plan_f)
         if update_stats and self.mode == 2:
             with torch.no_grad():

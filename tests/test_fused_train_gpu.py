@@ -204,3 +204,32 @@ def test_native_sequence_loss(with_valid):
     for k in mr:
         assert abs(mg[k].item() - mr[k].item()) < 1e-4, k
     assert _rel(pg.grad, pr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("factory", [raft_large, raft_small])
+def test_native_pack_table_matches_python_packing(factory):
+    """The one-launch weight repack of the training plans reproduces the
+    PyTorch packing (ops/native.py:pack_weight of the flipped / sliced /
+    concatenated kernels) of every forward, data-gradient and tap spec."""
+    from jax_raft_amd.train.fused import FusedModel
+
+    torch.manual_seed(13)
+    model, _ = factory()
+    model = model.cuda().train()
+    fm = FusedModel(model, 1, 128, 128, 2, "cuda", use_graph=False)
+    specs = list(fm.loop._specs.items())
+    for tag, enc in (("fe", fm.fe), ("ce", fm.ce)):
+        specs += [(f"{tag}{k}", v) for k, v in enc._specs.items()] + [(f"{tag}T{k}", v) for k, v in enc._tspecs.items()]
+    want = {n: (s.w.clone(), s.b.clone()) for n, s in specs}
+    fb = fm.loop._fh2_bias.clone()
+    for n, s in specs:
+        s.w.zero_()
+        s.b.zero_()
+    fm.loop._fh2_bias.zero_()
+    for pk in (fm.loop.packer, fm.fe.packer, fm.ce.packer):
+        pk.record(None)
+    torch.cuda.synchronize()
+    for n, s in specs:
+        assert torch.equal(s.w, want[n][0]), n
+        assert torch.equal(s.b, want[n][1]), n
+    assert torch.equal(fm.loop._fh2_bias, fb)
