@@ -179,6 +179,14 @@ struct PackPiece {
   int64_t src, dst, kh, kw, cin_s, cout_s, cin8, kpad, co0, co1, ci0, ci1, so_co, so_ci, mode, pad;
 };
 int jr_pack_pieces(const void* table, int n, long max_elems, hipStream_t stream);
+// Implicit-GEMM weight gradient (wgrad.hip): dW (fp32 HWIO [KH][KW][cin][cout]) and db (fp32
+// [cout], optional) of the conv X (bf16 NHWC [N][H][W][xcs], channels xoff.. xoff+cin8) ->
+// dY (bf16 [N][OH][OW][ycs], channels yoff.. yoff+cout).  part / bpart: split-K workspaces of
+// S * cout_pad * kpad and S * cout_pad floats from jr_wgrad_plan (S <= 0: the planned S).
+int jr_wgrad_plan(int M, int K, int cout, int* S, int* cout_pad, int* kpad);
+int jr_wgrad(const void* x, int xcs, int xoff, int N, int H, int W, int cin8, int KH, int KW, int SH, int SW, int PH,
+             int PW, const void* dy, int ycs, int yoff, int OH, int OW, int cout, int cin, float* part, float* bpart,
+             int S, float* dw, float* db, long x_bytes, long y_bytes, hipStream_t stream);
 // Sequence loss over N <= 32 predictions pred fp32 [N][P][2] vs gt fp32 [P][2]
 // (valid: optional fp32 [P]): part fp32 [jr_seq_loss_blocks(P)][37] per-block
 // partial sums (0..N-1: sum over valid pixels of |pred_i - gt|_1; 32: EPE sum of

@@ -1,0 +1,290 @@
+// Implicit-GEMM weight gradient of an NHWC convolution on gfx950 MFMA
+// (training: every conv of the fused forward, reference sites as in
+// conv_igemm.h).  dW[co][k] = sum_m dY[m][co] * im2col(X)[m][k], k = (tap, cin8
+// chunk), m = (n, oh, ow): a long-K GEMM (K = pixels, up to 2e5 for the
+// refinement loop's iteration-stacked convs) with a small output.
+//
+//  * No im2col in memory: each stage gathers a [64 pixel][BKK] tile of the
+//    implicit im2col matrix straight from X (16-B chunks, zero padding via
+//    buffer range checks) and a [64 pixel][BCO] tile of dY into LDS.
+//  * Both MFMA operands reduce over the pixel dimension, which is the ROW
+//    dimension of both LDS images: fragments are read with ds_read_b64_tr_b16
+//    (gfx950 transposed LDS read, 4 pixels x 16 channels per 16-lane group),
+//    two reads per 8-pixel fragment, on an XOR-swizzled image that keeps
+//    every 32-lane half of those reads on distinct banks.
+//  * Split-K over pixel ranges (grid.z): fp32 partial tiles, reduced in a
+//    fixed order by a second kernel that writes the HWIO fp32 gradient
+//    directly (the Flax kernel layout, no transpose copy) and the bias
+//    gradient (column sums of dY, accumulated by the k-tile-0 workgroups
+//    from the staged dY registers).
+#include <algorithm>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+constexpr int WPX = 64;  // pixels per stage
+
+// XOR swizzle (in 8-B units) of LDS image row r with U units per row, so that
+// the transposed reads of a 32-lane half (rows 8g+q, g in {0,1}, q in 0..3,
+// units 4a+p) hit 32 distinct bank pairs.
+template <int U>
+JR_DEVICE int swz(int r) {
+  if constexpr (U >= 32) return 4 * ((r & 3) | (((r >> 3) & 1) << 2));
+  else return 4 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
+}
+
+struct WgParams {
+  const void* x; int xcs, xoff, N, H, W, cin8, KH, KW, SH, SW, PH, PW;
+  const void* dy; int ycs, yoff, OH, OW, cout;
+  int K, M, px_split;
+  float* part; int cout_pad, kpad;  // [S][cout_pad][kpad]
+  float* bpart;                     // [S][cout_pad] (bias partials) or null
+  long x_bytes, y_bytes;
+};
+
+template <int BCO, int BKK>
+__global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
+  constexpr int UA = BCO / 4, UB = BKK / 4;        // 8-B units per LDS row
+  constexpr int A_EL = WPX * BCO, B_EL = WPX * BKK;
+  constexpr int CA = BCO / 8, CB = BKK / 8;        // 16-B chunks per pixel row
+  constexpr int NA = WPX * CA / 256, NB = WPX * CB / 256;  // chunks per thread
+  constexpr int TM = BCO / 32, TN = BKK / 32;      // 16x16 tiles per wave (2x2 waves)
+  static_assert(NA >= 1 && NB >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (A_EL + B_EL)];
+  constexpr unsigned OOB = 0x80000000u;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int k0 = blockIdx.x * BKK, co0 = blockIdx.y * BCO;
+  const int m_begin = blockIdx.z * p.px_split;
+  const int m_end = min(p.M, m_begin + p.px_split);
+  const int OHW = p.OH * p.OW;
+  const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, (short)0, (int)p.y_bytes, 0x00020000);
+
+  // fixed per-thread chunk columns: dY chunk cA = tid % CA (rows tid / CA + 256/CA * i),
+  // X chunk cB = tid % CB (its tap / channel are fixed for the whole reduction)
+  const int cA = tid % CA, rA = tid / CA;
+  const int cB = tid % CB, rB = tid / CB;
+  const bool a_ok = co0 + 8 * cA < p.cout;
+  const int kk = k0 + 8 * cB;
+  const int tap = kk / p.cin8, ci = kk - tap * p.cin8;
+  const bool b_tap = tap < p.KH * p.KW && kk < p.K;
+  const int kh = b_tap ? tap / p.KW : 0, kw = b_tap ? tap - (tap / p.KW) * p.KW : 0;
+
+  u32x4 ra[NA], rb[NB];
+  float bsum[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
+  const bool do_bias = p.bpart != nullptr && blockIdx.x == 0;
+
+  auto issue = [&](int mb) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int m = mb + rA + (256 / CA) * i;
+      const bool ok = a_ok && m < m_end;
+      const unsigned off = (unsigned)(((long)m * p.ycs + p.yoff + co0 + 8 * cA) * 2);
+      ra[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ys, ok ? off : OOB, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int m = mb + rB + (256 / CB) * i;
+      bool ok = b_tap && m < m_end;
+      unsigned off = OOB;
+      if (ok) {
+        const int n = m / OHW, rem = m - n * OHW;
+        const int oh = rem / p.OW, ow = rem - oh * p.OW;
+        const int ih = oh * p.SH - p.PH + kh, iw = ow * p.SW - p.PW + kw;
+        ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        off = ok ? (unsigned)(((((long)n * p.H + ih) * p.W + iw) * p.xcs + p.xoff + ci) * 2) : OOB;
+      }
+      rb[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xs, off, 0, 0));
+    }
+  };
+  auto store = [&](int buf) {
+    bf16* sA = smem + buf * (A_EL + B_EL);
+    bf16* sB = sA + A_EL;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int r = rA + (256 / CA) * i;
+      const int u = (2 * cA) ^ swz<UA>(r);
+      *(u32x4*)(sA + r * BCO + 4 * u) = ra[i];
+      if (do_bias) {
+        const bf16x8 v = __builtin_bit_cast(bf16x8, ra[i]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bsum[j] += bf2f(v[j]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int r = rB + (256 / CB) * i;
+      const int u = (2 * cB) ^ swz<UB>(r);
+      *(u32x4*)(sB + r * BKK + 4 * u) = rb[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  auto tr = [&](const bf16* img, int U, int cols, int r, int cb) -> s16x4 {
+    // row r, 8-B unit of columns cb + 4 pp (the lane's part of the 4 x 16 block)
+    const int u = cb / 4 + pp;
+    const int sw = (U >= 32) ? (4 * ((r & 3) | (((r >> 3) & 1) << 2))) : (4 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)));
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + r * cols + 4 * (u ^ sw)));
+  };
+  auto compute = [&](int buf) {
+    const bf16* sA = smem + buf * (A_EL + B_EL);
+    const bf16* sB = sA + A_EL;
+#pragma unroll
+    for (int ks = 0; ks < WPX / 32; ++ks) {
+      const int r0 = 32 * ks + 8 * g + q;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int cb = wr * (BCO / 2) + 16 * tm;
+        const s16x4 lo = tr(sA, UA, BCO, r0, cb), hi = tr(sA, UA, BCO, r0 + 4, cb);
+        af[tm] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int cb = wc * (BKK / 2) + 16 * tn;
+        const s16x4 lo = tr(sB, UB, BKK, r0, cb), hi = tr(sB, UB, BKK, r0 + 4, cb);
+        bfr[tn] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tm], bfr[tn], acc[tm][tn], 0, 0, 0);
+    }
+  };
+
+  // register-staged double buffer: loads of stage s+1 fly while stage s multiplies
+  int mb = m_begin;
+  issue(mb);
+  store(0);
+  __syncthreads();
+  int buf = 0;
+  for (mb += WPX; mb < m_end; mb += WPX) {
+    issue(mb);
+    compute(buf);
+    store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  compute(buf);
+
+  // partial tile -> part[z][co][k]
+  float* out = p.part + (long)blockIdx.z * p.cout_pad * p.kpad;
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int co = co0 + wr * (BCO / 2) + 16 * tm + 4 * g + j;
+        const int k = k0 + wc * (BKK / 2) + 16 * tn + (lane & 15);
+        out[(long)co * p.kpad + k] = acc[tm][tn][j];
+      }
+  if (do_bias) {
+    // threads with the same chunk column cA hold partial sums of the same 8 channels
+    __syncthreads();
+    float* red = (float*)smem;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = bsum[j];
+    __syncthreads();
+    if (tid < BCO) {
+      const int c8 = tid >> 3, j = tid & 7;
+      float s = 0.f;
+      for (int t = c8; t < 256; t += CA) s += red[t * 8 + j];
+      p.bpart[(long)blockIdx.z * p.cout_pad + co0 + tid] = s;
+    }
+  }
+}
+
+// dW_hwio[kh][kw][ci][co] = sum_z part[z][co][(kh*KW + kw)*cin8 + ci] (ci < cin), db[co] = sum_z bpart[z][co]
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, const float* __restrict__ bpart,
+                                                           int S, int cout_pad, int kpad, int KH, int KW, int cin8,
+                                                           int cin, int cout, float* __restrict__ dw,
+                                                           float* __restrict__ db) {
+  const long total = (long)KH * KW * cin * cout;
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e < total) {
+    const int co = (int)(e % cout);
+    const long r = e / cout;
+    const int ci = (int)(r % cin);
+    const int tap = (int)(r / cin);
+    const long k = (long)tap * cin8 + ci;
+    const float* pp = part + (long)co * kpad + k;
+    const long zs = (long)cout_pad * kpad;
+    float s = 0.f;
+    for (int z = 0; z < S; ++z) s += pp[z * zs];
+    dw[e] = s;
+  }
+  if (db && e < cout) {
+    float s = 0.f;
+    for (int z = 0; z < S; ++z) s += bpart[(long)z * cout_pad + e];
+    db[e] = s;
+  }
+}
+
+template <int BCO, int BKK>
+int launch(const WgParams& p, int S, hipStream_t st) {
+  dim3 grid((p.K + BKK - 1) / BKK, (p.cout + BCO - 1) / BCO, S);
+  hipLaunchKernelGGL((wgrad_kernel<BCO, BKK>), grid, dim3(256), 0, st, p);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int jr_wgrad_plan(int M, int K, int cout, int* S, int* cout_pad, int* kpad) {
+  const int bco = cout > 64 ? 128 : 64, bkk = K > 64 ? 128 : 64;
+  const int tiles = ((K + bkk - 1) / bkk) * ((cout + bco - 1) / bco);
+  // ~2 workgroups per CU, at least 4 stages of pixels per split
+  int s = std::max(1, std::min((512 + tiles - 1) / tiles, (M + 4 * WPX - 1) / (4 * WPX)));
+  *S = s;
+  *cout_pad = (cout + bco - 1) / bco * bco;
+  *kpad = (K + bkk - 1) / bkk * bkk;
+  return 0;
+}
+
+extern "C" int jr_wgrad(const void* x, int xcs, int xoff, int N, int H, int W, int cin8, int KH, int KW, int SH,
+                        int SW, int PH, int PW, const void* dy, int ycs, int yoff, int OH, int OW, int cout, int cin,
+                        float* part, float* bpart, int S, float* dw, float* db, long x_bytes, long y_bytes,
+                        hipStream_t stream) {
+  if (cin8 % 8 || xcs % 8 || xoff % 8 || ycs % 8 || yoff % 8) return (int)hipErrorInvalidValue;
+  WgParams p{};
+  p.x = x; p.xcs = xcs; p.xoff = xoff; p.N = N; p.H = H; p.W = W; p.cin8 = cin8;
+  p.KH = KH; p.KW = KW; p.SH = SH; p.SW = SW; p.PH = PH; p.PW = PW;
+  p.dy = dy; p.ycs = ycs; p.yoff = yoff; p.OH = OH; p.OW = OW; p.cout = cout;
+  p.K = KH * KW * cin8;
+  p.M = N * OH * OW;
+  int s_, cp, kp;
+  jr_wgrad_plan(p.M, p.K, cout, &s_, &cp, &kp);
+  if (S <= 0) S = s_;
+  const int per = (p.M + S - 1) / S;
+  p.px_split = (per + WPX - 1) / WPX * WPX;
+  S = (p.M + p.px_split - 1) / p.px_split;
+  p.part = part; p.cout_pad = cp; p.kpad = kp; p.bpart = db ? bpart : nullptr;
+  p.x_bytes = x_bytes; p.y_bytes = y_bytes;
+  const bool bc = cout > 64, bk = p.K > 64;
+  int r;
+  if (bc && bk) r = launch<128, 128>(p, S, stream);
+  else if (bc) r = launch<128, 64>(p, S, stream);
+  else if (bk) r = launch<64, 128>(p, S, stream);
+  else r = launch<64, 64>(p, S, stream);
+  if (r) return r;
+  const long total = (long)KH * KW * cin * cout;
+  const long nthreads = std::max<long>(total, cout);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, stream, part,
+                     p.bpart, S, cp, kp, KH, KW, cin8, cin, cout, dw, db);
+  return (int)hipGetLastError();
+}

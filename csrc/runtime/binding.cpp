@@ -360,6 +360,41 @@ static Launch make_pack(const TList& t, const IList& i, std::vector<at::Tensor>*
   return [=](hipStream_t s, int) { return jr_pack_pieces(tp, n, me, s); };
 }
 
+// t = [x, dy, dw (fp32 HWIO), db?, part?, bpart?],
+// i = [N, H, W, xoff, cin8, KH, KW, SH, SW, PH, PW, yoff, OH, OW, cout, cin]
+static Launch make_wgrad(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor x = opt(t, 0), dy = opt(t, 1), dw = opt(t, 2), db = opt(t, 3), part = opt(t, 4), bpart = opt(t, 5);
+  TORCH_CHECK(i.size() == 16, "wgrad: expected 16 ints");
+  check_bf16(x, "x"); check_bf16(dy, "dy"); check_f32(dw, "dw");
+  const int N = (int)i[0], H = (int)i[1], W = (int)i[2], xoff = (int)i[3], cin8 = (int)i[4], KH = (int)i[5];
+  const int KW = (int)i[6], SH = (int)i[7], SW = (int)i[8], PH = (int)i[9], PW = (int)i[10], yoff = (int)i[11];
+  const int OH = (int)i[12], OW = (int)i[13], cout = (int)i[14], cin = (int)i[15];
+  const int xcs = cs(x), ycs = cs(dy);
+  TORCH_CHECK(cin8 % 8 == 0 && cin <= cin8 && xoff % 8 == 0 && xcs % 8 == 0 && xoff + cin8 <= xcs, "wgrad: input slice");
+  TORCH_CHECK(yoff % 8 == 0 && ycs % 8 == 0 && yoff + cout <= ycs, "wgrad: gradient slice");
+  TORCH_CHECK(x.numel() >= (int64_t)N * H * W * xcs && dy.numel() >= (int64_t)N * OH * OW * ycs, "wgrad: sizes");
+  TORCH_CHECK(OH == (H + 2 * PH - KH) / SH + 1 && OW == (W + 2 * PW - KW) / SW + 1, "wgrad: output size");
+  TORCH_CHECK(dw.numel() == (int64_t)KH * KW * cin * cout, "wgrad: dw must be [KH][KW][cin][cout]");
+  TORCH_CHECK(x.numel() * 2 < (1LL << 31) && dy.numel() * 2 < (1LL << 31), "wgrad: operand larger than 2 GiB");
+  if (db.defined()) { check_f32(db, "db"); TORCH_CHECK(db.numel() == cout, "wgrad: db"); }
+  int S, cp, kp;
+  const int64_t M = (int64_t)N * OH * OW;
+  jr_wgrad_plan((int)M, KH * KW * cin8, cout, &S, &cp, &kp);
+  if (!part.defined()) part = at::empty({(int64_t)S * cp * kp}, dw.options());
+  if (!bpart.defined()) bpart = at::empty({(int64_t)S * cp}, dw.options());
+  check_f32(part, "part"); check_f32(bpart, "bpart");
+  TORCH_CHECK(part.numel() >= (int64_t)S * cp * kp && bpart.numel() >= (int64_t)S * cp, "wgrad: workspace");
+  if (keep) for (auto& v : {x, dy, dw, db, part, bpart}) if (v.defined()) keep->push_back(v);
+  const void *xp = x.data_ptr(), *yp = dy.data_ptr();
+  float *dwp = dw.data_ptr<float>(), *dbp = db.defined() ? db.data_ptr<float>() : nullptr;
+  float *pp = part.data_ptr<float>(), *bp = bpart.data_ptr<float>();
+  const long xb = x.numel() * 2, yb = dy.numel() * 2;
+  return [=](hipStream_t s, int) {
+    return jr_wgrad(xp, xcs, xoff, N, H, W, cin8, KH, KW, SH, SW, PH, PW, yp, ycs, yoff, OH, OW, cout, cin, pp, bp, S,
+                    dwp, dbp, xb, yb, s);
+  };
+}
+
 // t = [taps, dflow], i = [N, h, w]
 static Launch make_flow_gather_bwd(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
   at::Tensor taps = opt(t, 0), df = opt(t, 1);
@@ -815,6 +850,10 @@ void conv_train_op(const TList& t, IList i, double alpha, const TList& tx, IList
   run_now(make_conv(t, i, alpha, nullptr, &tx, &ix));
 }
 void upsample_convex_bwd_op(const TList& t, IList i, double alpha) { run_now(make_upsample_convex_bwd(t, i, alpha, nullptr)); }
+void wgrad_op(const TList& t, IList i) {
+  std::vector<at::Tensor> keep;
+  run_now(make_wgrad(t, i, &keep));
+}
 void pack_op(const TList& t, IList i) {
   std::vector<at::Tensor> keep;
   run_now(make_pack(t, i, &keep));
@@ -906,6 +945,7 @@ class Plan : public torch::CustomClassHolder {
   void add_upsample_convex_bwd(TList t, IList i, double alpha) {
     push(make_upsample_convex_bwd(t, i, alpha, &keep_), "upsample_convex_bwd");
   }
+  void add_wgrad(TList t, IList i) { push(make_wgrad(t, i, &keep_), "wgrad"); }
   void add_pack(TList t, IList i) { push(make_pack(t, i, &keep_), "pack"); }
   void add_norm_bwd(TList t, IList i, double eps) { push(make_norm_bwd(t, i, eps, &keep_), "norm_bwd"); }
   void add_flow_gather_bwd(TList t, IList i) { push(make_flow_gather_bwd(t, i, &keep_), "flow_gather_bwd"); }
@@ -1135,6 +1175,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("flow_gather_bwd(Tensor?[] t, int[] i) -> ()", &jr::flow_gather_bwd_op);
   m.def("norm_bwd(Tensor?[] t, int[] i, float eps) -> ()", &jr::norm_bwd_op);
   m.def("pack(Tensor?[] t, int[] i) -> ()", &jr::pack_op);
+  m.def("wgrad(Tensor?[] t, int[] i) -> ()", &jr::wgrad_op);
   m.def("upsample_bilinear_bwd(Tensor?[] t, int[] i) -> ()", &jr::upsample_bilinear_bwd_op);
   m.def("seq_loss(Tensor?[] t, int[] i, float max_flow) -> ()", &jr::seq_loss_op);
   m.def("seq_loss_blocks(int P) -> int", &jr::seq_loss_blocks_op);
@@ -1167,6 +1208,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_flow_gather_bwd", &jr::Plan::add_flow_gather_bwd)
       .def("add_norm_bwd", &jr::Plan::add_norm_bwd)
       .def("add_pack", &jr::Plan::add_pack)
+      .def("add_wgrad", &jr::Plan::add_wgrad)
       .def("add_upsample_bilinear_bwd", &jr::Plan::add_upsample_bilinear_bwd)
       .def("add_lookup_bwd", &jr::Plan::add_lookup_bwd)
       .def("add_im2col", &jr::Plan::add_im2col)

@@ -35,6 +35,7 @@ KERNEL_SOURCES = [
     CSRC / "kernels" / "flowhead.hip",
     CSRC / "kernels" / "conv_direct.hip",
     CSRC / "kernels" / "train.hip",
+    CSRC / "kernels" / "wgrad.hip",
 ]
 HOST_SOURCES = [CSRC / "runtime" / "binding.cpp"]
 HEADERS = [CSRC / "kernels" / "common.h", CSRC / "kernels" / "kernels.h", CSRC / "kernels" / "conv_igemm.h"]

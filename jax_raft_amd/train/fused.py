@@ -89,6 +89,46 @@ def _pad_last(k: torch.Tensor, n: int) -> torch.Tensor:
 _CFG_CACHE: Dict[tuple, int] = {}
 
 
+class GradArena:
+    """One flat fp32 buffer holding the gradients of a parameter list (HWIO
+    views the native weight-gradient kernels write into).  :meth:`snapshot`
+    hands autograd a fresh copy in ONE kernel, so a later step's in-place
+    writes never alias a gradient a caller still holds."""
+
+    def __init__(self, params, device):
+        self.params = list(params)
+        n = sum(p.numel() for p in self.params)
+        self.flat = torch.zeros(n, dtype=F32, device=device)
+        self.views: Dict[int, torch.Tensor] = {}
+        self._off: Dict[int, int] = {}
+        off = 0
+        for p in self.params:
+            self.views[id(p)] = self.flat[off:off + p.numel()].view(p.shape)
+            self._off[id(p)] = off
+            off += p.numel()
+
+    def __getitem__(self, p) -> torch.Tensor:
+        return self.views[id(p)]
+
+    def snapshot(self) -> Dict[int, torch.Tensor]:
+        c = self.flat.clone()
+        return {id(p): c[self._off[id(p)]:self._off[id(p)] + p.numel()].view(p.shape) for p in self.params}
+
+
+def record_wgrad(plan, x, n_img, H, W, x_coff, cin8, kernel_shape, stride, pad, dy, yoff, dw, db=None):
+    """Native implicit-GEMM weight (+ bias) gradient of one conv (wgrad.hip)
+    into the fp32 HWIO ``dw`` (+ ``db``); ``plan=None`` launches it now."""
+    kh, kw, cin, cout = kernel_shape
+    OH = (H + 2 * pad[0] - kh) // stride[0] + 1
+    OW = (W + 2 * pad[1] - kw) // stride[1] + 1
+    args = ([x, dy, dw, db], [n_img, H, W, x_coff, cin8, kh, kw, stride[0], stride[1], pad[0], pad[1], yoff, OH, OW,
+                              cout, cin])
+    if plan is None:
+        nat.ops().wgrad(*args)
+    else:
+        plan.add_wgrad(*args)
+
+
 class Packer:
     """Table of rectangular weight pieces repacked by ONE native launch
     (csrc/kernels/train.hip:pack_pieces_kernel) from the fp32 HWIO parameters
@@ -215,6 +255,7 @@ class FusedLoop:
         self._specs: Dict[str, nat.ConvSpec] = {}
         self._pack()
         self.packer = self._pieces()
+        self.arena = GradArena(self.params, self.device)
         self.plan_f = self._build_fwd()
         self.plan_b = self._build_bwd()
 
@@ -602,7 +643,50 @@ class FusedLoop:
             P.add_lookup_bwd([self.coords[t], self.dcorr] + self.lv_grads + [None] * (4 - self.L),
                              [self.L, B, h, w, self.radius])
             self._bconv(P, "cf2T", self.dcf[t], x_coff=cl[-1], s1=Seg(mask=self.f1[t], out=self.df1[t]))
+        self._record_wgrads(P)
         return P
+
+    def _record_wgrads(self, P):
+        """Weight gradients of the loop's convs over all iterations stacked
+        (n_img = T * B images): one implicit-GEMM launch per weight."""
+        T, G, hd, B, h, w = self.T, self.G, self.hd, self.B, self.h, self.w
+        nT = T * B
+        me, fh, mp, A = self.me, self.fh, self.mp, self.arena
+        dev = self.device
+
+        def wb(conv, x, x_coff, cin8, dy, yoff=0):
+            record_wgrad(P, x, nT, h, w, x_coff, cin8, tuple(conv.kernel.shape), (1, 1), conv.padding, dy, yoff,
+                         A[conv.kernel], A[conv.bias])
+
+        c1 = me.convcorr1.layers_0
+        if len(self.cl) == 2:
+            wb(c1, self.corr, 0, self.corr_cs, self.dc1)
+            wb(me.convcorr2.layers_0, self.c1, 0, self.cl[0], self.dcf)
+        else:
+            wb(c1, self.corr, 0, self.corr_cs, self.dcf)
+        wb(me.convflow1.layers_0, self.flow8, 0, 8, self.df1)
+        wb(me.convflow2.layers_0, self.f1, 0, self.fl[0], self.dcf, yoff=self.cl[-1])
+        wb(me.conv.layers_0, self.cf, 0, self.cf_cs, self.dm)
+        self.gAw, self.gBw = [], []
+        for g, gru in enumerate(self.grus):
+            kh, kw = gru.convz.kernel.shape[:2]
+            ga = torch.zeros(kh, kw, self.hx_cs, 2 * hd, device=dev)
+            gb = torch.zeros(kh, kw, self.hx_cs, hd, device=dev)
+            record_wgrad(P, self.hx[g], nT, h, w, 0, self.hx_cs, tuple(ga.shape), (1, 1), gru.padding, self.dzr[g], 0, ga)
+            record_wgrad(P, self.qx[g], nT, h, w, 0, self.hx_cs, tuple(gb.shape), (1, 1), gru.padding, self.dq[g], 0, gb)
+            self.gAw.append(ga)
+            self.gBw.append(gb)
+        fm_out = self.fh_hidden + self.mask_hidden
+        self.fh1w = torch.zeros(3, 3, hd, fm_out, device=dev)
+        self.fh1b = torch.zeros(fm_out, device=dev)
+        record_wgrad(P, self.hx[0, 1:], nT, h, w, 0, hd, tuple(self.fh1w.shape), (1, 1), (1, 1), self.dfmm, 0,
+                     self.fh1w, self.fh1b)
+        # flow-head output conv (256 -> 2): computed as the weight gradient of the 3x3 conv
+        # ddelta -> fm with the taps flipped (K = 9 x 8 instead of 9 x 256)
+        self.fh2w = torch.zeros(3, 3, 2, self.fh_hidden, device=dev)
+        record_wgrad(P, self.ddelta, nT, h, w, 0, 8, tuple(self.fh2w.shape), (1, 1), (1, 1), self.fmm, 0, self.fh2w)
+        if self.has_mask:
+            wb(mp.conv, self.fmm, self.fh_hidden, self.mask_hidden, self.dmask)
 
     def _run(self, plan):
         if self.use_graph:
@@ -644,82 +728,42 @@ class FusedLoop:
         return self._finish()
 
     # ---------------------------------------------------- weight gradients
-    def _wgrad(self, x, n_img, x_coff, cin8, kh, kw, pad, dy, cin, cout):
-        """dW (kh, kw, cin, cout) fp32 = im2col(x)^T dy over the stacked images."""
-        from ..ops.autograd import _wgrad_gemm
-
-        kpad = round_up(kh * kw * cin8, 64)
-        Mt = n_img * self.h * self.w
-        col = torch.empty(Mt, kpad, dtype=BF16, device=self.device)
-        nat.ops().im2col([x, col], [n_img, self.h, self.w, x_coff, cin8, kh, kw, 1, 1, pad[0], pad[1]])
-        gw = _wgrad_gemm(dy, col, cout)
-        return gw[: kh * kw * cin8].reshape(kh, kw, cin8, cout)[:, :, :cin]
-
     def _finish(self):
+        """After the backward plan (data gradients + stacked weight gradients):
+        the context share of the ConvGRU gates (iteration sums), the assembly of
+        the gate / flow-head kernels, the pyramid and context-encoder input
+        gradients."""
         T, G, M, hd, C = self.T, self.G, self.M, self.hd, self.ctx_ch
-        nT = T * self.B
-        me, fh, mp = self.me, self.fh, self.mp
-        grads: Dict[int, torch.Tensor] = {}
-
-        def put(p, g):
-            grads[id(p)] = g.to(p.dtype)
-
-        def wb(conv, x, n_img, x_coff, cin8, dy2, pad=None):
-            kh, kw, cin, cout = conv.kernel.shape
-            pad = conv.padding if pad is None else pad
-            put(conv.kernel, self._wgrad(x, n_img, x_coff, cin8, kh, kw, pad, dy2, cin, cout))
-            put(conv.bias, dy2.sum(0, dtype=F32))
-
-        c1 = me.convcorr1.layers_0
-        if len(self.cl) == 2:
-            wb(c1, self.corr, nT, 0, self.corr_cs, self.dc1.reshape(-1, self.cl[0]))
-            wb(me.convcorr2.layers_0, self.c1, nT, 0, self.cl[0], self.dcf.reshape(-1, self.cf_cs)[:, : self.cl[1]])
-        else:
-            wb(c1, self.corr, nT, 0, self.corr_cs, self.dcf.reshape(-1, self.cf_cs)[:, : self.cl[0]])
-        wb(me.convflow1.layers_0, self.flow8[:T], nT, 0, 8, self.df1.reshape(-1, self.fl[0]))
-        wb(me.convflow2.layers_0, self.f1, nT, 0, self.fl[0],
-           self.dcf.reshape(-1, self.cf_cs)[:, self.cl[-1]: self.cl[-1] + self.fl[1]])
-        wb(me.conv.layers_0, self.cf, nT, 0, self.cf_cs, self.dm.reshape(-1, self.mot_cs)[:, : self.mot_out - 2])
-        # ConvGRUs: loop part (h | motion) per iteration stacked; context part once over the iteration sum
+        fh, mp, A = self.fh, self.mp, self.arena
         dctx = self.dctx
         for g, gru in enumerate(self.grus):
             kh, kw = gru.convz.kernel.shape[:2]
-            pad = gru.padding
-            gA = self._wgrad(self.hx[g, :T], nT, 0, self.hx_cs, kh, kw, pad, self.dzr[g].reshape(-1, 2 * hd),
-                             self.hx_cs, 2 * hd)
-            gB = self._wgrad(self.qx[g, :T], nT, 0, self.hx_cs, kh, kw, pad, self.dq[g].reshape(-1, hd),
-                             self.hx_cs, hd)
             S = torch.cat([self.dzr[g].sum(0, dtype=F32), self.dq[g].sum(0, dtype=F32)], dim=1)  # (M, 3 hd)
             Sb = S.to(BF16)
-            gC = self._wgrad(self.ctx_in, self.B, 0, self.ctx_cs, kh, kw, pad, Sb, C, 3 * hd)
-            db = S.sum(0)
-            loop_in = gru.convz.kernel.shape[2]  # hd + C + mot
+            gC = torch.empty(kh, kw, C, 3 * hd, device=self.device)
+            db = torch.empty(3 * hd, device=self.device)
+            record_wgrad(None, self.ctx_in, self.B, self.h, self.w, 0, self.ctx_cs, tuple(gC.shape), (1, 1),
+                         gru.padding, Sb, 0, gC, db)
+            mot = self.mot_out
             for j, conv in enumerate((gru.convz, gru.convr, gru.convq)):
-                full = torch.zeros(kh, kw, loop_in, hd, device=self.device, dtype=F32)
-                src = gA[..., j * hd:(j + 1) * hd] if j < 2 else gB
+                full = A[conv.kernel]
+                src = self.gAw[g][..., j * hd:(j + 1) * hd] if j < 2 else self.gBw[g]
                 full[:, :, :hd] = src[:, :, :hd]
-                full[:, :, hd + C:] = src[:, :, hd: hd + loop_in - hd - C]
+                full[:, :, hd + C:] = src[:, :, hd: hd + mot]
                 full[:, :, hd:hd + C] = gC[..., j * hd:(j + 1) * hd]
-                put(conv.kernel, full)
-                put(conv.bias, db[j * hd:(j + 1) * hd])
+                A[conv.bias].copy_(db[j * hd:(j + 1) * hd])
             # context data gradient of this GRU's gates (accumulated over the GRUs)
             tx, ix = _tx(s1=Seg(gin=dctx if g > 0 else None, out=dctx))
             self._conv(None, f"gCT{g}", Sb, dctx, tx=tx, ix=ix, epi=EPI_BWD, hidden=0)
-        # flow head / mask predictor
-        dfm = self.dfmm.reshape(-1, self.fm_cs)
-        hx_next = self.hx[0, 1:T + 1]
+        fhn, mh = self.fh_hidden, self.mask_hidden
+        A[fh.conv1.kernel].copy_(self.fh1w[..., :fhn])
+        A[fh.conv1.bias].copy_(self.fh1b[:fhn])
         if self.has_mask:
             mr = mp.convrelu.layers_0
-            k = self._wgrad(hx_next, nT, 0, hd, 3, 3, (1, 1), dfm, hd, self.fh_hidden + self.mask_hidden)
-            put(fh.conv1.kernel, k[..., : self.fh_hidden])
-            put(mr.kernel, k[..., self.fh_hidden:])
-            db = dfm.sum(0, dtype=F32)
-            put(fh.conv1.bias, db[: self.fh_hidden])
-            put(mr.bias, db[self.fh_hidden: self.fh_hidden + self.mask_hidden])
-            wb(mp.conv, self.fmm, nT, self.fh_hidden, self.mask_hidden, self.dmask.reshape(-1, 576))
-        else:
-            wb(fh.conv1, hx_next, nT, 0, hd, dfm[:, : self.fh_hidden])
-        wb(fh.conv2, self.fmm, nT, 0, self.fh_hidden, self.ddelta.reshape(-1, 8)[:, :2])
+            A[mr.kernel].copy_(self.fh1w[..., fhn:fhn + mh])
+            A[mr.bias].copy_(self.fh1b[fhn:fhn + mh])
+        A[fh.conv2.kernel].copy_(torch.flip(self.fh2w, dims=(0, 1)).permute(0, 1, 3, 2))
+        A[fh.conv2.bias].copy_(self.ddelta.reshape(-1, 8)[:, :2].sum(0, dtype=F32))
         # correlation pyramid: pooling adjoints + the two GEMMs of fmap1 fmap2^T / sqrt(C)
         from ..ops.autograd import pyramid_backward
 
@@ -730,7 +774,8 @@ class FusedLoop:
         dc = torch.empty(M, hd + C, device=self.device, dtype=F32)
         dc[:, :hd] = self.dh_next * (1 - h0 * h0)
         dc[:, hd:] = dctx[:, :C] * (self.ctx_in[:, :C] > 0)
-        return g1, g2, dc.reshape(self.B, self.h, self.w, hd + C), [grads.get(id(p)) for p in self.params]
+        grads = A.snapshot()
+        return g1, g2, dc.reshape(self.B, self.h, self.w, hd + C), [grads[id(p)] for p in self.params]
 
 
 class FusedRefine(torch.autograd.Function):

@@ -83,6 +83,11 @@ class EncoderTrain:
             P.set_segment(0)
             P.set_lane(0)
         self._pack()
+        from .fused import GradArena
+
+        self.arena = GradArena([p for c in self._convs() for p in (c.kernel, c.bias)] +
+                               [p for m in enc.modules() if getattr(m, "scale", None) is not None
+                                for p in (m.scale, m.bias)], self.device)
         self.packer = self._pieces()
         self.packer.record(self.plan_f)   # first op of the forward plan: repack this step's weights
         self._record_fwd()
@@ -277,6 +282,13 @@ class EncoderTrain:
         # stem: dL/d(stem activation) = dout of the first block's input
         self.stem.dy = self._z(*self.stem.y.shape)
         self._norm_bwd(self.stem, dout, self.stem.dy, relu=1)
+        # weight (+ bias) gradients: one implicit-GEMM launch per conv
+        from .fused import record_wgrad
+
+        for u in self.units + [fin]:
+            c = u.conv
+            record_wgrad(self.plan_b, u.x, u.N, u.H, u.W, 0, u.cin8, tuple(c.kernel.shape), c.stride, c.padding,
+                         u.dy, 0, self.arena[c.kernel], self.arena[c.bias])
 
     # ---------------------------------------------------------------- run
     def _run(self, plan):
@@ -301,27 +313,13 @@ class EncoderTrain:
                     bn.var.mul_(bn.momentum).add_((1.0 - bn.momentum) * v)
 
     def backward(self) -> Dict[int, torch.Tensor]:
-        """Runs the backward plan (``dy_out`` must be filled); returns
-        {id(param): grad} for every encoder parameter."""
-        from ..ops.autograd import _wgrad_gemm
-
+        """Runs the backward plan (``dy_out`` must be filled): data gradients,
+        then every conv's weight / bias gradient; returns {id(param): grad}."""
         self._run(self.plan_b)
-        grads: Dict[int, torch.Tensor] = {}
-        for u in self.units + [self.fin]:
-            c = u.conv
-            kh, kw, cin, cout = c.kernel.shape
-            sh, sw = c.stride
-            ph, pw = c.padding
-            kpad = round_up(kh * kw * u.cin8, 64)
-            Mt = u.N * u.OH * u.OW
-            col = torch.empty(Mt, kpad, dtype=BF16, device=self.device)
-            nat.ops().im2col([u.x, col], [u.N, u.H, u.W, 0, u.cin8, kh, kw, sh, sw, ph, pw])
-            dy2 = u.dy.reshape(Mt, -1)
-            gw = _wgrad_gemm(dy2, col, cout)
-            grads[id(c.kernel)] = gw[: kh * kw * u.cin8].reshape(kh, kw, u.cin8, cout)[:, :, :cin].contiguous()
-            grads[id(c.bias)] = dy2.sum(0, dtype=F32)
-            if self.mode == 2 and u.norm_mod is not None:
-                r = u.red.sum(0)
-                grads[id(u.norm_mod.scale)] = r[:, 1].contiguous()
-                grads[id(u.norm_mod.bias)] = r[:, 0].contiguous()
-        return grads
+        if self.mode == 2:
+            for u in self.units:
+                if u.norm_mod is not None:
+                    r = u.red.sum(0)
+                    self.arena[u.norm_mod.scale].copy_(r[:, 1])
+                    self.arena[u.norm_mod.bias].copy_(r[:, 0])
+        return self.arena.snapshot()

@@ -233,3 +233,45 @@ def test_native_pack_table_matches_python_packing(factory):
         assert torch.equal(s.w, want[n][0]), n
         assert torch.equal(s.b, want[n][1]), n
     assert torch.equal(fm.loop._fh2_bias, fb)
+
+
+WG_CASES = [
+    # N, H, W, xcs, xoff, cin, cin8, cout, ycs, yoff, kh, kw, stride, pad
+    (2, 12, 16, 64, 0, 64, 64, 64, 64, 0, 3, 3, 1, (1, 1)),
+    (2, 12, 16, 64, 0, 64, 64, 96, 96, 0, 3, 3, 2, (1, 1)),
+    (2, 13, 17, 32, 0, 32, 32, 64, 64, 0, 1, 1, 2, (0, 0)),
+    (1, 24, 32, 8, 0, 3, 8, 64, 64, 0, 7, 7, 2, (3, 3)),
+    (2, 9, 11, 264, 8, 256, 256, 256, 256, 0, 1, 5, 1, (0, 2)),
+    (1, 10, 12, 512, 0, 256, 256, 2, 8, 0, 3, 3, 1, (1, 1)),
+    (1, 10, 12, 8, 0, 2, 8, 128, 128, 0, 7, 7, 1, (3, 3)),
+    (1, 10, 12, 328, 0, 324, 328, 256, 256, 0, 1, 1, 1, (0, 0)),
+    (2, 11, 9, 256, 0, 256, 256, 126, 128, 0, 3, 3, 1, (1, 1)),
+    (2, 11, 9, 512, 256, 256, 256, 64, 256, 192, 3, 3, 1, (1, 1)),
+    (3, 16, 20, 96, 0, 96, 96, 80, 88, 0, 3, 3, 1, (1, 1)),
+]
+
+
+@pytest.mark.parametrize("case", WG_CASES)
+def test_native_wgrad(case):
+    """Implicit-GEMM weight / bias gradient (csrc/kernels/wgrad.hip) against
+    fp32 autograd of the conv on the same bf16 operands."""
+    from jax_raft_amd.ops import native as nat
+
+    N, H, W, xcs, xoff, cin, cin8, cout, ycs, yoff, kh, kw, s, pad = case
+    torch.manual_seed(17)
+    OH = (H + 2 * pad[0] - kh) // s + 1
+    OW = (W + 2 * pad[1] - kw) // s + 1
+    x = torch.randn(N, H, W, xcs).to(torch.bfloat16)
+    dy = torch.randn(N, OH, OW, ycs).to(torch.bfloat16)
+    xr = x[..., xoff:xoff + cin].float().requires_grad_(False)
+    k = torch.zeros(kh, kw, cin, cout, requires_grad=True)
+    b = torch.zeros(cout, requires_grad=True)
+    y = R.conv2d_nhwc(xr, k, b, (s, s), pad)
+    y.backward(dy[..., yoff:yoff + cout].float())
+    dw = torch.empty(kh, kw, cin, cout, device="cuda")
+    db = torch.empty(cout, device="cuda")
+    nat.ops().wgrad([x.cuda(), dy.cuda(), dw, db],
+                    [N, H, W, xoff, cin8, kh, kw, s, s, pad[0], pad[1], yoff, OH, OW, cout, cin])
+    torch.cuda.synchronize()
+    assert _rel(dw, k.grad) < 1e-3, _rel(dw, k.grad)
+    assert _rel(db, b.grad) < 1e-3
