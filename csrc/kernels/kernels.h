@@ -187,6 +187,10 @@ int jr_wgrad_plan(int M, int K, int cout, int* S, int* cout_pad, int* kpad);
 int jr_wgrad(const void* x, int xcs, int xoff, int N, int H, int W, int cin8, int KH, int KW, int SH, int SW, int PH,
              int PW, const void* dy, int ycs, int yoff, int OH, int OW, int cout, int cin, float* part, float* bpart,
              int S, float* dw, float* db, long x_bytes, long y_bytes, hipStream_t stream);
+// Correlation pyramid backward: dc bf16 [M][h][w] = scale * sum_l (2x2 floor-pool adjoint)^l of the
+// fp32 level gradients g_l [M][h_l][w_l] (g1..g3 may be null past L levels).
+int jr_pyr_bwd_dc(const float* g0, const float* g1, const float* g2, const float* g3, int L, long M, int h, int w,
+                  float scale, void* dc, hipStream_t stream);
 // Sequence loss over N <= 32 predictions pred fp32 [N][P][2] vs gt fp32 [P][2]
 // (valid: optional fp32 [P]): part fp32 [jr_seq_loss_blocks(P)][37] per-block
 // partial sums (0..N-1: sum over valid pixels of |pred_i - gt|_1; 32: EPE sum of

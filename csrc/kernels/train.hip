@@ -452,9 +452,47 @@ __global__ __launch_bounds__(256) void pack_pieces_kernel(const PackPiece* __res
   }
 }
 
+// Correlation-pyramid backward, first half (jax_raft/model.py:443-445,472-481):
+// the 2x2 floor average-pooling adjoints of every level summed into the
+// full-resolution volume gradient, scaled by the 1/sqrt(C) of the volume and
+// stored bf16 for the two GEMMs dfmap1 = dC fmap2, dfmap2 = dC^T fmap1.
+//   dC[q][y][x] = s * sum_l g_l[q][y >> l][x >> l] / 4^l   (y < h_l 2^l, x < w_l 2^l)
+__global__ __launch_bounds__(256) void pyr_bwd_dc_kernel(const float* __restrict__ g0, const float* __restrict__ g1,
+                                                         const float* __restrict__ g2, const float* __restrict__ g3,
+                                                         int L, long M, int h, int w, float scale,
+                                                         bf16* __restrict__ dc) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  const long hw = (long)h * w;
+  if (e >= M * hw) return;
+  const long q = e / hw;
+  const int r = (int)(e - q * hw);
+  const int y = r / w, x = r - (r / w) * w;
+  float v = g0[e];
+  const float* gl[3] = {g1, g2, g3};
+  int hl = h, wl = w;
+#pragma unroll
+  for (int l = 1; l < 4; ++l) {
+    hl >>= 1;
+    wl >>= 1;
+    if (l < L) {
+      const int yy = y >> l, xx = x >> l;
+      if (yy < hl && xx < wl) v += gl[l - 1][(q * hl + yy) * wl + xx] * (1.0f / (float)(1 << (2 * l)));
+    }
+  }
+  dc[e] = f2bf(v * scale);
+}
+
 inline unsigned nblk(long total, int bs) { return (unsigned)((total + bs - 1) / bs); }
 
 }  // namespace
+
+extern "C" int jr_pyr_bwd_dc(const float* g0, const float* g1, const float* g2, const float* g3, int L, long M, int h,
+                             int w, float scale, void* dc, hipStream_t stream) {
+  if (L < 1 || L > 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(pyr_bwd_dc_kernel, dim3(nblk(M * h * w, 256)), dim3(256), 0, stream, g0, g1, g2, g3, L, M, h, w,
+                     scale, (bf16*)dc);
+  return (int)hipGetLastError();
+}
 
 extern "C" int jr_pack_pieces(const void* table, int n, long max_elems, hipStream_t stream) {
   if (n <= 0) return 0;

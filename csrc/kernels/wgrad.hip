@@ -210,29 +210,46 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
   }
 }
 
-// dW_hwio[kh][kw][ci][co] = sum_z part[z][co][(kh*KW + kw)*cin8 + ci] (ci < cin), db[co] = sum_z bpart[z][co]
+// dW_hwio[kh][kw][ci][co] = sum_z part[z][co][(kh*KW + kw)*cin8 + ci] (ci < cin), db[co] = sum_z bpart[z][co].
+// Block = one output channel co x 32 consecutive k: thread (k lane, z group of 8) sums
+// every 8th split along z with coalesced reads (k is the partials' contiguous dim),
+// the 8 groups combine through LDS in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, const float* __restrict__ bpart,
                                                            int S, int cout_pad, int kpad, int KH, int KW, int cin8,
                                                            int cin, int cout, float* __restrict__ dw,
                                                            float* __restrict__ db) {
-  const long total = (long)KH * KW * cin * cout;
-  const long e = (long)blockIdx.x * 256 + threadIdx.x;
-  if (e < total) {
-    const int co = (int)(e % cout);
-    const long r = e / cout;
-    const int ci = (int)(r % cin);
-    const int tap = (int)(r / cin);
-    const long k = (long)tap * cin8 + ci;
+  __shared__ float red[8][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int co = blockIdx.y;
+  const int k = blockIdx.x * 32 + tx;
+  const long zs = (long)cout_pad * kpad;
+  float s = 0.f;
+  if (k < kpad) {
     const float* pp = part + (long)co * kpad + k;
-    const long zs = (long)cout_pad * kpad;
-    float s = 0.f;
-    for (int z = 0; z < S; ++z) s += pp[z * zs];
-    dw[e] = s;
+#pragma unroll 4
+    for (int z = ty; z < S; z += 8) s += pp[z * zs];
   }
-  if (db && e < cout) {
-    float s = 0.f;
-    for (int z = 0; z < S; ++z) s += bpart[(long)z * cout_pad + e];
-    db[e] = s;
+  red[ty][tx] = s;
+  float b = 0.f;
+  if (db && blockIdx.x == 0 && tx == 0)
+    for (int z = ty; z < S; z += 8) b += bpart[(long)z * cout_pad + co];
+  __syncthreads();
+  if (ty == 0) {
+    float v = red[0][tx];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) v += red[j][tx];
+    const int tap = k / cin8, ci = k - tap * cin8;
+    if (tap < KH * KW && ci < cin) dw[((long)tap * cin + ci) * cout + co] = v;
+  }
+  __syncthreads();
+  if (db && blockIdx.x == 0) {
+    if (tx == 0) red[ty][0] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float v = red[0][0];
+      for (int j = 1; j < 8; ++j) v += red[j][0];
+      db[co] = v;
+    }
   }
 }
 
@@ -282,9 +299,7 @@ extern "C" int jr_wgrad(const void* x, int xcs, int xoff, int N, int H, int W, i
   else if (bk) r = launch<64, 128>(p, S, stream);
   else r = launch<64, 64>(p, S, stream);
   if (r) return r;
-  const long total = (long)KH * KW * cin * cout;
-  const long nthreads = std::max<long>(total, cout);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, stream, part,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((p.K + 31) / 32), (unsigned)cout), dim3(256), 0, stream, part,
                      p.bpart, S, cp, kp, KH, KW, cin8, cin, cout, dw, db);
   return (int)hipGetLastError();
 }

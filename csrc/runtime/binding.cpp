@@ -850,6 +850,25 @@ void conv_train_op(const TList& t, IList i, double alpha, const TList& tx, IList
   run_now(make_conv(t, i, alpha, nullptr, &tx, &ix));
 }
 void upsample_convex_bwd_op(const TList& t, IList i, double alpha) { run_now(make_upsample_convex_bwd(t, i, alpha, nullptr)); }
+// t = [dc (bf16 [M][h][w]), g0, g1?, g2?, g3?], i = [L, M, h, w]
+void pyr_bwd_dc_op(const TList& t, IList i, double scale) {
+  at::Tensor dc = opt(t, 0);
+  TORCH_CHECK(i.size() == 4, "pyr_bwd_dc: expected [L, M, h, w]");
+  const int L = (int)i[0], h = (int)i[2], w = (int)i[3];
+  const int64_t M = i[1];
+  check_bf16(dc, "dc");
+  TORCH_CHECK(L >= 1 && L <= 4 && dc.numel() >= M * h * w, "pyr_bwd_dc: shapes");
+  const float* g[4] = {nullptr, nullptr, nullptr, nullptr};
+  int hl = h, wl = w;
+  for (int l = 0; l < L; ++l) {
+    at::Tensor v = opt(t, 1 + l);
+    check_f32(v, "level gradient");
+    TORCH_CHECK(v.numel() >= M * hl * wl, "pyr_bwd_dc: level ", l, " size");
+    g[l] = v.data_ptr<float>();
+    hl >>= 1; wl >>= 1;
+  }
+  JR_CHECK_OK(jr_pyr_bwd_dc(g[0], g[1], g[2], g[3], L, M, h, w, (float)scale, dc.data_ptr(), cur_stream()));
+}
 void wgrad_op(const TList& t, IList i) {
   std::vector<at::Tensor> keep;
   run_now(make_wgrad(t, i, &keep));
@@ -1176,6 +1195,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("norm_bwd(Tensor?[] t, int[] i, float eps) -> ()", &jr::norm_bwd_op);
   m.def("pack(Tensor?[] t, int[] i) -> ()", &jr::pack_op);
   m.def("wgrad(Tensor?[] t, int[] i) -> ()", &jr::wgrad_op);
+  m.def("pyr_bwd_dc(Tensor?[] t, int[] i, float scale) -> ()", &jr::pyr_bwd_dc_op);
   m.def("upsample_bilinear_bwd(Tensor?[] t, int[] i) -> ()", &jr::upsample_bilinear_bwd_op);
   m.def("seq_loss(Tensor?[] t, int[] i, float max_flow) -> ()", &jr::seq_loss_op);
   m.def("seq_loss_blocks(int P) -> int", &jr::seq_loss_blocks_op);

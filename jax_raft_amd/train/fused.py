@@ -717,7 +717,7 @@ class FusedLoop:
         self.gen += 1
         return self.out.clone()
 
-    def backward(self, gout: torch.Tensor, gen: int):
+    def backward(self, gout: torch.Tensor, gen: int, fe_dy=None):
         if gen != self.gen or self.done_gen == gen:
             raise RuntimeError("fused refinement loop: this backward's saved activations were overwritten by a "
                                "later forward of the same loop (run backward before the next forward) or it "
@@ -725,10 +725,35 @@ class FusedLoop:
         self.done_gen = gen
         self.gout.copy_(gout)
         self._run(self.plan_b)
-        return self._finish()
+        return self._finish(fe_dy)
+
+    def _pyramid_backward(self, out1=None, out2=None):
+        """Correlation pyramid backward: the pooling adjoints of all levels as one
+        native pass to a bf16 volume gradient dC (with the 1/sqrt(C) scale), then
+        dfmap1 = dC fmap2 and dfmap2 = dC^T fmap1 as batched bf16 GEMMs with fp32
+        accumulation (written straight into ``out1`` / ``out2`` when given)."""
+        B, h, w, C = self.B, self.h, self.w, self.fmap_ch
+        hw = h * w
+        if getattr(self, "_dC", None) is None:
+            self._dC = torch.empty(B, hw, hw, dtype=BF16, device=self.device)
+        nat.ops().pyr_bwd_dc([self._dC] + self.lv_grads + [None] * (4 - self.L), [self.L, self.M, h, w],
+                             1.0 / float(C) ** 0.5)
+        f1 = self.fm1.reshape(B, hw, C)
+        f2 = self.fm2.reshape(B, hw, C)
+        if out1 is not None:
+            torch.bmm(self._dC, f2, out=out1.reshape(B, hw, C))
+            torch.bmm(self._dC.transpose(1, 2), f1, out=out2.reshape(B, hw, C))
+            return out1, out2
+        try:
+            g1 = torch.bmm(self._dC, f2, out_dtype=F32)
+            g2 = torch.bmm(self._dC.transpose(1, 2), f1, out_dtype=F32)
+        except (RuntimeError, TypeError):
+            g1 = torch.bmm(self._dC, f2).float()
+            g2 = torch.bmm(self._dC.transpose(1, 2), f1).float()
+        return g1.reshape(B, h, w, C), g2.reshape(B, h, w, C)
 
     # ---------------------------------------------------- weight gradients
-    def _finish(self):
+    def _finish(self, fe_dy=None):
         """After the backward plan (data gradients + stacked weight gradients):
         the context share of the ConvGRU gates (iteration sums), the assembly of
         the gate / flow-head kernels, the pyramid and context-encoder input
@@ -764,11 +789,10 @@ class FusedLoop:
             A[mr.bias].copy_(self.fh1b[fhn:fhn + mh])
         A[fh.conv2.kernel].copy_(torch.flip(self.fh2w, dims=(0, 1)).permute(0, 1, 3, 2))
         A[fh.conv2.bias].copy_(self.ddelta.reshape(-1, 8)[:, :2].sum(0, dtype=F32))
-        # correlation pyramid: pooling adjoints + the two GEMMs of fmap1 fmap2^T / sqrt(C)
-        from ..ops.autograd import pyramid_backward
-
-        g1, g2 = pyramid_backward(self.fm1, self.fm2, (self.B, self.h, self.w, self.h, self.w, self.fmap_ch, self.L),
-                                  self.lv_grads)
+        if fe_dy is not None:   # whole-model path: straight into the feature encoder's bf16 output gradient
+            g1, g2 = self._pyramid_backward(fe_dy[: self.B], fe_dy[self.B:])
+        else:
+            g1, g2 = self._pyramid_backward()
         # context-encoder output gradient: [tanh'(h0) dh | relu'(ctx) dctx]
         h0 = self.hf[0, 0]
         dc = torch.empty(M, hd + C, device=self.device, dtype=F32)
@@ -833,9 +857,7 @@ class FusedModel:
 
     def backward(self, gout, gen: int):
         B = self.B
-        g1, g2, dctx, pgrads = self.loop.backward(gout, gen)
-        self.fe.dy_out[:B].copy_(g1)
-        self.fe.dy_out[B:].copy_(g2)
+        _, _, dctx, pgrads = self.loop.backward(gout, gen, fe_dy=self.fe.dy_out)
         self.ce.dy_out.copy_(dctx)
         grads = {id(p): g for p, g in zip(self.loop.params, pgrads)}
         grads.update(self.fe.backward())

@@ -53,9 +53,9 @@ def main():
     L._SeqLoss.forward = staticmethod(timed("loss_fwd", L._SeqLoss.forward))
     orig_backward = F.FusedLoop.backward
 
-    def bwd(self, gout, gen):
+    def bwd(self, gout, gen, fe_dy=None):
         if gen != self.gen or self.done_gen == gen:
-            return orig_backward(self, gout, gen)
+            return orig_backward(self, gout, gen, fe_dy)
         self.done_gen = gen
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -63,7 +63,7 @@ def main():
         self._run(self.plan_b)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        r = self._finish()
+        r = self._finish(fe_dy)
         torch.cuda.synchronize()
         T_["loop_bwd_plan"] += t1 - t0
         T_["loop_wgrad_finish"] += time.perf_counter() - t1
