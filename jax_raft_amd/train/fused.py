@@ -247,6 +247,11 @@ class FusedLoop:
         self.M = B * self.h * self.w
         self.device = torch.device(device)
         self.use_graph = use_graph
+        # side lanes of the plans (flow features / mask head in the forward, the motion
+        # encoder's backward): opt-in, JR_FUSED_LANES=1.  Measured on MI355X (config 5):
+        # 183 pairs/s with lanes vs 267 on one in-order stream (cross-lane event waits in
+        # the captured graphs cost more than the overlap of the per-iteration kernels gains)
+        self.lanes = 1 if os.environ.get("JR_FUSED_LANES", "0") == "1" else 0
         self.gen = 0            # forward generation (a backward must match the latest forward)
         self.done_gen = -1
         self._analyse()
@@ -551,13 +556,26 @@ class FusedLoop:
         P.set_lane(0)
         T, G, hd, B, h, w = self.T, self.G, self.hd, self.B, self.h, self.w
         cl, fl = self.cl, self.fl
+        # lanes: 0 = critical path (lookup -> correlation convs -> motion conv -> GRUs -> flow
+        # head -> coordinate update), 1 = flow-feature convs of the next iteration's flow,
+        # 2 = mask head + x8 upsampling (read only per-iteration buffers; joined at the end)
+        E_PACK, E_FT, E_FLOW, E_FH = 0, 1, 2, 3
+        lanes = self.lanes
         self.packer.record(P)   # this step's weights -> every spec (forward and data-gradient layouts)
         P.add_corr([self.fm1, self.fm2] + self.levels + [None] * (4 - self.L), [B, h, w, self.fmap_ch, self.L],
                    1.0 / float(self.fmap_ch) ** 0.5)
+        P.add_record(E_PACK)
         for g in range(G):  # loop-invariant context share of every gate (+ biases), fp32
             self._conv(P, f"gC{g}", self.ctx_in, self.gbias[g])
         for t in range(T):
             hx0, qx0 = self.hx[0, t], self.qx[0, t]
+            P.set_lane(lanes)
+            P.add_wait(E_PACK)
+            P.add_wait(E_FT)   # flow8[t] written by the previous iteration's coordinate update
+            self._conv(P, "cf1", self.flow8[t], self.f1[t], act=ACT_RELU)
+            self._conv(P, "cf2", self.f1[t], self.cf[t], y_coff=cl[-1], act=ACT_RELU)
+            P.add_record(E_FLOW)
+            P.set_lane(0)
             P.add_lookup([self.coords[t], self.corr[t]] + self.levels + [None] * (4 - self.L),
                          [self.L, B, h, w, self.radius])
             if len(cl) == 2:
@@ -565,8 +583,7 @@ class FusedLoop:
                 self._conv(P, "cc2", self.c1[t], self.cf[t], act=ACT_RELU)
             else:
                 self._conv(P, "cc1", self.corr[t], self.cf[t], act=ACT_RELU)
-            self._conv(P, "cf1", self.flow8[t], self.f1[t], act=ACT_RELU)
-            self._conv(P, "cf2", self.f1[t], self.cf[t], y_coff=cl[-1], act=ACT_RELU)
+            P.add_wait(E_FLOW)
             self._conv(P, "mc", self.cf[t], hx0, y_coff=hd, act=ACT_RELU, y2=qx0, y2_coff=hd)
             for g in range(1, G):  # [motion | flow] into the other GRUs' inputs
                 P.add_copy_channels([hx0, self.hx[g, t]], [hd, hd, self.M, self.mot_cs])
@@ -587,12 +604,17 @@ class FusedLoop:
             P.add_copy([self.coords[t], self.coords[t + 1]])
             P.add_flow_taps([self.taps, self._fh2_bias, self.coords[t + 1], self.flow32[t], hn, self.qx[0, t + 1],
                              self.flow8[t + 1]], [B, h, w, self.flow_off, self.flow_off])
+            P.add_record(E_FT)
+            P.add_record(E_FH)
+            P.set_lane(2 * lanes)
+            P.add_wait(E_FH)
             if self.has_mask:
                 self._conv(P, "mask", self.fmm[t], self.mask[t], x_coff=self.fh_hidden,
                            alpha=self.mp.multiplier)
                 P.add_upsample_convex([self.mask[t], self.flow32[t], self.out[t]], [B, h, w, 0])
             else:
                 P.add_upsample_bilinear([self.flow32[t], self.out[t]], [B, h, w, 0])
+            P.set_lane(0)
         return P
 
     def _build_bwd(self):
@@ -601,6 +623,7 @@ class FusedLoop:
         P.set_lane(0)
         T, G, hd, B, h, w = self.T, self.G, self.hd, self.B, self.h, self.w
         cl = self.cl
+        E_DM, E_ME = 0, 1
         for g_ in self.lv_grads:
             P.add_memset([g_])
         for t in reversed(range(T)):
@@ -634,6 +657,11 @@ class FusedLoop:
                     self._bconv(P, "gAT0", self.dzr[0, t], split=hd, s0=Seg(gin=self.dh[0], out=self.dh_next),
                                 s1=Seg(gin=self.dmot, mask=self.hx[0, t], mask_coff=hd, valid=self.mot_out - 2,
                                        out=self.dm[t]))
+            # the motion encoder's backward (-> pyramid lookup scatter) only feeds the weight
+            # gradients: lane 1, overlapping the next (earlier) iteration's head / GRU backward
+            P.add_record(E_DM)
+            P.set_lane(self.lanes)
+            P.add_wait(E_DM)
             self._bconv(P, "mcT", self.dm[t], s1=Seg(mask=self.cf[t], out=self.dcf[t]))
             if len(cl) == 2:
                 self._bconv(P, "cc2T", self.dcf[t], s1=Seg(mask=self.c1[t], out=self.dc1[t]))
@@ -643,6 +671,9 @@ class FusedLoop:
             P.add_lookup_bwd([self.coords[t], self.dcorr] + self.lv_grads + [None] * (4 - self.L),
                              [self.L, B, h, w, self.radius])
             self._bconv(P, "cf2T", self.dcf[t], x_coff=cl[-1], s1=Seg(mask=self.f1[t], out=self.df1[t]))
+            P.add_record(E_ME)
+            P.set_lane(0)
+        P.add_wait(E_ME)
         self._record_wgrads(P)
         return P
 
@@ -847,21 +878,37 @@ class FusedModel:
         """Parameters re-allocated (e.g. moved) since the plans were recorded."""
         return self.loop.stale() or self.fe.packer.stale() or self.ce.packer.stale()
 
+    def _side(self):
+        """The context encoder's stream: its plans overlap the feature encoder's
+        (independent branches, model.py:562 vs :569)."""
+        if getattr(self, "_side_stream", None) is None:
+            self._side_stream = torch.cuda.Stream(device=self.loop.device)
+        return self._side_stream
+
     def forward(self, image1, image2, train: bool) -> torch.Tensor:
         self.img1.copy_(image1)
         self.img2.copy_(image2)
         nat.ops().prep([self.img1, self.img2, self.x0], [self.B, self.H, self.W])
+        cur, side = torch.cuda.current_stream(self.loop.device), self._side()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            self.ce.forward(update_stats=train)
         self.fe.forward(update_stats=train)
-        self.ce.forward(update_stats=train)
+        cur.wait_stream(side)
         return self.loop.forward_prepared(self.loop.ctx_raw)
 
     def backward(self, gout, gen: int):
-        B = self.B
         _, _, dctx, pgrads = self.loop.backward(gout, gen, fe_dy=self.fe.dy_out)
         self.ce.dy_out.copy_(dctx)
+        cur, side = torch.cuda.current_stream(self.loop.device), self._side()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            self.ce.run_backward()
+        self.fe.run_backward()
+        cur.wait_stream(side)
         grads = {id(p): g for p, g in zip(self.loop.params, pgrads)}
-        grads.update(self.fe.backward())
-        grads.update(self.ce.backward())
+        grads.update(self.fe.arena.snapshot())
+        grads.update(self.ce.arena.snapshot())
         return [grads.get(id(p)) for p in self.params]
 
 

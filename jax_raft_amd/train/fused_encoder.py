@@ -312,9 +312,9 @@ class EncoderTrain:
                     bn.mean.mul_(bn.momentum).add_((1.0 - bn.momentum) * m)
                     bn.var.mul_(bn.momentum).add_((1.0 - bn.momentum) * v)
 
-    def backward(self) -> Dict[int, torch.Tensor]:
+    def run_backward(self) -> None:
         """Runs the backward plan (``dy_out`` must be filled): data gradients,
-        then every conv's weight / bias gradient; returns {id(param): grad}."""
+        then every conv's weight / bias gradient into :attr:`arena`."""
         self._run(self.plan_b)
         if self.mode == 2:
             for u in self.units:
@@ -322,4 +322,8 @@ class EncoderTrain:
                     r = u.red.sum(0)
                     self.arena[u.norm_mod.scale].copy_(r[:, 1])
                     self.arena[u.norm_mod.bias].copy_(r[:, 0])
+
+    def backward(self) -> Dict[int, torch.Tensor]:
+        """:meth:`run_backward`, then {id(param): grad} (a fresh copy)."""
+        self.run_backward()
         return self.arena.snapshot()

@@ -58,6 +58,19 @@ class TrainConfig:
     fault_nan_step: int = -1       # fault injection: poison the loss of this step (tests)
 
 
+def _adamw(params, cfg: TrainConfig, device):
+    """AdamW; on the GPU the single-kernel (fused) implementation when this
+    PyTorch build provides it -- one launch for all ~230 parameter tensors."""
+    params = list(params)
+    kw = dict(lr=cfg.lr, weight_decay=cfg.weight_decay, eps=cfg.eps)
+    if device is not None and torch.device(device).type == "cuda":
+        try:
+            return torch.optim.AdamW(params, fused=True, **kw)
+        except (RuntimeError, TypeError, ValueError):
+            pass
+    return torch.optim.AdamW(params, **kw)
+
+
 class Trainer:
     def __init__(self, cfg: TrainConfig, device: Optional[torch.device] = None):
         self.cfg = cfg
@@ -71,7 +84,7 @@ class Trainer:
         if cfg.sync_bn and self.world > 1:
             dp.convert_sync_batchnorm(self.model)
         self.sync = dp.GradAllReducer(self.model, bucket_mb=cfg.bucket_mb)
-        self.opt = torch.optim.AdamW(self.model.parameters(), lr=cfg.lr, weight_decay=cfg.weight_decay, eps=cfg.eps)
+        self.opt = _adamw(self.model.parameters(), cfg, self.device)
         self.sched = torch.optim.lr_scheduler.OneCycleLR(
             self.opt, cfg.lr, total_steps=cfg.steps + 100, pct_start=0.05, cycle_momentum=False,
             anneal_strategy="linear")

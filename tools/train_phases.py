@@ -46,7 +46,7 @@ def main():
     m.feature_encoder.forward = timed("fe_fwd (autograd)", m.feature_encoder.forward)
     m.context_encoder.forward = timed("ce_fwd (autograd)", m.context_encoder.forward)
     FE.EncoderTrain.forward = timed("encoders_fwd (plans)", FE.EncoderTrain.forward)
-    FE.EncoderTrain.backward = timed("encoders_bwd (plan + wgrad)", FE.EncoderTrain.backward)
+    FE.EncoderTrain.run_backward = timed("encoders_bwd (plan + wgrad)", FE.EncoderTrain.run_backward)
     F.FusedLoop.forward_prepared = timed("loop_fwd", F.FusedLoop.forward_prepared)
     from jax_raft_amd.train import loss as L
 
