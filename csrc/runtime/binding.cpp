@@ -1106,7 +1106,22 @@ class Plan : public torch::CustomClassHolder {
     hipStream_t s = st[o.lane];
     if (debug_) fprintf(stderr, "[plan] it=%d lane=%d %s stream=%p\n", it, o.lane, o.name.c_str(), (void*)s);
     switch (o.kind) {
-      case OP_LAUNCH: return o.l(s, it);
+      case OP_LAUNCH: {
+        const int r = o.l(s, it);
+        // JR_PLAN_CHECK=1 (eager run only): synchronise after every launch so an asynchronous
+        // fault or launch error is attributed to the op that caused it (fault localisation,
+        // SURVEY.md 5.2); the failing op's segment index, lane, iteration and name are reported.
+        if (check_ && !capturing_) {
+          hipError_t e = r ? (hipError_t)r : hipStreamSynchronize(s);
+          if (e == hipSuccess) e = hipGetLastError();
+          if (e != hipSuccess) {
+            fprintf(stderr, "[plan check] op '%s' (lane %d, iteration %d) failed: %s\n", o.name.c_str(), o.lane, it,
+                    hipGetErrorString(e));
+            return (int)e;
+          }
+        }
+        return r;
+      }
       case OP_RECORD: recorded[o.ev] = (char)(1 + o.lane); return (int)hipEventRecord(events_[o.ev], s);
       default:
         if (!recorded[o.ev] || recorded[o.ev] == 1 + o.lane) return 0;
@@ -1116,6 +1131,8 @@ class Plan : public torch::CustomClassHolder {
   // part: -1 = the whole forward, 0 = prologue only, 1 = loop + epilogue only.
   int enqueue(hipStream_t s, int n_iters, bool capturing = false, int part = -1) {
     if (int r = ensure_resources()) return r;
+    check_ = std::getenv("JR_PLAN_CHECK") != nullptr && std::getenv("JR_PLAN_CHECK")[0] == '1';
+    capturing_ = capturing;
     // Eager: lane 0 is the private high-priority stream, forked from the caller's.
     // Capture: lane 0 is the capture stream itself (created with the greatest
     // priority); a capture whose origin stream holds only the fork/join event
@@ -1169,6 +1186,8 @@ class Plan : public torch::CustomClassHolder {
   hipGraphExec_t pexec_[2] = {};
   int64_t pcaptured_[2] = {-1, -1};
   bool debug_ = false;
+  bool check_ = false;
+  bool capturing_ = false;
 };
 
 }  // namespace jr

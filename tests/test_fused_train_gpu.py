@@ -275,3 +275,18 @@ def test_native_wgrad(case):
     torch.cuda.synchronize()
     assert _rel(dw, k.grad) < 1e-3, _rel(dw, k.grad)
     assert _rel(db, b.grad) < 1e-3
+
+
+def test_race_check_tool():
+    """tools/race_check.py: inference (graph / eager) and a fused training step
+    are bitwise reproducible, and equal under serialised kernel launches
+    (AMD_SERIALIZE_KERNEL=3) and per-op checked plans (JR_PLAN_CHECK=1)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "race_check.py"), "--size", "128", "128",
+                        "--iters", "2"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "race check ok" in r.stdout

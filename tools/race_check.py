@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Race / determinism check of the native paths.
+
+GPU address sanitizers are unavailable on this pool, so races between
+kernels (a missing stream / event dependency in a plan, a read of a buffer
+another lane still writes) are hunted the way they show: as run-to-run
+differences.  Every native path here is deterministic by construction (no
+float atomics; fixed-order reductions), so
+
+1. the inference engine (hipGraph replay and eager plan launches) and one
+   fused training step are run twice in this process and must be bitwise
+   equal; then
+2. the same computation runs in child processes with
+   ``AMD_SERIALIZE_KERNEL=3`` (every launch serialised by the runtime: no
+   concurrency, so no race can fire) and with ``JR_PLAN_CHECK=1`` (eager
+   plans synchronised and error-checked after every op, with the failing op
+   named), and their outputs must equal the concurrent run bitwise.
+
+Usage: ``python tools/race_check.py [--size H W] [--iters N]``; exit 0 on success.
+"""
+import argparse
+import os
+import subprocess
+import sys
+import tempfile
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def compute(size, iters):
+    import torch
+
+    from jax_raft_amd import raft_large
+    from jax_raft_amd.train.loss import sequence_loss
+
+    torch.manual_seed(0)
+    model, _ = raft_large()
+    model = model.cuda()
+    g = torch.Generator().manual_seed(1)
+    H, W = size
+    i1 = (torch.rand(2, H, W, 3, generator=g) * 2 - 1).cuda()
+    i2 = (torch.rand(2, H, W, 3, generator=g) * 2 - 1).cuda()
+    gt = (torch.randn(2, H, W, 2, generator=g) * 3).cuda()
+    out = {}
+    model.eval()
+    with torch.no_grad():
+        out["infer_graph"] = model(i1, i2, num_flow_updates=iters).cpu()
+        out["infer_graph_2"] = model(i1, i2, num_flow_updates=iters).cpu()
+        out["infer_eager"] = model(i1, i2, num_flow_updates=iters, use_graph=False).cpu()
+    model.train()
+    state = {k: v.clone() for k, v in model.state_dict().items()}
+    for rep in range(2):
+        model.load_state_dict(state)
+        model.zero_grad(set_to_none=True)
+        preds = model(i1, i2, train=True, num_flow_updates=iters)
+        loss, _ = sequence_loss(preds, gt)
+        loss.backward()
+        out[f"train_preds_{rep}"] = preds.detach().cpu()
+        out[f"train_grads_{rep}"] = torch.cat([p.grad.detach().float().flatten().cpu() for p in model.parameters()])
+    torch.cuda.synchronize()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, nargs=2, default=[128, 256])
+    ap.add_argument("--iters", type=int, default=4)
+    ap.add_argument("--child", default=None, help=argparse.SUPPRESS)
+    a = ap.parse_args()
+    import torch
+
+    if a.child:
+        torch.save(compute(a.size, a.iters), a.child)
+        return 0
+    ref = compute(a.size, a.iters)
+    bad = []
+    for k1, k2 in (("infer_graph", "infer_graph_2"), ("infer_graph", "infer_eager"),
+                   ("train_preds_0", "train_preds_1"), ("train_grads_0", "train_grads_1")):
+        if not torch.equal(ref[k1], ref[k2]):
+            bad.append(f"{k1} != {k2} (max |diff| {(ref[k1] - ref[k2]).abs().max().item():.3g})")
+    with tempfile.TemporaryDirectory() as d:
+        for name, env in (("serialised", {"AMD_SERIALIZE_KERNEL": "3"}), ("plan-check", {"JR_PLAN_CHECK": "1"})):
+            path = os.path.join(d, name + ".pt")
+            e = dict(os.environ, **env)
+            if name == "plan-check":
+                e["JR_FUSED_GRAPH"] = "0"   # eager plans: the per-op check runs outside graph capture
+            r = subprocess.run([sys.executable, __file__, "--size", *map(str, a.size), "--iters", str(a.iters),
+                                "--child", path], env=e, timeout=900)
+            if r.returncode != 0:
+                bad.append(f"{name} child failed (exit {r.returncode})")
+                continue
+            other = torch.load(path, weights_only=True)
+            for k, v in ref.items():
+                if not torch.equal(v, other[k]):
+                    bad.append(f"{name}: {k} differs (max |diff| {(v - other[k]).abs().max().item():.3g})")
+    if bad:
+        print("RACE CHECK FAILED:\n  " + "\n  ".join(bad))
+        return 1
+    print(f"race check ok: {len(ref)} outputs bitwise equal across repeats, serialised launches and per-op checked plans")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
