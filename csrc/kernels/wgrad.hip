@@ -18,6 +18,7 @@
 //    gradient (column sums of dY, accumulated by the k-tile-0 workgroups
 //    from the staged dY registers).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "kernels.h"
@@ -76,54 +77,69 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
   const bool b_tap = tap < p.KH * p.KW && kk < p.K;
   const int kh = b_tap ? tap / p.KW : 0, kw = b_tap ? tap - (tap / p.KW) * p.KW : 0;
 
-  u32x4 ra[NA], rb[NB];
+  struct Regs { u32x4 a[NA]; u32x4 b[NB]; };
+  Regs ra;
   float bsum[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
   const bool do_bias = p.bpart != nullptr && blockIdx.x == 0;
 
-  auto issue = [&](int mb) {
+  // X rows of this thread: pixels m = stage base + rB + (256 / CB) i, tracked incrementally as
+  // (n, oh, ow) (no integer division in the loop); every issue() advances them by one stage
+  int xn[NB], xoh[NB], xow[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int m = m_begin + rB + (256 / CB) * i;
+    xn[i] = m / OHW;
+    const int rem = m - xn[i] * OHW;
+    xoh[i] = rem / p.OW;
+    xow[i] = rem - xoh[i] * p.OW;
+  }
+  int mb_next = m_begin;
+
+  auto issue = [&](Regs& r) {
+    const int mb = mb_next;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int m = mb + rA + (256 / CA) * i;
       const bool ok = a_ok && m < m_end;
       const unsigned off = (unsigned)(((long)m * p.ycs + p.yoff + co0 + 8 * cA) * 2);
-      ra[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ys, ok ? off : OOB, 0, 0));
+      r.a[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ys, ok ? off : OOB, 0, 0));
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int m = mb + rB + (256 / CB) * i;
-      bool ok = b_tap && m < m_end;
-      unsigned off = OOB;
-      if (ok) {
-        const int n = m / OHW, rem = m - n * OHW;
-        const int oh = rem / p.OW, ow = rem - oh * p.OW;
-        const int ih = oh * p.SH - p.PH + kh, iw = ow * p.SW - p.PW + kw;
-        ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-        off = ok ? (unsigned)(((((long)n * p.H + ih) * p.W + iw) * p.xcs + p.xoff + ci) * 2) : OOB;
+      const int ih = xoh[i] * p.SH - p.PH + kh, iw = xow[i] * p.SW - p.PW + kw;
+      const bool ok = b_tap && m < m_end && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      const unsigned off = (unsigned)(((((long)xn[i] * p.H + ih) * p.W + iw) * p.xcs + p.xoff + ci) * 2);
+      r.b[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xs, ok ? off : OOB, 0, 0));
+      xow[i] += WPX;   // advance to the next stage's pixel
+      while (xow[i] >= p.OW) {
+        xow[i] -= p.OW;
+        if (++xoh[i] == p.OH) { xoh[i] = 0; ++xn[i]; }
       }
-      rb[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xs, off, 0, 0));
     }
+    mb_next = mb + WPX;
   };
-  auto store = [&](int buf) {
+  auto store = [&](const Regs& r, int buf) {
     bf16* sA = smem + buf * (A_EL + B_EL);
     bf16* sB = sA + A_EL;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int r = rA + (256 / CA) * i;
-      const int u = (2 * cA) ^ swz<UA>(r);
-      *(u32x4*)(sA + r * BCO + 4 * u) = ra[i];
+      const int row = rA + (256 / CA) * i;
+      const int u = (2 * cA) ^ swz<UA>(row);
+      *(u32x4*)(sA + row * BCO + 4 * u) = r.a[i];
       if (do_bias) {
-        const bf16x8 v = __builtin_bit_cast(bf16x8, ra[i]);
+        const bf16x8 v = __builtin_bit_cast(bf16x8, r.a[i]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) bsum[j] += bf2f(v[j]);
       }
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int r = rB + (256 / CB) * i;
-      const int u = (2 * cB) ^ swz<UB>(r);
-      *(u32x4*)(sB + r * BKK + 4 * u) = rb[i];
+      const int row = rB + (256 / CB) * i;
+      const int u = (2 * cB) ^ swz<UB>(row);
+      *(u32x4*)(sB + row * BKK + 4 * u) = r.b[i];
     }
   };
 
@@ -167,20 +183,21 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
     }
   };
 
-  // register-staged double buffer: loads of stage s+1 fly while stage s multiplies
-  int mb = m_begin;
-  issue(mb);
-  store(0);
+  // Register-staged pipeline: the next stage's global loads fly while this stage
+  // multiplies (LDS double-buffered, one barrier per stage); loads past the split's
+  // end read zeros (range-checked).  (A second register set -- loads two stages
+  // ahead -- measured 10-15 % slower on the loop shapes: fewer resident waves.)
+  const int nst = (m_end - m_begin + WPX - 1) / WPX;
+  issue(ra);
+  store(ra, 0);
   __syncthreads();
-  int buf = 0;
-  for (mb += WPX; mb < m_end; mb += WPX) {
-    issue(mb);
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nst) issue(ra);
     compute(buf);
-    store(buf ^ 1);
+    if (st + 1 < nst) store(ra, buf ^ 1);
     __syncthreads();
-    buf ^= 1;
   }
-  compute(buf);
 
   // partial tile -> part[z][co][k]
   float* out = p.part + (long)blockIdx.z * p.cout_pad * p.kpad;
@@ -265,8 +282,9 @@ int launch(const WgParams& p, int S, hipStream_t st) {
 extern "C" int jr_wgrad_plan(int M, int K, int cout, int* S, int* cout_pad, int* kpad) {
   const int bco = cout > 64 ? 128 : 64, bkk = K > 64 ? 128 : 64;
   const int tiles = ((K + bkk - 1) / bkk) * ((cout + bco - 1) / bco);
-  // ~2 workgroups per CU, at least 4 stages of pixels per split
-  int s = std::max(1, std::min((512 + tiles - 1) / tiles, (M + 4 * WPX - 1) / (4 * WPX)));
+  // one round of 2 resident workgroups per CU (64 KB of LDS each): S = floor(512 / tiles)
+  // (rounding up left a few workgroups for a second round), >= 4 stages of pixels per split
+  int s = std::max(1, std::min(512 / tiles, (M + 4 * WPX - 1) / (4 * WPX)));
   *S = s;
   *cout_pad = (cout + bco - 1) / bco * bco;
   *kpad = (K + bkk - 1) / bkk * bkk;
@@ -287,6 +305,7 @@ extern "C" int jr_wgrad(const void* x, int xcs, int xoff, int N, int H, int W, i
   int s_, cp, kp;
   jr_wgrad_plan(p.M, p.K, cout, &s_, &cp, &kp);
   if (S <= 0) S = s_;
+  if (const char* e = std::getenv("JR_WGRAD_S")) S = std::max(1, std::min(S, atoi(e)));  // tuning probe (<= planned S)
   const int per = (p.M + S - 1) / S;
   p.px_split = (per + WPX - 1) / WPX * WPX;
   S = (p.M + p.px_split - 1) / p.px_split;
