@@ -191,6 +191,14 @@ int jr_wgrad(const void* x, int xcs, int xoff, int N, int H, int W, int cin8, in
 // fp32 level gradients g_l [M][h_l][w_l] (g1..g3 may be null past L levels).
 int jr_pyr_bwd_dc(const float* g0, const float* g1, const float* g2, const float* g3, int L, long M, int h, int w,
                   float scale, void* dc, hipStream_t stream);
+// BatchNorm bookkeeping table (train.hip): mode 0 running-stat update from per-(n, c)
+// (sum, sumsq) `src` [N][C][2] into dst0 = running mean, dst1 = running var (momentum as float
+// bits, count = N*HW); mode 1 affine gradients from the norm backward's [N][C][2] reduction:
+// dst0 = d scale, dst1 = d bias.  All fields 64-bit (host-built int64 table).
+struct BnRow {
+  int64_t src, dst0, dst1, N, C, count, momentum_bits, mode;
+};
+int jr_bn_table(const void* rows, int n, int max_c, hipStream_t stream);
 // Sequence loss over N <= 32 predictions pred fp32 [N][P][2] vs gt fp32 [P][2]
 // (valid: optional fp32 [P]): part fp32 [jr_seq_loss_blocks(P)][37] per-block
 // partial sums (0..N-1: sum over valid pixels of |pred_i - gt|_1; 32: EPE sum of

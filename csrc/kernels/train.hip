@@ -482,9 +482,46 @@ __global__ __launch_bounds__(256) void pyr_bwd_dc_kernel(const float* __restrict
   dc[e] = f2bf(v * scale);
 }
 
+// BatchNorm bookkeeping of the encoder training plans, one launch for all layers
+// (blockIdx.y = layer): forward (mode 0) the Flax running statistics
+// (model.py:147, momentum m: ra = m ra + (1 - m) batch, biased batch variance)
+// from the per-(n, c) (sum, sumsq) of the layer's conv output; backward (mode 1)
+// the scale / bias gradients (sum over n of the norm backward's (sum g xhat, sum g)).
+__global__ __launch_bounds__(256) void bn_table_kernel(const BnRow* __restrict__ rows) {
+  const BnRow r = rows[blockIdx.y];
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= r.C) return;
+  const float* st = (const float*)r.src;
+  float s0 = 0.f, s1 = 0.f;
+  for (int n = 0; n < r.N; ++n) {
+    s0 += st[((long)n * r.C + c) * 2];
+    s1 += st[((long)n * r.C + c) * 2 + 1];
+  }
+  float* a = (float*)r.dst0;
+  float* b = (float*)r.dst1;
+  if (r.mode == 0) {
+    const float mom = __builtin_bit_cast(float, (int)r.momentum_bits);
+    const float cnt = (float)r.count;
+    const float m = s0 / cnt;
+    const float v = fmaxf(s1 / cnt - m * m, 0.f);
+    a[c] = mom * a[c] + (1.f - mom) * m;
+    b[c] = mom * b[c] + (1.f - mom) * v;
+  } else {
+    a[c] = s1;   // d scale = sum g xhat
+    b[c] = s0;   // d bias  = sum g
+  }
+}
+
 inline unsigned nblk(long total, int bs) { return (unsigned)((total + bs - 1) / bs); }
 
 }  // namespace
+
+extern "C" int jr_bn_table(const void* rows, int n, int max_c, hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(bn_table_kernel, dim3((unsigned)((max_c + 255) / 256), (unsigned)n), dim3(256), 0, stream,
+                     (const BnRow*)rows);
+  return (int)hipGetLastError();
+}
 
 extern "C" int jr_pyr_bwd_dc(const float* g0, const float* g1, const float* g2, const float* g3, int L, long M, int h,
                              int w, float scale, void* dc, hipStream_t stream) {

@@ -395,6 +395,18 @@ static Launch make_wgrad(const TList& t, const IList& i, std::vector<at::Tensor>
   };
 }
 
+// t = [table (int64 [n][8] device), *referenced tensors (kept alive)], i = [n, max_c]
+static Launch make_bn_table(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor tab = opt(t, 0);
+  TORCH_CHECK(i.size() == 2, "bn_table: expected [n, max_c]");
+  TORCH_CHECK(tab.defined() && tab.is_cuda() && tab.is_contiguous() && tab.scalar_type() == at::kLong &&
+                  tab.numel() == i[0] * 8, "bn_table: table must be a contiguous int64 [n][8] GPU tensor");
+  if (keep) for (size_t k = 0; k < t.size(); ++k) { at::Tensor v = opt(t, k); if (v.defined()) keep->push_back(v); }
+  const void* tp = tab.data_ptr();
+  const int n = (int)i[0], mc = (int)i[1];
+  return [=](hipStream_t s, int) { return jr_bn_table(tp, n, mc, s); };
+}
+
 // t = [taps, dflow], i = [N, h, w]
 static Launch make_flow_gather_bwd(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
   at::Tensor taps = opt(t, 0), df = opt(t, 1);
@@ -964,6 +976,7 @@ class Plan : public torch::CustomClassHolder {
   void add_upsample_convex_bwd(TList t, IList i, double alpha) {
     push(make_upsample_convex_bwd(t, i, alpha, &keep_), "upsample_convex_bwd");
   }
+  void add_bn_table(TList t, IList i) { push(make_bn_table(t, i, &keep_), "bn_table"); }
   void add_wgrad(TList t, IList i) { push(make_wgrad(t, i, &keep_), "wgrad"); }
   void add_pack(TList t, IList i) { push(make_pack(t, i, &keep_), "pack"); }
   void add_norm_bwd(TList t, IList i, double eps) { push(make_norm_bwd(t, i, eps, &keep_), "norm_bwd"); }
@@ -1248,6 +1261,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_norm_bwd", &jr::Plan::add_norm_bwd)
       .def("add_pack", &jr::Plan::add_pack)
       .def("add_wgrad", &jr::Plan::add_wgrad)
+      .def("add_bn_table", &jr::Plan::add_bn_table)
       .def("add_upsample_bilinear_bwd", &jr::Plan::add_upsample_bilinear_bwd)
       .def("add_lookup_bwd", &jr::Plan::add_lookup_bwd)
       .def("add_im2col", &jr::Plan::add_im2col)

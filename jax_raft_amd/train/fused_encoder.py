@@ -216,6 +216,9 @@ class EncoderTrain:
                 x, H, W = out, hh, ww
         self.tuner(self.plan_f, self._specs[id(enc.conv)], x, N, H, W, self.y_out, act=ACT_NONE)
         self.final_x = x
+        if self.mode == 2:   # BatchNorm running statistics (Flax momentum semantics), one launch
+            self._bn_table(self.plan_f, [(u.st, u.norm_mod.mean, u.norm_mod.var, u.N, u.cout, u.N * u.OH * u.OW,
+                                          u.norm_mod.momentum, 0) for u in self.units])
 
     # ----------------------------------------------------------- backward
     def _dgrad(self, u: _Unit, dy: torch.Tensor, out: torch.Tensor, gin: Optional[torch.Tensor] = None):
@@ -289,6 +292,21 @@ class EncoderTrain:
             c = u.conv
             record_wgrad(self.plan_b, u.x, u.N, u.H, u.W, 0, u.cin8, tuple(c.kernel.shape), c.stride, c.padding,
                          u.dy, 0, self.arena[c.kernel], self.arena[c.bias])
+        if self.mode == 2:   # BatchNorm scale / bias gradients from the norm backward's reductions
+            self._bn_table(self.plan_b, [(u.red, self.arena[u.norm_mod.scale], self.arena[u.norm_mod.bias], u.N,
+                                          u.cout, 1, 0.0, 1) for u in self.units])
+
+    def _bn_table(self, plan, rows):
+        import struct
+
+        tab = []
+        for src, d0, d1, n, c, cnt, mom, mode in rows:
+            bits = struct.unpack("<i", struct.pack("<f", float(mom)))[0]
+            tab.append([src.data_ptr(), d0.data_ptr(), d1.data_ptr(), n, c, cnt, bits, mode])
+        t = torch.tensor(tab, dtype=torch.int64).to(self.device).contiguous()
+        self.bufs.append(t)
+        keep = [t] + [v for r in rows for v in r[:3]]
+        plan.add_bn_table(keep, [len(tab), max(r[4] for r in rows)])
 
     # ---------------------------------------------------------------- run
     def _run(self, plan):
@@ -299,29 +317,17 @@ class EncoderTrain:
         else:
             plan.run(0)
 
-    def forward(self, update_stats: bool, momentum: float = 0.99):
+    def forward(self, update_stats: bool = True):
+        """Runs the forward plan; with BatchNorm it also updates the running
+        statistics (the fused path trains with batch statistics only)."""
+        if self.mode == 2 and not update_stats:
+            raise ValueError("the fused encoder plans update BatchNorm statistics (train mode only)")
         self._run(self.plan_f)
-        if update_stats and self.mode == 2:
-            with torch.no_grad():
-                for u in self.units:
-                    bn = u.norm_mod
-                    s = u.st.sum(0)  # (C, 2)
-                    cnt = float(u.N * u.OH * u.OW)
-                    m = s[:, 0] / cnt
-                    v = (s[:, 1] / cnt - m * m).clamp_min(0.0)
-                    bn.mean.mul_(bn.momentum).add_((1.0 - bn.momentum) * m)
-                    bn.var.mul_(bn.momentum).add_((1.0 - bn.momentum) * v)
 
     def run_backward(self) -> None:
         """Runs the backward plan (``dy_out`` must be filled): data gradients,
         then every conv's weight / bias gradient into :attr:`arena`."""
         self._run(self.plan_b)
-        if self.mode == 2:
-            for u in self.units:
-                if u.norm_mod is not None:
-                    r = u.red.sum(0)
-                    self.arena[u.norm_mod.scale].copy_(r[:, 1])
-                    self.arena[u.norm_mod.bias].copy_(r[:, 0])
 
     def backward(self) -> Dict[int, torch.Tensor]:
         """:meth:`run_backward`, then {id(param): grad} (a fresh copy)."""

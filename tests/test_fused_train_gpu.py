@@ -103,8 +103,12 @@ def test_fused_matches_unfused(factory, encoders, monkeypatch):
     (w * (out_r - target).abs()).mean().backward()
     g_r = {n: p.grad for n, p in mc.named_parameters() if p.grad is not None}
     out_u, g_u = _run(model, i1, i2, target, iters, fused=False)
+    bufs_u = {k: v.clone() for k, v in model.state_dict().items() if k.endswith(".mean") or k.endswith(".var")}
     model.load_state_dict(state)
     out_f, g_f = _run(model, i1, i2, target, iters, fused=True)
+    for k, v in model.state_dict().items():   # BatchNorm running statistics updated alike
+        if k in bufs_u:
+            assert _rel(v, bufs_u[k]) < 1e-2, k
     assert out_f.shape == out_u.shape
     ef, eu = _rel(out_f, out_r), _rel(out_u, out_r)
     assert ef < max(2e-2, 1.5 * eu), (ef, eu)
