@@ -81,7 +81,9 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_f32(bias, "bias");
-  TORCH_CHECK(y.defined() && y.is_contiguous(), "y");
+  // EPI_CONVEX writes a (B, 8h, 8w, 2) block of the flows output, which may be a per-part
+  // view (engine split mode) -- check_flow_out validates that block; all else is dense
+  TORCH_CHECK(y.defined() && ((int)i[19] == EPI_CONVEX || y.is_contiguous()), "conv: y must be contiguous");
   ConvParams p{};
   p.x = x.data_ptr();
   p.N = (int)i[0]; p.H = (int)i[1]; p.W = (int)i[2];

@@ -208,3 +208,24 @@ def test_streams_auto_matches_lanes_and_single_lane():
         torch.cuda.synchronize()
         assert (d[-1] - c[-1]).abs().max().item() < 1e-3
         assert eng._states[(B, 128, 128, 3, False)].plan.num_lanes() == 1
+
+
+def test_engine_split_parts_match_single():
+    """split=2 (independent batch halves, one graph each, concurrent lanes) with the
+    fused convex-upsample epilogue writing per-part views of the output."""
+    import torch
+
+    from jax_raft_amd import raft_large
+
+    torch.manual_seed(0)
+    model, _ = raft_large()
+    model = model.cuda().eval()
+    g = torch.Generator().manual_seed(2)
+    i1 = (torch.rand(4, 128, 160, 3, generator=g) * 2 - 1).cuda()
+    i2 = (torch.rand(4, 128, 160, 3, generator=g) * 2 - 1).cuda()
+    with torch.no_grad():
+        a = model(i1, i2, num_flow_updates=3)
+        b = model(i1, i2, num_flow_updates=3, split=2)
+    torch.cuda.synchronize()
+    assert a.shape == b.shape
+    assert ((a - b).abs().max() / (a.abs().max() + 1e-6)).item() < 1e-2
