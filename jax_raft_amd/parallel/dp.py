@@ -99,6 +99,35 @@ def broadcast_module(module: torch.nn.Module, src: int = 0) -> None:
             t.add_(0)  # bump the version counter (.data writes do not): invalidates cached weight packs
 
 
+class FlatGradComm:
+    """Asynchronous averaging of flat gradient buffers for the fused native
+    training step (:class:`jax_raft_amd.train.fused.FusedModel`), whose
+    gradients live in three flat fp32 arenas (refinement loop, feature
+    encoder, context encoder).  :meth:`start` launches an all-reduce of one
+    buffer on the communicator right when the backward has produced it -- the
+    loop's (~13 MB for raft_large) overlaps the encoders' backward -- with no
+    per-bucket concatenation; :meth:`finish` waits and divides by the world
+    size.  The parameters are then marked as reduced so the hook-based
+    :class:`GradAllReducer` skips them."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = world_size()
+        self._works: List[Tuple[object, torch.Tensor]] = []
+        self.reduced_ids: set = set()
+
+    def start(self, flat: torch.Tensor) -> None:
+        if self.world > 1:
+            self._works.append((dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True), flat))
+
+    def finish(self, params=()) -> None:
+        for work, flat in self._works:
+            work.wait()
+            flat.div_(self.world)
+        self._works = []
+        self.reduced_ids = {id(p) for p in params}
+
+
 class GradAllReducer:
     """Bucketed, backward-overlapped gradient averaging.
 
@@ -109,8 +138,10 @@ class GradAllReducer:
         sync.finish()            # waits for the in-flight buckets, writes averaged grads
     """
 
-    def __init__(self, module: torch.nn.Module, bucket_mb: float = 32.0, group=None):
+    def __init__(self, module: torch.nn.Module, bucket_mb: float = 32.0, group=None,
+                 flat_comm: Optional[FlatGradComm] = None):
         self.group = group
+        self.flat_comm = flat_comm
         self.params = [p for p in module.parameters() if p.requires_grad]
         self.world = world_size()
         cap = int(bucket_mb * 1024 * 1024 / 4)
@@ -138,14 +169,19 @@ class GradAllReducer:
         self._pending = [len(b) for b in self.buckets]
         self._works = {}
 
+    def _prereduced(self, p) -> bool:
+        return self.flat_comm is not None and id(p) in self.flat_comm.reduced_ids
+
     def _on_grad(self, p: torch.nn.Parameter):
+        if self._prereduced(p):
+            return  # averaged by the fused step's flat-buffer all-reduce
         b = self._bucket_of[id(p)]
         self._pending[b] -= 1
         if self._pending[b] == 0:
             self._launch(b)
 
     def _launch(self, b: int):
-        ps = self.buckets[b]
+        ps = [p for p in self.buckets[b] if not self._prereduced(p)]
         grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in ps]
         flat = torch.cat([g.reshape(-1).float() for g in grads])
         work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
@@ -157,13 +193,13 @@ class GradAllReducer:
         if self.world == 1:
             return
         for b in range(len(self.buckets)):
-            if b not in self._works:
+            if b not in self._works and not all(self._prereduced(p) for p in self.buckets[b]):
                 self._launch(b)
         for b, (work, flat) in self._works.items():
             work.wait()
             flat.div_(self.world)
             off = 0
-            for p in self.buckets[b]:
+            for p in [p for p in self.buckets[b] if not self._prereduced(p)]:
                 n = p.numel()
                 g = flat[off:off + n].view_as(p).to(p.dtype)
                 if p.grad is None:
@@ -171,6 +207,8 @@ class GradAllReducer:
                 else:
                     p.grad.copy_(g)
                 off += n
+        if self.flat_comm is not None:
+            self.flat_comm.reduced_ids = set()
         self._reset()
 
     def remove(self):

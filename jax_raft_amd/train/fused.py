@@ -112,6 +112,7 @@ class GradArena:
 
     def snapshot(self) -> Dict[int, torch.Tensor]:
         c = self.flat.clone()
+        self.last_snapshot = c   # the flat copy the returned views alias (data-parallel reduction)
         return {id(p): c[self._off[id(p)]:self._off[id(p)] + p.numel()].view(p.shape) for p in self.params}
 
 
@@ -830,6 +831,7 @@ class FusedLoop:
         dc[:, :hd] = self.dh_next * (1 - h0 * h0)
         dc[:, hd:] = dctx[:, :C] * (self.ctx_in[:, :C] > 0)
         grads = A.snapshot()
+        self.last_snapshot = A.last_snapshot
         return g1, g2, dc.reshape(self.B, self.h, self.w, hd + C), [grads[id(p)] for p in self.params]
 
 
@@ -898,7 +900,10 @@ class FusedModel:
         return self.loop.forward_prepared(self.loop.ctx_raw)
 
     def backward(self, gout, gen: int):
+        comm = _GRAD_COMM
         _, _, dctx, pgrads = self.loop.backward(gout, gen, fe_dy=self.fe.dy_out)
+        if comm is not None:   # data parallel: the loop's gradients reduce while the encoders run backward
+            comm.start(self.loop.last_snapshot)
         self.ce.dy_out.copy_(dctx)
         cur, side = torch.cuda.current_stream(self.loop.device), self._side()
         side.wait_stream(cur)
@@ -907,8 +912,13 @@ class FusedModel:
         self.fe.run_backward()
         cur.wait_stream(side)
         grads = {id(p): g for p, g in zip(self.loop.params, pgrads)}
-        grads.update(self.fe.arena.snapshot())
-        grads.update(self.ce.arena.snapshot())
+        for enc in (self.fe, self.ce):
+            snap = enc.arena.snapshot()
+            if comm is not None:
+                comm.start(enc.arena.last_snapshot)
+            grads.update(snap)
+        if comm is not None:
+            comm.finish(self.params)
         return [grads.get(id(p)) for p in self.params]
 
 
@@ -929,6 +939,14 @@ class FusedRAFT(torch.autograd.Function):
 
 
 _LOOPS: Dict[tuple, object] = {}
+_GRAD_COMM = None
+
+
+def set_grad_comm(comm) -> None:
+    """Register a flat-buffer gradient communicator (``parallel.dp.FlatGradComm``)
+    used by the whole-model fused step; ``None`` disables it."""
+    global _GRAD_COMM
+    _GRAD_COMM = comm
 
 
 def enabled() -> bool:

@@ -83,7 +83,12 @@ class Trainer:
         dp.broadcast_module(self.model)
         if cfg.sync_bn and self.world > 1:
             dp.convert_sync_batchnorm(self.model)
-        self.sync = dp.GradAllReducer(self.model, bucket_mb=cfg.bucket_mb)
+        self.flat_comm = dp.FlatGradComm() if self.world > 1 else None
+        self.sync = dp.GradAllReducer(self.model, bucket_mb=cfg.bucket_mb, flat_comm=self.flat_comm)
+        if self.flat_comm is not None and self.device.type == "cuda":
+            from . import fused
+
+            fused.set_grad_comm(self.flat_comm)
         self.opt = _adamw(self.model.parameters(), cfg, self.device)
         self.sched = torch.optim.lr_scheduler.OneCycleLR(
             self.opt, cfg.lr, total_steps=cfg.steps + 100, pct_start=0.05, cycle_momentum=False,

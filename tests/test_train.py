@@ -204,3 +204,74 @@ def test_sync_batchnorm_matches_full_batch_gloo(tmp_path):
     for n, p in enc.named_parameters():
         a, b = st[n], p.grad
         assert torch.allclose(a, b, rtol=1e-2, atol=1e-4 * gmax + 1e-2 * b.abs().max().item()), n
+
+
+class _FlatArenaFn(torch.autograd.Function):
+    """Stand-in for the fused training step: gradients of ``w`` are produced
+    into one flat buffer and averaged through FlatGradComm inside backward."""
+
+    @staticmethod
+    def forward(ctx, comm, x, w):
+        ctx.comm, ctx.w_param = comm, w
+        ctx.save_for_backward(x, w)
+        return x @ w
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        flat = (x.t() @ g).flatten().clone()
+        ctx.comm.start(flat)
+        ctx.comm.finish([ctx.w_param])
+        return None, g @ w.t(), flat.view(w.shape)
+
+
+def _flat_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from jax_raft_amd.parallel import dp
+
+    dp.init_distributed(backend="gloo")
+    model = _FlatModel()
+    comm = dp.FlatGradComm()
+    sync = dp.GradAllReducer(model, bucket_mb=1e-4, flat_comm=comm)
+    grads = []
+    for step in range(2):   # the pre-reduced set must reset between steps
+        model.zero_grad(set_to_none=True)
+        x = torch.randn(8, 6, generator=torch.Generator().manual_seed(step))[rank * 4:(rank + 1) * 4]
+        model(x, comm).square().sum().backward()
+        sync.finish()
+        assert comm.reduced_ids == set()
+        grads.append({n: p.grad.clone() for n, p in model.named_parameters()})
+    if rank == 0:
+        torch.save({f"{i}.{n}": g for i, gs in enumerate(grads) for n, g in gs.items()}, out)
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+class _FlatModel(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        g = torch.Generator().manual_seed(3)
+        self.a = torch.nn.Parameter(torch.randn(6, 5, generator=g))   # hook-reduced
+        self.w = torch.nn.Parameter(torch.randn(5, 3, generator=g))   # flat-buffer reduced
+
+    def forward(self, x, comm=None):
+        h = torch.tanh(x @ self.a)
+        return h @ self.w if comm is None else _FlatArenaFn.apply(comm, h, self.w)
+
+
+def test_flat_grad_comm_matches_full_batch_gloo(tmp_path):
+    """FlatGradComm (fused step's flat-arena all-reduce) + GradAllReducer's
+    hooks over 2 gloo ranks == full-batch gradients; parameters the flat comm
+    averaged are not reduced a second time by the hooks."""
+    out = str(tmp_path / "f.pt")
+    mp.spawn(_flat_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    model = _FlatModel()
+    for step in range(2):
+        model.zero_grad(set_to_none=True)
+        x = torch.randn(8, 6, generator=torch.Generator().manual_seed(step))
+        (model(x).square().sum() / 2).backward()
+        for n, p in model.named_parameters():
+            assert torch.allclose(got[f"{step}.{n}"], p.grad, rtol=1e-5, atol=1e-5), (step, n)
