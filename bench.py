@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--gate-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="storage of the GRU z gate / folded context bias map (the hidden state is fp32 either way)")
     ap.add_argument("--flow-lane", default="side", choices=["side", "main"])
+    ap.add_argument("--convex", default="fused", choices=["fused", "separate", "head"],
+                    help="mask predictor 1x1 conv + convex upsampling: conv epilogue / two kernels / dedicated kernel")
     ap.add_argument("--mask-head", default="split", choices=["split", "fused"],
                     help="mask predictor 3x3 conv on the mask lane (split) or batched with the flow head's (fused)")
     ap.add_argument("--double-buffer", action="store_true", help="parity double-buffering of the flow head outputs")
@@ -130,7 +132,8 @@ def main():
     engine_kw = dict(use_graph=not args.no_graph, streams=streams, split=args.split,
                      flow_head=args.flow_head, double_buffer=args.double_buffer, direct_flow=not args.no_direct_flow,
                      gate_dtype=torch.bfloat16 if args.gate_dtype == "bf16" else torch.float32,
-                     flow_lane=args.flow_lane, mask_head=args.mask_head)
+                     flow_lane=args.flow_lane, mask_head=args.mask_head,
+                     convex=args.convex)
     pipelined = args.pipeline and not args.no_graph
     eng = model.engine(dev, **engine_kw) if pipelined else None
 
@@ -219,6 +222,7 @@ def main():
                 "gate_dtype": args.gate_dtype,
                 "flow_lane": args.flow_lane,
                 "mask_head": args.mask_head,
+                "convex": args.convex,
                 "direct_flow_conv": not args.no_direct_flow,
                 "batch_parts": args.split,
                 "cross_batch_pipeline": bool(pipelined),

@@ -142,6 +142,14 @@ int jr_corr_lookup_bwd(void* const* dlevels, int num_levels, int B, int h, int w
 // Flow upsampling x8.
 // ---------------------------------------------------------------------------
 // mask bf16 [B*h*w][576] (already scaled), flow fp32 [B*h*w][2] -> out fp32 [B][8h][8w][2]
+// Fused inference mask head (convex_head.hip): 1x1 conv 256 -> 576 of the mask
+// features feat bf16 [M][feat_cstride] (channels feat_coff ..+256, 16-byte
+// aligned), weights packed by ops/native.py:pack_convex_head, bias fp32 [576]
+// (reference channel order k*64 + s), logits * alpha -> softmax over the 9
+// taps -> convex combination of 8 * flow (fp32 [M][2]) -> out (B, 8h, 8w, 2).
+// tiles: 16-pixel tiles per wave (1 / 2; 0 = by problem size).
+int jr_convex_head(const void* feat, int feat_cstride, int feat_coff, const void* wpk, const float* bias,
+                   float alpha, const float* flow, int B, int h, int w, float* out, int tiles, hipStream_t stream);
 int jr_upsample_convex(const void* mask, int mask_cstride, const float* flow, int B, int h, int w,
                        float* out, hipStream_t stream);
 int jr_upsample_bilinear(const float* flow, int B, int h, int w, float* out, hipStream_t stream);

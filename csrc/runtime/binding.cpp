@@ -635,6 +635,41 @@ static Launch make_upsample_convex(const TList& t, const IList& i, std::vector<a
   };
 }
 
+// t = [feat, wpk, bias, flow, out], i = [B, h, w, feat_coff, out_iter_stride(, tiles per wave: 0 = auto)]
+static Launch make_convex_head(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep) {
+  at::Tensor feat = opt(t, 0), wpk = opt(t, 1), bias = opt(t, 2), flow = opt(t, 3), out = opt(t, 4);
+  check_bf16(feat, "feat"); check_bf16(wpk, "wpk"); check_f32(bias, "bias"); check_f32(flow, "flow");
+  TORCH_CHECK(i.size() == 5 || i.size() == 6, "convex_head: expected 5 or 6 ints");
+  const int tiles = i.size() == 6 ? (int)i[5] : 0;
+  TORCH_CHECK(tiles == 0 || tiles == 1 || tiles == 2, "convex_head: tiles per wave 0/1/2");
+  const int B = (int)i[0], h = (int)i[1], w = (int)i[2], coff = (int)i[3];
+  const int64_t stride = i[4];
+  const int64_t M = (int64_t)B * h * w;
+  const int fcs = cs(feat);
+  TORCH_CHECK(fcs % 8 == 0 && coff % 8 == 0 && coff >= 0 && coff + 256 <= fcs && feat.numel() >= M * fcs &&
+                  reinterpret_cast<uintptr_t>(feat.data_ptr()) % 16 == 0,
+              "convex_head: feat must be [M][cs] with a 16-byte aligned 256-channel slice");
+  TORCH_CHECK(wpk.numel() == 576 * 256 && reinterpret_cast<uintptr_t>(wpk.data_ptr()) % 16 == 0,
+              "convex_head: packed weights (pack_convex_head)");
+  TORCH_CHECK(bias.numel() == 576 && reinterpret_cast<uintptr_t>(bias.data_ptr()) % 16 == 0, "convex_head: bias [576]");
+  TORCH_CHECK(flow.numel() >= 2 * M, "convex_head: flow [M][2]");
+  TORCH_CHECK(stride >= 0 && stride % 8 == 0, "convex_head: iteration stride");
+  const int64_t cap = check_flow_out(out, B, h, w);
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 32 == 0, "convex_head: out must be 32-byte aligned");
+  if (keep) { keep->push_back(feat); keep->push_back(wpk); keep->push_back(bias); keep->push_back(flow); keep->push_back(out); }
+  const void* fp = feat.data_ptr();
+  const void* wp = wpk.data_ptr();
+  const float* bp = bias.data_ptr<float>();
+  const float* flp = flow.data_ptr<float>();
+  float* op = out.data_ptr<float>();
+  const float a = (float)alpha;
+  return [=](hipStream_t s, int it) {
+    const int64_t off = stride * it;
+    if (off + M * 128 > cap) return (int)hipErrorInvalidValue;
+    return jr_convex_head(fp, fcs, coff, wp, bp, a, flp, B, h, w, op + off, tiles, s);
+  };
+}
+
 // t = [flow, out], i = [B, h, w, out_iter_stride]
 static Launch make_upsample_bilinear(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
   at::Tensor flow = opt(t, 0), out = opt(t, 1);
@@ -846,6 +881,7 @@ void conv_op(const TList& t, IList i, double alpha) { run_now(make_conv(t, i, al
 void corr_op(const TList& t, IList i, double scale) { run_now(make_corr(t, i, scale, nullptr)); }
 void lookup_op(const TList& t, IList i) { run_now(make_lookup(t, i, nullptr)); }
 void upsample_convex_op(const TList& t, IList i) { run_now(make_upsample_convex(t, i, nullptr)); }
+void convex_head_op(const TList& t, IList i, double alpha) { run_now(make_convex_head(t, i, alpha, nullptr)); }
 void upsample_bilinear_op(const TList& t, IList i) { run_now(make_upsample_bilinear(t, i, nullptr)); }
 void stats_op(const TList& t, IList i) {
   std::vector<at::Tensor> keep;  // keeps an internally allocated workspace alive until the launch is queued
@@ -961,6 +997,7 @@ class Plan : public torch::CustomClassHolder {
   void add_corr(TList t, IList i, double scale) { push(make_corr(t, i, scale, &keep_), "corr"); }
   void add_lookup(TList t, IList i) { push(make_lookup(t, i, &keep_), "lookup"); }
   void add_upsample_convex(TList t, IList i) { push(make_upsample_convex(t, i, &keep_), "upsample_convex"); }
+  void add_convex_head(TList t, IList i, double alpha) { push(make_convex_head(t, i, alpha, &keep_), "convex_head"); }
   void add_upsample_bilinear(TList t, IList i) { push(make_upsample_bilinear(t, i, &keep_), "upsample_bilinear"); }
   void add_stats(TList t, IList i) { push(make_stats(t, i, &keep_), "stats"); }
   void add_norm_act(TList t, IList i, double eps) { push(make_norm_act(t, i, eps, &keep_), "norm_act"); }
@@ -1212,6 +1249,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("corr(Tensor?[] t, int[] i, float scale) -> ()", &jr::corr_op);
   m.def("lookup(Tensor?[] t, int[] i) -> ()", &jr::lookup_op);
   m.def("upsample_convex(Tensor?[] t, int[] i) -> ()", &jr::upsample_convex_op);
+  m.def("convex_head(Tensor?[] t, int[] i, float alpha) -> ()", &jr::convex_head_op);
   m.def("upsample_bilinear(Tensor?[] t, int[] i) -> ()", &jr::upsample_bilinear_op);
   m.def("stats(Tensor?[] t, int[] i) -> ()", &jr::stats_op);
   m.def("norm_act(Tensor?[] t, int[] i, float eps) -> ()", &jr::norm_act_op);
@@ -1246,6 +1284,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_corr", &jr::Plan::add_corr)
       .def("add_lookup", &jr::Plan::add_lookup)
       .def("add_upsample_convex", &jr::Plan::add_upsample_convex)
+      .def("add_convex_head", &jr::Plan::add_convex_head)
       .def("add_upsample_bilinear", &jr::Plan::add_upsample_bilinear)
       .def("add_stats", &jr::Plan::add_stats)
       .def("add_norm_act", &jr::Plan::add_norm_act)

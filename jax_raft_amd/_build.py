@@ -36,6 +36,7 @@ KERNEL_SOURCES = [
     CSRC / "kernels" / "conv_direct.hip",
     CSRC / "kernels" / "train.hip",
     CSRC / "kernels" / "wgrad.hip",
+    CSRC / "kernels" / "convex_head.hip",
 ]
 HOST_SOURCES = [CSRC / "runtime" / "binding.cpp"]
 HEADERS = [CSRC / "kernels" / "common.h", CSRC / "kernels" / "kernels.h", CSRC / "kernels" / "conv_igemm.h"]

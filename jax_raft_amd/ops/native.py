@@ -241,6 +241,28 @@ def convex_mask_kernel(kernel: torch.Tensor, bias: torch.Tensor) -> Tuple[torch.
     return kp.reshape(kh, kw, cin, 1024), bp.reshape(1024)
 
 
+def pack_convex_head(kernel: torch.Tensor, bias: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """MaskPredictor 1x1 conv (1, 1, 256, 576) -> the A-fragment order of
+    csrc/kernels/convex_head.hip: [kstep 8][tap 9][wave 4][lane 64][8] bf16 with
+    lane = 16 q + r holding W[ci = 32 kstep + 8 q + j][co = 64 tap + 16 wave + r]
+    (co in the reference order k*64 + s, ``model.py:86``); bias stays fp32 [576]."""
+    kh, kw, cin, c = kernel.shape
+    assert (kh, kw, cin, c) == (1, 1, 256, 576), kernel.shape
+    wc = kernel.detach().float().reshape(8, 4, 8, 9, 4, 16)      # (ks, q, j, k, w, r)
+    wp = wc.permute(0, 3, 4, 1, 5, 2).contiguous().to(torch.bfloat16)
+    return wp.reshape(-1), bias.detach().float().contiguous()
+
+
+def convex_head(feat: torch.Tensor, wpk: torch.Tensor, bias: torch.Tensor, flow: torch.Tensor, B: int, h: int,
+                w: int, alpha: float, coff: int = 0, out: Optional[torch.Tensor] = None, tiles: int = 0) -> torch.Tensor:
+    """Eager fused mask head: feat bf16 [M][cs] (channels coff..coff+256), flow fp32
+    [M][2] -> upsampled flow (B, 8h, 8w, 2) (csrc/kernels/convex_head.hip)."""
+    if out is None:
+        out = torch.empty(B, 8 * h, 8 * w, 2, device=feat.device, dtype=torch.float32)
+    ops().convex_head([feat, wpk, bias, flow, out], [B, h, w, coff, 0, tiles], float(alpha))
+    return out
+
+
 def conv2d(spec: ConvSpec, x: torch.Tensor, act: int = ACT_NONE, out_dtype=torch.bfloat16, alpha: float = 1.0,
            res: Optional[torch.Tensor] = None, res_post: int = 0, cfg: Optional[int] = None) -> torch.Tensor:
     """Eager NHWC conv of a contiguous bf16 tensor [N, H, W, C] (C == cin8)."""

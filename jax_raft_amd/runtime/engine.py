@@ -190,7 +190,10 @@ class RaftEngine:
             flow neighbourhood and the x8 pixel shuffle (``model.py:85-98``) in
             registers, the upsampled flow written straight to the output (no
             576-channel mask round trip, one launch less per iteration);
-            "separate" = mask conv + upsample_convex kernel.
+            "separate" = mask conv + upsample_convex kernel; "head" = the
+            dedicated mask-head kernel (convex_head.hip): the same fusion with
+            tap-major MFMA rows (576 rows of work instead of the 1024 of the
+            padded sub-pixel-major layout) and one 32-byte store per lane.
     """
 
     def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True,
@@ -200,7 +203,7 @@ class RaftEngine:
                  flow_lane: str = "side", direct_flow: bool = True, mask_head: str = "split",
                  convex: str = "fused"):
         nat.require()
-        assert convex in ("fused", "separate"), convex
+        assert convex in ("fused", "separate", "head"), convex
         self.convex = convex
         assert mask_head in ("split", "fused"), mask_head
         assert streams in (True, False, "auto"), streams
@@ -219,6 +222,7 @@ class RaftEngine:
         self.split = split
         self._part_streams: List[torch.cuda.Stream] = []
         self._fh2_w = self._fh2_b = None
+        self._convex_w = self._convex_b = None
         self.model = model
         self.device = torch.device(device)
         self.use_graph = use_graph
@@ -296,6 +300,16 @@ class RaftEngine:
         else:
             self._fh2_w.copy_(wf)
             self._fh2_b.copy_(bf)
+        mp = self.model.mask_predictor
+        if mp is not None and tuple(mp.conv.kernel.shape) == (1, 1, 256, 576):
+            wc, bc = nat.pack_convex_head(mp.conv.kernel.to(self.device), mp.conv.bias.to(self.device))
+            if self._convex_w is None:
+                self._convex_w, self._convex_b = wc, bc
+            else:
+                self._convex_w.copy_(wc)
+                self._convex_b.copy_(bc)
+        elif self.convex == "head":
+            self.convex = "fused"   # the dedicated kernel is specialised to raft_large's 256 -> 576 head
         cf1 = self.model.update_block.motion_encoder.convflow1.layers_0
         if self.direct_flow and nat.direct_conv_ok(cf1.kernel, cf1.stride):
             wd = nat.pack_direct_weight(cf1.kernel).to(self.device)
@@ -639,7 +653,7 @@ class RaftEngine:
         s1 = sp["fh1"] if (all_iters and not split_mask or not self.has_mask) else sp["fh1.flow"]
         fm_ch = round_up((s1 if split_mask else sp["fh1"]).cout, 8)
         mfeat = alloc("mfeat", (M, round_up(sp["mask.convrelu"].cout, 8))) if split_mask else None
-        mask = alloc("mask", (M, 576)) if self.has_mask and self.convex != "fused" else None
+        mask = alloc("mask", (M, 576)) if self.has_mask and self.convex == "separate" else None
         stride = st.out.shape[1] * H * W * 2  # one iteration of the full-batch output
         taps = alloc("fh2.taps", (M, 24), F32) if self.flow_head == "taps" else None
 
@@ -666,7 +680,10 @@ class RaftEngine:
                     fm, coff = mfeat, 0
                 else:
                     coff = self.fh_hidden
-                if self.convex == "fused":
+                if self.convex == "head":
+                    plan.add_convex_head([fm, self._convex_w, self._convex_b, f32, out], [B, h, w, coff, stride],
+                                         m.mask_predictor.multiplier)
+                elif self.convex in ("fused", "head"):
                     # mask logits never leave the CU: softmax + convex combination in the epilogue
                     self._conv(plan, sp["mask.convex"], fm, B, h, w, out, x_coff=coff, epi=EPI_CONVEX,
                                flow32=f32, alpha=m.mask_predictor.multiplier, it_stride=stride)

@@ -180,12 +180,46 @@ def test_fused_convex_upsample_matches_separate(final_only):
     model = model.cuda()
     a = model(i1.cuda(), i2.cuda(), num_flow_updates=3, convex="fused", return_all_iters=not final_only)
     b = model(i1.cuda(), i2.cuda(), num_flow_updates=3, convex="separate", return_all_iters=not final_only)
+    c = model(i1.cuda(), i2.cuda(), num_flow_updates=3, convex="head", return_all_iters=not final_only)
     torch.cuda.synchronize()
-    assert a.shape == b.shape
+    assert a.shape == b.shape == c.shape
     mag = ref.norm(dim=-1).mean().item()
     for it in range(a.shape[0]):
         assert _epe(a[it], b[it]) < 0.01 * mag + 0.01, it
+        assert _epe(c[it], b[it]) < 0.01 * mag + 0.01, it
     assert _epe(a[-1].cpu(), ref[-1]) < 0.05 * mag + 0.05
+    assert _epe(c[-1].cpu(), ref[-1]) < 0.05 * mag + 0.05
+
+
+@pytest.mark.parametrize("tiles", [0, 1, 2])
+@pytest.mark.parametrize("B,h,w,cs,coff", [(1, 9, 13, 256, 0), (2, 55, 16, 512, 256), (4, 17, 128, 264, 8)])
+def test_convex_head_kernel_matches_fp32(B, h, w, cs, coff, tiles):
+    """convex_head.hip (1x1 conv 256 -> 576 on MFMA + softmax over the 9 taps +
+    convex combination + x8 pixel shuffle) vs the fp32 PyTorch composition of
+    model.py:85-98, :394-400; odd sizes exercise the partial pixel tiles, every
+    block shape (1 / 2 pixel tiles per wave) and the automatic choice."""
+    import torch.nn.functional as F
+
+    from jax_raft_amd.ops import native as nat
+
+    g = torch.Generator().manual_seed(B * 1000 + h)
+    M = B * h * w
+    feat = (torch.randn(M, cs, generator=g)).to(torch.bfloat16)
+    kern = torch.randn(1, 1, 256, 576, generator=g) * 0.06
+    bias = torch.randn(576, generator=g) * 0.5
+    flow = torch.randn(M, 2, generator=g) * 3
+    wpk, bp = nat.pack_convex_head(kern, bias)
+    out = nat.convex_head(feat.cuda(), wpk.cuda(), bp.cuda(), flow.cuda(), B, h, w, 0.25, coff=coff, tiles=tiles)
+    torch.cuda.synchronize()
+    x = feat[:, coff:coff + 256].float()
+    logits = (x @ kern.reshape(256, 576) + bias) * 0.25                       # [M][k*64 + s]
+    msk = torch.softmax(logits.reshape(B, h, w, 9, 8, 8), dim=3)
+    fl = (8 * flow).reshape(B, h, w, 2).permute(0, 3, 1, 2)
+    nb = F.unfold(fl, 3, padding=1).reshape(B, 2, 9, h, w).permute(0, 3, 4, 1, 2)  # (B,h,w,2,9)
+    up = torch.einsum("bhwkyx,bhwck->bhwcyx", msk, nb)
+    ref = up.permute(0, 1, 4, 2, 5, 3).reshape(B, 8 * h, 8 * w, 2)
+    err = (out.cpu() - ref).abs().max().item()
+    assert err < 2e-3 * ref.abs().max().item() + 1e-3, err
 
 
 def test_streams_auto_matches_lanes_and_single_lane():
