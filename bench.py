@@ -70,7 +70,7 @@ def main():
     ap.add_argument("--gate-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="storage of the GRU z gate / folded context bias map (the hidden state is fp32 either way)")
     ap.add_argument("--flow-lane", default="side", choices=["side", "main"])
-    ap.add_argument("--convex", default="fused", choices=["fused", "separate", "head"],
+    ap.add_argument("--convex", default="head", choices=["fused", "separate", "head"],
                     help="mask predictor 1x1 conv + convex upsampling: conv epilogue / two kernels / dedicated kernel")
     ap.add_argument("--mask-head", default="split", choices=["split", "fused"],
                     help="mask predictor 3x3 conv on the mask lane (split) or batched with the flow head's (fused)")

@@ -206,62 +206,152 @@ struct LevelPtrs {
   const void* p[4];
 };
 
-// blockDim = 256 (4 queries / block); lane = level*16 + window column i.
-template <int R, typename T>
+// blockDim = 256: 4 waves x QPW queries each; lane = level*16 + window column i.
+// General-shape path (any level size); see corr_lookup_wide_kernel below for
+// the fast path.
+template <int R, typename T, int QPW>
 __global__ __launch_bounds__(256) void corr_lookup_kernel(LevelPtrs lv, int nlev, int total, int h, int w,
                                                           const float* __restrict__ coords, bf16* __restrict__ out,
                                                           int ocs) {
   constexpr int S = 2 * R + 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
-  bf16* stage = (bf16*)dyn_smem;  // [4][ocs]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int q = blockIdx.x * 4 + wave;
-  bf16* st = stage + wave * ocs;
-  for (int c = lane; c < ocs; c += 64) st[c] = f2bf(0.f);
+  const int q0 = (blockIdx.x * 4 + wave) * QPW;
+  bf16* st = (bf16*)dyn_smem + wave * QPW * ocs;  // [QPW][ocs]
+  for (int c = lane; c < QPW * ocs; c += 64) st[c] = f2bf(0.f);
   const int lvl = lane >> 4;
   const int i = lane & 15;
-  float vv[S];
+  const bool on = lvl < nlev && i <= S;
+  const float sc = 1.0f / (float)(1 << lvl);
+  const int hl = h >> lvl, wl = w >> lvl;
+  float fx[QPW], fy[QPW], colv[QPW][S + 1];
 #pragma unroll
-  for (int j = 0; j < S; ++j) vv[j] = 0.f;
-  float fx = 0.f;
-  if (q < total && lvl < nlev && i <= S) {
-    const float x = coords[2 * (long)q];
-    const float y = coords[2 * (long)q + 1];
-    const float sc = 1.0f / (float)(1 << lvl);
-    const float cx = x * sc, cy = y * sc;
-    const float flx = floorf(cx), fly = floorf(cy);
-    fx = cx - flx;
-    const float fy = cy - fly;
-    const int hl = h >> lvl, wl = w >> lvl;
-    const int col = (int)flx - R + i;
-    const int row0 = (int)fly - R;
-    const T* map = (const T*)lv.p[lvl] + (long)q * (hl * wl);
-    const bool colok = (unsigned)col < (unsigned)wl;
-    float colv[S + 1];
+  for (int u = 0; u < QPW; ++u) {
+    const int q = q0 + u;
+    fx[u] = fy[u] = 0.f;
 #pragma unroll
-    for (int j = 0; j <= S; ++j) {
-      const int rr = row0 + j;
-      colv[j] = (colok && (unsigned)rr < (unsigned)hl) ? to_f(map[rr * wl + col]) : 0.f;
+    for (int j = 0; j <= S; ++j) colv[u][j] = 0.f;
+    if (q < total && on) {
+      const float cx = coords[2 * (long)q] * sc, cy = coords[2 * (long)q + 1] * sc;
+      const float flx = floorf(cx), fly = floorf(cy);
+      fx[u] = cx - flx;
+      fy[u] = cy - fly;
+      const int col = (int)flx - R + i;
+      const int row0 = (int)fly - R;
+      const T* map = (const T*)lv.p[lvl] + (long)q * (hl * wl);
+      const bool colok = (unsigned)col < (unsigned)wl;
+#pragma unroll
+      for (int j = 0; j <= S; ++j) {
+        const int rr = row0 + j;
+        if (colok && (unsigned)rr < (unsigned)hl) colv[u][j] = to_f(map[rr * wl + col]);
+      }
     }
-#pragma unroll
-    for (int j = 0; j < S; ++j) vv[j] = (1.f - fy) * colv[j] + fy * colv[j + 1];
   }
-  // horizontal interpolation with the neighbouring column (lane + 1)
+  __syncthreads();  // staging zeroed
 #pragma unroll
-  for (int j = 0; j < S; ++j) {
-    const float nb = __shfl_down(vv[j], 1);
-    vv[j] = (1.f - fx) * vv[j] + fx * nb;
+  for (int u = 0; u < QPW; ++u) {
+    float vv[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) vv[j] = (1.f - fy[u]) * colv[u][j] + fy[u] * colv[u][j + 1];
+    // horizontal interpolation with the neighbouring column (lane + 1)
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const float nb = __shfl_down(vv[j], 1);
+      vv[j] = (1.f - fx[u]) * vv[j] + fx[u] * nb;
+    }
+    if (q0 + u < total && lvl < nlev && i < S) {
+      const int base = u * ocs + lvl * S * S + i * S;
+#pragma unroll
+      for (int j = 0; j < S; ++j) st[base + j] = f2bf(vv[j]);
+    }
   }
   __syncthreads();
-  if (q < total && lvl < nlev && i < S) {
-    const int base = lvl * S * S + i * S;
+  // the wave's QPW output rows are contiguous: [q0, q0 + QPW) x ocs
+  const int nq = min(QPW, total - q0);
+  if (nq > 0) {
+    bf16* dst = out + (long)q0 * ocs;
+    for (int c = lane * 8; c < nq * ocs; c += 64 * 8) *(u32x4*)(dst + c) = *(const u32x4*)(st + c);
+  }
+}
+
+// Wide-load lookup (every level's row length and map size a multiple of one
+// 16-byte chunk, 16-byte aligned levels: raft's /64-wide frames).  The
+// per-lane 2-byte column loads above cost ~1 cycle per lane address in the
+// vector memory pipe (67 cycles per load instruction measured at raft_large
+// batch 4, 31 us per lookup, with only 35 MB fetched).  Here a query's window
+// rows are fetched as aligned 16-byte chunks: (2r+2) rows x NCH chunks per
+// level, e.g. 120 lane-loads = 2 instructions per query instead of 10, into a
+// per-wave LDS window image [query][level][row][NCH * EPC]; the bilinear
+// taps are then read from LDS (no shuffles).  Chunks are wholly inside or
+// wholly outside a row (row length % EPC == 0), so zero padding stays exact.
+template <int R, typename T, int QPW>
+__global__ __launch_bounds__(256) void corr_lookup_wide_kernel(LevelPtrs lv, int nlev, int total, int h, int w,
+                                                               const float* __restrict__ coords,
+                                                               bf16* __restrict__ out, int ocs) {
+  constexpr int S = 2 * R + 1;
+  constexpr int EPC = 16 / sizeof(T);                   // elements per chunk
+  constexpr int NCH = (S + 1 + EPC - 1) / EPC + 1;      // chunks per window row
+  constexpr int RW = NCH * EPC;                         // image row length (elements)
+  constexpr int NT = QPW * 4 * (S + 1) * NCH;           // chunk loads per wave
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q0 = (blockIdx.x * 4 + wave) * QPW;
+  T* win = (T*)dyn_smem + (long)wave * NT * EPC;                       // [QPW][4][S+1][RW]
+  bf16* st = (bf16*)(dyn_smem + 4L * NT * 16) + wave * QPW * ocs;     // [QPW][ocs]
+  for (int c = lane; c < QPW * ocs; c += 64) st[c] = f2bf(0.f);
+  u32x4 v[(NT + 63) / 64];
 #pragma unroll
-    for (int j = 0; j < S; ++j) st[base + j] = f2bf(vv[j]);
+  for (int n = 0; n < (NT + 63) / 64; ++n) {
+    const int t = n * 64 + lane;
+    v[n] = u32x4{0u, 0u, 0u, 0u};
+    const int k = t % NCH, j = (t / NCH) % (S + 1), l = (t / (NCH * (S + 1))) % 4, u = t / (NCH * (S + 1) * 4);
+    const int q = q0 + u;
+    if (t < NT && q < total && l < nlev) {
+      const float sc = 1.0f / (float)(1 << l);
+      const int hl = h >> l, wl = w >> l;
+      const int col0 = (int)floorf(coords[2 * (long)q] * sc) - R;
+      const int rr = (int)floorf(coords[2 * (long)q + 1] * sc) - R + j;
+      const int cc = (col0 >= 0 ? col0 / EPC : -((-col0 + EPC - 1) / EPC)) * EPC + k * EPC;
+      if ((unsigned)rr < (unsigned)hl && (unsigned)cc < (unsigned)wl)
+        v[n] = *(const u32x4*)((const T*)lv.p[l] + (long)q * (hl * wl) + rr * wl + cc);
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < (NT + 63) / 64; ++n) {
+    const int t = n * 64 + lane;
+    if (t < NT) ((u32x4*)win)[t] = v[n];
   }
   __syncthreads();
-  if (q < total) {
-    bf16* dst = out + (long)q * ocs;
-    for (int c = lane * 8; c < ocs; c += 64 * 8) *(u32x4*)(dst + c) = *(const u32x4*)(st + c);
+  const int l = lane >> 4, i = lane & 15;
+  if (l < nlev && i < S) {
+    const float sc = 1.0f / (float)(1 << l);
+#pragma unroll
+    for (int u = 0; u < QPW; ++u) {
+      const int q = q0 + u;
+      if (q >= total) break;
+      const float cx = coords[2 * (long)q] * sc, cy = coords[2 * (long)q + 1] * sc;
+      const float flx = floorf(cx), fly = floorf(cy);
+      const float fx = cx - flx, fy = cy - fly;
+      const int col0 = (int)flx - R;
+      const int o = col0 - (col0 >= 0 ? col0 / EPC : -((-col0 + EPC - 1) / EPC)) * EPC;  // col0 mod EPC
+      const T* wr = win + ((u * 4 + l) * (S + 1)) * RW + o + i;
+      float a0 = to_f(wr[0]), a1 = to_f(wr[1]);
+      const int base = u * ocs + l * S * S + i * S;
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        const float b0 = to_f(wr[(j + 1) * RW]), b1 = to_f(wr[(j + 1) * RW + 1]);
+        const float top = (1.f - fx) * a0 + fx * a1, bot = (1.f - fx) * b0 + fx * b1;
+        st[base + j] = f2bf((1.f - fy) * top + fy * bot);
+        a0 = b0;
+        a1 = b1;
+      }
+    }
+  }
+  __syncthreads();
+  const int nq = min(QPW, total - q0);
+  if (nq > 0) {
+    bf16* dst = out + (long)q0 * ocs;
+    for (int c = lane * 8; c < nq * ocs; c += 64 * 8) *(u32x4*)(dst + c) = *(const u32x4*)(st + c);
   }
 }
 
@@ -325,13 +415,44 @@ __global__ __launch_bounds__(256) void corr_lookup_bwd_kernel(LevelPtrs dlv, int
   }
 }
 
+// The wide kernel needs every level's row length and map size to be a whole
+// number of 16-byte chunks and 16-byte aligned level bases.
+template <typename T>
+bool lookup_wide_ok(const LevelPtrs& lv, int L, int h, int w) {
+  constexpr int EPC = 16 / sizeof(T);
+  for (int l = 0; l < L; ++l) {
+    const int hl = h >> l, wl = w >> l;
+    if (wl % EPC || (hl * wl) % EPC || reinterpret_cast<uintptr_t>(lv.p[l]) % 16) return false;
+  }
+  return true;
+}
+
 template <typename T>
 int launch_lookup(const LevelPtrs& lv, int L, int total, int h, int w, int r, const float* coords, bf16* out, int ocs,
                   hipStream_t stream) {
-  dim3 grid((total + 3) / 4);
-  const size_t smem = 4 * ocs * sizeof(bf16);
+  if (r <= 4 && lookup_wide_ok<T>(lv, L, h, w)) {
+    constexpr int QPW = 2;
+    constexpr int EPC = 16 / sizeof(T);
+    dim3 grid((total + 4 * QPW - 1) / (4 * QPW));
+    switch (r) {
+#define JR_LKW(RR)                                                                                                    \
+  case RR: {                                                                                                        \
+    constexpr int NT = QPW * 4 * (2 * RR + 2) * ((2 * RR + 2 + EPC - 1) / EPC + 1);                                 \
+    const size_t smem = 4 * NT * 16 + 4 * QPW * ocs * sizeof(bf16);                                                 \
+    hipLaunchKernelGGL((corr_lookup_wide_kernel<RR, T, QPW>), grid, dim3(256), smem, stream, lv, L, total, h, w,    \
+                       coords, out, ocs);                                                                            \
+    break;                                                                                                          \
+  }
+      JR_LKW(1) JR_LKW(2) JR_LKW(3) JR_LKW(4)
+#undef JR_LKW
+    }
+    return (int)hipGetLastError();
+  }
+  constexpr int QPW = 1;
+  dim3 grid((total + 4 * QPW - 1) / (4 * QPW));
+  const size_t smem = 4 * QPW * ocs * sizeof(bf16);
   switch (r) {
-#define JR_LK(RR) case RR: hipLaunchKernelGGL((corr_lookup_kernel<RR, T>), grid, dim3(256), smem, stream, lv, L, total, h, w, coords, out, ocs); break;
+#define JR_LK(RR) case RR: hipLaunchKernelGGL((corr_lookup_kernel<RR, T, QPW>), grid, dim3(256), smem, stream, lv, L, total, h, w, coords, out, ocs); break;
     JR_LK(1) JR_LK(2) JR_LK(3) JR_LK(4) JR_LK(5) JR_LK(6)
 #undef JR_LK
     default: return (int)hipErrorInvalidValue;

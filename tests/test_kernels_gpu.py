@@ -194,16 +194,21 @@ def test_corr_pyramid(h, w, C, L):
         assert (got - ref[l]).abs().max().item() < 1e-3 * max(1.0, ref[l].abs().max().item()), l
 
 
-@pytest.mark.parametrize("radius,L", [(4, 4), (3, 4), (2, 2)])
-def test_corr_lookup(radius, L):
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("h,w", [(17, 19), (17, 64)])
+@pytest.mark.parametrize("radius,L", [(4, 4), (3, 4), (2, 2), (5, 2)])
+def test_corr_lookup(radius, L, h, w, dtype):
+    """Radius-r pyramid lookup vs the fp32 reference (model.py:448-470): odd
+    widths take the per-lane column kernel, /64 widths (every level a whole
+    number of 16-byte chunks) the wide-load kernel (radius <= 4)."""
     nat = _nat()
     torch.manual_seed(5)
-    B, h, w = 2, 17, 19
+    B = 2
     M = B * h * w
     pyr = []
     hl, wl = h, w
     for _ in range(L):
-        pyr.append(torch.randn(M, hl, wl))
+        pyr.append(torch.randn(M, hl, wl).to(dtype).float())
         hl //= 2
         wl //= 2
     # coords: in range, fractional, and far outside (zero padding)
@@ -214,8 +219,8 @@ def test_corr_lookup(radius, L):
     S = 2 * radius + 1
     ocs = nat.round_up(L * S * S, 8)
     out = torch.full((M, ocs), 5.0, dtype=torch.bfloat16, device=DEV)
-    nat.ops().lookup([coords.reshape(M, 2).to(DEV).contiguous(), out] + [p.to(DEV) for p in pyr] + [None] * (4 - L),
-                     [L, B, h, w, radius])
+    nat.ops().lookup([coords.reshape(M, 2).to(DEV).contiguous(), out] + [p.to(DEV, dtype) for p in pyr]
+                     + [None] * (4 - L), [L, B, h, w, radius])
     torch.cuda.synchronize()
     got = out.float().cpu()
     assert (got[:, L * S * S:] == 0).all()

@@ -47,6 +47,7 @@ def main():
         for t in (0, 1, 2):
             res[f"B{B} head tiles={t}"] = round(timeit(lambda: nat.convex_head(feat, wpk, bp, flow, B, h, w, 0.25,
                                                                                out=out, tiles=t)), 2)
+        res[f"B{B} out.zero_()"] = round(timeit(lambda: out.zero_()), 2)
         mask = torch.empty(M, 576, device=dev, dtype=torch.bfloat16)
         res[f"B{B} upsample_convex only"] = round(timeit(lambda: nat.ops().upsample_convex([mask, flow, out],
                                                                                           [B, h, w, 0])), 2)
