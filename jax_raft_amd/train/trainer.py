@@ -97,6 +97,7 @@ class Trainer:
         self.step = 0
         self.skipped = 0           # total dropped steps
         self._skip_run = 0         # consecutive dropped steps
+        self._pending = []         # (step, pinned non-finite flag, event): GPU steps not yet settled
         if cfg.resume and cfg.ckpt_dir and os.path.exists(os.path.join(cfg.ckpt_dir, "latest.json")):
             self.load(cfg.ckpt_dir)
 
@@ -115,19 +116,57 @@ class Trainer:
         gnorm = torch.nn.utils.clip_grad_norm_(self.model.parameters(), cfg.clip)
         # Failure detection: the gradient is all-reduced, so every rank sees the
         # same norm and takes the same decision (no extra collective needed).
-        if cfg.skip_nonfinite and not bool(torch.isfinite(gnorm)):
+        if cfg.skip_nonfinite and self._async_skip():
+            # GPU, fused AdamW: the optimizer kernel itself drops the update when
+            # the norm is non-finite (found_inf), so no host sync stalls the
+            # launch queue here; the host-side bookkeeping (skip counters, the
+            # consecutive-skip abort) reads the flag one step later, when the
+            # GPU is already busy with the next step (see _settle).
+            bad = (~torch.isfinite(gnorm)).float()
+            self.opt.found_inf = bad
+            self.opt.step()
+            self.opt.found_inf = None
+            flag = torch.empty((), dtype=torch.float32, pin_memory=True)
+            flag.copy_(bad, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._settle(keep_last=True)
+            self._pending.append((self.step + 1, flag, ev))
+        elif cfg.skip_nonfinite and not bool(torch.isfinite(gnorm)):
             self.opt.zero_grad(set_to_none=True)
-            self.skipped += 1
-            self._skip_run += 1
-            if self._skip_run > cfg.max_skipped:
-                raise FloatingPointError(f"{self._skip_run} consecutive non-finite gradients at step {self.step + 1}")
+            self._record_skip(self.step + 1, True)
         else:
-            self._skip_run = 0
+            if cfg.skip_nonfinite:
+                self._record_skip(self.step + 1, False)
             self.opt.step()
         self.sched.step()
         self.step += 1
         out = {"loss": loss.detach(), "grad_norm": gnorm.detach(), **{k: v.detach() for k, v in metrics.items()}}
         return out
+
+    def _async_skip(self) -> bool:
+        return self.device.type == "cuda" and bool(getattr(self.opt, "defaults", {}).get("fused"))
+
+    def _record_skip(self, step: int, bad: bool) -> None:
+        if bad:
+            self.skipped += 1
+            self._skip_run += 1
+            if self._skip_run > self.cfg.max_skipped:
+                raise FloatingPointError(f"{self._skip_run} consecutive non-finite gradients at step {step}")
+        else:
+            self._skip_run = 0
+
+    def _settle(self, keep_last: bool = False) -> None:
+        """Fold the non-finite flags of finished steps into the skip counters
+        (``keep_last``: leave the newest pending step, which may still run)."""
+        while len(self._pending) > (1 if keep_last else 0):
+            step, flag, ev = self._pending.pop(0)
+            ev.synchronize()
+            self._record_skip(step, bool(flag.item()))
+
+    def flush(self) -> None:
+        """Settle every pending failure-detection flag (waits for the GPU)."""
+        self._settle()
 
     def batch_for(self, step: int):
         cfg = self.cfg
@@ -144,6 +183,7 @@ class Trainer:
             batch = self.batch_for(self.step)
             m = self.train_step(batch)
             if self.step % cfg.log_every == 0 or self.step == cfg.steps:
+                self.flush()
                 vals = dp.all_reduce_scalars({k: float(v) for k, v in m.items()}, self.device)
                 if self.device.type == "cuda":
                     torch.cuda.synchronize(self.device)
@@ -161,6 +201,7 @@ class Trainer:
 
     # ------------------------------------------------------------ checkpoint
     def save(self, d: str) -> None:
+        self.flush()
         if self.rank != 0:
             if dp.is_dist():
                 torch.distributed.barrier()

@@ -40,3 +40,31 @@ def test_dp_two_ranks_shared_gpu(tmp_path):
     b = (tmp_path / "rank1.txt").read_text().split()
     assert a[:2] == b[:2], (a, b)      # identical parameters on both replicas
     assert a[2] != b[2]                # but each rank saw its own data
+
+
+def test_gpu_nonfinite_step_dropped_without_host_sync():
+    """Failure detection on the GPU: a poisoned step's update is dropped by the
+    fused AdamW kernel itself (found_inf), the skip counters settle one step
+    later (no host sync in the step), and the consecutive-skip abort still fires."""
+    cfg = TrainConfig(arch="raft_small", steps=4, batch=1, iters=2, size=(128, 128), log_every=100, lr=1e-4,
+                      fault_nan_step=2)
+    tr = Trainer(cfg)
+    if not tr._async_skip():
+        pytest.skip("fused AdamW unavailable in this PyTorch build")
+    tr.train_step(tr.batch_for(0))
+    tr.flush()
+    w1 = {n: p.detach().clone() for n, p in tr.model.named_parameters()}
+    m = tr.train_step(tr.batch_for(1))   # step 2: NaN loss -> update dropped on the device
+    assert not torch.isfinite(m["grad_norm"])
+    tr.flush()
+    assert tr.skipped == 1
+    assert all(torch.equal(w1[n], p) for n, p in tr.model.named_parameters())
+    tr.train_step(tr.batch_for(2))
+    tr.flush()
+    assert tr.step == 3 and tr.skipped == 1
+    assert not all(torch.equal(w1[n], p) for n, p in tr.model.named_parameters())
+    assert all(torch.isfinite(p).all() for p in tr.model.parameters())
+    cfg.max_skipped, cfg.fault_nan_step = 0, 4
+    with pytest.raises(FloatingPointError):
+        tr.train_step(tr.batch_for(3))
+        tr.flush()
