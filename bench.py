@@ -69,7 +69,7 @@ def main():
                     help="serving mode: upsample/return only the final flow (not the reference's output)")
     ap.add_argument("--gate-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="storage of the GRU z gate / folded context bias map (the hidden state is fp32 either way)")
-    ap.add_argument("--flow-lane", default="side", choices=["side", "main"])
+    ap.add_argument("--flow-lane", default="mask", choices=["side", "main", "mask"])
     ap.add_argument("--convex", default="head", choices=["fused", "separate", "head"],
                     help="mask predictor 1x1 conv + convex upsampling: conv epilogue / two kernels / dedicated kernel")
     ap.add_argument("--mask-head", default="split", choices=["split", "fused"],

@@ -165,9 +165,13 @@ class RaftEngine:
         gate_dtype: storage dtype of the ConvGRU z gate and of the folded
             context bias map (bf16 default, fp32 for bit-closer parity); the
             hidden state itself is always carried in fp32.
-        flow_lane: "side" runs the motion encoder's flow-feature convs on a side
-            lane concurrently with the lookup + correlation convs; "main" runs
-            them on the critical-path lane before the lookup.
+        flow_lane: "mask" (default) runs the motion encoder's flow-feature convs
+            of iteration i+1 on the mask lane right after iteration i's flow
+            update, ahead of its mask head (three cross-lane edges per
+            iteration instead of five; 289 vs 279 pairs/s at raft_large batch
+            4; falls back to "side" without a split mask head); "side" runs
+            them on their own lane concurrently with the lookup + correlation
+            convs; "main" runs them on the critical-path lane before the lookup.
         double_buffer: ("lanes" schedule) double-buffer the flow head outputs by iteration
             parity, so iteration i+1's flow head need not wait for iteration
             i's mask head (otherwise one buffer and a WAR wait).  Off by
@@ -203,7 +207,7 @@ class RaftEngine:
                  corr_dtype: torch.dtype = torch.bfloat16, autotune: bool = True, streams="auto",
                  split: int = 1, flow_head: str = "taps", double_buffer: bool = False,
                  fused_flow_head: bool = False, gate_dtype: torch.dtype = torch.bfloat16,
-                 flow_lane: str = "side", direct_flow: bool = True, mask_head: str = "split",
+                 flow_lane: str = "mask", direct_flow: bool = True, mask_head: str = "split",
                  convex: str = "head"):
         nat.require()
         assert convex in ("fused", "separate", "head"), convex
@@ -216,7 +220,7 @@ class RaftEngine:
         self.direct_flow = direct_flow
         self._cf1_w = self._cf1_b = None
         self.gate_dtype = gate_dtype
-        assert flow_lane in ("side", "main"), flow_lane
+        assert flow_lane in ("side", "main", "mask"), flow_lane
         self.flow_lane = flow_lane if streams else "main"
         self.double_buffer = double_buffer
         self.flow_head = "fused" if fused_flow_head else flow_head
@@ -653,6 +657,22 @@ class RaftEngine:
             self._conv(plan, sp["me.convflow2"], f1, B, h, w, cf, y_coff=cl[-1], act=ACT_RELU)
 
         split_mask = self.has_mask and all_iters and self.mask_head == "split" and not self.double_buffer
+        # flow_lane "mask": the flow features of iteration i+1 run on the mask lane
+        # right after iteration i's flow update, ahead of iteration i's mask head
+        # (both need only that update), so an iteration has three cross-lane
+        # edges: E_FH (flow update -> mask lane), E_FLOW (flow features -> motion
+        # conv) and E_MASK (mask head done -> first GRU conv, which overwrites the
+        # h the mask head reads; the next flow update, which overwrites flow32,
+        # comes later on the main lane).  Iteration 0's flow features (zero flow)
+        # run once in the prologue.
+        mask_lane_flow = self.flow_lane == "mask" and split_mask and self.flow_head == "taps"
+        side_flow = self.flow_lane == "side" or (self.flow_lane == "mask" and not mask_lane_flow)
+        if mask_lane_flow:
+            plan.set_segment(0)
+            lane(main)
+            flow_features()
+            plan.set_segment(1)
+            lane(main)
         s1 = sp["fh1"] if (all_iters and not split_mask or not self.has_mask) else sp["fh1.flow"]
         fm_ch = round_up((s1 if split_mask else sp["fh1"]).cout, 8)
         mfeat = alloc("mfeat", (M, round_up(sp["mask.convrelu"].cout, 8))) if split_mask else None
@@ -697,7 +717,9 @@ class RaftEngine:
             else:
                 plan.add_upsample_bilinear([f32, out], [B, h, w, stride])
 
-        if self.flow_lane == "side":
+        if mask_lane_flow:
+            pass
+        elif side_flow:
             plan.add_record(E_IT)
             lane(side)
             plan.add_wait(E_IT)
@@ -713,7 +735,7 @@ class RaftEngine:
             self._conv(plan, sp["me.convcorr2"], c1, B, h, w, cf, act=ACT_RELU)
         else:
             self._conv(plan, sp["me.convcorr1"], corr, B, h, w, cf, act=ACT_RELU)
-        if self.flow_lane == "side":
+        if side_flow or mask_lane_flow:
             plan.add_wait(E_FLOW)
         self._conv(plan, sp["me.conv"], cf, B, h, w, hx, y_coff=self.mot_off, act=ACT_RELU, y2=qx,
                    y2_coff=self.mot_off)
@@ -721,7 +743,9 @@ class RaftEngine:
             # r*h from the bf16 h of the conv's own input hx (no fp32 state read)
             self._conv(plan, sp[f"gru{gi}.a"], hx, B, h, w, qx, zbuf=zb, hidden=self.hidden,
                        epi=EPI_GRU_A, bmap=gbias[gi], bmap_coff=0)
-            if gi == 0 and split_mask:
+            if gi == 0 and mask_lane_flow:
+                plan.add_wait(E_MASK)  # the previous iteration's mask head has read h (and flow32)
+            elif gi == 0 and split_mask:
                 plan.add_wait(E_MR)  # the previous iteration's mask head has read h
             self._conv(plan, sp[f"gru{gi}.b"], qx, B, h, w, hx, h32=h32, zbuf=zb, hidden=self.hidden,
                        epi=EPI_GRU_B, bmap=gbias[gi], bmap_coff=2 * self.hidden)
@@ -739,7 +763,9 @@ class RaftEngine:
                 if len(fms) > 1:
                     plan.set_parity(par)
                 lane(main)
-                if split_mask and self.flow_head == "taps":
+                if mask_lane_flow:
+                    flow_head(fms[par], f32s[par])   # ordered after the mask lane by E_MASK (first GRU conv)
+                elif split_mask and self.flow_head == "taps":
                     # the flow head's features are not read by the mask lane: only
                     # the flow update (flow32) must wait for the last upsampling
                     flow_head(fms[par], f32s[par], before_update=lambda p=par: plan.add_wait(E_MASK + p))
@@ -749,6 +775,9 @@ class RaftEngine:
                 plan.add_record(E_FH)
                 lane(side2)
                 plan.add_wait(E_FH)
+                if mask_lane_flow:
+                    flow_features()   # for the next iteration
+                    plan.add_record(E_FLOW)
                 upsample(fms[par], f32s[par], stride)
                 plan.add_record(E_MASK + par)
             plan.set_parity(-1)

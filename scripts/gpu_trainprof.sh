@@ -12,3 +12,5 @@ db=$(ls $o/k/run_results.db $o/k/*/run_results.db 2>/dev/null | head -1 || true)
 if [ -z "$db" ]; then db=$(find $o/k -name '*kernel_trace.csv' | head -1); fi
 python3 tools/kernel_breakdown.py "$db" --steps 5 --marker seq_loss_kernel --top 60 > $o/breakdown.txt
 cat $o/breakdown.txt
+(cd tools && python3 step_gaps.py "../$db") > $o/gaps.txt
+cat $o/gaps.txt

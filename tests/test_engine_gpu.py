@@ -263,3 +263,21 @@ def test_engine_split_parts_match_single():
     torch.cuda.synchronize()
     assert a.shape == b.shape
     assert ((a - b).abs().max() / (a.abs().max() + 1e-6)).item() < 1e-2
+
+
+@pytest.mark.parametrize("flow_lane", ["main", "side"])
+def test_flow_lane_schedules_match(flow_lane):
+    """The lane schedules are orderings of the same ops: flow features on the
+    main lane, on their own side lane or on the mask lane after the flow update
+    (default) all give the same flows, eager and graph-replayed."""
+    from jax_raft_amd import raft_large
+
+    model, _ = raft_large()
+    model = model.cuda()
+    i1, i2 = (t.cuda() for t in _inputs(4, 128, 160, seed=77))
+    ref = model(i1, i2, num_flow_updates=5, streams=True)   # flow_lane="mask"
+    a = model(i1, i2, num_flow_updates=5, streams=True, flow_lane=flow_lane)
+    b = model(i1, i2, num_flow_updates=5, streams=True, flow_lane=flow_lane, use_graph=False)
+    torch.cuda.synchronize()
+    assert (a - ref).abs().max().item() < 1e-3
+    assert (b - ref).abs().max().item() < 1e-3
