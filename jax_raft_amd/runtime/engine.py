@@ -168,8 +168,12 @@ class RaftEngine:
         flow_lane: "mask" (default) runs the motion encoder's flow-feature convs
             of iteration i+1 on the mask lane right after iteration i's flow
             update, ahead of its mask head (three cross-lane edges per
-            iteration instead of five; 289 vs 279 pairs/s at raft_large batch
-            4; falls back to "side" without a split mask head); "side" runs
+            iteration instead of five; 289-294 vs 279 pairs/s at raft_large
+            batch 4; falls back to "side" without a split mask head.  Measured
+            and dropped: two edges with the mask conv ahead of the flow
+            features and the flow double-buffered by parity, 276 -- the
+            longer chain before E_FLOW stalls the motion conv; one event after
+            the whole mask lane, 289-292); "side" runs
             them on their own lane concurrently with the lookup + correlation
             convs; "main" runs them on the critical-path lane before the lookup.
         double_buffer: ("lanes" schedule) double-buffer the flow head outputs by iteration
