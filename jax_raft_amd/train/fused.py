@@ -248,11 +248,13 @@ class FusedLoop:
         self.M = B * self.h * self.w
         self.device = torch.device(device)
         self.use_graph = use_graph
-        # side lanes of the plans (flow features / mask head in the forward, the motion
-        # encoder's backward): opt-in, JR_FUSED_LANES=1.  Measured on MI355X (config 5):
-        # 183 pairs/s with lanes vs 267 on one in-order stream (cross-lane event waits in
-        # the captured graphs cost more than the overlap of the per-iteration kernels gains)
+        # side lanes of the plans: opt-in.  JR_FUSED_LANES=1: the motion encoder's backward
+        # on a side lane (183 pairs/s vs 267 on one in-order stream, config 5);
+        # JR_FUSED_FWD_LANES=1: the forward's two-edge flow-feature / mask-head lane (189-196
+        # vs 288, although the same schedule speeds up the inference engine by 4 %: in the
+        # training step the multi-lane graphs' replays stall the launch queue around them)
         self.lanes = 1 if os.environ.get("JR_FUSED_LANES", "0") == "1" else 0
+        self.fwd_lanes = 1 if os.environ.get("JR_FUSED_FWD_LANES", "0") == "1" else 0
         self.gen = 0            # forward generation (a backward must match the latest forward)
         self.done_gen = -1
         self._analyse()
@@ -557,26 +559,43 @@ class FusedLoop:
         P.set_lane(0)
         T, G, hd, B, h, w = self.T, self.G, self.hd, self.B, self.h, self.w
         cl, fl = self.cl, self.fl
-        # lanes: 0 = critical path (lookup -> correlation convs -> motion conv -> GRUs -> flow
-        # head -> coordinate update), 1 = flow-feature convs of the next iteration's flow,
-        # 2 = mask head + x8 upsampling (read only per-iteration buffers; joined at the end)
-        E_PACK, E_FT, E_FLOW, E_FH = 0, 1, 2, 3
-        lanes = self.lanes
+        # lanes (fwd_lanes): 0 = critical path (lookup -> correlation convs -> motion conv ->
+        # GRUs -> flow head -> coordinate update); 1 = after iteration t's coordinate update,
+        # the flow-feature convs of iteration t+1 (they need only that update), then iteration
+        # t's mask head + x8 upsampling (read only per-iteration buffers; joined at the end).
+        # Two cross-lane edges per iteration: E_FH (update -> lane 1), E_FLOW (flow features
+        # -> motion conv), as in the inference engine's mask-lane schedule.
+        E_PACK, E_FLOW, E_FH = 0, 2, 3
+        fl = self.fwd_lanes
         self.packer.record(P)   # this step's weights -> every spec (forward and data-gradient layouts)
         P.add_corr([self.fm1, self.fm2] + self.levels + [None] * (4 - self.L), [B, h, w, self.fmap_ch, self.L],
                    1.0 / float(self.fmap_ch) ** 0.5)
         P.add_record(E_PACK)
         for g in range(G):  # loop-invariant context share of every gate (+ biases), fp32
             self._conv(P, f"gC{g}", self.ctx_in, self.gbias[g])
-        for t in range(T):
-            hx0, qx0 = self.hx[0, t], self.qx[0, t]
-            P.set_lane(lanes)
-            P.add_wait(E_PACK)
-            P.add_wait(E_FT)   # flow8[t] written by the previous iteration's coordinate update
+
+        def flow_features(t):
             self._conv(P, "cf1", self.flow8[t], self.f1[t], act=ACT_RELU)
             self._conv(P, "cf2", self.f1[t], self.cf[t], y_coff=cl[-1], act=ACT_RELU)
+
+        def mask_head(t):
+            if self.has_mask:
+                self._conv(P, "mask", self.fmm[t], self.mask[t], x_coff=self.fh_hidden,
+                           alpha=self.mp.multiplier)
+                P.add_upsample_convex([self.mask[t], self.flow32[t], self.out[t]], [B, h, w, 0])
+            else:
+                P.add_upsample_bilinear([self.flow32[t], self.out[t]], [B, h, w, 0])
+
+        if fl:
+            P.set_lane(1)
+            P.add_wait(E_PACK)
+            flow_features(0)
             P.add_record(E_FLOW)
             P.set_lane(0)
+        for t in range(T):
+            hx0, qx0 = self.hx[0, t], self.qx[0, t]
+            if not fl:
+                flow_features(t)
             P.add_lookup([self.coords[t], self.corr[t]] + self.levels + [None] * (4 - self.L),
                          [self.L, B, h, w, self.radius])
             if len(cl) == 2:
@@ -584,7 +603,8 @@ class FusedLoop:
                 self._conv(P, "cc2", self.c1[t], self.cf[t], act=ACT_RELU)
             else:
                 self._conv(P, "cc1", self.corr[t], self.cf[t], act=ACT_RELU)
-            P.add_wait(E_FLOW)
+            if fl:
+                P.add_wait(E_FLOW)
             self._conv(P, "mc", self.cf[t], hx0, y_coff=hd, act=ACT_RELU, y2=qx0, y2_coff=hd)
             for g in range(1, G):  # [motion | flow] into the other GRUs' inputs
                 P.add_copy_channels([hx0, self.hx[g, t]], [hd, hd, self.M, self.mot_cs])
@@ -605,17 +625,17 @@ class FusedLoop:
             P.add_copy([self.coords[t], self.coords[t + 1]])
             P.add_flow_taps([self.taps, self._fh2_bias, self.coords[t + 1], self.flow32[t], hn, self.qx[0, t + 1],
                              self.flow8[t + 1]], [B, h, w, self.flow_off, self.flow_off])
-            P.add_record(E_FT)
-            P.add_record(E_FH)
-            P.set_lane(2 * lanes)
-            P.add_wait(E_FH)
-            if self.has_mask:
-                self._conv(P, "mask", self.fmm[t], self.mask[t], x_coff=self.fh_hidden,
-                           alpha=self.mp.multiplier)
-                P.add_upsample_convex([self.mask[t], self.flow32[t], self.out[t]], [B, h, w, 0])
+            if fl:
+                P.add_record(E_FH)
+                P.set_lane(1)
+                P.add_wait(E_FH)
+                if t + 1 < T:
+                    flow_features(t + 1)
+                    P.add_record(E_FLOW)
+                mask_head(t)
+                P.set_lane(0)
             else:
-                P.add_upsample_bilinear([self.flow32[t], self.out[t]], [B, h, w, 0])
-            P.set_lane(0)
+                mask_head(t)
         return P
 
     def _build_bwd(self):
