@@ -1034,6 +1034,12 @@ class Plan : public torch::CustomClassHolder {
 
   // Launch prologue, n_iters x loop body, epilogue (lane 0 = current stream).
   void run(int64_t n_iters) { JR_CHECK_OK(enqueue(cur_stream(), (int)n_iters)); }
+  // Enqueue into a stream that an outer capture is recording (e.g. a whole
+  // training step captured by torch.cuda.graph): lane 0 is the caller's stream
+  // itself, as in capture(), so the origin stream never holds only fork / join
+  // event nodes (which crashes hipStreamEndCapture on this ROCm); no per-op
+  // checks (no synchronisation inside a capture).
+  void run_inline(int64_t n_iters) { JR_CHECK_OK(enqueue(cur_stream(), (int)n_iters, true)); }
 
   // Capture the same sequence into one hipGraph (on a private stream: the
   // legacy default stream cannot be captured) and instantiate it.
@@ -1309,6 +1315,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("num_ops", &jr::Plan::num_ops)
       .def("op_names", &jr::Plan::op_names)
       .def("run", &jr::Plan::run)
+      .def("run_inline", &jr::Plan::run_inline)
       .def("capture", &jr::Plan::capture)
       .def("captured_iters", &jr::Plan::captured_iters)
       .def("replay", &jr::Plan::replay)

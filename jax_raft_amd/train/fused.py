@@ -741,12 +741,7 @@ class FusedLoop:
             wb(mp.conv, self.fmm, self.fh_hidden, self.mask_hidden, self.dmask)
 
     def _run(self, plan):
-        if self.use_graph:
-            if plan.captured_iters() != 0:
-                plan.capture(0)
-            plan.replay()
-        else:
-            plan.run(0)
+        _run_plan(plan, self.use_graph)
 
     # --------------------------------------------------------------- steps
     def forward(self, fmap1: torch.Tensor, fmap2: torch.Tensor, ctx_raw: torch.Tensor) -> torch.Tensor:
@@ -960,6 +955,20 @@ class FusedRAFT(torch.autograd.Function):
 
 _LOOPS: Dict[tuple, object] = {}
 _GRAD_COMM = None
+
+
+def _run_plan(plan, use_graph: bool) -> None:
+    """Replay a plan's own hipGraph, or enqueue it eagerly -- inline (lane 0 =
+    the caller's stream) inside an outer stream capture (the trainer's
+    optional whole-step graph), which records the plan's launches into it."""
+    if torch.cuda.is_current_stream_capturing():
+        plan.run_inline(0)
+    elif use_graph:
+        if plan.captured_iters() != 0:
+            plan.capture(0)
+        plan.replay()
+    else:
+        plan.run(0)
 
 
 def set_grad_comm(comm) -> None:

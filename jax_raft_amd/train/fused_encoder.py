@@ -310,12 +310,9 @@ class EncoderTrain:
 
     # ---------------------------------------------------------------- run
     def _run(self, plan):
-        if self.use_graph:
-            if plan.captured_iters() != 0:
-                plan.capture(0)
-            plan.replay()
-        else:
-            plan.run(0)
+        from .fused import _run_plan
+
+        _run_plan(plan, self.use_graph)
 
     def forward(self, update_stats: bool = True):
         """Runs the forward plan; with BatchNorm it also updates the running

@@ -56,14 +56,28 @@ class TrainConfig:
     skip_nonfinite: bool = True    # drop a step whose (all-reduced) gradient is NaN/Inf
     max_skipped: int = 10          # ... but abort after this many consecutive drops
     fault_nan_step: int = -1       # fault injection: poison the loss of this step (tests)
+    # GPU, one rank: replay the whole step (fwd + bwd + clip + AdamW) as one captured graph.
+    # Bitwise equal to the eager step, but measured slower on MI355X / ROCm 7 (config 5:
+    # 259-265 vs 288 pairs/s: the native plans' own hipGraphs + eager PyTorch glue beat
+    # one ~2000-node graph), so off by default.
+    graph_step: bool = False
+    graph_warmup: int = 3          # eager steps before the capture (plan build, autotune, allocator warm-up)
 
 
-def _adamw(params, cfg: TrainConfig, device):
+def _adamw(params, cfg: TrainConfig, device, capturable: bool = False):
     """AdamW; on the GPU the single-kernel (fused) implementation when this
-    PyTorch build provides it -- one launch for all ~230 parameter tensors."""
+    PyTorch build provides it -- one launch for all ~230 parameter tensors.
+    ``capturable``: graph-replayable (device-side step counters, the learning
+    rate a device tensor that the LR schedule updates in place)."""
     params = list(params)
     kw = dict(lr=cfg.lr, weight_decay=cfg.weight_decay, eps=cfg.eps)
     if device is not None and torch.device(device).type == "cuda":
+        if capturable:
+            try:
+                return torch.optim.AdamW(params, fused=True, capturable=True,
+                                         **dict(kw, lr=torch.tensor(cfg.lr, device=device)))
+            except (RuntimeError, TypeError, ValueError):
+                pass
         try:
             return torch.optim.AdamW(params, fused=True, **kw)
         except (RuntimeError, TypeError, ValueError):
@@ -89,7 +103,10 @@ class Trainer:
             from . import fused
 
             fused.set_grad_comm(self.flat_comm)
-        self.opt = _adamw(self.model.parameters(), cfg, self.device)
+        self._graph_ok = (cfg.graph_step and self.device.type == "cuda" and self.world == 1
+                          and os.environ.get("JR_GRAPH_STEP", "1") != "0")
+        self.opt = _adamw(self.model.parameters(), cfg, self.device, capturable=self._graph_ok)
+        self._graph = None         # captured whole-step graph (see _graph_step)
         self.sched = torch.optim.lr_scheduler.OneCycleLR(
             self.opt, cfg.lr, total_steps=cfg.steps + 100, pct_start=0.05, cycle_momentum=False,
             anneal_strategy="linear")
@@ -103,6 +120,58 @@ class Trainer:
 
     # ------------------------------------------------------------------ step
     def train_step(self, batch) -> Dict[str, float]:
+        cfg = self.cfg
+        if (self._graph_ok and self.step >= cfg.graph_warmup and cfg.fault_nan_step < 0
+                and self.opt.defaults.get("capturable") and self._async_skip()):
+            return self._graph_step(batch)
+        return self._eager_step(batch)
+
+    def _graph_step(self, batch) -> Dict[str, float]:
+        """The whole step as one replayed graph: the native plans enqueue
+        eagerly into the capture (fused.py), the loss, backward, clipping,
+        the non-finite guard and fused AdamW (device-side step, tensor LR) are
+        captured with them, so the launch queue never runs dry on Python or
+        launch overhead between the pieces.  Captured once, after the eager
+        warm-up steps; the batch is copied into static inputs each step."""
+        if self._graph is None:
+            self._capture(batch)
+        for dst, src in zip(self._static_in, batch):
+            dst.copy_(src)
+        self._graph.replay()
+        if self.cfg.skip_nonfinite:
+            flag = torch.empty((), dtype=torch.float32, pin_memory=True)
+            flag.copy_(self._static_bad, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._settle(keep_last=True)
+            self._pending.append((self.step + 1, flag, ev))
+        self.sched.step()
+        self.step += 1
+        return {k: v.clone() for k, v in self._static_out.items()}
+
+    def _capture(self, batch) -> None:
+        cfg = self.cfg
+        self._static_in = [t.clone() for t in batch]
+        torch.cuda.synchronize(self.device)
+        self.opt.zero_grad(set_to_none=True)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            img1, img2, flow, valid = self._static_in
+            preds = self.model(img1, img2, train=not cfg.freeze_bn, num_flow_updates=cfg.iters, autograd=True)
+            loss, metrics = sequence_loss(preds, flow, valid, cfg.gamma, cfg.max_flow)
+            loss.backward()
+            gnorm = torch.nn.utils.clip_grad_norm_(self.model.parameters(), cfg.clip)
+            bad = (~torch.isfinite(gnorm)).float()
+            if cfg.skip_nonfinite:
+                self.opt.found_inf = bad
+            self.opt.step()
+            self.opt.found_inf = None
+        self._graph = g
+        self._static_bad = bad
+        self._static_out = {"loss": loss.detach(), "grad_norm": gnorm.detach(),
+                            **{k: v.detach() for k, v in metrics.items()}}
+
+    def _eager_step(self, batch) -> Dict[str, float]:
         img1, img2, flow, valid = batch
         cfg = self.cfg
         self.opt.zero_grad(set_to_none=True)
@@ -188,7 +257,7 @@ class Trainer:
                 if self.device.type == "cuda":
                     torch.cuda.synchronize(self.device)
                 dt = time.perf_counter() - t0
-                vals.update(step=self.step, skipped=self.skipped, lr=self.sched.get_last_lr()[0], elapsed_s=dt,
+                vals.update(step=self.step, skipped=self.skipped, lr=float(self.sched.get_last_lr()[0]), elapsed_s=dt,
                             pairs_per_s=self.step * cfg.batch * self.world / dt)
                 last = vals
                 if self.rank == 0:

@@ -68,3 +68,27 @@ def test_gpu_nonfinite_step_dropped_without_host_sync():
     with pytest.raises(FloatingPointError):
         tr.train_step(tr.batch_for(3))
         tr.flush()
+
+
+def test_graph_step_matches_eager_steps():
+    """Whole-step graph capture (forward plans, loss, backward, clipping, the
+    non-finite guard and fused AdamW as one replayed graph) gives bitwise the
+    same losses and weights as the same steps run eagerly, and the LR schedule
+    still advances between replays (device-tensor learning rate)."""
+    kw = dict(arch="raft_large", steps=8, batch=2, iters=3, size=(128, 160), lr=2e-4, graph_warmup=2, graph_step=True,
+              log_every=100)
+    a = Trainer(TrainConfig(**kw))
+    b = Trainer(TrainConfig(**kw))
+    if not (a._graph_ok and a.opt.defaults.get("capturable")):
+        pytest.skip("capturable fused AdamW unavailable in this PyTorch build")
+    b._graph_ok = False   # same (capturable) optimizer, eager steps
+    for i in range(6):
+        ma = a.train_step(a.batch_for(i))
+        mb = b.train_step(b.batch_for(i))
+        assert torch.equal(ma["loss"], mb["loss"]), (i, ma["loss"].item(), mb["loss"].item())
+    assert a._graph is not None and b._graph is None
+    a.flush()
+    b.flush()
+    for (n, p), q in zip(a.model.named_parameters(), b.model.parameters()):
+        assert torch.equal(p, q), n
+    assert float(a.opt.param_groups[0]["lr"]) == float(b.opt.param_groups[0]["lr"]) != kw["lr"]
