@@ -42,19 +42,30 @@ JR_DEVICE bf16 cvt_out<bf16>(float v) { return f2bf(v); }
 JR_DEVICE float to_f(float v) { return v; }
 JR_DEVICE float to_f(bf16 v) { return bf2f(v); }
 
-template <typename T>
+template <typename T, bool WIDE>
 __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restrict__ f1, const bf16* __restrict__ f2,
                                                            int h, int w, int nq, int C, int cs, T* __restrict__ l0,
                                                            T* __restrict__ l1, T* __restrict__ l2,
-                                                           T* __restrict__ l3, int nlev, float scale) {
+                                                           T* __restrict__ l3, int nlev, float scale, int blocked) {
   constexpr int TM = 2, TN = 8;
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * (CQ + CT) * BK];
   const int P = h * w;
-  const int b = blockIdx.z;
-  const int q0 = blockIdx.x * CQ;
-  const int ntx = (w + TX - 1) / TX;
-  const int ty0 = (blockIdx.y / ntx) * TY;
-  const int tx0 = (blockIdx.y % ntx) * TX;
+  // 1-D grid, XCD-aware order: MI355X dispatches blocks round-robin over its 8
+  // XCDs, so block id k runs on XCD k % 8.  Each XCD walks a contiguous run of
+  // tasks, and tasks are ordered (image, query tile, target row, target tile)
+  // with the target tile fastest: the 16-wide tiles that share a 128-byte
+  // line of a query's level-0 / level-1 row are written back to back from one
+  // L2, which then evicts whole lines instead of 32-byte pieces from 8 L2s.
+  const int ntx = (w + TX - 1) / TX, nty = (h + TY - 1) / TY, nqt = (nq + CQ - 1) / CQ;
+  int task = blockIdx.x;
+  {
+    const int nwg = gridDim.x, xcd = task & 7, qq = nwg >> 3, rr = nwg & 7;
+    if (nwg > 8) task = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (task >> 3);
+  }
+  const int tx0 = (task % ntx) * TX;
+  const int ty0 = ((task / ntx) % nty) * TY;
+  const int q0 = ((task / (ntx * nty)) % nqt) * CQ;
+  const int b = task / (ntx * nty * nqt);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ch = tid & 7;
   const bf16* A = f1 + (long)b * nq * cs;
@@ -135,17 +146,30 @@ __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restric
   // Epilogue: D[query = qbase + 4*lq + r][target = (ty0 + tn, tx0 + li)]
   const int x0 = tx0 + li;
   const int h1 = h >> 1, w1 = w >> 1, h2 = h1 >> 1, w2 = w1 >> 1, h3 = h2 >> 1, w3 = w2 >> 1;
+  // WIDE (bf16 levels, w % 16 == 0): the tile's level blocks (per query 8x16,
+  // 4x8, 2x4, 1x2) are staged in LDS (the GEMM buffers are free now) and
+  // written with 16 / 16 / 8 / 4-byte stores.  Per-lane 2-byte stores cost the
+  // vector memory pipe about a cycle per lane: 452 us for the raft_large
+  // batch-4 pyramid, bound by store issue, not by its 500 MB of writes.
+  bf16* st0 = smem;                       // [CQ][TY][TX]
+  bf16* st1 = st0 + CQ * CT;              // [CQ][TY/2][TX/2]
+  bf16* st2 = st1 + CQ * CT / 4;          // [CQ][TY/4][TX/4]
+  bf16* st3 = st2 + CQ * CT / 16;         // [CQ][TY/8][TX/8]
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int q = q0 + wave * (TM * 16) + tm * 16 + 4 * lq + r;
+      const int qi = wave * (TM * 16) + tm * 16 + 4 * lq + r;
+      const int q = q0 + qi;
       const bool qok = q < nq;
       float v[TN];
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) v[tn] = acc[tm][tn][r] * scale;
       // level 0
-      if (qok && x0 < w) {
+      if constexpr (WIDE) {
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) st0[(qi * TY + tn) * TX + li] = f2bf(v[tn]);
+      } else if (qok && x0 < w) {
         T* dst = l0 + ((long)b * nq + q) * P;
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn)
@@ -161,7 +185,12 @@ __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restric
       }
       {
         const int X1 = x0 >> 1;
-        if (qok && (li & 1) == 0 && X1 < w1) {
+        if constexpr (WIDE) {
+          if ((li & 1) == 0) {
+#pragma unroll
+            for (int t = 0; t < TN / 2; ++t) st1[(qi * (TY / 2) + t) * (TX / 2) + (li >> 1)] = f2bf(v1[t]);
+          }
+        } else if (qok && (li & 1) == 0 && X1 < w1) {
           T* dst = l1 + ((long)b * nq + q) * (h1 * w1);
 #pragma unroll
           for (int t = 0; t < TN / 2; ++t) {
@@ -179,7 +208,12 @@ __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restric
       }
       {
         const int X2 = x0 >> 2;
-        if (qok && (li & 3) == 0 && X2 < w2) {
+        if constexpr (WIDE) {
+          if ((li & 3) == 0) {
+#pragma unroll
+            for (int t = 0; t < TN / 4; ++t) st2[(qi * (TY / 4) + t) * (TX / 4) + (li >> 2)] = f2bf(v2[t]);
+          }
+        } else if (qok && (li & 3) == 0 && X2 < w2) {
           T* dst = l2 + ((long)b * nq + q) * (h2 * w2);
 #pragma unroll
           for (int t = 0; t < TN / 4; ++t) {
@@ -194,9 +228,68 @@ __global__ __launch_bounds__(256) void corr_pyramid_kernel(const bf16* __restric
         const float v3 = 0.25f * (s + __shfl_xor(s, 4));
         const int X3 = x0 >> 3;
         const int Y3 = ty0 >> 3;
-        if (qok && (li & 7) == 0 && X3 < w3 && Y3 < h3) {
+        if constexpr (WIDE) {
+          if ((li & 7) == 0) st3[qi * (TX / 8) + (li >> 3)] = f2bf(v3);
+        } else if (qok && (li & 7) == 0 && X3 < w3 && Y3 < h3) {
           l3[((long)b * nq + q) * (h3 * w3) + Y3 * w3 + X3] = cvt_out<T>(v3);
         }
+      }
+    }
+  }
+  if constexpr (WIDE) {
+    __syncthreads();
+    if (blocked) {
+      // levels 0 / 1: the query's block is contiguous (tile rows past h land in padding rows)
+      const long blk = (long)(ty0 / TY) * ntx + tx0 / TX;
+      const long qs0 = (long)nty * ntx * CT, qs1 = qs0 / 4;
+#pragma unroll
+      for (int i = tid; i < CQ * 16; i += 256) {
+        const int qi = i >> 4, c = i & 15;
+        if (q0 + qi < nq)
+          *(u32x4*)((bf16*)l0 + ((long)b * nq + q0 + qi) * qs0 + blk * CT + 8 * c) = *(const u32x4*)(st0 + qi * CT + 8 * c);
+      }
+      if (nlev >= 2) {
+        for (int i = tid; i < CQ * 4; i += 256) {
+          const int qi = i >> 2, c = i & 3;
+          if (q0 + qi < nq)
+            *(u32x4*)((bf16*)l1 + ((long)b * nq + q0 + qi) * qs1 + blk * (CT / 4) + 8 * c) =
+                *(const u32x4*)(st1 + qi * (CT / 4) + 8 * c);
+        }
+      }
+    }
+    // level 0: per query 8 rows x 2 chunks of 8; consecutive threads -> one query's chunks
+#pragma unroll
+    for (int i = tid; !blocked && i < CQ * TY * 2; i += 256) {
+      const int qi = i >> 4, row = (i >> 1) & 7, half = i & 1;
+      const int q = q0 + qi;
+      if (q < nq && ty0 + row < h)
+        *(u32x4*)((bf16*)l0 + ((long)b * nq + q) * P + (ty0 + row) * w + tx0 + 8 * half) =
+            *(const u32x4*)(st0 + (qi * TY + row) * TX + 8 * half);
+    }
+    if (nlev >= 2 && !blocked) {
+      for (int i = tid; i < CQ * (TY / 2); i += 256) {   // 4 rows x 8 (16 B)
+        const int qi = i >> 2, row = i & 3;
+        const int q = q0 + qi, Y1 = (ty0 >> 1) + row;
+        if (q < nq && Y1 < h1)
+          *(u32x4*)((bf16*)l1 + ((long)b * nq + q) * (h1 * w1) + Y1 * w1 + (tx0 >> 1)) =
+              *(const u32x4*)(st1 + (qi * (TY / 2) + row) * (TX / 2));
+      }
+    }
+    if (nlev >= 3) {
+      for (int i = tid; i < CQ * (TY / 4); i += 256) {   // 2 rows x 4 (8 B)
+        const int qi = i >> 1, row = i & 1;
+        const int q = q0 + qi, Y2 = (ty0 >> 2) + row;
+        if (q < nq && Y2 < h2)
+          *(u32x2*)((bf16*)l2 + ((long)b * nq + q) * (h2 * w2) + Y2 * w2 + (tx0 >> 2)) =
+              *(const u32x2*)(st2 + (qi * (TY / 4) + row) * (TX / 4));
+      }
+    }
+    if (nlev >= 4) {
+      for (int i = tid; i < CQ; i += 256) {               // 1 row x 2 (4 B)
+        const int q = q0 + i, Y3 = ty0 >> 3;
+        if (q < nq && Y3 < h3)
+          *(unsigned*)((bf16*)l3 + ((long)b * nq + q) * (h3 * w3) + Y3 * w3 + (tx0 >> 3)) =
+              *(const unsigned*)(st3 + i * (TX / 8));
       }
     }
   }
@@ -206,13 +299,34 @@ struct LevelPtrs {
   const void* p[4];
 };
 
+// Level layout.  Row-major: [hl][wl] per query.  Blocked (inference, bf16
+// levels of /16-wide maps): levels 0 and 1 are stored as the correlation tile
+// grid's blocks, [ceil(h/8)][ceil(w/16)] blocks of (8 >> l) x (16 >> l)
+// elements (256 / 64 B), i.e. exactly what one corr_pyramid_kernel tile
+// produces per query: the pyramid writes whole cache lines, and a lookup
+// window (10 x 10) touches 2 x 2 blocks instead of 10 row segments.  Levels
+// 2 and 3 stay row-major.
+struct LvGeom {
+  int blocked, nty, ntx;
+};
+JR_DEVICE long lv_qstride(const LvGeom& g, int l, int hl, int wl) {
+  return (g.blocked && l < 2) ? (long)g.nty * g.ntx * (128 >> (2 * l)) : (long)hl * wl;
+}
+JR_DEVICE int lv_off(const LvGeom& g, int l, int wl, int y, int x) {  // y, x >= 0
+  if (g.blocked && l < 2) {
+    const int sh = 3 - l, sw = 4 - l;
+    return (((y >> sh) * g.ntx + (x >> sw)) << (sh + sw)) + ((y & ((1 << sh) - 1)) << sw) + (x & ((1 << sw) - 1));
+  }
+  return y * wl + x;
+}
+
 // blockDim = 256: 4 waves x QPW queries each; lane = level*16 + window column i.
 // General-shape path (any level size); see corr_lookup_wide_kernel below for
 // the fast path.
 template <int R, typename T, int QPW>
 __global__ __launch_bounds__(256) void corr_lookup_kernel(LevelPtrs lv, int nlev, int total, int h, int w,
                                                           const float* __restrict__ coords, bf16* __restrict__ out,
-                                                          int ocs) {
+                                                          int ocs, LvGeom geo) {
   constexpr int S = 2 * R + 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -238,12 +352,12 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LevelPtrs lv, int nlev
       fy[u] = cy - fly;
       const int col = (int)flx - R + i;
       const int row0 = (int)fly - R;
-      const T* map = (const T*)lv.p[lvl] + (long)q * (hl * wl);
+      const T* map = (const T*)lv.p[lvl] + (long)q * lv_qstride(geo, lvl, hl, wl);
       const bool colok = (unsigned)col < (unsigned)wl;
 #pragma unroll
       for (int j = 0; j <= S; ++j) {
         const int rr = row0 + j;
-        if (colok && (unsigned)rr < (unsigned)hl) colv[u][j] = to_f(map[rr * wl + col]);
+        if (colok && (unsigned)rr < (unsigned)hl) colv[u][j] = to_f(map[lv_off(geo, lvl, wl, rr, col)]);
       }
     }
   }
@@ -287,7 +401,7 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LevelPtrs lv, int nlev
 template <int R, typename T, int QPW>
 __global__ __launch_bounds__(256) void corr_lookup_wide_kernel(LevelPtrs lv, int nlev, int total, int h, int w,
                                                                const float* __restrict__ coords,
-                                                               bf16* __restrict__ out, int ocs) {
+                                                               bf16* __restrict__ out, int ocs, LvGeom geo) {
   constexpr int S = 2 * R + 1;
   constexpr int EPC = 16 / sizeof(T);                   // elements per chunk
   constexpr int NCH = (S + 1 + EPC - 1) / EPC + 1;      // chunks per window row
@@ -313,7 +427,7 @@ __global__ __launch_bounds__(256) void corr_lookup_wide_kernel(LevelPtrs lv, int
       const int rr = (int)floorf(coords[2 * (long)q + 1] * sc) - R + j;
       const int cc = (col0 >= 0 ? col0 / EPC : -((-col0 + EPC - 1) / EPC)) * EPC + k * EPC;
       if ((unsigned)rr < (unsigned)hl && (unsigned)cc < (unsigned)wl)
-        v[n] = *(const u32x4*)((const T*)lv.p[l] + (long)q * (hl * wl) + rr * wl + cc);
+        v[n] = *(const u32x4*)((const T*)lv.p[l] + (long)q * lv_qstride(geo, l, hl, wl) + lv_off(geo, l, wl, rr, cc));
     }
   }
 #pragma unroll
@@ -418,19 +532,21 @@ __global__ __launch_bounds__(256) void corr_lookup_bwd_kernel(LevelPtrs dlv, int
 // The wide kernel needs every level's row length and map size to be a whole
 // number of 16-byte chunks and 16-byte aligned level bases.
 template <typename T>
-bool lookup_wide_ok(const LevelPtrs& lv, int L, int h, int w) {
+bool lookup_wide_ok(const LevelPtrs& lv, int L, int h, int w, const LvGeom& geo) {
   constexpr int EPC = 16 / sizeof(T);
   for (int l = 0; l < L; ++l) {
     const int hl = h >> l, wl = w >> l;
-    if (wl % EPC || (hl * wl) % EPC || reinterpret_cast<uintptr_t>(lv.p[l]) % 16) return false;
+    if (reinterpret_cast<uintptr_t>(lv.p[l]) % 16) return false;
+    if (geo.blocked && l < 2) continue;   // 16-byte chunks never cross a block row
+    if (wl % EPC || (hl * wl) % EPC) return false;
   }
   return true;
 }
 
 template <typename T>
 int launch_lookup(const LevelPtrs& lv, int L, int total, int h, int w, int r, const float* coords, bf16* out, int ocs,
-                  hipStream_t stream) {
-  if (r <= 4 && lookup_wide_ok<T>(lv, L, h, w)) {
+                  const LvGeom& geo, hipStream_t stream) {
+  if (r <= 4 && lookup_wide_ok<T>(lv, L, h, w, geo)) {
     constexpr int QPW = 2;
     constexpr int EPC = 16 / sizeof(T);
     dim3 grid((total + 4 * QPW - 1) / (4 * QPW));
@@ -440,7 +556,7 @@ int launch_lookup(const LevelPtrs& lv, int L, int total, int h, int w, int r, co
     constexpr int NT = QPW * 4 * (2 * RR + 2) * ((2 * RR + 2 + EPC - 1) / EPC + 1);                                 \
     const size_t smem = 4 * NT * 16 + 4 * QPW * ocs * sizeof(bf16);                                                 \
     hipLaunchKernelGGL((corr_lookup_wide_kernel<RR, T, QPW>), grid, dim3(256), smem, stream, lv, L, total, h, w,    \
-                       coords, out, ocs);                                                                            \
+                       coords, out, ocs, geo);                                                                       \
     break;                                                                                                          \
   }
       JR_LKW(1) JR_LKW(2) JR_LKW(3) JR_LKW(4)
@@ -452,7 +568,7 @@ int launch_lookup(const LevelPtrs& lv, int L, int total, int h, int w, int r, co
   dim3 grid((total + 4 * QPW - 1) / (4 * QPW));
   const size_t smem = 4 * QPW * ocs * sizeof(bf16);
   switch (r) {
-#define JR_LK(RR) case RR: hipLaunchKernelGGL((corr_lookup_kernel<RR, T, QPW>), grid, dim3(256), smem, stream, lv, L, total, h, w, coords, out, ocs); break;
+#define JR_LK(RR) case RR: hipLaunchKernelGGL((corr_lookup_kernel<RR, T, QPW>), grid, dim3(256), smem, stream, lv, L, total, h, w, coords, out, ocs, geo); break;
     JR_LK(1) JR_LK(2) JR_LK(3) JR_LK(4) JR_LK(5) JR_LK(6)
 #undef JR_LK
     default: return (int)hipErrorInvalidValue;
@@ -464,30 +580,43 @@ int launch_lookup(const LevelPtrs& lv, int L, int total, int h, int w, int r, co
 
 extern "C" int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int w, int nq, int C, int cs, void* lvl0,
                                void* lvl1, void* lvl2, void* lvl3, int num_levels, float scale, int out_bf16,
-                               hipStream_t stream) {
+                               int blocked, hipStream_t stream) {
   if (C % BK != 0 || cs % 8 != 0 || num_levels < 1 || num_levels > 4 || nq < 1) return (int)hipErrorInvalidValue;
-  dim3 grid((nq + CQ - 1) / CQ, ((h + TY - 1) / TY) * ((w + TX - 1) / TX), B);
-  if (out_bf16)
-    hipLaunchKernelGGL(corr_pyramid_kernel<bf16>, grid, dim3(256), 0, stream, (const bf16*)f1, (const bf16*)f2, h, w,
-                       nq, C, cs, (bf16*)lvl0, (bf16*)lvl1, (bf16*)lvl2, (bf16*)lvl3, num_levels, scale);
+  dim3 grid(((nq + CQ - 1) / CQ) * ((h + TY - 1) / TY) * ((w + TX - 1) / TX) * B);
+  // wide stores: whole 16-wide tiles and 16-byte aligned rows / query maps at every level
+  bool wide = out_bf16 && w % 16 == 0 && (h * w) % 8 == 0;
+  void* lv[4] = {lvl0, lvl1, lvl2, lvl3};
+  for (int l = 0; l < num_levels; ++l) wide = wide && reinterpret_cast<uintptr_t>(lv[l]) % 16 == 0;
+  if (blocked && !wide) return (int)hipErrorInvalidValue;   // the blocked layout is written by the wide epilogue only
+  if (wide)
+    hipLaunchKernelGGL((corr_pyramid_kernel<bf16, true>), grid, dim3(256), 0, stream, (const bf16*)f1, (const bf16*)f2,
+                       h, w, nq, C, cs, (bf16*)lvl0, (bf16*)lvl1, (bf16*)lvl2, (bf16*)lvl3, num_levels, scale, blocked);
+  else if (out_bf16)
+    hipLaunchKernelGGL((corr_pyramid_kernel<bf16, false>), grid, dim3(256), 0, stream, (const bf16*)f1,
+                       (const bf16*)f2, h, w, nq, C, cs, (bf16*)lvl0, (bf16*)lvl1, (bf16*)lvl2, (bf16*)lvl3,
+                       num_levels, scale, 0);
   else
-    hipLaunchKernelGGL(corr_pyramid_kernel<float>, grid, dim3(256), 0, stream, (const bf16*)f1, (const bf16*)f2, h, w,
-                       nq, C, cs, (float*)lvl0, (float*)lvl1, (float*)lvl2, (float*)lvl3, num_levels, scale);
+    hipLaunchKernelGGL((corr_pyramid_kernel<float, false>), grid, dim3(256), 0, stream, (const bf16*)f1,
+                       (const bf16*)f2, h, w, nq, C, cs, (float*)lvl0, (float*)lvl1, (float*)lvl2, (float*)lvl3,
+                       num_levels, scale, 0);
   return (int)hipGetLastError();
 }
 
 // h, w: the (target) level-0 map size; nq: query pixels per image (h * w
 // unless the queries are a slab of rows, cp.py).
 extern "C" int jr_corr_lookup(const void* const* levels, int num_levels, int B, int h, int w, int nq, int radius,
-                              const float* coords, void* out, int out_cstride, int lv_bf16, hipStream_t stream) {
+                              const float* coords, void* out, int out_cstride, int lv_bf16, int blocked,
+                              hipStream_t stream) {
   const int S = 2 * radius + 1;
   if (num_levels > 4 || radius < 1 || radius > 6 || out_cstride % 8 != 0 || out_cstride < num_levels * S * S)
     return (int)hipErrorInvalidValue;
   LevelPtrs lv;
   for (int l = 0; l < 4; ++l) lv.p[l] = l < num_levels ? levels[l] : nullptr;
   const int total = B * nq;
-  if (lv_bf16) return launch_lookup<bf16>(lv, num_levels, total, h, w, radius, coords, (bf16*)out, out_cstride, stream);
-  return launch_lookup<float>(lv, num_levels, total, h, w, radius, coords, (bf16*)out, out_cstride, stream);
+  const LvGeom geo{blocked, (h + TY - 1) / TY, (w + TX - 1) / TX};
+  if (lv_bf16)
+    return launch_lookup<bf16>(lv, num_levels, total, h, w, radius, coords, (bf16*)out, out_cstride, geo, stream);
+  return launch_lookup<float>(lv, num_levels, total, h, w, radius, coords, (bf16*)out, out_cstride, geo, stream);
 }
 
 extern "C" int jr_corr_lookup_bwd(void* const* dlevels, int num_levels, int B, int h, int w, int nq, int radius,

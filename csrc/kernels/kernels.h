@@ -124,14 +124,16 @@ int jr_norm_act(const void* x, const float* sx, int mode_x, const float* gamma, 
 // ---------------------------------------------------------------------------
 // f1: bf16 [B][nq][C] query pixels (nq = h*w, or a slab of query rows for
 // context parallelism), f2: bf16 [B][h*w][C] (channel stride cs of both).
-// levels[l]: fp32 or bf16 [B][nq][h_l][w_l].
+// levels[l]: fp32 or bf16 [B][nq][h_l][w_l]; blocked (bf16, w % 16 == 0):
+// levels 0 and 1 as [B][nq][ceil(h/8)][ceil(w/16)] blocks of (8>>l) x (16>>l)
+// (the pyramid kernel's tiles; corr.hip LvGeom), levels 2 and 3 row-major.
 int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int w, int nq, int C, int cs,
                     void* lvl0, void* lvl1, void* lvl2, void* lvl3, int num_levels, float scale, int out_bf16,
-                    hipStream_t stream);
+                    int blocked, hipStream_t stream);
 // coords fp32 [B][nq][2]; out bf16 [B*nq][out_cstride] channels l*(2r+1)^2 + i*(2r+1) + j,
 // zero-filled up to out_cstride.  h, w: level-0 map size.  radius 1..6.
 int jr_corr_lookup(const void* const* levels, int num_levels, int B, int h, int w, int nq, int radius,
-                   const float* coords, void* out, int out_cstride, int lv_bf16, hipStream_t stream);
+                   const float* coords, void* out, int out_cstride, int lv_bf16, int blocked, hipStream_t stream);
 
 // Backward of jr_corr_lookup w.r.t. the levels: accumulates into fp32 dlevels
 // (same shapes as the levels).  gout: bf16 (g_bf16=1) or fp32 [B*nq][gcs].

@@ -541,8 +541,13 @@ static Launch make_corr(const TList& t, const IList& i, double scale, std::vecto
   at::Tensor f1 = opt(t, 0), f2 = opt(t, 1);
   check_bf16(f1, "f1"); check_bf16(f2, "f2");
   const int B = (int)i[0], h = (int)i[1], w = (int)i[2], C = (int)i[3], L = (int)i[4];
-  // optional i[5]: query pixels per image in f1 (a slab of query rows; default all h*w)
+  // optional i[5]: query pixels per image in f1 (a slab of query rows; default all h*w);
+  // optional i[6]: 1 = blocked level layout (kernels.h)
   const int nq = i.size() > 5 ? (int)i[5] : h * w;
+  const int blocked = i.size() > 6 ? (int)i[6] : 0;
+  TORCH_CHECK(!blocked || (w % 16 == 0 && (h * w) % 8 == 0 && nq == h * w),
+              "corr: the blocked level layout needs w % 16 == 0 and whole query maps");
+  const int nty = (h + 7) / 8, ntx = (w + 15) / 16;
   TORCH_CHECK(L >= 1 && L <= 4, "corr: 1..4 levels");
   TORCH_CHECK(C % 64 == 0, "corr: feature channels must be a multiple of 64");
   TORCH_CHECK(nq >= 1 && f1.numel() >= (int64_t)B * nq * cs(f1) && f2.numel() >= (int64_t)B * h * w * cs(f2) &&
@@ -555,7 +560,9 @@ static Launch make_corr(const TList& t, const IList& i, double scale, std::vecto
   for (int l = 0; l < L; ++l) {
     at::Tensor v = opt(t, 2 + l);
     check_level(v, dt);
-    TORCH_CHECK(v.numel() >= (int64_t)B * nq * hl * wl, "corr: level ", l, " too small");
+    TORCH_CHECK(!blocked || dt == at::kBFloat16, "corr: the blocked level layout is bf16");
+    const int64_t per_q = (blocked && l < 2) ? (int64_t)nty * ntx * (128 >> (2 * l)) : (int64_t)hl * wl;
+    TORCH_CHECK(v.numel() >= (int64_t)B * nq * per_q, "corr: level ", l, " too small");
     lv[l] = v.data_ptr();
     if (keep) keep->push_back(v);
     hl >>= 1; wl >>= 1;
@@ -566,7 +573,9 @@ static Launch make_corr(const TList& t, const IList& i, double scale, std::vecto
   const int fcs = cs(f1);
   const float sc = (float)scale;
   const int obf = dt == at::kBFloat16;
-  return [=](hipStream_t s, int) { return jr_corr_pyramid(a, b, B, h, w, nq, C, fcs, lv[0], lv[1], lv[2], lv[3], L, sc, obf, s); };
+  return [=](hipStream_t s, int) {
+    return jr_corr_pyramid(a, b, B, h, w, nq, C, fcs, lv[0], lv[1], lv[2], lv[3], L, sc, obf, blocked, s);
+  };
 }
 
 // t = [coords, out, l0, l1, l2, l3], i = [num_levels, B, h, w, radius]
@@ -575,6 +584,8 @@ static Launch make_lookup(const TList& t, const IList& i, std::vector<at::Tensor
   check_f32(coords, "coords"); check_bf16(out, "out");
   const int L = (int)i[0], B = (int)i[1], h = (int)i[2], w = (int)i[3], r = (int)i[4];
   const int nq = i.size() > 5 ? (int)i[5] : h * w;  // queries per image (slab of rows) vs level-0 map h x w
+  const int blocked = i.size() > 6 ? (int)i[6] : 0;  // blocked level layout (kernels.h)
+  const int nty = (h + 7) / 8, ntx = (w + 15) / 16;
   const int S = 2 * r + 1;
   TORCH_CHECK(L >= 1 && L <= 4 && r >= 1 && r <= 6 && nq >= 1, "lookup: levels 1..4, radius 1..6");
   TORCH_CHECK(cs(out) % 8 == 0 && cs(out) >= L * S * S, "lookup: output channel stride");
@@ -588,7 +599,8 @@ static Launch make_lookup(const TList& t, const IList& i, std::vector<at::Tensor
     at::Tensor v = opt(t, 2 + l);
     check_level(v, dt);
     TORCH_CHECK(hl >= 2 && wl >= 2, "lookup: pyramid level too small");
-    TORCH_CHECK(v.numel() >= (int64_t)B * nq * hl * wl, "lookup: level size");
+    const int64_t per_q = (blocked && l < 2) ? (int64_t)nty * ntx * (128 >> (2 * l)) : (int64_t)hl * wl;
+    TORCH_CHECK(v.numel() >= (int64_t)B * nq * per_q, "lookup: level size");
     lv[l] = v.data_ptr();
     if (keep) keep->push_back(v);
     hl >>= 1; wl >>= 1;
@@ -598,7 +610,7 @@ static Launch make_lookup(const TList& t, const IList& i, std::vector<at::Tensor
   void* op = out.data_ptr();
   const int ocs = cs(out);
   const int lbf = dt == at::kBFloat16;
-  return [=](hipStream_t s, int) { return jr_corr_lookup(lv.data(), L, B, h, w, nq, r, cp, op, ocs, lbf, s); };
+  return [=](hipStream_t s, int) { return jr_corr_lookup(lv.data(), L, B, h, w, nq, r, cp, op, ocs, lbf, blocked, s); };
 }
 
 // ------------------------------------------------------------------ upsample

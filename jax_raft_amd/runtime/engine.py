@@ -629,13 +629,18 @@ class RaftEngine:
         assert (fh_, fw_) == (h, w), "The feature encoder should downsample H and W by 8"
         fmap = alloc("fmap", (2 * B, h, w, self.fmap_ch))
         self._conv(plan, sp["fe.conv"], feat, 2 * B, h, w, fmap)
+        # bf16 levels of /16-wide maps: levels 0 / 1 in the blocked layout (one
+        # pyramid tile per block: whole-line writes, 2 x 2 blocks per lookup window)
+        blocked = int(self.corr_dtype == BF16 and w % 16 == 0 and (h * w) % 8 == 0)
+        self.corr_blocked = bool(blocked)
         levels = []
         hl, wl = h, w
         for l in range(L):
-            levels.append(alloc(f"corr.l{l}", (M, hl, wl), self.corr_dtype))
+            shape = (M, -(-h // 8) * (8 >> l), -(-w // 16) * (16 >> l)) if blocked and l < 2 else (M, hl, wl)
+            levels.append(alloc(f"corr.l{l}", shape, self.corr_dtype))
             hl //= 2
             wl //= 2
-        plan.add_corr([fmap[:B], fmap[B:]] + levels + [None] * (4 - L), [B, h, w, self.fmap_ch, L],
+        plan.add_corr([fmap[:B], fmap[B:]] + levels + [None] * (4 - L), [B, h, w, self.fmap_ch, L, h * w, blocked],
                       1.0 / float(self.fmap_ch) ** 0.5)
         plan.add_wait(E_CTX)
 
@@ -732,7 +737,7 @@ class RaftEngine:
             lane(main)
         else:
             flow_features()
-        plan.add_lookup([coords, corr] + levels + [None] * (4 - L), [L, B, h, w, self.radius])
+        plan.add_lookup([coords, corr] + levels + [None] * (4 - L), [L, B, h, w, self.radius, h * w, blocked])
         if len(cl) == 2:
             c1 = alloc("c1", (M, cl[0]))
             self._conv(plan, sp["me.convcorr1"], corr, B, h, w, c1, act=ACT_RELU)

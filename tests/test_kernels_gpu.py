@@ -169,8 +169,13 @@ def test_flow_epilogue(cfg):
     assert (f8[:, :2].float().cpu() - (new - c0).reshape(M, 2)).abs().max() < 5e-2
 
 
-@pytest.mark.parametrize("h,w,C,L", [(16, 16, 64, 4), (23, 37, 128, 4), (55, 128, 256, 4), (17, 20, 64, 2)])
-def test_corr_pyramid(h, w, C, L):
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("h,w,C,L", [(16, 16, 64, 4), (23, 37, 128, 4), (55, 128, 256, 4), (17, 20, 64, 2),
+                                     (13, 48, 64, 3)])
+def test_corr_pyramid(h, w, C, L, dtype):
+    """All-pairs volume + pooled levels vs the fp32 reference; bf16 levels of
+    /16-wide maps take the LDS-staged wide-store epilogue (odd heights: partial
+    tiles and floor-pooled rows), the rest the per-lane stores."""
     nat = _nat()
     torch.manual_seed(4)
     B = 2
@@ -181,17 +186,18 @@ def test_corr_pyramid(h, w, C, L):
     lv = []
     hl, wl = h, w
     for _ in range(L):
-        lv.append(torch.full((M, hl, wl), float("nan"), device=DEV))
+        lv.append(torch.full((M, hl, wl), float("nan"), device=DEV, dtype=dtype))
         hl //= 2
         wl //= 2
     g1 = f1.to(DEV, torch.bfloat16).contiguous()
     g2 = f2.to(DEV, torch.bfloat16).contiguous()
     nat.ops().corr([g1, g2] + lv + [None] * (4 - L), [B, h, w, C, L], 1.0 / math.sqrt(C))
     torch.cuda.synchronize()
+    tol = 1e-3 if dtype == torch.float32 else 8e-3
     for l in range(L):
-        got = lv[l].cpu()
+        got = lv[l].float().cpu()
         assert not torch.isnan(got).any(), f"level {l} has unwritten cells"
-        assert (got - ref[l]).abs().max().item() < 1e-3 * max(1.0, ref[l].abs().max().item()), l
+        assert (got - ref[l]).abs().max().item() < tol * max(1.0, ref[l].abs().max().item()), l
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -462,3 +468,54 @@ def test_conv_direct(kh, cout, xcs, ycs, ycoff):
     got = y.float().cpu()
     assert (got[:, :ycoff] == 7.0).all() and (got[:, ycoff + cout:] == 7.0).all()
     assert _rel(got[:, ycoff:ycoff + cout], ref.reshape(-1, cout)) < 1e-2
+
+
+@pytest.mark.parametrize("h,w,L,radius", [(55, 128, 4, 4), (13, 48, 3, 3), (16, 32, 2, 4)])
+def test_corr_blocked_layout_pyramid_and_lookup(h, w, L, radius):
+    """Blocked level layout (levels 0 / 1 stored as the pyramid kernel's 8x16
+    tiles): the pyramid written blocked equals the row-major reference once
+    un-blocked, and the lookup on it (wide and per-lane kernels) matches the
+    reference lookup of the row-major pyramid."""
+    nat = _nat()
+    torch.manual_seed(9)
+    B, C = 2, 64
+    f1 = torch.randn(B, h, w, C)
+    f2 = torch.randn(B, h, w, C)
+    ref = R.build_pyramid(_bf(f1), _bf(f2), L)
+    M = B * h * w
+    nty, ntx = -(-h // 8), -(-w // 16)
+    lv = []
+    hl, wl = h, w
+    for l in range(L):
+        shape = (M, nty * (8 >> l), ntx * (16 >> l)) if l < 2 else (M, hl, wl)
+        lv.append(torch.full(shape, float("nan"), device=DEV, dtype=torch.bfloat16))
+        hl //= 2
+        wl //= 2
+    g1 = f1.to(DEV, torch.bfloat16).contiguous()
+    g2 = f2.to(DEV, torch.bfloat16).contiguous()
+    nat.ops().corr([g1, g2] + lv + [None] * (4 - L), [B, h, w, C, L, h * w, 1], 1.0 / math.sqrt(C))
+    torch.cuda.synchronize()
+    hl, wl = h, w
+    for l in range(L):
+        got = lv[l].float().cpu()
+        if l < 2:
+            bh, bw = 8 >> l, 16 >> l
+            got = got.reshape(M, nty, ntx, bh, bw).permute(0, 1, 3, 2, 4).reshape(M, nty * bh, ntx * bw)[:, :hl, :wl]
+        assert not torch.isnan(got).any(), f"level {l} has unwritten cells"
+        assert (got - ref[l]).abs().max().item() < 8e-3 * max(1.0, ref[l].abs().max().item()), l
+        hl //= 2
+        wl //= 2
+    coords = R.make_coords_grid(B, h, w) + torch.randn(B, h, w, 2) * 5
+    coords[0, 0, 0] = torch.tensor([-30.5, 3.25])
+    coords[1, 2, 3] = torch.tensor([w + 9.0, h - 0.5])
+    want = R.index_pyramid([r.to(torch.bfloat16).float() for r in ref], coords, radius)
+    S = 2 * radius + 1
+    ocs = nat.round_up(L * S * S, 8)
+    out = torch.full((M, ocs), 5.0, dtype=torch.bfloat16, device=DEV)
+    nat.ops().lookup([coords.reshape(M, 2).to(DEV).contiguous(), out] + lv + [None] * (4 - L),
+                     [L, B, h, w, radius, h * w, 1])
+    torch.cuda.synchronize()
+    got = out.float().cpu()
+    assert (got[:, L * S * S:] == 0).all()
+    err = (got[:, : L * S * S] - want.reshape(M, -1)).abs().max().item()
+    assert err < 3e-2 * want.abs().max().item(), err
