@@ -23,16 +23,20 @@ def _inputs(B, H, W, seed=0):
 
 @pytest.mark.parametrize("factory", [raft_small, raft_large])
 @pytest.mark.parametrize("use_graph", [False, True])
-def test_engine_matches_golden(factory, use_graph):
+@pytest.mark.parametrize("B,W", [(2, 160), (2, 256), (4, 256)])
+def test_engine_matches_golden(factory, use_graph, B, W):
+    """Engine vs the fp32 golden forward.  W = 160 (w = 20): row-major pyramid,
+    per-lane lookup; W = 256 (w = 32): blocked pyramid levels + wide lookup;
+    B = 4: the lane schedule (streams auto)."""
     torch.manual_seed(0)
     model, variables = factory()
-    i1, i2 = _inputs(2, 128, 160)
+    i1, i2 = _inputs(B, 128, W)
     iters = 4
     ref = model.apply(variables, i1, i2, train=False, num_flow_updates=iters)
     model = model.cuda()
     out = model(i1.cuda(), i2.cuda(), num_flow_updates=iters, use_graph=use_graph)
     torch.cuda.synchronize()
-    assert out.shape == ref.shape == (iters, 2, 128, 160, 2)
+    assert out.shape == ref.shape == (iters, B, 128, W, 2)
     assert torch.isfinite(out).all()
     out = out.cpu()
     mag = ref.norm(dim=-1).mean().item()
