@@ -212,6 +212,62 @@ __global__ __launch_bounds__(256) void flow_taps_kernel(const float* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// Flow head output conv as per-pixel taps (the "taps" formulation above):
+// taps[m][0..24) = fm[m][fcoff .. fcoff + K) . Wt[K][24] (18 real columns,
+// tap * 2 + o; the rest zero).  A skinny GEMM (N = 18): the generic conv tile
+// pads the 18 output rows to 64 and runs 220 one-round workgroups at batch 4
+// (10.7 us, latency bound); here one wave owns 16 pixels and all 32 (padded)
+// output rows as two 16x16x32 MFMA row tiles, and loads every k-step's
+// fragments up front (K = 256: 8 x 16 B features + 16 x 16 B weights per
+// lane), so a wave costs one memory round trip.  Weights are packed host-side
+// (ops/native.py:pack_taps) as A fragments [k-step][row tile 2][lane 64][8].
+// ---------------------------------------------------------------------------
+template <int KS>  // K / 32
+__global__ __launch_bounds__(256) void taps_gemm_kernel(const bf16* __restrict__ fm, int fcs, int fcoff,
+                                                        const u32x4* __restrict__ wpk, float* __restrict__ taps,
+                                                        int tcs, int M) {
+  const int lane = threadIdx.x & 63;
+  const int p0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+  if (p0 >= M) return;  // whole wave
+  const int col = lane & 15, q = lane >> 4;
+  const bf16* bp = fm + (long)min(p0 + col, M - 1) * fcs + fcoff + 8 * q;
+  u32x4 b[KS], a0[KS], a1[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    b[ks] = *(const u32x4*)(bp + 32 * ks);
+    a0[ks] = wpk[(ks * 2) * 64 + lane];
+    a1[ks] = wpk[(ks * 2 + 1) * 64 + lane];
+  }
+  f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const bf16x8 bv = __builtin_bit_cast(bf16x8, b[ks]);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a0[ks]), bv, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a1[ks]), bv, c1, 0, 0, 0);
+  }
+  if (p0 + col < M) {  // lane holds rows 4q .. 4q+3 of each row tile for pixel p0 + col
+    float* tp = taps + (long)(p0 + col) * tcs;
+    *(f32x4*)(tp + 4 * q) = c0;
+    if (q < 2) *(f32x4*)(tp + 16 + 4 * q) = c1;
+  }
+}
+
+extern "C" int jr_taps_gemm(const void* fm, int fcs, int fcoff, int K, const void* wpk, float* taps, int tcs, int M,
+                            hipStream_t stream) {
+  if (tcs < 24 || tcs % 4 || fcs % 8 || fcoff % 8) return (int)hipErrorInvalidValue;
+  const dim3 grid((M + 63) / 64);
+  if (K == 256)
+    hipLaunchKernelGGL(taps_gemm_kernel<8>, grid, dim3(256), 0, stream, (const bf16*)fm, fcs, fcoff,
+                       (const u32x4*)wpk, taps, tcs, M);
+  else if (K == 128)
+    hipLaunchKernelGGL(taps_gemm_kernel<4>, grid, dim3(256), 0, stream, (const bf16*)fm, fcs, fcoff,
+                       (const u32x4*)wpk, taps, tcs, M);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
 extern "C" int jr_flow_taps(const float* t, int tcs, const float* bias, int N, int h, int w, float* coords,
                             float* flow32, void* hx, int hx_cs, int hx_off, void* qx, int qx_cs, int qx_off, void* f8,
                             int f8_cs, hipStream_t stream) {

@@ -240,6 +240,10 @@ int jr_flow_head(const void* fm, int fcs, const void* wt, const float* bias, int
                  void* f8, int f8_cs, hipStream_t stream);
 // delta(p) = bias + sum of the 9 shifted per-tap partials t[p + d][tap] ([M][tcs] fp32,
 // tap-major pairs), then the EPI_FLOW coordinate / flow update (flowhead.hip)
+// taps[m][0..24) = fm[m][fcoff .. fcoff+K) . W (K = 128 / 256, 18 real columns);
+// weights packed by ops/native.py:pack_taps.  taps fp32 [M][tcs >= 24].
+int jr_taps_gemm(const void* fm, int fcs, int fcoff, int K, const void* wpk, float* taps, int tcs, int M,
+                 hipStream_t stream);
 int jr_flow_taps(const float* t, int tcs, const float* bias, int N, int h, int w, float* coords, float* flow32,
                  void* hx, int hx_cs, int hx_off, void* qx, int qx_cs, int qx_off, void* f8, int f8_cs,
                  hipStream_t stream);

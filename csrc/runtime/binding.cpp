@@ -471,6 +471,30 @@ static Launch make_flow_taps(const TList& t, const IList& i, std::vector<at::Ten
   };
 }
 
+// t = [fm (bf16 [M][cs]), wpk (bf16, pack_taps), taps (fp32 [M][>=24])], i = [M, K, fcoff]
+static Launch make_taps_gemm(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor fm = opt(t, 0), wpk = opt(t, 1), taps = opt(t, 2);
+  check_bf16(fm, "fm"); check_bf16(wpk, "wpk"); check_f32(taps, "taps");
+  TORCH_CHECK(i.size() == 3, "taps_gemm: expected 3 ints");
+  const int64_t M = i[0];
+  const int K = (int)i[1], fcoff = (int)i[2];
+  TORCH_CHECK(K == 128 || K == 256, "taps_gemm: K must be 128 or 256");
+  TORCH_CHECK(cs(fm) % 8 == 0 && fcoff % 8 == 0 && fcoff >= 0 && fcoff + K <= cs(fm) && fm.numel() >= M * cs(fm) &&
+                  reinterpret_cast<uintptr_t>(fm.data_ptr()) % 16 == 0,
+              "taps_gemm: fm [M][cs] with a 16-byte aligned K-channel slice");
+  TORCH_CHECK(wpk.numel() == (int64_t)K / 32 * 2 * 64 * 8 && reinterpret_cast<uintptr_t>(wpk.data_ptr()) % 16 == 0,
+              "taps_gemm: packed weights (pack_taps)");
+  TORCH_CHECK(cs(taps) >= 24 && cs(taps) % 4 == 0 && taps.numel() >= M * cs(taps) &&
+                  reinterpret_cast<uintptr_t>(taps.data_ptr()) % 16 == 0,
+              "taps_gemm: taps [M][>=24], 16-byte rows");
+  if (keep) { keep->push_back(fm); keep->push_back(wpk); keep->push_back(taps); }
+  const void* fp = fm.data_ptr();
+  const void* wp = wpk.data_ptr();
+  float* tp = taps.data_ptr<float>();
+  const int fcs = cs(fm), tcs = cs(taps);
+  return [=](hipStream_t s, int) { return jr_taps_gemm(fp, fcs, fcoff, K, wp, tp, tcs, (int)M, s); };
+}
+
 // ---------------------------------------------------------------- direct conv
 // t = [x (bf16 NHWC, 2 channels used), w (bf16 A fragments [cout/16][NKC][64][8]), bias (fp32 [cout]), y (bf16)]
 // i = [N, H, W, cin, KH, KW, PH, PW, cout, relu, y_coff]   (stride 1, output H x W)
@@ -907,6 +931,7 @@ void lookup_bwd_op(const TList& t, IList i) { run_now(make_lookup_bwd(t, i, null
 void im2col_op(const TList& t, IList i) { run_now(make_im2col(t, i, nullptr)); }
 void flow_head_op(const TList& t, IList i) { run_now(make_flow_head(t, i, nullptr)); }
 void flow_taps_op(const TList& t, IList i) { run_now(make_flow_taps(t, i, nullptr)); }
+void taps_gemm_op(const TList& t, IList i) { run_now(make_taps_gemm(t, i, nullptr)); }
 void conv_direct_op(const TList& t, IList i) { run_now(make_conv_direct(t, i, nullptr)); }
 void conv_train_op(const TList& t, IList i, double alpha, const TList& tx, IList ix) {
   run_now(make_conv(t, i, alpha, nullptr, &tx, &ix));
@@ -1020,6 +1045,7 @@ class Plan : public torch::CustomClassHolder {
   void add_copy_channels(TList t, IList i) { push(make_copy_channels(t, i, &keep_), "copy_channels"); }
   void add_flow_head(TList t, IList i) { push(make_flow_head(t, i, &keep_), "flow_head"); }
   void add_flow_taps(TList t, IList i) { push(make_flow_taps(t, i, &keep_), "flow_taps"); }
+  void add_taps_gemm(TList t, IList i) { push(make_taps_gemm(t, i, &keep_), "taps_gemm"); }
   void add_conv_direct(TList t, IList i) { push(make_conv_direct(t, i, &keep_), "conv_direct"); }
   void add_conv_train(TList t, IList i, double alpha, TList tx, IList ix) {
     push(make_conv(t, i, alpha, &keep_, &tx, &ix), "conv_train");
@@ -1278,6 +1304,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("im2col(Tensor?[] t, int[] i) -> ()", &jr::im2col_op);
   m.def("flow_head(Tensor?[] t, int[] i) -> ()", &jr::flow_head_op);
   m.def("flow_taps(Tensor?[] t, int[] i) -> ()", &jr::flow_taps_op);
+  m.def("taps_gemm(Tensor?[] t, int[] i) -> ()", &jr::taps_gemm_op);
   m.def("conv_direct(Tensor?[] t, int[] i) -> ()", &jr::conv_direct_op);
   m.def("conv_train(Tensor?[] t, int[] i, float alpha, Tensor?[] tx, int[] ix) -> ()", &jr::conv_train_op);
   m.def("upsample_convex_bwd(Tensor?[] t, int[] i, float alpha) -> ()", &jr::upsample_convex_bwd_op);
@@ -1313,6 +1340,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_copy_channels", &jr::Plan::add_copy_channels)
       .def("add_flow_head", &jr::Plan::add_flow_head)
       .def("add_flow_taps", &jr::Plan::add_flow_taps)
+      .def("add_taps_gemm", &jr::Plan::add_taps_gemm)
       .def("add_conv_direct", &jr::Plan::add_conv_direct)
       .def("add_conv_train", &jr::Plan::add_conv_train)
       .def("add_upsample_convex_bwd", &jr::Plan::add_upsample_convex_bwd)

@@ -253,6 +253,28 @@ def pack_convex_head(kernel: torch.Tensor, bias: torch.Tensor) -> Tuple[torch.Te
     return wp.reshape(-1), bias.detach().float().contiguous()
 
 
+def pack_taps(kernel: torch.Tensor) -> torch.Tensor:
+    """Flow head output conv (3, 3, K, 2) -> the A fragments of
+    flowhead.hip:taps_gemm_kernel: rows o = tap * 2 + c (18 real of 32), packed
+    [k-step K/32][row tile 2][lane 64][8] bf16 with lane = 16 q + r holding
+    W[k = 32 ks + 8 q + j][o = 16 t + r]."""
+    kh, kw, K, co = kernel.shape
+    assert (kh, kw, co) == (3, 3, 2) and K % 32 == 0, kernel.shape
+    w = kernel.detach().float().reshape(9, K, 2).permute(1, 0, 2).reshape(K, 18)     # [k][tap * 2 + c]
+    a = torch.zeros(K, 32, dtype=torch.float32, device=kernel.device)
+    a[:, :18] = w
+    a = a.reshape(K // 32, 4, 8, 2, 16)            # (ks, q, j, t, r)
+    return a.permute(0, 3, 1, 4, 2).contiguous().to(torch.bfloat16).reshape(-1)
+
+
+def taps_gemm(fm: torch.Tensor, wpk: torch.Tensor, K: int, coff: int = 0) -> torch.Tensor:
+    """Eager flow-head taps: fm bf16 [M][cs] -> fp32 [M][24]."""
+    M = fm.shape[0]
+    out = torch.empty(M, 24, device=fm.device, dtype=torch.float32)
+    ops().taps_gemm([fm, wpk, out], [M, K, coff])
+    return out
+
+
 def convex_head(feat: torch.Tensor, wpk: torch.Tensor, bias: torch.Tensor, flow: torch.Tensor, B: int, h: int,
                 w: int, alpha: float, coff: int = 0, out: Optional[torch.Tensor] = None, tiles: int = 0) -> torch.Tensor:
     """Eager fused mask head: feat bf16 [M][cs] (channels coff..coff+256), flow fp32

@@ -234,6 +234,7 @@ class RaftEngine:
         self._part_streams: List[torch.cuda.Stream] = []
         self._fh2_w = self._fh2_b = None
         self._convex_w = self._convex_b = None
+        self._taps_w = None
         self.model = model
         self.device = torch.device(device)
         self.use_graph = use_graph
@@ -311,6 +312,12 @@ class RaftEngine:
         else:
             self._fh2_w.copy_(wf)
             self._fh2_b.copy_(bf)
+        if fh2.kernel.shape[2] in (128, 256):
+            wt = nat.pack_taps(fh2.kernel.to(self.device))
+            if self._taps_w is None:
+                self._taps_w = wt
+            else:
+                self._taps_w.copy_(wt)
         mp = self.model.mask_predictor
         if mp is not None and tuple(mp.conv.kernel.shape) == (1, 1, 256, 576):
             wc, bc = nat.pack_convex_head(mp.conv.kernel.to(self.device), mp.conv.bias.to(self.device))
@@ -693,7 +700,10 @@ class RaftEngine:
             self._conv(plan, s1, hx, B, h, w, fm, act=ACT_RELU)
             # flow head conv2 + coordinate update (model.py:505) + flow into hx/qx/flow8
             if self.flow_head == "taps":
-                self._conv(plan, sp["fh2.taps"], fm, B, h, w, taps)
+                if self._taps_w is not None:   # skinny GEMM kernel (flowhead.hip), N = 18
+                    plan.add_taps_gemm([fm, self._taps_w, taps], [M, self.fh_hidden, 0])
+                else:
+                    self._conv(plan, sp["fh2.taps"], fm, B, h, w, taps)
                 if before_update is not None:
                     before_update()
                 plan.add_flow_taps([taps, self._fh2_b, coords, f32, hx, qx, flow8], [B, h, w, self.flow_off, self.flow_off])

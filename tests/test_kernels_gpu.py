@@ -519,3 +519,19 @@ def test_corr_blocked_layout_pyramid_and_lookup(h, w, L, radius):
     assert (got[:, L * S * S:] == 0).all()
     err = (got[:, : L * S * S] - want.reshape(M, -1)).abs().max().item()
     assert err < 3e-2 * want.abs().max().item(), err
+
+
+@pytest.mark.parametrize("K,cs,coff,M", [(256, 256, 0, 1000), (256, 512, 0, 28160), (128, 136, 8, 777)])
+def test_taps_gemm_matches_fp32(K, cs, coff, M):
+    """flowhead.hip taps GEMM (the flow head's 3x3 output conv as 9 x 2 per-pixel
+    taps) vs an fp32 matmul with the engine's tap order (tap * 2 + channel)."""
+    nat = _nat()
+    g = torch.Generator().manual_seed(K + M)
+    fm = torch.randn(M, cs, generator=g).to(torch.bfloat16)
+    kern = torch.randn(3, 3, K, 2, generator=g) * 0.05
+    wpk = nat.pack_taps(kern)
+    got = nat.taps_gemm(fm.to(DEV), wpk.to(DEV), K, coff).cpu()
+    w = kern.reshape(9, K, 2).permute(1, 0, 2).reshape(K, 18)
+    ref = fm[:, coff:coff + K].float() @ w.to(torch.bfloat16).float()
+    assert (got[:, 18:] == 0).all()
+    assert (got[:, :18] - ref).abs().max().item() < 1e-3 * ref.abs().max().item() + 1e-4
