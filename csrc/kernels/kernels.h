@@ -240,6 +240,11 @@ int jr_flow_head(const void* fm, int fcs, const void* wt, const float* bias, int
                  void* f8, int f8_cs, hipStream_t stream);
 // delta(p) = bias + sum of the 9 shifted per-tap partials t[p + d][tap] ([M][tcs] fp32,
 // tap-major pairs), then the EPI_FLOW coordinate / flow update (flowhead.hip)
+// Pointwise conv with LDS-resident weights (conv1x1.hip): y[m][y_coff + co] =
+// act(x[m][0 .. kvalid) . W + bias) for co < cout (cout % 64 == 0), weights
+// packed by ops/native.py:pack_conv1x1 with K padded to kpad (128 / 256 / 352 / 384).
+int jr_conv1x1_lds(const void* x, int x_cstride, int kvalid, int kpad, const void* wpk, const float* bias, int act,
+                   void* y, int y_cstride, int y_coff, int cout, int M, hipStream_t stream);
 // taps[m][0..24) = fm[m][fcoff .. fcoff+K) . W (K = 128 / 256, 18 real columns);
 // weights packed by ops/native.py:pack_taps.  taps fp32 [M][tcs >= 24].
 int jr_taps_gemm(const void* fm, int fcs, int fcoff, int K, const void* wpk, float* taps, int tcs, int M,

@@ -471,6 +471,35 @@ static Launch make_flow_taps(const TList& t, const IList& i, std::vector<at::Ten
   };
 }
 
+// t = [x (bf16 [M][cs]), wpk (bf16, pack_conv1x1), bias (fp32 [cout]), y (bf16 [M][ycs])],
+// i = [M, kvalid, kpad, cout, act, y_coff]
+static Launch make_conv1x1(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor x = opt(t, 0), wpk = opt(t, 1), bias = opt(t, 2), y = opt(t, 3);
+  check_bf16(x, "x"); check_bf16(wpk, "wpk"); check_f32(bias, "bias"); check_bf16(y, "y");
+  TORCH_CHECK(i.size() == 6, "conv1x1: expected 6 ints");
+  const int64_t M = i[0];
+  const int kvalid = (int)i[1], kpad = (int)i[2], cout = (int)i[3], act = (int)i[4], ycoff = (int)i[5];
+  TORCH_CHECK(cout % 64 == 0 && kpad % 32 == 0 && kvalid <= kpad && kvalid % 8 == 0 && kvalid <= cs(x),
+              "conv1x1: shapes");
+  TORCH_CHECK(cs(x) % 8 == 0 && x.numel() >= M * cs(x) && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "conv1x1: x [M][cs], 16-byte rows");
+  TORCH_CHECK(wpk.numel() == (int64_t)cout * kpad && reinterpret_cast<uintptr_t>(wpk.data_ptr()) % 16 == 0,
+              "conv1x1: packed weights (pack_conv1x1)");
+  TORCH_CHECK(bias.numel() >= cout && reinterpret_cast<uintptr_t>(bias.data_ptr()) % 16 == 0, "conv1x1: bias");
+  TORCH_CHECK(cs(y) % 8 == 0 && ycoff % 8 == 0 && ycoff + cout <= cs(y) && y.numel() >= M * cs(y) &&
+                  reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
+              "conv1x1: y [M][cs] with a 16-byte aligned cout-channel slice");
+  if (keep) { keep->push_back(x); keep->push_back(wpk); keep->push_back(bias); keep->push_back(y); }
+  const void* xp = x.data_ptr();
+  const void* wp = wpk.data_ptr();
+  const float* bp = bias.data_ptr<float>();
+  void* yp = y.data_ptr();
+  const int xcs = cs(x), ycs = cs(y);
+  return [=](hipStream_t s, int) {
+    return jr_conv1x1_lds(xp, xcs, kvalid, kpad, wp, bp, act, yp, ycs, ycoff, cout, (int)M, s);
+  };
+}
+
 // t = [fm (bf16 [M][cs]), wpk (bf16, pack_taps), taps (fp32 [M][>=24])], i = [M, K, fcoff]
 static Launch make_taps_gemm(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
   at::Tensor fm = opt(t, 0), wpk = opt(t, 1), taps = opt(t, 2);
@@ -932,6 +961,7 @@ void im2col_op(const TList& t, IList i) { run_now(make_im2col(t, i, nullptr)); }
 void flow_head_op(const TList& t, IList i) { run_now(make_flow_head(t, i, nullptr)); }
 void flow_taps_op(const TList& t, IList i) { run_now(make_flow_taps(t, i, nullptr)); }
 void taps_gemm_op(const TList& t, IList i) { run_now(make_taps_gemm(t, i, nullptr)); }
+void conv1x1_op(const TList& t, IList i) { run_now(make_conv1x1(t, i, nullptr)); }
 void conv_direct_op(const TList& t, IList i) { run_now(make_conv_direct(t, i, nullptr)); }
 void conv_train_op(const TList& t, IList i, double alpha, const TList& tx, IList ix) {
   run_now(make_conv(t, i, alpha, nullptr, &tx, &ix));
@@ -1046,6 +1076,7 @@ class Plan : public torch::CustomClassHolder {
   void add_flow_head(TList t, IList i) { push(make_flow_head(t, i, &keep_), "flow_head"); }
   void add_flow_taps(TList t, IList i) { push(make_flow_taps(t, i, &keep_), "flow_taps"); }
   void add_taps_gemm(TList t, IList i) { push(make_taps_gemm(t, i, &keep_), "taps_gemm"); }
+  void add_conv1x1(TList t, IList i) { push(make_conv1x1(t, i, &keep_), "conv1x1"); }
   void add_conv_direct(TList t, IList i) { push(make_conv_direct(t, i, &keep_), "conv_direct"); }
   void add_conv_train(TList t, IList i, double alpha, TList tx, IList ix) {
     push(make_conv(t, i, alpha, &keep_, &tx, &ix), "conv_train");
@@ -1305,6 +1336,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("flow_head(Tensor?[] t, int[] i) -> ()", &jr::flow_head_op);
   m.def("flow_taps(Tensor?[] t, int[] i) -> ()", &jr::flow_taps_op);
   m.def("taps_gemm(Tensor?[] t, int[] i) -> ()", &jr::taps_gemm_op);
+  m.def("conv1x1(Tensor?[] t, int[] i) -> ()", &jr::conv1x1_op);
   m.def("conv_direct(Tensor?[] t, int[] i) -> ()", &jr::conv_direct_op);
   m.def("conv_train(Tensor?[] t, int[] i, float alpha, Tensor?[] tx, int[] ix) -> ()", &jr::conv_train_op);
   m.def("upsample_convex_bwd(Tensor?[] t, int[] i, float alpha) -> ()", &jr::upsample_convex_bwd_op);
@@ -1341,6 +1373,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_flow_head", &jr::Plan::add_flow_head)
       .def("add_flow_taps", &jr::Plan::add_flow_taps)
       .def("add_taps_gemm", &jr::Plan::add_taps_gemm)
+      .def("add_conv1x1", &jr::Plan::add_conv1x1)
       .def("add_conv_direct", &jr::Plan::add_conv_direct)
       .def("add_conv_train", &jr::Plan::add_conv_train)
       .def("add_upsample_convex_bwd", &jr::Plan::add_upsample_convex_bwd)

@@ -253,6 +253,37 @@ def pack_convex_head(kernel: torch.Tensor, bias: torch.Tensor) -> Tuple[torch.Te
     return wp.reshape(-1), bias.detach().float().contiguous()
 
 
+CONV1X1_KPADS = (128, 256, 352, 384)
+
+
+def pack_conv1x1(kernel: torch.Tensor, kpad: int) -> torch.Tensor:
+    """1x1 conv (1, 1, K, N) -> the A fragments of conv1x1.hip: per output group
+    g of 64 channels [g][k-step kpad/32][row tile 4][lane 64][8] bf16, lane =
+    16 q + r holding W[k = 32 ks + 8 q + j][co = 64 g + 16 (r >> 2) + 4 t + (r & 3)]
+    (zero for k >= K), so that a lane's accumulators are 16 contiguous channels."""
+    _, _, K, N = kernel.shape
+    assert N % 64 == 0 and K <= kpad and kpad % 32 == 0, (kernel.shape, kpad)
+    w = torch.zeros(kpad, N, dtype=torch.float32, device=kernel.device)
+    w[:K] = kernel.detach().float().reshape(K, N)
+    dev = kernel.device
+    g, ks, t, l, j = torch.meshgrid(torch.arange(N // 64, device=dev), torch.arange(kpad // 32, device=dev),
+                                    torch.arange(4, device=dev), torch.arange(64, device=dev),
+                                    torch.arange(8, device=dev), indexing="ij")
+    r = l & 15
+    k = 32 * ks + 8 * (l >> 4) + j
+    co = 64 * g + 16 * (r >> 2) + 4 * t + (r & 3)
+    return w[k, co].to(torch.bfloat16).reshape(-1).contiguous()
+
+
+def conv1x1(x: torch.Tensor, wpk: torch.Tensor, bias: torch.Tensor, kvalid: int, kpad: int, cout: int,
+            act: int = ACT_NONE) -> torch.Tensor:
+    """Eager pointwise conv with LDS-resident weights: x bf16 [M][cs] -> bf16 [M][cout]."""
+    M = x.shape[0]
+    y = torch.empty(M, cout, device=x.device, dtype=torch.bfloat16)
+    ops().conv1x1([x, wpk, bias, y], [M, kvalid, kpad, cout, act, 0])
+    return y
+
+
 def pack_taps(kernel: torch.Tensor) -> torch.Tensor:
     """Flow head output conv (3, 3, K, 2) -> the A fragments of
     flowhead.hip:taps_gemm_kernel: rows o = tap * 2 + c (18 real of 32), packed

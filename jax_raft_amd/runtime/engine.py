@@ -235,6 +235,7 @@ class RaftEngine:
         self._fh2_w = self._fh2_b = None
         self._convex_w = self._convex_b = None
         self._taps_w = None
+        self._cc1_w = self._cc1_b = None
         self.model = model
         self.device = torch.device(device)
         self.use_graph = use_graph
@@ -312,6 +313,17 @@ class RaftEngine:
         else:
             self._fh2_w.copy_(wf)
             self._fh2_b.copy_(bf)
+        # the correlation features' first 1x1 conv on the LDS-resident-weight kernel (conv1x1.hip)
+        cc1 = self.model.update_block.motion_encoder.convcorr1.layers_0
+        kpad = next((k for k in nat.CONV1X1_KPADS if k >= self.corr_cs), None)
+        if kpad is not None and cc1.kernel.shape[:2] == (1, 1) and cc1.kernel.shape[3] % 64 == 0:
+            wc = nat.pack_conv1x1(cc1.kernel.to(self.device), kpad)
+            bc = cc1.bias.detach().float().to(self.device).contiguous()
+            if self._cc1_w is None:
+                self._cc1_w, self._cc1_b, self._cc1_kpad = wc, bc, kpad
+            else:
+                self._cc1_w.copy_(wc)
+                self._cc1_b.copy_(bc)
         if fh2.kernel.shape[2] in (128, 256):
             wt = nat.pack_taps(fh2.kernel.to(self.device))
             if self._taps_w is None:
@@ -750,7 +762,11 @@ class RaftEngine:
         plan.add_lookup([coords, corr] + levels + [None] * (4 - L), [L, B, h, w, self.radius, h * w, blocked])
         if len(cl) == 2:
             c1 = alloc("c1", (M, cl[0]))
-            self._conv(plan, sp["me.convcorr1"], corr, B, h, w, c1, act=ACT_RELU)
+            if self._cc1_w is not None:
+                plan.add_conv1x1([corr, self._cc1_w, self._cc1_b, c1],
+                                 [M, self.corr_cs, self._cc1_kpad, cl[0], ACT_RELU, 0])
+            else:
+                self._conv(plan, sp["me.convcorr1"], corr, B, h, w, c1, act=ACT_RELU)
             self._conv(plan, sp["me.convcorr2"], c1, B, h, w, cf, act=ACT_RELU)
         else:
             self._conv(plan, sp["me.convcorr1"], corr, B, h, w, cf, act=ACT_RELU)

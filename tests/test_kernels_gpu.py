@@ -535,3 +535,22 @@ def test_taps_gemm_matches_fp32(K, cs, coff, M):
     ref = fm[:, coff:coff + K].float() @ w.to(torch.bfloat16).float()
     assert (got[:, 18:] == 0).all()
     assert (got[:, :18] - ref).abs().max().item() < 1e-3 * ref.abs().max().item() + 1e-4
+
+
+@pytest.mark.parametrize("K,cs,kpad,N,M", [(324, 328, 352, 256, 28160), (324, 328, 352, 256, 1001), (256, 256, 256, 128, 777),
+                                           (120, 128, 128, 64, 64)])
+def test_conv1x1_lds_matches_fp32(K, cs, kpad, N, M):
+    """conv1x1.hip (weights per 64-channel group in LDS, all k-steps of a
+    wave's pixels loaded up front, packed row permutation) vs fp32 matmul +
+    bias + ReLU; channels past K in the input rows are zero-weighted."""
+    nat = _nat()
+    g = torch.Generator().manual_seed(K + M)
+    x = torch.randn(M, cs, generator=g)
+    x[:, K:] = 0
+    x = x.to(torch.bfloat16)
+    kern = torch.randn(1, 1, K, N, generator=g) * 0.05
+    bias = torch.randn(N, generator=g) * 0.1
+    wpk = nat.pack_conv1x1(kern, kpad)
+    y = nat.conv1x1(x.to(DEV), wpk.to(DEV), bias.to(DEV), cs, kpad, N, act=nat.ACT_RELU).float().cpu()
+    ref = torch.relu(x[:, :K].float() @ kern.reshape(K, N).to(torch.bfloat16).float() + bias)
+    assert (y - ref).abs().max().item() < 1e-2 * ref.abs().max().item() + 1e-3
