@@ -38,8 +38,9 @@ def compute(size, iters):
     model = model.cuda()
     g = torch.Generator().manual_seed(1)
     H, W = size
-    i1 = (torch.rand(2, H, W, 3, generator=g) * 2 - 1).cuda()
-    i2 = (torch.rand(2, H, W, 3, generator=g) * 2 - 1).cuda()
+    j1 = (torch.rand(4, H, W, 3, generator=g) * 2 - 1).cuda()
+    j2 = (torch.rand(4, H, W, 3, generator=g) * 2 - 1).cuda()
+    i1, i2 = j1[:2].contiguous(), j2[:2].contiguous()
     gt = (torch.randn(2, H, W, 2, generator=g) * 3).cuda()
     out = {}
     model.eval()
@@ -47,6 +48,10 @@ def compute(size, iters):
         out["infer_graph"] = model(i1, i2, num_flow_updates=iters).cpu()
         out["infer_graph_2"] = model(i1, i2, num_flow_updates=iters).cpu()
         out["infer_eager"] = model(i1, i2, num_flow_updates=iters, use_graph=False).cpu()
+        # batch 4: the multi-lane schedule (flow features + mask head on a second lane)
+        out["lanes_graph"] = model(j1, j2, num_flow_updates=iters, streams=True).cpu()
+        out["lanes_graph_2"] = model(j1, j2, num_flow_updates=iters, streams=True).cpu()
+        out["lanes_eager"] = model(j1, j2, num_flow_updates=iters, streams=True, use_graph=False).cpu()
     model.train()
     state = {k: v.clone() for k, v in model.state_dict().items()}
     for rep in range(2):
@@ -75,6 +80,7 @@ def main():
     ref = compute(a.size, a.iters)
     bad = []
     for k1, k2 in (("infer_graph", "infer_graph_2"), ("infer_graph", "infer_eager"),
+                   ("lanes_graph", "lanes_graph_2"), ("lanes_graph", "lanes_eager"),
                    ("train_preds_0", "train_preds_1"), ("train_grads_0", "train_grads_1")):
         if not torch.equal(ref[k1], ref[k2]):
             bad.append(f"{k1} != {k2} (max |diff| {(ref[k1] - ref[k2]).abs().max().item():.3g})")
