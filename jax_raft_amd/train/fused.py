@@ -345,14 +345,21 @@ class FusedLoop:
         self.taps = z(M, 24, dtype=F32)
         self.mask = z(T, M, 576) if self.has_mask else None
         self.out = z(T, self.B, self.H, self.W, 2, dtype=F32)
-        levels = []
+        # forward pyramid: bf16 levels, 0 / 1 in the blocked layout when the maps are /16
+        # wide (as in the inference engine: whole-line pyramid writes, 2 x 2 blocks per
+        # lookup window); the lookup output feeding the convs is bf16 anyway.  Its
+        # gradients accumulate in fp32 row-major maps (lookup backward, pyramid backward).
+        self.blocked = int(w % 16 == 0 and (h * w) % 8 == 0)
+        levels, lv_grads = [], []
         hl, wl = h, w
-        for _ in range(self.L):
-            levels.append(z(M, hl, wl, dtype=F32))
+        for l in range(self.L):
+            shape = (M, -(-h // 8) * (8 >> l), -(-w // 16) * (16 >> l)) if self.blocked and l < 2 else (M, hl, wl)
+            levels.append(z(*shape))
+            lv_grads.append(z(M, hl, wl, dtype=F32))
             hl //= 2
             wl //= 2
         self.levels = levels
-        self.lv_grads = [torch.zeros_like(l) for l in levels]
+        self.lv_grads = lv_grads
         # backward
         self.gout = z(T, self.B, self.H, self.W, 2, dtype=F32)
         self.dmask = z(T, M, 576) if self.has_mask else None
@@ -568,7 +575,8 @@ class FusedLoop:
         E_PACK, E_FLOW, E_FH = 0, 2, 3
         fl = self.fwd_lanes
         self.packer.record(P)   # this step's weights -> every spec (forward and data-gradient layouts)
-        P.add_corr([self.fm1, self.fm2] + self.levels + [None] * (4 - self.L), [B, h, w, self.fmap_ch, self.L],
+        P.add_corr([self.fm1, self.fm2] + self.levels + [None] * (4 - self.L),
+                   [B, h, w, self.fmap_ch, self.L, h * w, self.blocked],
                    1.0 / float(self.fmap_ch) ** 0.5)
         P.add_record(E_PACK)
         for g in range(G):  # loop-invariant context share of every gate (+ biases), fp32
@@ -597,7 +605,7 @@ class FusedLoop:
             if not fl:
                 flow_features(t)
             P.add_lookup([self.coords[t], self.corr[t]] + self.levels + [None] * (4 - self.L),
-                         [self.L, B, h, w, self.radius])
+                         [self.L, B, h, w, self.radius, h * w, self.blocked])
             if len(cl) == 2:
                 self._conv(P, "cc1", self.corr[t], self.c1[t], act=ACT_RELU)
                 self._conv(P, "cc2", self.c1[t], self.cf[t], act=ACT_RELU)
