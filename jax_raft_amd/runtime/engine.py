@@ -173,7 +173,9 @@ class RaftEngine:
             and dropped: two edges with the mask conv ahead of the flow
             features and the flow double-buffered by parity, 276 -- the
             longer chain before E_FLOW stalls the motion conv; one event after
-            the whole mask lane, 289-292); "side" runs
+            the whole mask lane, 289-292; the first GRU's h-part conv moved onto
+            the mask lane as a bias map, 298 vs 302 -- it contends with the
+            correlation convs); "side" runs
             them on their own lane concurrently with the lookup + correlation
             convs; "main" runs them on the critical-path lane before the lookup.
         double_buffer: ("lanes" schedule) double-buffer the flow head outputs by iteration
