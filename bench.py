@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--gate-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="storage of the GRU z gate / folded context bias map (the hidden state is fp32 either way)")
     ap.add_argument("--flow-lane", default="mask", choices=["side", "main", "mask"])
+    ap.add_argument("--no-copy-output", action="store_true",
+                    help="return the engine's static output buffer instead of a fresh copy (measurement knob)")
     ap.add_argument("--convex", default="head", choices=["fused", "separate", "head"],
                     help="mask predictor 1x1 conv + convex upsampling: conv epilogue / two kernels / dedicated kernel")
     ap.add_argument("--mask-head", default="split", choices=["split", "fused"],
@@ -133,7 +135,7 @@ def main():
                      flow_head=args.flow_head, double_buffer=args.double_buffer, direct_flow=not args.no_direct_flow,
                      gate_dtype=torch.bfloat16 if args.gate_dtype == "bf16" else torch.float32,
                      flow_lane=args.flow_lane, mask_head=args.mask_head,
-                     convex=args.convex)
+                     convex=args.convex, copy_output=not args.no_copy_output)
     pipelined = args.pipeline and not args.no_graph
     eng = model.engine(dev, **engine_kw) if pipelined else None
 

@@ -40,12 +40,14 @@ __global__ __launch_bounds__(256, 2) void convex_head_kernel(const bf16* __restr
                                                              const u32x4* __restrict__ wpk,
                                                              const float* __restrict__ bias, float alpha,
                                                              const float* __restrict__ flow, int B, int h, int w,
-                                                             float* __restrict__ out, int nblk) {
+                                                             float* __restrict__ out, const long long* __restrict__ out_slot,
+                                                             long out_off, int nblk) {
   __shared__ u32x4 sA[8 * 9 * 64];  // this group's A fragments: [ks][tap][lane]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int id = blockIdx.x;
   const int g = (id >> 3) & 3, pb = (id >> 5) * 8 + (id & 7);
   if (pb >= nblk) return;  // whole block, before any barrier
+  if (out_slot) out = (float*)(*out_slot) + out_off;  // output address supplied at run time (fresh tensor per call)
   const int HW = h * w, M = B * HW;
   for (int f = wave; f < 72; f += 4)
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(wpk + (f * 4 + g) * 64 + lane),
@@ -135,8 +137,8 @@ __global__ __launch_bounds__(256, 2) void convex_head_kernel(const bf16* __restr
 }  // namespace
 
 extern "C" int jr_convex_head(const void* feat, int feat_cstride, int feat_coff, const void* wpk, const float* bias,
-                              float alpha, const float* flow, int B, int h, int w, float* out, int tiles,
-                              hipStream_t stream) {
+                              float alpha, const float* flow, int B, int h, int w, float* out, const void* out_slot,
+                              long out_off, int tiles, hipStream_t stream) {
   const int M = B * h * w;
   // pixel tiles per wave (`tiles` 1 / 2, or 0 = auto): 2 when that still gives
   // >= 384 blocks (2 per CU fit: 72 KB of LDS each), else 1
@@ -146,9 +148,9 @@ extern "C" int jr_convex_head(const void* feat, int feat_cstride, int feat_coff,
   const dim3 grid((nblk + 7) / 8 * 32);
   if (nc == 2)
     hipLaunchKernelGGL(convex_head_kernel<2>, grid, dim3(256), 0, stream, (const bf16*)feat, feat_cstride, feat_coff,
-                       (const u32x4*)wpk, bias, alpha, flow, B, h, w, out, nblk);
+                       (const u32x4*)wpk, bias, alpha, flow, B, h, w, out, (const long long*)out_slot, out_off, nblk);
   else
     hipLaunchKernelGGL(convex_head_kernel<1>, grid, dim3(256), 0, stream, (const bf16*)feat, feat_cstride, feat_coff,
-                       (const u32x4*)wpk, bias, alpha, flow, B, h, w, out, nblk);
+                       (const u32x4*)wpk, bias, alpha, flow, B, h, w, out, (const long long*)out_slot, out_off, nblk);
   return (int)hipGetLastError();
 }

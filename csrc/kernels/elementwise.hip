@@ -51,8 +51,9 @@ __global__ __launch_bounds__(256) void upsample_convex_kernel(const bf16* __rest
 }
 
 __global__ void upsample_bilinear_kernel(const float* __restrict__ flow, int B, int h, int w,
-                                         float* __restrict__ out) {
+                                         float* __restrict__ out, const long long* __restrict__ out_slot, long out_off) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (out_slot) out = (float*)(*out_slot) + out_off;  // output address supplied at run time
   const int H8 = 8 * h, W8 = 8 * w;
   const long total = (long)B * H8 * W8;
   if (idx >= total) return;
@@ -295,9 +296,11 @@ extern "C" int jr_upsample_convex(const void* mask, int mask_cstride, const floa
   return (int)hipGetLastError();
 }
 
-extern "C" int jr_upsample_bilinear(const float* flow, int B, int h, int w, float* out, hipStream_t stream) {
+extern "C" int jr_upsample_bilinear(const float* flow, int B, int h, int w, float* out, const void* out_slot,
+                                    long out_off, hipStream_t stream) {
   const long total = (long)B * 64 * h * w;
-  hipLaunchKernelGGL(upsample_bilinear_kernel, dim3(nblk(total, 256)), dim3(256), 0, stream, flow, B, h, w, out);
+  hipLaunchKernelGGL(upsample_bilinear_kernel, dim3(nblk(total, 256)), dim3(256), 0, stream, flow, B, h, w, out,
+                     (const long long*)out_slot, out_off);
   return (int)hipGetLastError();
 }
 

@@ -150,11 +150,17 @@ int jr_corr_lookup_bwd(void* const* dlevels, int num_levels, int B, int h, int w
 // (reference channel order k*64 + s), logits * alpha -> softmax over the 9
 // taps -> convex combination of 8 * flow (fp32 [M][2]) -> out (B, 8h, 8w, 2).
 // tiles: 16-pixel tiles per wave (1 / 2; 0 = by problem size).
+// out_slot (optional): as jr_upsample_bilinear.
 int jr_convex_head(const void* feat, int feat_cstride, int feat_coff, const void* wpk, const float* bias,
-                   float alpha, const float* flow, int B, int h, int w, float* out, int tiles, hipStream_t stream);
+                   float alpha, const float* flow, int B, int h, int w, float* out, const void* out_slot, long out_off,
+                   int tiles, hipStream_t stream);
 int jr_upsample_convex(const void* mask, int mask_cstride, const float* flow, int B, int h, int w,
                        float* out, hipStream_t stream);
-int jr_upsample_bilinear(const float* flow, int B, int h, int w, float* out, hipStream_t stream);
+// out_slot (optional, device int64): the output base address, read at run time
+// (+ out_off floats) instead of `out` -- a captured graph can write a fresh
+// output tensor per replay.
+int jr_upsample_bilinear(const float* flow, int B, int h, int w, float* out, const void* out_slot, long out_off,
+                         hipStream_t stream);
 // Backward of jr_upsample_convex (training): mask bf16 [M][mask_cs] (the 576 logits, already
 // scaled by alpha), flow fp32 [M][2], gout fp32 [B][8h][8w][2] ->
 //   dmask bf16 [M][dmask_cs]: alpha * dL/dlogit (the gradient of the un-scaled mask conv output)

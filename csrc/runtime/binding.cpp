@@ -700,12 +700,17 @@ static Launch make_upsample_convex(const TList& t, const IList& i, std::vector<a
   };
 }
 
-// t = [feat, wpk, bias, flow, out], i = [B, h, w, feat_coff, out_iter_stride(, tiles per wave: 0 = auto)]
+// t = [feat, wpk, bias, flow, out, out_slot?], i = [B, h, w, feat_coff, out_iter_stride(, tiles per wave: 0 =
+// auto(, out_slot offset in floats))].  out_slot: device int64 holding the output base address at run time
+// (the engine points it at a fresh tensor per call); `out` (same shape) bounds the writes.
 static Launch make_convex_head(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep) {
-  at::Tensor feat = opt(t, 0), wpk = opt(t, 1), bias = opt(t, 2), flow = opt(t, 3), out = opt(t, 4);
+  at::Tensor feat = opt(t, 0), wpk = opt(t, 1), bias = opt(t, 2), flow = opt(t, 3), out = opt(t, 4), slot = opt(t, 5);
   check_bf16(feat, "feat"); check_bf16(wpk, "wpk"); check_f32(bias, "bias"); check_f32(flow, "flow");
-  TORCH_CHECK(i.size() == 5 || i.size() == 6, "convex_head: expected 5 or 6 ints");
-  const int tiles = i.size() == 6 ? (int)i[5] : 0;
+  TORCH_CHECK(i.size() >= 5 && i.size() <= 7, "convex_head: expected 5 to 7 ints");
+  const int tiles = i.size() >= 6 ? (int)i[5] : 0;
+  const int64_t slot_off = i.size() >= 7 ? i[6] : 0;
+  TORCH_CHECK(!slot.defined() || (slot.is_cuda() && slot.scalar_type() == at::kLong && slot.numel() == 1),
+              "convex_head: out_slot must be one device int64");
   TORCH_CHECK(tiles == 0 || tiles == 1 || tiles == 2, "convex_head: tiles per wave 0/1/2");
   const int B = (int)i[0], h = (int)i[1], w = (int)i[2], coff = (int)i[3];
   const int64_t stride = i[4];
@@ -722,6 +727,8 @@ static Launch make_convex_head(const TList& t, const IList& i, double alpha, std
   const int64_t cap = check_flow_out(out, B, h, w);
   TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 32 == 0, "convex_head: out must be 32-byte aligned");
   if (keep) { keep->push_back(feat); keep->push_back(wpk); keep->push_back(bias); keep->push_back(flow); keep->push_back(out); }
+  if (keep && slot.defined()) keep->push_back(slot);
+  const void* sp = slot.defined() ? slot.data_ptr() : nullptr;
   const void* fp = feat.data_ptr();
   const void* wp = wpk.data_ptr();
   const float* bp = bias.data_ptr<float>();
@@ -731,24 +738,29 @@ static Launch make_convex_head(const TList& t, const IList& i, double alpha, std
   return [=](hipStream_t s, int it) {
     const int64_t off = stride * it;
     if (off + M * 128 > cap) return (int)hipErrorInvalidValue;
-    return jr_convex_head(fp, fcs, coff, wp, bp, a, flp, B, h, w, op + off, tiles, s);
+    return jr_convex_head(fp, fcs, coff, wp, bp, a, flp, B, h, w, op + off, sp, (long)(slot_off + off), tiles, s);
   };
 }
 
 // t = [flow, out], i = [B, h, w, out_iter_stride]
+// (t[2]: optional out_slot, i[4]: its offset in floats; see make_convex_head)
 static Launch make_upsample_bilinear(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
-  at::Tensor flow = opt(t, 0), out = opt(t, 1);
+  at::Tensor flow = opt(t, 0), out = opt(t, 1), slot = opt(t, 2);
   check_f32(flow, "flow");
   const int B = (int)i[0], h = (int)i[1], w = (int)i[2];
   const int64_t stride = i[3];
+  const int64_t slot_off = i.size() > 4 ? i[4] : 0;
+  TORCH_CHECK(!slot.defined() || (slot.is_cuda() && slot.scalar_type() == at::kLong && slot.numel() == 1),
+              "upsample_bilinear: out_slot must be one device int64");
   const int64_t cap = check_flow_out(out, B, h, w);
-  if (keep) { keep->push_back(flow); keep->push_back(out); }
+  if (keep) { keep->push_back(flow); keep->push_back(out); if (slot.defined()) keep->push_back(slot); }
   const float* fp = flow.data_ptr<float>();
   float* op = out.data_ptr<float>();
+  const void* sp = slot.defined() ? slot.data_ptr() : nullptr;
   return [=](hipStream_t s, int it) {
     const int64_t off = stride * it;
     if (off + (int64_t)B * 64 * h * w * 2 > cap) return (int)hipErrorInvalidValue;
-    return jr_upsample_bilinear(fp, B, h, w, op + off, s);
+    return jr_upsample_bilinear(fp, B, h, w, op + off, sp, (long)(slot_off + off), s);
   };
 }
 

@@ -114,6 +114,13 @@ class _PlanState:
     inp2: Optional[torch.Tensor] = None
     out: Optional[torch.Tensor] = None
     n_iters: int = 0
+    # Output indirection: every output writer (convex head / bilinear
+    # upsampling) reads its destination base from this device int64, so a
+    # replay can write into a fresh tensor (forward with copy_output) instead
+    # of the captured buffer + a clone of it.  slot_ok: all writers use it.
+    out_slot: Optional[torch.Tensor] = None
+    slot_ok: bool = True
+    slot_ptr: int = 0
 
 
 class PendingFlow:
@@ -568,6 +575,8 @@ class RaftEngine:
         st.inp1 = torch.zeros((B, H, W, 3), dtype=F32, device=dev)
         st.inp2 = torch.zeros((B, H, W, 3), dtype=F32, device=dev)
         st.out = torch.zeros((n_iters if all_iters else 1, B, H, W, 2), dtype=F32, device=dev)
+        st.slot_ptr = st.out.data_ptr()
+        st.out_slot = torch.tensor([st.slot_ptr], dtype=torch.int64, device=dev)
         lanes = (0, 1, 2) if self.streams else (0, 0, 0)
         for part, plan in enumerate(plans):
             self._build_part(st, plan, part * nb, nb, H, W, n_iters, f"p{part}.", lanes, 0, all_iters)
@@ -600,6 +609,7 @@ class RaftEngine:
         inp1 = st.inp1[b0:b0 + B]
         inp2 = st.inp2[b0:b0 + B]
         out = st.out[:, b0:b0 + B]
+        out_off = (out.data_ptr() - st.out.data_ptr()) // 4   # in floats, from the slot's base
 
         # ---------------- prologue: encoders + correlation pyramid
         # lanes: 0 = feature encoder + correlation pyramid, 1 = context encoder
@@ -737,18 +747,20 @@ class RaftEngine:
                 else:
                     coff = self.fh_hidden
                 if self.convex == "head":
-                    plan.add_convex_head([fm, self._convex_w, self._convex_b, f32, out], [B, h, w, coff, stride],
-                                         m.mask_predictor.multiplier)
+                    plan.add_convex_head([fm, self._convex_w, self._convex_b, f32, out, st.out_slot],
+                                         [B, h, w, coff, stride, 0, out_off], m.mask_predictor.multiplier)
                 elif self.convex in ("fused", "head"):
+                    st.slot_ok = False
                     # mask logits never leave the CU: softmax + convex combination in the epilogue
                     self._conv(plan, sp["mask.convex"], fm, B, h, w, out, x_coff=coff, epi=EPI_CONVEX,
                                flow32=f32, alpha=m.mask_predictor.multiplier, it_stride=stride)
                 else:
+                    st.slot_ok = False
                     self._conv(plan, sp["mask"], fm, B, h, w, mask, x_coff=coff,
                                alpha=m.mask_predictor.multiplier)
                     plan.add_upsample_convex([mask, f32, out], [B, h, w, stride])
             else:
-                plan.add_upsample_bilinear([f32, out], [B, h, w, stride])
+                plan.add_upsample_bilinear([f32, out, st.out_slot], [B, h, w, stride, out_off])
 
         if mask_lane_flow:
             pass
@@ -844,6 +856,9 @@ class RaftEngine:
             self._states[key] = st
         st.inp1.copy_(image1)
         st.inp2.copy_(image2)
+        fresh = self.copy_output and st.slot_ok
+        out = torch.empty_like(st.out) if fresh else st.out
+        self._point_slot(st, out)
         if len(st.plans) == 1:
             self._launch(st.plan, num_flow_updates)
         else:
@@ -856,7 +871,17 @@ class RaftEngine:
                     self._launch(plan, num_flow_updates)
             for strm in self._part_streams[:len(st.plans)]:
                 cur.wait_stream(strm)
+        if fresh:
+            return out
         return st.out.clone() if self.copy_output else st.out
+
+    @staticmethod
+    def _point_slot(st: _PlanState, out: torch.Tensor) -> None:
+        """Aim the plan's output writers at ``out`` (stream-ordered: the
+        update is a tiny copy on the current stream, before the launch)."""
+        if st.slot_ptr != out.data_ptr():
+            st.out_slot.fill_(out.data_ptr())
+            st.slot_ptr = out.data_ptr()
 
     # ------------------------------------------------- pipelined (serving)
     @torch.no_grad()
@@ -902,6 +927,7 @@ class RaftEngine:
         plan = st.plan
         cur = torch.cuda.current_stream(self.device)
         cur.wait_event(pipe["e_pro"][slot])      # the slot's last prologue has read its inputs
+        self._point_slot(st, st.out)
         st.inp1.copy_(image1)
         st.inp2.copy_(image2)
         pipe["e_in"][slot].record(cur)

@@ -58,6 +58,29 @@ def test_graph_replay_equals_eager():
     assert (a - b).abs().max().item() < 1e-3
 
 
+@pytest.mark.parametrize("factory", [raft_small, raft_large])
+def test_fresh_outputs_are_not_overwritten(factory):
+    """The output slot: each graph replay writes a fresh tensor (bilinear
+    upsampling at raft_small, the convex head at raft_large), so an earlier
+    result survives later calls, and the results equal the static-buffer mode's."""
+    from jax_raft_amd.runtime.engine import RaftEngine
+    model, _ = factory()
+    model = model.cuda()
+    xa = [t.cuda() for t in _inputs(2, 128, 256, seed=5)]
+    xb = [t.cuda() for t in _inputs(2, 128, 256, seed=6)]
+    eng = RaftEngine(model, torch.device("cuda"), use_graph=True)
+    a = eng.forward(*xa, num_flow_updates=3)
+    b = eng.forward(*xb, num_flow_updates=3)
+    torch.cuda.synchronize()
+    assert a.data_ptr() != b.data_ptr()
+    eng.copy_output = False   # the same plan, writing its static buffer
+    ra = eng.forward(*xa, num_flow_updates=3).clone()
+    rb = eng.forward(*xb, num_flow_updates=3).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(a, ra) and torch.equal(b, rb)
+    assert (a - b).abs().max().item() > 1e-3
+
+
 def test_weight_update_repacks():
     model, _ = raft_small()
     model = model.cuda()
