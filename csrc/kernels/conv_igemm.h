@@ -957,8 +957,8 @@ JR_DEVICE void raw_barrier() {
 // A stage is (BCO + BP) LDS rows of 128 B (64 bf16 of K): the weight tile then
 // the im2col pixel tile.  It is filled by 1-KiB LDS-DMA pieces
 // (`buffer_load_dwordx4 ... lds`, lane i -> piece base + 16 i) of 8 whole
-// rows, (BCO + BP) / 32 pieces per wave, so every wave issues the same count
-// and the ring waits are exact counted `vmcnt`s with raw barriers: stage
+// rows, (BCO + BP) / (8 NW) pieces per wave, so every wave issues the same
+// count and the ring waits are exact counted `vmcnt`s with raw barriers: stage
 // ks + NS - 1 is in flight while stage ks feeds the MFMAs.  Row r keeps
 // 16-B chunk c at slot c ^ (r & 6).  That swizzle depends only on the row
 // inside a piece, so each DMA lane fetches one FIXED chunk
@@ -968,20 +968,23 @@ JR_DEVICE void raw_barrier() {
 // {0-3,12-15,20-27}, {4-11,16-19,28-31}, ... (rows li and li^4.. of a group
 // land on distinct (row parity, slot) pairs).  No staging VGPRs and no
 // ds_write traffic: the LDS array only serves the fragment reads.
+// NW = 8 / 16 waves (one block per CU at 256x128 tiles, 144 KiB ring at NS 3)
+// with the FAST im2col loader (ConvParams::fast) are the configs that compete
+// with kernels R / P on the refinement-loop convs (configs 35..39).
 // ---------------------------------------------------------------------------
-template <int BCO, int BP, int WCO, int NS, int EPI>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, (BCO + BP) * NS * 128 > 81920 ? 1 : 2))) void conv_d2_kernel(const ConvParams p) {
-  constexpr int WP = 4 / WCO;
+template <int BCO, int BP, int WCO, int NS, int EPI, bool FAST = false, int NW = 4>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW > 4 || (BCO + BP) * NS * 128 > 81920 ? 1 : 2))) void conv_d2_kernel(const ConvParams p) {
+  constexpr int WP = NW / WCO;
   constexpr int WTCO = BCO / WCO;
   constexpr int WTP = BP / WP;
   constexpr int TM = WTCO / 16;
   constexpr int TN = WTP / 16;
   constexpr int ROWS = BCO + BP;
-  constexpr int PPW = ROWS / 32;                   // 8-row pieces per wave per stage
+  constexpr int PPW = ROWS / (8 * NW);             // 8-row pieces per wave per stage
   constexpr int STAGE = ROWS * BK;                 // bf16 elements
   constexpr unsigned OOB = 0x80000000u;
-  static_assert(TM >= 1 && TN >= 1 && WCO * WP == 4 && ROWS % 32 == 0, "tile");
-  static_assert(NS >= 2 && NS <= 4, "ring depth");
+  static_assert(TM >= 1 && TN >= 1 && WCO * WP == NW && ROWS % (8 * NW) == 0, "tile");
+  static_assert(NS >= 2 && NS <= 4 && NS * STAGE * 2 <= 160 * 1024, "ring depth");
   __shared__ __attribute__((aligned(16))) bf16 smem[NS * STAGE];
 
   const int tid = threadIdx.x;
@@ -1000,11 +1003,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, (BCO + B
       __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wsrd =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)p.w_bytes, 0x00020000);
+  const unsigned xrow_bytes = (unsigned)p.x_cstride * 2;
 
   // piece j of this wave covers stage rows q*8 .. q*8+7, q = wave*PPW + j:
   // rows < BCO are weight rows, the rest pixel rows.  Per-lane row = q*8 + lane/8.
   int ih0[PPW], iw0[PPW];
   unsigned rbase[PPW];
+  [[maybe_unused]] FastRow frow[PPW];
 #pragma unroll
   for (int j = 0; j < PPW; ++j) {
     const int row = (wave * PPW + j) * 8 + (lane >> 3);
@@ -1029,6 +1034,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, (BCO + B
         iw0[j] = -(1 << 28);
         rbase[j] = 0;
       }
+      if constexpr (FAST) frow[j] = fast_row(p, ih0[j], iw0[j], rbase[j], m < p.M, cl, xrow_bytes);
     }
   }
 
@@ -1039,20 +1045,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, (BCO + B
   int kh = tap / p.KW;
   int kw = tap - kh * p.KW;
   int ks_next = 0;
-  const unsigned xrow_bytes = (unsigned)p.x_cstride * 2;
   const int nks = p.kpad / BK;
+  [[maybe_unused]] FastStage fst;
+  [[maybe_unused]] const int cpb = (p.KH * p.KW == 1) ? (p.kpad / BK) : (p.cin8 >> 6);
 
   auto issue = [&]() {
     bf16* st = smem + (ks_next % NS) * STAGE;
     const bool kvalid = kh < p.KH;
     const bool kin = ks_next < nks;
     const unsigned kofs = (unsigned)ks_next * (BK * 2);
+    [[maybe_unused]] bool cv = false;
+    [[maybe_unused]] unsigned soff = 0;
+    if constexpr (FAST) {
+      cv = kin && cl * 8 < p.cin8 - fst.cb * 64;   // channel tail of a 1x1 conv
+      soff = (unsigned)(fst.kh * p.W + fst.kw) * xrow_bytes + (unsigned)fst.cb * 128u;
+    }
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
       const int q = wave * PPW + j;               // wave-uniform
       bf16* dst = st + q * 8 * BK;
       if (q * 8 < BCO) {
         dma16(wsrd, dst, (kin && ih0[j] == 0) ? rbase[j] + kofs : OOB);
+      } else if constexpr (FAST) {
+        const bool ok = cv && ((frow[j].mask >> (fst.tap & 31)) & 1u);
+        dma16(xsrd, dst, ok ? frow[j].off + soff : OOB);
       } else {
         const int ihl = ih0[j] + kh, iwl = iw0[j] + kw;  // coordinates in the (dilated) input
         const int ih = ihl >> p.dsh, iw = iwl >> p.dsw;
@@ -1063,10 +1079,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, (BCO + B
       }
     }
     ++ks_next;
-    cc += 8;
-    while (cc >= cpt) {
-      cc -= cpt;
-      if (++kw == p.KW) { kw = 0; ++kh; }
+    if constexpr (FAST) {
+      fst.advance(p, cpb);
+    } else {
+      cc += 8;
+      while (cc >= cpt) {
+        cc -= cpt;
+        if (++kw == p.KW) { kw = 0; ++kh; }
+      }
     }
   };
 
@@ -1136,6 +1156,11 @@ int launch_cfg(const ConvParams* p, int epi, hipStream_t s) {
     if (p->fast) hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, true, NW_>), grid, dim3(NW_ * 64), 0, s, *p); \
     else hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, false, NW_>), grid, dim3(NW_ * 64), 0, s, *p);         \
   } else if constexpr (KIND == 3 || KIND == 4) hipLaunchKernelGGL((conv_d2_kernel<BCO, BP, WCO, KIND - 1, E>), grid, block, 0, s, *p); \
+  else if constexpr (KIND >= 12 && KIND <= 14) {                                              \
+    constexpr int NW_ = KIND == 13 ? 8 : 16, NS_ = KIND == 14 ? 2 : 3;                          \
+    if (p->fast) hipLaunchKernelGGL((conv_d2_kernel<BCO, BP, WCO, NS_, E, true, NW_>), grid, dim3(NW_ * 64), 0, s, *p); \
+    else hipLaunchKernelGGL((conv_d2_kernel<BCO, BP, WCO, NS_, E, false, NW_>), grid, dim3(NW_ * 64), 0, s, *p);         \
+  } \
   else if constexpr (KIND == 2) {                                                              \
     if (p->fast) hipLaunchKernelGGL((conv_m32_kernel<BCO, BP, WCO, E, true>), grid, block, 0, s, *p); \
     else hipLaunchKernelGGL((conv_m32_kernel<BCO, BP, WCO, E, false>), grid, block, 0, s, *p);         \

@@ -193,13 +193,13 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
     TORCH_CHECK(p.cout % 16 == 0 && p.cout >= 16 && p.act == 0 /* ACT_NONE */ && !bmap.defined(),
                 "CONVEX: logits in 16-channel sub-pixel groups, no activation / bias map");
     // the epilogue needs 16 contiguous channels per lane: every config but the 16- / 32-row wave tiles
-    TORCH_CHECK(cfg != 3 && cfg != 5 && cfg != 19 && cfg != 21, "CONVEX: tile config ", cfg,
+    TORCH_CHECK(cfg != 3 && cfg != 5 && cfg != 19 && cfg != 21 && cfg != 36, "CONVEX: tile config ", cfg,
                 " has < 16 channels per lane");
     TORCH_CHECK(it_stride >= 0, "CONVEX: iteration stride");
   } else {
     TORCH_CHECK(false, "conv: unknown epilogue ", epi);
   }
-  TORCH_CHECK(cfg >= 0 && cfg <= 34 && !(cfg >= 29 && cfg <= 32), "conv: unknown tile config ", cfg);
+  TORCH_CHECK(cfg >= 0 && cfg <= 41 && !(cfg >= 29 && cfg <= 32), "conv: unknown tile config ", cfg);
   if (tx) conv_train_extras(p, epi, *tx, *ix, keep);
   if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3, bmap}) if (v.defined()) keep->push_back(v);
   if (epi == EPI_CONVEX) {

@@ -25,7 +25,7 @@ _load_error: Optional[BaseException] = None
 ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, ACT_SPLIT_TANH_RELU = 0, 1, 2, 3, 4
 EPI_STD, EPI_GRU_A, EPI_GRU_B, EPI_FLOW, EPI_CONVEX = 0, 1, 2, 3, 4
 # tile configs whose lanes hold < 16 contiguous output channels (no EPI_CONVEX)
-NARROW_CFGS = (3, 5, 19, 21)
+NARROW_CFGS = (3, 5, 19, 21, 36)
 # tile configs of conv_igemm.hip: (BCO, BP)
 CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (16, 256), 4: (64, 64), 5: (16, 64)}
 # configs 6..11: LDS-DMA kernel D2 (csrc/kernels/conv_igemm.hip)
@@ -42,10 +42,14 @@ CFG_TILES.update({21: (128, 128), 22: (256, 128), 23: (128, 64), 24: (64, 128)})
 CFG_TILES.update({25: (256, 128), 26: (128, 256), 27: (128, 128), 28: (64, 256)})
 # configs 33/34: kernel P (register double-buffered fragments), 8 / 16 waves
 CFG_TILES.update({33: (128, 128), 34: (256, 128)})
+# configs 35..41: kernel D2 (LDS-DMA ring) at 8 / 16 waves with the FAST loader
+CFG_TILES.update({35: (256, 128), 36: (128, 128), 37: (128, 128), 38: (256, 128), 39: (256, 128), 40: (128, 256),
+                  41: (64, 128)})
 # Autotune candidates: configs that win at least one RAFT conv on MI355X
 # (tools/microbench.py, profiles/r1_microbench_conv_cfgs.txt); the others stay
 # compiled and tested but are not timed at plan build.
-TUNE_CFGS = (0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34)
+TUNE_CFGS = (0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34,
+             35, 36, 37, 38, 39, 40, 41)
 NUM_CUS = 256
 
 

@@ -69,7 +69,8 @@ def test_conv_matches_reference(case, cfg):
     assert err < 2e-3, err
 
 
-@pytest.mark.parametrize("cfg", [0, 4, 6, 7, 9, 10, 11, 12, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34])
+@pytest.mark.parametrize("cfg", [0, 4, 6, 7, 9, 10, 11, 12, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34,
+                                 35, 36, 37, 38, 39, 40, 41])
 def test_conv_epilogues(cfg):
     """relu / residual (pre and post) / alpha / bf16 output / channel offsets."""
     nat = _nat()
@@ -109,7 +110,8 @@ def _gru_ref(h, x, kz, bz, kr, br, kq, bq, pad):
     return (1 - z) * h + z * q
 
 
-@pytest.mark.parametrize("cfg", [None, 0, 6, 8, 9, 10, 11, 12, 13, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34])
+@pytest.mark.parametrize("cfg", [None, 0, 6, 8, 9, 10, 11, 12, 13, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34,
+                                 35, 36, 37, 38, 39, 40, 41])
 @pytest.mark.parametrize("hidden,xin,ks,pad", [(128, 256, (1, 5), (0, 2)), (128, 256, (5, 1), (2, 0)),
                                                (96, 146, (3, 3), (1, 1))])
 def test_gru_fused_epilogues(hidden, xin, ks, pad, cfg):
@@ -315,7 +317,8 @@ def test_flow_head_fused(cin):
     assert (hx[:, :16] == 0).all() and (hx[:, 18:] == 0).all()
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34,
+                                 35, 36, 37, 38, 39, 40, 41])
 def test_conv_bias_map(cfg):
     """Per-pixel fp32 bias map (the folded context share of the GRU gates):
     conv(x) + bias + bmap[:, coff:coff+cout] before the activation."""

@@ -63,6 +63,10 @@ def main():
         ("gru.a(1x5)", 256, 256, 256, 1, 5, (0, 2)),
         ("gru.b(1x5)", 256, 256, 128, 1, 5, (0, 2)),
         ("gru.a(5x1)", 256, 256, 256, 5, 1, (2, 0)),
+        ("conv1x5.nobmap", 256, 256, 256, 1, 5, (0, 2)),   # gru.a without the bias-map epilogue read
+        # fixed-cost probes: one / four 64-deep K stages at the loop's M and N = 256
+        ("probe.k64", 64, 64, 256, 1, 1, (0, 0)),
+        ("probe.k256", 256, 256, 256, 1, 1, (0, 0)),
         ("fh1+mask1", 128, 128, 512, 3, 3, (1, 1)),
         ("fh2", 256, 256, 2, 3, 3, (1, 1)),
         ("mask2", 256, 256, 576, 1, 1, (0, 0)),
