@@ -12,6 +12,8 @@ extern "C" int jr_conv_family_g(const ConvParams* p, int cfg, int epi, hipStream
     case 39: return launch_cfg<256, 128, 2, 13>(p, epi, stream);   // 8 waves, 128x32
     case 40: return launch_cfg<128, 256, 2, 12>(p, epi, stream);   // 16 waves, 64x32
     case 41: return launch_cfg<64, 128, 1, 13>(p, epi, stream);    // 8 waves, 64x16
+    case 42: return launch_cfg<256, 128, 4, 13>(p, epi, stream);   // 8 waves, 64x64
+    case 43: return launch_cfg<256, 128, 2, 4>(p, epi, stream);    // 4 waves, 128x64 (one wave per SIMD)
     default: return -1;
   }
 }

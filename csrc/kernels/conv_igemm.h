@@ -404,6 +404,74 @@ JR_DEVICE void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM][TN], int mbas
   });
 }
 
+// EPI_TAPS epilogue (FlowHead conv1 -> the 18 taps of conv2, model.py:347-350):
+// the block holds all 256 channels of its 128 pixels (one N tile, 16 waves of
+// 64 x 32).  Lane (li, lq) of wave (wco, wp) owns channels wco*64 + 16 lq + (0..15)
+// of pixels wp*32 + 16 tn + li; after bias + activation those 16 values ARE the
+// B fragments (k-steps s = 0, 1) of a second MFMA against the packed tap weights
+// (ops/native.py:pack_taps_epi, same k order), giving each wave the 32 (18 real)
+// tap partial sums of its 64 channels.  The four channel groups are summed through
+// LDS (the staging buffers, free after the K loop) and written as fp32 [M][y_cstride].
+JR_DEVICE void taps_epilogue(const ConvParams& p, f32x4 (&acc)[4][2], bf16* smem, int p0, int wco, int wp,
+                             int lane) {
+  const int li = lane & 15, lq = lane >> 4;
+  const int c0 = wco * 64 + 16 * lq;
+  float b[16];
+  load_f32<16>(p.bias + c0, b);
+  const u32x4* wt = (const u32x4*)p.tapw + wco * 4 * 64 + lane;
+  u32x4 a[2][2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) a[s][t] = wt[(s * 2 + t) * 64];
+  f32x4 d[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn) d[t][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 bf;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = acc[2 * s + (j >> 2)][tn][j & 3] + b[8 * s + j];
+        bf[j] = f2bf(apply_act(v, p.act, c0 + 8 * s + j, p.split));
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        d[t][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[s][t]), bf, d[t][tn], 0, 0, 0);
+    }
+  __syncthreads();  // every wave is done with the staging LDS
+  f32x4* red = (f32x4*)smem;  // [wp 4][wco 4][t 2][tn 2][lane 64]
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn) red[(((wp * 4 + wco) * 2 + t) * 2 + tn) * 64 + lane] = d[t][tn];
+  __syncthreads();
+  if (wco != 0) return;
+#pragma unroll
+  for (int tn = 0; tn < 2; ++tn) {
+    const int m = p0 + wp * 32 + tn * 16 + li;
+    f32x4 sum[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      sum[t] = red[(((wp * 4 + 0) * 2 + t) * 2 + tn) * 64 + lane];
+#pragma unroll
+      for (int g = 1; g < 4; ++g) {
+        const f32x4 v = red[(((wp * 4 + g) * 2 + t) * 2 + tn) * 64 + lane];
+        sum[t] += v;
+      }
+    }
+    if (m >= p.M) continue;
+    // lane (li, lq) holds taps o = 16 t + 4 lq + r of pixel m
+    float* yp = (float*)p.y + (long)m * p.y_cstride;
+    *(f32x4*)(yp + 4 * lq) = sum[0];
+    if (lq == 0) *(float2*)(yp + 16) = make_float2(sum[1][0], sum[1][1]);
+  }
+}
+
 // XCD-aware tile order.  MI355X dispatches workgroups round-robin over its 8
 // XCDs (private L2 each), so consecutive linear ids -- neighbouring pixel
 // tiles, which share the input rows of a 3x3 / 1x5 / 5x1 window -- land on
@@ -687,8 +755,13 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(const ConvParams p)
       mma(fa, fb);
       mma(ga, gb);
     }
-    const int wrow0 = co0 + wco * WTCO;
-    conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, wrow0, lq, li);
+    if constexpr (EPI == EPI_TAPS) {
+      static_assert(TM == 4 && TN == 2 && WCO == 4 && NW == 16, "EPI_TAPS tiling");
+      taps_epilogue(p, acc, smem, p0, wco, wp, lane);
+    } else {
+      const int wrow0 = co0 + wco * WTCO;
+      conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, wrow0, lq, li);
+    }
     return;
   }
 
@@ -714,8 +787,13 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(const ConvParams p)
   }
   if (nks & 1) compute(0);
 
-  const int wrow0 = co0 + wco * WTCO;
-  conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, wrow0, lq, li);
+  if constexpr (EPI == EPI_TAPS) {
+    static_assert(TM == 4 && TN == 2 && WCO == 4 && NW == 16, "EPI_TAPS tiling");
+    taps_epilogue(p, acc, smem, p0, wco, wp, lane);
+  } else {
+    const int wrow0 = co0 + wco * WTCO;
+    conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, wrow0, lq, li);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1136,8 +1214,13 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW >
   }
   wait_vmcnt<0>();
 
-  const int wrow0 = co0 + wco * WTCO;
-  conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, wrow0, lq, li);
+  if constexpr (EPI == EPI_TAPS) {
+    static_assert(TM == 4 && TN == 2 && WCO == 4 && NW == 16, "EPI_TAPS tiling");
+    taps_epilogue(p, acc, smem, p0, wco, wp, lane);
+  } else {
+    const int wrow0 = co0 + wco * WTCO;
+    conv_epilogue<TM, TN, EPI>(p, acc, p0 + wp * WTP, wrow0, lq, li);
+  }
 }
 
 template <int BCO, int BP, int WCO, int KIND>
@@ -1178,6 +1261,14 @@ int launch_cfg(const ConvParams* p, int epi, hipStream_t s) {
     case EPI_FLOW: JR_LAUNCH(EPI_FLOW) break;
     case EPI_CONVEX: JR_LAUNCH(EPI_CONVEX) break;
     case EPI_BWD: JR_LAUNCH(EPI_BWD) break;
+    case EPI_TAPS:
+      // one N tile of 256 channels, 16 waves of 64 x 32 (configs 22, 34, 35, 38)
+      if constexpr (BCO == 256 && BP == 128 && WCO == 4 && (KIND == 7 || KIND == 11 || KIND == 12 || KIND == 14)) {
+        if (p->cout != 256) return (int)hipErrorInvalidValue;
+        JR_LAUNCH(EPI_TAPS) break;
+      } else {
+        return (int)hipErrorInvalidValue;
+      }
     default: return (int)hipErrorInvalidValue;
   }
 #undef JR_LAUNCH

@@ -22,6 +22,8 @@ enum ConvEpi : int {
                   // fp32 upsampled flow written straight into y = out[B][8 OH][8 OW][2]
   EPI_BWD = 5,    // data-gradient conv of the training loop's backward (no bias): channels
                   // [0, hidden) -> seg[0], [hidden, cout) -> seg[1] (see BwdSeg)
+  EPI_TAPS = 6,   // FlowHead conv1 (256 channels, bias + act) -> its features never leave the CU:
+                  // times the 18 per-pixel taps of conv2 (tapw) on MFMA -> fp32 taps [M][y_cstride]
 };
 
 // One channel segment of the EPI_BWD epilogue.  Local channel lc = c - base.
@@ -95,6 +97,8 @@ struct ConvParams {
   BwdSeg seg[2];
   const void* gz; const void* gr; const void* gq; const float* ghp;
   void* gdq; void* gdzr;
+  // EPI_TAPS: conv2 tap weights as MFMA A fragments [64-channel group 4][k-step 2][row tile 2][lane 64][8] bf16
+  const void* tapw;
 };
 
 // cfg (co x px block tile): kernel R (register-staged, 16x16x32 MFMA) 0 = 128x128, 1 = 64x128,

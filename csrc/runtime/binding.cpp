@@ -63,7 +63,7 @@ static void check_f32(const at::Tensor& t, const char* name) {
 }
 
 // ----------------------------------------------------------------------- conv
-// t = [x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3, bmap]
+// t = [x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3, bmap(, tapw)]
 // i = [N, H, W, x_coff, cin8, KH, KW, SH, SW, PH, PW, cout, act, split,
 //      y_coff, y2_coff, res_coff, hidden, y3_coff, epi, cfg, res_post
 //      (, OH_override, OW_override, log2 dil_h, log2 dil_w (, bmap_coff))]
@@ -77,7 +77,7 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
               "conv: expected 22, 26, 27 or 28 ints");
   at::Tensor x = opt(t, 0), w = opt(t, 1), bias = opt(t, 2), y = opt(t, 3), y2 = opt(t, 4), res = opt(t, 5);
   at::Tensor h32 = opt(t, 6), zbuf = opt(t, 7), coords = opt(t, 8), flow32 = opt(t, 9), y3 = opt(t, 10);
-  at::Tensor bmap = opt(t, 11);
+  at::Tensor bmap = opt(t, 11), tapw;
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_f32(bias, "bias");
@@ -187,6 +187,18 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
     TORCH_CHECK(tx != nullptr, "EPI_BWD needs the training operands (conv_train)");
     TORCH_CHECK(!bmap.defined() && !res.defined(), "EPI_BWD: no bias map / residual");
     TORCH_CHECK(p.hidden >= 0 && p.hidden % 16 == 0 && p.hidden <= p.cout, "EPI_BWD: split must be a multiple of 16 <= cout");
+  } else if (epi == EPI_TAPS) {
+    tapw = opt(t, 12);
+    check_f32(y, "y (taps)");
+    check_bf16(tapw, "tapw");
+    TORCH_CHECK(tapw.numel() == 4 * 2 * 2 * 64 * 8 && reinterpret_cast<uintptr_t>(tapw.data_ptr()) % 16 == 0,
+                "TAPS: tap weights must be pack_taps_epi's [4][2][2][64][8] bf16");
+    TORCH_CHECK(p.cout == 256 && p.y_coff == 0 && p.y_cstride >= 18 && p.y_cstride % 4 == 0 && !bmap.defined() &&
+                    !res.defined() && reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
+                "TAPS: 256 channels in, fp32 taps [M][>=18] out, no bias map / residual");
+    TORCH_CHECK(cfg == 22 || cfg == 34 || cfg == 35 || cfg == 38, "TAPS: tile config ", cfg,
+                " is not a 256-channel 16-wave 64x32 tiling");
+    p.tapw = tapw.data_ptr();
   } else if (epi == EPI_CONVEX) {
     check_f32(flow32, "flow32");
     TORCH_CHECK(flow32.numel() >= (int64_t)p.M * 2, "CONVEX: flow32 must be [M][2]");
@@ -199,9 +211,9 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   } else {
     TORCH_CHECK(false, "conv: unknown epilogue ", epi);
   }
-  TORCH_CHECK(cfg >= 0 && cfg <= 41 && !(cfg >= 29 && cfg <= 32), "conv: unknown tile config ", cfg);
+  TORCH_CHECK(cfg >= 0 && cfg <= 43 && !(cfg >= 29 && cfg <= 32), "conv: unknown tile config ", cfg);
   if (tx) conv_train_extras(p, epi, *tx, *ix, keep);
-  if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3, bmap}) if (v.defined()) keep->push_back(v);
+  if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3, bmap, tapw}) if (v.defined()) keep->push_back(v);
   if (epi == EPI_CONVEX) {
     const int64_t need = (int64_t)p.N * 64 * p.OH * p.OW * 2;
     return [p, epi, cfg, it_stride, out_cap, need](hipStream_t s, int it) {

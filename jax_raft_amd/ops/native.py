@@ -24,6 +24,9 @@ _load_error: Optional[BaseException] = None
 # activation / epilogue codes (csrc/kernels/common.h, kernels.h)
 ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, ACT_SPLIT_TANH_RELU = 0, 1, 2, 3, 4
 EPI_STD, EPI_GRU_A, EPI_GRU_B, EPI_FLOW, EPI_CONVEX = 0, 1, 2, 3, 4
+EPI_TAPS = 6
+# tile configs with the EPI_TAPS epilogue (256 channels in one N tile, 16 waves of 64 x 32)
+TAPS_CFGS = (34, 22, 35, 38)
 # tile configs whose lanes hold < 16 contiguous output channels (no EPI_CONVEX)
 NARROW_CFGS = (3, 5, 19, 21, 36)
 # tile configs of conv_igemm.hip: (BCO, BP)
@@ -44,12 +47,14 @@ CFG_TILES.update({25: (256, 128), 26: (128, 256), 27: (128, 128), 28: (64, 256)}
 CFG_TILES.update({33: (128, 128), 34: (256, 128)})
 # configs 35..41: kernel D2 (LDS-DMA ring) at 8 / 16 waves with the FAST loader
 CFG_TILES.update({35: (256, 128), 36: (128, 128), 37: (128, 128), 38: (256, 128), 39: (256, 128), 40: (128, 256),
-                  41: (64, 128)})
+                  41: (64, 128), 42: (256, 128), 43: (256, 128)})
 # Autotune candidates: configs that win at least one RAFT conv on MI355X
 # (tools/microbench.py, profiles/r1_microbench_conv_cfgs.txt); the others stay
 # compiled and tested but are not timed at plan build.
+# Of the D2 configs 35..43 only the 16-wave 64x32 ones (35, 38) come within a few
+# percent of kernel P on a loop conv (profiles/r2_conv_d2_microbench.txt).
 TUNE_CFGS = (0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34,
-             35, 36, 37, 38, 39, 40, 41)
+             35, 38)
 NUM_CUS = 256
 
 
@@ -213,7 +218,7 @@ def conv_args(spec: ConvSpec, x: torch.Tensor, N: int, H: int, W: int, y: torch.
               y_coff: int = 0, act: int = ACT_NONE, split: int = 0, alpha: float = 1.0, y2=None, y2_coff: int = 0,
               res=None, res_coff: int = 0, res_post: int = 0, h32=None, zbuf=None, hidden: int = 0, coords=None,
               flow32=None, y3=None, y3_coff: int = 0, epi: int = EPI_STD, cfg: Optional[int] = None,
-              bmap=None, bmap_coff: int = 0, it_stride: int = 0):
+              bmap=None, bmap_coff: int = 0, it_stride: int = 0, tapw=None):
     """Build the (tensors, ints, alpha) argument triple of the ``conv`` op.
     ``bmap``: optional fp32 per-pixel bias map [M, C], channels from ``bmap_coff``.
     ``it_stride``: (EPI_CONVEX) output floats between loop iterations of a plan."""
@@ -221,6 +226,8 @@ def conv_args(spec: ConvSpec, x: torch.Tensor, N: int, H: int, W: int, y: torch.
     if cfg is None:
         cfg = pick_cfg(N * OH * OW, spec.cout)
     t = [x, spec.w, spec.b, y, y2, res, h32, zbuf, coords, flow32, y3, bmap]
+    if tapw is not None:
+        t.append(tapw)
     i = [N, H, W, x_coff, spec.cin8, spec.kh, spec.kw, spec.sh, spec.sw, spec.ph, spec.pw, spec.cout, act, split,
          y_coff, y2_coff, res_coff, hidden, y3_coff, epi, cfg, res_post]
     if bmap is not None or it_stride:
@@ -255,6 +262,27 @@ def pack_convex_head(kernel: torch.Tensor, bias: torch.Tensor) -> Tuple[torch.Te
     wc = kernel.detach().float().reshape(8, 4, 8, 9, 4, 16)      # (ks, q, j, k, w, r)
     wp = wc.permute(0, 3, 4, 1, 5, 2).contiguous().to(torch.bfloat16)
     return wp.reshape(-1), bias.detach().float().contiguous()
+
+
+def pack_taps_epi(kernel: torch.Tensor) -> torch.Tensor:
+    """FlowHead conv2 (3, 3, 256, 2) -> the A fragments of the EPI_TAPS conv
+    epilogue (csrc/kernels/conv_igemm.h:taps_epilogue): [group 4][kstep 2][tile 2][lane 64][8]
+    bf16 with lane = 16 q + r holding Wt[o = 16 tile + r][c = 64 group + 16 q + 8 kstep + j],
+    Wt[o = 2 tap + comp][c] = W[tap // 3, tap % 3, c, comp] (rows 18..31 zero) -- the k
+    order of the 16 contiguous channels each conv1 epilogue lane owns."""
+    kh, kw, cin, co = kernel.shape
+    assert (kh, kw, cin, co) == (3, 3, 256, 2), kernel.shape
+    dev = kernel.device
+    wt = torch.zeros(32, 256, dtype=torch.float32, device=dev)
+    wt[:18] = kernel.detach().float().reshape(9, cin, 2).permute(0, 2, 1).reshape(18, cin)
+    g = torch.arange(4, device=dev).view(4, 1, 1, 1, 1)
+    s = torch.arange(2, device=dev).view(1, 2, 1, 1, 1)
+    t = torch.arange(2, device=dev).view(1, 1, 2, 1, 1)
+    lane = torch.arange(64, device=dev).view(1, 1, 1, 64, 1)
+    j = torch.arange(8, device=dev).view(1, 1, 1, 1, 8)
+    o = 16 * t + lane % 16
+    c = 64 * g + 16 * (lane // 16) + 8 * s + j
+    return wt[o.expand(4, 2, 2, 64, 8), c.expand(4, 2, 2, 64, 8)].to(torch.bfloat16).contiguous()
 
 
 CONV1X1_KPADS = (128, 256, 352, 384)

@@ -53,6 +53,7 @@ from ..ops.native import (
     EPI_GRU_A,
     EPI_GRU_B,
     EPI_STD,
+    EPI_TAPS,
     ConvSpec,
     conv_args,
     round_up,
@@ -68,7 +69,7 @@ def _tune(spec: ConvSpec, x, N, H, W, y, kw, reps: int = 5) -> int:
     """Time every tile config of one conv problem; return the fastest."""
     ops = nat.ops()
     best, best_t = None, None
-    for cfg in nat.TUNE_CFGS:
+    for cfg in (nat.TAPS_CFGS if kw.get("epi") == nat.EPI_TAPS else nat.TUNE_CFGS):
         if kw.get("epi") == nat.EPI_CONVEX and cfg in nat.NARROW_CFGS:
             continue
         args = conv_args(spec, x, N, H, W, y, **dict(kw, cfg=cfg))
@@ -221,8 +222,9 @@ class RaftEngine:
                  split: int = 1, flow_head: str = "taps", double_buffer: bool = False,
                  fused_flow_head: bool = False, gate_dtype: torch.dtype = torch.bfloat16,
                  flow_lane: str = "mask", direct_flow: bool = True, mask_head: str = "split",
-                 convex: str = "head"):
+                 convex: str = "head", taps_epi: bool = True):
         nat.require()
+        self.taps_epi = taps_epi
         assert convex in ("fused", "separate", "head"), convex
         self.convex = convex
         assert mask_head in ("split", "fused"), mask_head
@@ -244,6 +246,7 @@ class RaftEngine:
         self._fh2_w = self._fh2_b = None
         self._convex_w = self._convex_b = None
         self._taps_w = None
+        self._taps_epi_w = None
         self._cc1_w = self._cc1_b = None
         self.model = model
         self.device = torch.device(device)
@@ -339,6 +342,12 @@ class RaftEngine:
                 self._taps_w = wt
             else:
                 self._taps_w.copy_(wt)
+        if tuple(fh2.kernel.shape) == (3, 3, 256, 2):
+            wt = nat.pack_taps_epi(fh2.kernel.to(self.device))
+            if self._taps_epi_w is None:
+                self._taps_epi_w = wt
+            else:
+                self._taps_epi_w.copy_(wt)
         mp = self.model.mask_predictor
         if mp is not None and tuple(mp.conv.kernel.shape) == (1, 1, 256, 576):
             wc, bc = nat.pack_convex_head(mp.conv.kernel.to(self.device), mp.conv.bias.to(self.device))
@@ -446,6 +455,8 @@ class RaftEngine:
     # ------------------------------------------------------------- autotune
     def _conv(self, plan, spec: ConvSpec, x, N, H, W, y, **kw):
         """Append one conv to ``plan``, choosing its tile config (autotuned)."""
+        if kw.get("epi") == EPI_TAPS and not self.autotune and kw.get("cfg") is None:
+            kw = dict(kw, cfg=nat.TAPS_CFGS[0])
         if self.autotune and kw.get("cfg") is None:
             OH, OW = spec.out_hw(H, W)
             key = (N * OH * OW, spec.cout, spec.kh, spec.kw, spec.sh, spec.sw, spec.cin8, x.shape[-1],
@@ -720,11 +731,21 @@ class RaftEngine:
         stride = st.out.shape[1] * H * W * 2  # one iteration of the full-batch output
         taps = alloc("fh2.taps", (M, 24), F32) if self.flow_head == "taps" else None
 
+        # FlowHead conv1 with the taps epilogue: its 256 features never leave the CU
+        # (the mask head reads h, not them, when it is split onto the mask lane)
+        taps_epi = (self.taps_epi and self.flow_head == "taps" and self._taps_epi_w is not None and s1.cout == 256
+                    and (split_mask or not self.has_mask or not all_iters))
+
         def flow_head(fm, f32, before_update=None):
-            self._conv(plan, s1, hx, B, h, w, fm, act=ACT_RELU)
+            if taps_epi:
+                self._conv(plan, s1, hx, B, h, w, taps, act=ACT_RELU, epi=EPI_TAPS, tapw=self._taps_epi_w)
+            else:
+                self._conv(plan, s1, hx, B, h, w, fm, act=ACT_RELU)
             # flow head conv2 + coordinate update (model.py:505) + flow into hx/qx/flow8
             if self.flow_head == "taps":
-                if self._taps_w is not None:   # skinny GEMM kernel (flowhead.hip), N = 18
+                if taps_epi:
+                    pass
+                elif self._taps_w is not None:   # skinny GEMM kernel (flowhead.hip), N = 18
                     plan.add_taps_gemm([fm, self._taps_w, taps], [M, self.fh_hidden, 0])
                 else:
                     self._conv(plan, sp["fh2.taps"], fm, B, h, w, taps)

@@ -70,7 +70,7 @@ def test_conv_matches_reference(case, cfg):
 
 
 @pytest.mark.parametrize("cfg", [0, 4, 6, 7, 9, 10, 11, 12, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34,
-                                 35, 36, 37, 38, 39, 40, 41])
+                                 35, 36, 37, 38, 39, 40, 41, 42, 43])
 def test_conv_epilogues(cfg):
     """relu / residual (pre and post) / alpha / bf16 output / channel offsets."""
     nat = _nat()
@@ -111,7 +111,7 @@ def _gru_ref(h, x, kz, bz, kr, br, kq, bq, pad):
 
 
 @pytest.mark.parametrize("cfg", [None, 0, 6, 8, 9, 10, 11, 12, 13, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34,
-                                 35, 36, 37, 38, 39, 40, 41])
+                                 35, 36, 37, 38, 39, 40, 41, 42, 43])
 @pytest.mark.parametrize("hidden,xin,ks,pad", [(128, 256, (1, 5), (0, 2)), (128, 256, (5, 1), (2, 0)),
                                                (96, 146, (3, 3), (1, 1))])
 def test_gru_fused_epilogues(hidden, xin, ks, pad, cfg):
@@ -318,7 +318,7 @@ def test_flow_head_fused(cin):
 
 
 @pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34,
-                                 35, 36, 37, 38, 39, 40, 41])
+                                 35, 36, 37, 38, 39, 40, 41, 42, 43])
 def test_conv_bias_map(cfg):
     """Per-pixel fp32 bias map (the folded context share of the GRU gates):
     conv(x) + bias + bmap[:, coff:coff+cout] before the activation."""
@@ -557,3 +557,31 @@ def test_conv1x1_lds_matches_fp32(K, cs, kpad, N, M):
     y = nat.conv1x1(x.to(DEV), wpk.to(DEV), bias.to(DEV), cs, kpad, N, act=nat.ACT_RELU).float().cpu()
     ref = torch.relu(x[:, :K].float() @ kern.reshape(K, N).to(torch.bfloat16).float() + bias)
     assert (y - ref).abs().max().item() < 1e-2 * ref.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("cfg", [34, 22, 35, 38])
+def test_conv_taps_epilogue(cfg):
+    """EPI_TAPS: FlowHead conv1 (3x3, 128 -> 256, relu) whose epilogue multiplies
+    its features by the 18 taps of conv2 (MFMA) -> fp32 taps [M][24]; against
+    fp32 torch of relu(conv1) . Wt (features rounded to bf16 as the kernel feeds them)."""
+    nat = _nat()
+    torch.manual_seed(11)
+    N, H, W, cin = 2, 11, 37, 128
+    M = N * H * W
+    x = torch.randn(N, H, W, cin)
+    k1 = torch.randn(3, 3, cin, 256) / math.sqrt(9 * cin)
+    b1 = torch.randn(256) * 0.1
+    k2 = torch.randn(3, 3, 256, 2) * 0.05
+    fm = torch.relu(R.conv2d_nhwc(_bf(x), _bf(k1), b1, (1, 1), (1, 1))).reshape(M, 256)
+    wt = k2.reshape(9, 256, 2).permute(1, 0, 2).reshape(256, 18)
+    ref = _bf(fm) @ _bf(wt)
+    spec = nat.make_spec(k1, b1, (1, 1), (1, 1), device=DEV)
+    xg = x.to(DEV, torch.bfloat16).contiguous()
+    taps = torch.full((M, 24), 7.0, device=DEV)
+    t, i, a = nat.conv_args(spec, xg, N, H, W, taps, act=nat.ACT_RELU, epi=nat.EPI_TAPS, cfg=cfg,
+                            tapw=nat.pack_taps_epi(k2.to(DEV)))
+    nat.ops().conv(t, i, a)
+    torch.cuda.synchronize()
+    out = taps.cpu()
+    assert _rel(out[:, :18], ref) < 5e-3
+    assert (out[:, 18:] == 7.0).all()

@@ -52,3 +52,16 @@ def test_pack_convex_head_decodes_to_weights():
         r, kk = _frag(lane, j)
         assert pk[ks, k, g, lane, j].item() == wb[32 * ks + kk, 64 * k + 16 * g + r].item()
     assert torch.equal(bias, b)
+
+
+def test_pack_taps_epi_decodes_to_weights():
+    w = torch.randn(3, 3, 256, 2)
+    pk = nat.pack_taps_epi(w).float()              # [group 4][kstep 2][tile 2][lane 64][8]
+    wt = w.reshape(9, 256, 2).permute(0, 2, 1).reshape(18, 256).to(torch.bfloat16).float()
+    for g, s, t, lane, j in [(0, 0, 0, 0, 0), (3, 1, 0, 63, 7), (2, 0, 1, 16, 3), (1, 1, 1, 1, 5), (0, 1, 0, 47, 2)]:
+        o = 16 * t + (lane & 15)
+        c = 64 * g + 16 * (lane >> 4) + 8 * s + j
+        want = wt[o, c].item() if o < 18 else 0.0
+        assert pk[g, s, t, lane, j].item() == want
+    # every (o < 18, c) weight appears exactly once
+    assert torch.allclose(pk.sum(), wt.sum(), rtol=1e-3, atol=1e-2)
