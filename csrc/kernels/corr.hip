@@ -320,13 +320,67 @@ JR_DEVICE int lv_off(const LvGeom& g, int l, int wl, int y, int x) {  // y, x >=
   return y * wl + x;
 }
 
+// Query coordinates of a lookup wave (QPW queries q0 ..), with the optional
+// fused flow update (TapsUpd): lane 18 k + 2 t + c loads tap t, component c of
+// query k's 3x3 neighbour (zero outside the image); lanes 18 k + c sum bias[c]
+// and the nine taps in jr_flow_taps' order, store the new coords / flow, and
+// every lane receives the new coords by shuffle.  All lanes take part.
+template <int QPW>
+JR_DEVICE void lookup_coords(const TapsUpd& u, const float* coords, int q0, int total, int h, int w, int lane,
+                             float (&cx)[QPW], float (&cy)[QPW]) {
+  static_assert(QPW * 18 <= 64, "QPW");
+  if (!u.on) {
+#pragma unroll
+    for (int k = 0; k < QPW; ++k) {
+      const int q = q0 + k;
+      cx[k] = q < total ? coords[2 * (long)q] : 0.f;
+      cy[k] = q < total ? coords[2 * (long)q + 1] : 0.f;
+    }
+    return;
+  }
+  const int uq = lane / 18, k = lane - uq * 18;
+  const int tap = k >> 1, c = k & 1;
+  const long q = (long)q0 + uq;
+  const bool own = uq < QPW && q < total;
+  const int hw = h * w;
+  int y = 0, x = 0;
+  float val = 0.f;
+  if (own) {
+    const int rem = (int)(q % hw);
+    y = rem / w;
+    x = rem - y * w;
+    const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+    if ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w)
+      val = u.taps[(q - rem + (long)yy * w + xx) * u.tcs + k];
+  }
+  float d = u.bias[c];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) d += __shfl(val, min(uq * 18 + 2 * t + c, 63));
+  float cn = 0.f;
+  if (own && k < 2) {
+    cn = coords[2 * q + k] + d;
+    u.coords[2 * q + k] = cn;
+    const float f = cn - (float)(k == 0 ? x : y);
+    u.flow32[2 * q + k] = f;
+    const bf16 fb = f2bf(f);
+    ((bf16*)u.hx)[q * u.hx_cs + u.hx_off + k] = fb;
+    if (u.qx) ((bf16*)u.qx)[q * u.qx_cs + u.qx_off + k] = fb;
+    if (u.f8) ((bf16*)u.f8)[q * u.f8_cs + k] = fb;
+  }
+#pragma unroll
+  for (int kk = 0; kk < QPW; ++kk) {
+    cx[kk] = __shfl(cn, kk * 18);
+    cy[kk] = __shfl(cn, kk * 18 + 1);
+  }
+}
+
 // blockDim = 256: 4 waves x QPW queries each; lane = level*16 + window column i.
 // General-shape path (any level size); see corr_lookup_wide_kernel below for
 // the fast path.
 template <int R, typename T, int QPW>
 __global__ __launch_bounds__(256) void corr_lookup_kernel(LevelPtrs lv, int nlev, int total, int h, int w,
-                                                          const float* __restrict__ coords, bf16* __restrict__ out,
-                                                          int ocs, LvGeom geo) {
+                                                          const float* coords, bf16* __restrict__ out,
+                                                          int ocs, LvGeom geo, TapsUpd upd) {
   constexpr int S = 2 * R + 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -338,6 +392,8 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LevelPtrs lv, int nlev
   const bool on = lvl < nlev && i <= S;
   const float sc = 1.0f / (float)(1 << lvl);
   const int hl = h >> lvl, wl = w >> lvl;
+  float qcx[QPW], qcy[QPW];
+  lookup_coords<QPW>(upd, coords, q0, total, h, w, lane, qcx, qcy);
   float fx[QPW], fy[QPW], colv[QPW][S + 1];
 #pragma unroll
   for (int u = 0; u < QPW; ++u) {
@@ -346,7 +402,7 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LevelPtrs lv, int nlev
 #pragma unroll
     for (int j = 0; j <= S; ++j) colv[u][j] = 0.f;
     if (q < total && on) {
-      const float cx = coords[2 * (long)q] * sc, cy = coords[2 * (long)q + 1] * sc;
+      const float cx = qcx[u] * sc, cy = qcy[u] * sc;
       const float flx = floorf(cx), fly = floorf(cy);
       fx[u] = cx - flx;
       fy[u] = cy - fly;
@@ -400,8 +456,9 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LevelPtrs lv, int nlev
 // wholly outside a row (row length % EPC == 0), so zero padding stays exact.
 template <int R, typename T, int QPW>
 __global__ __launch_bounds__(256) void corr_lookup_wide_kernel(LevelPtrs lv, int nlev, int total, int h, int w,
-                                                               const float* __restrict__ coords,
-                                                               bf16* __restrict__ out, int ocs, LvGeom geo) {
+                                                               const float* coords,
+                                                               bf16* __restrict__ out, int ocs, LvGeom geo,
+                                                               TapsUpd upd) {
   constexpr int S = 2 * R + 1;
   constexpr int EPC = 16 / sizeof(T);                   // elements per chunk
   constexpr int NCH = (S + 1 + EPC - 1) / EPC + 1;      // chunks per window row
@@ -413,6 +470,8 @@ __global__ __launch_bounds__(256) void corr_lookup_wide_kernel(LevelPtrs lv, int
   T* win = (T*)dyn_smem + (long)wave * NT * EPC;                       // [QPW][4][S+1][RW]
   bf16* st = (bf16*)(dyn_smem + 4L * NT * 16) + wave * QPW * ocs;     // [QPW][ocs]
   for (int c = lane; c < QPW * ocs; c += 64) st[c] = f2bf(0.f);
+  float qcx[QPW], qcy[QPW];
+  lookup_coords<QPW>(upd, coords, q0, total, h, w, lane, qcx, qcy);
   u32x4 v[(NT + 63) / 64];
 #pragma unroll
   for (int n = 0; n < (NT + 63) / 64; ++n) {
@@ -420,11 +479,15 @@ __global__ __launch_bounds__(256) void corr_lookup_wide_kernel(LevelPtrs lv, int
     v[n] = u32x4{0u, 0u, 0u, 0u};
     const int k = t % NCH, j = (t / NCH) % (S + 1), l = (t / (NCH * (S + 1))) % 4, u = t / (NCH * (S + 1) * 4);
     const int q = q0 + u;
+    float ucx = qcx[0], ucy = qcy[0];
+#pragma unroll
+    for (int kk = 1; kk < QPW; ++kk)
+      if (u == kk) { ucx = qcx[kk]; ucy = qcy[kk]; }
     if (t < NT && q < total && l < nlev) {
       const float sc = 1.0f / (float)(1 << l);
       const int hl = h >> l, wl = w >> l;
-      const int col0 = (int)floorf(coords[2 * (long)q] * sc) - R;
-      const int rr = (int)floorf(coords[2 * (long)q + 1] * sc) - R + j;
+      const int col0 = (int)floorf(ucx * sc) - R;
+      const int rr = (int)floorf(ucy * sc) - R + j;
       const int cc = (col0 >= 0 ? col0 / EPC : -((-col0 + EPC - 1) / EPC)) * EPC + k * EPC;
       if ((unsigned)rr < (unsigned)hl && (unsigned)cc < (unsigned)wl)
         v[n] = *(const u32x4*)((const T*)lv.p[l] + (long)q * lv_qstride(geo, l, hl, wl) + lv_off(geo, l, wl, rr, cc));
@@ -443,7 +506,7 @@ __global__ __launch_bounds__(256) void corr_lookup_wide_kernel(LevelPtrs lv, int
     for (int u = 0; u < QPW; ++u) {
       const int q = q0 + u;
       if (q >= total) break;
-      const float cx = coords[2 * (long)q] * sc, cy = coords[2 * (long)q + 1] * sc;
+      const float cx = qcx[u] * sc, cy = qcy[u] * sc;
       const float flx = floorf(cx), fly = floorf(cy);
       const float fx = cx - flx, fy = cy - fly;
       const int col0 = (int)flx - R;
@@ -545,7 +608,7 @@ bool lookup_wide_ok(const LevelPtrs& lv, int L, int h, int w, const LvGeom& geo)
 
 template <typename T>
 int launch_lookup(const LevelPtrs& lv, int L, int total, int h, int w, int r, const float* coords, bf16* out, int ocs,
-                  const LvGeom& geo, hipStream_t stream) {
+                  const LvGeom& geo, const TapsUpd& upd, hipStream_t stream) {
   if (r <= 4 && lookup_wide_ok<T>(lv, L, h, w, geo)) {
     constexpr int QPW = 2;
     constexpr int EPC = 16 / sizeof(T);
@@ -556,7 +619,7 @@ int launch_lookup(const LevelPtrs& lv, int L, int total, int h, int w, int r, co
     constexpr int NT = QPW * 4 * (2 * RR + 2) * ((2 * RR + 2 + EPC - 1) / EPC + 1);                                 \
     const size_t smem = 4 * NT * 16 + 4 * QPW * ocs * sizeof(bf16);                                                 \
     hipLaunchKernelGGL((corr_lookup_wide_kernel<RR, T, QPW>), grid, dim3(256), smem, stream, lv, L, total, h, w,    \
-                       coords, out, ocs, geo);                                                                       \
+                       coords, out, ocs, geo, upd);                                                                  \
     break;                                                                                                          \
   }
       JR_LKW(1) JR_LKW(2) JR_LKW(3) JR_LKW(4)
@@ -568,7 +631,7 @@ int launch_lookup(const LevelPtrs& lv, int L, int total, int h, int w, int r, co
   dim3 grid((total + 4 * QPW - 1) / (4 * QPW));
   const size_t smem = 4 * QPW * ocs * sizeof(bf16);
   switch (r) {
-#define JR_LK(RR) case RR: hipLaunchKernelGGL((corr_lookup_kernel<RR, T, QPW>), grid, dim3(256), smem, stream, lv, L, total, h, w, coords, out, ocs, geo); break;
+#define JR_LK(RR) case RR: hipLaunchKernelGGL((corr_lookup_kernel<RR, T, QPW>), grid, dim3(256), smem, stream, lv, L, total, h, w, coords, out, ocs, geo, upd); break;
     JR_LK(1) JR_LK(2) JR_LK(3) JR_LK(4) JR_LK(5) JR_LK(6)
 #undef JR_LK
     default: return (int)hipErrorInvalidValue;
@@ -606,17 +669,23 @@ extern "C" int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int
 // unless the queries are a slab of rows, cp.py).
 extern "C" int jr_corr_lookup(const void* const* levels, int num_levels, int B, int h, int w, int nq, int radius,
                               const float* coords, void* out, int out_cstride, int lv_bf16, int blocked,
-                              hipStream_t stream) {
+                              hipStream_t stream, const TapsUpd* upd) {
   const int S = 2 * radius + 1;
   if (num_levels > 4 || radius < 1 || radius > 6 || out_cstride % 8 != 0 || out_cstride < num_levels * S * S)
     return (int)hipErrorInvalidValue;
+  TapsUpd u{};
+  if (upd && upd->on) {
+    if (nq != h * w || !upd->taps || upd->tcs < 18 || !upd->bias || upd->coords != coords || !upd->flow32 || !upd->hx)
+      return (int)hipErrorInvalidValue;
+    u = *upd;
+  }
   LevelPtrs lv;
   for (int l = 0; l < 4; ++l) lv.p[l] = l < num_levels ? levels[l] : nullptr;
   const int total = B * nq;
   const LvGeom geo{blocked, (h + TY - 1) / TY, (w + TX - 1) / TX};
   if (lv_bf16)
-    return launch_lookup<bf16>(lv, num_levels, total, h, w, radius, coords, (bf16*)out, out_cstride, geo, stream);
-  return launch_lookup<float>(lv, num_levels, total, h, w, radius, coords, (bf16*)out, out_cstride, geo, stream);
+    return launch_lookup<bf16>(lv, num_levels, total, h, w, radius, coords, (bf16*)out, out_cstride, geo, u, stream);
+  return launch_lookup<float>(lv, num_levels, total, h, w, radius, coords, (bf16*)out, out_cstride, geo, u, stream);
 }
 
 extern "C" int jr_corr_lookup_bwd(void* const* dlevels, int num_levels, int B, int h, int w, int nq, int radius,

@@ -136,8 +136,21 @@ int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int w, int nq,
                     int blocked, hipStream_t stream);
 // coords fp32 [B][nq][2]; out bf16 [B*nq][out_cstride] channels l*(2r+1)^2 + i*(2r+1) + j,
 // zero-filled up to out_cstride.  h, w: level-0 map size.  radius 1..6.
+// Optional flow update fused ahead of the lookup (upd != nullptr, upd->on): coords
+// += bias + the 3x3 sum of the FlowHead conv2 taps (jr_flow_taps' semantics, same
+// summation order), then the new flow is written as jr_flow_taps writes it and
+// the lookup samples around the updated coords.  Needs nq == h * w.
+struct TapsUpd {
+  const float* taps; int tcs; const float* bias;
+  float* coords; float* flow32;
+  void* hx; int hx_cs, hx_off;
+  void* qx; int qx_cs, qx_off;
+  void* f8; int f8_cs;
+  int on;
+};
 int jr_corr_lookup(const void* const* levels, int num_levels, int B, int h, int w, int nq, int radius,
-                   const float* coords, void* out, int out_cstride, int lv_bf16, int blocked, hipStream_t stream);
+                   const float* coords, void* out, int out_cstride, int lv_bf16, int blocked, hipStream_t stream,
+                   const TapsUpd* upd = nullptr);
 
 // Backward of jr_corr_lookup w.r.t. the levels: accumulates into fp32 dlevels
 // (same shapes as the levels).  gout: bf16 (g_bf16=1) or fp32 [B*nq][gcs].

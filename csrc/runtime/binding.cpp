@@ -675,7 +675,30 @@ static Launch make_lookup(const TList& t, const IList& i, std::vector<at::Tensor
   void* op = out.data_ptr();
   const int ocs = cs(out);
   const int lbf = dt == at::kBFloat16;
-  return [=](hipStream_t s, int) { return jr_corr_lookup(lv.data(), L, B, h, w, nq, r, cp, op, ocs, lbf, blocked, s); };
+  // optional fused flow update (t[6..11] = taps, bias, flow32, hx, qx?, flow8?; i[7..8] = hx_off, qx_off):
+  // applied in loop iterations > 0 (iteration i's lookup applies iteration i-1's FlowHead taps)
+  TapsUpd upd{};
+  at::Tensor tp = opt(t, 6);
+  if (tp.defined()) {
+    at::Tensor bias = opt(t, 7), f32 = opt(t, 8), hx = opt(t, 9), qx = opt(t, 10), f8 = opt(t, 11);
+    TORCH_CHECK(i.size() >= 9, "lookup: the fused flow update needs [.., hx_off, qx_off]");
+    check_f32(tp, "taps"); check_f32(bias, "bias"); check_f32(f32, "flow32"); check_bf16(hx, "hx");
+    const int64_t M = (int64_t)B * nq;
+    TORCH_CHECK(nq == h * w && cs(tp) >= 18 && tp.numel() >= M * cs(tp) && bias.numel() >= 2 && f32.numel() >= 2 * M,
+                "lookup: fused update needs whole maps, taps [M][>=18], bias [2], flow32 [M][2]");
+    const int hx_off = (int)i[7], qx_off = (int)i[8];
+    TORCH_CHECK(hx.numel() >= M * cs(hx) && hx_off + 2 <= cs(hx), "lookup: hx");
+    if (qx.defined()) { check_bf16(qx, "qx"); TORCH_CHECK(qx.numel() >= M * cs(qx) && qx_off + 2 <= cs(qx), "lookup: qx"); }
+    if (f8.defined()) { check_bf16(f8, "flow8"); TORCH_CHECK(f8.numel() >= M * cs(f8) && cs(f8) >= 2, "lookup: flow8"); }
+    upd = TapsUpd{tp.data_ptr<float>(), cs(tp), bias.data_ptr<float>(), coords.data_ptr<float>(), f32.data_ptr<float>(),
+                  hx.data_ptr(), cs(hx), hx_off, ptr(qx), cs(qx), qx_off, ptr(f8), cs(f8), 1};
+    if (keep) for (auto& v : {tp, bias, f32, hx, qx, f8}) if (v.defined()) keep->push_back(v);
+  }
+  return [=](hipStream_t s, int it) {
+    TapsUpd u = upd;
+    u.on = upd.on && it > 0;
+    return jr_corr_lookup(lv.data(), L, B, h, w, nq, r, cp, op, ocs, lbf, blocked, s, &u);
+  };
 }
 
 // ------------------------------------------------------------------ upsample
@@ -1070,7 +1093,18 @@ class Plan : public torch::CustomClassHolder {
     TORCH_CHECK(s >= 0 && s <= 2, "segment must be 0 (prologue), 1 (loop) or 2 (epilogue)");
     seg_ = (int)s;
     parity_ = -1;
+    defer_ = 0;
     reset_graph();
+  }
+  // Deferred ops (set_defer 1, loop body / epilogue): the work of the PREVIOUS
+  // iteration -- skipped in loop iteration 0 and called with iteration index
+  // it - 1; in the epilogue (called with n_iters) they finish the last
+  // iteration.  Used when iteration i's flow update is fused into iteration
+  // i+1's lookup, so iteration i's mask head / upsampling run one iteration later.
+  void set_defer(int64_t d) {
+    TORCH_CHECK(d == 0 || d == 1, "defer must be 0 or 1");
+    TORCH_CHECK(d == 0 || seg_ != 0, "deferred ops belong to the loop body or the epilogue");
+    defer_ = (int)d;
   }
   void set_parity(int64_t p) {
     TORCH_CHECK(p >= -1 && p <= 1, "parity must be -1 (every iteration), 0 (even) or 1 (odd)");
@@ -1213,14 +1247,15 @@ class Plan : public torch::CustomClassHolder {
     int ev;
     std::string name;
     int parity;  // -1: every iteration; 0 / 1: even / odd loop iterations only
+    int defer;   // 1: previous iteration's work (see set_defer)
   };
   void push(Launch l, const char* name) {
-    segs_[seg_].push_back(Op{std::move(l), lane_, OP_LAUNCH, -1, name, parity_});
+    segs_[seg_].push_back(Op{std::move(l), lane_, OP_LAUNCH, -1, name, parity_, defer_});
     reset_graph();
   }
   void push_sync(int kind, int64_t ev, const char* name) {
     TORCH_CHECK(ev >= 0 && ev < kMaxEvents, "event id out of range");
-    segs_[seg_].push_back(Op{Launch(), lane_, kind, (int)ev, std::string(name) + std::to_string(ev), parity_});
+    segs_[seg_].push_back(Op{Launch(), lane_, kind, (int)ev, std::string(name) + std::to_string(ev), parity_, defer_});
     reset_graph();
   }
   // JR_LANE_PRIORITY=0 disables the lane priorities (A/B measurements)
@@ -1254,6 +1289,10 @@ class Plan : public torch::CustomClassHolder {
   // also crashes hipStreamEndCapture on this ROCm).
   int exec_op(const Op& o, hipStream_t* st, int it, std::vector<char>& recorded) {
     if (o.parity >= 0 && (it & 1) != o.parity) return 0;
+    if (o.defer) {
+      if (it == 0) return 0;
+      --it;
+    }
     hipStream_t s = st[o.lane];
     if (debug_) fprintf(stderr, "[plan] it=%d lane=%d %s stream=%p\n", it, o.lane, o.name.c_str(), (void*)s);
     switch (o.kind) {
@@ -1324,6 +1363,7 @@ class Plan : public torch::CustomClassHolder {
   int seg_ = 0;
   int lane_ = 0;
   int parity_ = -1;
+  int defer_ = 0;
   int used_lanes_ = 1;
   std::vector<hipEvent_t> events_;
   hipEvent_t fork_ = nullptr;
@@ -1378,6 +1418,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("set_segment", &jr::Plan::set_segment)
       .def("set_lane", &jr::Plan::set_lane)
       .def("set_parity", &jr::Plan::set_parity)
+      .def("set_defer", &jr::Plan::set_defer)
       .def("add_record", &jr::Plan::add_record)
       .def("add_wait", &jr::Plan::add_wait)
       .def("num_lanes", &jr::Plan::num_lanes)

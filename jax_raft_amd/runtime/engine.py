@@ -222,9 +222,10 @@ class RaftEngine:
                  split: int = 1, flow_head: str = "taps", double_buffer: bool = False,
                  fused_flow_head: bool = False, gate_dtype: torch.dtype = torch.bfloat16,
                  flow_lane: str = "mask", direct_flow: bool = True, mask_head: str = "split",
-                 convex: str = "head", taps_epi: bool = True):
+                 convex: str = "head", taps_epi: bool = True, fuse_update: bool = True):
         nat.require()
         self.taps_epi = taps_epi
+        self.fuse_update = fuse_update
         assert convex in ("fused", "separate", "head"), convex
         self.convex = convex
         assert mask_head in ("split", "fused"), mask_head
@@ -736,6 +737,15 @@ class RaftEngine:
         taps_epi = (self.taps_epi and self.flow_head == "taps" and self._taps_epi_w is not None and s1.cout == 256
                     and (split_mask or not self.has_mask or not all_iters))
 
+        # Deferred flow update (mask-lane schedule + taps epilogue): iteration i's
+        # coordinate update (the 3x3 tap sum) runs inside iteration i+1's lookup
+        # kernel, so the loop body ends with FlowHead conv1; iteration i's flow
+        # features, mask head and upsampling follow that lookup on the mask lane
+        # (deferred ops, Plan.set_defer), and the epilogue applies the last update
+        # and upsamples the last iteration.  One kernel less per iteration on the
+        # critical path (corr.hip:lookup_coords).
+        defer_update = self.fuse_update and taps_epi and mask_lane_flow and all_iters
+
         def flow_head(fm, f32, before_update=None):
             if taps_epi:
                 self._conv(plan, s1, hx, B, h, w, taps, act=ACT_RELU, epi=EPI_TAPS, tapw=self._taps_epi_w)
@@ -794,7 +804,21 @@ class RaftEngine:
             lane(main)
         else:
             flow_features()
-        plan.add_lookup([coords, corr] + levels + [None] * (4 - L), [L, B, h, w, self.radius, h * w, blocked])
+        if defer_update:
+            plan.add_lookup([coords, corr] + levels + [None] * (4 - L) + [taps, self._fh2_b, flow32, hx, qx, flow8],
+                            [L, B, h, w, self.radius, h * w, blocked, self.flow_off, self.flow_off])
+            plan.add_record(E_FH)
+            lane(side2)
+            plan.set_defer(1)   # skipped in iteration 0: its flow features ran in the prologue
+            plan.add_wait(E_FH)
+            flow_features()
+            plan.add_record(E_FLOW)
+            upsample(None, flow32, stride)   # iteration i-1 (h still intact: GRU-B waits E_MASK)
+            plan.add_record(E_MASK)
+            plan.set_defer(0)
+            lane(main)
+        else:
+            plan.add_lookup([coords, corr] + levels + [None] * (4 - L), [L, B, h, w, self.radius, h * w, blocked])
         if len(cl) == 2:
             c1 = alloc("c1", (M, cl[0]))
             if self._cc1_w is not None:
@@ -819,7 +843,17 @@ class RaftEngine:
                 plan.add_wait(E_MR)  # the previous iteration's mask head has read h
             self._conv(plan, sp[f"gru{gi}.b"], qx, B, h, w, hx, h32=h32, zbuf=zb, hidden=self.hidden,
                        epi=EPI_GRU_B, bmap=gbias[gi], bmap_coff=2 * self.hidden)
-        if all_iters:
+        if defer_update:
+            lane(main)
+            self._conv(plan, s1, hx, B, h, w, taps, act=ACT_RELU, epi=EPI_TAPS, tapw=self._taps_epi_w)
+            plan.set_segment(2)  # epilogue: the last iteration's update, mask head and upsampling
+            lane(main)
+            plan.add_flow_taps([taps, self._fh2_b, coords, flow32, hx, qx, flow8],
+                               [B, h, w, self.flow_off, self.flow_off])
+            plan.set_defer(1)
+            upsample(None, flow32, stride)
+            plan.set_defer(0)
+        elif all_iters:
             # The mask head + upsampling of iteration i run on a side lane while
             # iteration i+1 proceeds; the flow head's features / flow they read
             # are double-buffered by iteration parity, so the next flow head

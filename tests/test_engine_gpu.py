@@ -326,3 +326,20 @@ def test_flow_lane_schedules_match(flow_lane):
         c = model(i1, i2, num_flow_updates=5, streams=True, flow_lane="main")
         torch.cuda.synchronize()
         assert (a - c).abs().max().item() < 1e-3
+
+
+@pytest.mark.parametrize("W", [160, 256])
+def test_update_fused_into_lookup_is_bitwise(W):
+    """Iteration i's flow update inside iteration i+1's lookup kernel (deferred
+    mask head / upsampling, last update in the epilogue) gives bitwise the flows
+    of the separate update kernel: same tap-sum order, same kernels otherwise.
+    W = 160: per-lane lookup kernel; W = 256: wide (blocked-level) kernel."""
+    model, _ = raft_large()
+    model = model.cuda()
+    i1, i2 = _inputs(2, 128, W, seed=21)
+    i1, i2 = i1.cuda(), i2.cuda()
+    for use_graph in (False, True):
+        a = model(i1, i2, num_flow_updates=5, streams=True, use_graph=use_graph)
+        b = model(i1, i2, num_flow_updates=5, streams=True, use_graph=use_graph, fuse_update=False)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b), (use_graph, (a - b).abs().max().item())
