@@ -743,7 +743,11 @@ class RaftEngine:
         # features, mask head and upsampling follow that lookup on the mask lane
         # (deferred ops, Plan.set_defer), and the epilogue applies the last update
         # and upsamples the last iteration.  One kernel less per iteration on the
-        # critical path (corr.hip:lookup_coords).
+        # critical path (corr.hip:lookup_coords).  Measured and dropped: removing
+        # the E_MASK join by giving the mask head parity copies of h (a second
+        # GRU-B output) and of the flow -- 314 vs 305 us per iteration: the copy
+        # costs the last GRU-B ~4.6 us and the unjoined mask lane slows the
+        # motion / GRU convs it then overlaps.
         defer_update = self.fuse_update and taps_epi and mask_lane_flow and all_iters
 
         def flow_head(fm, f32, before_update=None):
