@@ -222,8 +222,9 @@ class RaftEngine:
                  split: int = 1, flow_head: str = "taps", double_buffer: bool = False,
                  fused_flow_head: bool = False, gate_dtype: torch.dtype = torch.bfloat16,
                  flow_lane: str = "mask", direct_flow: bool = True, mask_head: str = "split",
-                 convex: str = "head", taps_epi: bool = True, fuse_update: bool = True):
+                 convex: str = "head", taps_epi: bool = True, fuse_update: bool = True, fe_split: bool = True):
         nat.require()
+        self.fe_split = fe_split
         self.taps_epi = taps_epi
         self.fuse_update = fuse_update
         assert convex in ("fused", "separate", "head"), convex
@@ -667,11 +668,28 @@ class RaftEngine:
         plan.add_init_coords([coords], [B, h, w])
         plan.add_record(E_CTX)
 
-        lane(main)
-        feat, fh_, fw_ = self._encoder(st, plan, "fe", m.feature_encoder, x0, 2 * B, H, W, bt=pt)
-        assert (fh_, fw_) == (h, w), "The feature encoder should downsample H and W by 8"
         fmap = alloc("fmap", (2 * B, h, w, self.fmap_ch))
-        self._conv(plan, sp["fe.conv"], feat, 2 * B, h, w, fmap)
+        E_FE2 = ev0 + 8
+        if self.fe_split and side2 != main:
+            # the feature encoder of image2 on a third lane, concurrent with image1's
+            # (and the context encoder): per-image instance norms, so the halves are
+            # exact, and the sequential encoder chain that gates the correlation
+            # pyramid is half as long
+            lane(side2)
+            plan.add_wait(E_PREP)
+            featb, _, _ = self._encoder(st, plan, "fe", m.feature_encoder, x0[B:], B, H, W, bt=pt + "fe2.")
+            self._conv(plan, sp["fe.conv"], featb, B, h, w, fmap[B:])
+            plan.add_record(E_FE2)
+            lane(main)
+            feat, fh_, fw_ = self._encoder(st, plan, "fe", m.feature_encoder, x0[:B], B, H, W, bt=pt)
+            assert (fh_, fw_) == (h, w), "The feature encoder should downsample H and W by 8"
+            self._conv(plan, sp["fe.conv"], feat, B, h, w, fmap[:B])
+            plan.add_wait(E_FE2)
+        else:
+            lane(main)
+            feat, fh_, fw_ = self._encoder(st, plan, "fe", m.feature_encoder, x0, 2 * B, H, W, bt=pt)
+            assert (fh_, fw_) == (h, w), "The feature encoder should downsample H and W by 8"
+            self._conv(plan, sp["fe.conv"], feat, 2 * B, h, w, fmap)
         # bf16 levels of /16-wide maps: levels 0 / 1 in the blocked layout (one
         # pyramid tile per block: whole-line writes, 2 x 2 blocks per lookup window)
         blocked = int(self.corr_dtype == BF16 and w % 16 == 0 and (h * w) % 8 == 0)
