@@ -56,6 +56,17 @@ CFG_TILES.update({35: (256, 128), 36: (128, 128), 37: (128, 128), 38: (256, 128)
 TUNE_CFGS = (0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34,
              35, 38)
 NUM_CUS = 256
+# config 44: the 3x3 halo-tiled kernel (csrc/kernels/conv_halo.hip); valid only
+# for the shapes halo_ok() accepts, so it is not in CFG_TILES / TUNE_CFGS
+HALO_CFG = 44
+
+
+def halo_ok(spec: "ConvSpec", OW: int, x_coff: int = 0, epi: int = EPI_STD) -> bool:
+    """Whether conv_halo.hip runs this conv (3x3, stride 1, pad 1, cin 64 / 128,
+    <= 128 outputs, rows a multiple of 64 pixels, plain epilogue)."""
+    return (spec.kh == 3 and spec.kw == 3 and spec.sh == 1 and spec.sw == 1 and spec.ph == 1 and spec.pw == 1
+            and spec.cin8 in (64, 128) and spec.cout <= 128 and OW % 64 == 0 and x_coff % 8 == 0
+            and epi == EPI_STD)
 
 
 def load(build_if_missing: bool = True) -> None:

@@ -69,7 +69,8 @@ def _tune(spec: ConvSpec, x, N, H, W, y, kw, reps: int = 5) -> int:
     """Time every tile config of one conv problem; return the fastest."""
     ops = nat.ops()
     best, best_t = None, None
-    for cfg in (nat.TAPS_CFGS if kw.get("epi") == nat.EPI_TAPS else nat.TUNE_CFGS):
+    cfgs = nat.TAPS_CFGS if kw.get("epi") == nat.EPI_TAPS else nat.TUNE_CFGS
+    for cfg in cfgs:
         if kw.get("epi") == nat.EPI_CONVEX and cfg in nat.NARROW_CFGS:
             continue
         args = conv_args(spec, x, N, H, W, y, **dict(kw, cfg=cfg))

@@ -585,3 +585,27 @@ def test_conv_taps_epilogue(cfg):
     out = taps.cpu()
     assert _rel(out[:, :18], ref) < 5e-3
     assert (out[:, 18:] == 7.0).all()
+
+
+@pytest.mark.parametrize("N,H,W,cin,cout", [(2, 9, 64, 64, 64), (1, 6, 128, 128, 128), (2, 5, 64, 64, 96),
+                                            (1, 4, 192, 128, 64)])
+def test_conv_halo_matches_reference(N, H, W, cin, cout):
+    """conv_halo.hip (config 44): 3x3 / s1 / p1 with the LDS input halo, against
+    fp32 torch; bias + relu + residual epilogue and bf16 output as in the encoders."""
+    nat = _nat()
+    torch.manual_seed(12)
+    x = torch.randn(N, H, W, cin)
+    k = torch.randn(3, 3, cin, cout) / math.sqrt(9 * cin)
+    b = torch.randn(cout) * 0.1
+    res = torch.randn(N, H, W, cout)
+    spec = nat.make_spec(k, b, (1, 1), (1, 1), device=DEV)
+    assert nat.halo_ok(spec, W)
+    xg = x.to(DEV, torch.bfloat16).contiguous()
+    base = R.conv2d_nhwc(_bf(x), _bf(k), b, (1, 1), (1, 1))
+    y = nat.conv2d(spec, xg, out_dtype=torch.float32, cfg=nat.HALO_CFG)
+    torch.cuda.synchronize()
+    assert _rel(y.cpu(), base) < 2e-3
+    rg = res.to(DEV, torch.bfloat16).contiguous()
+    y = nat.conv2d(spec, xg, act=nat.ACT_RELU, out_dtype=torch.bfloat16, res=rg, res_post=1, cfg=nat.HALO_CFG)
+    torch.cuda.synchronize()
+    assert _rel(y.float().cpu(), torch.relu(torch.relu(base) + _bf(res))) < 1e-2
