@@ -83,6 +83,8 @@ def main():
                     help="separate flow-update kernel after the flow head instead of inside the next lookup")
     ap.add_argument("--no-fe-split", action="store_true",
                     help="one feature-encoder pass over both images instead of one per image on two lanes")
+    ap.add_argument("--fork-after", default="lookup", choices=["lookup", "cc1"],
+                    help="main-lane kernel after which the mask lane forks each iteration")
     ap.add_argument("--no-direct-flow", action="store_true", help="flow branch 7x7 conv on the implicit GEMM instead of the direct VALU kernel")
     ap.add_argument("--split", type=int, default=1, help="independent batch parts (one hipGraph each) run concurrently per GPU")
     ap.add_argument("--pipeline", action=argparse.BooleanOptionalAction, default=False,
@@ -142,7 +144,8 @@ def main():
                      gate_dtype=torch.bfloat16 if args.gate_dtype == "bf16" else torch.float32,
                      flow_lane=args.flow_lane, mask_head=args.mask_head,
                      convex=args.convex, copy_output=not args.no_copy_output, taps_epi=not args.no_taps_epi,
-                     fuse_update=not args.no_fuse_update, fe_split=not args.no_fe_split)
+                     fuse_update=not args.no_fuse_update, fe_split=not args.no_fe_split,
+                     fork_after=args.fork_after)
     pipelined = args.pipeline and not args.no_graph
     eng = model.engine(dev, **engine_kw) if pipelined else None
 
@@ -236,6 +239,7 @@ def main():
                 "taps_epilogue": not args.no_taps_epi,
                 "update_in_lookup": not args.no_fuse_update,
                 "feature_encoder_split": not args.no_fe_split,
+                "fork_after": args.fork_after,
                 "batch_parts": args.split,
                 "cross_batch_pipeline": bool(pipelined),
                 "h2d_in_timed_region": not args.no_h2d,

@@ -223,8 +223,11 @@ class RaftEngine:
                  split: int = 1, flow_head: str = "taps", double_buffer: bool = False,
                  fused_flow_head: bool = False, gate_dtype: torch.dtype = torch.bfloat16,
                  flow_lane: str = "mask", direct_flow: bool = True, mask_head: str = "split",
-                 convex: str = "head", taps_epi: bool = True, fuse_update: bool = True, fe_split: bool = True):
+                 convex: str = "head", taps_epi: bool = True, fuse_update: bool = True, fe_split: bool = True,
+                 fork_after: str = "lookup"):
         nat.require()
+        assert fork_after in ("lookup", "cc1"), fork_after
+        self.fork_after = fork_after
         self.fe_split = fe_split
         self.taps_epi = taps_epi
         self.fuse_update = fuse_update
@@ -827,9 +830,22 @@ class RaftEngine:
             lane(main)
         else:
             flow_features()
+        c1 = alloc("c1", (M, cl[0])) if len(cl) == 2 else None
+
+        def convcorr1():
+            if self._cc1_w is not None:
+                plan.add_conv1x1([corr, self._cc1_w, self._cc1_b, c1],
+                                 [M, self.corr_cs, self._cc1_kpad, cl[0], ACT_RELU, 0])
+            else:
+                self._conv(plan, sp["me.convcorr1"], corr, B, h, w, c1, act=ACT_RELU)
+
+        cc1_done = False
         if defer_update:
             plan.add_lookup([coords, corr] + levels + [None] * (4 - L) + [taps, self._fh2_b, flow32, hx, qx, flow8],
                             [L, B, h, w, self.radius, h * w, blocked, self.flow_off, self.flow_off])
+            if self.fork_after == "cc1" and c1 is not None:
+                convcorr1()   # the mask lane forks one kernel later
+                cc1_done = True
             plan.add_record(E_FH)
             lane(side2)
             plan.set_defer(1)   # skipped in iteration 0: its flow features ran in the prologue
@@ -843,12 +859,8 @@ class RaftEngine:
         else:
             plan.add_lookup([coords, corr] + levels + [None] * (4 - L), [L, B, h, w, self.radius, h * w, blocked])
         if len(cl) == 2:
-            c1 = alloc("c1", (M, cl[0]))
-            if self._cc1_w is not None:
-                plan.add_conv1x1([corr, self._cc1_w, self._cc1_b, c1],
-                                 [M, self.corr_cs, self._cc1_kpad, cl[0], ACT_RELU, 0])
-            else:
-                self._conv(plan, sp["me.convcorr1"], corr, B, h, w, c1, act=ACT_RELU)
+            if not cc1_done:
+                convcorr1()
             self._conv(plan, sp["me.convcorr2"], c1, B, h, w, cf, act=ACT_RELU)
         else:
             self._conv(plan, sp["me.convcorr1"], corr, B, h, w, cf, act=ACT_RELU)
