@@ -771,6 +771,22 @@ class RaftEngine:
         # costs the last GRU-B ~4.6 us and the unjoined mask lane slows the
         # motion / GRU convs it then overlaps.
         defer_update = self.fuse_update and taps_epi and mask_lane_flow and all_iters
+        # the same deferral on one in-order lane (batch < 4 and raft_small): the
+        # update in the lookup, iteration i's flow features right after it, the
+        # upsampling of iteration i-1 next, FlowHead conv1 (+ taps GEMM) last
+        defer_single = (self.fuse_update and self.flow_head == "taps" and all_iters and main == side == side2
+                        and not self.double_buffer)
+        fm_buf = alloc("fm", (M, fm_ch)) if defer_single else None
+
+        def taps_only(fm):
+            if taps_epi:
+                self._conv(plan, s1, hx, B, h, w, taps, act=ACT_RELU, epi=EPI_TAPS, tapw=self._taps_epi_w)
+                return
+            self._conv(plan, s1, hx, B, h, w, fm, act=ACT_RELU)
+            if self._taps_w is not None:
+                plan.add_taps_gemm([fm, self._taps_w, taps], [M, self.fh_hidden, 0])
+            else:
+                self._conv(plan, sp["fh2.taps"], fm, B, h, w, taps)
 
         def flow_head(fm, f32, before_update=None):
             if taps_epi:
@@ -828,7 +844,7 @@ class RaftEngine:
             flow_features()
             plan.add_record(E_FLOW)
             lane(main)
-        else:
+        elif not defer_single:
             flow_features()
         c1 = alloc("c1", (M, cl[0])) if len(cl) == 2 else None
 
@@ -840,7 +856,14 @@ class RaftEngine:
                 self._conv(plan, sp["me.convcorr1"], corr, B, h, w, c1, act=ACT_RELU)
 
         cc1_done = False
-        if defer_update:
+        if defer_single:
+            plan.add_lookup([coords, corr] + levels + [None] * (4 - L) + [taps, self._fh2_b, flow32, hx, qx, flow8],
+                            [L, B, h, w, self.radius, h * w, blocked, self.flow_off, self.flow_off])
+            flow_features()
+            plan.set_defer(1)
+            upsample(fm_buf, flow32, stride)   # iteration i-1
+            plan.set_defer(0)
+        elif defer_update:
             plan.add_lookup([coords, corr] + levels + [None] * (4 - L) + [taps, self._fh2_b, flow32, hx, qx, flow8],
                             [L, B, h, w, self.radius, h * w, blocked, self.flow_off, self.flow_off])
             if self.fork_after == "cc1" and c1 is not None:
@@ -878,7 +901,15 @@ class RaftEngine:
                 plan.add_wait(E_MR)  # the previous iteration's mask head has read h
             self._conv(plan, sp[f"gru{gi}.b"], qx, B, h, w, hx, h32=h32, zbuf=zb, hidden=self.hidden,
                        epi=EPI_GRU_B, bmap=gbias[gi], bmap_coff=2 * self.hidden)
-        if defer_update:
+        if defer_single:
+            taps_only(fm_buf)
+            plan.set_segment(2)  # epilogue: the last iteration's update and upsampling
+            plan.add_flow_taps([taps, self._fh2_b, coords, flow32, hx, qx, flow8],
+                               [B, h, w, self.flow_off, self.flow_off])
+            plan.set_defer(1)
+            upsample(fm_buf, flow32, stride)
+            plan.set_defer(0)
+        elif defer_update:
             lane(main)
             self._conv(plan, s1, hx, B, h, w, taps, act=ACT_RELU, epi=EPI_TAPS, tapw=self._taps_epi_w)
             plan.set_segment(2)  # epilogue: the last iteration's update, mask head and upsampling

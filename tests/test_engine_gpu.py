@@ -328,18 +328,20 @@ def test_flow_lane_schedules_match(flow_lane):
         assert (a - c).abs().max().item() < 1e-3
 
 
+@pytest.mark.parametrize("factory,streams", [(raft_large, True), (raft_large, False), (raft_small, False)])
 @pytest.mark.parametrize("W", [160, 256])
-def test_update_fused_into_lookup_is_bitwise(W):
+def test_update_fused_into_lookup_is_bitwise(W, factory, streams):
     """Iteration i's flow update inside iteration i+1's lookup kernel (deferred
     mask head / upsampling, last update in the epilogue) gives bitwise the flows
     of the separate update kernel: same tap-sum order, same kernels otherwise.
-    W = 160: per-lane lookup kernel; W = 256: wide (blocked-level) kernel."""
-    model, _ = raft_large()
+    W = 160: per-lane lookup kernel; W = 256: wide (blocked-level) kernel.
+    streams=False: the one-lane deferral (batch < 4, raft_small)."""
+    model, _ = factory()
     model = model.cuda()
     i1, i2 = _inputs(2, 128, W, seed=21)
     i1, i2 = i1.cuda(), i2.cuda()
     for use_graph in (False, True):
-        a = model(i1, i2, num_flow_updates=5, streams=True, use_graph=use_graph)
-        b = model(i1, i2, num_flow_updates=5, streams=True, use_graph=use_graph, fuse_update=False)
+        a = model(i1, i2, num_flow_updates=5, streams=streams, use_graph=use_graph)
+        b = model(i1, i2, num_flow_updates=5, streams=streams, use_graph=use_graph, fuse_update=False)
         torch.cuda.synchronize()
         assert torch.equal(a, b), (use_graph, (a - b).abs().max().item())
