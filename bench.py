@@ -229,7 +229,7 @@ def main():
                 "num_flow_updates": args.iters,
                 "outputs": "final iteration only (serving mode)" if args.final_only else "all iterations upsampled (reference semantics)",
                 "hipgraph": not args.no_graph,
-                "concurrent_branches": (streams if streams != "auto" else ("auto (on: batch >= 4)" if not args.final_only else "auto (off in final-only mode)")),
+                "concurrent_branches": (streams if streams != "auto" else ("auto (on: batch >= 4 with a mask predictor)" if not args.final_only else "auto (off in final-only mode)")),
                 "flow_head": args.flow_head,
                 "gate_dtype": args.gate_dtype,
                 "flow_lane": args.flow_lane,

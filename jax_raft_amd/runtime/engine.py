@@ -287,7 +287,11 @@ class RaftEngine:
         self.mot_out = me.out_channels
         # loop buffers hold [h | motion | flow]; the context part of the GRU input is folded (see module doc)
         self.hx_real = self.hidden + self.mot_out
-        self.hx_cs = round_up(self.hx_real, 8)
+        # padded to a multiple of 64 channels when that costs <= 16 zero channels
+        # (raft_small: 178 -> 192): the GRU convs' 64-deep K stages then lie inside
+        # one tap and take the FAST im2col loader (conv_igemm.h:FastRow)
+        hx64 = round_up(self.hx_real, 64)
+        self.hx_cs = hx64 if hx64 - self.hx_real <= 16 else round_up(self.hx_real, 8)
         self.mot_off = self.hidden
         self.flow_off = self.mot_off + self.mot_out - 2
         self.gate_cs = round_up(3 * self.hidden, 8)   # fp32 context bias map: [z | r | q] per GRU
@@ -557,14 +561,16 @@ class RaftEngine:
     # at batch 4 than one in-order lane.  In final-only mode the loop has no
     # mask head to overlap, only the flow-feature convs: there lanes measured
     # 13.1 (one lane) vs 12.7-24.9 ms (lanes, schedule-dependent run to run)
-    # at batch 4, so "auto" keeps one lane.
+    # at batch 4, so "auto" keeps one lane.  Without a mask predictor
+    # (raft_small) only the flow-feature convs could overlap: one lane measured
+    # 562 vs 528 pairs/s at batch 4, so "auto" keeps one lane there too.
     AUTO_STREAMS_MIN_BATCH = 4
 
     def _build(self, B: int, H: int, W: int, n_iters: int, all_iters: bool = True) -> _PlanState:
         if self.streams_mode != "auto":
             return self._build_impl(B, H, W, n_iters, all_iters)
         nb = B // self.split if (self.split > 1 and B % self.split == 0) else B
-        on = nb >= self.AUTO_STREAMS_MIN_BATCH and all_iters
+        on = nb >= self.AUTO_STREAMS_MIN_BATCH and all_iters and self.has_mask
         saved = (self.streams, self.flow_lane, self.mask_head)
         self.streams = on
         self.flow_lane = self._flow_lane_opt if on else "main"

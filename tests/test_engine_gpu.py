@@ -258,10 +258,12 @@ def test_convex_head_kernel_matches_fp32(B, h, w, cs, coff, tiles):
     assert err < 2e-3 * ref.abs().max().item() + 1e-3, err
 
 
-def test_streams_auto_matches_lanes_and_single_lane():
-    """streams="auto" picks the single in-order lane below batch 4 and the lane
-    schedule from batch 4; all three schedules give the same flows."""
-    model, _ = raft_small()
+@pytest.mark.parametrize("factory", [raft_small, raft_large])
+def test_streams_auto_matches_lanes_and_single_lane(factory):
+    """streams="auto" picks the single in-order lane below batch 4 (and always
+    without a mask predictor: raft_small) and the lane schedule from batch 4;
+    all three schedules give the same flows."""
+    model, _ = factory()
     model = model.cuda()
     for B in (1, 4):
         i1, i2 = (t.cuda() for t in _inputs(B, 128, 128, seed=40 + B))
@@ -269,14 +271,21 @@ def test_streams_auto_matches_lanes_and_single_lane():
         b = model(i1, i2, num_flow_updates=3, streams=True)
         c = model(i1, i2, num_flow_updates=3, streams=False)
         torch.cuda.synchronize()
-        assert (a - b).abs().max().item() < 1e-3 and (a - c).abs().max().item() < 1e-3
+        if factory is raft_small:   # same kernels in every schedule
+            assert (a - b).abs().max().item() < 1e-3 and (a - c).abs().max().item() < 1e-3
+        else:   # lanes: split mask head + FlowHead taps epilogue (bf16-level differences)
+            mag = c.norm(dim=-1).mean().item()
+            assert _epe(a, b if B >= 4 else c) < 1e-4 and _epe(b, c) < 1e-2 * mag + 1e-2
         eng = model.engine(torch.device("cuda", 0), streams="auto")
         st = eng._states[(B, 128, 128, 3, True)]
-        assert (st.plan.num_lanes() > 1) == (B >= eng.AUTO_STREAMS_MIN_BATCH)
+        assert (st.plan.num_lanes() > 1) == (B >= eng.AUTO_STREAMS_MIN_BATCH and eng.has_mask)
         # final-only (serving) mode: "auto" keeps one lane at every batch
         d = model(i1, i2, num_flow_updates=3, streams="auto", return_all_iters=False)
         torch.cuda.synchronize()
-        assert (d[-1] - c[-1]).abs().max().item() < 1e-3
+        if factory is raft_small:
+            assert (d[-1] - c[-1]).abs().max().item() < 1e-3
+        else:
+            assert _epe(d[-1], c[-1]) < 1e-2 * c[-1].norm(dim=-1).mean().item() + 1e-2
         assert eng._states[(B, 128, 128, 3, False)].plan.num_lanes() == 1
 
 
