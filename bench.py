@@ -195,7 +195,10 @@ def main():
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     barrier()
-    step_ms = sorted(events[i].elapsed_time(events[i + 1]) for i in range(args.steps))
+    step_seq = [events[i].elapsed_time(events[i + 1]) for i in range(args.steps)]
+    if os.environ.get("JR_BENCH_STEPS"):   # per-step device times in order (diagnostics)
+        print("step_ms", [round(t, 3) for t in step_seq], file=sys.stderr)
+    step_ms = sorted(step_seq)
     pct = lambda q: round(step_ms[min(len(step_ms) - 1, int(q * len(step_ms)))], 3)
     dt = torch.tensor([t1 - t0], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
     if pg is not None:
