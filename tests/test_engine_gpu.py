@@ -92,6 +92,12 @@ def test_weight_update_repacks():
     b = model(i1, i2, num_flow_updates=2)
     torch.cuda.synchronize()
     assert (a - b).abs().max().item() > 1.0
+    # a replaced parameter object (not an in-place update) is noticed too
+    fh2 = model.update_block.flow_head.conv2
+    fh2.bias = torch.nn.Parameter(fh2.bias.detach() - 1.0)
+    c = model(i1, i2, num_flow_updates=2)
+    torch.cuda.synchronize()
+    assert (a - c).abs().max().item() < 1e-3
 
 
 def test_engine_fp32_pyramid_closer_to_golden():
