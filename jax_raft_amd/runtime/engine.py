@@ -792,7 +792,10 @@ class RaftEngine:
         # the E_MASK join by giving the mask head parity copies of h (a second
         # GRU-B output) and of the flow -- 314 vs 305 us per iteration: the copy
         # costs the last GRU-B ~4.6 us and the unjoined mask lane slows the
-        # motion / GRU convs it then overlaps.
+        # motion / GRU convs it then overlaps.  Also dropped: mask-lane kernels
+        # capped at 62 KB of LDS per block (conv configs filtered, convex-head
+        # weights staged in two halves) so they could share a CU with a 98 KB
+        # critical-lane block: 310 vs 316 pairs/s.
         defer_update = self.fuse_update and taps_epi and mask_lane_flow and all_iters
         # the same deferral on one in-order lane (batch < 4 and raft_small): the
         # update in the lookup, iteration i's flow features right after it, the
