@@ -87,9 +87,11 @@ def main():
                     help="main-lane kernel after which the mask lane forks each iteration")
     ap.add_argument("--no-direct-flow", action="store_true", help="flow branch 7x7 conv on the implicit GEMM instead of the direct VALU kernel")
     ap.add_argument("--split", type=int, default=1, help="independent batch parts (one hipGraph each) run concurrently per GPU")
-    ap.add_argument("--pipeline", action=argparse.BooleanOptionalAction, default=False,
-                    help="cross-batch pipelining: batch i+1's encoders + correlation pyramid run concurrently "
-                         "with batch i's refinement loop (two plan slots, prologue / loop graphs on two streams)")
+    ap.add_argument("--pipeline", default="off", choices=["off", "graph", "streams"],
+                    help="cross-batch software pipelining: 'graph' = each step replays ONE hipGraph holding batch i's "
+                         "refinement loop and batch i+1's encoders + correlation pyramid as parallel branches "
+                         "(engine.pipelined); 'streams' = the two phases as separate graphs on two streams "
+                         "(engine.submit, measured to serialise)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse >1 rank on fewer GPUs")
     args = ap.parse_args()
@@ -146,11 +148,20 @@ def main():
                      convex=args.convex, copy_output=not args.no_copy_output, taps_epi=not args.no_taps_epi,
                      fuse_update=not args.no_fuse_update, fe_split=not args.no_fe_split,
                      fork_after=args.fork_after)
-    pipelined = args.pipeline and not args.no_graph
-    eng = model.engine(dev, **engine_kw) if pipelined else None
+    pipelined = args.pipeline == "streams" and not args.no_graph
+    copipe = args.pipeline == "graph" and not args.no_graph
+    eng = model.engine(dev, **engine_kw) if (pipelined or copipe) else None
+    if copipe:
+        # fill the pipeline: the first batch's prologue (its loop runs in the first warmup / timed step)
+        eng.pipelined(img1.to(dev), img2.to(dev), args.iters, return_all_iters=not args.final_only)
 
     def forward(a, b):
-        """One step; returns (flows, stream the step's work ends on)."""
+        """One step; returns (flows, stream the step's work ends on).  Pipelined
+        'graph' mode: the flows of the previous step's inputs (one loop + one
+        prologue of work per step)."""
+        if copipe:
+            return (eng.pipelined(a, b, args.iters, return_all_iters=not args.final_only),
+                    torch.cuda.current_stream(dev))
         if pipelined:
             # batch i's encoders + correlation pyramid overlap batch i-1's refinement loop
             h = eng.submit(a, b, args.iters, return_all_iters=not args.final_only)
@@ -183,6 +194,8 @@ def main():
 
     out = run(args.warmup)
     torch.cuda.synchronize(dev)
+    if out is None:   # pipelined with --warmup 0: nothing finished yet
+        out = torch.zeros((1 if args.final_only else args.iters, B, H, W, 2))
     assert out.shape == (1 if args.final_only else args.iters, B, H, W, 2) and bool(torch.isfinite(out[-1]).all())
 
     # per-step device timestamps (hipEvents on the compute stream) for the
@@ -195,6 +208,9 @@ def main():
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     barrier()
+    if copipe:
+        eng.flush()   # the last prologue's batch (untimed)
+        torch.cuda.synchronize(dev)
     step_seq = [events[i].elapsed_time(events[i + 1]) for i in range(args.steps)]
     if os.environ.get("JR_BENCH_STEPS"):   # per-step device times in order (diagnostics)
         print("step_ms", [round(t, 3) for t in step_seq], file=sys.stderr)
@@ -244,7 +260,7 @@ def main():
                 "feature_encoder_split": not args.no_fe_split,
                 "fork_after": args.fork_after,
                 "batch_parts": args.split,
-                "cross_batch_pipeline": bool(pipelined),
+                "cross_batch_pipeline": args.pipeline if not args.no_graph else "off",
                 "h2d_in_timed_region": not args.no_h2d,
                 "h2d_overlapped": not (args.no_h2d or args.sync_h2d),
                 "parallelism": f"dp{world}",

@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <functional>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../kernels/kernels.h"
@@ -1192,20 +1193,130 @@ class Plan : public torch::CustomClassHolder {
     TORCH_CHECK(e == hipSuccess, "graph launch failed: ", hipGetErrorString(e));
   }
 
- private:
-  void reset_part(int64_t part) {
-    if (pexec_[part]) { (void)hipGraphExecDestroy(pexec_[part]); pexec_[part] = nullptr; }
-    if (pgraph_[part]) { (void)hipGraphDestroy(pgraph_[part]); pgraph_[part] = nullptr; }
-    pcaptured_[part] = -1;
+  // Software-pipelined step: ONE hipGraph holding this plan's refinement loop
+  // + epilogue (batch i) and `next`'s prologue (encoders + correlation pyramid
+  // of batch i+1, a plan with its own buffers) as independent branches.  The
+  // loop is latency-bound (one workgroup per CU, ~220 of 256 CUs per kernel);
+  // the throughput-bound encoder convs fill the idle SIMD slots.  Two graphs
+  // launched on two streams serialise on this ROCm (measured 196 pairs/s,
+  // engine.submit), the branches of one graph do not.  The loop branch is
+  // enqueued first, so its nodes come first in the graph's launch order.
+  void capture_pipelined(c10::intrusive_ptr<Plan> next, int64_t n_iters) {
+    TORCH_CHECK(next.get() != this, "capture_pipelined: the next plan must have its own buffers");
+    reset_pipe();
+    // The two phases are captured on their own (capture_part) and their nodes
+    // copied, with their dependency edges, into one graph with no edge between
+    // the two: every lane of both stays a parallel branch.  (Enqueueing both
+    // into one stream capture -- the next plan's lanes forked from this one's
+    // capture stream -- crashed hipStreamEndCapture on this ROCm whenever both
+    // plans use several lanes (batch 4); a child-graph node runs its graph's
+    // nodes in order on one stream, i.e. without the lanes.)
+    if (pcaptured_[1] != n_iters) capture_part(1, n_iters);
+    if (next->pcaptured_[0] != n_iters) next->capture_part(0, n_iters);
+    debug_ = std::getenv("JR_PLAN_DEBUG") != nullptr;
+    hipGraph_t g = nullptr;
+    TORCH_CHECK(hipGraphCreate(&g, 0) == hipSuccess, "graph create");
+    pipe_graph_ = g;
+    append_graph(g, pgraph_[1]);
+    // JR_PIPE_PROLOGUE=child: the prologue as ONE child-graph node (its nodes
+    // in order on one stream), so the step uses the loop's lanes + one stream
+    const char* pm = std::getenv("JR_PIPE_PROLOGUE");
+    if (pm && std::string(pm) == "child") {
+      hipGraphNode_t np = nullptr;
+      hipError_t e2 = hipGraphAddChildGraphNode(&np, g, nullptr, 0, next->pgraph_[0]);
+      TORCH_CHECK(e2 == hipSuccess, "child graph (prologue): ", hipGetErrorString(e2));
+    } else {
+      append_graph(g, next->pgraph_[0]);
+    }
+    hipError_t e3 = hipGraphInstantiate(&pipe_exec_, g, nullptr, nullptr, 0);
+    if (debug_) fprintf(stderr, "[plan] pipelined instantiate %d\n", (int)e3);
+    TORCH_CHECK(e3 == hipSuccess, "graph instantiate failed: ", hipGetErrorString(e3));
+    pipe_iters_ = n_iters;
+    pipe_next_ = next.get();
   }
-  void capture_into(int64_t n_iters, int part, hipGraph_t* graph_out, hipGraphExec_t* exec_out) {
+  // Copy every node of src (kernel / empty nodes: what a plan capture holds)
+  // into dst in dependency order, keeping src's edges.
+  static void append_graph(hipGraph_t dst, hipGraph_t src) {
+    size_t n = 0;
+    TORCH_CHECK(hipGraphGetNodes(src, nullptr, &n) == hipSuccess, "graph nodes");
+    std::vector<hipGraphNode_t> nodes(n);
+    TORCH_CHECK(hipGraphGetNodes(src, nodes.data(), &n) == hipSuccess, "graph nodes");
+    std::unordered_map<hipGraphNode_t, size_t> index;
+    for (size_t i = 0; i < n; ++i) index[nodes[i]] = i;
+    std::vector<std::vector<size_t>> deps(n), users(n);
+    std::vector<size_t> missing(n, 0);
+    for (size_t i = 0; i < n; ++i) {
+      size_t nd = 0;
+      TORCH_CHECK(hipGraphNodeGetDependencies(nodes[i], nullptr, &nd) == hipSuccess, "node deps");
+      std::vector<hipGraphNode_t> d(nd);
+      if (nd) TORCH_CHECK(hipGraphNodeGetDependencies(nodes[i], d.data(), &nd) == hipSuccess, "node deps");
+      for (auto x : d) {
+        const size_t j = index.at(x);
+        deps[i].push_back(j);
+        users[j].push_back(i);
+      }
+      missing[i] = deps[i].size();
+    }
+    std::vector<hipGraphNode_t> copy(n, nullptr);
+    std::vector<size_t> ready;
+    for (size_t i = 0; i < n; ++i) if (!missing[i]) ready.push_back(i);
+    size_t done = 0;
+    while (!ready.empty()) {
+      const size_t i = ready.back();
+      ready.pop_back();
+      std::vector<hipGraphNode_t> d;
+      for (size_t j : deps[i]) d.push_back(copy[j]);
+      hipGraphNodeType type;
+      TORCH_CHECK(hipGraphNodeGetType(nodes[i], &type) == hipSuccess, "node type");
+      hipError_t e = hipSuccess;
+      if (type == hipGraphNodeTypeKernel) {
+        hipKernelNodeParams kp;
+        e = hipGraphKernelNodeGetParams(nodes[i], &kp);
+        if (e == hipSuccess) e = hipGraphAddKernelNode(&copy[i], dst, d.data(), d.size(), &kp);
+      } else if (type == hipGraphNodeTypeEmpty) {
+        e = hipGraphAddEmptyNode(&copy[i], dst, d.data(), d.size());
+      } else {
+        TORCH_CHECK(false, "capture_pipelined: unsupported graph node type ", (int)type);
+      }
+      TORCH_CHECK(e == hipSuccess, "capture_pipelined: node copy failed: ", hipGetErrorString(e));
+      ++done;
+      for (size_t u : users[i]) if (--missing[u] == 0) ready.push_back(u);
+    }
+    TORCH_CHECK(done == n, "capture_pipelined: cyclic graph");
+  }
+  // n_iters of the pipelined graph if it was captured with `next`, else -1.
+  int64_t pipelined_iters(c10::intrusive_ptr<Plan> next) const {
+    return pipe_next_ == next.get() ? pipe_iters_ : -1;
+  }
+  void replay_pipelined() {
+    TORCH_CHECK(pipe_exec_ != nullptr, "plan: no pipelined graph captured");
+    hipError_t e = hipGraphLaunch(pipe_exec_, cur_stream());
+    TORCH_CHECK(e == hipSuccess, "graph launch failed: ", hipGetErrorString(e));
+  }
+
+ private:
+  void reset_pipe() {
+    if (pipe_exec_) { (void)hipGraphExecDestroy(pipe_exec_); pipe_exec_ = nullptr; }
+    if (pipe_graph_) { (void)hipGraphDestroy(pipe_graph_); pipe_graph_ = nullptr; }
+    pipe_iters_ = -1;
+    pipe_next_ = nullptr;
+  }
+  hipStream_t ensure_cap_stream() {
     if (!cap_stream_) {
       int least = 0, greatest = 0;
       TORCH_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess, "priority range");
       if (!use_priority()) greatest = 0;
       TORCH_CHECK(hipStreamCreateWithPriority(&cap_stream_, hipStreamNonBlocking, greatest) == hipSuccess, "stream");
     }
-    hipStream_t s = cap_stream_;
+    return cap_stream_;
+  }
+  void reset_part(int64_t part) {
+    if (pexec_[part]) { (void)hipGraphExecDestroy(pexec_[part]); pexec_[part] = nullptr; }
+    if (pgraph_[part]) { (void)hipGraphDestroy(pgraph_[part]); pgraph_[part] = nullptr; }
+    pcaptured_[part] = -1;
+  }
+  void capture_into(int64_t n_iters, int part, hipGraph_t* graph_out, hipGraphExec_t* exec_out) {
+    hipStream_t s = ensure_cap_stream();
     debug_ = std::getenv("JR_PLAN_DEBUG") != nullptr;
     // order the capture after work already queued on the current stream
     TORCH_CHECK(hipStreamSynchronize(cur_stream()) == hipSuccess, "sync");
@@ -1236,6 +1347,7 @@ class Plan : public torch::CustomClassHolder {
     captured_iters_ = -1;
     reset_part(0);
     reset_part(1);
+    reset_pipe();
   }
 
  private:
@@ -1330,8 +1442,19 @@ class Plan : public torch::CustomClassHolder {
     const int l0 = capturing ? 1 : 0;
     hipStream_t st[kMaxLanes] = {};
     st[0] = s;
+    // fork / join only the lanes that hold ops in the enqueued segments: a forked
+    // capture stream holding nothing but the fork wait and the join record
+    // crashes hipStreamEndCapture on this ROCm (e.g. the context-encoder lane in
+    // a loop-only capture, capture_part(1))
+    bool used[kMaxLanes] = {};
+    used[0] = true;
+    for (int sg = 0; sg < 3; ++sg) {
+      if ((sg == 0 && part == 1) || (sg != 0 && part == 0)) continue;
+      for (const auto& o : segs_[sg]) used[o.lane] = true;
+    }
     if (int r = (int)hipEventRecord(fork_, s)) return r;
     for (int l = l0; l < used_lanes_; ++l) {
+      if (!used[l]) continue;
       st[l] = lanes_[l];
       if (int r = (int)hipStreamWaitEvent(st[l], fork_, 0)) return r;
     }
@@ -1353,6 +1476,7 @@ class Plan : public torch::CustomClassHolder {
       for (auto& o : segs_[2]) if (int e = exec_op(o, st, n_iters, recorded)) return e;
     }
     for (int l = l0; l < used_lanes_; ++l) {
+      if (!used[l]) continue;
       if (int r = (int)hipEventRecord(join_[l], st[l])) return r;
       if (int r = (int)hipStreamWaitEvent(s, join_[l], 0)) return r;
     }
@@ -1376,6 +1500,10 @@ class Plan : public torch::CustomClassHolder {
   hipGraph_t pgraph_[2] = {};
   hipGraphExec_t pexec_[2] = {};
   int64_t pcaptured_[2] = {-1, -1};
+  hipGraph_t pipe_graph_ = nullptr;
+  hipGraphExec_t pipe_exec_ = nullptr;
+  int64_t pipe_iters_ = -1;
+  const Plan* pipe_next_ = nullptr;
   bool debug_ = false;
   bool check_ = false;
   bool capturing_ = false;
@@ -1416,6 +1544,9 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.class_<jr::Plan>("Plan")
       .def(torch::init<>())
       .def("set_segment", &jr::Plan::set_segment)
+      .def("capture_pipelined", &jr::Plan::capture_pipelined)
+      .def("pipelined_iters", &jr::Plan::pipelined_iters)
+      .def("replay_pipelined", &jr::Plan::replay_pipelined)
       .def("set_lane", &jr::Plan::set_lane)
       .def("set_parity", &jr::Plan::set_parity)
       .def("set_defer", &jr::Plan::set_defer)

@@ -266,6 +266,7 @@ class RaftEngine:
         self._sig = None
         self._sig_modules = None
         self._pipe = None
+        self._pp = None   # pipelined(): {key, n, pending slot}
         self._analyse()
         self._pack()
 
@@ -1097,6 +1098,92 @@ class RaftEngine:
             done.record(sl)
         out.record_stream(cur)
         return PendingFlow(out, done, self.device)
+
+    # ------------------------------------- software-pipelined graphs (throughput)
+    def _slot_state(self, key, slot: int) -> _PlanState:
+        skey = key + ("pslot", slot)
+        st = self._states.get(skey)
+        if st is None:
+            saved, self.split = self.split, 1
+            try:
+                st = self._build(*key)
+            finally:
+                self.split = saved
+            self._states[skey] = st
+        return st
+
+    @torch.no_grad()
+    def pipelined(self, image1: torch.Tensor, image2: torch.Tensor, num_flow_updates: int = 12,
+                  return_all_iters: bool = True) -> Optional[torch.Tensor]:
+        """Software-pipelined forward for throughput (batch inference, serving):
+        returns the flows of the PREVIOUS call's images (``None`` on the first
+        call); :meth:`flush` returns the last pending batch's flows.
+
+        Each call replays ONE hipGraph (``Plan.capture_pipelined``) whose
+        independent branches are the previous batch's refinement loop +
+        epilogue and this batch's prologue (encoders + correlation pyramid).
+        The loop kernels are latency-bound (one workgroup per CU on ~220 of
+        256 CUs at batch 4), the encoder convs throughput-bound, so the
+        prologue mostly fills SIMD slots the loop leaves idle.  Two plan slots
+        (own buffers, own graphs) alternate; every call does one prologue and
+        one loop, i.e. one forward's work.  (:meth:`submit` replays the two
+        phases as separate graphs on two streams, which serialise on this
+        ROCm.)  The result of each batch is bitwise equal to :meth:`forward`
+        (tests/test_engine_gpu.py)."""
+        if self._signature() != self._sig:
+            self._pack()
+        B, H, W, C = image1.shape
+        assert C == 3, "images must be NHWC with 3 channels"
+        assert self.use_graph, "pipelined() replays captured graphs (use_graph=True)"
+        n = num_flow_updates
+        key = (B, H, W, n, bool(return_all_iters))
+        pp = self._pp
+        if pp is not None and pp["key"] != key and pp["pending"] is not None:
+            raise RuntimeError("pipelined(): flush() the pending batch before changing the input shape / iterations")
+        if pp is None or pp["key"] != key:
+            pp = self._pp = dict(key=key, n=0, pending=None)
+        slot = pp["n"] & 1
+        st = self._slot_state(key, slot)
+        st.inp1.copy_(image1)
+        st.inp2.copy_(image2)
+        prev = pp["pending"]
+        result = None
+        if prev is None:
+            if st.plan.captured_part_iters(0) != n:
+                st.plan.capture_part(0, n)
+            st.plan.replay_part(0)
+        else:
+            pst = self._slot_state(key, prev)
+            fresh = self.copy_output and pst.slot_ok
+            out = torch.empty_like(pst.out) if fresh else pst.out
+            self._point_slot(pst, out)
+            if pst.plan.pipelined_iters(st.plan) != n:
+                pst.plan.capture_pipelined(st.plan, n)
+            pst.plan.replay_pipelined()
+            result = out if fresh else (pst.out.clone() if self.copy_output else pst.out)
+        pp["pending"] = slot
+        pp["n"] += 1
+        return result
+
+    @torch.no_grad()
+    def flush(self) -> Optional[torch.Tensor]:
+        """Finish the batch :meth:`pipelined` left pending (its refinement loop
+        + epilogue as one graph); returns its flows, or ``None`` if none."""
+        pp = self._pp
+        if pp is None or pp["pending"] is None:
+            return None
+        key = pp["key"]
+        st = self._slot_state(key, pp["pending"])
+        n = key[3]
+        fresh = self.copy_output and st.slot_ok
+        out = torch.empty_like(st.out) if fresh else st.out
+        self._point_slot(st, out)
+        if st.plan.captured_part_iters(1) != n:
+            st.plan.capture_part(1, n)
+        st.plan.replay_part(1)
+        pp["pending"] = None
+        pp["n"] = 0
+        return out if fresh else (st.out.clone() if self.copy_output else st.out)
 
     @property
     def loop_stream(self) -> Optional[torch.cuda.Stream]:

@@ -194,6 +194,37 @@ def test_pipelined_submit_matches_forward(final_only):
         assert torch.equal(o, r)
 
 
+@pytest.mark.parametrize("factory,B", [(raft_large, 4), (raft_large, 1), (raft_small, 2)])
+@pytest.mark.parametrize("final_only", [False, True])
+def test_graph_pipelined_matches_forward(factory, B, final_only):
+    """Graph-pipelined steps (one hipGraph = batch i's loop || batch i+1's
+    prologue, two plan slots): call k returns batch k-1's flows, flush() the
+    last; each equals the synchronous forward of the same batch, bitwise.  A
+    shape change without flush() raises."""
+    model, _ = factory()
+    model = model.cuda()
+    eng = model.engine(torch.device("cuda", 0))
+    batches = [tuple(t.cuda() for t in _inputs(B, 128, 256, seed=20 + k)) for k in range(5)]
+    refs = [eng.forward(a, b, 4, return_all_iters=not final_only) for a, b in batches]
+    torch.cuda.synchronize()
+    outs = [eng.pipelined(a, b, 4, return_all_iters=not final_only) for a, b in batches]
+    assert outs[0] is None
+    outs = outs[1:] + [eng.flush()]
+    assert eng.flush() is None
+    torch.cuda.synchronize()
+    for r, o in zip(refs, outs):
+        assert o.shape == r.shape
+        assert torch.equal(o, r)
+    # a second pipelined run re-uses the captured graphs
+    a, b = batches[0]
+    assert eng.pipelined(a, b, 4, return_all_iters=not final_only) is None
+    assert torch.equal(eng.flush(), refs[0])
+    eng.pipelined(a, b, 4, return_all_iters=not final_only)
+    with pytest.raises(RuntimeError):
+        eng.pipelined(a, b, 5, return_all_iters=not final_only)
+    eng.flush()
+
+
 def test_split_mask_head_matches_fused():
     """The mask predictor's 3x3 conv on the mask lane (event-ordered against the
     next iteration's GRU) gives the same flows as the fused 128->512 flow/mask
