@@ -87,8 +87,9 @@ def main():
                     help="main-lane kernel after which the mask lane forks each iteration")
     ap.add_argument("--no-direct-flow", action="store_true", help="flow branch 7x7 conv on the implicit GEMM instead of the direct VALU kernel")
     ap.add_argument("--split", type=int, default=1, help="independent batch parts (one hipGraph each) run concurrently per GPU")
-    ap.add_argument("--pipeline", default="off", choices=["off", "graph", "streams"],
-                    help="cross-batch software pipelining: 'graph' = each step replays ONE hipGraph holding batch i's "
+    ap.add_argument("--pipeline", default="auto", choices=["auto", "off", "graph", "streams"],
+                    help="cross-batch software pipelining: 'auto' = 'graph' where the engine runs one lane (batch < 4, "
+                         "raft_small, final-only; measured faster there) else off; 'graph' = each step replays ONE hipGraph holding batch i's "
                          "refinement loop and batch i+1's encoders + correlation pyramid as parallel branches "
                          "(engine.pipelined); 'streams' = the two phases as separate graphs on two streams "
                          "(engine.submit, measured to serialise)")
@@ -148,8 +149,12 @@ def main():
                      convex=args.convex, copy_output=not args.no_copy_output, taps_epi=not args.no_taps_epi,
                      fuse_update=not args.no_fuse_update, fe_split=not args.no_fe_split,
                      fork_after=args.fork_after)
-    pipelined = args.pipeline == "streams" and not args.no_graph
-    copipe = args.pipeline == "graph" and not args.no_graph
+    mode = args.pipeline
+    if mode == "auto":
+        lanes = model.engine(dev, **engine_kw).uses_lanes(B, not args.final_only)
+        mode = "off" if (lanes or args.split > 1) else "graph"
+    pipelined = mode == "streams" and not args.no_graph
+    copipe = mode == "graph" and not args.no_graph
     eng = model.engine(dev, **engine_kw) if (pipelined or copipe) else None
     if copipe:
         # fill the pipeline: the first batch's prologue (its loop runs in the first warmup / timed step)
@@ -260,7 +265,7 @@ def main():
                 "feature_encoder_split": not args.no_fe_split,
                 "fork_after": args.fork_after,
                 "batch_parts": args.split,
-                "cross_batch_pipeline": args.pipeline if not args.no_graph else "off",
+                "cross_batch_pipeline": mode if not args.no_graph else "off",
                 "h2d_in_timed_region": not args.no_h2d,
                 "h2d_overlapped": not (args.no_h2d or args.sync_h2d),
                 "parallelism": f"dp{world}",

@@ -584,11 +584,21 @@ class RaftEngine:
     # 562 vs 528 pairs/s at batch 4, so "auto" keeps one lane there too.
     AUTO_STREAMS_MIN_BATCH = 4
 
+    def uses_lanes(self, B: int, all_iters: bool = True) -> bool:
+        """Whether the plan for batch ``B`` runs the model's branches on several
+        lanes (``streams`` / its "auto" rule).  Graph-pipelined steps
+        (:meth:`pipelined`) measured faster only on one-lane plans: batch 1
+        145 -> 157 pairs/s, raft_small batch 4 559 -> 602, final-only 326 -> 346;
+        with lanes (raft_large batch 4) 319 -> 289 (profiles/r2_pipelined_graph_ab.txt)."""
+        if self.streams_mode != "auto":
+            return bool(self.streams)
+        nb = B // self.split if (self.split > 1 and B % self.split == 0) else B
+        return nb >= self.AUTO_STREAMS_MIN_BATCH and all_iters and self.has_mask
+
     def _build(self, B: int, H: int, W: int, n_iters: int, all_iters: bool = True) -> _PlanState:
         if self.streams_mode != "auto":
             return self._build_impl(B, H, W, n_iters, all_iters)
-        nb = B // self.split if (self.split > 1 and B % self.split == 0) else B
-        on = nb >= self.AUTO_STREAMS_MIN_BATCH and all_iters and self.has_mask
+        on = self.uses_lanes(B, all_iters)
         saved = (self.streams, self.flow_lane, self.mask_head)
         self.streams = on
         self.flow_lane = self._flow_lane_opt if on else "main"
