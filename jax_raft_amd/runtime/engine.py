@@ -500,7 +500,13 @@ class RaftEngine:
     def _encoder(self, st: _PlanState, plan, tag: str, enc: FeatureEncoder, x: torch.Tensor, N: int, H: int,
                  W: int, bt: str = ""):
         """Lower a FeatureEncoder up to (not including) its final 1x1 conv.  ``tag``
-        names the conv specs ("fe"/"ce"), ``bt`` prefixes the buffers (batch part)."""
+        names the conv specs ("fe"/"ce"), ``bt`` prefixes the buffers (batch part).
+        Instance norms: a two-pass statistics op, then normalise + activation
+        (+ residual).  Measured and dropped: the statistics fused into the conv
+        kernels (per-tile partials re-read from L2 after the epilogue, only
+        configs with one channel tile / image-aligned pixel tiles): 319-320 vs
+        321-323 pairs/s; a one-launch statistics kernel with a last-block
+        reduction: 0.9 ms/step slower (profiles/r2_pipelined_graph_ab.txt)."""
         inorm = enc.norm_kind == NORM_INSTANCE
         sp = self._specs
         bufs = st.bufs
