@@ -11,7 +11,14 @@ each rank processes ``--batch`` pairs per step (default 4, so 8 GPUs = the
 BASELINE config's batch of 32).  Each timed step includes the host->device
 copy of its input pair (the reference times H2D + forward as well,
 validate_sintel.py:185-186); the copy of step i+1 is overlapped with step i
-on a copy stream (runtime/pipeline.py), as a serving loop would.  Timing: W untimed warmup steps, then exactly K
+on a copy stream (runtime/pipeline.py), as a serving loop would.  With
+``--pipeline auto`` (default) the configs whose plan runs on one lane (batch
+< 4, raft_small, final-only) replay graph-pipelined steps (engine.pipelined):
+one hipGraph per step holding batch i's refinement loop and batch i+1's
+encoders + correlation pyramid, so every timed step does exactly one forward's
+work (K loops + K prologues; the pipeline is filled before the warmup and the
+last prologue's batch is drained after the timer).  The headline config
+(raft_large, batch 4) runs the lane schedule without it.  Timing: W untimed warmup steps, then exactly K
 steps bracketed by barrier + synchronize; the MAX over ranks is reported.
 Weights are random-init (no network for checkpoints), data is synthetic, so
 EPE is not measurable here and is reported as null.
