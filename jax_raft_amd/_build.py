@@ -70,12 +70,27 @@ def _run(cmd):
     return r.stdout
 
 
-def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -> Path:
-    """Compile all kernels + runtime for gfx950 and link ``_C.so``."""
+SAN_BUILD = REPO / "build" / "native_san"
+SAN_SO_PATH = PKG_DIR / "_C_san.so"
+
+
+def build(force: bool = False, verbose: bool = False, jobs: int | None = None, sanitize: bool = False) -> Path:
+    """Compile all kernels + runtime for gfx950 and link ``_C.so``.
+
+    ``sanitize=True`` (``python -m jax_raft_amd._build --sanitize``) links
+    ``_C_san.so`` instead: the same kernel objects, the host runtime (plan
+    executor, graph capture / node copy, bindings) built with UndefinedBehavior
+    + bounds sanitizers (host code only -- no GPU sanitizer runs on this pool).
+    Load it with ``JR_NATIVE_SO=jax_raft_amd/_C_san.so`` (scripts/gpu_sanitize.sh)."""
     BUILD.mkdir(parents=True, exist_ok=True)
     inc, lib, abi = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
     common = ["-O3", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}"]
+    host_dir, so_path, host_flags = BUILD, SO_PATH, []
+    if sanitize:
+        SAN_BUILD.mkdir(parents=True, exist_ok=True)
+        host_dir, so_path = SAN_BUILD, SAN_SO_PATH
+        host_flags = ["-fsanitize=undefined,bounds", "-fno-sanitize=vptr", "-fno-omit-frame-pointer", "-g"]
     jobs = jobs or min(8, os.cpu_count() or 4)
     cmds = []
     objs = []
@@ -85,30 +100,33 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
         if force or _stale(obj, src):
             cmds.append([HIPCC, f"--offload-arch={ARCH}", *common, "-c", str(src), "-o", str(obj)])
     for src in HOST_SOURCES:
-        obj = BUILD / (src.stem + ".o")
+        obj = host_dir / (src.stem + ".o")
         objs.append(obj)
         if force or _stale(obj, src):
             incs = [f"-I{p}" for p in inc] + [f"-I{py_inc}"]
-            cmds.append([CXX, *common, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_API_INCLUDE_EXTENSION_H",
-                         *incs, "-I/opt/rocm/include", "-c", str(src), "-o", str(obj)])
+            cmds.append([CXX, *common, *host_flags, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+                         "-DTORCH_API_INCLUDE_EXTENSION_H", *incs, "-I/opt/rocm/include", "-c", str(src), "-o", str(obj)])
     if cmds:
         with cf.ThreadPoolExecutor(jobs) as ex:
             for out in ex.map(_run, cmds):
                 if verbose and out.strip():
                     print(out)
-    need_link = force or not SO_PATH.exists() or any(o.stat().st_mtime > SO_PATH.stat().st_mtime for o in objs)
+    need_link = force or not so_path.exists() or any(o.stat().st_mtime > so_path.stat().st_mtime for o in objs)
     if need_link:
-        tmp = SO_PATH.with_suffix(".so.tmp")
+        tmp = so_path.with_suffix(".so.tmp")
         link = [
             HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp),
             f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
             f"-Wl,-rpath,{lib}", "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib",
         ]
+        if sanitize:   # the g++-instrumented host objects need GCC's UBSan runtime as a dependency
+            ubsan = subprocess.run([CXX, "-print-file-name=libubsan.so"], stdout=subprocess.PIPE, text=True).stdout
+            link.append(os.path.realpath(ubsan.strip()))
         _run(link)
-        os.replace(tmp, SO_PATH)
-    return SO_PATH
+        os.replace(tmp, so_path)
+    return so_path
 
 
 if __name__ == "__main__":
-    p = build(force="--force" in sys.argv, verbose=True)
+    p = build(force="--force" in sys.argv, verbose=True, sanitize="--sanitize" in sys.argv)
     print(p)

@@ -11,11 +11,16 @@ import math
 import os
 import threading
 from dataclasses import dataclass
+from pathlib import Path
 from typing import List, Optional, Sequence, Tuple
 
 import torch
 
-from .._build import SO_PATH
+from .._build import SO_PATH as _DEFAULT_SO
+
+# JR_NATIVE_SO: load another build of the library (e.g. the host-sanitizer
+# build _C_san.so, jax_raft_amd/_build.py --sanitize); default: the in-tree _C.so
+SO_PATH = Path(os.environ["JR_NATIVE_SO"]).resolve() if os.environ.get("JR_NATIVE_SO") else _DEFAULT_SO
 
 _lock = threading.Lock()
 _loaded = False
