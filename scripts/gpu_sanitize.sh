@@ -16,3 +16,4 @@ cat $o/gputests.log $o/bench.err $o/train.err > $o/all.log
 n=$(grep -c "runtime error" $o/all.log || true)
 echo "ubsan runtime errors: $n"
 grep "runtime error" $o/all.log | sort | uniq -c | head -20 || true
+[ "$n" = "0" ]
