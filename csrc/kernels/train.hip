@@ -312,6 +312,7 @@ __global__ __launch_bounds__(256) void norm_bwd_partial_kernel(const bf16* __res
     NormCo co;
     norm_co(co, st, mode, gam, bet, n, N, HW, C, g8 * 8, eps);
     const long base = (long)n * HW * C + g8 * 8;
+#pragma unroll 4
     for (int r = r0 + rg; r < r1; r += nrg) {
       const long off = base + (long)r * C;
       float g[8], xh[8];
@@ -387,6 +388,7 @@ __global__ __launch_bounds__(256) void norm_bwd_apply_kernel(const bf16* __restr
   const long base = (long)n * HW * C + c0;
   const int r0 = blockIdx.x * rows;
   const int r1 = min(r0 + rows, HW);
+#pragma unroll 2
   for (int row = r0 + rg; row < r1; row += nrg) {
     const long off = base + (long)row * C;
     float g[8], xh[8];
