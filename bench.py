@@ -93,6 +93,8 @@ def main():
     ap.add_argument("--fork-after", default="lookup", choices=["lookup", "cc1"],
                     help="main-lane kernel after which the mask lane forks each iteration")
     ap.add_argument("--no-direct-flow", action="store_true", help="flow branch 7x7 conv on the implicit GEMM instead of the direct VALU kernel")
+    ap.add_argument("--no-merge-parts", action="store_true",
+                    help="with --split: one graph per part on its own stream instead of all parts in one graph")
     ap.add_argument("--split", type=int, default=1, help="independent batch parts (one hipGraph each) run concurrently per GPU")
     ap.add_argument("--pipeline", default="auto", choices=["auto", "off", "graph", "streams"],
                     help="cross-batch software pipelining: 'auto' = 'graph' where the engine runs one lane (batch < 4, "
@@ -155,7 +157,7 @@ def main():
                      flow_lane=args.flow_lane, mask_head=args.mask_head,
                      convex=args.convex, copy_output=not args.no_copy_output, taps_epi=not args.no_taps_epi,
                      fuse_update=not args.no_fuse_update, fe_split=not args.no_fe_split,
-                     fork_after=args.fork_after)
+                     fork_after=args.fork_after, merge_parts=not args.no_merge_parts)
     mode = args.pipeline
     if mode == "auto":
         lanes = model.engine(dev, **engine_kw).uses_lanes(B, not args.final_only)

@@ -1288,6 +1288,36 @@ class Plan : public torch::CustomClassHolder {
     }
     TORCH_CHECK(done == n, "capture_pipelined: cyclic graph");
   }
+  // Batch parts as ONE graph: every part plan's full-forward capture (own
+  // buffers, own lanes) copied into a single graph with no edge between the
+  // parts, so their in-order chains interleave on the GPU without any
+  // cross-stream edge (separate graphs on separate streams serialise on this
+  // ROCm).  merge_reset(); merge_add(part) for every part; merge_finish(n);
+  // replay_pipelined().
+  void merge_reset() {
+    reset_pipe();
+    TORCH_CHECK(hipGraphCreate(&pipe_graph_, 0) == hipSuccess, "graph create");
+  }
+  void merge_add(c10::intrusive_ptr<Plan> part, int64_t n_iters) {
+    TORCH_CHECK(pipe_graph_ != nullptr && pipe_exec_ == nullptr, "merge_add: call merge_reset() first");
+    if (part->captured_iters_ != n_iters) {
+      // capture() resets this plan's graphs, the merge in progress included
+      hipGraph_t merging = pipe_graph_;
+      pipe_graph_ = nullptr;
+      part->capture(n_iters);
+      pipe_graph_ = merging;
+    }
+    append_graph(pipe_graph_, part->graph_);
+  }
+  void merge_finish(int64_t n_iters) {
+    TORCH_CHECK(pipe_graph_ != nullptr && pipe_exec_ == nullptr, "merge_finish: call merge_reset() first");
+    hipError_t e = hipGraphInstantiate(&pipe_exec_, pipe_graph_, nullptr, nullptr, 0);
+    TORCH_CHECK(e == hipSuccess, "graph instantiate failed: ", hipGetErrorString(e));
+    pipe_iters_ = n_iters;
+    pipe_next_ = this;
+  }
+  int64_t merged_iters() const { return pipe_next_ == this ? pipe_iters_ : -1; }
+
   // n_iters of the pipelined graph if it was captured with `next`, else -1.
   int64_t pipelined_iters(c10::intrusive_ptr<Plan> next) const {
     return pipe_next_ == next.get() ? pipe_iters_ : -1;
@@ -1551,6 +1581,10 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("capture_pipelined", &jr::Plan::capture_pipelined)
       .def("pipelined_iters", &jr::Plan::pipelined_iters)
       .def("replay_pipelined", &jr::Plan::replay_pipelined)
+      .def("merge_reset", &jr::Plan::merge_reset)
+      .def("merge_add", &jr::Plan::merge_add)
+      .def("merge_finish", &jr::Plan::merge_finish)
+      .def("merged_iters", &jr::Plan::merged_iters)
       .def("set_lane", &jr::Plan::set_lane)
       .def("set_parity", &jr::Plan::set_parity)
       .def("set_defer", &jr::Plan::set_defer)

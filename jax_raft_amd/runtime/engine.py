@@ -168,9 +168,12 @@ class RaftEngine:
             shifted partials (fm read once instead of 9 times); "conv" = the
             3x3 implicit-GEMM conv with the EPI_FLOW epilogue; "fused" = the
             dedicated halo-tiled flow_head kernel (flowhead.hip).
-        split: run the batch as this many independent half-forwards on
-            separate lanes (when the batch divides evenly), so that one
-            part's kernels fill the CUs another part's leave idle.
+        split: run the batch as this many independent part-forwards (when
+            the batch divides evenly), so that one part's kernels fill the
+            CUs another part's leave idle.  merge_parts (default): with
+            use_graph, the parts' captures are copied into ONE hipGraph (no
+            edge between them); else each part's graph is replayed on its
+            own stream (measured to serialise on this ROCm).
         gate_dtype: storage dtype of the ConvGRU z gate and of the folded
             context bias map (bf16 default, fp32 for bit-closer parity); the
             hidden state itself is always carried in fp32.
@@ -224,7 +227,7 @@ class RaftEngine:
                  fused_flow_head: bool = False, gate_dtype: torch.dtype = torch.bfloat16,
                  flow_lane: str = "mask", direct_flow: bool = True, mask_head: str = "split",
                  convex: str = "head", taps_epi: bool = True, fuse_update: bool = True, fe_split: bool = True,
-                 fork_after: str = "lookup"):
+                 fork_after: str = "lookup", merge_parts: bool = True):
         nat.require()
         assert fork_after in ("lookup", "cc1"), fork_after
         self.fork_after = fork_after
@@ -248,6 +251,7 @@ class RaftEngine:
         assert self.flow_head in ("taps", "conv", "fused"), self.flow_head
         self.streams = streams
         self.split = split
+        self.merge_parts = merge_parts
         self._part_streams: List[torch.cuda.Stream] = []
         self._fh2_w = self._fh2_b = None
         self._convex_w = self._convex_b = None
@@ -1025,6 +1029,16 @@ class RaftEngine:
         self._point_slot(st, out)
         if len(st.plans) == 1:
             self._launch(st.plan, num_flow_updates)
+        elif self.use_graph and self.merge_parts:
+            # the parts' captures copied into ONE graph (Plan.merge_*): their chains
+            # interleave with no cross-stream edge; separate graphs serialise
+            p0 = st.plans[0]
+            if p0.merged_iters() != num_flow_updates:
+                p0.merge_reset()
+                for plan in st.plans:
+                    p0.merge_add(plan, num_flow_updates)
+                p0.merge_finish(num_flow_updates)
+            p0.replay_pipelined()
         else:
             cur = torch.cuda.current_stream(self.device)
             fork = torch.cuda.Event()
