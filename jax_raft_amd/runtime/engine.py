@@ -29,7 +29,7 @@ iteration: K = 5 x 256 instead of 5 x 384 for raft_large.
 """
 from __future__ import annotations
 
-
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -227,7 +227,8 @@ class RaftEngine:
                  fused_flow_head: bool = False, gate_dtype: torch.dtype = torch.bfloat16,
                  flow_lane: str = "mask", direct_flow: bool = True, mask_head: str = "split",
                  convex: str = "head", taps_epi: bool = True, fuse_update: bool = True, fe_split: bool = True,
-                 fork_after: str = "lookup", merge_parts: bool = True):
+                 fork_after: str = "lookup", merge_parts: bool = True,
+                 cfg_override: Optional[Dict[str, int]] = None):
         nat.require()
         assert fork_after in ("lookup", "cc1"), fork_after
         self.fork_after = fork_after
@@ -252,6 +253,12 @@ class RaftEngine:
         self.streams = streams
         self.split = split
         self.merge_parts = merge_parts
+        # tile configs fixed per conv spec name (e.g. {"gru0.b": 27}; tools/schedule_tune.py),
+        # else the isolated-timing autotuner picks; JR_CFG_OVERRIDE="name=cfg,..." adds entries
+        self.cfg_override = dict(cfg_override or {})
+        for item in filter(None, os.environ.get("JR_CFG_OVERRIDE", "").split(",")):
+            k, v = item.split("=")
+            self.cfg_override[k.strip()] = int(v)
         self._part_streams: List[torch.cuda.Stream] = []
         self._fh2_w = self._fh2_b = None
         self._convex_w = self._convex_b = None
@@ -487,6 +494,10 @@ class RaftEngine:
     # ------------------------------------------------------------- autotune
     def _conv(self, plan, spec: ConvSpec, x, N, H, W, y, **kw):
         """Append one conv to ``plan``, choosing its tile config (autotuned)."""
+        if self.cfg_override and kw.get("cfg") is None:
+            name = next((k for k, v in self._specs.items() if v is spec), None)
+            if name in self.cfg_override:
+                kw = dict(kw, cfg=self.cfg_override[name])
         if kw.get("epi") == EPI_TAPS and not self.autotune and kw.get("cfg") is None:
             kw = dict(kw, cfg=nat.TAPS_CFGS[0])
         if self.autotune and kw.get("cfg") is None:
