@@ -1262,12 +1262,16 @@ class Plan : public torch::CustomClassHolder {
       missing[i] = deps[i].size();
     }
     std::vector<hipGraphNode_t> copy(n, nullptr);
+    // ready nodes are copied in src creation order: the executor maps a node's
+    // successors onto its streams in creation order, and a depth-first copy of
+    // the forward graph measured 6 % slower (profiles/r2_pipelined_graph_ab.txt)
     std::vector<size_t> ready;
     for (size_t i = 0; i < n; ++i) if (!missing[i]) ready.push_back(i);
     size_t done = 0;
     while (!ready.empty()) {
-      const size_t i = ready.back();
-      ready.pop_back();
+      const auto it = std::min_element(ready.begin(), ready.end());
+      const size_t i = *it;
+      ready.erase(it);
       std::vector<hipGraphNode_t> d;
       for (size_t j : deps[i]) d.push_back(copy[j]);
       hipGraphNodeType type;
