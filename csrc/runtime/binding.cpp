@@ -1221,17 +1221,15 @@ class Plan : public torch::CustomClassHolder {
     hipGraph_t g = nullptr;
     TORCH_CHECK(hipGraphCreate(&g, 0) == hipSuccess, "graph create");
     pipe_graph_ = g;
-    append_graph(g, pgraph_[1]);
-    // JR_PIPE_PROLOGUE=child: the prologue as ONE child-graph node (its nodes
-    // in order on one stream), so the step uses the loop's lanes + one stream
+    // loop nodes first (the executor launches in creation order); JR_PIPE_PROLOGUE=first
+    // creates the prologue's first (A/B: batch 1 157 -> 78 pairs/s, the two phases then
+    // run one after the other).  (The prologue as one child-graph node, i.e. its nodes
+    // in order on one stream, measured 264 vs 289 pairs/s at batch 4.)
     const char* pm = std::getenv("JR_PIPE_PROLOGUE");
-    if (pm && std::string(pm) == "child") {
-      hipGraphNode_t np = nullptr;
-      hipError_t e2 = hipGraphAddChildGraphNode(&np, g, nullptr, 0, next->pgraph_[0]);
-      TORCH_CHECK(e2 == hipSuccess, "child graph (prologue): ", hipGetErrorString(e2));
-    } else {
-      append_graph(g, next->pgraph_[0]);
-    }
+    const bool pro_first = pm && std::string(pm) == "first";
+    if (pro_first) append_graph(g, next->pgraph_[0]);
+    append_graph(g, pgraph_[1]);
+    if (!pro_first) append_graph(g, next->pgraph_[0]);
     hipError_t e3 = hipGraphInstantiate(&pipe_exec_, g, nullptr, nullptr, 0);
     if (debug_) fprintf(stderr, "[plan] pipelined instantiate %d\n", (int)e3);
     TORCH_CHECK(e3 == hipSuccess, "graph instantiate failed: ", hipGetErrorString(e3));
