@@ -10,18 +10,25 @@ launched by torch.distributed.run, one rank per GPU (RCCL).  Weak scaling:
 each rank processes ``--batch`` pairs per step (default 4, so 8 GPUs = the
 BASELINE config's batch of 32).  Each timed step includes the host->device
 copy of its input pair (the reference times H2D + forward as well,
-validate_sintel.py:185-186); the copy of step i+1 is overlapped with step i
-on a copy stream (runtime/pipeline.py), as a serving loop would.  With
-``--pipeline auto`` (default) the configs whose plan runs on one lane (batch
-< 4, raft_small, final-only) replay graph-pipelined steps (engine.pipelined):
-one hipGraph per step holding batch i's refinement loop and batch i+1's
-encoders + correlation pyramid, so every timed step does exactly one forward's
-work (K loops + K prologues; the pipeline is filled before the warmup and the
-last prologue's batch is drained after the timer).  The headline config
-(raft_large, batch 4) runs the lane schedule without it.  Timing: W untimed warmup steps, then exactly K
-steps bracketed by barrier + synchronize; the MAX over ranks is reported.
+validate_sintel.py:185-186), overlapped with the previous step on a copy
+stream (runtime/pipeline.py), and -- for N>1 -- the RCCL gather of every
+rank's final flows to rank 0 (the DP batched-inference result
+gather), issued asynchronously so it overlaps the next step's compute.  W
+untimed warmup steps, then exactly K steps bracketed by barrier + synchronize;
+the MAX over ranks is reported.
+
+After the headline, the secondary BASELINE configurations are measured the same
+way and added to the SAME JSON line (``extras``; each one's failure gives
+``null`` without losing the headline): raft_large batch 1 (the reference's
+FPS protocol), raft_small batch 1 at 32 and at 12 iterations (config 2), and
+training (config 5: raft_large, 384x512, 12 iterations, batch 6 per GPU,
+sequence loss + AdamW through the Trainer, RCCL gradient all-reduce for N>1,
+synthetic data generated inside each timed step).
+
 Weights are random-init (no network for checkpoints), data is synthetic, so
-EPE is not measurable here and is reported as null.
+EPE is not measurable here and is reported as null; the numerical drift of the
+bf16 engine against the fp32 golden model at this configuration is in
+profiles/r3_drift.md (tools/drift.py).
 """
 from __future__ import annotations
 
@@ -33,7 +40,8 @@ import time
 
 import torch
 
-BASELINE_FPS = 11.8  # README.md:9 of the reference (RTX 3090 Ti, raft_large, 32 iters, batch 1)
+BASELINE_FPS = 11.8         # README.md:9 of the reference (RTX 3090 Ti, raft_large, 32 iters, batch 1)
+BASELINE_SMALL_FPS = 36.6   # README.md:11 (raft_small, 32 iters, batch 1)
 METRIC = "image-pairs/sec + Sintel-clean EPE, raft_large 32 iters at 1/2/4/8 MI355X"
 
 
@@ -54,11 +62,225 @@ def _relaunch(n: int) -> int:
     return subprocess.call(cmd)
 
 
+class Ctx:
+    """Process / device / process-group context of one benchmark run."""
+
+    def __init__(self, args):
+        self.args = args
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        ndev = torch.cuda.device_count()
+        self.gloo = args.dist_backend == "gloo"
+        idx = local_rank % ndev if self.gloo else local_rank
+        torch.cuda.set_device(idx)
+        self.dev = torch.device("cuda", idx)
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+
+            if self.gloo:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=self.dev)
+            self.pg = dist
+
+    def barrier(self):
+        if self.pg is not None:
+            self.pg.barrier()
+        torch.cuda.synchronize(self.dev)
+
+    def _coll_dev(self):
+        return "cpu" if self.gloo else self.dev
+
+    def max_all(self, v: float) -> float:
+        if self.pg is None:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=self._coll_dev())
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
+        return t.item()
+
+    def all_values(self, v: float):
+        if self.pg is None:
+            return [v]
+        t = torch.tensor([v], dtype=torch.float64, device=self._coll_dev())
+        out = [torch.zeros_like(t) for _ in range(self.world)]
+        self.pg.all_gather(out, t)
+        return [x.item() for x in out]
+
+    def world_check(self) -> int:
+        """All-reduce of ones over the job's process group: must equal N."""
+        if self.pg is None:
+            return 1
+        t = torch.ones(1, device=self._coll_dev())
+        self.pg.all_reduce(t)
+        return int(round(t.item()))
+
+
+class FlowGather:
+    """Gather every rank's final flows (B, H, W, 2) fp32 to rank 0.  With RCCL the
+    collective is asynchronous (its own stream, ordered after the producing
+    step by the process group) and overlaps the next step's compute; at most
+    ``depth`` are in flight.  With gloo (the CPU-side rehearsal) it is a
+    synchronous gather of host copies."""
+
+    def __init__(self, ctx: Ctx, shape, depth: int = 2):
+        self.ctx, self.depth = ctx, depth
+        dev = "cpu" if ctx.gloo else ctx.dev
+        self.recv = ([[torch.empty(shape, dtype=torch.float32, device=dev) for _ in range(ctx.world)]
+                      for _ in range(depth)] if ctx.rank == 0 else None)
+        self.inflight = []
+        self.n = 0
+
+    def __call__(self, flows: torch.Tensor) -> None:
+        dist = self.ctx.pg
+        if len(self.inflight) >= self.depth:
+            self.inflight.pop(0).wait()
+        slot = self.n % self.depth
+        self.n += 1
+        glist = self.recv[slot] if self.recv is not None else None
+        if self.ctx.gloo:
+            dist.gather(flows.cpu(), gather_list=glist, dst=0)
+            return
+        self.inflight.append(dist.gather(flows, gather_list=glist, dst=0, async_op=True))
+
+    def drain(self) -> None:
+        while self.inflight:
+            self.inflight.pop(0).wait()
+
+
+def run_inference(ctx: Ctx, model, *, B: int, H: int, W: int, iters: int, steps: int, warmup: int,
+                  final_only: bool, gather: bool, seed: int, engine_kw: dict, pipeline: str = "auto",
+                  h2d: bool = True, sync_h2d: bool = False) -> dict:
+    """Time ``steps`` inference steps of ``B`` pairs per rank; returns the run record."""
+    from jax_raft_amd.runtime.pipeline import InputPrefetcher
+
+    dev = ctx.dev
+    g = torch.Generator().manual_seed(seed + ctx.rank)
+    img1 = torch.rand(B, H, W, 3, generator=g) * 2 - 1
+    img2 = torch.rand(B, H, W, 3, generator=g) * 2 - 1
+    if h2d:
+        img1, img2 = img1.pin_memory(), img2.pin_memory()
+    else:
+        img1, img2 = img1.to(dev), img2.to(dev)
+    pf = InputPrefetcher([(B, H, W, 3), (B, H, W, 3)], dev) if (h2d and not sync_h2d) else None
+    eng = model.engine(dev, **engine_kw)
+    mode = pipeline
+    if mode == "auto":
+        mode = "off" if (eng.uses_lanes(B, not final_only) or engine_kw.get("split", 1) > 1) else "graph"
+    copipe = mode == "graph" and engine_kw.get("use_graph", True)
+    all_iters = not final_only
+    if copipe:   # fill the pipeline: the first batch's prologue (its loop runs in the first step)
+        eng.pipelined(img1.to(dev), img2.to(dev), iters, return_all_iters=all_iters)
+    gat = FlowGather(ctx, (B, H, W, 2)) if (gather and ctx.world > 1) else None
+
+    def forward(a, b):
+        if copipe:
+            return eng.pipelined(a, b, iters, return_all_iters=all_iters)
+        return eng.forward(a, b, iters, return_all_iters=all_iters)
+
+    def run(n, events=None):
+        out = None
+        if pf is not None:
+            pf.put(0, [img1, img2])
+        for i in range(n):
+            if pf is not None:
+                a, b = pf.get(i)
+            else:
+                a, b = img1.to(dev, non_blocking=True), img2.to(dev, non_blocking=True)
+            out = forward(a, b)
+            if gat is not None and out is not None:
+                gat(out[-1])
+            if events is not None:
+                events[i + 1].record()
+            if pf is not None:
+                pf.release(i)
+                if i + 1 < n:
+                    pf.put(i + 1, [img1, img2])
+        return out
+
+    out = run(warmup)
+    if gat is not None:
+        gat.drain()
+    torch.cuda.synchronize(dev)
+    if out is not None:
+        assert out.shape == ((iters if all_iters else 1), B, H, W, 2) and bool(torch.isfinite(out[-1]).all())
+    events = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    ctx.barrier()
+    t0 = time.perf_counter()
+    events[0].record()
+    run(steps, events)
+    if gat is not None:
+        gat.drain()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    ctx.barrier()
+    if copipe:
+        eng.flush()   # the last prologue's batch (untimed)
+        torch.cuda.synchronize(dev)
+    step_ms = sorted(events[i].elapsed_time(events[i + 1]) for i in range(steps))
+    pct = lambda q: round(step_ms[min(len(step_ms) - 1, int(q * len(step_ms)))], 3)
+    el = t1 - t0
+    per_rank = [round(1000.0 * e / steps, 3) for e in ctx.all_values(el)]
+    elapsed = ctx.max_all(el)
+    rec = dict(value=round(ctx.world * B * steps / elapsed, 3), ms_per_step=round(1000.0 * elapsed / steps, 3),
+               steps=steps, warmup=warmup, step_ms_p50=pct(0.5), step_ms_p99=pct(0.99), per_rank_ms_per_step=per_rank,
+               cross_batch_pipeline=mode if engine_kw.get("use_graph", True) else "off",
+               concurrent_branches=bool(eng.uses_lanes(B, all_iters)))
+    if gat is not None:
+        rec["gather"] = "final flows of every rank -> rank 0, async (overlapped with the next step)"
+        rec["gather_ms"] = round(_gather_ms(ctx, gat, out[-1] if out is not None else None, (B, H, W, 2)), 3)
+    rec["tile_cfgs"] = dict(sorted(eng.chosen_cfgs.items()))
+    return rec
+
+
+def _gather_ms(ctx: Ctx, gat: FlowGather, flows, shape) -> float:
+    """Stand-alone time of one final-flow gather (barrier-bracketed, mean of 3)."""
+    flows = flows if flows is not None else torch.zeros(shape, device=ctx.dev)
+    ts = []
+    for _ in range(3):
+        ctx.barrier()
+        t0 = time.perf_counter()
+        gat(flows)
+        gat.drain()
+        torch.cuda.synchronize(ctx.dev)
+        ts.append(time.perf_counter() - t0)
+    return 1000.0 * ctx.max_all(sum(ts) / len(ts))
+
+
+def run_training(ctx: Ctx, *, arch: str, B: int, size, iters: int, steps: int, warmup: int) -> dict:
+    """BASELINE config 5 through the Trainer (fused native step, AdamW, RCCL
+    gradient all-reduce for N>1); each step synthesises its batch on the GPU."""
+    from jax_raft_amd.train.trainer import TrainConfig, Trainer
+
+    cfg = TrainConfig(arch=arch, steps=steps + warmup, batch=B, iters=iters, size=tuple(size), log_every=10 ** 9)
+    tr = Trainer(cfg, device=ctx.dev)
+    for i in range(warmup):
+        tr.train_step(tr.batch_for(i))
+    tr.flush()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        m = tr.train_step(tr.batch_for(warmup + i))
+    tr.flush()
+    torch.cuda.synchronize(ctx.dev)
+    el = time.perf_counter() - t0
+    ctx.barrier()
+    elapsed = ctx.max_all(el)
+    return dict(value=round(ctx.world * B * steps / elapsed, 3), ms_per_step=round(1000.0 * elapsed / steps, 3),
+                steps=steps, warmup=warmup, loss=round(float(m["loss"]), 4),
+                per_rank_ms_per_step=[round(1000.0 * e / steps, 3) for e in ctx.all_values(el)],
+                config=dict(model=arch, per_gpu_batch=B, global_batch=ctx.world * B, image_size=list(size),
+                            num_flow_updates=iters, optimizer="AdamW + one-cycle, clip 1.0",
+                            loss="sequence loss gamma 0.8", grad_allreduce="RCCL" if ctx.world > 1 else None,
+                            data="synthetic, generated on the GPU inside each timed step"))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=4, help="image pairs per GPU per step")
     ap.add_argument("--arch", default="raft_large", choices=["raft_large", "raft_small"])
     ap.add_argument("--height", type=int, default=440)
@@ -68,40 +290,24 @@ def main():
     ap.add_argument("--no-h2d", action="store_true", help="inputs already resident on the GPU")
     ap.add_argument("--sync-h2d", action="store_true", help="copy each step's inputs synchronously (no prefetch overlap)")
     ap.add_argument("--streams", default="auto", choices=["auto", "on", "off"],
-                    help="concurrent model branches on plan lanes: auto = at batch >= 4 per GPU with all iterations upsampled (measured break-even)")
-    ap.add_argument("--no-streams", action="store_true", help="same as --streams off")
-    ap.add_argument("--flow-head", default="taps", choices=["taps", "conv", "fused"],
-                    help="flow head output conv: 1x1 GEMM + tap sum (default), 3x3 conv, or the halo-tiled kernel")
+                    help="concurrent model branches on plan lanes: auto = at batch >= 4 per GPU with all "
+                         "iterations upsampled (measured break-even)")
     ap.add_argument("--final-only", action="store_true",
                     help="serving mode: upsample/return only the final flow (not the reference's output)")
     ap.add_argument("--gate-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="storage of the GRU z gate / folded context bias map (the hidden state is fp32 either way)")
-    ap.add_argument("--flow-lane", default="mask", choices=["side", "main", "mask"])
+    ap.add_argument("--corr-dtype", default="bf16", choices=["bf16", "fp32"], help="correlation pyramid storage")
     ap.add_argument("--no-copy-output", action="store_true",
-                    help="return the engine's static output buffer instead of a fresh copy (measurement knob)")
-    ap.add_argument("--convex", default="head", choices=["fused", "separate", "head"],
-                    help="mask predictor 1x1 conv + convex upsampling: conv epilogue / two kernels / dedicated kernel")
-    ap.add_argument("--mask-head", default="split", choices=["split", "fused"],
-                    help="mask predictor 3x3 conv on the mask lane (split) or batched with the flow head's (fused)")
-    ap.add_argument("--double-buffer", action="store_true", help="parity double-buffering of the flow head outputs")
-    ap.add_argument("--no-taps-epi", action="store_true",
-                    help="FlowHead conv1 stores its features and a separate GEMM forms conv2's taps")
-    ap.add_argument("--no-fuse-update", action="store_true",
-                    help="separate flow-update kernel after the flow head instead of inside the next lookup")
-    ap.add_argument("--no-fe-split", action="store_true",
-                    help="one feature-encoder pass over both images instead of one per image on two lanes")
-    ap.add_argument("--fork-after", default="lookup", choices=["lookup", "cc1"],
-                    help="main-lane kernel after which the mask lane forks each iteration")
-    ap.add_argument("--no-direct-flow", action="store_true", help="flow branch 7x7 conv on the implicit GEMM instead of the direct VALU kernel")
-    ap.add_argument("--no-merge-parts", action="store_true",
-                    help="with --split: one graph per part on its own stream instead of all parts in one graph")
-    ap.add_argument("--split", type=int, default=1, help="independent batch parts (one hipGraph each) run concurrently per GPU")
-    ap.add_argument("--pipeline", default="auto", choices=["auto", "off", "graph", "streams"],
+                    help="return the engine's static output buffer instead of a fresh tensor (measurement knob)")
+    ap.add_argument("--split", type=int, default=1, help="independent batch parts captured into one hipGraph")
+    ap.add_argument("--pipeline", default="auto", choices=["auto", "off", "graph"],
                     help="cross-batch software pipelining: 'auto' = 'graph' where the engine runs one lane (batch < 4, "
-                         "raft_small, final-only; measured faster there) else off; 'graph' = each step replays ONE hipGraph holding batch i's "
-                         "refinement loop and batch i+1's encoders + correlation pyramid as parallel branches "
-                         "(engine.pipelined); 'streams' = the two phases as separate graphs on two streams "
-                         "(engine.submit, measured to serialise)")
+                         "raft_small, final-only; measured faster there) else off; 'graph' = each step replays ONE "
+                         "hipGraph holding batch i's refinement loop and batch i+1's encoders + correlation pyramid")
+    ap.add_argument("--no-gather", action="store_true", help="N>1: skip the RCCL gather of the final flows")
+    ap.add_argument("--extras", default="auto", choices=["auto", "on", "off"],
+                    help="secondary configs after the headline (auto: on for the default headline config)")
+    ap.add_argument("--extra-steps", type=int, default=20)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse >1 rank on fewer GPUs")
     args = ap.parse_args()
@@ -112,177 +318,107 @@ def main():
         # rather than silently benchmarking one GPU.
         sys.exit(_relaunch(args.gpus))
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} != WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    ndev = torch.cuda.device_count()
-    dev_index = local_rank % ndev if args.dist_backend == "gloo" else local_rank
-    torch.cuda.set_device(dev_index)
-    dev = torch.device("cuda", dev_index)
-    pg = None
-    if world > 1:
-        import torch.distributed as dist
-
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
-        pg = dist
-
+    ctx = Ctx(args)
+    if args.gpus != ctx.world and ctx.world > 1:
+        print(f"warning: --gpus {args.gpus} != WORLD_SIZE {ctx.world}; using WORLD_SIZE", file=sys.stderr)
     from jax_raft_amd import raft_large, raft_small
+    from jax_raft_amd.runtime import tunedb
 
-    model, _ = (raft_large if args.arch == "raft_large" else raft_small)(seed=0)
-    model = model.to(dev).eval()
-    B, H, W = args.batch, args.height, args.width
-    g = torch.Generator().manual_seed(1234 + rank)
-    img1 = (torch.rand(B, H, W, 3, generator=g) * 2 - 1)
-    img2 = (torch.rand(B, H, W, 3, generator=g) * 2 - 1)
-    if args.no_h2d:
-        img1, img2 = img1.to(dev), img2.to(dev)
-    else:
-        img1, img2 = img1.pin_memory(), img2.pin_memory()
-    from jax_raft_amd.runtime.pipeline import InputPrefetcher
-
-    # Every step copies its input pair host -> device (the reference times H2D
-    # too); the copy of step i+1 runs on a copy stream while step i computes
-    # (InputPrefetcher), so only the first copy of a run is exposed.
-    pf = None if (args.no_h2d or args.sync_h2d) else InputPrefetcher([(B, H, W, 3), (B, H, W, 3)], dev)
-
-    streams = False if args.no_streams else {"auto": "auto", "on": True, "off": False}[args.streams]
+    factory = raft_large if args.arch == "raft_large" else raft_small
+    model = factory(seed=0)[0].to(ctx.dev).eval()
+    streams = {"auto": "auto", "on": True, "off": False}[args.streams]
     engine_kw = dict(use_graph=not args.no_graph, streams=streams, split=args.split,
-                     flow_head=args.flow_head, double_buffer=args.double_buffer, direct_flow=not args.no_direct_flow,
                      gate_dtype=torch.bfloat16 if args.gate_dtype == "bf16" else torch.float32,
-                     flow_lane=args.flow_lane, mask_head=args.mask_head,
-                     convex=args.convex, copy_output=not args.no_copy_output, taps_epi=not args.no_taps_epi,
-                     fuse_update=not args.no_fuse_update, fe_split=not args.no_fe_split,
-                     fork_after=args.fork_after, merge_parts=not args.no_merge_parts)
-    mode = args.pipeline
-    if mode == "auto":
-        lanes = model.engine(dev, **engine_kw).uses_lanes(B, not args.final_only)
-        mode = "off" if (lanes or args.split > 1) else "graph"
-    pipelined = mode == "streams" and not args.no_graph
-    copipe = mode == "graph" and not args.no_graph
-    eng = model.engine(dev, **engine_kw) if (pipelined or copipe) else None
-    if copipe:
-        # fill the pipeline: the first batch's prologue (its loop runs in the first warmup / timed step)
-        eng.pipelined(img1.to(dev), img2.to(dev), args.iters, return_all_iters=not args.final_only)
+                     corr_dtype=torch.bfloat16 if args.corr_dtype == "bf16" else torch.float32,
+                     copy_output=not args.no_copy_output)
+    B, H, W = args.batch, args.height, args.width
+    head = run_inference(ctx, model, B=B, H=H, W=W, iters=args.iters, steps=args.steps, warmup=args.warmup,
+                         final_only=args.final_only, gather=not args.no_gather, seed=1234, engine_kw=engine_kw,
+                         pipeline=args.pipeline, h2d=not args.no_h2d, sync_h2d=args.sync_h2d)
+    rccl_world = ctx.world_check()
+    del model
+    torch.cuda.empty_cache()
 
-    def forward(a, b):
-        """One step; returns (flows, stream the step's work ends on).  Pipelined
-        'graph' mode: the flows of the previous step's inputs (one loop + one
-        prologue of work per step)."""
-        if copipe:
-            return (eng.pipelined(a, b, args.iters, return_all_iters=not args.final_only),
-                    torch.cuda.current_stream(dev))
-        if pipelined:
-            # batch i's encoders + correlation pyramid overlap batch i-1's refinement loop
-            h = eng.submit(a, b, args.iters, return_all_iters=not args.final_only)
-            return h.out, eng.loop_stream
-        return (model(a, b, num_flow_updates=args.iters, return_all_iters=not args.final_only, **engine_kw),
-                torch.cuda.current_stream(dev))
+    default_cfg = (args.arch == "raft_large" and (B, H, W, args.iters) == (4, 440, 1024, 32) and not args.final_only
+                   and not args.no_graph)
+    extras = {}
+    if args.extras == "on" or (args.extras == "auto" and default_cfg):
+        t_ex = time.perf_counter()
+        ks, kw_ = args.extra_steps, max(3, args.warmup)
+        plan = [("b1_fps", "raft_large", 32, BASELINE_FPS), ("small_b1_fps_32it", "raft_small", 32, BASELINE_SMALL_FPS),
+                ("small_b1_fps_12it", "raft_small", 12, None)]
+        for key, arch, it, base in plan:
+            try:
+                m = (raft_large if arch == "raft_large" else raft_small)(seed=0)[0].to(ctx.dev).eval()
+                r = run_inference(ctx, m, B=1, H=H, W=W, iters=it, steps=ks, warmup=kw_, final_only=False,
+                                  gather=not args.no_gather, seed=99, engine_kw=dict(engine_kw, split=1))
+                r.pop("tile_cfgs", None)
+                r["config"] = dict(model=arch, per_gpu_batch=1, num_flow_updates=it, image_size=[H, W])
+                r["vs_baseline"] = round(r["value"] / ctx.world / base, 3) if base else None
+                extras[key] = r
+                del m
+            except Exception as e:  # noqa: BLE001 -- a failed extra must not lose the headline
+                extras[key] = None
+                print(f"bench.py: extra {key} failed: {type(e).__name__}: {e}", file=sys.stderr)
+            torch.cuda.empty_cache()
+        try:
+            extras["train_pairs_per_s"] = run_training(ctx, arch="raft_large", B=6, size=(384, 512), iters=12,
+                                                       steps=max(5, ks // 2), warmup=3)
+        except Exception as e:  # noqa: BLE001
+            extras["train_pairs_per_s"] = None
+            print(f"bench.py: extra train_pairs_per_s failed: {type(e).__name__}: {e}", file=sys.stderr)
+        extras["extras_wall_s"] = round(time.perf_counter() - t_ex, 1)
 
-    def run(n, events=None):
-        if pf is None:
-            for i in range(n):
-                out, s = forward(img1.to(dev, non_blocking=True), img2.to(dev, non_blocking=True))
-                if events is not None:
-                    events[i + 1].record(s)
-            return out
-        pf.put(0, [img1, img2])
-        for i in range(n):
-            a, b = pf.get(i)
-            out, s = forward(a, b)
-            if events is not None:
-                events[i + 1].record(s)
-            pf.release(i)
-            if i + 1 < n:
-                pf.put(i + 1, [img1, img2])
-        return out
-
-    def barrier():
-        if pg is not None:
-            pg.barrier()
-        torch.cuda.synchronize(dev)
-
-    out = run(args.warmup)
-    torch.cuda.synchronize(dev)
-    if out is None:   # pipelined with --warmup 0: nothing finished yet
-        out = torch.zeros((1 if args.final_only else args.iters, B, H, W, 2))
-    assert out.shape == (1 if args.final_only else args.iters, B, H, W, 2) and bool(torch.isfinite(out[-1]).all())
-
-    # per-step device timestamps (hipEvents on the compute stream) for the
-    # step-time distribution; the headline uses the host clock around all K steps
-    events = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
-    barrier()
-    t0 = time.perf_counter()
-    events[0].record()
-    out = run(args.steps, events)
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    barrier()
-    if copipe:
-        eng.flush()   # the last prologue's batch (untimed)
-        torch.cuda.synchronize(dev)
-    step_seq = [events[i].elapsed_time(events[i + 1]) for i in range(args.steps)]
-    if os.environ.get("JR_BENCH_STEPS"):   # per-step device times in order (diagnostics)
-        print("step_ms", [round(t, 3) for t in step_seq], file=sys.stderr)
-    step_ms = sorted(step_seq)
-    pct = lambda q: round(step_ms[min(len(step_ms) - 1, int(q * len(step_ms)))], 3)
-    dt = torch.tensor([t1 - t0], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
-    if pg is not None:
-        pg.all_reduce(dt, op=pg.ReduceOp.MAX)
-    elapsed = dt.item()
-    ms_per_step = 1000.0 * elapsed / args.steps
-    pairs_per_s = world * B * args.steps / elapsed
-    if rank == 0:
+    if ctx.rank == 0:
         rec = {
             "metric": METRIC,
-            "value": round(pairs_per_s, 3),
+            "value": head["value"],
             "unit": "image-pairs/s",
-            "n_gpus": world,
+            "n_gpus": ctx.world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 3),
-            "step_ms_p50": pct(0.5),
-            "step_ms_p99": pct(0.99),
+            "ms_per_step": head["ms_per_step"],
+            "step_ms_p50": head["step_ms_p50"],
+            "step_ms_p99": head["step_ms_p99"],
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(pairs_per_s / BASELINE_FPS, 3) if args.arch == "raft_large" and args.iters == 32 and not args.final_only else None,
+            "vs_baseline": (round(head["value"] / BASELINE_FPS, 3)
+                            if args.arch == "raft_large" and args.iters == 32 and not args.final_only else None),
+            "vs_baseline_note": "batch-4-per-GPU throughput / the reference's batch-1 FPS; "
+                                "extras.b1_fps.vs_baseline is the like-for-like batch-1 ratio",
             "dtype": "bf16",
             "data": "synthetic (random Sintel-shaped 440x1024 frames, random-init weights; EPE not measurable)",
             "epe_sintel_clean": None,
+            "rccl_world": rccl_world,
+            "per_rank_ms_per_step": head["per_rank_ms_per_step"],
+            "gather_ms": head.get("gather_ms"),
             "config": {
                 "model": args.arch,
-                "global_batch": world * B,
+                "global_batch": ctx.world * B,
                 "per_gpu_batch": B,
                 "image_size": [H, W],
                 "seq_len": None,
                 "num_flow_updates": args.iters,
-                "outputs": "final iteration only (serving mode)" if args.final_only else "all iterations upsampled (reference semantics)",
+                "outputs": ("final iteration only (serving mode)" if args.final_only
+                            else "all iterations upsampled (reference semantics)"),
                 "hipgraph": not args.no_graph,
-                "concurrent_branches": (streams if streams != "auto" else ("auto (on: batch >= 4 with a mask predictor)" if not args.final_only else "auto (off in final-only mode)")),
-                "flow_head": args.flow_head,
+                "concurrent_branches": head["concurrent_branches"],
+                "cross_batch_pipeline": head["cross_batch_pipeline"],
                 "gate_dtype": args.gate_dtype,
-                "flow_lane": args.flow_lane,
-                "mask_head": args.mask_head,
-                "convex": args.convex,
-                "direct_flow_conv": not args.no_direct_flow,
-                "taps_epilogue": not args.no_taps_epi,
-                "update_in_lookup": not args.no_fuse_update,
-                "feature_encoder_split": not args.no_fe_split,
-                "fork_after": args.fork_after,
+                "corr_dtype": args.corr_dtype,
                 "batch_parts": args.split,
-                "cross_batch_pipeline": mode if not args.no_graph else "off",
                 "h2d_in_timed_region": not args.no_h2d,
                 "h2d_overlapped": not (args.no_h2d or args.sync_h2d),
-                "parallelism": f"dp{world}",
+                "result_gather": head.get("gather"),
+                "parallelism": f"dp{ctx.world}",
             },
+            "autotune": {"source": "jax_raft_amd/tuned/<arch>.json + in-process timing of misses",
+                         **tunedb.stats(), "tile_cfgs": head["tile_cfgs"]},
+            "extras": extras or None,
         }
         print(json.dumps(rec), flush=True)
-    if pg is not None:
-        pg.destroy_process_group()
+    if ctx.pg is not None:
+        ctx.pg.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -186,14 +186,19 @@ __global__ __launch_bounds__(256) void seq_loss_kernel(const float* __restrict__
   for (int k = 0; k < LOSS_MAX_N + 5; ++k) acc[k] = 0.f;
   const long stride = (long)gridDim.x * 256;
   for (long p = (long)blockIdx.x * 256 + threadIdx.x; p < P; p += stride) {
-    if (!loss_valid(gt, vin, p, max_flow)) continue;
+    // As the PyTorch oracle (train/loss.py:sequence_loss_reference): the L1 term
+    // is valid * |d| over EVERY pixel, so a non-finite prediction (or gt) at an
+    // invalid pixel still poisons the loss (0 * NaN = NaN) and reaches the
+    // non-finite step guard; the metrics count valid pixels only.
+    const bool ok = loss_valid(gt, vin, p, max_flow);
+    const float vw = ok ? 1.f : 0.f;
     const float2 g = *(const float2*)(gt + 2 * p);
 #pragma unroll
     for (int i = 0; i < LOSS_MAX_N; ++i) {
       if (i < N) {
         const float2 f = *(const float2*)(pred + 2 * ((long)i * P + p));
-        acc[i] += fabsf(f.x - g.x) + fabsf(f.y - g.y);
-        if (i == N - 1) {
+        acc[i] += vw * (fabsf(f.x - g.x) + fabsf(f.y - g.y));
+        if (i == N - 1 && ok) {
           const float e = sqrtf((f.x - g.x) * (f.x - g.x) + (f.y - g.y) * (f.y - g.y));
           acc[LOSS_MAX_N] += e;
           acc[LOSS_MAX_N + 1] += e < 1.f ? 1.f : 0.f;
@@ -230,6 +235,8 @@ __global__ __launch_bounds__(256) void seq_loss_bwd_kernel(const float* __restri
     const long o = 2 * ((long)i * P + p);
     const float2 f = *(const float2*)(pred + o);
     const float s = v ? scale[i] : 0.f;
+    // s * sign(d) with torch's sign(NaN) = 0 (the oracle's abs backward gives 0 there;
+    // the NaN reaches the step guard through the loss value, seq_loss_kernel)
     const float dx = f.x > g.x ? s : (f.x < g.x ? -s : 0.f);
     const float dy = f.y > g.y ? s : (f.y < g.y ? -s : 0.f);
     *(float2*)(grad + o) = make_float2(dx, dy);

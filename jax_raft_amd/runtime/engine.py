@@ -44,6 +44,7 @@ from ..models.layers import (
     ResidualBlock,
 )
 from ..ops import native as nat
+from . import tunedb
 from ..ops.native import (
     ACT_NONE,
     ACT_RELU,
@@ -272,6 +273,8 @@ class RaftEngine:
         self.corr_dtype = corr_dtype
         self.autotune = autotune
         self._specs: Dict[str, ConvSpec] = {}
+        self.arch = tunedb.gpu_arch(self.device)
+        self.chosen_cfgs: Dict[str, Optional[int]] = {}   # conv spec name -> tile config of the last plan built
         self._sources: Dict[str, callable] = {}
         self._states: Dict[Tuple[int, int, int, int], _PlanState] = {}
         self._sig = None
@@ -503,12 +506,18 @@ class RaftEngine:
         if self.autotune and kw.get("cfg") is None:
             OH, OW = spec.out_hw(H, W)
             key = (N * OH * OW, spec.cout, spec.kh, spec.kw, spec.sh, spec.sw, spec.cin8, x.shape[-1],
-                   kw.get("epi", EPI_STD), kw.get("bmap") is not None, str(self.device))
-            cfg = _TUNE_CACHE.get(key)
+                   kw.get("epi", EPI_STD), kw.get("bmap") is not None)
+            cfg = _TUNE_CACHE.get(key + (str(self.device),))
             if cfg is None:
-                cfg = _tune(spec, x, N, H, W, y, kw)
-                _TUNE_CACHE[key] = cfg
+                cfg = tunedb.lookup(self.arch, key)   # persisted decision (runtime/tunedb.py)
+                if cfg is None:
+                    cfg = _tune(spec, x, N, H, W, y, kw)
+                    tunedb.record(self.arch, key, cfg)
+                _TUNE_CACHE[key + (str(self.device),)] = cfg
             kw = dict(kw, cfg=cfg)
+        name = next((k for k, v in self._specs.items() if v is spec), None)
+        if name is not None:
+            self.chosen_cfgs[name] = kw.get("cfg")
         plan.add_conv(*conv_args(spec, x, N, H, W, y, **kw))
 
     # ------------------------------------------------------------- lowering
@@ -1172,6 +1181,10 @@ class RaftEngine:
         ROCm.)  The result of each batch is bitwise equal to :meth:`forward`
         (tests/test_engine_gpu.py)."""
         if self._signature() != self._sig:
+            if self._pp is not None and self._pp["pending"] is not None:
+                # the pending batch's encoders + pyramid ran with the old weights; its loop
+                # would run with the new ones (a result matching neither forward)
+                raise RuntimeError("pipelined(): the weights changed while a batch is pending; flush() it first")
             self._pack()
         B, H, W, C = image1.shape
         assert C == 3, "images must be NHWC with 3 channels"

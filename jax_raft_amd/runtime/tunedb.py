@@ -1,0 +1,85 @@
+"""Persistent tile-config decisions of the implicit-GEMM conv autotuner.
+
+Every conv problem (pixels, channels, kernel, strides, channel strides,
+epilogue) picks one of the precompiled tile configs of ``conv_igemm.hip``.
+Timing ~25 configs per conv at plan build costs seconds per process -- on
+every rank of a multi-GPU job -- and a near-tie can flip between runs, so
+run-to-run results differ.  The decisions are therefore kept in a JSON file
+per GPU architecture shipped with the package (``tuned/<gfx>.json``),
+produced on the target hardware by ``tools/autotune_db.py``:
+
+* a hit returns the stored config (no timing);
+* a miss is timed once in-process (the caller's tuner) and remembered for
+  the process; ``save()`` writes the merged table back.
+
+``JR_TUNE=fresh`` ignores the file (re-times every problem, e.g. to refresh
+it); ``JR_TUNE=db`` (default) uses it.
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+from pathlib import Path
+from typing import Dict, Optional
+
+DB_DIR = Path(__file__).resolve().parent.parent / "tuned"
+_lock = threading.Lock()
+_tables: Dict[str, Dict[str, int]] = {}
+_stats = {"hits": 0, "misses": 0}
+
+
+def gpu_arch(device=None) -> str:
+    """'gfx950' for an MI355X (the gcnArchName without feature suffixes)."""
+    import torch
+
+    props = torch.cuda.get_device_properties(device if device is not None else torch.cuda.current_device())
+    return str(getattr(props, "gcnArchName", "unknown")).split(":")[0]
+
+
+def path(arch: str) -> Path:
+    return DB_DIR / f"{arch}.json"
+
+
+def _key(key) -> str:
+    return json.dumps([k if isinstance(k, (int, float, str, bool)) or k is None else str(k) for k in key],
+                      separators=(",", ":"))
+
+
+def _table(arch: str) -> Dict[str, int]:
+    with _lock:
+        t = _tables.get(arch)
+        if t is None:
+            t = {}
+            p = path(arch)
+            if os.environ.get("JR_TUNE", "db") != "fresh" and p.exists():
+                with open(p) as f:
+                    t = {k: int(v) for k, v in json.load(f).get("entries", {}).items()}
+            _tables[arch] = t
+        return t
+
+
+def lookup(arch: str, key) -> Optional[int]:
+    cfg = _table(arch).get(_key(key))
+    _stats["hits" if cfg is not None else "misses"] += 1
+    return cfg
+
+
+def record(arch: str, key, cfg: int) -> None:
+    _table(arch)[_key(key)] = int(cfg)
+
+
+def stats() -> Dict[str, int]:
+    return dict(_stats)
+
+
+def save(arch: str) -> Path:
+    """Write this process's table (file entries + new decisions) for ``arch``."""
+    t = _table(arch)
+    DB_DIR.mkdir(parents=True, exist_ok=True)
+    p = path(arch)
+    tmp = p.with_suffix(".json.tmp")
+    with open(tmp, "w") as f:
+        json.dump({"version": 1, "arch": arch, "entries": dict(sorted(t.items()))}, f, indent=0)
+    os.replace(tmp, p)
+    return p

@@ -37,6 +37,7 @@ followed by its backward before the next forward of the same loop (checked).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional
@@ -46,6 +47,7 @@ import torch
 from ..models.layers import FeatureEncoder
 from ..ops import native as nat
 from ..ops.native import ACT_NONE, ACT_RELU, EPI_GRU_A, EPI_GRU_B, EPI_STD, round_up
+from ..runtime import tunedb
 
 BF16, F32 = torch.bfloat16, torch.float32
 EPI_BWD = 5
@@ -184,9 +186,12 @@ def record_conv(plan, spec, x, N, H, W, y, *, tx=None, ix=None, extra=None, **kw
     output, so epilogues that accumulate into their buffers are never re-run."""
     x_coff = kw.get("x_coff", 0)
     OH, OW = (extra[0], extra[1]) if extra else spec.out_hw(H, W)
+    arch = tunedb.gpu_arch(x.device)
     key = ("train", N, H, W, OH, OW, spec.kh, spec.kw, spec.sh, spec.sw, spec.ph, spec.pw, spec.cin8, spec.cout,
-           x.shape[-1], tuple(extra) if extra else None, str(x.device))
-    cfg = _CFG_CACHE.get(key)
+           x.shape[-1], tuple(extra) if extra else None)
+    cfg = _CFG_CACHE.get(key + (str(x.device),))
+    if cfg is None:
+        cfg = tunedb.lookup(arch, key)   # persisted decision (runtime/tunedb.py)
     ops = nat.ops()
     if cfg is None:
         scratch = torch.empty(N * OH * OW, round_up(spec.cout, 8), dtype=BF16, device=x.device)
@@ -206,7 +211,8 @@ def record_conv(plan, spec, x, N, H, W, y, *, tx=None, ix=None, extra=None, **kw
             if best is None or el < best[0]:
                 best = (el, c)
         cfg = best[1]
-        _CFG_CACHE[key] = cfg
+        tunedb.record(arch, key, cfg)
+    _CFG_CACHE[key + (str(x.device),)] = cfg
     t, i, a = nat.conv_args(spec, x, N, H, W, y, cfg=cfg, **kw)
     if extra:
         if len(i) > 22:
@@ -923,7 +929,7 @@ class FusedModel:
         return self.loop.forward_prepared(self.loop.ctx_raw)
 
     def backward(self, gout, gen: int):
-        comm = _GRAD_COMM
+        comm = _ACTIVE_COMM.get(id(self.model))
         _, _, dctx, pgrads = self.loop.backward(gout, gen, fe_dy=self.fe.dy_out)
         if comm is not None:   # data parallel: the loop's gradients reduce while the encoders run backward
             comm.start(self.loop.last_snapshot)
@@ -962,7 +968,10 @@ class FusedRAFT(torch.autograd.Function):
 
 
 _LOOPS: Dict[tuple, object] = {}
-_GRAD_COMM = None
+# Gradient communicators of the models whose Trainer step is running: set only
+# inside :func:`grad_comm` (around one step's backward), keyed by the model, so a
+# backward outside a training step, or of another model, never starts a collective.
+_ACTIVE_COMM: Dict[int, object] = {}
 
 
 def _run_plan(plan, use_graph: bool) -> None:
@@ -979,11 +988,24 @@ def _run_plan(plan, use_graph: bool) -> None:
         plan.run(0)
 
 
-def set_grad_comm(comm) -> None:
-    """Register a flat-buffer gradient communicator (``parallel.dp.FlatGradComm``)
-    used by the whole-model fused step; ``None`` disables it."""
-    global _GRAD_COMM
-    _GRAD_COMM = comm
+@contextlib.contextmanager
+def grad_comm(model, comm):
+    """Within this block, the whole-model fused backward of ``model`` all-reduces
+    its flat gradient arenas through ``comm`` (``parallel.dp.FlatGradComm``) as
+    they are produced.  ``comm=None`` is a no-op.  The registration is per model
+    and ends with the block (the Trainer wraps each step's backward in it)."""
+    if comm is None:
+        yield
+        return
+    prev = _ACTIVE_COMM.get(id(model))
+    _ACTIVE_COMM[id(model)] = comm
+    try:
+        yield
+    finally:
+        if prev is None:
+            _ACTIVE_COMM.pop(id(model), None)
+        else:
+            _ACTIVE_COMM[id(model)] = prev
 
 
 def enabled() -> bool:
@@ -1001,14 +1023,34 @@ def full_model_ok(model, train: bool) -> bool:
     return os.environ.get("JR_FUSED_ENCODERS", "1") != "0"
 
 
+def _tensor_sig(model) -> tuple:
+    """Identity + storage of every parameter and buffer the module tree holds
+    RIGHT NOW.  The plans pack / differentiate / update the tensors they were
+    recorded with, so any swap -- ``torch.func.functional_call`` (the Flax-style
+    ``RAFT.apply`` with foreign variables), a new ``nn.Parameter``, ``p.data =
+    ...``, ``.to()`` -- must rebuild them.  (Comparing the recorded tensors with
+    their own pointers cannot see a swap: they are still alive and unchanged.)"""
+    sig = []
+    for mod in model.modules():
+        for t in mod._parameters.values():
+            if t is not None:
+                sig.append((id(t), t.data_ptr()))
+        for t in mod._buffers.values():
+            if t is not None:
+                sig.append((id(t), t.data_ptr()))
+    return tuple(sig)
+
+
 def _cached(kind, model, B, H, W, T, device):
     key = (kind, id(model), B, H, W, T, str(device))
     obj = _LOOPS.get(key)
-    if obj is None or obj.model is not model or obj.stale():
+    sig = _tensor_sig(model)
+    if obj is None or obj.model is not model or getattr(obj, "_sig", None) != sig or obj.stale():
         for k in [k for k, v in _LOOPS.items() if k[1] == id(model)]:
             del _LOOPS[k]   # one plan set per model: drop other shapes / kinds
         g = os.environ.get("JR_FUSED_GRAPH", "1") != "0"
         obj = (FusedModel if kind == "model" else FusedLoop)(model, B, H, W, T, device, use_graph=g)
+        obj._sig = sig
         _LOOPS[key] = obj
     return obj
 

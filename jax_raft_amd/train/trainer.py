@@ -99,10 +99,6 @@ class Trainer:
             dp.convert_sync_batchnorm(self.model)
         self.flat_comm = dp.FlatGradComm() if self.world > 1 else None
         self.sync = dp.GradAllReducer(self.model, bucket_mb=cfg.bucket_mb, flat_comm=self.flat_comm)
-        if self.flat_comm is not None and self.device.type == "cuda":
-            from . import fused
-
-            fused.set_grad_comm(self.flat_comm)
         self._graph_ok = (cfg.graph_step and self.device.type == "cuda" and self.world == 1
                           and os.environ.get("JR_GRAPH_STEP", "1") != "0")
         self.opt = _adamw(self.model.parameters(), cfg, self.device, capturable=self._graph_ok)
@@ -159,7 +155,8 @@ class Trainer:
             img1, img2, flow, valid = self._static_in
             preds = self.model(img1, img2, train=not cfg.freeze_bn, num_flow_updates=cfg.iters, autograd=True)
             loss, metrics = sequence_loss(preds, flow, valid, cfg.gamma, cfg.max_flow)
-            loss.backward()
+            with self._comm():
+                loss.backward()
             gnorm = torch.nn.utils.clip_grad_norm_(self.model.parameters(), cfg.clip)
             bad = (~torch.isfinite(gnorm)).float()
             if cfg.skip_nonfinite:
@@ -180,7 +177,8 @@ class Trainer:
         loss, metrics = sequence_loss(preds, flow, valid, cfg.gamma, cfg.max_flow)
         if self.step + 1 == cfg.fault_nan_step:
             loss = loss * float("nan")
-        loss.backward()
+        with self._comm():
+            loss.backward()
         self.sync.finish()
         gnorm = torch.nn.utils.clip_grad_norm_(self.model.parameters(), cfg.clip)
         # Failure detection: the gradient is all-reduced, so every rank sees the
@@ -212,6 +210,13 @@ class Trainer:
         self.step += 1
         out = {"loss": loss.detach(), "grad_norm": gnorm.detach(), **{k: v.detach() for k, v in metrics.items()}}
         return out
+
+    def _comm(self):
+        """The fused native backward's flat-arena all-reduce, registered for
+        this model only while its step's backward runs (train/fused.py:grad_comm)."""
+        from . import fused
+
+        return fused.grad_comm(self.model, self.flat_comm if self.device.type == "cuda" else None)
 
     def _async_skip(self) -> bool:
         return self.device.type == "cuda" and bool(getattr(self.opt, "defaults", {}).get("fused"))

@@ -72,6 +72,18 @@ def test_mpi_sintel_and_validate_cpu(tmp_path):
         assert r["pairs"] == 4 and np.isfinite(r["epe"]) and 0 <= r["1px"] <= r["3px"] <= r["5px"] <= 1
 
 
+def test_validate_batched_equals_per_pair(tmp_path):
+    """batch_size > 1 (a partial last batch included) gives the per-pair metrics."""
+    _make_sintel(str(tmp_path), scenes=2, frames=3)
+    model, _ = raft_small()
+    kw = dict(iters=2, device=torch.device("cpu"), verbose=False, dstypes=("clean",))
+    r1 = validate_sintel(model, str(tmp_path), batch_size=1, **kw)["clean"]
+    r3 = validate_sintel(model, str(tmp_path), batch_size=3, **kw)["clean"]
+    assert r3["batch_size"] == 3 and r3["pairs"] == r1["pairs"] == 4
+    for k in ("epe", "1px", "3px", "5px"):
+        assert abs(r1[k] - r3[k]) < 1e-5 * max(1.0, abs(r1[k])), k
+
+
 def test_flow_to_color():
     img = flow_to_color(np.random.default_rng(2).normal(size=(5, 6, 2)))
     assert img.shape == (5, 6, 3) and img.dtype == np.uint8

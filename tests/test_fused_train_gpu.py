@@ -210,6 +210,73 @@ def test_native_sequence_loss(with_valid):
     assert _rel(pg.grad, pr.grad) < 1e-5
 
 
+def test_fused_plans_follow_swapped_parameters():
+    """``RAFT.apply`` with foreign variables (``torch.func.functional_call``) on
+    the fused training path runs and differentiates THOSE leaves, not the
+    plans cached for the module's own weights; an ordinary step afterwards
+    runs the module's own weights again (fused.py:_tensor_sig)."""
+    from jax_raft_amd.train import fused as F
+    from jax_raft_amd.utils import checkpoint as ckpt
+
+    F._LOOPS.clear()
+    model, i1, i2, target = _setup(raft_small, B=1, seed=21)
+    i1, i2, tg = i1.cuda(), i2.cuda(), target.cuda()
+
+    def step(fn):
+        out = fn()
+        (out.float() - tg).abs().mean().backward()
+        torch.cuda.synchronize()
+        return out.detach().clone()
+
+    model.zero_grad(set_to_none=True)
+    o_own = step(lambda: model(i1, i2, train=True, num_flow_updates=2))
+    g_own = {n: p.grad.clone() for n, p in model.named_parameters()}
+    other = raft_small(seed=1)[0].cuda().train()
+    fv = ckpt.variables_from_module(other)          # differentiable CUDA leaves of another init
+    o_app = step(lambda: model.apply(fv, i1, i2, train=True, num_flow_updates=2))
+    g_app = {n: p.grad.clone() for n, p in other.named_parameters()}
+    other.zero_grad(set_to_none=True)
+    o_oth = step(lambda: other(i1, i2, train=True, num_flow_updates=2))
+    assert torch.equal(o_app, o_oth) and not torch.equal(o_app, o_own)
+    for n, p in other.named_parameters():
+        assert torch.equal(g_app[n], p.grad), n
+    model.zero_grad(set_to_none=True)
+    o_again = step(lambda: model(i1, i2, train=True, num_flow_updates=2))
+    assert torch.equal(o_again, o_own)
+    for n, p in model.named_parameters():
+        assert torch.equal(g_own[n], p.grad), n
+
+
+@pytest.mark.parametrize("where", ["valid", "invalid"])
+def test_native_sequence_loss_nonfinite(where):
+    """A NaN prediction poisons the native loss as it does the PyTorch
+    oracle's -- also at a pixel the valid mask excludes (0 * NaN = NaN), so the
+    trainer's non-finite step guard sees it -- and the gradients agree (the
+    oracle's abs backward uses sign(NaN) = 0)."""
+    from jax_raft_amd.train.loss import sequence_loss, sequence_loss_reference
+
+    torch.manual_seed(12)
+    N, B, H, W = 3, 1, 16, 24
+    preds = torch.randn(N, B, H, W, 2)
+    gt = torch.randn(B, H, W, 2)
+    valid = torch.ones(B, H, W)
+    valid[0, 3, 5] = 0.0
+    y, x = (3, 5) if where == "invalid" else (7, 9)
+    preds[1, 0, y, x, 0] = float("nan")
+    pr = preds.clone().requires_grad_(True)
+    lr, _ = sequence_loss_reference(pr, gt, valid)
+    lr.backward()
+    pg = preds.cuda().requires_grad_(True)
+    lg, _ = sequence_loss(pg, gt.cuda(), valid.cuda())
+    lg.backward()
+    torch.cuda.synchronize()
+    assert torch.isnan(lr) and torch.isnan(lg.cpu())
+    gg = pg.grad.cpu()
+    assert torch.equal(torch.isnan(gg), torch.isnan(pr.grad))
+    fin = ~torch.isnan(pr.grad)
+    assert torch.allclose(gg[fin], pr.grad[fin], rtol=1e-5, atol=1e-12)
+
+
 @pytest.mark.parametrize("factory", [raft_large, raft_small])
 def test_native_pack_table_matches_python_packing(factory):
     """The one-launch weight repack of the training plans reproduces the
