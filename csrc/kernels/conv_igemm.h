@@ -20,8 +20,8 @@
 //    stage).  LDS rows are 128 B with XOR swizzles chosen so that the
 //    ds_read_b128 fragment reads of both operands are bank-conflict free.
 //  * Fused epilogues: bias, residual, activation (incl. the context-encoder
-//    tanh/relu split), scaling, dual stores into concat buffers, and the
-//    ConvGRU gate/blend and flow-head coordinate update of the RAFT loop.
+//    tanh/relu split), scaling, dual stores into concat buffers, the
+//    ConvGRU gate/blend of the RAFT loop and the FlowHead taps (EPI_TAPS).
 #pragma once
 #include <type_traits>
 
@@ -265,38 +265,6 @@ JR_DEVICE void epi_pixel(const ConvParams& p, float (&v)[NV], int m, int cbase) 
         for (int j = 0; j < NV; ++j) if (cbase + j < p.split) hp[j] = v[j];
       }
     }
-  } else if constexpr (EPI == EPI_CONVEX) {
-    // Fused MaskPredictor 1x1 conv + convex x8 upsampling (model.py:85-98, :394-400):
-    // this lane holds the 9 neighbour logits of sub-pixel s = cbase / 16 of pixel m.
-    if constexpr (NV == 16) {
-      const int OHW = p.OH * p.OW;
-      const int b = m / OHW, rem = m - b * OHW;
-      const int y = rem / p.OW, x = rem - y * p.OW;
-      const int s = cbase >> 4;
-      float mx = -3.0e38f;
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        v[k] *= p.alpha;
-        mx = fmaxf(mx, v[k]);
-      }
-      float sum = 0.f, ux = 0.f, uy = 0.f;
-      const float* fb = p.flow32 + 2L * b * OHW;
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        const int yy = y + k / 3 - 1, xx = x + k % 3 - 1;
-        const float e = __expf(v[k] - mx);
-        sum += e;
-        if ((unsigned)yy < (unsigned)p.OH && (unsigned)xx < (unsigned)p.OW) {
-          const float2 f = *(const float2*)(fb + 2 * (yy * p.OW + xx));
-          ux += e * f.x;
-          uy += e * f.y;
-        }
-      }
-      const float inv = 8.0f / sum;
-      const long W8 = 8L * p.OW;
-      float* op = (float*)p.y + 2 * (((long)b * 8 * p.OH + 8 * y + (s >> 3)) * W8 + 8 * x + (s & 7));
-      *(float2*)op = make_float2(ux * inv, uy * inv);
-    }
   } else if constexpr (EPI == EPI_GRU_A) {
     // [z | r] logits -> z (fp32 / bf16) and r*h (bf16) into the q-input buffer.
     // h comes from the fp32 state when given, else from the conv's own bf16
@@ -337,30 +305,6 @@ JR_DEVICE void epi_pixel(const ConvParams& p, float (&v)[NV], int m, int cbase) 
     store_f32<NV>(hp, v);
     store_bf16<NV>((bf16*)p.y + (long)m * p.y_cstride + p.y_coff + cbase, v);
     if (p.y2) store_bf16<NV>((bf16*)p.y2 + (long)m * p.y2_cstride + p.y2_coff + cbase, v);
-  } else if constexpr (EPI == EPI_FLOW) {
-    if (cbase == 0) {
-      const int rem = m % OHW;
-      const int py = rem / p.OW;
-      const int px = rem - py * p.OW;
-      const float cx = p.coords[2 * (long)m] + v[0];
-      const float cy = p.coords[2 * (long)m + 1] + v[1];
-      p.coords[2 * (long)m] = cx;
-      p.coords[2 * (long)m + 1] = cy;
-      const float fx = cx - (float)px;
-      const float fy = cy - (float)py;
-      p.flow32[2 * (long)m] = fx;
-      p.flow32[2 * (long)m + 1] = fy;
-      bf16* yp = (bf16*)p.y + (long)m * p.y_cstride + p.y_coff;
-      yp[0] = f2bf(fx); yp[1] = f2bf(fy);
-      if (p.y2) {
-        bf16* y2p = (bf16*)p.y2 + (long)m * p.y2_cstride + p.y2_coff;
-        y2p[0] = f2bf(fx); y2p[1] = f2bf(fy);
-      }
-      if (p.y3) {
-        bf16* y3p = (bf16*)p.y3 + (long)m * p.y3_cstride + p.y3_coff;
-        y3p[0] = f2bf(fx); y3p[1] = f2bf(fy);
-      }
-    }
   } else if constexpr (EPI == EPI_BWD) {
     epi_bwd<NV>(p, v, m, cbase);
   }
@@ -1258,8 +1202,6 @@ int launch_cfg(const ConvParams* p, int epi, hipStream_t s) {
     case EPI_STD: JR_LAUNCH(EPI_STD) break;
     case EPI_GRU_A: JR_LAUNCH(EPI_GRU_A) break;
     case EPI_GRU_B: JR_LAUNCH(EPI_GRU_B) break;
-    case EPI_FLOW: JR_LAUNCH(EPI_FLOW) break;
-    case EPI_CONVEX: JR_LAUNCH(EPI_CONVEX) break;
     case EPI_BWD: JR_LAUNCH(EPI_BWD) break;
     case EPI_TAPS:
       // one N tile of 256 channels, 16 waves of 64 x 32 (configs 22, 34, 35, 38)

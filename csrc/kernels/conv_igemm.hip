@@ -8,11 +8,9 @@ extern "C" int jr_conv_family_p(const ConvParams* p, int cfg, int epi, hipStream
 extern "C" int jr_conv_family_m32(const ConvParams* p, int cfg, int epi, hipStream_t stream);
 extern "C" int jr_conv_family_d2(const ConvParams* p, int cfg, int epi, hipStream_t stream);
 extern "C" int jr_conv_family_g(const ConvParams* p, int cfg, int epi, hipStream_t stream);
-extern "C" int jr_conv_halo(const ConvParams* p, int epi, hipStream_t stream);
 
 extern "C" int jr_conv_forward(const ConvParams* p, int cfg, int epi, hipStream_t stream) {
   if (p->M <= 0) return 0;
-  if (cfg == 44) return jr_conv_halo(p, epi, stream);  // conv_halo.hip (3x3 halo-tiled)
   int r = jr_conv_family_r(p, cfg, epi, stream);
   if (r == -1) r = jr_conv_family_rw(p, cfg, epi, stream);
   if (r == -1) r = jr_conv_family_p(p, cfg, epi, stream);

@@ -16,10 +16,8 @@ enum ConvEpi : int {
   EPI_STD = 0,    // bias (+residual) -> act -> *alpha -> store (bf16|fp32) (+copy)
   EPI_GRU_A = 1,  // channels [0,Hd): z = sigmoid -> zbuf ; [Hd,2Hd): r = sigmoid -> rh = r*h32 -> y
   EPI_GRU_B = 2,  // q = tanh ; h = (1-z) h + z q -> h32, y (bf16 copy of h), y2 (second copy)
-  EPI_FLOW = 3,   // delta = acc+bias (2 ch): coords += delta ; flow = coords - coords0 -> flow32, y/y2 (bf16)
-  EPI_CONVEX = 4, // mask logits in subpixel-major order (channel s*16 + k, k < 9 real): *alpha -> softmax
-                  // over the 9 neighbours -> convex combination of 8*flow32 at the 3x3 neighbours ->
-                  // fp32 upsampled flow written straight into y = out[B][8 OH][8 OW][2]
+  // 3, 4: retired (the 3x3 flow-head conv epilogue and the EPI_CONVEX mask-head epilogue,
+  //       superseded by EPI_TAPS + the update fused into the lookup, and convex_head.hip)
   EPI_BWD = 5,    // data-gradient conv of the training loop's backward (no bias): channels
                   // [0, hidden) -> seg[0], [hidden, cout) -> seg[1] (see BwdSeg)
   EPI_TAPS = 6,   // FlowHead conv1 (256 channels, bias + act) -> its features never leave the CU:
@@ -152,6 +150,15 @@ int jr_corr_lookup(const void* const* levels, int num_levels, int B, int h, int 
                    const float* coords, void* out, int out_cstride, int lv_bf16, int blocked, hipStream_t stream,
                    const TapsUpd* upd = nullptr);
 
+// Fused lookup + MotionEncoder.convcorr1 (1x1 conv + ReLU): the lookup's
+// features stay in LDS as the GEMM operand.  Levels bf16 (wide-lookup layout),
+// nq == h * w, radius 3 / 4 with kpad = 224 / 352 (L = 4) and cout = 256;
+// weights packed by ops/native.py:pack_conv1x1(kernel, kpad); y bf16 channels
+// [y_coff, y_coff + 256) of [B*h*w][y_cstride].  upd: as jr_corr_lookup.
+int jr_lookup_cc1(const void* const* levels, int num_levels, int B, int h, int w, int radius, const float* coords,
+                  int blocked, const void* wpk, int kpad, const float* bias, void* y, int y_cstride, int y_coff,
+                  int cout, hipStream_t stream, const TapsUpd* upd = nullptr);
+
 // Backward of jr_corr_lookup w.r.t. the levels: accumulates into fp32 dlevels
 // (same shapes as the levels).  gout: bf16 (g_bf16=1) or fp32 [B*nq][gcs].
 int jr_corr_lookup_bwd(void* const* dlevels, int num_levels, int B, int h, int w, int nq, int radius,
@@ -255,14 +262,9 @@ int jr_im2col(const void* x, int N, int H, int W, int x_cstride, int x_coff, int
               int SH, int SW, int PH, int PW, int OH, int OW, int kpad, void* col, hipStream_t stream);
 // copy bf16 channel slice: dst[m][doff + c] = src[m][soff + c], c < C
 int jr_zero_fill(void* p, long bytes, hipStream_t stream);
-// Flow-head conv2 (3x3, cin -> 2, cin in {128, 256}) fused with the coordinate update
-// (flowhead.hip): fm bf16 [N*h*w][fcs] (channels [0, cin) used), wt bf16 [2][9][cin]
-// (output, tap kh*3+kw, channel).
-int jr_flow_head(const void* fm, int fcs, const void* wt, const float* bias, int N, int h, int w, int cin,
-                 float* coords, float* flow32, void* hx, int hx_cs, int hx_off, void* qx, int qx_cs, int qx_off,
-                 void* f8, int f8_cs, hipStream_t stream);
 // delta(p) = bias + sum of the 9 shifted per-tap partials t[p + d][tap] ([M][tcs] fp32,
-// tap-major pairs), then the EPI_FLOW coordinate / flow update (flowhead.hip)
+// tap-major pairs), then the coordinate / flow update (flowhead.hip): coords += delta,
+// flow = coords - coords0 -> flow32 (fp32) and bf16 copies into hx / qx / f8
 // Pointwise conv with LDS-resident weights (conv1x1.hip): y[m][y_coff + co] =
 // act(x[m][0 .. kvalid) . W + bias) for co < cout (cout % 64 == 0), weights
 // packed by ops/native.py:pack_conv1x1 with K padded to kpad (128 / 256 / 352 / 384).

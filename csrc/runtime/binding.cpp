@@ -74,17 +74,14 @@ static void conv_train_extras(ConvParams& p, int epi, const TList& tx, const ILi
 
 static Launch make_conv(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep,
                         const TList* tx = nullptr, const IList* ix = nullptr) {
-  TORCH_CHECK(i.size() == 22 || i.size() == 26 || i.size() == 27 || i.size() == 28,
-              "conv: expected 22, 26, 27 or 28 ints");
+  TORCH_CHECK(i.size() == 22 || i.size() == 26 || i.size() == 27, "conv: expected 22, 26 or 27 ints");
   at::Tensor x = opt(t, 0), w = opt(t, 1), bias = opt(t, 2), y = opt(t, 3), y2 = opt(t, 4), res = opt(t, 5);
   at::Tensor h32 = opt(t, 6), zbuf = opt(t, 7), coords = opt(t, 8), flow32 = opt(t, 9), y3 = opt(t, 10);
   at::Tensor bmap = opt(t, 11), tapw;
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_f32(bias, "bias");
-  // EPI_CONVEX writes a (B, 8h, 8w, 2) block of the flows output, which may be a per-part
-  // view (engine split mode) -- check_flow_out validates that block; all else is dense
-  TORCH_CHECK(y.defined() && ((int)i[19] == EPI_CONVEX || y.is_contiguous()), "conv: y must be contiguous");
+  TORCH_CHECK(y.defined() && y.is_contiguous(), "conv: y must be contiguous");
   ConvParams p{};
   p.x = x.data_ptr();
   p.N = (int)i[0]; p.H = (int)i[1]; p.W = (int)i[2];
@@ -116,7 +113,6 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   p.bmap = ptr(bmap);
   p.bmap_cstride = bmap.defined() ? cs(bmap) : 0;
   p.bmap_coff = i.size() >= 27 ? (int)i[26] : 0;
-  const int64_t it_stride = i.size() >= 28 ? i[27] : 0;  // EPI_CONVEX: output floats per loop iteration
   p.bmap_bf16 = bmap.defined() && bmap.scalar_type() == at::kBFloat16;
   p.z_bf16 = zbuf.defined() && zbuf.scalar_type() == at::kBFloat16;
   if (bmap.defined()) {
@@ -150,13 +146,8 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   TORCH_CHECK(p.kpad % 64 == 0 && p.kpad >= p.KH * p.KW * p.cin8, "conv: packed weight K mismatch");
   TORCH_CHECK(p.cout_pad % 64 == 0 && p.cout_pad >= p.cout && bias.numel() >= p.cout, "conv: packed weight rows (64-row groups)");
   TORCH_CHECK(p.OH > 0 && p.OW > 0, "conv: empty output");
-  int64_t out_cap = 0;
-  if (epi == EPI_CONVEX) {
-    out_cap = check_flow_out(y, p.N, p.OH, p.OW);
-  } else {
-    TORCH_CHECK(p.y_cstride % 8 == 0, "conv: output channel stride must be a multiple of 8");
-    TORCH_CHECK((int64_t)p.M * p.y_cstride <= y.numel(), "conv: output tensor too small");
-  }
+  TORCH_CHECK(p.y_cstride % 8 == 0, "conv: output channel stride must be a multiple of 8");
+  TORCH_CHECK((int64_t)p.M * p.y_cstride <= y.numel(), "conv: output tensor too small");
   if (epi == EPI_STD) {
     TORCH_CHECK(p.y_coff % 8 == 0 && p.y_coff + p.cout <= p.y_cstride, "conv: output slice");
     TORCH_CHECK(y.scalar_type() == at::kBFloat16 || y.scalar_type() == at::kFloat, "conv: output dtype");
@@ -181,9 +172,6 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
     TORCH_CHECK(p.cout == p.hidden && p.hidden % 16 == 0, "GRU-B: cout must be hidden");
     TORCH_CHECK(p.y_coff % 8 == 0, "GRU-B align");
     if (y2.defined()) { check_bf16(y2, "y2"); TORCH_CHECK(p.y2_coff % 8 == 0, "y2 align"); }
-  } else if (epi == EPI_FLOW) {
-    check_f32(coords, "coords"); check_f32(flow32, "flow32"); check_bf16(y, "y");
-    TORCH_CHECK(p.cout == 2, "FLOW: cout must be 2");
   } else if (epi == EPI_BWD) {
     TORCH_CHECK(tx != nullptr, "EPI_BWD needs the training operands (conv_train)");
     TORCH_CHECK(!bmap.defined() && !res.defined(), "EPI_BWD: no bias map / residual");
@@ -200,31 +188,12 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
     TORCH_CHECK(cfg == 22 || cfg == 34 || cfg == 35 || cfg == 38, "TAPS: tile config ", cfg,
                 " is not a 256-channel 16-wave 64x32 tiling");
     p.tapw = tapw.data_ptr();
-  } else if (epi == EPI_CONVEX) {
-    check_f32(flow32, "flow32");
-    TORCH_CHECK(flow32.numel() >= (int64_t)p.M * 2, "CONVEX: flow32 must be [M][2]");
-    TORCH_CHECK(p.cout % 16 == 0 && p.cout >= 16 && p.act == 0 /* ACT_NONE */ && !bmap.defined(),
-                "CONVEX: logits in 16-channel sub-pixel groups, no activation / bias map");
-    // the epilogue needs 16 contiguous channels per lane: every config but the 16- / 32-row wave tiles
-    TORCH_CHECK(cfg != 3 && cfg != 5 && cfg != 19 && cfg != 21 && cfg != 36, "CONVEX: tile config ", cfg,
-                " has < 16 channels per lane");
-    TORCH_CHECK(it_stride >= 0, "CONVEX: iteration stride");
   } else {
     TORCH_CHECK(false, "conv: unknown epilogue ", epi);
   }
-  TORCH_CHECK(cfg >= 0 && cfg <= 44 && !(cfg >= 29 && cfg <= 32), "conv: unknown tile config ", cfg);
+  TORCH_CHECK(cfg >= 0 && cfg <= 43 && !(cfg >= 29 && cfg <= 32), "conv: unknown tile config ", cfg);
   if (tx) conv_train_extras(p, epi, *tx, *ix, keep);
   if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3, bmap, tapw}) if (v.defined()) keep->push_back(v);
-  if (epi == EPI_CONVEX) {
-    const int64_t need = (int64_t)p.N * 64 * p.OH * p.OW * 2;
-    return [p, epi, cfg, it_stride, out_cap, need](hipStream_t s, int it) {
-      const int64_t off = it_stride * it;
-      if (off + need > out_cap) return (int)hipErrorInvalidValue;
-      ConvParams q = p;
-      q.y = (float*)p.y + off;
-      return jr_conv_forward(&q, cfg, epi, s);
-    };
-  }
   return [p, epi, cfg](hipStream_t s, int) { return jr_conv_forward(&p, cfg, epi, s); };
 }
 
@@ -565,38 +534,6 @@ static Launch make_conv_direct(const TList& t, const IList& i, std::vector<at::T
 // ------------------------------------------------------------------ flow head
 // t = [fm, wt (bf16 [2][9][cin]), bias (fp32 [2]), coords, flow32, hx, qx?, flow8?]
 // i = [N, h, w, cin, fm_coff, hx_off, qx_off]
-static Launch make_flow_head(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
-  at::Tensor fm = opt(t, 0), wt = opt(t, 1), bias = opt(t, 2), coords = opt(t, 3), flow32 = opt(t, 4), hx = opt(t, 5),
-             qx = opt(t, 6), f8 = opt(t, 7);
-  TORCH_CHECK(i.size() == 7, "flow_head: expected 7 ints");
-  check_bf16(fm, "fm"); check_bf16(wt, "wt"); check_f32(bias, "bias"); check_f32(coords, "coords");
-  check_f32(flow32, "flow32"); check_bf16(hx, "hx");
-  const int N = (int)i[0], h = (int)i[1], w = (int)i[2], cin = (int)i[3], coff = (int)i[4];
-  const int hx_off = (int)i[5], qx_off = (int)i[6];
-  const int64_t M = (int64_t)N * h * w;
-  TORCH_CHECK(cin == 128 || cin == 256, "flow_head: cin must be 128 or 256");
-  TORCH_CHECK(wt.numel() == 9 * cin * 2 && bias.numel() >= 2, "flow_head: weight shape");
-  TORCH_CHECK(cs(fm) % 8 == 0 && coff % 8 == 0 && coff + cin <= cs(fm) && fm.numel() >= M * cs(fm), "flow_head: fm");
-  TORCH_CHECK(coords.numel() >= 2 * M && flow32.numel() >= 2 * M, "flow_head: coords / flow32");
-  TORCH_CHECK(hx.numel() >= M * cs(hx) && hx_off + 2 <= cs(hx), "flow_head: hx");
-  if (qx.defined()) { check_bf16(qx, "qx"); TORCH_CHECK(qx.numel() >= M * cs(qx) && qx_off + 2 <= cs(qx), "flow_head: qx"); }
-  if (f8.defined()) { check_bf16(f8, "flow8"); TORCH_CHECK(f8.numel() >= M * cs(f8) && cs(f8) >= 2, "flow_head: flow8"); }
-  if (keep) for (auto& v : {fm, wt, bias, coords, flow32, hx, qx, f8}) if (v.defined()) keep->push_back(v);
-  const void* fp = (const char*)fm.data_ptr() + 2 * (int64_t)coff;
-  const void* wp = wt.data_ptr();
-  const float* bp = bias.data_ptr<float>();
-  float* cp = coords.data_ptr<float>();
-  float* f32p = flow32.data_ptr<float>();
-  void* hp = hx.data_ptr();
-  void* qp = ptr(qx);
-  void* f8p = ptr(f8);
-  const int fcs = cs(fm), hcs = cs(hx), qcs = qx.defined() ? cs(qx) : 0, f8cs = f8.defined() ? cs(f8) : 0;
-  return [=](hipStream_t s, int) {
-    return jr_flow_head(fp, fcs, wp, bp, N, h, w, cin, cp, f32p, hp, hcs, hx_off, qp, qcs, qx_off, f8p, f8cs, s);
-  };
-}
-
-// --------------------------------------------------------------- correlation
 // t = [f1, f2, l0, l1, l2, l3], i = [B, h, w, C, num_levels]; levels all fp32 or all bf16
 static void check_level(const at::Tensor& v, at::ScalarType dt) {
   TORCH_CHECK(v.defined() && v.is_cuda() && v.is_contiguous(), "pyramid level must be a contiguous GPU tensor");
@@ -699,6 +636,63 @@ static Launch make_lookup(const TList& t, const IList& i, std::vector<at::Tensor
     TapsUpd u = upd;
     u.on = upd.on && it > 0;
     return jr_corr_lookup(lv.data(), L, B, h, w, nq, r, cp, op, ocs, lbf, blocked, s, &u);
+  };
+}
+
+// Fused lookup + convcorr1 (jr_lookup_cc1):
+// t = [coords, y, l0, l1, l2, l3, wpk, bias, (taps, fbias, flow32, hx, qx?, flow8?)],
+// i = [num_levels, B, h, w, radius, blocked, kpad, cout, y_coff, (hx_off, qx_off)]
+static Launch make_lookup_cc1(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor coords = opt(t, 0), y = opt(t, 1), wpk = opt(t, 6), bias = opt(t, 7);
+  check_f32(coords, "coords"); check_bf16(y, "y"); check_bf16(wpk, "wpk"); check_f32(bias, "bias");
+  TORCH_CHECK(i.size() == 9 || i.size() == 11, "lookup_cc1: expected 9 or 11 ints");
+  const int L = (int)i[0], B = (int)i[1], h = (int)i[2], w = (int)i[3], r = (int)i[4], blocked = (int)i[5];
+  const int kpad = (int)i[6], cout = (int)i[7], y_coff = (int)i[8];
+  const int S = 2 * r + 1, nty = (h + 7) / 8, ntx = (w + 15) / 16;
+  const int64_t M = (int64_t)B * h * w;
+  TORCH_CHECK(L >= 1 && L <= 4 && (r == 3 || r == 4), "lookup_cc1: radius 3 / 4, 1..4 levels");
+  TORCH_CHECK(cout == 256 && kpad % 32 == 0 && kpad >= L * S * S && kpad - L * S * S < 32 &&
+                  wpk.numel() == (int64_t)kpad * cout && bias.numel() >= cout, "lookup_cc1: packed weights / bias");
+  TORCH_CHECK(cs(y) % 8 == 0 && y_coff % 8 == 0 && y_coff + cout <= cs(y) && y.numel() >= M * cs(y), "lookup_cc1: y");
+  TORCH_CHECK(coords.numel() >= 2 * M, "lookup_cc1: coords");
+  std::vector<const void*> lv(4, nullptr);
+  int hl = h, wl = w;
+  for (int l = 0; l < L; ++l) {
+    at::Tensor v = opt(t, 2 + l);
+    check_level(v, at::kBFloat16);
+    TORCH_CHECK(hl >= 2 && wl >= 2, "lookup_cc1: pyramid level too small");
+    const int64_t per_q = (blocked && l < 2) ? (int64_t)nty * ntx * (128 >> (2 * l)) : (int64_t)hl * wl;
+    TORCH_CHECK(v.numel() >= M * per_q, "lookup_cc1: level size");
+    lv[l] = v.data_ptr();
+    if (keep) keep->push_back(v);
+    hl >>= 1; wl >>= 1;
+  }
+  if (keep) for (auto& v : {coords, y, wpk, bias}) keep->push_back(v);
+  TapsUpd upd{};
+  at::Tensor tp = opt(t, 8);
+  if (tp.defined()) {
+    at::Tensor fb = opt(t, 9), f32 = opt(t, 10), hx = opt(t, 11), qx = opt(t, 12), f8 = opt(t, 13);
+    TORCH_CHECK(i.size() == 11, "lookup_cc1: the fused flow update needs [.., hx_off, qx_off]");
+    check_f32(tp, "taps"); check_f32(fb, "bias"); check_f32(f32, "flow32"); check_bf16(hx, "hx");
+    const int hx_off = (int)i[9], qx_off = (int)i[10];
+    TORCH_CHECK(cs(tp) >= 18 && tp.numel() >= M * cs(tp) && fb.numel() >= 2 && f32.numel() >= 2 * M,
+                "lookup_cc1: taps [M][>=18], bias [2], flow32 [M][2]");
+    TORCH_CHECK(hx.numel() >= M * cs(hx) && hx_off + 2 <= cs(hx), "lookup_cc1: hx");
+    if (qx.defined()) { check_bf16(qx, "qx"); TORCH_CHECK(qx.numel() >= M * cs(qx) && qx_off + 2 <= cs(qx), "lookup_cc1: qx"); }
+    if (f8.defined()) { check_bf16(f8, "flow8"); TORCH_CHECK(f8.numel() >= M * cs(f8) && cs(f8) >= 2, "lookup_cc1: flow8"); }
+    upd = TapsUpd{tp.data_ptr<float>(), cs(tp), fb.data_ptr<float>(), coords.data_ptr<float>(), f32.data_ptr<float>(),
+                  hx.data_ptr(), cs(hx), hx_off, ptr(qx), cs(qx), qx_off, ptr(f8), cs(f8), 1};
+    if (keep) for (auto& v : {tp, fb, f32, hx, qx, f8}) if (v.defined()) keep->push_back(v);
+  }
+  const float* cp = coords.data_ptr<float>();
+  void* yp = y.data_ptr();
+  const void* wp = wpk.data_ptr();
+  const float* bp = bias.data_ptr<float>();
+  const int ycs = cs(y);
+  return [=](hipStream_t s, int it) {
+    TapsUpd u = upd;
+    u.on = upd.on && it > 0;
+    return jr_lookup_cc1(lv.data(), L, B, h, w, r, cp, blocked, wp, kpad, bp, yp, ycs, y_coff, cout, s, &u);
   };
 }
 
@@ -996,7 +990,10 @@ void seq_loss_bwd_op(const TList& t, IList i, double max_flow) {
 // ---------------------------------------------------------------- eager ops
 void conv_op(const TList& t, IList i, double alpha) { run_now(make_conv(t, i, alpha, nullptr)); }
 void corr_op(const TList& t, IList i, double scale) { run_now(make_corr(t, i, scale, nullptr)); }
-void lookup_op(const TList& t, IList i) { run_now(make_lookup(t, i, nullptr)); }
+// a stand-alone lookup applies its fused flow update when one is given (in a
+// plan the update is skipped in loop iteration 0, which has no previous taps)
+void lookup_op(const TList& t, IList i) { JR_CHECK_OK(make_lookup(t, i, nullptr)(cur_stream(), 1)); }
+void lookup_cc1_op(const TList& t, IList i) { JR_CHECK_OK(make_lookup_cc1(t, i, nullptr)(cur_stream(), 1)); }
 void upsample_convex_op(const TList& t, IList i) { run_now(make_upsample_convex(t, i, nullptr)); }
 void convex_head_op(const TList& t, IList i, double alpha) { run_now(make_convex_head(t, i, alpha, nullptr)); }
 void upsample_bilinear_op(const TList& t, IList i) { run_now(make_upsample_bilinear(t, i, nullptr)); }
@@ -1010,7 +1007,6 @@ void init_coords_op(const TList& t, IList i) { run_now(make_init_coords(t, i, nu
 void copy_channels_op(const TList& t, IList i) { run_now(make_copy_channels(t, i, nullptr)); }
 void lookup_bwd_op(const TList& t, IList i) { run_now(make_lookup_bwd(t, i, nullptr)); }
 void im2col_op(const TList& t, IList i) { run_now(make_im2col(t, i, nullptr)); }
-void flow_head_op(const TList& t, IList i) { run_now(make_flow_head(t, i, nullptr)); }
 void flow_taps_op(const TList& t, IList i) { run_now(make_flow_taps(t, i, nullptr)); }
 void taps_gemm_op(const TList& t, IList i) { run_now(make_taps_gemm(t, i, nullptr)); }
 void conv1x1_op(const TList& t, IList i) { run_now(make_conv1x1(t, i, nullptr)); }
@@ -1067,10 +1063,6 @@ void upsample_bilinear_bwd_op(const TList& t, IList i) { run_now(make_upsample_b
 // execute concurrently.  A wait on an event not yet recorded during the
 // current enqueue is skipped (e.g. the first iteration's wait on the previous
 // iteration's mask head), which also keeps graph capture self-contained.
-// Loop-body ops can carry a parity (set_parity 0/1): they are enqueued only in
-// even / odd iterations, which double-buffers a tensor that a side lane still
-// reads while the next iteration rewrites it (the flow head's features and
-// flow vs. the mask head + upsampling of the previous iteration).
 // Lane 0 runs on a private stream of the device's greatest priority (forked
 // from / joined to the caller's stream): the model's critical path (lookup ->
 // motion encoder -> GRU -> flow head) wins the dispatcher over the side lanes'
@@ -1097,7 +1089,6 @@ class Plan : public torch::CustomClassHolder {
   void set_segment(int64_t s) {
     TORCH_CHECK(s >= 0 && s <= 2, "segment must be 0 (prologue), 1 (loop) or 2 (epilogue)");
     seg_ = (int)s;
-    parity_ = -1;
     defer_ = 0;
     reset_graph();
   }
@@ -1111,11 +1102,6 @@ class Plan : public torch::CustomClassHolder {
     TORCH_CHECK(d == 0 || seg_ != 0, "deferred ops belong to the loop body or the epilogue");
     defer_ = (int)d;
   }
-  void set_parity(int64_t p) {
-    TORCH_CHECK(p >= -1 && p <= 1, "parity must be -1 (every iteration), 0 (even) or 1 (odd)");
-    TORCH_CHECK(p == -1 || seg_ == 1, "parity applies to loop-body ops only");
-    parity_ = (int)p;
-  }
   void set_lane(int64_t l) {
     TORCH_CHECK(l >= 0 && l < kMaxLanes, "lane must be in [0, ", kMaxLanes, ")");
     lane_ = (int)l;
@@ -1126,6 +1112,7 @@ class Plan : public torch::CustomClassHolder {
   void add_conv(TList t, IList i, double alpha) { push(make_conv(t, i, alpha, &keep_), "conv"); }
   void add_corr(TList t, IList i, double scale) { push(make_corr(t, i, scale, &keep_), "corr"); }
   void add_lookup(TList t, IList i) { push(make_lookup(t, i, &keep_), "lookup"); }
+  void add_lookup_cc1(TList t, IList i) { push(make_lookup_cc1(t, i, &keep_), "lookup_cc1"); }
   void add_upsample_convex(TList t, IList i) { push(make_upsample_convex(t, i, &keep_), "upsample_convex"); }
   void add_convex_head(TList t, IList i, double alpha) { push(make_convex_head(t, i, alpha, &keep_), "convex_head"); }
   void add_upsample_bilinear(TList t, IList i) { push(make_upsample_bilinear(t, i, &keep_), "upsample_bilinear"); }
@@ -1136,7 +1123,6 @@ class Plan : public torch::CustomClassHolder {
   void add_memset(TList t) { push(make_memset(t, &keep_), "memset"); }
   void add_copy(TList t) { push(make_copy(t, &keep_), "copy"); }
   void add_copy_channels(TList t, IList i) { push(make_copy_channels(t, i, &keep_), "copy_channels"); }
-  void add_flow_head(TList t, IList i) { push(make_flow_head(t, i, &keep_), "flow_head"); }
   void add_flow_taps(TList t, IList i) { push(make_flow_taps(t, i, &keep_), "flow_taps"); }
   void add_taps_gemm(TList t, IList i) { push(make_taps_gemm(t, i, &keep_), "taps_gemm"); }
   void add_conv1x1(TList t, IList i) { push(make_conv1x1(t, i, &keep_), "conv1x1"); }
@@ -1394,16 +1380,15 @@ class Plan : public torch::CustomClassHolder {
     int kind;
     int ev;
     std::string name;
-    int parity;  // -1: every iteration; 0 / 1: even / odd loop iterations only
     int defer;   // 1: previous iteration's work (see set_defer)
   };
   void push(Launch l, const char* name) {
-    segs_[seg_].push_back(Op{std::move(l), lane_, OP_LAUNCH, -1, name, parity_, defer_});
+    segs_[seg_].push_back(Op{std::move(l), lane_, OP_LAUNCH, -1, name, defer_});
     reset_graph();
   }
   void push_sync(int kind, int64_t ev, const char* name) {
     TORCH_CHECK(ev >= 0 && ev < kMaxEvents, "event id out of range");
-    segs_[seg_].push_back(Op{Launch(), lane_, kind, (int)ev, std::string(name) + std::to_string(ev), parity_, defer_});
+    segs_[seg_].push_back(Op{Launch(), lane_, kind, (int)ev, std::string(name) + std::to_string(ev), defer_});
     reset_graph();
   }
   // JR_LANE_PRIORITY=0 disables the lane priorities (A/B measurements)
@@ -1436,7 +1421,6 @@ class Plan : public torch::CustomClassHolder {
   // order and is skipped (a same-stream record/wait pair on a forked capture stream
   // also crashes hipStreamEndCapture on this ROCm).
   int exec_op(const Op& o, hipStream_t* st, int it, std::vector<char>& recorded) {
-    if (o.parity >= 0 && (it & 1) != o.parity) return 0;
     if (o.defer) {
       if (it == 0) return 0;
       --it;
@@ -1522,7 +1506,6 @@ class Plan : public torch::CustomClassHolder {
   std::vector<at::Tensor> keep_;
   int seg_ = 0;
   int lane_ = 0;
-  int parity_ = -1;
   int defer_ = 0;
   int used_lanes_ = 1;
   std::vector<hipEvent_t> events_;
@@ -1551,6 +1534,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("conv(Tensor?[] t, int[] i, float alpha) -> ()", &jr::conv_op);
   m.def("corr(Tensor?[] t, int[] i, float scale) -> ()", &jr::corr_op);
   m.def("lookup(Tensor?[] t, int[] i) -> ()", &jr::lookup_op);
+  m.def("lookup_cc1(Tensor?[] t, int[] i) -> ()", &jr::lookup_cc1_op);
   m.def("upsample_convex(Tensor?[] t, int[] i) -> ()", &jr::upsample_convex_op);
   m.def("convex_head(Tensor?[] t, int[] i, float alpha) -> ()", &jr::convex_head_op);
   m.def("upsample_bilinear(Tensor?[] t, int[] i) -> ()", &jr::upsample_bilinear_op);
@@ -1561,7 +1545,6 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("copy_channels(Tensor?[] t, int[] i) -> ()", &jr::copy_channels_op);
   m.def("lookup_bwd(Tensor?[] t, int[] i) -> ()", &jr::lookup_bwd_op);
   m.def("im2col(Tensor?[] t, int[] i) -> ()", &jr::im2col_op);
-  m.def("flow_head(Tensor?[] t, int[] i) -> ()", &jr::flow_head_op);
   m.def("flow_taps(Tensor?[] t, int[] i) -> ()", &jr::flow_taps_op);
   m.def("taps_gemm(Tensor?[] t, int[] i) -> ()", &jr::taps_gemm_op);
   m.def("conv1x1(Tensor?[] t, int[] i) -> ()", &jr::conv1x1_op);
@@ -1588,7 +1571,6 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("merge_finish", &jr::Plan::merge_finish)
       .def("merged_iters", &jr::Plan::merged_iters)
       .def("set_lane", &jr::Plan::set_lane)
-      .def("set_parity", &jr::Plan::set_parity)
       .def("set_defer", &jr::Plan::set_defer)
       .def("add_record", &jr::Plan::add_record)
       .def("add_wait", &jr::Plan::add_wait)
@@ -1596,6 +1578,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_conv", &jr::Plan::add_conv)
       .def("add_corr", &jr::Plan::add_corr)
       .def("add_lookup", &jr::Plan::add_lookup)
+      .def("add_lookup_cc1", &jr::Plan::add_lookup_cc1)
       .def("add_upsample_convex", &jr::Plan::add_upsample_convex)
       .def("add_convex_head", &jr::Plan::add_convex_head)
       .def("add_upsample_bilinear", &jr::Plan::add_upsample_bilinear)
@@ -1606,7 +1589,6 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_memset", &jr::Plan::add_memset)
       .def("add_copy", &jr::Plan::add_copy)
       .def("add_copy_channels", &jr::Plan::add_copy_channels)
-      .def("add_flow_head", &jr::Plan::add_flow_head)
       .def("add_flow_taps", &jr::Plan::add_flow_taps)
       .def("add_taps_gemm", &jr::Plan::add_taps_gemm)
       .def("add_conv1x1", &jr::Plan::add_conv1x1)

@@ -28,12 +28,10 @@ _load_error: Optional[BaseException] = None
 
 # activation / epilogue codes (csrc/kernels/common.h, kernels.h)
 ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, ACT_SPLIT_TANH_RELU = 0, 1, 2, 3, 4
-EPI_STD, EPI_GRU_A, EPI_GRU_B, EPI_FLOW, EPI_CONVEX = 0, 1, 2, 3, 4
-EPI_TAPS = 6
+EPI_STD, EPI_GRU_A, EPI_GRU_B = 0, 1, 2   # 3, 4: retired epilogues (kernels.h)
+EPI_BWD, EPI_TAPS = 5, 6
 # tile configs with the EPI_TAPS epilogue (256 channels in one N tile, 16 waves of 64 x 32)
 TAPS_CFGS = (34, 22, 35, 38)
-# tile configs whose lanes hold < 16 contiguous output channels (no EPI_CONVEX)
-NARROW_CFGS = (3, 5, 19, 21, 36)
 # tile configs of conv_igemm.hip: (BCO, BP)
 CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (16, 256), 4: (64, 64), 5: (16, 64)}
 # configs 6..11: LDS-DMA kernel D2 (csrc/kernels/conv_igemm.hip)
@@ -61,19 +59,6 @@ CFG_TILES.update({35: (256, 128), 36: (128, 128), 37: (128, 128), 38: (256, 128)
 TUNE_CFGS = (0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34,
              35, 38)
 NUM_CUS = 256
-# config 44: the 3x3 halo-tiled kernel (csrc/kernels/conv_halo.hip); valid only
-# for the shapes halo_ok() accepts, so it is not in CFG_TILES / TUNE_CFGS
-HALO_CFG = 44
-
-
-def halo_ok(spec: "ConvSpec", OW: int, x_coff: int = 0, epi: int = EPI_STD) -> bool:
-    """Whether conv_halo.hip runs this conv (3x3, stride 1, pad 1, cin 64 / 128,
-    <= 128 outputs, rows a multiple of 64 pixels, plain epilogue)."""
-    return (spec.kh == 3 and spec.kw == 3 and spec.sh == 1 and spec.sw == 1 and spec.ph == 1 and spec.pw == 1
-            and spec.cin8 in (64, 128) and spec.cout <= 128 and OW % 64 == 0 and x_coff % 8 == 0
-            and epi == EPI_STD)
-
-
 def load(build_if_missing: bool = True) -> None:
     """Load ``_C.so`` (building it with hipcc first if it is missing)."""
     global _loaded, _load_error
@@ -234,10 +219,9 @@ def conv_args(spec: ConvSpec, x: torch.Tensor, N: int, H: int, W: int, y: torch.
               y_coff: int = 0, act: int = ACT_NONE, split: int = 0, alpha: float = 1.0, y2=None, y2_coff: int = 0,
               res=None, res_coff: int = 0, res_post: int = 0, h32=None, zbuf=None, hidden: int = 0, coords=None,
               flow32=None, y3=None, y3_coff: int = 0, epi: int = EPI_STD, cfg: Optional[int] = None,
-              bmap=None, bmap_coff: int = 0, it_stride: int = 0, tapw=None):
+              bmap=None, bmap_coff: int = 0, tapw=None):
     """Build the (tensors, ints, alpha) argument triple of the ``conv`` op.
-    ``bmap``: optional fp32 per-pixel bias map [M, C], channels from ``bmap_coff``.
-    ``it_stride``: (EPI_CONVEX) output floats between loop iterations of a plan."""
+    ``bmap``: optional fp32 per-pixel bias map [M, C], channels from ``bmap_coff``."""
     OH, OW = spec.out_hw(H, W)
     if cfg is None:
         cfg = pick_cfg(N * OH * OW, spec.cout)
@@ -246,26 +230,9 @@ def conv_args(spec: ConvSpec, x: torch.Tensor, N: int, H: int, W: int, y: torch.
         t.append(tapw)
     i = [N, H, W, x_coff, spec.cin8, spec.kh, spec.kw, spec.sh, spec.sw, spec.ph, spec.pw, spec.cout, act, split,
          y_coff, y2_coff, res_coff, hidden, y3_coff, epi, cfg, res_post]
-    if bmap is not None or it_stride:
+    if bmap is not None:
         i += [0, 0, 0, 0, bmap_coff]
-    if it_stride:
-        i.append(int(it_stride))
     return t, i, float(alpha)
-
-
-def convex_mask_kernel(kernel: torch.Tensor, bias: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """MaskPredictor 1x1 conv (..., 576) with output channel k*64 + s (model.py:86)
-    -> (..., 1024) in sub-pixel-major order s*16 + k (k < 9; 7 zero channels per
-    sub-pixel), so one lane of the EPI_CONVEX epilogue holds all 9 neighbour
-    logits of one sub-pixel."""
-    kh, kw, cin, c = kernel.shape
-    assert c == 576, c
-    k = kernel.detach().float().reshape(kh, kw, cin, 9, 64).permute(0, 1, 2, 4, 3)
-    kp = torch.zeros(kh, kw, cin, 64, 16, dtype=torch.float32, device=kernel.device)
-    kp[..., :9] = k
-    bp = torch.zeros(64, 16, dtype=torch.float32, device=bias.device)
-    bp[:, :9] = bias.detach().float().reshape(9, 64).t()
-    return kp.reshape(kh, kw, cin, 1024), bp.reshape(1024)
 
 
 def pack_convex_head(kernel: torch.Tensor, bias: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -49,8 +49,6 @@ from ..ops.native import (
     ACT_NONE,
     ACT_RELU,
     ACT_SPLIT_TANH_RELU,
-    EPI_CONVEX,
-    EPI_FLOW,
     EPI_GRU_A,
     EPI_GRU_B,
     EPI_STD,
@@ -72,8 +70,6 @@ def _tune(spec: ConvSpec, x, N, H, W, y, kw, reps: int = 5) -> int:
     best, best_t = None, None
     cfgs = nat.TAPS_CFGS if kw.get("epi") == nat.EPI_TAPS else nat.TUNE_CFGS
     for cfg in cfgs:
-        if kw.get("epi") == nat.EPI_CONVEX and cfg in nat.NARROW_CFGS:
-            continue
         args = conv_args(spec, x, N, H, W, y, **dict(kw, cfg=cfg))
         ops.conv(*args)  # warm (and JIT-free: all configs are precompiled)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -126,24 +122,6 @@ class _PlanState:
     slot_ptr: int = 0
 
 
-class PendingFlow:
-    """Result of :meth:`RaftEngine.submit`: the flows tensor plus the event
-    that marks it complete (recorded on the engine's loop stream)."""
-
-    def __init__(self, out: torch.Tensor, done: torch.cuda.Event, device):
-        self.out, self.done, self.device = out, done, device
-
-    def wait(self, stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
-        """Order ``stream`` (default: current) after the result; returns it."""
-        (stream or torch.cuda.current_stream(self.device)).wait_event(self.done)
-        return self.out
-
-    def result(self) -> torch.Tensor:
-        """Block the host until the result is ready; returns it."""
-        self.done.synchronize()
-        return self.out
-
-
 class RaftEngine:
     """Inference engine bound to one model and one GPU.
 
@@ -155,117 +133,63 @@ class RaftEngine:
         corr_dtype: storage dtype of the correlation pyramid (bf16 default:
             the lookup output feeding the bf16 MFMA convs is bf16 anyway;
             fp32 for bit-closer parity with the fp32 reference).
-        autotune: time every conv tile config on the real buffers when a plan
-            is built and keep the fastest (cached per problem signature).
-        streams: (True / False / "auto" = True at batch >= 4 per plan with all
-            iterations upsampled, where it measured faster) place the model's independent branches on side lanes of the
-            plan (context encoder || feature encoder + correlation pyramid;
-            flow-feature convs || lookup + correlation convs; mask head +
-            upsampling of iteration i || iteration i+1) so they overlap on
-            the GPU (parallel branches of the captured hipGraph).
-        flow_head: how the flow head's output conv (3x3, 256 -> 2) + the
-            coordinate update run: "taps" (default) = a 1x1 implicit-GEMM conv
-            to the 9 x 2 per-tap partials + the flow_taps kernel that sums the
-            shifted partials (fm read once instead of 9 times); "conv" = the
-            3x3 implicit-GEMM conv with the EPI_FLOW epilogue; "fused" = the
-            dedicated halo-tiled flow_head kernel (flowhead.hip).
-        split: run the batch as this many independent part-forwards (when
-            the batch divides evenly), so that one part's kernels fill the
-            CUs another part's leave idle.  merge_parts (default): with
-            use_graph, the parts' captures are copied into ONE hipGraph (no
-            edge between them); else each part's graph is replayed on its
-            own stream (measured to serialise on this ROCm).
         gate_dtype: storage dtype of the ConvGRU z gate and of the folded
             context bias map (bf16 default, fp32 for bit-closer parity); the
             hidden state itself is always carried in fp32.
-        flow_lane: "mask" (default) runs the motion encoder's flow-feature convs
-            of iteration i+1 on the mask lane right after iteration i's flow
-            update, ahead of its mask head (three cross-lane edges per
-            iteration instead of five; 289-294 vs 279 pairs/s at raft_large
-            batch 4; falls back to "side" without a split mask head.  Measured
-            and dropped: two edges with the mask conv ahead of the flow
-            features and the flow double-buffered by parity, 276 -- the
-            longer chain before E_FLOW stalls the motion conv; one event after
-            the whole mask lane, 289-292; the first GRU's h-part conv moved onto
-            the mask lane as a bias map, 298 vs 302 -- it contends with the
-            correlation convs); "side" runs
-            them on their own lane concurrently with the lookup + correlation
-            convs; "main" runs them on the critical-path lane before the lookup.
-        double_buffer: ("lanes" schedule) double-buffer the flow head outputs by iteration
-            parity, so iteration i+1's flow head need not wait for iteration
-            i's mask head (otherwise one buffer and a WAR wait).  Off by
-            default: the extra overlap measured slower (233 vs 244 pairs/s),
-            the mask head then contends with the next iteration's critical path.
-        direct_flow: run the flow branch's first conv (7x7 on the 2-channel
-            flow, ``model.py:282-283``) on the direct VALU kernel
-            (conv_direct.hip) instead of the implicit GEMM, whose 49 gathered
-            taps of 2 real channels starve the MFMA loader.
-        mask_head: (raft_large, all-iterations output) "split" (default) runs
-            only the flow head's 3x3 conv (128 -> 256) on the critical path and
-            the mask predictor's 3x3 conv (128 -> 256, ``model.py:389-390``) on
-            the mask lane, reading h before the next iteration's first GRU
-            overwrites it (event-ordered); "fused" runs both 3x3 convs as one
-            128 -> 512 GEMM on the critical path.
-        convex: (raft_large) "head" (default): the dedicated mask-head kernel
-            below; "fused" computes the mask predictor's
-            1x1 conv (256 -> 576, ``model.py:394-400``) with the EPI_CONVEX
-            epilogue: output channels reordered sub-pixel-major (9 logits of a
-            sub-pixel in one lane), softmax + convex combination of the 3x3
-            flow neighbourhood and the x8 pixel shuffle (``model.py:85-98``) in
-            registers, the upsampled flow written straight to the output (no
-            576-channel mask round trip, one launch less per iteration);
-            "separate" = mask conv + upsample_convex kernel; "head" = the
-            dedicated mask-head kernel (convex_head.hip): the same fusion with
-            tap-major MFMA rows (576 rows of work instead of the 1024 of the
-            padded sub-pixel-major layout), weights per sub-pixel group in
-            LDS, one 32-byte store per lane (raft_large batch 4: 22 us vs
-            37 us for the EPI_CONVEX conv; bench 278-282 vs 267-269 pairs/s).
+        autotune: pick every conv's tile config from the persisted table
+            (runtime/tunedb.py) or, on a miss, by timing the candidates on the
+            real buffers when a plan is built; ``False``: a size heuristic.
+        streams: (True / False / "auto") run the model's independent branches
+            on concurrent lanes of the plan (parallel branches of the captured
+            hipGraph): context encoder || the two feature-encoder halves ||
+            correlation pyramid in the prologue; in the loop, iteration i+1's
+            flow-feature convs and iteration i's mask head + upsampling on a
+            side lane while the critical lane runs lookup -> correlation convs
+            -> motion conv -> ConvGRU -> flow head.  "auto" (default) = on at
+            batch >= 4 per plan with every iteration upsampled and a
+            256 -> 576 mask head (raft_large), where it measured faster.
+        split: run the batch as this many independent part-forwards captured
+            into ONE hipGraph with no edge between them (when the batch
+            divides evenly), so one part's kernels fill CUs another part's
+            leave idle.
+        cfg_override: fixed tile configs per conv spec name (e.g. {"gru0.b": 27},
+            tools/schedule_tune.py); ``JR_CFG_OVERRIDE="name=cfg,..."`` adds entries.
+
+    Schedules (chosen per plan, see :meth:`_build_part`): the lane schedule
+    above; one in-order lane with every iteration upsampled (batch < 4,
+    raft_small); and the final-only serving mode.  In all of them the flow
+    update of iteration i runs inside iteration i+1's lookup kernel and the
+    FlowHead's second conv is an MFMA epilogue of its first (raft_large) or a
+    skinny taps GEMM (raft_small).  Variants measured and removed in round 3
+    (kept in the history): double-buffered flow-head outputs, the 3x3 EPI_FLOW
+    and halo-tiled flow heads, the EPI_CONVEX conv epilogue, the side-lane and
+    main-lane flow-feature placements, the mask lane forking after convcorr1,
+    separate per-part graphs on separate streams, and submit() (the two phases
+    as separate graphs on two streams, which serialise on this ROCm).
     """
 
     def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True,
-                 corr_dtype: torch.dtype = torch.bfloat16, autotune: bool = True, streams="auto",
-                 split: int = 1, flow_head: str = "taps", double_buffer: bool = False,
-                 fused_flow_head: bool = False, gate_dtype: torch.dtype = torch.bfloat16,
-                 flow_lane: str = "mask", direct_flow: bool = True, mask_head: str = "split",
-                 convex: str = "head", taps_epi: bool = True, fuse_update: bool = True, fe_split: bool = True,
-                 fork_after: str = "lookup", merge_parts: bool = True,
+                 corr_dtype: torch.dtype = torch.bfloat16, gate_dtype: torch.dtype = torch.bfloat16,
+                 autotune: bool = True, streams="auto", split: int = 1,
                  cfg_override: Optional[Dict[str, int]] = None):
         nat.require()
-        assert fork_after in ("lookup", "cc1"), fork_after
-        self.fork_after = fork_after
-        self.fe_split = fe_split
-        self.taps_epi = taps_epi
-        self.fuse_update = fuse_update
-        assert convex in ("fused", "separate", "head"), convex
-        self.convex = convex
-        assert mask_head in ("split", "fused"), mask_head
         assert streams in (True, False, "auto"), streams
         self.streams_mode = streams
-        self._mask_head_opt, self._flow_lane_opt = mask_head, flow_lane
-        self.mask_head = mask_head if streams else "fused"
-        self.direct_flow = direct_flow
-        self._cf1_w = self._cf1_b = None
+        self.streams = bool(streams)
+        self.mask_head = "split"      # per plan: "split" (mask lane) | "fused" (one lane, 128 -> 512 conv)
         self.gate_dtype = gate_dtype
-        assert flow_lane in ("side", "main", "mask"), flow_lane
-        self.flow_lane = flow_lane if streams else "main"
-        self.double_buffer = double_buffer
-        self.flow_head = "fused" if fused_flow_head else flow_head
-        assert self.flow_head in ("taps", "conv", "fused"), self.flow_head
-        self.streams = streams
         self.split = split
-        self.merge_parts = merge_parts
-        # tile configs fixed per conv spec name (e.g. {"gru0.b": 27}; tools/schedule_tune.py),
-        # else the isolated-timing autotuner picks; JR_CFG_OVERRIDE="name=cfg,..." adds entries
         self.cfg_override = dict(cfg_override or {})
         for item in filter(None, os.environ.get("JR_CFG_OVERRIDE", "").split(",")):
             k, v = item.split("=")
             self.cfg_override[k.strip()] = int(v)
-        self._part_streams: List[torch.cuda.Stream] = []
-        self._fh2_w = self._fh2_b = None
+        self._cf1_w = self._cf1_b = None
+        self._fh2_b = None
         self._convex_w = self._convex_b = None
         self._taps_w = None
         self._taps_epi_w = None
         self._cc1_w = self._cc1_b = None
+        self._lc1_w = None   # convcorr1 packed for the fused lookup kernel
         self.model = model
         self.device = torch.device(device)
         self.use_graph = use_graph
@@ -279,7 +203,6 @@ class RaftEngine:
         self._states: Dict[Tuple[int, int, int, int], _PlanState] = {}
         self._sig = None
         self._sig_modules = None
-        self._pipe = None
         self._pp = None   # pipelined(): {key, n, pending slot}
         self._analyse()
         self._pack()
@@ -357,15 +280,11 @@ class RaftEngine:
                 sp.b.copy_(b.float().to(self.device))
             else:
                 self._specs[name] = nat.make_spec(k, b.to(self.device), stride, pad, cin8=cin8, device=self.device)
-        # flow head output conv for the fused flow_head kernel: bf16 [2][9][cin]
         fh2 = self.model.update_block.flow_head.conv2
-        k = fh2.kernel.detach().float()
-        wf = k.permute(3, 0, 1, 2).reshape(2, 9, k.shape[2]).to(self.device, torch.bfloat16).contiguous()
         bf = fh2.bias.detach().float().to(self.device).contiguous()
-        if getattr(self, "_fh2_w", None) is None:
-            self._fh2_w, self._fh2_b = wf, bf
+        if self._fh2_b is None:
+            self._fh2_b = bf
         else:
-            self._fh2_w.copy_(wf)
             self._fh2_b.copy_(bf)
         # the correlation features' first 1x1 conv on the LDS-resident-weight kernel (conv1x1.hip)
         cc1 = self.model.update_block.motion_encoder.convcorr1.layers_0
@@ -378,6 +297,16 @@ class RaftEngine:
             else:
                 self._cc1_w.copy_(wc)
                 self._cc1_b.copy_(bc)
+        # the same conv fused into the lookup kernel (corr.hip:lookup_cc1_kernel): K padded to 32 only
+        S = 2 * self.radius + 1
+        kf = round_up(self.num_levels * S * S, 32)
+        if (cc1.kernel.shape[:2] == (1, 1) and cc1.kernel.shape[3] == 256 and self.num_levels <= 4
+                and (self.radius, kf) in ((4, 352), (3, 224))):
+            wl = nat.pack_conv1x1(cc1.kernel.to(self.device), kf)
+            if self._lc1_w is None:
+                self._lc1_w, self._lc1_kpad = wl, kf
+            else:
+                self._lc1_w.copy_(wl)
         if fh2.kernel.shape[2] in (128, 256):
             wt = nat.pack_taps(fh2.kernel.to(self.device))
             if self._taps_w is None:
@@ -398,10 +327,8 @@ class RaftEngine:
             else:
                 self._convex_w.copy_(wc)
                 self._convex_b.copy_(bc)
-        elif self.convex == "head":
-            self.convex = "fused"   # the dedicated kernel is specialised to raft_large's 256 -> 576 head
         cf1 = self.model.update_block.motion_encoder.convflow1.layers_0
-        if self.direct_flow and nat.direct_conv_ok(cf1.kernel, cf1.stride):
+        if nat.direct_conv_ok(cf1.kernel, cf1.stride):
             wd = nat.pack_direct_weight(cf1.kernel).to(self.device)
             bd = cf1.bias.detach().float().to(self.device).contiguous()
             if self._cf1_w is None:
@@ -480,11 +407,8 @@ class RaftEngine:
             self._reg("fh1.flow", conv_src(fh.conv1))  # final-only mode / split mask head: flow head alone
             self._reg("mask.convrelu", cna_src(mp.convrelu))
             self._reg("mask", conv_src(mp.conv))
-            self._reg("mask.convex", lambda: (*nat.convex_mask_kernel(mp.conv.kernel, mp.conv.bias), (1, 1), (0, 0),
-                                              None))
         else:
             self._reg("fh1", conv_src(fh.conv1))
-        self._reg("fh2", conv_src(fh.conv2))
 
         def fh2_taps():  # (3,3,cin,2) -> (1,1,cin,18): out channel tap*2 + o
             k = fh.conv2.kernel.detach().float()
@@ -604,15 +528,19 @@ class RaftEngine:
         return x, H, W
 
     # lanes pay off once the per-iteration kernels fill the chip: measured on
-    # MI355X (raft_large, 440x1024, 32 iters; tools/probe_launch.py) the lane
-    # schedule is 17-21 % slower at batch 1, equal at batch 2 and 2 % faster
-    # at batch 4 than one in-order lane.  In final-only mode the loop has no
-    # mask head to overlap, only the flow-feature convs: there lanes measured
-    # 13.1 (one lane) vs 12.7-24.9 ms (lanes, schedule-dependent run to run)
-    # at batch 4, so "auto" keeps one lane.  Without a mask predictor
-    # (raft_small) only the flow-feature convs could overlap: one lane measured
-    # 562 vs 528 pairs/s at batch 4, so "auto" keeps one lane there too.
+    # MI355X (raft_large, 440x1024, 32 iters) the lane schedule is 17-21 % slower
+    # at batch 1, equal at batch 2 and 2 % faster at batch 4 than one in-order
+    # lane.  In final-only mode the loop has no mask head to overlap, only the
+    # flow-feature convs: one lane measured 13.1 vs 12.7-24.9 ms (lanes,
+    # schedule-dependent run to run) at batch 4.  Without a mask predictor
+    # (raft_small) one lane measured 562 vs 528 pairs/s at batch 4.
     AUTO_STREAMS_MIN_BATCH = 4
+
+    def _lanes_ok(self, all_iters: bool) -> bool:
+        """The lane schedule needs a mask head to overlap (every iteration
+        upsampled) and the FlowHead taps epilogue (a 256-channel conv1)."""
+        return (all_iters and self.has_mask and self._taps_epi_w is not None and self._convex_w is not None
+                and self._specs["fh1.flow"].cout == 256)
 
     def uses_lanes(self, B: int, all_iters: bool = True) -> bool:
         """Whether the plan for batch ``B`` runs the model's branches on several
@@ -620,25 +548,17 @@ class RaftEngine:
         (:meth:`pipelined`) measured faster only on one-lane plans: batch 1
         145 -> 157 pairs/s, raft_small batch 4 559 -> 602, final-only 326 -> 346;
         with lanes (raft_large batch 4) 319 -> 289 (profiles/r2_pipelined_graph_ab.txt)."""
+        if not self._lanes_ok(all_iters):
+            return False
         if self.streams_mode != "auto":
-            return bool(self.streams)
+            return bool(self.streams_mode)
         nb = B // self.split if (self.split > 1 and B % self.split == 0) else B
-        return nb >= self.AUTO_STREAMS_MIN_BATCH and all_iters and self.has_mask
+        return nb >= self.AUTO_STREAMS_MIN_BATCH
 
     def _build(self, B: int, H: int, W: int, n_iters: int, all_iters: bool = True) -> _PlanState:
-        if self.streams_mode != "auto":
-            return self._build_impl(B, H, W, n_iters, all_iters)
         on = self.uses_lanes(B, all_iters)
-        saved = (self.streams, self.flow_lane, self.mask_head)
         self.streams = on
-        self.flow_lane = self._flow_lane_opt if on else "main"
-        self.mask_head = self._mask_head_opt if on else "fused"
-        try:
-            return self._build_impl(B, H, W, n_iters, all_iters)
-        finally:
-            self.streams, self.flow_lane, self.mask_head = saved
-
-    def _build_impl(self, B: int, H: int, W: int, n_iters: int, all_iters: bool = True) -> _PlanState:
+        self.mask_head = "split" if on else "fused"
         h, w = H // 8, W // 8
         L = self.num_levels
         min_sz = 2 * (2 ** (L - 1))
@@ -648,9 +568,9 @@ class RaftEngine:
         dev = self.device
         parts = self.split if (self.split > 1 and B % self.split == 0) else 1
         nb = B // parts
-        # Each part is an independent forward with its own Plan, captured as its
-        # own hipGraph and replayed on its own stream, so the parts' kernels fill
-        # each other's idle CUs (kernel tails, launch gaps, small kernels).
+        # Each part is an independent forward with its own Plan; with use_graph
+        # their captures are copied into ONE hipGraph (Plan.merge_*), so the
+        # parts' kernels fill each other's idle CUs.
         plans = [nat.new_plan() for _ in range(parts)]
         st = _PlanState(plan=plans[0], plans=plans, n_iters=n_iters)
         st.inp1 = torch.zeros((B, H, W, 3), dtype=F32, device=dev)
@@ -658,22 +578,36 @@ class RaftEngine:
         st.out = torch.zeros((n_iters if all_iters else 1, B, H, W, 2), dtype=F32, device=dev)
         st.slot_ptr = st.out.data_ptr()
         st.out_slot = torch.tensor([st.slot_ptr], dtype=torch.int64, device=dev)
-        lanes = (0, 1, 2) if self.streams else (0, 0, 0)
+        lanes = (0, 1, 2) if on else (0, 0, 0)
         for part, plan in enumerate(plans):
             self._build_part(st, plan, part * nb, nb, H, W, n_iters, f"p{part}.", lanes, 0, all_iters)
             plan.set_lane(0)
             plan.set_segment(2)
-        if parts > 1 and len(self._part_streams) < parts:
-            self._part_streams = [torch.cuda.Stream(device=dev) for _ in range(parts)]
         return st
 
     def _build_part(self, st: _PlanState, plan, b0: int, B: int, H: int, W: int, n_iters: int, pt: str,
                     lanes: Tuple[int, int, int], ev0: int, all_iters: bool = True):
         """Lower one forward over images [b0, b0 + B) onto ``plan`` using lanes
-        (main, side, side2) and events ev0 .. ev0 + 6.  ``all_iters=False`` is the
-        final-only serving mode: the loop runs the flow head alone (no mask head)
-        and the mask head + x8 upsampling run once, in the epilogue segment, on
-        the final hidden state and flow."""
+        (main, side, side2) and events ev0 .. ev0 + 8.
+
+        Three loop schedules (``model.py:495-510`` per iteration):
+
+        * lanes (``main != side``): the critical lane runs lookup (+ the
+          previous iteration's flow update) -> convcorr1/2 -> motion conv ->
+          2 x ConvGRU -> FlowHead conv1 with the taps epilogue; the mask lane,
+          forked after the lookup, runs the flow-feature convs of this
+          iteration and the mask head + convex upsampling of the previous one
+          (deferred ops, skipped in iteration 0).  Three cross-lane edges per
+          iteration (E_FH, E_FLOW, E_MASK): each costs ~6-12 us in a captured
+          graph on this ROCm.
+        * one lane, every iteration upsampled: the same deferral in order:
+          lookup (+ update), flow features, upsampling of iteration i-1,
+          correlation / motion / GRU convs, FlowHead conv1 (fused with the mask
+          predictor's 3x3 conv as one 128 -> 512 GEMM when there is a mask
+          head) + the taps GEMM.
+        * final-only (``all_iters=False``, serving): the loop runs the flow head
+          alone; the mask head + x8 upsampling run once in the epilogue on the
+          final hidden state and flow."""
         m = self.model
         dev = self.device
         bufs = st.bufs
@@ -693,10 +627,11 @@ class RaftEngine:
         out_off = (out.data_ptr() - st.out.data_ptr()) // 4   # in floats, from the slot's base
 
         # ---------------- prologue: encoders + correlation pyramid
-        # lanes: 0 = feature encoder + correlation pyramid, 1 = context encoder
-        E_PREP, E_CTX, E_IT, E_FLOW, E_FH, E_MASK = range(ev0, ev0 + 6)  # E_MASK + 1: odd-iteration mask head
-        E_MR = ev0 + 7  # split mask head: the mask lane has read h (the next GRU may overwrite it)
+        # lanes: 0 = feature encoder (image 1) + correlation pyramid, 1 = context
+        # encoder, 2 = feature encoder (image 2)
+        E_PREP, E_CTX, E_FLOW, E_FH, E_MASK, E_FE2 = range(ev0, ev0 + 6)
         main, side, side2 = lanes
+        lanes_on = main != side
 
         def lane(l):
             plan.set_lane(l)
@@ -727,7 +662,7 @@ class RaftEngine:
         self._conv(plan, sp["ce.conv"], ctxf, B, h, w, ce_out, act=ACT_SPLIT_TANH_RELU, split=self.hidden,
                    h32=h32, hidden=self.hidden)
         plan.add_copy_channels([ce_out, hx], [0, 0, M, self.hidden])
-        # loop-invariant context share of every GRU gate (+ gate biases), fp32
+        # loop-invariant context share of every GRU gate (+ gate biases)
         gbias = []
         for gi in range(len(m.update_block.recurrent_block.kernel_size)):
             gb = alloc(f"gru{gi}.cbias", (M, self.gate_cs), self.gate_dtype)
@@ -737,8 +672,7 @@ class RaftEngine:
         plan.add_record(E_CTX)
 
         fmap = alloc("fmap", (2 * B, h, w, self.fmap_ch))
-        E_FE2 = ev0 + 8
-        if self.fe_split and side2 != main:
+        if lanes_on:
             # the feature encoder of image2 on a third lane, concurrent with image1's
             # (and the context encoder): per-image instance norms, so the halves are
             # exact, and the sequential encoder chain that gates the correlation
@@ -774,15 +708,29 @@ class RaftEngine:
         plan.add_wait(E_CTX)
 
         # ---------------- loop body: one refinement iteration (model.py:495-510)
-        # lanes: 0 = lookup -> corr convs -> motion conv -> GRU -> flow head,
-        # 1 = flow-feature convs, 2 = mask head + upsampling (off the critical path)
-        plan.set_segment(1)
-        lane(main)
-        corr = alloc("corr", (M, self.corr_cs))
         me = m.update_block.motion_encoder
         cl, fl = me.corr_layers, me.flow_layers
+        # lookup + convcorr1 as ONE kernel (the corr features stay in LDS) where the
+        # wide lookup applies: bf16 levels with 16-byte chunks never crossing a row
+        fuse_lc = (self._lc1_w is not None and len(cl) == 2 and self._cc1_w is not None and self.corr_dtype == BF16
+                   and L == 4 and all(blocked and l < 2 or ((w >> l) % 8 == 0 and ((h >> l) * (w >> l)) % 8 == 0)
+                                      for l in range(L)))
+        corr = None if fuse_lc else alloc("corr", (M, self.corr_cs))
         cf = alloc("cf", (M, cl[-1] + fl[-1]))
         f1 = alloc("f1", (M, fl[0]))
+        c1 = alloc("c1", (M, cl[0])) if len(cl) == 2 else None
+        taps = alloc("fh2.taps", (M, 24), F32)
+        stride = st.out.shape[1] * H * W * 2  # one iteration of the full-batch output
+        split_mask = lanes_on   # mask predictor's 3x3 conv on the mask lane (else fused into FlowHead conv1)
+        # FlowHead conv1 of the loop: alone (lanes / final-only / no mask head) or
+        # fused with the mask predictor's 3x3 conv (one lane, every iteration upsampled)
+        s1 = sp["fh1"] if (self.has_mask and all_iters and not split_mask) else sp["fh1.flow"] if self.has_mask else sp["fh1"]
+        # the taps epilogue: the 256 FlowHead features never leave the CU
+        taps_epi = self._taps_epi_w is not None and s1.cout == 256
+        fm = None if taps_epi else alloc("fm", (M, round_up(s1.cout, 8)))
+        mfeat = (alloc("mfeat", (M, round_up(sp["mask.convrelu"].cout, 8)))
+                 if self.has_mask and (split_mask or not all_iters) else None)
+        mask = alloc("mask", (M, 576)) if self.has_mask and self._convex_w is None else None
 
         def flow_features():
             if self._cf1_w is not None:
@@ -794,237 +742,128 @@ class RaftEngine:
                 self._conv(plan, sp["me.convflow1"], flow8, B, h, w, f1, act=ACT_RELU)
             self._conv(plan, sp["me.convflow2"], f1, B, h, w, cf, y_coff=cl[-1], act=ACT_RELU)
 
-        split_mask = self.has_mask and all_iters and self.mask_head == "split" and not self.double_buffer
-        # flow_lane "mask": the flow features of iteration i+1 run on the mask lane
-        # right after iteration i's flow update, ahead of iteration i's mask head
-        # (both need only that update), so an iteration has three cross-lane
-        # edges: E_FH (flow update -> mask lane), E_FLOW (flow features -> motion
-        # conv) and E_MASK (mask head done -> first GRU conv, which overwrites the
-        # h the mask head reads; the next flow update, which overwrites flow32,
-        # comes later on the main lane).  Iteration 0's flow features (zero flow)
-        # run once in the prologue.
-        mask_lane_flow = self.flow_lane == "mask" and split_mask and self.flow_head == "taps"
-        side_flow = self.flow_lane == "side" or (self.flow_lane == "mask" and not mask_lane_flow)
-        if mask_lane_flow:
+        def flow_head():
+            """FlowHead conv1 (+ conv2 as per-pixel tap partials into ``taps``)."""
+            if taps_epi:
+                self._conv(plan, s1, hx, B, h, w, taps, act=ACT_RELU, epi=EPI_TAPS, tapw=self._taps_epi_w)
+                return
+            self._conv(plan, s1, hx, B, h, w, fm, act=ACT_RELU)
+            if self._taps_w is not None:   # skinny GEMM kernel (flowhead.hip), N = 18
+                plan.add_taps_gemm([fm, self._taps_w, taps], [M, self.fh_hidden, 0])
+            else:
+                self._conv(plan, sp["fh2.taps"], fm, B, h, w, taps)
+
+        def flow_update():
+            """``coords1 += delta`` (model.py:505) from the taps; flow into hx / qx / flow8."""
+            plan.add_flow_taps([taps, self._fh2_b, coords, flow32, hx, qx, flow8],
+                               [B, h, w, self.flow_off, self.flow_off])
+
+        def upsample(stride, mask_from_fm: bool):
+            """x8 upsampling of flow32 into the output (model.py:508): convex with
+            the mask head (its 3x3 conv from hx, or the fused FlowHead conv1's
+            second half in ``fm``), else bilinear."""
+            if not self.has_mask:
+                plan.add_upsample_bilinear([flow32, out, st.out_slot], [B, h, w, stride, out_off])
+                return
+            if mask_from_fm:
+                feat_, coff = fm, self.fh_hidden
+            else:
+                self._conv(plan, sp["mask.convrelu"], hx, B, h, w, mfeat, act=ACT_RELU)
+                feat_, coff = mfeat, 0
+            if self._convex_w is not None:
+                plan.add_convex_head([feat_, self._convex_w, self._convex_b, flow32, out, st.out_slot],
+                                     [B, h, w, coff, stride, 0, out_off], m.mask_predictor.multiplier)
+            else:   # generic mask head (an injected MaskPredictor): 1x1 conv + convex upsampling
+                st.slot_ok = False
+                self._conv(plan, sp["mask"], feat_, B, h, w, mask, x_coff=coff, alpha=m.mask_predictor.multiplier)
+                plan.add_upsample_convex([mask, flow32, out], [B, h, w, stride])
+
+        def lookup(with_update: bool):
+            upd = [taps, self._fh2_b, flow32, hx, qx, flow8] if with_update else []
+            extra = [self.flow_off, self.flow_off] if with_update else []
+            if fuse_lc:   # + convcorr1 (1x1 + ReLU) into c1
+                plan.add_lookup_cc1([coords, c1] + levels + [None] * (4 - L) + [self._lc1_w, self._cc1_b] + upd,
+                                    [L, B, h, w, self.radius, blocked, self._lc1_kpad, cl[0], 0] + extra)
+                return
+            plan.add_lookup([coords, corr] + levels + [None] * (4 - L) + upd,
+                            [L, B, h, w, self.radius, h * w, blocked] + extra)
+
+        def motion_and_gru(wait_flow: bool, wait_mask: bool):
+            if len(cl) == 2:
+                if fuse_lc:
+                    pass   # convcorr1 ran inside the lookup kernel
+                elif self._cc1_w is not None:   # LDS-resident-weight 1x1 kernel (conv1x1.hip)
+                    plan.add_conv1x1([corr, self._cc1_w, self._cc1_b, c1],
+                                     [M, self.corr_cs, self._cc1_kpad, cl[0], ACT_RELU, 0])
+                else:
+                    self._conv(plan, sp["me.convcorr1"], corr, B, h, w, c1, act=ACT_RELU)
+                self._conv(plan, sp["me.convcorr2"], c1, B, h, w, cf, act=ACT_RELU)
+            else:
+                self._conv(plan, sp["me.convcorr1"], corr, B, h, w, cf, act=ACT_RELU)
+            if wait_flow:
+                plan.add_wait(E_FLOW)
+            self._conv(plan, sp["me.conv"], cf, B, h, w, hx, y_coff=self.mot_off, act=ACT_RELU, y2=qx,
+                       y2_coff=self.mot_off)
+            for gi in range(len(m.update_block.recurrent_block.kernel_size)):
+                # r*h from the bf16 h of the conv's own input hx (no fp32 state read)
+                self._conv(plan, sp[f"gru{gi}.a"], hx, B, h, w, qx, zbuf=zb, hidden=self.hidden,
+                           epi=EPI_GRU_A, bmap=gbias[gi], bmap_coff=0)
+                if gi == 0 and wait_mask:
+                    plan.add_wait(E_MASK)  # the previous iteration's mask head has read h (and flow32)
+                self._conv(plan, sp[f"gru{gi}.b"], qx, B, h, w, hx, h32=h32, zbuf=zb, hidden=self.hidden,
+                           epi=EPI_GRU_B, bmap=gbias[gi], bmap_coff=2 * self.hidden)
+
+        if lanes_on:
+            # iteration 0's flow features (zero flow) run once in the prologue
             plan.set_segment(0)
             lane(main)
             flow_features()
             plan.set_segment(1)
             lane(main)
-        s1 = sp["fh1"] if (all_iters and not split_mask or not self.has_mask) else sp["fh1.flow"]
-        fm_ch = round_up((s1 if split_mask else sp["fh1"]).cout, 8)
-        mfeat = alloc("mfeat", (M, round_up(sp["mask.convrelu"].cout, 8))) if split_mask else None
-        mask = alloc("mask", (M, 576)) if self.has_mask and self.convex == "separate" else None
-        stride = st.out.shape[1] * H * W * 2  # one iteration of the full-batch output
-        taps = alloc("fh2.taps", (M, 24), F32) if self.flow_head == "taps" else None
-
-        # FlowHead conv1 with the taps epilogue: its 256 features never leave the CU
-        # (the mask head reads h, not them, when it is split onto the mask lane)
-        taps_epi = (self.taps_epi and self.flow_head == "taps" and self._taps_epi_w is not None and s1.cout == 256
-                    and (split_mask or not self.has_mask or not all_iters))
-
-        # Deferred flow update (mask-lane schedule + taps epilogue): iteration i's
-        # coordinate update (the 3x3 tap sum) runs inside iteration i+1's lookup
-        # kernel, so the loop body ends with FlowHead conv1; iteration i's flow
-        # features, mask head and upsampling follow that lookup on the mask lane
-        # (deferred ops, Plan.set_defer), and the epilogue applies the last update
-        # and upsamples the last iteration.  One kernel less per iteration on the
-        # critical path (corr.hip:lookup_coords).  Measured and dropped: removing
-        # the E_MASK join by giving the mask head parity copies of h (a second
-        # GRU-B output) and of the flow -- 314 vs 305 us per iteration: the copy
-        # costs the last GRU-B ~4.6 us and the unjoined mask lane slows the
-        # motion / GRU convs it then overlaps.  Also dropped: mask-lane kernels
-        # capped at 62 KB of LDS per block (conv configs filtered, convex-head
-        # weights staged in two halves) so they could share a CU with a 98 KB
-        # critical-lane block: 310 vs 316 pairs/s.
-        defer_update = self.fuse_update and taps_epi and mask_lane_flow and all_iters
-        # the same deferral on one in-order lane (batch < 4 and raft_small): the
-        # update in the lookup, iteration i's flow features right after it, the
-        # upsampling of iteration i-1 next, FlowHead conv1 (+ taps GEMM) last
-        defer_single = (self.fuse_update and self.flow_head == "taps" and all_iters and main == side == side2
-                        and not self.double_buffer)
-        fm_buf = alloc("fm", (M, fm_ch)) if defer_single else None
-
-        def taps_only(fm):
-            if taps_epi:
-                self._conv(plan, s1, hx, B, h, w, taps, act=ACT_RELU, epi=EPI_TAPS, tapw=self._taps_epi_w)
-                return
-            self._conv(plan, s1, hx, B, h, w, fm, act=ACT_RELU)
-            if self._taps_w is not None:
-                plan.add_taps_gemm([fm, self._taps_w, taps], [M, self.fh_hidden, 0])
-            else:
-                self._conv(plan, sp["fh2.taps"], fm, B, h, w, taps)
-
-        def flow_head(fm, f32, before_update=None):
-            if taps_epi:
-                self._conv(plan, s1, hx, B, h, w, taps, act=ACT_RELU, epi=EPI_TAPS, tapw=self._taps_epi_w)
-            else:
-                self._conv(plan, s1, hx, B, h, w, fm, act=ACT_RELU)
-            # flow head conv2 + coordinate update (model.py:505) + flow into hx/qx/flow8
-            if self.flow_head == "taps":
-                if taps_epi:
-                    pass
-                elif self._taps_w is not None:   # skinny GEMM kernel (flowhead.hip), N = 18
-                    plan.add_taps_gemm([fm, self._taps_w, taps], [M, self.fh_hidden, 0])
-                else:
-                    self._conv(plan, sp["fh2.taps"], fm, B, h, w, taps)
-                if before_update is not None:
-                    before_update()
-                plan.add_flow_taps([taps, self._fh2_b, coords, f32, hx, qx, flow8], [B, h, w, self.flow_off, self.flow_off])
-            elif self.flow_head == "fused" and self.fh_hidden in (128, 256):
-                plan.add_flow_head([fm, self._fh2_w, self._fh2_b, coords, f32, hx, qx, flow8],
-                                   [B, h, w, self.fh_hidden, 0, self.flow_off, self.flow_off])
-            else:
-                self._conv(plan, sp["fh2"], fm, B, h, w, hx, y_coff=self.flow_off, y2=qx, y2_coff=self.flow_off,
-                           y3=flow8, y3_coff=0, coords=coords, flow32=f32, epi=EPI_FLOW)
-
-        def upsample(fm, f32, stride):
-            if self.has_mask:
-                if split_mask:
-                    self._conv(plan, sp["mask.convrelu"], hx, B, h, w, mfeat, act=ACT_RELU)
-                    plan.add_record(E_MR)
-                    fm, coff = mfeat, 0
-                else:
-                    coff = self.fh_hidden
-                if self.convex == "head":
-                    plan.add_convex_head([fm, self._convex_w, self._convex_b, f32, out, st.out_slot],
-                                         [B, h, w, coff, stride, 0, out_off], m.mask_predictor.multiplier)
-                elif self.convex in ("fused", "head"):
-                    st.slot_ok = False
-                    # mask logits never leave the CU: softmax + convex combination in the epilogue
-                    self._conv(plan, sp["mask.convex"], fm, B, h, w, out, x_coff=coff, epi=EPI_CONVEX,
-                               flow32=f32, alpha=m.mask_predictor.multiplier, it_stride=stride)
-                else:
-                    st.slot_ok = False
-                    self._conv(plan, sp["mask"], fm, B, h, w, mask, x_coff=coff,
-                               alpha=m.mask_predictor.multiplier)
-                    plan.add_upsample_convex([mask, f32, out], [B, h, w, stride])
-            else:
-                plan.add_upsample_bilinear([f32, out, st.out_slot], [B, h, w, stride, out_off])
-
-        if mask_lane_flow:
-            pass
-        elif side_flow:
-            plan.add_record(E_IT)
-            lane(side)
-            plan.add_wait(E_IT)
-            flow_features()
-            plan.add_record(E_FLOW)
-            lane(main)
-        elif not defer_single:
-            flow_features()
-        c1 = alloc("c1", (M, cl[0])) if len(cl) == 2 else None
-
-        def convcorr1():
-            if self._cc1_w is not None:
-                plan.add_conv1x1([corr, self._cc1_w, self._cc1_b, c1],
-                                 [M, self.corr_cs, self._cc1_kpad, cl[0], ACT_RELU, 0])
-            else:
-                self._conv(plan, sp["me.convcorr1"], corr, B, h, w, c1, act=ACT_RELU)
-
-        cc1_done = False
-        if defer_single:
-            plan.add_lookup([coords, corr] + levels + [None] * (4 - L) + [taps, self._fh2_b, flow32, hx, qx, flow8],
-                            [L, B, h, w, self.radius, h * w, blocked, self.flow_off, self.flow_off])
-            flow_features()
-            plan.set_defer(1)
-            upsample(fm_buf, flow32, stride)   # iteration i-1
-            plan.set_defer(0)
-        elif defer_update:
-            plan.add_lookup([coords, corr] + levels + [None] * (4 - L) + [taps, self._fh2_b, flow32, hx, qx, flow8],
-                            [L, B, h, w, self.radius, h * w, blocked, self.flow_off, self.flow_off])
-            if self.fork_after == "cc1" and c1 is not None:
-                convcorr1()   # the mask lane forks one kernel later
-                cc1_done = True
+            lookup(with_update=True)      # + iteration i-1's flow update
             plan.add_record(E_FH)
             lane(side2)
-            plan.set_defer(1)   # skipped in iteration 0: its flow features ran in the prologue
+            plan.set_defer(1)             # skipped in iteration 0
             plan.add_wait(E_FH)
             flow_features()
             plan.add_record(E_FLOW)
-            upsample(None, flow32, stride)   # iteration i-1 (h still intact: GRU-B waits E_MASK)
+            upsample(stride, mask_from_fm=False)   # iteration i-1 (h intact: GRU-B waits E_MASK)
             plan.add_record(E_MASK)
             plan.set_defer(0)
             lane(main)
-        else:
-            plan.add_lookup([coords, corr] + levels + [None] * (4 - L), [L, B, h, w, self.radius, h * w, blocked])
-        if len(cl) == 2:
-            if not cc1_done:
-                convcorr1()
-            self._conv(plan, sp["me.convcorr2"], c1, B, h, w, cf, act=ACT_RELU)
-        else:
-            self._conv(plan, sp["me.convcorr1"], corr, B, h, w, cf, act=ACT_RELU)
-        if side_flow or mask_lane_flow:
-            plan.add_wait(E_FLOW)
-        self._conv(plan, sp["me.conv"], cf, B, h, w, hx, y_coff=self.mot_off, act=ACT_RELU, y2=qx,
-                   y2_coff=self.mot_off)
-        for gi in range(len(m.update_block.recurrent_block.kernel_size)):
-            # r*h from the bf16 h of the conv's own input hx (no fp32 state read)
-            self._conv(plan, sp[f"gru{gi}.a"], hx, B, h, w, qx, zbuf=zb, hidden=self.hidden,
-                       epi=EPI_GRU_A, bmap=gbias[gi], bmap_coff=0)
-            if gi == 0 and mask_lane_flow:
-                plan.add_wait(E_MASK)  # the previous iteration's mask head has read h (and flow32)
-            elif gi == 0 and split_mask:
-                plan.add_wait(E_MR)  # the previous iteration's mask head has read h
-            self._conv(plan, sp[f"gru{gi}.b"], qx, B, h, w, hx, h32=h32, zbuf=zb, hidden=self.hidden,
-                       epi=EPI_GRU_B, bmap=gbias[gi], bmap_coff=2 * self.hidden)
-        if defer_single:
-            taps_only(fm_buf)
-            plan.set_segment(2)  # epilogue: the last iteration's update and upsampling
-            plan.add_flow_taps([taps, self._fh2_b, coords, flow32, hx, qx, flow8],
-                               [B, h, w, self.flow_off, self.flow_off])
-            plan.set_defer(1)
-            upsample(fm_buf, flow32, stride)
-            plan.set_defer(0)
-        elif defer_update:
+            motion_and_gru(wait_flow=True, wait_mask=True)
+            flow_head()
+            plan.set_segment(2)           # epilogue: the last iteration's update, mask head and upsampling
             lane(main)
-            self._conv(plan, s1, hx, B, h, w, taps, act=ACT_RELU, epi=EPI_TAPS, tapw=self._taps_epi_w)
-            plan.set_segment(2)  # epilogue: the last iteration's update, mask head and upsampling
-            lane(main)
-            plan.add_flow_taps([taps, self._fh2_b, coords, flow32, hx, qx, flow8],
-                               [B, h, w, self.flow_off, self.flow_off])
+            flow_update()
             plan.set_defer(1)
-            upsample(None, flow32, stride)
+            upsample(stride, mask_from_fm=False)
             plan.set_defer(0)
         elif all_iters:
-            # The mask head + upsampling of iteration i run on a side lane while
-            # iteration i+1 proceeds; the flow head's features / flow they read
-            # are double-buffered by iteration parity, so the next flow head
-            # only waits for the mask head of iteration i-1 (same buffers).
-            fms = [alloc("fm", (M, fm_ch))]
-            f32s = [flow32]
-            if self.double_buffer:
-                fms.append(alloc("fm.odd", (M, fm_ch)))
-                f32s.append(alloc("flow32.odd", (M, 2), F32))
-            for par in range(len(fms)):
-                if len(fms) > 1:
-                    plan.set_parity(par)
-                lane(main)
-                if mask_lane_flow:
-                    flow_head(fms[par], f32s[par])   # ordered after the mask lane by E_MASK (first GRU conv)
-                elif split_mask and self.flow_head == "taps":
-                    # the flow head's features are not read by the mask lane: only
-                    # the flow update (flow32) must wait for the last upsampling
-                    flow_head(fms[par], f32s[par], before_update=lambda p=par: plan.add_wait(E_MASK + p))
-                else:
-                    plan.add_wait(E_MASK + par)
-                    flow_head(fms[par], f32s[par])
-                plan.add_record(E_FH)
-                lane(side2)
-                plan.add_wait(E_FH)
-                if mask_lane_flow:
-                    flow_features()   # for the next iteration
-                    plan.add_record(E_FLOW)
-                upsample(fms[par], f32s[par], stride)
-                plan.add_record(E_MASK + par)
-            plan.set_parity(-1)
+            plan.set_segment(1)
+            lane(main)
+            lookup(with_update=True)
+            flow_features()
+            plan.set_defer(1)
+            upsample(stride, mask_from_fm=fm is not None and self.has_mask)   # iteration i-1
+            plan.set_defer(0)
+            motion_and_gru(wait_flow=False, wait_mask=False)
+            flow_head()
+            plan.set_segment(2)
+            flow_update()
+            plan.set_defer(1)
+            upsample(stride, mask_from_fm=fm is not None and self.has_mask)
+            plan.set_defer(0)
         else:
-            fm = alloc("fm", (M, fm_ch))
-            flow_head(fm, flow32)
-            plan.set_segment(2)  # epilogue: upsample the final flow once (out has one iteration)
-            if self.has_mask:
-                self._conv(plan, sp["fh1"], hx, B, h, w, fm, act=ACT_RELU)  # mask head input on the final h
-            upsample(fm, flow32, 0)
+            plan.set_segment(1)
+            lane(main)
+            flow_features()
+            lookup(with_update=False)
+            motion_and_gru(wait_flow=False, wait_mask=False)
+            flow_head()
+            flow_update()
+            plan.set_segment(2)           # epilogue: upsample the final flow once (out has one iteration)
+            upsample(0, mask_from_fm=False)
         lane(main)
 
     # --------------------------------------------------------------- forward
@@ -1047,11 +886,12 @@ class RaftEngine:
         fresh = self.copy_output and st.slot_ok
         out = torch.empty_like(st.out) if fresh else st.out
         self._point_slot(st, out)
-        if len(st.plans) == 1:
-            self._launch(st.plan, num_flow_updates)
-        elif self.use_graph and self.merge_parts:
+        if len(st.plans) == 1 or not self.use_graph:
+            for plan in st.plans:
+                self._launch(plan, num_flow_updates)
+        else:
             # the parts' captures copied into ONE graph (Plan.merge_*): their chains
-            # interleave with no cross-stream edge; separate graphs serialise
+            # interleave with no cross-stream edge (separate graphs serialise)
             p0 = st.plans[0]
             if p0.merged_iters() != num_flow_updates:
                 p0.merge_reset()
@@ -1059,16 +899,6 @@ class RaftEngine:
                     p0.merge_add(plan, num_flow_updates)
                 p0.merge_finish(num_flow_updates)
             p0.replay_pipelined()
-        else:
-            cur = torch.cuda.current_stream(self.device)
-            fork = torch.cuda.Event()
-            fork.record(cur)
-            for plan, strm in zip(st.plans, self._part_streams):
-                strm.wait_event(fork)
-                with torch.cuda.stream(strm):
-                    self._launch(plan, num_flow_updates)
-            for strm in self._part_streams[:len(st.plans)]:
-                cur.wait_stream(strm)
         if fresh:
             return out
         return st.out.clone() if self.copy_output else st.out
@@ -1080,74 +910,6 @@ class RaftEngine:
         if st.slot_ptr != out.data_ptr():
             st.out_slot.fill_(out.data_ptr())
             st.slot_ptr = out.data_ptr()
-
-    # ------------------------------------------------- pipelined (serving)
-    @torch.no_grad()
-    def submit(self, image1: torch.Tensor, image2: torch.Tensor, num_flow_updates: int = 12,
-               return_all_iters: bool = True, depth: int = 2) -> "PendingFlow":
-        """Asynchronous forward for serving loops: batch i's encoders +
-        correlation pyramid (the prologue graph, on a low-priority stream) run
-        concurrently with batch i-1's refinement loop (the loop graph, on a
-        high-priority stream), filling the CUs the latency-bound loop leaves
-        idle.  ``depth`` plan slots (own buffers + graphs) rotate; a slot's
-        prologue waits until the loop that last used it is done.
-
-        The inputs are read on the current stream (copied into the slot); the
-        current stream is never made to wait on the GPU work, so the next
-        submit can be issued at once.  Returns a :class:`PendingFlow`; call
-        ``.wait()`` (orders the current stream after the result) or
-        ``.result()``."""
-        if self._signature() != self._sig:
-            self._pack()
-        B, H, W, C = image1.shape
-        assert C == 3, "images must be NHWC with 3 channels"
-        assert self.use_graph, "submit() replays captured graphs (use_graph=True)"
-        pipe = self._pipe
-        if pipe is None or pipe["depth"] != depth:
-            pipe = self._pipe = dict(
-                depth=depth, n=0,
-                sp=torch.cuda.Stream(device=self.device, priority=0),
-                sl=torch.cuda.Stream(device=self.device, priority=-1),
-                e_in=[torch.cuda.Event() for _ in range(depth)],
-                e_pro=[torch.cuda.Event() for _ in range(depth)],
-                e_loop=[torch.cuda.Event() for _ in range(depth)])
-        slot = pipe["n"] % depth
-        pipe["n"] += 1
-        key = (B, H, W, num_flow_updates, bool(return_all_iters), "slot", slot)
-        st = self._states.get(key)
-        if st is None:
-            saved, self.split = self.split, 1
-            try:
-                st = self._build(B, H, W, num_flow_updates, bool(return_all_iters))
-            finally:
-                self.split = saved
-            self._states[key] = st
-        plan = st.plan
-        cur = torch.cuda.current_stream(self.device)
-        cur.wait_event(pipe["e_pro"][slot])      # the slot's last prologue has read its inputs
-        self._point_slot(st, st.out)
-        st.inp1.copy_(image1)
-        st.inp2.copy_(image2)
-        pipe["e_in"][slot].record(cur)
-        sp, sl = pipe["sp"], pipe["sl"]
-        with torch.cuda.stream(sp):
-            sp.wait_event(pipe["e_in"][slot])
-            sp.wait_event(pipe["e_loop"][slot])  # the slot's last loop is done with its buffers
-            if plan.captured_part_iters(0) != num_flow_updates:
-                plan.capture_part(0, num_flow_updates)
-            plan.replay_part(0)
-            pipe["e_pro"][slot].record(sp)
-        with torch.cuda.stream(sl):
-            sl.wait_event(pipe["e_pro"][slot])
-            if plan.captured_part_iters(1) != num_flow_updates:
-                plan.capture_part(1, num_flow_updates)
-            plan.replay_part(1)
-            out = st.out.clone()
-            pipe["e_loop"][slot].record(sl)
-            done = torch.cuda.Event()
-            done.record(sl)
-        out.record_stream(cur)
-        return PendingFlow(out, done, self.device)
 
     # ------------------------------------- software-pipelined graphs (throughput)
     def _slot_state(self, key, slot: int) -> _PlanState:
@@ -1238,11 +1000,6 @@ class RaftEngine:
         pp["pending"] = None
         pp["n"] = 0
         return out if fresh else (st.out.clone() if self.copy_output else st.out)
-
-    @property
-    def loop_stream(self) -> Optional[torch.cuda.Stream]:
-        """The stream :meth:`submit` replays loop graphs on (None before the first submit)."""
-        return None if self._pipe is None else self._pipe["sl"]
 
     def _launch(self, plan, n_iters: int) -> None:
         if self.use_graph:

@@ -97,8 +97,17 @@ class GradArena:
     hands autograd a fresh copy in ONE kernel, so a later step's in-place
     writes never alias a gradient a caller still holds."""
 
-    def __init__(self, params, device):
+    def __init__(self, params, device, model=None):
         self.params = list(params)
+        # (module, attribute) -> the parameter recorded here: the backward assembles
+        # gradients by module slot, so it needs no live module attribute (under
+        # torch.func.functional_call the slots hold other tensors than after it)
+        self.slots: Dict[tuple, int] = {}
+        if model is not None:
+            for mod in model.modules():
+                for name, t in mod._parameters.items():
+                    if t is not None:
+                        self.slots[(id(mod), name)] = id(t)
         n = sum(p.numel() for p in self.params)
         self.flat = torch.zeros(n, dtype=F32, device=device)
         self.views: Dict[int, torch.Tensor] = {}
@@ -111,6 +120,10 @@ class GradArena:
 
     def __getitem__(self, p) -> torch.Tensor:
         return self.views[id(p)]
+
+    def of(self, module, name: str) -> torch.Tensor:
+        """The gradient view of ``module.<name>`` as recorded at construction."""
+        return self.views[self.slots[(id(module), name)]]
 
     def snapshot(self) -> Dict[int, torch.Tensor]:
         c = self.flat.clone()
@@ -269,7 +282,7 @@ class FusedLoop:
         self._specs: Dict[str, nat.ConvSpec] = {}
         self._pack()
         self.packer = self._pieces()
-        self.arena = GradArena(self.params, self.device)
+        self.arena = GradArena(self.params, self.device, model=self.model)
         self.plan_f = self._build_fwd()
         self.plan_b = self._build_bwd()
 
@@ -722,7 +735,7 @@ class FusedLoop:
 
         def wb(conv, x, x_coff, cin8, dy, yoff=0):
             record_wgrad(P, x, nT, h, w, x_coff, cin8, tuple(conv.kernel.shape), (1, 1), conv.padding, dy, yoff,
-                         A[conv.kernel], A[conv.bias])
+                         A.of(conv, "kernel"), A.of(conv, "bias"))
 
         c1 = me.convcorr1.layers_0
         if len(self.cl) == 2:
@@ -832,24 +845,24 @@ class FusedLoop:
                          gru.padding, Sb, 0, gC, db)
             mot = self.mot_out
             for j, conv in enumerate((gru.convz, gru.convr, gru.convq)):
-                full = A[conv.kernel]
+                full = A.of(conv, "kernel")
                 src = self.gAw[g][..., j * hd:(j + 1) * hd] if j < 2 else self.gBw[g]
                 full[:, :, :hd] = src[:, :, :hd]
                 full[:, :, hd + C:] = src[:, :, hd: hd + mot]
                 full[:, :, hd:hd + C] = gC[..., j * hd:(j + 1) * hd]
-                A[conv.bias].copy_(db[j * hd:(j + 1) * hd])
+                A.of(conv, "bias").copy_(db[j * hd:(j + 1) * hd])
             # context data gradient of this GRU's gates (accumulated over the GRUs)
             tx, ix = _tx(s1=Seg(gin=dctx if g > 0 else None, out=dctx))
             self._conv(None, f"gCT{g}", Sb, dctx, tx=tx, ix=ix, epi=EPI_BWD, hidden=0)
         fhn, mh = self.fh_hidden, self.mask_hidden
-        A[fh.conv1.kernel].copy_(self.fh1w[..., :fhn])
-        A[fh.conv1.bias].copy_(self.fh1b[:fhn])
+        A.of(fh.conv1, "kernel").copy_(self.fh1w[..., :fhn])
+        A.of(fh.conv1, "bias").copy_(self.fh1b[:fhn])
         if self.has_mask:
             mr = mp.convrelu.layers_0
-            A[mr.kernel].copy_(self.fh1w[..., fhn:fhn + mh])
-            A[mr.bias].copy_(self.fh1b[fhn:fhn + mh])
-        A[fh.conv2.kernel].copy_(torch.flip(self.fh2w, dims=(0, 1)).permute(0, 1, 3, 2))
-        A[fh.conv2.bias].copy_(self.ddelta.reshape(-1, 8)[:, :2].sum(0, dtype=F32))
+            A.of(mr, "kernel").copy_(self.fh1w[..., fhn:fhn + mh])
+            A.of(mr, "bias").copy_(self.fh1b[fhn:fhn + mh])
+        A.of(fh.conv2, "kernel").copy_(torch.flip(self.fh2w, dims=(0, 1)).permute(0, 1, 3, 2))
+        A.of(fh.conv2, "bias").copy_(self.ddelta.reshape(-1, 8)[:, :2].sum(0, dtype=F32))
         if fe_dy is not None:   # whole-model path: straight into the feature encoder's bf16 output gradient
             g1, g2 = self._pyramid_backward(fe_dy[: self.B], fe_dy[self.B:])
         else:

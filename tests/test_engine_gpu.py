@@ -145,53 +145,17 @@ def test_final_only_mode_equals_last_iteration(factory, use_graph):
     model = model.cuda()
     i1, i2 = _inputs(2, 128, 128, seed=6)
     i1, i2 = i1.cuda(), i2.cuda()
-    # same flow-head lowering in both modes (at batch 2 the all-iterations plan
-    # runs the fused 512-channel flow + mask conv, which has no taps epilogue)
-    full = model(i1, i2, num_flow_updates=4, use_graph=use_graph, taps_epi=False)
-    last = model(i1, i2, num_flow_updates=4, use_graph=use_graph, return_all_iters=False, taps_epi=False)
+    # batch 2: the all-iterations plan runs one lane with the fused 128 -> 512
+    # FlowHead / mask conv + taps GEMM; final-only runs FlowHead conv1 with the
+    # taps epilogue and the mask conv once (bf16-level differences, raft_large)
+    full = model(i1, i2, num_flow_updates=4, use_graph=use_graph)
+    last = model(i1, i2, num_flow_updates=4, use_graph=use_graph, return_all_iters=False)
     torch.cuda.synchronize()
     assert last.shape == (1,) + tuple(full.shape[1:])
-    assert (last[0] - full[-1]).abs().max().item() < 1e-4
-    # default final-only mode: FlowHead conv1 with the taps epilogue (bf16-level differences)
-    last = model(i1, i2, num_flow_updates=4, use_graph=use_graph, return_all_iters=False)
     mag = full[-1].norm(dim=-1).mean().item()
+    if factory is raft_small:   # same kernels, same order
+        assert (last[0] - full[-1]).abs().max().item() < 1e-4
     assert _epe(last[0], full[-1]) < 1e-2 * mag + 1e-2
-
-
-@pytest.mark.parametrize("flow_head", ["conv", "fused", "taps_gemm"])
-def test_flow_head_modes_agree(flow_head):
-    """The lowerings of FlowHead.conv2 + coords update give the same flows:
-    default = conv1 with the taps epilogue (split mask head, lanes on) vs the
-    3x3 conv, the halo-tiled kernel, and conv1 + the separate taps GEMM."""
-    model, _ = raft_large()
-    model = model.cuda()
-    i1, i2 = _inputs(1, 128, 128, seed=9)
-    i1, i2 = i1.cuda(), i2.cuda()
-    a = model(i1, i2, num_flow_updates=4, streams=True)
-    kw = dict(taps_epi=False) if flow_head == "taps_gemm" else dict(flow_head=flow_head)
-    b = model(i1, i2, num_flow_updates=4, streams=True, **kw)
-    torch.cuda.synchronize()
-    mag = a.norm(dim=-1).mean().item()
-    assert _epe(a[-1], b[-1]) < 0.01 * mag + 0.01
-
-
-
-@pytest.mark.parametrize("final_only", [False, True])
-def test_pipelined_submit_matches_forward(final_only):
-    """Cross-batch pipelining (prologue graph of batch i+1 || loop graph of
-    batch i, two plan slots): every result equals the synchronous forward of
-    the same batch, bitwise (same kernels and tile configs, own buffers)."""
-    model, _ = raft_large()
-    model = model.cuda()
-    eng = model.engine(torch.device("cuda", 0))
-    batches = [tuple(t.cuda() for t in _inputs(2, 128, 160, seed=10 + k)) for k in range(4)]
-    refs = [eng.forward(a, b, 3, return_all_iters=not final_only) for a, b in batches]
-    torch.cuda.synchronize()
-    pend = [eng.submit(a, b, 3, return_all_iters=not final_only) for a, b in batches]
-    outs = [p.result() for p in pend]
-    for r, o in zip(refs, outs):
-        assert o.shape == r.shape
-        assert torch.equal(o, r)
 
 
 @pytest.mark.parametrize("factory,B", [(raft_large, 4), (raft_large, 1), (raft_small, 2)])
@@ -226,42 +190,43 @@ def test_graph_pipelined_matches_forward(factory, B, final_only):
 
 
 def test_split_mask_head_matches_fused():
-    """The mask predictor's 3x3 conv on the mask lane (event-ordered against the
-    next iteration's GRU) gives the same flows as the fused 128->512 flow/mask
-    head GEMM (same math, different GEMM tiling -> bf16 rounding only)."""
+    """The lane schedule (mask predictor's 3x3 conv on the mask lane, event-ordered
+    against the next iteration's GRU; FlowHead taps epilogue) gives the flows of
+    the one-lane schedule (fused 128->512 flow/mask head GEMM + taps GEMM): same
+    math, different GEMM tiling -> bf16 rounding only; lanes graph == eager."""
     model, _ = raft_large()
     model = model.cuda()
     i1, i2 = (t.cuda() for t in _inputs(2, 128, 160, seed=21))
-    a = model(i1, i2, num_flow_updates=6, mask_head="split", streams=True)
-    b = model(i1, i2, num_flow_updates=6, mask_head="fused", streams=True)
-    c = model(i1, i2, num_flow_updates=6, mask_head="split", streams=True, use_graph=False)
+    a = model(i1, i2, num_flow_updates=6, streams=True)
+    b = model(i1, i2, num_flow_updates=6, streams=False)
+    c = model(i1, i2, num_flow_updates=6, streams=True, use_graph=False)
     torch.cuda.synchronize()
     mag = b.norm(dim=-1).mean().item()
     for it in range(6):
         assert _epe(a[it], b[it]) < 0.02 * mag + 0.02, it
-    assert (a - c).abs().max().item() < 1e-3
+    assert torch.equal(a, c)
 
 
 @pytest.mark.parametrize("final_only", [False, True])
-def test_fused_convex_upsample_matches_separate(final_only):
-    """The EPI_CONVEX conv (MaskPredictor 1x1 conv with softmax + convex x8
-    upsampling in its epilogue, sub-pixel-major logits) equals the mask conv +
-    upsample_convex kernel pair, and both track the fp32 golden forward."""
-    model, variables = raft_large()
+def test_generic_mask_head_matches_golden(final_only):
+    """An injected MaskPredictor that is not the 256 -> 576 head (here 128
+    hidden channels) runs the generic lowering (mask conv + upsample_convex
+    kernel) and tracks the fp32 golden forward like the dedicated head."""
+    from jax_raft_amd.models.layers import MaskPredictor
+
+    mp = MaskPredictor(128, hidden_size=128, multiplier=0.25, gen=torch.Generator().manual_seed(5))
+    model, variables = raft_large(mask_predictor=mp)
     i1, i2 = _inputs(2, 128, 160, seed=31)
-    ref = model.apply(variables, i1, i2, num_flow_updates=3)
+    ref = model.apply(variables, i1, i2, num_flow_updates=3, return_all_iters=not final_only)
     model = model.cuda()
-    a = model(i1.cuda(), i2.cuda(), num_flow_updates=3, convex="fused", return_all_iters=not final_only)
-    b = model(i1.cuda(), i2.cuda(), num_flow_updates=3, convex="separate", return_all_iters=not final_only)
-    c = model(i1.cuda(), i2.cuda(), num_flow_updates=3, convex="head", return_all_iters=not final_only)
+    a = model(i1.cuda(), i2.cuda(), num_flow_updates=3, return_all_iters=not final_only)
+    eng = model.engine(torch.device("cuda", 0))
+    assert eng._convex_w is None
     torch.cuda.synchronize()
-    assert a.shape == b.shape == c.shape
+    assert a.shape == ref.shape
     mag = ref.norm(dim=-1).mean().item()
     for it in range(a.shape[0]):
-        assert _epe(a[it], b[it]) < 0.01 * mag + 0.01, it
-        assert _epe(c[it], b[it]) < 0.01 * mag + 0.01, it
-    assert _epe(a[-1].cpu(), ref[-1]) < 0.05 * mag + 0.05
-    assert _epe(c[-1].cpu(), ref[-1]) < 0.05 * mag + 0.05
+        assert _epe(a[it].cpu(), ref[it]) < 0.05 * mag + 0.05, it
 
 
 @pytest.mark.parametrize("tiles", [0, 1, 2])
@@ -347,47 +312,19 @@ def test_engine_split_parts_match_single():
     assert ((a - b).abs().max() / (a.abs().max() + 1e-6)).item() < 1e-2
 
 
-@pytest.mark.parametrize("flow_lane", ["main", "side", "mask"])
-def test_flow_lane_schedules_match(flow_lane):
-    """The lane schedules: flow features on the main lane, on their own side lane
-    or on the mask lane after the flow update (default; it also moves the first
-    GRU's h part onto the mask lane as a bias map, a split of the same sum).
-    Each is graph == eager bitwise and tracks the golden forward; "main" and
-    "side" are the same arithmetic and agree to 1e-3."""
-    from jax_raft_amd import raft_large
-
+def test_lane_schedule_graph_equals_eager_and_tracks_golden():
+    """The lane schedule (flow features + mask head of the previous iteration on
+    the mask lane, three cross-lane events per iteration) is bitwise graph ==
+    eager and tracks the golden forward at every iteration."""
     model, variables = raft_large()
     i1, i2 = _inputs(4, 128, 160, seed=77)
     gold = model.apply(variables, i1, i2, num_flow_updates=5)
     model = model.cuda()
     i1, i2 = i1.cuda(), i2.cuda()
-    a = model(i1, i2, num_flow_updates=5, streams=True, flow_lane=flow_lane)
-    b = model(i1, i2, num_flow_updates=5, streams=True, flow_lane=flow_lane, use_graph=False)
+    a = model(i1, i2, num_flow_updates=5, streams=True)
+    b = model(i1, i2, num_flow_updates=5, streams=True, use_graph=False)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
     mag = gold.norm(dim=-1).mean().item()
     for it in range(5):
         assert _epe(a[it].cpu(), gold[it]) < 0.05 * mag + 0.05, it
-    if flow_lane == "side":
-        c = model(i1, i2, num_flow_updates=5, streams=True, flow_lane="main")
-        torch.cuda.synchronize()
-        assert (a - c).abs().max().item() < 1e-3
-
-
-@pytest.mark.parametrize("factory,streams", [(raft_large, True), (raft_large, False), (raft_small, False)])
-@pytest.mark.parametrize("W", [160, 256])
-def test_update_fused_into_lookup_is_bitwise(W, factory, streams):
-    """Iteration i's flow update inside iteration i+1's lookup kernel (deferred
-    mask head / upsampling, last update in the epilogue) gives bitwise the flows
-    of the separate update kernel: same tap-sum order, same kernels otherwise.
-    W = 160: per-lane lookup kernel; W = 256: wide (blocked-level) kernel.
-    streams=False: the one-lane deferral (batch < 4, raft_small)."""
-    model, _ = factory()
-    model = model.cuda()
-    i1, i2 = _inputs(2, 128, W, seed=21)
-    i1, i2 = i1.cuda(), i2.cuda()
-    for use_graph in (False, True):
-        a = model(i1, i2, num_flow_updates=5, streams=streams, use_graph=use_graph)
-        b = model(i1, i2, num_flow_updates=5, streams=streams, use_graph=use_graph, fuse_update=False)
-        torch.cuda.synchronize()
-        assert torch.equal(a, b), (use_graph, (a - b).abs().max().item())

@@ -1,0 +1,114 @@
+"""CPU checks of the inference engine's plan lowering (runtime/engine.py): the
+op sequence each schedule records, without a GPU (a recording stand-in for
+the native Plan; weights packed on the CPU).  The numerics of the same plans
+are covered on the MI355X by tests/test_engine_gpu.py."""
+import pytest
+import torch
+
+from jax_raft_amd import raft_large, raft_small
+from jax_raft_amd.ops import native as nat
+from jax_raft_amd.runtime import engine as E
+from jax_raft_amd.runtime import tunedb
+
+
+class FakePlan:
+    """Records (segment, lane, defer, op) for every add_* call."""
+
+    def __init__(self):
+        self.ops = []
+        self.seg, self.ln, self.defer = 0, 0, 0
+
+    def set_segment(self, s):
+        self.seg = s
+
+    def set_lane(self, l):
+        self.ln = l
+
+    def set_defer(self, d):
+        self.defer = d
+
+    def __getattr__(self, name):
+        if not name.startswith("add_"):
+            raise AttributeError(name)
+
+        def rec(*args):
+            self.ops.append((self.seg, self.ln, self.defer, name[4:], args))
+        return rec
+
+    def names(self, seg):
+        return [op for s, _, _, op, _ in self.ops if s == seg]
+
+
+@pytest.fixture
+def fake(monkeypatch):
+    monkeypatch.setattr(nat, "require", lambda: None)
+    monkeypatch.setattr(nat, "new_plan", FakePlan)
+    monkeypatch.setattr(tunedb, "gpu_arch", lambda device=None: "cpu")
+
+
+def _plan(factory, B, all_iters=True, streams="auto", H=128, W=256):
+    model = factory()[0].eval()
+    eng = E.RaftEngine(model, "cpu", autotune=False, streams=streams)
+    st = eng._build(B, H, W, 3, all_iters)
+    return eng, st.plan
+
+
+def test_lane_schedule_raft_large(fake):
+    eng, p = _plan(raft_large, 4)
+    assert eng.uses_lanes(4) and not eng.uses_lanes(1) and not eng.uses_lanes(4, all_iters=False)
+    loop = [(ln, d, op) for s, ln, d, op, _ in p.ops if s == 1]
+    ops = [op for _, _, op in loop]
+    # critical lane: lookup (+ update) -> cc1 (LDS kernel) -> cc2 -> motion -> 2 x GRU(A, B) -> FlowHead taps
+    assert ops.count("lookup") == 1 and ops.count("flow_taps") == 0
+    assert [op for ln, d, op in loop if ln == 0 and op not in ("record", "wait")] == \
+        ["lookup", "conv1x1", "conv", "conv", "conv", "conv", "conv", "conv", "conv"]
+    # mask lane: deferred flow features + mask conv + convex head of the previous iteration
+    side = [op for ln, d, op in loop if ln == 2 and op not in ("record", "wait")]
+    assert side == ["conv_direct", "conv", "conv", "convex_head"]
+    assert all(d == 1 for ln, d, op in loop if ln == 2 and op not in ("record", "wait"))
+    assert p.names(2).count("flow_taps") == 1 and p.names(2).count("convex_head") == 1
+    # three cross-lane waits per iteration
+    assert ops.count("wait") == 3
+
+
+@pytest.mark.parametrize("factory", [raft_large, raft_small])
+def test_one_lane_schedule(factory, fake):
+    eng, p = _plan(factory, 1)
+    assert not eng.uses_lanes(1)
+    loop = [(ln, d, op) for s, ln, d, op, _ in p.ops if s == 1]
+    assert {ln for ln, _, _ in loop} == {0} and not any(op in ("record", "wait") for _, _, op in loop)
+    ops = [op for _, _, op in loop]
+    assert ops[0] == "lookup" and "flow_taps" not in ops   # the update runs inside the lookup
+    up = "convex_head" if factory is raft_large else "upsample_bilinear"
+    assert ops.count(up) == 1 and [d for _, d, op in loop if op == up] == [1]
+    assert "taps_gemm" in ops   # raft_large: fused 128 -> 512 FlowHead/mask conv + taps GEMM
+    assert p.names(2) == ["flow_taps", up]
+
+
+@pytest.mark.parametrize("factory", [raft_large, raft_small])
+def test_final_only_schedule(factory, fake):
+    eng, p = _plan(factory, 4, all_iters=False)
+    ops = p.names(1)
+    assert "flow_taps" in ops and "convex_head" not in ops and "upsample_bilinear" not in ops
+    ep = p.names(2)
+    assert ep[-1] == ("convex_head" if factory is raft_large else "upsample_bilinear")
+
+
+@pytest.mark.parametrize("B", [1, 4])
+def test_headline_shape_fuses_lookup_and_convcorr1(fake, B):
+    """At 440x1024 (55 x 128 feature maps: blocked bf16 levels) the lookup and
+    MotionEncoder.convcorr1 run as one kernel (corr.hip:lookup_cc1_kernel)."""
+    eng, p = _plan(raft_large, B, H=440, W=1024)
+    ops = p.names(1)
+    assert "lookup_cc1" in ops and "lookup" not in ops and "conv1x1" not in ops
+    # fp32 pyramid: no fusion (the fused kernel reads bf16 levels)
+    eng = E.RaftEngine(raft_large()[0].eval(), "cpu", autotune=False, corr_dtype=torch.float32)
+    st = eng._build(B, 440, 1024, 2, True)
+    assert "lookup_cc1" not in st.plan.names(1) and "lookup" in st.plan.names(1)
+
+
+def test_engine_knobs_are_few(fake):
+    import inspect
+
+    params = [n for n in inspect.signature(E.RaftEngine.__init__).parameters if n not in ("self", "model", "device")]
+    assert len(params) <= 10, params

@@ -143,34 +143,6 @@ def test_gru_fused_epilogues(hidden, xin, ks, pad, cfg):
     assert (hx[:, :hidden].float().cpu() - ref.reshape(M, hidden)).abs().max().item() < 2.5e-2
 
 
-@pytest.mark.parametrize("cfg", [None, 5, 11, 3, 9, 15, 25, 28])
-def test_flow_epilogue(cfg):
-    nat = _nat()
-    torch.manual_seed(3)
-    B, h, w, cin = 2, 9, 10, 256
-    M = B * h * w
-    x = torch.randn(B, h, w, cin)
-    k = torch.randn(3, 3, cin, 2) / math.sqrt(9 * cin)
-    b = torch.randn(2) * 0.1
-    delta = R.conv2d_nhwc(_bf(x), _bf(k), b, (1, 1), (1, 1))
-    c0 = R.make_coords_grid(B, h, w)
-    c1 = c0 + torch.randn(B, h, w, 2)
-    spec = nat.make_spec(k, b, (1, 1), (1, 1), device=DEV)
-    coords = c1.reshape(M, 2).to(DEV).contiguous()
-    flow32 = torch.zeros(M, 2, device=DEV)
-    hx = torch.zeros(M, 16, dtype=torch.bfloat16, device=DEV)
-    f8 = torch.zeros(M, 8, dtype=torch.bfloat16, device=DEV)
-    xg = x.to(DEV, torch.bfloat16).contiguous()
-    nat.ops().conv(*nat.conv_args(spec, xg, B, h, w, hx, y_coff=14, y3=f8, coords=coords, flow32=flow32,
-                                  epi=nat.EPI_FLOW, cfg=cfg))
-    torch.cuda.synchronize()
-    new = c1 + delta
-    assert (coords.cpu().reshape(B, h, w, 2) - new).abs().max() < 2e-3
-    assert (flow32.cpu().reshape(B, h, w, 2) - (new - c0)).abs().max() < 2e-3
-    assert (hx[:, 14:16].float().cpu() - (new - c0).reshape(M, 2)).abs().max() < 5e-2
-    assert (f8[:, :2].float().cpu() - (new - c0).reshape(M, 2)).abs().max() < 5e-2
-
-
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("h,w,C,L", [(16, 16, 64, 4), (23, 37, 128, 4), (55, 128, 256, 4), (17, 20, 64, 2),
                                      (13, 48, 64, 3)])
@@ -282,39 +254,6 @@ def test_instance_norm_stats_apply(C):
     torch.cuda.synchronize()
     ref2 = torch.relu(R.instance_norm_nhwc(x) + r)
     assert (y2.float().cpu() - ref2).abs().max().item() < 3e-2
-
-
-@pytest.mark.parametrize("cin", [256, 128])
-def test_flow_head_fused(cin):
-    """flow_head (flowhead.hip) = FlowHead.conv2 (3x3, cin -> 2) + coords update + flow copies."""
-    nat = _nat()
-    torch.manual_seed(7)
-    B, h, w = 2, 9, 70          # w not a multiple of the 32-pixel wave segment
-    M = B * h * w
-    fcs, coff = cin + 64, 32    # channel slice of a wider buffer, like the fused fh1+mask1 output
-    fm = torch.randn(B, h, w, fcs) * 0.5
-    k = torch.randn(3, 3, cin, 2) / math.sqrt(9 * cin)
-    b = torch.randn(2) * 0.1
-    coords = torch.randn(M, 2) * 5
-    delta = R.conv2d_nhwc(_bf(fm[..., coff:coff + cin]), _bf(k), b, (1, 1), (1, 1)).reshape(M, 2)
-    new = coords + delta
-    grid = torch.stack(torch.meshgrid(torch.arange(w).float(), torch.arange(h).float(), indexing="xy"), -1)
-    flow_ref = new - grid[None].expand(B, h, w, 2).reshape(M, 2)
-    fmg = fm.reshape(M, fcs).to(DEV, torch.bfloat16).contiguous()
-    cg = coords.to(DEV).contiguous()
-    f32 = torch.zeros(M, 2, device=DEV)
-    hx = torch.zeros(M, 24, device=DEV, dtype=torch.bfloat16)
-    qx = torch.zeros(M, 24, device=DEV, dtype=torch.bfloat16)
-    f8 = torch.zeros(M, 8, device=DEV, dtype=torch.bfloat16)
-    wt = k.permute(3, 0, 1, 2).reshape(2, 9, cin).to(DEV, torch.bfloat16).contiguous()
-    nat.ops().flow_head([fmg, wt, b.to(DEV), cg, f32, hx, qx, f8], [B, h, w, cin, coff, 16, 8])
-    torch.cuda.synchronize()
-    tol = 1e-3 * flow_ref.abs().max().item() + 1e-3
-    assert (cg.cpu() - new).abs().max().item() < tol
-    assert (f32.cpu() - flow_ref).abs().max().item() < tol
-    assert (hx[:, 16:18].float().cpu() - flow_ref).abs().max().item() < 0.02 * flow_ref.abs().max().item() + 1e-2
-    assert torch.equal(hx[:, 16:18], qx[:, 8:10]) and torch.equal(hx[:, 16:18], f8[:, :2])
-    assert (hx[:, :16] == 0).all() and (hx[:, 18:] == 0).all()
 
 
 @pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34,
@@ -524,6 +463,107 @@ def test_corr_blocked_layout_pyramid_and_lookup(h, w, L, radius):
     assert err < 3e-2 * want.abs().max().item(), err
 
 
+@pytest.mark.parametrize("blocked,w", [(1, 64), (0, 20)])
+def test_lookup_with_fused_update_is_bitwise(blocked, w):
+    """The flow update fused into the lookup (corr.hip: lookup_coords; the engine
+    runs iteration i's update inside iteration i+1's lookup) = the separate
+    flow_taps kernel followed by the plain lookup, bitwise: coordinates, flow
+    copies and sampled features (wide blocked-level kernel and per-lane kernel)."""
+    nat = _nat()
+    torch.manual_seed(19)
+    B, h, C, L, radius = 2, 16, 64, 4, 4
+    M = B * h * w
+    g1 = torch.randn(B, h, w, C).to(DEV, torch.bfloat16)
+    g2 = torch.randn(B, h, w, C).to(DEV, torch.bfloat16)
+    nty, ntx = -(-h // 8), -(-w // 16)
+    lv, hl, wl = [], h, w
+    for l in range(L):
+        shape = (M, nty * (8 >> l), ntx * (16 >> l)) if (blocked and l < 2) else (M, hl, wl)
+        lv.append(torch.zeros(shape, device=DEV, dtype=torch.bfloat16))
+        hl //= 2
+        wl //= 2
+    nat.ops().corr([g1, g2] + lv, [B, h, w, C, L, h * w, blocked], 1.0 / math.sqrt(C))
+    taps = (torch.randn(M, 24) * 2).to(DEV)
+    bias = torch.randn(2).to(DEV)
+    coords0 = (R.make_coords_grid(B, h, w).reshape(M, 2) + torch.randn(M, 2) * 3).to(DEV)
+    S = 2 * radius + 1
+    ocs = nat.round_up(L * S * S, 8)
+    res = []
+    for fused in (False, True):
+        coords = coords0.clone()
+        f32 = torch.zeros(M, 2, device=DEV)
+        hx = torch.zeros(M, 24, device=DEV, dtype=torch.bfloat16)
+        qx = torch.zeros(M, 24, device=DEV, dtype=torch.bfloat16)
+        f8 = torch.zeros(M, 2, device=DEV, dtype=torch.bfloat16)
+        out = torch.zeros(M, ocs, device=DEV, dtype=torch.bfloat16)
+        if fused:
+            nat.ops().lookup([coords, out] + lv + [taps, bias, f32, hx, qx, f8], [L, B, h, w, radius, h * w, blocked, 16, 8])
+        else:
+            nat.ops().flow_taps([taps, bias, coords, f32, hx, qx, f8], [B, h, w, 16, 8])
+            nat.ops().lookup([coords, out] + lv, [L, B, h, w, radius, h * w, blocked])
+        torch.cuda.synchronize()
+        res.append((coords, f32, hx, qx, f8, out))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B,h,w,radius", [(1, 55, 128, 4), (2, 16, 64, 4), (3, 24, 48, 3)])
+@pytest.mark.parametrize("update", [False, True])
+def test_lookup_cc1_matches_lookup_then_conv1x1(B, h, w, radius, update):
+    """The fused lookup + convcorr1 kernel (corr.hip:lookup_cc1_kernel, features
+    kept in LDS) = the wide lookup kernel followed by the 1x1 conv kernel on the
+    same packed weights: the same bf16 features and the same MFMA k order, so
+    the outputs (and, with the fused flow update, coords / flow copies) are
+    bitwise equal; both match the fp32 reference composition."""
+    nat = _nat()
+    torch.manual_seed(23)
+    C, L = 64, 4
+    S = 2 * radius + 1
+    M = B * h * w
+    blocked = int(w % 16 == 0)
+    g1 = torch.randn(B, h, w, C).to(DEV, torch.bfloat16)
+    g2 = torch.randn(B, h, w, C).to(DEV, torch.bfloat16)
+    nty, ntx = -(-h // 8), -(-w // 16)
+    lv, hl, wl = [], h, w
+    for l in range(L):
+        shape = (M, nty * (8 >> l), ntx * (16 >> l)) if (blocked and l < 2) else (M, hl, wl)
+        lv.append(torch.zeros(shape, device=DEV, dtype=torch.bfloat16))
+        hl //= 2
+        wl //= 2
+    nat.ops().corr([g1, g2] + lv, [B, h, w, C, L, h * w, blocked], 1.0 / math.sqrt(C))
+    K = L * S * S
+    kpad = nat.round_up(K, 32)
+    kern = torch.randn(1, 1, K, 256) / math.sqrt(K)
+    bias = (torch.randn(256) * 0.1).to(DEV)
+    wpk = nat.pack_conv1x1(kern.to(DEV), kpad)
+    coords0 = (R.make_coords_grid(B, h, w).reshape(M, 2) + torch.randn(M, 2) * 4).to(DEV)
+    taps = (torch.randn(M, 24) * 2).to(DEV)
+    fb = torch.randn(2).to(DEV)
+    res = []
+    for fused in (False, True):
+        coords = coords0.clone()
+        f32 = torch.zeros(M, 2, device=DEV)
+        hx = torch.zeros(M, 24, device=DEV, dtype=torch.bfloat16)
+        y = torch.full((M, 264), 7.0, device=DEV, dtype=torch.bfloat16)
+        upd = [taps, fb, f32, hx, None, None] if update else []
+        extra = [16, 0] if update else []
+        if fused:
+            nat.ops().lookup_cc1([coords, y] + lv + [wpk, bias] + upd, [L, B, h, w, radius, blocked, kpad, 256, 8] + extra)
+        else:
+            corr = torch.zeros(M, nat.round_up(K, 8), device=DEV, dtype=torch.bfloat16)
+            nat.ops().lookup([coords, corr] + lv + upd, [L, B, h, w, radius, h * w, blocked] + extra)
+            kp = next(k for k in nat.CONV1X1_KPADS if k >= corr.shape[1])
+            wc = nat.pack_conv1x1(kern.to(DEV), kp)
+            nat.ops().conv1x1([corr, wc, bias, y], [M, corr.shape[1], kp, 256, nat.ACT_RELU, 8])
+        torch.cuda.synchronize()
+        res.append((coords, f32, hx, y))
+    (c0, f0, h0, y0), (c1, f1, h1, y1) = res
+    assert torch.equal(c0, c1) and torch.equal(f0, f1) and torch.equal(h0, h1)
+    assert (y1[:, :8] == 7.0).all()
+    err = (y1[:, 8:264].float() - y0[:, 8:264].float()).abs().max().item()
+    assert err <= 1e-2 * y0[:, 8:264].float().abs().max().item(), err
+
+
 @pytest.mark.parametrize("K,cs,coff,M", [(256, 256, 0, 1000), (256, 512, 0, 28160), (128, 136, 8, 777)])
 def test_taps_gemm_matches_fp32(K, cs, coff, M):
     """flowhead.hip taps GEMM (the flow head's 3x3 output conv as 9 x 2 per-pixel
@@ -585,27 +625,3 @@ def test_conv_taps_epilogue(cfg):
     out = taps.cpu()
     assert _rel(out[:, :18], ref) < 5e-3
     assert (out[:, 18:] == 7.0).all()
-
-
-@pytest.mark.parametrize("N,H,W,cin,cout", [(2, 9, 64, 64, 64), (1, 6, 128, 128, 128), (2, 5, 64, 64, 96),
-                                            (1, 4, 192, 128, 64)])
-def test_conv_halo_matches_reference(N, H, W, cin, cout):
-    """conv_halo.hip (config 44): 3x3 / s1 / p1 with the LDS input halo, against
-    fp32 torch; bias + relu + residual epilogue and bf16 output as in the encoders."""
-    nat = _nat()
-    torch.manual_seed(12)
-    x = torch.randn(N, H, W, cin)
-    k = torch.randn(3, 3, cin, cout) / math.sqrt(9 * cin)
-    b = torch.randn(cout) * 0.1
-    res = torch.randn(N, H, W, cout)
-    spec = nat.make_spec(k, b, (1, 1), (1, 1), device=DEV)
-    assert nat.halo_ok(spec, W)
-    xg = x.to(DEV, torch.bfloat16).contiguous()
-    base = R.conv2d_nhwc(_bf(x), _bf(k), b, (1, 1), (1, 1))
-    y = nat.conv2d(spec, xg, out_dtype=torch.float32, cfg=nat.HALO_CFG)
-    torch.cuda.synchronize()
-    assert _rel(y.cpu(), base) < 2e-3
-    rg = res.to(DEV, torch.bfloat16).contiguous()
-    y = nat.conv2d(spec, xg, act=nat.ACT_RELU, out_dtype=torch.bfloat16, res=rg, res_post=1, cfg=nat.HALO_CFG)
-    torch.cuda.synchronize()
-    assert _rel(y.float().cpu(), torch.relu(torch.relu(base) + _bf(res))) < 1e-2

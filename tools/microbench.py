@@ -128,16 +128,15 @@ def main():
         res["lookup"] = {"us": us}
         print(f"lookup       {us:8.1f} us")
     if not args.only or "flowhead" in args.only:
-        fm = rnd(M, 512)
-        wt = (torch.randn(2, 9, 256, device=dev) * 0.02).to(torch.bfloat16)
+        taps = torch.randn(M, 24, device=dev)
         bias = torch.zeros(2, device=dev)
         coords = torch.zeros(M, 2, device=dev)
         f32 = torch.zeros(M, 2, device=dev)
         hx = rnd(M, 400)
         f8 = rnd(M, 8)
-        us = timeit(lambda: nat.ops().flow_head([fm, wt, bias, coords, f32, hx, hx, f8], [B, h, w, 256, 0, 382, 382]))
-        res["flow_head"] = {"us": us}
-        print(f"flow_head    {us:8.1f} us")
+        us = timeit(lambda: nat.ops().flow_taps([taps, bias, coords, f32, hx, hx, f8], [B, h, w, 382, 382]))
+        res["flow_taps"] = {"us": us}
+        print(f"flow_taps    {us:8.1f} us")
     if not args.only or "upsample" in args.only:
         mask = rnd(M, 576)
         flow = torch.randn(M, 2, device=dev)
