@@ -308,6 +308,8 @@ def main():
     ap.add_argument("--extras", default="auto", choices=["auto", "on", "off"],
                     help="secondary configs after the headline (auto: on for the default headline config)")
     ap.add_argument("--extra-steps", type=int, default=20)
+    ap.add_argument("--train-batch", type=int, default=6, help="extras: training batch per GPU (config 5: 6)")
+    ap.add_argument("--train-size", type=int, nargs=2, default=[384, 512], help="extras: training image size")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL on ROCm) for real runs; gloo only to rehearse >1 rank on fewer GPUs")
     args = ap.parse_args()
@@ -362,8 +364,9 @@ def main():
                 print(f"bench.py: extra {key} failed: {type(e).__name__}: {e}", file=sys.stderr)
             torch.cuda.empty_cache()
         try:
-            extras["train_pairs_per_s"] = run_training(ctx, arch="raft_large", B=6, size=(384, 512), iters=12,
-                                                       steps=max(5, ks // 2), warmup=3)
+            extras["train_pairs_per_s"] = run_training(ctx, arch="raft_large", B=args.train_batch,
+                                                       size=tuple(args.train_size), iters=12,
+                                                       steps=max(2, ks // 2), warmup=3)
         except Exception as e:  # noqa: BLE001
             extras["train_pairs_per_s"] = None
             print(f"bench.py: extra train_pairs_per_s failed: {type(e).__name__}: {e}", file=sys.stderr)

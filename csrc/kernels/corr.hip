@@ -544,7 +544,7 @@ __global__ __launch_bounds__(256) void corr_lookup_wide_kernel(LevelPtrs lv, int
 // one launch from the loop's critical path.
 //   * lookup phase: the wide kernel's scheme (aligned 16-byte window chunks
 //     into a per-wave LDS window image, taps read from LDS), QPW = 2 queries
-//     per pass, the next pass's chunk loads issued before this pass's taps;
+//     per pass, the chunk loads of the next 4 passes in flight (rolling);
 //     the optional flow update of the previous iteration runs per pass
 //     (lookup_coords);
 //   * KROW = KS * 32 + 16 elements: the tile row stride is 8 dwords mod 16,
@@ -615,8 +615,6 @@ __global__ __launch_bounds__(256, 2) void lookup_cc1_kernel(LevelPtrs lv, int nl
       }
     }
   };
-  float cxa[QPW], cya[QPW], cxb[QPW], cyb[QPW];
-  u32x4 va[NL], vb[NL];
   auto consume = [&](int pass, const float (&qcx)[QPW], const float (&qcy)[QPW], const u32x4 (&v)[NL]) {
 #pragma unroll
     for (int n = 0; n < NL; ++n) {
@@ -654,15 +652,17 @@ __global__ __launch_bounds__(256, 2) void lookup_cc1_kernel(LevelPtrs lv, int nl
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
-  issue(0, cxa, cya, va);
+  // the window chunks of up to D passes in flight at once (a rolling window:
+  // the phase is gather-latency-bound at 2 blocks / CU)
+  constexpr int D = NPASS < 4 ? NPASS : 4;
+  float cxs[NPASS][QPW], cys[NPASS][QPW];
+  u32x4 vs[NPASS][NL];
 #pragma unroll
-  for (int p = 0; p < NPASS; p += 2) {
-    if (p + 1 < NPASS) issue(p + 1, cxb, cyb, vb);
-    consume(p, cxa, cya, va);
-    if (p + 1 < NPASS) {
-      if (p + 2 < NPASS) issue(p + 2, cxa, cya, va);
-      consume(p + 1, cxb, cyb, vb);
-    }
+  for (int p = 0; p < D; ++p) issue(p, cxs[p], cys[p], vs[p]);
+#pragma unroll
+  for (int p = 0; p < NPASS; ++p) {
+    consume(p, cxs[p], cys[p], vs[p]);
+    if (p + D < NPASS) issue(p + D, cxs[p + D], cys[p + D], vs[p + D]);
   }
   __syncthreads();   // the B tile is complete
 
@@ -879,7 +879,7 @@ extern "C" int jr_corr_lookup(const void* const* levels, int num_levels, int B, 
 }
 
 // Fused lookup + convcorr1 (lookup_cc1_kernel): bf16 levels in a layout the
-// wide lookup reads, radius 3 / 4 with kpad = 224 / 352 (L = 4), cout = 256.
+// wide lookup reads, radius 4 with kpad = 352 (L = 4: raft_large), cout = 256.
 extern "C" int jr_lookup_cc1(const void* const* levels, int num_levels, int B, int h, int w, int radius,
                              const float* coords, int blocked, const void* wpk, int kpad, const float* bias, void* y,
                              int y_cstride, int y_coff, int cout, hipStream_t stream, const TapsUpd* upd) {
@@ -910,7 +910,6 @@ extern "C" int jr_lookup_cc1(const void* const* levels, int num_levels, int B, i
     return (int)hipGetLastError();                                                                                  \
   }
   JR_LC(4, 11)
-  JR_LC(3, 7)
 #undef JR_LC
   return (int)hipErrorInvalidValue;
 }

@@ -152,7 +152,7 @@ int jr_corr_lookup(const void* const* levels, int num_levels, int B, int h, int 
 
 // Fused lookup + MotionEncoder.convcorr1 (1x1 conv + ReLU): the lookup's
 // features stay in LDS as the GEMM operand.  Levels bf16 (wide-lookup layout),
-// nq == h * w, radius 3 / 4 with kpad = 224 / 352 (L = 4) and cout = 256;
+// nq == h * w, radius 4 with kpad = 352 (L = 4) and cout = 256;
 // weights packed by ops/native.py:pack_conv1x1(kernel, kpad); y bf16 channels
 // [y_coff, y_coff + 256) of [B*h*w][y_cstride].  upd: as jr_corr_lookup.
 int jr_lookup_cc1(const void* const* levels, int num_levels, int B, int h, int w, int radius, const float* coords,

@@ -185,13 +185,13 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
     TORCH_CHECK(p.cout == 256 && p.y_coff == 0 && p.y_cstride >= 18 && p.y_cstride % 4 == 0 && !bmap.defined() &&
                     !res.defined() && reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
                 "TAPS: 256 channels in, fp32 taps [M][>=18] out, no bias map / residual");
-    TORCH_CHECK(cfg == 22 || cfg == 34 || cfg == 35 || cfg == 38, "TAPS: tile config ", cfg,
+    TORCH_CHECK(cfg == 22 || cfg == 34 || cfg == 35 || cfg == 38 || cfg == 47, "TAPS: tile config ", cfg,
                 " is not a 256-channel 16-wave 64x32 tiling");
     p.tapw = tapw.data_ptr();
   } else {
     TORCH_CHECK(false, "conv: unknown epilogue ", epi);
   }
-  TORCH_CHECK(cfg >= 0 && cfg <= 43 && !(cfg >= 29 && cfg <= 32), "conv: unknown tile config ", cfg);
+  TORCH_CHECK(cfg >= 0 && cfg <= 50 && !(cfg >= 29 && cfg <= 32), "conv: unknown tile config ", cfg);
   if (tx) conv_train_extras(p, epi, *tx, *ix, keep);
   if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3, bmap, tapw}) if (v.defined()) keep->push_back(v);
   return [p, epi, cfg](hipStream_t s, int) { return jr_conv_forward(&p, cfg, epi, s); };
@@ -650,7 +650,7 @@ static Launch make_lookup_cc1(const TList& t, const IList& i, std::vector<at::Te
   const int kpad = (int)i[6], cout = (int)i[7], y_coff = (int)i[8];
   const int S = 2 * r + 1, nty = (h + 7) / 8, ntx = (w + 15) / 16;
   const int64_t M = (int64_t)B * h * w;
-  TORCH_CHECK(L >= 1 && L <= 4 && (r == 3 || r == 4), "lookup_cc1: radius 3 / 4, 1..4 levels");
+  TORCH_CHECK(L >= 1 && L <= 4 && r == 4, "lookup_cc1: radius 4, 1..4 levels");
   TORCH_CHECK(cout == 256 && kpad % 32 == 0 && kpad >= L * S * S && kpad - L * S * S < 32 &&
                   wpk.numel() == (int64_t)kpad * cout && bias.numel() >= cout, "lookup_cc1: packed weights / bias");
   TORCH_CHECK(cs(y) % 8 == 0 && y_coff % 8 == 0 && y_coff + cout <= cs(y) && y.numel() >= M * cs(y), "lookup_cc1: y");

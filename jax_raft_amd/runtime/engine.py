@@ -301,7 +301,7 @@ class RaftEngine:
         S = 2 * self.radius + 1
         kf = round_up(self.num_levels * S * S, 32)
         if (cc1.kernel.shape[:2] == (1, 1) and cc1.kernel.shape[3] == 256 and self.num_levels <= 4
-                and (self.radius, kf) in ((4, 352), (3, 224))):
+                and (self.radius, kf) == (4, 352)):
             wl = nat.pack_conv1x1(cc1.kernel.to(self.device), kf)
             if self._lc1_w is None:
                 self._lc1_w, self._lc1_kpad = wl, kf

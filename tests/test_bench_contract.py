@@ -48,3 +48,21 @@ def test_bench_two_ranks_gloo_one_json_line():
     assert len(recs) == 1, r.stdout  # rank 0 only
     rec = recs[0]
     assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 2 and rec["config"]["parallelism"] == "dp2"
+    # the communication of the DP path: world check, per-rank step times, the final-flow gather
+    assert rec["rccl_world"] == 2 and len(rec["per_rank_ms_per_step"]) == 2
+    assert rec["gather_ms"] is not None and rec["gather_ms"] > 0 and rec["config"]["result_gather"]
+
+
+@pytest.mark.gpu
+def test_bench_extras_keys():
+    """--extras on: the secondary configs land in the same JSON line (each a
+    record or null), here at a small size so the test stays short."""
+    r = subprocess.run([sys.executable, "bench.py", "--extras", "on", "--extra-steps", "2", "--train-batch", "1",
+                        "--train-size", "128", "256"] + SMALL, cwd=ROOT,
+                       env=_env(), capture_output=True, text=True, timeout=115)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = _json_lines(r.stdout)[0]
+    ex = rec["extras"]
+    assert set(ex) >= {"b1_fps", "small_b1_fps_32it", "small_b1_fps_12it", "train_pairs_per_s", "extras_wall_s"}
+    for k in ("b1_fps", "small_b1_fps_32it", "small_b1_fps_12it", "train_pairs_per_s"):
+        assert ex[k] is not None and ex[k]["value"] > 0, (k, r.stderr[-1500:])

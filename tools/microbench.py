@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--json", default="")
     ap.add_argument("--gemm", action="store_true", help="also time the equivalent plain GEMM on hipBLASLt")
     ap.add_argument("--ablate", default="", help="comma list of cfgs: also time them with X / W / both loads dropped")
+    ap.add_argument("--encoder", action="store_true",
+                    help="time the encoder convs instead (raft_large FE half at batch 4: 4 images of 440x1024)")
     args = ap.parse_args()
     nat.require()
     dev = "cuda"
@@ -71,39 +73,57 @@ def main():
         ("fh2", 256, 256, 2, 3, 3, (1, 1)),
         ("mask2", 256, 256, 576, 1, 1, (0, 0)),
     ]
-    for name, cin, cs, cout, kh, kw, pad in convs:
+    if args.encoder:   # name, cin, cs, cout, kh, kw, pad, stride, input H, W
+        convs = [("stem7x7s2", 3, 8, 64, 7, 7, (3, 3), 2, 440, 1024),
+                 ("l1.3x3.64", 64, 64, 64, 3, 3, (1, 1), 1, 220, 512),
+                 ("l2.3x3s2.96", 64, 64, 96, 3, 3, (1, 1), 2, 220, 512),
+                 ("l2.3x3.96", 96, 96, 96, 3, 3, (1, 1), 1, 110, 256),
+                 ("l2.ds1x1s2", 64, 64, 96, 1, 1, (0, 0), 2, 220, 512),
+                 ("l3.3x3s2.128", 96, 96, 128, 3, 3, (1, 1), 2, 110, 256),
+                 ("l3.3x3.128", 128, 128, 128, 3, 3, (1, 1), 1, 55, 128),
+                 ("head1x1.256", 128, 128, 256, 1, 1, (0, 0), 1, 55, 128)]
+    else:
+        convs = [c + (1, h, w) for c in convs]
+    for name, cin, cs, cout, kh, kw, pad, st, H_, W_ in convs:
         if args.only and args.only not in name:
             continue
         k = torch.randn(kh, kw, cin, cout) / math.sqrt(kh * kw * cin)
         b = torch.randn(cout) * 0.1
-        spec = nat.make_spec(k, b, (1, 1), pad, cin8=cs, device=dev)
-        x = rnd(B, h, w, cs)
-        y = torch.empty(M, nat.round_up(cout, 8), device=dev, dtype=torch.bfloat16)
-        flops = 2.0 * M * cout * kh * kw * cin
+        spec = nat.make_spec(k, b, (st, st), pad, cin8=cs, device=dev)
+        x = rnd(B, H_, W_, cs)
+        OH, OW = spec.out_hw(H_, W_)
+        Mo = B * OH * OW
+        y = torch.empty(Mo, nat.round_up(cout, 8), device=dev, dtype=torch.bfloat16)
+        flops = 2.0 * Mo * cout * kh * kw * cin
         row = {}
         bm = torch.randn(M, 384, device=dev) if name.startswith("gru") else None
         for cfg in nat.TUNE_CFGS:
-            t, i, a = nat.conv_args(spec, x, B, h, w, y, act=nat.ACT_RELU, cfg=cfg, bmap=bm)
+            t, i, a = nat.conv_args(spec, x, B, H_, W_, y, act=nat.ACT_RELU, cfg=cfg, bmap=bm)
             us = timeit(lambda: nat.ops().conv(t, i, a))
             row[cfg] = us
         best = min(row, key=row.get)
         for cfg in [int(c) for c in args.ablate.split(",") if c]:
             parts = []
             for ab, nm in ((1, "noX"), (2, "noW"), (3, "noXW")):
-                t, i, a = nat.conv_args(spec, x, B, h, w, y, act=nat.ACT_RELU, cfg=cfg)
+                t, i, a = nat.conv_args(spec, x, B, H_, W_, y, act=nat.ACT_RELU, cfg=cfg)
                 i = list(i)
                 i[20] = cfg | (ab << 8)
                 parts.append(f"{nm}={timeit(lambda: nat.ops().conv(t, i, a)):6.1f}")
             print(f"{'':12s} ablate c{cfg}: full={row[cfg]:6.1f} " + " ".join(parts), flush=True)
         if args.gemm:  # same M x K x N as a library GEMM (no im2col, no epilogue): a yardstick
             K = kh * kw * cin
-            a_ = rnd(M, K)
+            a_ = rnd(Mo, K)
             b_ = rnd(K, cout)
             g_us = timeit(lambda: torch.matmul(a_, b_))
-            print(f"{'':12s} hipBLASLt {M}x{K}x{cout}: {g_us:7.1f} us {flops / g_us / 1e6:7.1f} TF/s")
-        res[name] = {"us": row, "best_cfg": best, "tflops": flops / row[best] / 1e6, "heuristic": nat.pick_cfg(M, cout)}
+            print(f"{'':12s} hipBLASLt {Mo}x{K}x{cout}: {g_us:7.1f} us {flops / g_us / 1e6:7.1f} TF/s")
+        res[name] = {"us": row, "best_cfg": best, "tflops": flops / row[best] / 1e6, "heuristic": nat.pick_cfg(Mo, cout)}
         print(f"{name:12s} " + " ".join(f"c{c}={u:7.1f}" for c, u in row.items()) +
-              f"  best=c{best} {flops / row[best] / 1e6:7.1f} TF/s  heur=c{nat.pick_cfg(M, cout)}", flush=True)
+              f"  best=c{best} {flops / row[best] / 1e6:7.1f} TF/s  heur=c{nat.pick_cfg(Mo, cout)}", flush=True)
+    if args.encoder:
+        if args.json:
+            with open(args.json, "w") as fh:
+                json.dump(res, fh, indent=1)
+        return
 
     # ------------------------------------------------------------- correlation
     if not args.only or "corr" in args.only or "lookup" in args.only:
