@@ -994,7 +994,7 @@ JR_DEVICE void raw_barrier() {
 // with the FAST im2col loader (ConvParams::fast) are the configs that compete
 // with kernels R / P on the refinement-loop convs (configs 35..39).
 // ---------------------------------------------------------------------------
-template <int BCO, int BP, int WCO, int NS, int EPI, bool FAST = false, int NW = 4, int PIPE = 0>
+template <int BCO, int BP, int WCO, int NS, int EPI, bool FAST = false, int NW = 4>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW > 4 || (BCO + BP) * NS * 128 > 81920 ? 1 : 2))) void conv_d2_kernel(const ConvParams p) {
   constexpr int WP = NW / WCO;
   constexpr int WTCO = BCO / WCO;
@@ -1150,53 +1150,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, NW >
   for (int s = 0; s < NS - 1; ++s) issue();
   wait_vmcnt<(NS - 2) * PPW>();
   raw_barrier();
-  if constexpr (PIPE == 1) {
-    // Kernel DP: the D2 ring with the MFMA fragments double-buffered in
-    // registers at half-stage (32-deep K) granularity, as kernel P: the second
-    // half's LDS reads overlap the first half's MFMAs, and the next stage's
-    // first half is read right after the barrier that publishes it, while the
-    // second half's MFMAs of this stage drain.  With 1-2 waves per SIMD (wide
-    // wave tiles: few LDS bytes per MFMA) nothing else hides those reads.
-    auto rdfrag = [&](int buf, int kk, bf16x8 (&af)[TM], bf16x8 (&bfr)[TN]) {
-      const bf16* sA = smem + buf * STAGE;
-      const bf16* sB = sA + BCO * BK;
-      const int chunk = kk * 4 + lq;
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm) {
-        const int row = wco * WTCO + tm * 16 + li;
-        af[tm] = *(const bf16x8*)(sA + row * BK + ((chunk ^ (row & 6)) << 3));
-      }
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn) {
-        const int row = wp * WTP + tn * 16 + li;
-        bfr[tn] = *(const bf16x8*)(sB + row * BK + ((chunk ^ (row & 6)) << 3));
-      }
-    };
-    auto mma = [&](const bf16x8 (&af)[TM], const bf16x8 (&bfr)[TN]) {
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tm], bfr[tn], acc[tm][tn], 0, 0, 0);
-    };
-    bf16x8 fa[TM], fb[TN], ga[TM], gb[TN];
-    rdfrag(0, 0, fa, fb);
-    for (int ks = 0; ks < nks; ++ks) {
-      issue();                        // stage ks+NS-1 into the buffer stage ks-1 used (read before the last barrier)
-      rdfrag(ks % NS, 1, ga, gb);     // second half of stage ks
-      mma(fa, fb);                    // first half
-      wait_vmcnt<(NS - 2) * PPW>();   // stage ks+1 has landed
-      raw_barrier();
-      if (ks + 1 < nks) rdfrag((ks + 1) % NS, 0, fa, fb);
-      mma(ga, gb);
-    }
-  } else {
-    for (int ks = 0; ks < nks; ++ks) {
-      issue();                      // stage ks+NS-1 into the buffer stage ks-1 used
-      compute(ks % NS);             // stage ks
-      wait_vmcnt<(NS - 2) * PPW>(); // stage ks+1 has landed (stages ks+2.. may still fly)
-      raw_barrier();
-    }
+  for (int ks = 0; ks < nks; ++ks) {
+    issue();                      // stage ks+NS-1 into the buffer stage ks-1 used
+    compute(ks % NS);             // stage ks
+    wait_vmcnt<(NS - 2) * PPW>(); // stage ks+1 has landed (stages ks+2.. may still fly)
+    raw_barrier();
   }
   wait_vmcnt<0>();
 
@@ -1225,11 +1183,6 @@ int launch_cfg(const ConvParams* p, int epi, hipStream_t s) {
     if (p->fast) hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, true, NW_>), grid, dim3(NW_ * 64), 0, s, *p); \
     else hipLaunchKernelGGL((conv_igemm_kernel<BCO, BP, WCO, E, false, NW_>), grid, dim3(NW_ * 64), 0, s, *p);         \
   } else if constexpr (KIND == 3 || KIND == 4) hipLaunchKernelGGL((conv_d2_kernel<BCO, BP, WCO, KIND - 1, E>), grid, block, 0, s, *p); \
-  else if constexpr (KIND >= 15 && KIND <= 18) {                                              \
-    constexpr int NW_ = KIND == 15 ? 4 : (KIND == 17 ? 16 : 8), NS_ = KIND == 18 ? 2 : 3;       \
-    if (p->fast) hipLaunchKernelGGL((conv_d2_kernel<BCO, BP, WCO, NS_, E, true, NW_, 1>), grid, dim3(NW_ * 64), 0, s, *p); \
-    else hipLaunchKernelGGL((conv_d2_kernel<BCO, BP, WCO, NS_, E, false, NW_, 1>), grid, dim3(NW_ * 64), 0, s, *p);         \
-  }                                                                                             \
   else if constexpr (KIND >= 12 && KIND <= 14) {                                              \
     constexpr int NW_ = KIND == 13 ? 8 : 16, NS_ = KIND == 14 ? 2 : 3;                          \
     if (p->fast) hipLaunchKernelGGL((conv_d2_kernel<BCO, BP, WCO, NS_, E, true, NW_>), grid, dim3(NW_ * 64), 0, s, *p); \
@@ -1252,7 +1205,7 @@ int launch_cfg(const ConvParams* p, int epi, hipStream_t s) {
     case EPI_BWD: JR_LAUNCH(EPI_BWD) break;
     case EPI_TAPS:
       // one N tile of 256 channels, 16 waves of 64 x 32 (configs 22, 34, 35, 38)
-      if constexpr (BCO == 256 && BP == 128 && WCO == 4 && (KIND == 7 || KIND == 11 || KIND == 12 || KIND == 14 || KIND == 17)) {
+      if constexpr (BCO == 256 && BP == 128 && WCO == 4 && (KIND == 7 || KIND == 11 || KIND == 12 || KIND == 14)) {
         if (p->cout != 256) return (int)hipErrorInvalidValue;
         JR_LAUNCH(EPI_TAPS) break;
       } else {

@@ -8,7 +8,6 @@ extern "C" int jr_conv_family_p(const ConvParams* p, int cfg, int epi, hipStream
 extern "C" int jr_conv_family_m32(const ConvParams* p, int cfg, int epi, hipStream_t stream);
 extern "C" int jr_conv_family_d2(const ConvParams* p, int cfg, int epi, hipStream_t stream);
 extern "C" int jr_conv_family_g(const ConvParams* p, int cfg, int epi, hipStream_t stream);
-extern "C" int jr_conv_family_dp(const ConvParams* p, int cfg, int epi, hipStream_t stream);
 
 extern "C" int jr_conv_forward(const ConvParams* p, int cfg, int epi, hipStream_t stream) {
   if (p->M <= 0) return 0;
@@ -18,6 +17,5 @@ extern "C" int jr_conv_forward(const ConvParams* p, int cfg, int epi, hipStream_
   if (r == -1) r = jr_conv_family_m32(p, cfg, epi, stream);
   if (r == -1) r = jr_conv_family_d2(p, cfg, epi, stream);
   if (r == -1) r = jr_conv_family_g(p, cfg, epi, stream);
-  if (r == -1) r = jr_conv_family_dp(p, cfg, epi, stream);
   return r == -1 ? (int)hipErrorInvalidValue : r;
 }

@@ -532,196 +532,6 @@ __global__ __launch_bounds__(256) void corr_lookup_wide_kernel(LevelPtrs lv, int
   }
 }
 
-// ---------------------------------------------------------------------------
-// Fused pyramid lookup + MotionEncoder.convcorr1 (SURVEY K6 + K7a; reference
-// index_pyramid model.py:448-470 feeding the 1x1 conv + ReLU of :275): the
-// radius-r samples of a block's NQ queries are written straight into an LDS
-// B tile [NQ][KROW] (the GEMM operand, never stored to HBM), then the 1x1 conv
-// K = L(2r+1)^2 -> 4 x 64 channels runs on MFMA from that tile: wave g owns
-// output channels [64 g, 64 g + 64) of all NQ queries, its A fragments (the
-// conv1x1.hip packing) streamed from L2 two k-steps ahead.  This removes the
-// corr-feature round trip (write + re-read of M x 328 bf16 per iteration) and
-// one launch from the loop's critical path.
-//   * lookup phase: the wide kernel's scheme (aligned 16-byte window chunks
-//     into a per-wave LDS window image, taps read from LDS), QPW = 2 queries
-//     per pass, the chunk loads of the next 4 passes in flight (rolling);
-//     the optional flow update of the previous iteration runs per pass
-//     (lookup_coords);
-//   * KROW = KS * 32 + 16 elements: the tile row stride is 8 dwords mod 16,
-//     so every ds_read_b128 lane group of the B-fragment reads hits 16
-//     distinct 4-bank groups (conflict-free);
-//   * epilogue: bias + ReLU, each lane two 16-byte stores of 16 contiguous
-//     channels (pack-time row permutation).
-// ---------------------------------------------------------------------------
-template <int R, int KS, int NQ>
-__global__ __launch_bounds__(256, 2) void lookup_cc1_kernel(LevelPtrs lv, int nlev, int total, int h, int w,
-                                                            const float* coords, LvGeom geo, TapsUpd upd,
-                                                            const u32x4* __restrict__ wpk,
-                                                            const float* __restrict__ bias, bf16* __restrict__ y,
-                                                            int ycs, int ycoff) {
-  using T = bf16;
-  constexpr int S = 2 * R + 1;
-  constexpr int EPC = 8;                                // bf16 elements per 16-byte chunk
-  constexpr int NCH = (S + 1 + EPC - 1) / EPC + 1;      // chunks per window row
-  constexpr int RW = NCH * EPC;                         // window image row length
-  constexpr int QPW = 2;
-  constexpr int NT = QPW * 4 * (S + 1) * NCH;           // chunk loads per pass per wave
-  constexpr int NL = (NT + 63) / 64;
-  constexpr int QW = NQ / 4;                            // queries per wave
-  constexpr int NPASS = QW / QPW;
-  constexpr int KROW = KS * 32 + 16;
-  constexpr int NC = NQ / 16;                           // 16-query column tiles
-  static_assert(QW % QPW == 0 && NQ % 16 == 0, "NQ");
-  __shared__ __attribute__((aligned(16))) bf16 smem[NQ * KROW + 4 * NT * EPC];
-  bf16* Bt = smem;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  T* win = smem + NQ * KROW + wave * NT * EPC;          // [QPW][4][S+1][RW]
-  const int qb = blockIdx.x * NQ;
-
-  // this wave's A fragments (output group g = wave) for the first two k-steps
-  const u32x4* ap = wpk + (long)wave * KS * 4 * 64 + lane;
-  u32x4 a0[4], a1[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) a0[t] = ap[t * 64];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) a1[t] = KS > 1 ? ap[(4 + t) * 64] : u32x4{0u, 0u, 0u, 0u};
-
-  // zero the K padding columns [nlev S^2, 32 KS) of every row
-  const int kval = nlev * S * S;
-  for (int e = tid; e < NQ * (KS * 32 - kval); e += 256) {
-    const int r = e / (KS * 32 - kval), c = kval + e % (KS * 32 - kval);
-    Bt[r * KROW + c] = f2bf(0.f);
-  }
-
-  // ---- lookup phase
-  auto issue = [&](int pass, float (&qcx)[QPW], float (&qcy)[QPW], u32x4 (&v)[NL]) {
-    const int q0 = qb + wave * QW + pass * QPW;
-    lookup_coords<QPW>(upd, coords, q0, total, h, w, lane, qcx, qcy);
-#pragma unroll
-    for (int n = 0; n < NL; ++n) {
-      const int t = n * 64 + lane;
-      v[n] = u32x4{0u, 0u, 0u, 0u};
-      const int k = t % NCH, j = (t / NCH) % (S + 1), l = (t / (NCH * (S + 1))) % 4, u = t / (NCH * (S + 1) * 4);
-      const int q = q0 + u;
-      const float ucx = u == 0 ? qcx[0] : qcx[1], ucy = u == 0 ? qcy[0] : qcy[1];
-      if (t < NT && q < total && l < nlev) {
-        const float sc = 1.0f / (float)(1 << l);
-        const int hl = h >> l, wl = w >> l;
-        const int col0 = (int)floorf(ucx * sc) - R;
-        const int rr = (int)floorf(ucy * sc) - R + j;
-        const int cc = (col0 >= 0 ? col0 / EPC : -((-col0 + EPC - 1) / EPC)) * EPC + k * EPC;
-        if ((unsigned)rr < (unsigned)hl && (unsigned)cc < (unsigned)wl)
-          v[n] = *(const u32x4*)((const T*)lv.p[l] + (long)q * lv_qstride(geo, l, hl, wl) + lv_off(geo, l, wl, rr, cc));
-      }
-    }
-  };
-  auto consume = [&](int pass, const float (&qcx)[QPW], const float (&qcy)[QPW], const u32x4 (&v)[NL]) {
-#pragma unroll
-    for (int n = 0; n < NL; ++n) {
-      const int t = n * 64 + lane;
-      if (t < NT) ((u32x4*)win)[t] = v[n];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int l = lane >> 4, i = lane & 15;
-    if (l < nlev && i < S) {
-      const float sc = 1.0f / (float)(1 << l);
-#pragma unroll
-      for (int u = 0; u < QPW; ++u) {
-        const int row = wave * QW + pass * QPW + u;
-        const float cx = qcx[u] * sc, cy = qcy[u] * sc;
-        const float flx = floorf(cx), fly = floorf(cy);
-        const float fx = cx - flx, fy = cy - fly;
-        const int col0 = (int)flx - R;
-        const int o = col0 - (col0 >= 0 ? col0 / EPC : -((-col0 + EPC - 1) / EPC)) * EPC;
-        const T* wr = win + ((u * 4 + l) * (S + 1)) * RW + o + i;
-        float x0 = to_f(wr[0]), x1 = to_f(wr[1]);
-        bf16* dst = Bt + row * KROW + l * S * S + i * S;
-#pragma unroll
-        for (int j = 0; j < S; ++j) {
-          const float b0 = to_f(wr[(j + 1) * RW]), b1 = to_f(wr[(j + 1) * RW + 1]);
-          const float top = (1.f - fx) * x0 + fx * x1, bot = (1.f - fx) * b0 + fx * b1;
-          dst[j] = f2bf((1.f - fy) * top + fy * bot);
-          x0 = b0;
-          x1 = b1;
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
-  // the window chunks of up to D passes in flight at once (a rolling window:
-  // the phase is gather-latency-bound at 2 blocks / CU)
-  constexpr int D = NPASS < 4 ? NPASS : 4;
-  float cxs[NPASS][QPW], cys[NPASS][QPW];
-  u32x4 vs[NPASS][NL];
-#pragma unroll
-  for (int p = 0; p < D; ++p) issue(p, cxs[p], cys[p], vs[p]);
-#pragma unroll
-  for (int p = 0; p < NPASS; ++p) {
-    consume(p, cxs[p], cys[p], vs[p]);
-    if (p + D < NPASS) issue(p + D, cxs[p + D], cys[p + D], vs[p + D]);
-  }
-  __syncthreads();   // the B tile is complete
-
-  // ---- GEMM phase: wave g -> channels [64 g, 64 g + 64) x NQ queries
-  const int col = lane & 15, q4 = lane >> 4;
-  f32x4 acc[4][NC];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int c = 0; c < NC; ++c) acc[t][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    u32x4 b[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) b[c] = *(const u32x4*)(Bt + (c * 16 + col) * KROW + ks * 32 + 8 * q4);
-    u32x4 a[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) a[t] = (ks & 1) ? a1[t] : a0[t];
-    if (ks + 2 < KS) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        if (ks & 1) a1[t] = ap[((ks + 2) * 4 + t) * 64];
-        else a0[t] = ap[((ks + 2) * 4 + t) * 64];
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-        acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[t]),
-                                                            __builtin_bit_cast(bf16x8, b[c]), acc[t][c], 0, 0, 0);
-  }
-  // lane (col, q4): channels 64 g + 16 q4 + (4 t + j) <- acc[t][c][j] (pack_conv1x1 row permutation)
-  const int c0 = wave * 64 + 16 * q4;
-  float bv[16];
-#pragma unroll
-  for (int i = 0; i < 16; i += 4) {
-    const float4 t4 = *(const float4*)(bias + c0 + i);
-    bv[i] = t4.x; bv[i + 1] = t4.y; bv[i + 2] = t4.z; bv[i + 3] = t4.w;
-  }
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const int m = qb + 16 * c + col;
-    if (m >= total) continue;
-    bf16x8 o0, o1;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float v = fmaxf(acc[t][c][j] + bv[4 * t + j], 0.f);
-        if (t < 2) o0[4 * t + j] = f2bf(v);
-        else o1[4 * (t - 2) + j] = f2bf(v);
-      }
-    bf16* yp = y + (long)m * ycs + ycoff + c0;
-    *(bf16x8*)yp = o0;
-    *(bf16x8*)(yp + 8) = o1;
-  }
-}
-
 // Backward of the lookup w.r.t. the pyramid levels: grad_out [q][ocs]
 // (channel l*S^2 + i*S + j) -> dlevels fp32 [q][hl][wl] (accumulated).
 // Lane (level, i) folds the bilinear weights of its (2r+1) samples into the
@@ -876,42 +686,6 @@ extern "C" int jr_corr_lookup(const void* const* levels, int num_levels, int B, 
   if (lv_bf16)
     return launch_lookup<bf16>(lv, num_levels, total, h, w, radius, coords, (bf16*)out, out_cstride, geo, u, stream);
   return launch_lookup<float>(lv, num_levels, total, h, w, radius, coords, (bf16*)out, out_cstride, geo, u, stream);
-}
-
-// Fused lookup + convcorr1 (lookup_cc1_kernel): bf16 levels in a layout the
-// wide lookup reads, radius 4 with kpad = 352 (L = 4: raft_large), cout = 256.
-extern "C" int jr_lookup_cc1(const void* const* levels, int num_levels, int B, int h, int w, int radius,
-                             const float* coords, int blocked, const void* wpk, int kpad, const float* bias, void* y,
-                             int y_cstride, int y_coff, int cout, hipStream_t stream, const TapsUpd* upd) {
-  const int S = 2 * radius + 1;
-  if (num_levels < 1 || num_levels > 4 || cout != 256 || y_cstride % 8 || y_coff % 8 || kpad % 32 ||
-      kpad < num_levels * S * S || kpad - num_levels * S * S >= 32)
-    return (int)hipErrorInvalidValue;
-  TapsUpd u{};
-  if (upd && upd->on) {
-    if (!upd->taps || upd->tcs < 18 || !upd->bias || upd->coords != coords || !upd->flow32 || !upd->hx)
-      return (int)hipErrorInvalidValue;
-    u = *upd;
-  }
-  LevelPtrs lv;
-  for (int l = 0; l < 4; ++l) lv.p[l] = l < num_levels ? levels[l] : nullptr;
-  const LvGeom geo{blocked, (h + TY - 1) / TY, (w + TX - 1) / TX};
-  if (!lookup_wide_ok<bf16>(lv, num_levels, h, w, geo)) return (int)hipErrorInvalidValue;
-  const int total = B * h * w;
-  const bool big = total >= 256 * 64;   // 64 queries per block once that still fills the chip
-#define JR_LC(RR, KS_)                                                                                              \
-  if (radius == RR && kpad == 32 * KS_) {                                                                           \
-    if (big)                                                                                                        \
-      hipLaunchKernelGGL((lookup_cc1_kernel<RR, KS_, 64>), dim3((total + 63) / 64), dim3(256), 0, stream, lv,      \
-                         num_levels, total, h, w, coords, geo, u, (const u32x4*)wpk, bias, (bf16*)y, y_cstride, y_coff); \
-    else                                                                                                            \
-      hipLaunchKernelGGL((lookup_cc1_kernel<RR, KS_, 32>), dim3((total + 31) / 32), dim3(256), 0, stream, lv,      \
-                         num_levels, total, h, w, coords, geo, u, (const u32x4*)wpk, bias, (bf16*)y, y_cstride, y_coff); \
-    return (int)hipGetLastError();                                                                                  \
-  }
-  JR_LC(4, 11)
-#undef JR_LC
-  return (int)hipErrorInvalidValue;
 }
 
 extern "C" int jr_corr_lookup_bwd(void* const* dlevels, int num_levels, int B, int h, int w, int nq, int radius,

@@ -150,15 +150,6 @@ int jr_corr_lookup(const void* const* levels, int num_levels, int B, int h, int 
                    const float* coords, void* out, int out_cstride, int lv_bf16, int blocked, hipStream_t stream,
                    const TapsUpd* upd = nullptr);
 
-// Fused lookup + MotionEncoder.convcorr1 (1x1 conv + ReLU): the lookup's
-// features stay in LDS as the GEMM operand.  Levels bf16 (wide-lookup layout),
-// nq == h * w, radius 4 with kpad = 352 (L = 4) and cout = 256;
-// weights packed by ops/native.py:pack_conv1x1(kernel, kpad); y bf16 channels
-// [y_coff, y_coff + 256) of [B*h*w][y_cstride].  upd: as jr_corr_lookup.
-int jr_lookup_cc1(const void* const* levels, int num_levels, int B, int h, int w, int radius, const float* coords,
-                  int blocked, const void* wpk, int kpad, const float* bias, void* y, int y_cstride, int y_coff,
-                  int cout, hipStream_t stream, const TapsUpd* upd = nullptr);
-
 // Backward of jr_corr_lookup w.r.t. the levels: accumulates into fp32 dlevels
 // (same shapes as the levels).  gout: bf16 (g_bf16=1) or fp32 [B*nq][gcs].
 int jr_corr_lookup_bwd(void* const* dlevels, int num_levels, int B, int h, int w, int nq, int radius,

@@ -185,13 +185,13 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
     TORCH_CHECK(p.cout == 256 && p.y_coff == 0 && p.y_cstride >= 18 && p.y_cstride % 4 == 0 && !bmap.defined() &&
                     !res.defined() && reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
                 "TAPS: 256 channels in, fp32 taps [M][>=18] out, no bias map / residual");
-    TORCH_CHECK(cfg == 22 || cfg == 34 || cfg == 35 || cfg == 38 || cfg == 47, "TAPS: tile config ", cfg,
+    TORCH_CHECK(cfg == 22 || cfg == 34 || cfg == 35 || cfg == 38, "TAPS: tile config ", cfg,
                 " is not a 256-channel 16-wave 64x32 tiling");
     p.tapw = tapw.data_ptr();
   } else {
     TORCH_CHECK(false, "conv: unknown epilogue ", epi);
   }
-  TORCH_CHECK(cfg >= 0 && cfg <= 50 && !(cfg >= 29 && cfg <= 32), "conv: unknown tile config ", cfg);
+  TORCH_CHECK(cfg >= 0 && cfg <= 43 && !(cfg >= 29 && cfg <= 32), "conv: unknown tile config ", cfg);
   if (tx) conv_train_extras(p, epi, *tx, *ix, keep);
   if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3, bmap, tapw}) if (v.defined()) keep->push_back(v);
   return [p, epi, cfg](hipStream_t s, int) { return jr_conv_forward(&p, cfg, epi, s); };
@@ -639,63 +639,6 @@ static Launch make_lookup(const TList& t, const IList& i, std::vector<at::Tensor
   };
 }
 
-// Fused lookup + convcorr1 (jr_lookup_cc1):
-// t = [coords, y, l0, l1, l2, l3, wpk, bias, (taps, fbias, flow32, hx, qx?, flow8?)],
-// i = [num_levels, B, h, w, radius, blocked, kpad, cout, y_coff, (hx_off, qx_off)]
-static Launch make_lookup_cc1(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
-  at::Tensor coords = opt(t, 0), y = opt(t, 1), wpk = opt(t, 6), bias = opt(t, 7);
-  check_f32(coords, "coords"); check_bf16(y, "y"); check_bf16(wpk, "wpk"); check_f32(bias, "bias");
-  TORCH_CHECK(i.size() == 9 || i.size() == 11, "lookup_cc1: expected 9 or 11 ints");
-  const int L = (int)i[0], B = (int)i[1], h = (int)i[2], w = (int)i[3], r = (int)i[4], blocked = (int)i[5];
-  const int kpad = (int)i[6], cout = (int)i[7], y_coff = (int)i[8];
-  const int S = 2 * r + 1, nty = (h + 7) / 8, ntx = (w + 15) / 16;
-  const int64_t M = (int64_t)B * h * w;
-  TORCH_CHECK(L >= 1 && L <= 4 && r == 4, "lookup_cc1: radius 4, 1..4 levels");
-  TORCH_CHECK(cout == 256 && kpad % 32 == 0 && kpad >= L * S * S && kpad - L * S * S < 32 &&
-                  wpk.numel() == (int64_t)kpad * cout && bias.numel() >= cout, "lookup_cc1: packed weights / bias");
-  TORCH_CHECK(cs(y) % 8 == 0 && y_coff % 8 == 0 && y_coff + cout <= cs(y) && y.numel() >= M * cs(y), "lookup_cc1: y");
-  TORCH_CHECK(coords.numel() >= 2 * M, "lookup_cc1: coords");
-  std::vector<const void*> lv(4, nullptr);
-  int hl = h, wl = w;
-  for (int l = 0; l < L; ++l) {
-    at::Tensor v = opt(t, 2 + l);
-    check_level(v, at::kBFloat16);
-    TORCH_CHECK(hl >= 2 && wl >= 2, "lookup_cc1: pyramid level too small");
-    const int64_t per_q = (blocked && l < 2) ? (int64_t)nty * ntx * (128 >> (2 * l)) : (int64_t)hl * wl;
-    TORCH_CHECK(v.numel() >= M * per_q, "lookup_cc1: level size");
-    lv[l] = v.data_ptr();
-    if (keep) keep->push_back(v);
-    hl >>= 1; wl >>= 1;
-  }
-  if (keep) for (auto& v : {coords, y, wpk, bias}) keep->push_back(v);
-  TapsUpd upd{};
-  at::Tensor tp = opt(t, 8);
-  if (tp.defined()) {
-    at::Tensor fb = opt(t, 9), f32 = opt(t, 10), hx = opt(t, 11), qx = opt(t, 12), f8 = opt(t, 13);
-    TORCH_CHECK(i.size() == 11, "lookup_cc1: the fused flow update needs [.., hx_off, qx_off]");
-    check_f32(tp, "taps"); check_f32(fb, "bias"); check_f32(f32, "flow32"); check_bf16(hx, "hx");
-    const int hx_off = (int)i[9], qx_off = (int)i[10];
-    TORCH_CHECK(cs(tp) >= 18 && tp.numel() >= M * cs(tp) && fb.numel() >= 2 && f32.numel() >= 2 * M,
-                "lookup_cc1: taps [M][>=18], bias [2], flow32 [M][2]");
-    TORCH_CHECK(hx.numel() >= M * cs(hx) && hx_off + 2 <= cs(hx), "lookup_cc1: hx");
-    if (qx.defined()) { check_bf16(qx, "qx"); TORCH_CHECK(qx.numel() >= M * cs(qx) && qx_off + 2 <= cs(qx), "lookup_cc1: qx"); }
-    if (f8.defined()) { check_bf16(f8, "flow8"); TORCH_CHECK(f8.numel() >= M * cs(f8) && cs(f8) >= 2, "lookup_cc1: flow8"); }
-    upd = TapsUpd{tp.data_ptr<float>(), cs(tp), fb.data_ptr<float>(), coords.data_ptr<float>(), f32.data_ptr<float>(),
-                  hx.data_ptr(), cs(hx), hx_off, ptr(qx), cs(qx), qx_off, ptr(f8), cs(f8), 1};
-    if (keep) for (auto& v : {tp, fb, f32, hx, qx, f8}) if (v.defined()) keep->push_back(v);
-  }
-  const float* cp = coords.data_ptr<float>();
-  void* yp = y.data_ptr();
-  const void* wp = wpk.data_ptr();
-  const float* bp = bias.data_ptr<float>();
-  const int ycs = cs(y);
-  return [=](hipStream_t s, int it) {
-    TapsUpd u = upd;
-    u.on = upd.on && it > 0;
-    return jr_lookup_cc1(lv.data(), L, B, h, w, r, cp, blocked, wp, kpad, bp, yp, ycs, y_coff, cout, s, &u);
-  };
-}
-
 // ------------------------------------------------------------------ upsample
 // Upsampled-flow output: a view whose trailing (B, 8h, 8w, 2) block is dense
 // (the engine passes out[:, b0:b1] of the (iters, B_total, H, W, 2) buffer).
@@ -993,7 +936,6 @@ void corr_op(const TList& t, IList i, double scale) { run_now(make_corr(t, i, sc
 // a stand-alone lookup applies its fused flow update when one is given (in a
 // plan the update is skipped in loop iteration 0, which has no previous taps)
 void lookup_op(const TList& t, IList i) { JR_CHECK_OK(make_lookup(t, i, nullptr)(cur_stream(), 1)); }
-void lookup_cc1_op(const TList& t, IList i) { JR_CHECK_OK(make_lookup_cc1(t, i, nullptr)(cur_stream(), 1)); }
 void upsample_convex_op(const TList& t, IList i) { run_now(make_upsample_convex(t, i, nullptr)); }
 void convex_head_op(const TList& t, IList i, double alpha) { run_now(make_convex_head(t, i, alpha, nullptr)); }
 void upsample_bilinear_op(const TList& t, IList i) { run_now(make_upsample_bilinear(t, i, nullptr)); }
@@ -1112,7 +1054,6 @@ class Plan : public torch::CustomClassHolder {
   void add_conv(TList t, IList i, double alpha) { push(make_conv(t, i, alpha, &keep_), "conv"); }
   void add_corr(TList t, IList i, double scale) { push(make_corr(t, i, scale, &keep_), "corr"); }
   void add_lookup(TList t, IList i) { push(make_lookup(t, i, &keep_), "lookup"); }
-  void add_lookup_cc1(TList t, IList i) { push(make_lookup_cc1(t, i, &keep_), "lookup_cc1"); }
   void add_upsample_convex(TList t, IList i) { push(make_upsample_convex(t, i, &keep_), "upsample_convex"); }
   void add_convex_head(TList t, IList i, double alpha) { push(make_convex_head(t, i, alpha, &keep_), "convex_head"); }
   void add_upsample_bilinear(TList t, IList i) { push(make_upsample_bilinear(t, i, &keep_), "upsample_bilinear"); }
@@ -1534,7 +1475,6 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("conv(Tensor?[] t, int[] i, float alpha) -> ()", &jr::conv_op);
   m.def("corr(Tensor?[] t, int[] i, float scale) -> ()", &jr::corr_op);
   m.def("lookup(Tensor?[] t, int[] i) -> ()", &jr::lookup_op);
-  m.def("lookup_cc1(Tensor?[] t, int[] i) -> ()", &jr::lookup_cc1_op);
   m.def("upsample_convex(Tensor?[] t, int[] i) -> ()", &jr::upsample_convex_op);
   m.def("convex_head(Tensor?[] t, int[] i, float alpha) -> ()", &jr::convex_head_op);
   m.def("upsample_bilinear(Tensor?[] t, int[] i) -> ()", &jr::upsample_bilinear_op);
@@ -1578,7 +1518,6 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_conv", &jr::Plan::add_conv)
       .def("add_corr", &jr::Plan::add_corr)
       .def("add_lookup", &jr::Plan::add_lookup)
-      .def("add_lookup_cc1", &jr::Plan::add_lookup_cc1)
       .def("add_upsample_convex", &jr::Plan::add_upsample_convex)
       .def("add_convex_head", &jr::Plan::add_convex_head)
       .def("add_upsample_bilinear", &jr::Plan::add_upsample_bilinear)

@@ -31,7 +31,6 @@ KERNEL_SOURCES = [
     CSRC / "kernels" / "conv_fam_m32.hip",
     CSRC / "kernels" / "conv_fam_d2.hip",
     CSRC / "kernels" / "conv_fam_g.hip",
-    CSRC / "kernels" / "conv_fam_dp.hip",
     CSRC / "kernels" / "corr.hip",
     CSRC / "kernels" / "elementwise.hip",
     CSRC / "kernels" / "flowhead.hip",

@@ -31,7 +31,7 @@ ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, ACT_SPLIT_TANH_RELU = 0, 1, 2, 3, 4
 EPI_STD, EPI_GRU_A, EPI_GRU_B = 0, 1, 2   # 3, 4: retired epilogues (kernels.h)
 EPI_BWD, EPI_TAPS = 5, 6
 # tile configs with the EPI_TAPS epilogue (256 channels in one N tile, 16 waves of 64 x 32)
-TAPS_CFGS = (34, 22, 35, 38, 47)
+TAPS_CFGS = (34, 22, 35, 38)
 # tile configs of conv_igemm.hip: (BCO, BP)
 CFG_TILES = {0: (128, 128), 1: (64, 128), 2: (128, 64), 3: (16, 256), 4: (64, 64), 5: (16, 64)}
 # configs 6..11: LDS-DMA kernel D2 (csrc/kernels/conv_igemm.hip)
@@ -51,16 +51,13 @@ CFG_TILES.update({33: (128, 128), 34: (256, 128)})
 # configs 35..41: kernel D2 (LDS-DMA ring) at 8 / 16 waves with the FAST loader
 CFG_TILES.update({35: (256, 128), 36: (128, 128), 37: (128, 128), 38: (256, 128), 39: (256, 128), 40: (128, 256),
                   41: (64, 128), 42: (256, 128), 43: (256, 128)})
-# configs 44..50: kernel DP (the D2 ring + register double-buffered fragments, wide wave tiles)
-CFG_TILES.update({44: (256, 128), 45: (256, 128), 46: (256, 128), 47: (256, 128), 48: (128, 128), 49: (128, 128),
-                  50: (256, 128)})
 # Autotune candidates: configs that win at least one RAFT conv on MI355X
 # (tools/microbench.py, profiles/r1_microbench_conv_cfgs.txt); the others stay
 # compiled and tested but are not timed at plan build.
 # Of the D2 configs 35..43 only the 16-wave 64x32 ones (35, 38) come within a few
 # percent of kernel P on a loop conv (profiles/r2_conv_d2_microbench.txt).
 TUNE_CFGS = (0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34,
-             35, 38, 44, 45, 46, 47, 48, 49, 50)
+             35, 38)
 NUM_CUS = 256
 def load(build_if_missing: bool = True) -> None:
     """Load ``_C.so`` (building it with hipcc first if it is missing)."""

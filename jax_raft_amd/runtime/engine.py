@@ -189,7 +189,6 @@ class RaftEngine:
         self._taps_w = None
         self._taps_epi_w = None
         self._cc1_w = self._cc1_b = None
-        self._lc1_w = None   # convcorr1 packed for the fused lookup kernel
         self.model = model
         self.device = torch.device(device)
         self.use_graph = use_graph
@@ -297,16 +296,6 @@ class RaftEngine:
             else:
                 self._cc1_w.copy_(wc)
                 self._cc1_b.copy_(bc)
-        # the same conv fused into the lookup kernel (corr.hip:lookup_cc1_kernel): K padded to 32 only
-        S = 2 * self.radius + 1
-        kf = round_up(self.num_levels * S * S, 32)
-        if (cc1.kernel.shape[:2] == (1, 1) and cc1.kernel.shape[3] == 256 and self.num_levels <= 4
-                and (self.radius, kf) == (4, 352)):
-            wl = nat.pack_conv1x1(cc1.kernel.to(self.device), kf)
-            if self._lc1_w is None:
-                self._lc1_w, self._lc1_kpad = wl, kf
-            else:
-                self._lc1_w.copy_(wl)
         if fh2.kernel.shape[2] in (128, 256):
             wt = nat.pack_taps(fh2.kernel.to(self.device))
             if self._taps_w is None:
@@ -710,12 +699,7 @@ class RaftEngine:
         # ---------------- loop body: one refinement iteration (model.py:495-510)
         me = m.update_block.motion_encoder
         cl, fl = me.corr_layers, me.flow_layers
-        # lookup + convcorr1 as ONE kernel (the corr features stay in LDS) where the
-        # wide lookup applies: bf16 levels with 16-byte chunks never crossing a row
-        fuse_lc = (self._lc1_w is not None and len(cl) == 2 and self._cc1_w is not None and self.corr_dtype == BF16
-                   and L == 4 and all(blocked and l < 2 or ((w >> l) % 8 == 0 and ((h >> l) * (w >> l)) % 8 == 0)
-                                      for l in range(L)))
-        corr = None if fuse_lc else alloc("corr", (M, self.corr_cs))
+        corr = alloc("corr", (M, self.corr_cs))
         cf = alloc("cf", (M, cl[-1] + fl[-1]))
         f1 = alloc("f1", (M, fl[0]))
         c1 = alloc("c1", (M, cl[0])) if len(cl) == 2 else None
@@ -781,18 +765,12 @@ class RaftEngine:
         def lookup(with_update: bool):
             upd = [taps, self._fh2_b, flow32, hx, qx, flow8] if with_update else []
             extra = [self.flow_off, self.flow_off] if with_update else []
-            if fuse_lc:   # + convcorr1 (1x1 + ReLU) into c1
-                plan.add_lookup_cc1([coords, c1] + levels + [None] * (4 - L) + [self._lc1_w, self._cc1_b] + upd,
-                                    [L, B, h, w, self.radius, blocked, self._lc1_kpad, cl[0], 0] + extra)
-                return
             plan.add_lookup([coords, corr] + levels + [None] * (4 - L) + upd,
                             [L, B, h, w, self.radius, h * w, blocked] + extra)
 
         def motion_and_gru(wait_flow: bool, wait_mask: bool):
             if len(cl) == 2:
-                if fuse_lc:
-                    pass   # convcorr1 ran inside the lookup kernel
-                elif self._cc1_w is not None:   # LDS-resident-weight 1x1 kernel (conv1x1.hip)
+                if self._cc1_w is not None:   # LDS-resident-weight 1x1 kernel (conv1x1.hip)
                     plan.add_conv1x1([corr, self._cc1_w, self._cc1_b, c1],
                                      [M, self.corr_cs, self._cc1_kpad, cl[0], ACT_RELU, 0])
                 else:

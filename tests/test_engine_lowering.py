@@ -94,19 +94,6 @@ def test_final_only_schedule(factory, fake):
     assert ep[-1] == ("convex_head" if factory is raft_large else "upsample_bilinear")
 
 
-@pytest.mark.parametrize("B", [1, 4])
-def test_headline_shape_fuses_lookup_and_convcorr1(fake, B):
-    """At 440x1024 (55 x 128 feature maps: blocked bf16 levels) the lookup and
-    MotionEncoder.convcorr1 run as one kernel (corr.hip:lookup_cc1_kernel)."""
-    eng, p = _plan(raft_large, B, H=440, W=1024)
-    ops = p.names(1)
-    assert "lookup_cc1" in ops and "lookup" not in ops and "conv1x1" not in ops
-    # fp32 pyramid: no fusion (the fused kernel reads bf16 levels)
-    eng = E.RaftEngine(raft_large()[0].eval(), "cpu", autotune=False, corr_dtype=torch.float32)
-    st = eng._build(B, 440, 1024, 2, True)
-    assert "lookup_cc1" not in st.plan.names(1) and "lookup" in st.plan.names(1)
-
-
 def test_engine_knobs_are_few(fake):
     import inspect
 

@@ -507,63 +507,6 @@ def test_lookup_with_fused_update_is_bitwise(blocked, w):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("B,h,w,radius", [(1, 55, 128, 4), (2, 16, 64, 4), (3, 32, 64, 4)])
-@pytest.mark.parametrize("update", [False, True])
-def test_lookup_cc1_matches_lookup_then_conv1x1(B, h, w, radius, update):
-    """The fused lookup + convcorr1 kernel (corr.hip:lookup_cc1_kernel, features
-    kept in LDS) = the wide lookup kernel followed by the 1x1 conv kernel on the
-    same packed weights: the same bf16 features and the same MFMA k order, so
-    the outputs (and, with the fused flow update, coords / flow copies) are
-    bitwise equal; both match the fp32 reference composition."""
-    nat = _nat()
-    torch.manual_seed(23)
-    C, L = 64, 4
-    S = 2 * radius + 1
-    M = B * h * w
-    blocked = int(w % 16 == 0)
-    g1 = torch.randn(B, h, w, C).to(DEV, torch.bfloat16)
-    g2 = torch.randn(B, h, w, C).to(DEV, torch.bfloat16)
-    nty, ntx = -(-h // 8), -(-w // 16)
-    lv, hl, wl = [], h, w
-    for l in range(L):
-        shape = (M, nty * (8 >> l), ntx * (16 >> l)) if (blocked and l < 2) else (M, hl, wl)
-        lv.append(torch.zeros(shape, device=DEV, dtype=torch.bfloat16))
-        hl //= 2
-        wl //= 2
-    nat.ops().corr([g1, g2] + lv, [B, h, w, C, L, h * w, blocked], 1.0 / math.sqrt(C))
-    K = L * S * S
-    kpad = nat.round_up(K, 32)
-    kern = torch.randn(1, 1, K, 256) / math.sqrt(K)
-    bias = (torch.randn(256) * 0.1).to(DEV)
-    wpk = nat.pack_conv1x1(kern.to(DEV), kpad)
-    coords0 = (R.make_coords_grid(B, h, w).reshape(M, 2) + torch.randn(M, 2) * 4).to(DEV)
-    taps = (torch.randn(M, 24) * 2).to(DEV)
-    fb = torch.randn(2).to(DEV)
-    res = []
-    for fused in (False, True):
-        coords = coords0.clone()
-        f32 = torch.zeros(M, 2, device=DEV)
-        hx = torch.zeros(M, 24, device=DEV, dtype=torch.bfloat16)
-        y = torch.full((M, 264), 7.0, device=DEV, dtype=torch.bfloat16)
-        upd = [taps, fb, f32, hx, None, None] if update else []
-        extra = [16, 0] if update else []
-        if fused:
-            nat.ops().lookup_cc1([coords, y] + lv + [wpk, bias] + upd, [L, B, h, w, radius, blocked, kpad, 256, 8] + extra)
-        else:
-            corr = torch.zeros(M, nat.round_up(K, 8), device=DEV, dtype=torch.bfloat16)
-            nat.ops().lookup([coords, corr] + lv + upd, [L, B, h, w, radius, h * w, blocked] + extra)
-            kp = next(k for k in nat.CONV1X1_KPADS if k >= corr.shape[1])
-            wc = nat.pack_conv1x1(kern.to(DEV), kp)
-            nat.ops().conv1x1([corr, wc, bias, y], [M, corr.shape[1], kp, 256, nat.ACT_RELU, 8])
-        torch.cuda.synchronize()
-        res.append((coords, f32, hx, y))
-    (c0, f0, h0, y0), (c1, f1, h1, y1) = res
-    assert torch.equal(c0, c1) and torch.equal(f0, f1) and torch.equal(h0, h1)
-    assert (y1[:, :8] == 7.0).all()
-    err = (y1[:, 8:264].float() - y0[:, 8:264].float()).abs().max().item()
-    assert err <= 1e-2 * y0[:, 8:264].float().abs().max().item(), err
-
-
 @pytest.mark.parametrize("K,cs,coff,M", [(256, 256, 0, 1000), (256, 512, 0, 28160), (128, 136, 8, 777)])
 def test_taps_gemm_matches_fp32(K, cs, coff, M):
     """flowhead.hip taps GEMM (the flow head's 3x3 output conv as 9 x 2 per-pixel
