@@ -279,4 +279,48 @@ int jr_conv_direct(const void* x, int x_cstride, int N, int H, int W, int cin, i
 int jr_copy_channels(const void* src, int s_cstride, int s_coff, void* dst, int d_cstride, int d_coff,
                      int M, int C, hipStream_t stream);
 
+// ---------------------------------------------------------------------------
+// fp32 parity mode (engine precision="fp32"; conv_f32.hip, f32.hip): the
+// reference's own precision end to end -- fp32 operands on the f32 MFMA
+// (v_mfma_f32_16x16x4_f32), fp32 activations, correlation and hidden state.
+// ---------------------------------------------------------------------------
+// Implicit-GEMM conv, fp32 NHWC: x [N][H][W][x_cs] (channels x_coff .. + cin4),
+// w fp32 [cout][K], K = (kh, kw, cin4) (cin4 % 4 == 0, zero-padded), bias [cout].
+// epi 0: bias (+bmap) (+res: pre-act add, or post-act add + relu when res_post)
+//        -> act -> *alpha -> y (+y2) (+h32 [M][hidden] for channels < split)
+// epi 1: ConvGRU z / r (cout = 2 hidden): z -> zbuf [M][hidden], r * h32 -> y
+// epi 2: ConvGRU q (cout = hidden): h = (1 - z) h + z tanh(q) -> h32, y (+y2)
+struct ConvF32Params {
+  const float* x; int N, H, W, x_cs, x_coff, cin4;
+  int KH, KW, SH, SW, PH, PW, OH, OW, M;
+  const float* w; int K, cout;
+  const float* bias; float alpha; int act, split;
+  float* y; int y_cs, y_coff;
+  float* y2; int y2_cs, y2_coff;
+  const float* res; int res_cs, res_coff, res_post;
+  float* h32; float* zbuf; int hidden;
+  const float* bmap; int bmap_cs, bmap_coff;
+};
+int jr_conv_f32(const ConvF32Params* p, int epi, hipStream_t stream);
+// jr_channel_stats / jr_norm_act / jr_prep_images / jr_copy_channels /
+// jr_upsample_convex on fp32 tensors (prep: [2B][H][W][4], channel 3 = 0)
+int jr_channel_stats_f32(const float* x, int N, int HW, int C, float* stats, float* partial, hipStream_t stream);
+int jr_norm_act_f32(const float* x, const float* sx, int mode_x, const float* res, const float* sr, int mode_r,
+                    float* y, int N, int HW, int C, float eps, int relu, hipStream_t stream);
+int jr_prep_images_f32(const float* img1, const float* img2, int B, int H, int W, float* out, hipStream_t stream);
+int jr_copy_channels_f32(const float* src, int s_cstride, int s_coff, float* dst, int d_cstride, int d_coff, int M,
+                         int C, hipStream_t stream);
+int jr_upsample_convex_f32(const float* mask, int mask_cstride, const float* flow, int B, int h, int w, float* out,
+                           const void* out_slot, long out_off, hipStream_t stream);
+// 2x2 average pooling (floor) of per-query correlation maps: src [M][hl][wl] -> dst [M][hl/2][wl/2]
+int jr_corr_pool_f32(const float* src, long M, int hl, int wl, float* dst, hipStream_t stream);
+// Pyramid lookup with fp32 output (jr_corr_lookup's semantics and channel order;
+// row-major fp32 levels, no fused update): out [B*h*w][out_cstride]
+int jr_corr_lookup_f32(const float* const* levels, int num_levels, int B, int h, int w, int radius,
+                       const float* coords, float* out, int out_cstride, hipStream_t stream);
+// coords += delta (delta [M][dcs], channels 0, 1: the FlowHead output incl. its bias);
+// flow = coords - coords0 -> flow32 [M][2], hx / qx (channel offsets) and flow4 [M][4] (channels 0, 1)
+int jr_flow_update_f32(const float* delta, int dcs, int N, int h, int w, float* coords, float* flow32, float* hx,
+                       int hx_cs, int hx_off, float* qx, int qx_cs, int qx_off, float* flow4, hipStream_t stream);
+
 }  // extern "C"

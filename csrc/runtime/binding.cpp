@@ -896,6 +896,220 @@ static Launch make_im2col(const TList& t, const IList& i, std::vector<at::Tensor
   };
 }
 
+// ------------------------------------------------------------ fp32 parity mode
+// (engine precision="fp32", runtime/engine_f32.py; kernels conv_f32.hip, f32.hip)
+static void check_f32_min(const at::Tensor& t, const char* name, int64_t n) {
+  check_f32(t, name);
+  TORCH_CHECK(t.numel() >= n, name, ": tensor too small (", t.numel(), " < ", n, ")");
+}
+
+// t = [x, w ([cout][K] fp32), bias, y, y2, res, h32, zbuf, bmap]
+// i = [N, H, W, x_coff, cin4, KH, KW, SH, SW, PH, PW, cout, act, split, y_coff, y2_coff, res_coff, res_post,
+//      hidden, bmap_coff, epi]
+static Launch make_conv_f32(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep) {
+  TORCH_CHECK(i.size() == 21, "conv_f32: expected 21 ints");
+  at::Tensor x = opt(t, 0), w = opt(t, 1), bias = opt(t, 2), y = opt(t, 3), y2 = opt(t, 4), res = opt(t, 5);
+  at::Tensor h32 = opt(t, 6), zbuf = opt(t, 7), bmap = opt(t, 8);
+  ConvF32Params p{};
+  p.N = (int)i[0]; p.H = (int)i[1]; p.W = (int)i[2]; p.x_coff = (int)i[3]; p.cin4 = (int)i[4];
+  p.KH = (int)i[5]; p.KW = (int)i[6]; p.SH = (int)i[7]; p.SW = (int)i[8]; p.PH = (int)i[9]; p.PW = (int)i[10];
+  p.cout = (int)i[11]; p.act = (int)i[12]; p.split = (int)i[13];
+  p.y_coff = (int)i[14]; p.y2_coff = (int)i[15]; p.res_coff = (int)i[16]; p.res_post = (int)i[17];
+  p.hidden = (int)i[18]; p.bmap_coff = (int)i[19];
+  const int epi = (int)i[20];
+  TORCH_CHECK(epi >= 0 && epi <= 2, "conv_f32: epi 0..2");
+  TORCH_CHECK(p.SH >= 1 && p.SW >= 1 && p.KH >= 1 && p.KW >= 1 && p.cout >= 1, "conv_f32: geometry");
+  p.OH = (p.H + 2 * p.PH - p.KH) / p.SH + 1;
+  p.OW = (p.W + 2 * p.PW - p.KW) / p.SW + 1;
+  p.M = p.N * p.OH * p.OW;
+  p.K = p.KH * p.KW * p.cin4;
+  const int64_t M = p.M;
+  check_f32(x, "x");
+  p.x_cs = cs(x);
+  TORCH_CHECK(p.x_coff + p.cin4 <= p.x_cs && x.numel() >= (int64_t)p.N * p.H * p.W * p.x_cs, "conv_f32: x");
+  check_f32(w, "w");
+  TORCH_CHECK(w.numel() == (int64_t)p.cout * p.K, "conv_f32: w must be [cout][KH*KW*cin4]");
+  check_f32_min(bias, "bias", p.cout);
+  check_f32(y, "y");
+  p.y_cs = cs(y);
+  const int ych = epi == 1 ? p.hidden : p.cout;   // GRU-A writes r*h (hidden channels) to y
+  TORCH_CHECK(p.y_coff + ych <= p.y_cs && y.numel() >= M * p.y_cs, "conv_f32: y");
+  if (y2.defined()) {
+    check_f32(y2, "y2"); p.y2_cs = cs(y2);
+    TORCH_CHECK(p.y2_coff + p.cout <= p.y2_cs && y2.numel() >= M * p.y2_cs, "conv_f32: y2");
+  }
+  if (res.defined()) {
+    check_f32(res, "res"); p.res_cs = cs(res);
+    TORCH_CHECK(p.res_coff + p.cout <= p.res_cs && res.numel() >= M * p.res_cs, "conv_f32: res");
+  }
+  if (h32.defined()) check_f32_min(h32, "h32", M * p.hidden);
+  if (zbuf.defined()) check_f32_min(zbuf, "zbuf", M * p.hidden);
+  if (epi == 0 && h32.defined()) TORCH_CHECK(p.split <= p.hidden && p.split <= p.cout, "conv_f32: h32 copy");
+  if (bmap.defined()) {
+    check_f32(bmap, "bmap"); p.bmap_cs = cs(bmap);
+    TORCH_CHECK(p.bmap_coff + p.cout <= p.bmap_cs && bmap.numel() >= M * p.bmap_cs, "conv_f32: bmap");
+  }
+  p.x = x.data_ptr<float>(); p.w = w.data_ptr<float>(); p.bias = bias.data_ptr<float>(); p.alpha = (float)alpha;
+  p.y = y.data_ptr<float>();
+  p.y2 = y2.defined() ? y2.data_ptr<float>() : nullptr;
+  p.res = res.defined() ? res.data_ptr<float>() : nullptr;
+  p.h32 = h32.defined() ? h32.data_ptr<float>() : nullptr;
+  p.zbuf = zbuf.defined() ? zbuf.data_ptr<float>() : nullptr;
+  p.bmap = bmap.defined() ? bmap.data_ptr<float>() : nullptr;
+  if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, bmap}) if (v.defined()) keep->push_back(v);
+  return [=](hipStream_t s, int) { return jr_conv_f32(&p, epi, s); };
+}
+
+// t = [x, stats, partial?], i = [N, HW, C]
+static Launch make_stats_f32(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor x = opt(t, 0), st = opt(t, 1), part = opt(t, 2);
+  const int N = (int)i[0], HW = (int)i[1], C = (int)i[2];
+  check_f32(x, "x");
+  TORCH_CHECK(C % 4 == 0 && C <= 1024 && cs(x) == C && x.numel() >= (int64_t)N * HW * C, "stats_f32: shape");
+  check_f32_min(st, "stats", (int64_t)N * C * 2);
+  const int64_t need = (int64_t)jr_channel_stats_partials(N, HW) * C * 2;
+  if (!part.defined()) part = at::empty({need}, st.options());
+  check_f32_min(part, "partial", need);
+  if (keep) for (auto& v : {x, st, part}) keep->push_back(v);
+  const float* xp = x.data_ptr<float>();
+  float* sp = st.data_ptr<float>();
+  float* pp = part.data_ptr<float>();
+  return [=](hipStream_t s, int) { return jr_channel_stats_f32(xp, N, HW, C, sp, pp, s); };
+}
+
+// t = [x, sx, res, sr, y], i = [mode_x, mode_r, N, HW, C, relu]
+static Launch make_norm_act_f32(const TList& t, const IList& i, double eps, std::vector<at::Tensor>* keep) {
+  at::Tensor x = opt(t, 0), sx = opt(t, 1), r = opt(t, 2), sr = opt(t, 3), y = opt(t, 4);
+  const int mx = (int)i[0], mr = (int)i[1], N = (int)i[2], HW = (int)i[3], C = (int)i[4], relu = (int)i[5];
+  const int64_t n = (int64_t)N * HW * C;
+  check_f32_min(x, "x", n); check_f32_min(y, "y", n);
+  TORCH_CHECK(C % 4 == 0 && C <= 1024 && cs(x) == C && cs(y) == C, "norm_act_f32: shape");
+  if (mx) check_f32_min(sx, "sx", (int64_t)N * C * 2);
+  if (r.defined()) {
+    check_f32_min(r, "res", n);
+    TORCH_CHECK(cs(r) == C, "norm_act_f32: residual channels");
+    if (mr) check_f32_min(sr, "sr", (int64_t)N * C * 2);
+  }
+  if (keep) for (auto& v : {x, sx, r, sr, y}) if (v.defined()) keep->push_back(v);
+  auto fp = [](const at::Tensor& v) -> float* { return v.defined() ? v.data_ptr<float>() : nullptr; };
+  const float *xp = fp(x), *sxp = fp(sx), *rp = fp(r), *srp = fp(sr);
+  float* yp = fp(y);
+  const float e = (float)eps;
+  return [=](hipStream_t s, int) { return jr_norm_act_f32(xp, sxp, mx, rp, srp, mr, yp, N, HW, C, e, relu, s); };
+}
+
+// t = [img1, img2, out ([2B][H][W][4])], i = [B, H, W]
+static Launch make_prep_f32(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor a = opt(t, 0), b = opt(t, 1), out = opt(t, 2);
+  const int B = (int)i[0], H = (int)i[1], W = (int)i[2];
+  check_f32(a, "img1"); check_f32(b, "img2"); check_f32(out, "out");
+  TORCH_CHECK(a.numel() == (int64_t)B * H * W * 3 && b.numel() == a.numel(), "prep_f32: image shape");
+  TORCH_CHECK(out.numel() >= 2LL * B * H * W * 4 && cs(out) == 4, "prep_f32: output");
+  if (keep) for (auto& v : {a, b, out}) keep->push_back(v);
+  const float *ap = a.data_ptr<float>(), *bp = b.data_ptr<float>();
+  float* op = out.data_ptr<float>();
+  return [=](hipStream_t s, int) { return jr_prep_images_f32(ap, bp, B, H, W, op, s); };
+}
+
+// t = [src, dst], i = [s_coff, d_coff, M, C]
+static Launch make_copy_channels_f32(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor a = opt(t, 0), b = opt(t, 1);
+  check_f32(a, "src"); check_f32(b, "dst");
+  const int so = (int)i[0], dof = (int)i[1], M = (int)i[2], C = (int)i[3];
+  TORCH_CHECK(so + C <= cs(a) && dof + C <= cs(b) && a.numel() >= (int64_t)M * cs(a) && b.numel() >= (int64_t)M * cs(b),
+              "copy_channels_f32: shape");
+  if (keep) { keep->push_back(a); keep->push_back(b); }
+  const float* ap = a.data_ptr<float>();
+  float* bp = b.data_ptr<float>();
+  const int acs = cs(a), bcs = cs(b);
+  return [=](hipStream_t s, int) { return jr_copy_channels_f32(ap, acs, so, bp, bcs, dof, M, C, s); };
+}
+
+// t = [mask (fp32 [M][>=576]), flow, out, out_slot?], i = [B, h, w, out_iter_stride(, slot offset)]
+static Launch make_upsample_convex_f32(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor mask = opt(t, 0), flow = opt(t, 1), out = opt(t, 2), slot = opt(t, 3);
+  const int B = (int)i[0], h = (int)i[1], w = (int)i[2];
+  const int64_t stride = i[3], slot_off = i.size() > 4 ? i[4] : 0;
+  const int64_t M = (int64_t)B * h * w;
+  check_f32_min(mask, "mask", M * 576); check_f32_min(flow, "flow", M * 2);
+  TORCH_CHECK(cs(mask) >= 576 && mask.numel() >= M * cs(mask), "upsample_convex_f32: mask needs 576 channels");
+  TORCH_CHECK(!slot.defined() || (slot.is_cuda() && slot.scalar_type() == at::kLong && slot.numel() == 1),
+              "upsample_convex_f32: out_slot must be one device int64");
+  const int64_t cap = check_flow_out(out, B, h, w);
+  if (keep) for (auto& v : {mask, flow, out, slot}) if (v.defined()) keep->push_back(v);
+  const float *mp = mask.data_ptr<float>(), *fp = flow.data_ptr<float>();
+  float* op = out.data_ptr<float>();
+  const void* sp = slot.defined() ? slot.data_ptr() : nullptr;
+  const int mcs = cs(mask);
+  return [=](hipStream_t s, int it) {
+    const int64_t off = stride * it;
+    if (off + M * 128 > cap) return (int)hipErrorInvalidValue;
+    return jr_upsample_convex_f32(mp, mcs, fp, B, h, w, op + off, sp, (long)(slot_off + off), s);
+  };
+}
+
+// t = [src ([M][hl][wl]), dst ([M][hl/2][wl/2])], i = [M, hl, wl]
+static Launch make_corr_pool_f32(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor a = opt(t, 0), b = opt(t, 1);
+  const int64_t M = i[0];
+  const int hl = (int)i[1], wl = (int)i[2];
+  TORCH_CHECK(hl >= 2 && wl >= 2, "corr_pool_f32: level too small");
+  check_f32_min(a, "src", M * hl * wl); check_f32_min(b, "dst", M * (hl / 2) * (wl / 2));
+  if (keep) { keep->push_back(a); keep->push_back(b); }
+  const float* ap = a.data_ptr<float>();
+  float* bp = b.data_ptr<float>();
+  return [=](hipStream_t s, int) { return jr_corr_pool_f32(ap, (long)M, hl, wl, bp, s); };
+}
+
+// t = [coords, out, l0, l1, l2, l3], i = [num_levels, B, h, w, radius]
+static Launch make_lookup_f32(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor coords = opt(t, 0), out = opt(t, 1);
+  const int L = (int)i[0], B = (int)i[1], h = (int)i[2], w = (int)i[3], r = (int)i[4];
+  const int S = 2 * r + 1;
+  const int64_t M = (int64_t)B * h * w;
+  TORCH_CHECK(L >= 1 && L <= 4 && r >= 1 && r <= 4, "lookup_f32: levels 1..4, radius 1..4");
+  check_f32_min(coords, "coords", M * 2);
+  check_f32(out, "out");
+  TORCH_CHECK(cs(out) >= L * S * S && out.numel() >= M * cs(out), "lookup_f32: out");
+  std::vector<const float*> lv(4, nullptr);
+  int hl = h, wl = w;
+  for (int l = 0; l < L; ++l) {
+    at::Tensor v = opt(t, 2 + l);
+    TORCH_CHECK(hl >= 2 && wl >= 2, "lookup_f32: pyramid level too small");
+    check_f32_min(v, "level", M * hl * wl);
+    lv[l] = v.data_ptr<float>();
+    if (keep) keep->push_back(v);
+    hl >>= 1; wl >>= 1;
+  }
+  if (keep) { keep->push_back(coords); keep->push_back(out); }
+  const float* cp = coords.data_ptr<float>();
+  float* op = out.data_ptr<float>();
+  const int ocs = cs(out);
+  return [=](hipStream_t s, int) { return jr_corr_lookup_f32(lv.data(), L, B, h, w, r, cp, op, ocs, s); };
+}
+
+// t = [delta ([M][dcs]), coords, flow32, hx, qx?, flow4?], i = [N, h, w, hx_off, qx_off]
+static Launch make_flow_update_f32(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor d = opt(t, 0), coords = opt(t, 1), f32 = opt(t, 2), hx = opt(t, 3), qx = opt(t, 4), f4 = opt(t, 5);
+  const int N = (int)i[0], h = (int)i[1], w = (int)i[2], hx_off = (int)i[3], qx_off = (int)i[4];
+  const int64_t M = (int64_t)N * h * w;
+  check_f32(d, "delta");
+  TORCH_CHECK(cs(d) >= 2 && d.numel() >= M * cs(d), "flow_update_f32: delta");
+  check_f32_min(coords, "coords", 2 * M); check_f32_min(f32, "flow32", 2 * M);
+  check_f32(hx, "hx");
+  TORCH_CHECK(hx_off + 2 <= cs(hx) && hx.numel() >= M * cs(hx), "flow_update_f32: hx");
+  if (qx.defined()) { check_f32(qx, "qx"); TORCH_CHECK(qx_off + 2 <= cs(qx) && qx.numel() >= M * cs(qx), "flow_update_f32: qx"); }
+  if (f4.defined()) { check_f32_min(f4, "flow4", 4 * M); TORCH_CHECK(cs(f4) == 4, "flow_update_f32: flow4 [M][4]"); }
+  if (keep) for (auto& v : {d, coords, f32, hx, qx, f4}) if (v.defined()) keep->push_back(v);
+  auto fp = [](const at::Tensor& v) -> float* { return v.defined() ? v.data_ptr<float>() : nullptr; };
+  const float* dp = fp(d);
+  float *cp = fp(coords), *fl = fp(f32), *hp = fp(hx), *qp = fp(qx), *f4p = fp(f4);
+  const int dcs = cs(d), hcs = cs(hx), qcs = qx.defined() ? cs(qx) : 0;
+  return [=](hipStream_t s, int) {
+    return jr_flow_update_f32(dp, dcs, N, h, w, cp, fl, hp, hcs, hx_off, qp, qcs, qx_off, f4p, s);
+  };
+}
+
 static void run_now(const Launch& l) { JR_CHECK_OK(l(cur_stream(), 0)); }
 
 // ------------------------------------------------------------- sequence loss
@@ -932,6 +1146,16 @@ void seq_loss_bwd_op(const TList& t, IList i, double max_flow) {
 
 // ---------------------------------------------------------------- eager ops
 void conv_op(const TList& t, IList i, double alpha) { run_now(make_conv(t, i, alpha, nullptr)); }
+void conv_f32_op(const TList& t, IList i, double alpha) { run_now(make_conv_f32(t, i, alpha, nullptr)); }
+void stats_f32_op(const TList& t, IList i) { run_now(make_stats_f32(t, i, nullptr)); }
+void norm_act_f32_op(const TList& t, IList i, double eps) { run_now(make_norm_act_f32(t, i, eps, nullptr)); }
+void prep_f32_op(const TList& t, IList i) { run_now(make_prep_f32(t, i, nullptr)); }
+void copy_channels_f32_op(const TList& t, IList i) { run_now(make_copy_channels_f32(t, i, nullptr)); }
+void upsample_convex_f32_op(const TList& t, IList i) { run_now(make_upsample_convex_f32(t, i, nullptr)); }
+void corr_pool_f32_op(const TList& t, IList i) { run_now(make_corr_pool_f32(t, i, nullptr)); }
+void lookup_f32_op(const TList& t, IList i) { run_now(make_lookup_f32(t, i, nullptr)); }
+void flow_update_f32_op(const TList& t, IList i) { run_now(make_flow_update_f32(t, i, nullptr)); }
+
 void corr_op(const TList& t, IList i, double scale) { run_now(make_corr(t, i, scale, nullptr)); }
 // a stand-alone lookup applies its fused flow update when one is given (in a
 // plan the update is skipped in loop iteration 0, which has no previous taps)
@@ -1082,6 +1306,15 @@ class Plan : public torch::CustomClassHolder {
   void add_upsample_bilinear_bwd(TList t, IList i) { push(make_upsample_bilinear_bwd(t, i, &keep_), "upsample_bilinear_bwd"); }
   void add_lookup_bwd(TList t, IList i) { push(make_lookup_bwd(t, i, &keep_), "lookup_bwd"); }
   void add_im2col(TList t, IList i) { push(make_im2col(t, i, &keep_), "im2col"); }
+  void add_conv_f32(TList t, IList i, double alpha) { push(make_conv_f32(t, i, alpha, &keep_), "conv_f32"); }
+  void add_stats_f32(TList t, IList i) { push(make_stats_f32(t, i, &keep_), "stats_f32"); }
+  void add_norm_act_f32(TList t, IList i, double eps) { push(make_norm_act_f32(t, i, eps, &keep_), "norm_act_f32"); }
+  void add_prep_f32(TList t, IList i) { push(make_prep_f32(t, i, &keep_), "prep_f32"); }
+  void add_copy_channels_f32(TList t, IList i) { push(make_copy_channels_f32(t, i, &keep_), "copy_channels_f32"); }
+  void add_upsample_convex_f32(TList t, IList i) { push(make_upsample_convex_f32(t, i, &keep_), "upsample_convex_f32"); }
+  void add_corr_pool_f32(TList t, IList i) { push(make_corr_pool_f32(t, i, &keep_), "corr_pool_f32"); }
+  void add_lookup_f32(TList t, IList i) { push(make_lookup_f32(t, i, &keep_), "lookup_f32"); }
+  void add_flow_update_f32(TList t, IList i) { push(make_flow_update_f32(t, i, &keep_), "flow_update_f32"); }
 
   int64_t num_ops(int64_t seg) const { return (int64_t)segs_[seg].size(); }
   std::vector<std::string> op_names(int64_t seg) const {
@@ -1500,6 +1733,15 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("seq_loss(Tensor?[] t, int[] i, float max_flow) -> ()", &jr::seq_loss_op);
   m.def("seq_loss_blocks(int P) -> int", &jr::seq_loss_blocks_op);
   m.def("seq_loss_bwd(Tensor?[] t, int[] i, float max_flow) -> ()", &jr::seq_loss_bwd_op);
+  m.def("conv_f32(Tensor?[] t, int[] i, float alpha) -> ()", &jr::conv_f32_op);
+  m.def("stats_f32(Tensor?[] t, int[] i) -> ()", &jr::stats_f32_op);
+  m.def("norm_act_f32(Tensor?[] t, int[] i, float eps) -> ()", &jr::norm_act_f32_op);
+  m.def("prep_f32(Tensor?[] t, int[] i) -> ()", &jr::prep_f32_op);
+  m.def("copy_channels_f32(Tensor?[] t, int[] i) -> ()", &jr::copy_channels_f32_op);
+  m.def("upsample_convex_f32(Tensor?[] t, int[] i) -> ()", &jr::upsample_convex_f32_op);
+  m.def("corr_pool_f32(Tensor?[] t, int[] i) -> ()", &jr::corr_pool_f32_op);
+  m.def("lookup_f32(Tensor?[] t, int[] i) -> ()", &jr::lookup_f32_op);
+  m.def("flow_update_f32(Tensor?[] t, int[] i) -> ()", &jr::flow_update_f32_op);
   m.class_<jr::Plan>("Plan")
       .def(torch::init<>())
       .def("set_segment", &jr::Plan::set_segment)
@@ -1542,6 +1784,15 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_upsample_bilinear_bwd", &jr::Plan::add_upsample_bilinear_bwd)
       .def("add_lookup_bwd", &jr::Plan::add_lookup_bwd)
       .def("add_im2col", &jr::Plan::add_im2col)
+      .def("add_conv_f32", &jr::Plan::add_conv_f32)
+      .def("add_stats_f32", &jr::Plan::add_stats_f32)
+      .def("add_norm_act_f32", &jr::Plan::add_norm_act_f32)
+      .def("add_prep_f32", &jr::Plan::add_prep_f32)
+      .def("add_copy_channels_f32", &jr::Plan::add_copy_channels_f32)
+      .def("add_upsample_convex_f32", &jr::Plan::add_upsample_convex_f32)
+      .def("add_corr_pool_f32", &jr::Plan::add_corr_pool_f32)
+      .def("add_lookup_f32", &jr::Plan::add_lookup_f32)
+      .def("add_flow_update_f32", &jr::Plan::add_flow_update_f32)
       .def("num_ops", &jr::Plan::num_ops)
       .def("op_names", &jr::Plan::op_names)
       .def("run", &jr::Plan::run)

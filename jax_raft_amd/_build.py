@@ -33,6 +33,8 @@ KERNEL_SOURCES = [
     CSRC / "kernels" / "conv_fam_g.hip",
     CSRC / "kernels" / "corr.hip",
     CSRC / "kernels" / "elementwise.hip",
+    CSRC / "kernels" / "conv_f32.hip",
+    CSRC / "kernels" / "f32.hip",
     CSRC / "kernels" / "flowhead.hip",
     CSRC / "kernels" / "conv_direct.hip",
     CSRC / "kernels" / "train.hip",

@@ -341,3 +341,69 @@ def conv2d(spec: ConvSpec, x: torch.Tensor, act: int = ACT_NONE, out_dtype=torch
     t, i, a = conv_args(spec, x, N, H, W, y, act=act, alpha=alpha, res=res, res_post=res_post, cfg=cfg)
     ops().conv(t, i, a)
     return y[..., : spec.cout] if y.shape[-1] != spec.cout else y
+
+
+# ------------------------------------------------------ fp32 parity mode convs
+
+
+@dataclass
+class ConvSpecF32:
+    """A conv for the fp32 implicit-GEMM kernel (csrc/kernels/conv_f32.hip):
+    ``w`` fp32 [cout, K], K ordered (kh, kw, cin4) with the input channels
+    zero-padded to ``cin4`` (a multiple of 4), rows in natural channel order;
+    ``b`` fp32 [cout]."""
+
+    w: torch.Tensor
+    b: torch.Tensor
+    kh: int
+    kw: int
+    sh: int
+    sw: int
+    ph: int
+    pw: int
+    cin: int
+    cin4: int
+    cout: int
+
+    def out_hw(self, H: int, W: int) -> Tuple[int, int]:
+        return (H + 2 * self.ph - self.kh) // self.sh + 1, (W + 2 * self.pw - self.kw) // self.sw + 1
+
+
+def pack_weight_f32(kernel: torch.Tensor, cin4: Optional[int] = None) -> torch.Tensor:
+    """HWIO kernel -> fp32 [cout, kh*kw*cin4] (input channels zero-padded)."""
+    kh, kw, cin, cout = kernel.shape
+    cin4 = cin4 or round_up(cin, 4)
+    assert cin4 >= cin and cin4 % 4 == 0
+    k = torch.zeros(kh, kw, cin4, cout, dtype=torch.float32, device=kernel.device)
+    k[:, :, :cin, :] = kernel.detach().float()
+    return k.permute(3, 0, 1, 2).reshape(cout, kh * kw * cin4).contiguous()
+
+
+def make_spec_f32(kernel: torch.Tensor, bias: torch.Tensor, stride=(1, 1), padding=(0, 0),
+                  cin4: Optional[int] = None, device=None) -> ConvSpecF32:
+    kh, kw, cin, cout = kernel.shape
+    cin4 = cin4 or round_up(cin, 4)
+    w = pack_weight_f32(kernel.to(device) if device is not None else kernel, cin4)
+    b = bias.detach().float().to(w.device).contiguous()
+    return ConvSpecF32(w, b, kh, kw, stride[0], stride[1], padding[0], padding[1], cin, cin4, cout)
+
+
+def conv_f32_args(spec: ConvSpecF32, x: torch.Tensor, N: int, H: int, W: int, y: torch.Tensor, *, x_coff: int = 0,
+                  y_coff: int = 0, act: int = ACT_NONE, split: int = 0, alpha: float = 1.0, y2=None, y2_coff: int = 0,
+                  res=None, res_coff: int = 0, res_post: int = 0, h32=None, zbuf=None, hidden: int = 0, bmap=None,
+                  bmap_coff: int = 0, epi: int = EPI_STD):
+    """(tensors, ints, alpha) of the ``conv_f32`` op / ``Plan.add_conv_f32``."""
+    t = [x, spec.w, spec.b, y, y2, res, h32, zbuf, bmap]
+    i = [N, H, W, x_coff, spec.cin4, spec.kh, spec.kw, spec.sh, spec.sw, spec.ph, spec.pw, spec.cout, act, split,
+         y_coff, y2_coff, res_coff, res_post, hidden, bmap_coff, epi]
+    return t, i, float(alpha)
+
+
+def conv2d_f32(spec: ConvSpecF32, x: torch.Tensor, act: int = ACT_NONE, alpha: float = 1.0, res=None,
+               res_post: int = 0) -> torch.Tensor:
+    """Eager fp32 NHWC conv (x: (N, H, W, C >= cin4) fp32) -> (N, OH, OW, cout)."""
+    N, H, W, _ = x.shape
+    OH, OW = spec.out_hw(H, W)
+    y = torch.empty((N, OH, OW, spec.cout), dtype=torch.float32, device=x.device)
+    ops().conv_f32(*conv_f32_args(spec, x, N, H, W, y, act=act, alpha=alpha, res=res, res_post=res_post))
+    return y

@@ -154,6 +154,10 @@ class RaftEngine:
             leave idle.
         cfg_override: fixed tile configs per conv spec name (e.g. {"gru0.b": 27},
             tools/schedule_tune.py); ``JR_CFG_OVERRIDE="name=cfg,..."`` adds entries.
+        precision: "bf16" (default: bf16 MFMA operands and activations, fp32
+            accumulation, fp32 hidden state / flow / upsampled output) or "fp32"
+            (the reference's own precision end to end on the f32 MFMA:
+            :class:`~jax_raft_amd.runtime.engine_f32.RaftEngineF32`).
 
     Schedules (chosen per plan, see :meth:`_build_part`): the lane schedule
     above; one in-order lane with every iteration upsampled (batch < 4,
@@ -168,10 +172,20 @@ class RaftEngine:
     as separate graphs on two streams, which serialise on this ROCm).
     """
 
+    def __new__(cls, *args, precision: str = "bf16", **kwargs):
+        if precision not in ("bf16", "fp32"):
+            raise ValueError(f"precision must be 'bf16' or 'fp32', got {precision!r}")
+        if precision == "fp32" and cls is RaftEngine:
+            from .engine_f32 import RaftEngineF32
+            cls = RaftEngineF32
+        return super().__new__(cls)
+
+    precision = "bf16"
+
     def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True,
                  corr_dtype: torch.dtype = torch.bfloat16, gate_dtype: torch.dtype = torch.bfloat16,
                  autotune: bool = True, streams="auto", split: int = 1,
-                 cfg_override: Optional[Dict[str, int]] = None):
+                 cfg_override: Optional[Dict[str, int]] = None, precision: str = "bf16"):
         nat.require()
         assert streams in (True, False, "auto"), streams
         self.streams_mode = streams

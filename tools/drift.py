@@ -124,6 +124,7 @@ VARIANTS = {
     "bf16": dict(),                                  # default: bf16 pyramid, bf16 z gate / context bias map
     "corr_fp32": dict(corr_dtype=torch.float32),     # fp32 pyramid
     "corr_gate_fp32": dict(corr_dtype=torch.float32, gate_dtype=torch.float32),
+    "fp32": dict(precision="fp32"),                  # fp32 engine (runtime/engine_f32.py)
 }
 
 
