@@ -297,6 +297,8 @@ def main():
     ap.add_argument("--gate-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="storage of the GRU z gate / folded context bias map (the hidden state is fp32 either way)")
     ap.add_argument("--corr-dtype", default="bf16", choices=["bf16", "fp32"], help="correlation pyramid storage")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
+                    help="engine compute precision: bf16 MFMA operands (default) or the fp32 parity mode")
     ap.add_argument("--no-copy-output", action="store_true",
                     help="return the engine's static output buffer instead of a fresh tensor (measurement knob)")
     ap.add_argument("--split", type=int, default=1, help="independent batch parts captured into one hipGraph")
@@ -332,7 +334,7 @@ def main():
     engine_kw = dict(use_graph=not args.no_graph, streams=streams, split=args.split,
                      gate_dtype=torch.bfloat16 if args.gate_dtype == "bf16" else torch.float32,
                      corr_dtype=torch.bfloat16 if args.corr_dtype == "bf16" else torch.float32,
-                     copy_output=not args.no_copy_output)
+                     copy_output=not args.no_copy_output, precision=args.precision)
     B, H, W = args.batch, args.height, args.width
     head = run_inference(ctx, model, B=B, H=H, W=W, iters=args.iters, steps=args.steps, warmup=args.warmup,
                          final_only=args.final_only, gather=not args.no_gather, seed=1234, engine_kw=engine_kw,
@@ -342,20 +344,24 @@ def main():
     torch.cuda.empty_cache()
 
     default_cfg = (args.arch == "raft_large" and (B, H, W, args.iters) == (4, 440, 1024, 32) and not args.final_only
-                   and not args.no_graph)
+                   and not args.no_graph and args.precision == "bf16")
     extras = {}
     if args.extras == "on" or (args.extras == "auto" and default_cfg):
         t_ex = time.perf_counter()
         ks, kw_ = args.extra_steps, max(3, args.warmup)
-        plan = [("b1_fps", "raft_large", 32, BASELINE_FPS), ("small_b1_fps_32it", "raft_small", 32, BASELINE_SMALL_FPS),
-                ("small_b1_fps_12it", "raft_small", 12, None)]
-        for key, arch, it, base in plan:
+        # fp32_b1_fps: the reference's own setting -- fp32 end to end, batch 1 (runtime/engine_f32.py)
+        plan = [("b1_fps", "raft_large", 32, BASELINE_FPS, "bf16"),
+                ("small_b1_fps_32it", "raft_small", 32, BASELINE_SMALL_FPS, "bf16"),
+                ("small_b1_fps_12it", "raft_small", 12, None, "bf16"),
+                ("fp32_b1_fps", "raft_large", 32, BASELINE_FPS, "fp32")]
+        for key, arch, it, base, prec in plan:
             try:
                 m = (raft_large if arch == "raft_large" else raft_small)(seed=0)[0].to(ctx.dev).eval()
                 r = run_inference(ctx, m, B=1, H=H, W=W, iters=it, steps=ks, warmup=kw_, final_only=False,
-                                  gather=not args.no_gather, seed=99, engine_kw=dict(engine_kw, split=1))
+                                  gather=not args.no_gather, seed=99,
+                                  engine_kw=dict(engine_kw, split=1, precision=prec))
                 r.pop("tile_cfgs", None)
-                r["config"] = dict(model=arch, per_gpu_batch=1, num_flow_updates=it, image_size=[H, W])
+                r["config"] = dict(model=arch, per_gpu_batch=1, num_flow_updates=it, image_size=[H, W], dtype=prec)
                 r["vs_baseline"] = round(r["value"] / ctx.world / base, 3) if base else None
                 extras[key] = r
                 del m
@@ -389,7 +395,7 @@ def main():
                             if args.arch == "raft_large" and args.iters == 32 and not args.final_only else None),
             "vs_baseline_note": "batch-4-per-GPU throughput / the reference's batch-1 FPS; "
                                 "extras.b1_fps.vs_baseline is the like-for-like batch-1 ratio",
-            "dtype": "bf16",
+            "dtype": args.precision,
             "data": "synthetic (random Sintel-shaped 440x1024 frames, random-init weights; EPE not measurable)",
             "epe_sintel_clean": None,
             "rccl_world": rccl_world,

@@ -42,6 +42,8 @@ def validate_main(argv: Optional[Sequence[str]] = None) -> int:
     ap.add_argument("--iters", type=int, default=32)
     ap.add_argument("--max-pairs", type=int, default=None)
     ap.add_argument("--batch-size", type=int, default=1, help="pairs per forward (1 = the reference protocol)")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
+                    help="native engine precision (fp32 = the reference's own, runtime/engine_f32.py)")
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--json", default=None)
     args = ap.parse_args(argv)
@@ -58,7 +60,8 @@ def validate_main(argv: Optional[Sequence[str]] = None) -> int:
         factory = raft_large if name == "raft_large" else raft_small
         model, _ = factory(weights=args.weights) if args.weights else factory(pretrained=True)
         out[name] = validate_sintel(model, args.data_root, iters=args.iters, device=device, max_pairs=args.max_pairs,
-                                    batch_size=args.batch_size)
+                                    batch_size=args.batch_size,
+                                    **({} if device.type == "cpu" else dict(precision=args.precision)))
     if args.json and (world == 1 or torch.distributed.get_rank() == 0):
         with open(args.json, "w") as f:
             json.dump(out, f, indent=1)

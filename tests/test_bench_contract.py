@@ -63,6 +63,8 @@ def test_bench_extras_keys():
     assert r.returncode == 0, r.stderr[-2000:]
     rec = _json_lines(r.stdout)[0]
     ex = rec["extras"]
-    assert set(ex) >= {"b1_fps", "small_b1_fps_32it", "small_b1_fps_12it", "train_pairs_per_s", "extras_wall_s"}
-    for k in ("b1_fps", "small_b1_fps_32it", "small_b1_fps_12it", "train_pairs_per_s"):
+    assert set(ex) >= {"b1_fps", "small_b1_fps_32it", "small_b1_fps_12it", "fp32_b1_fps", "train_pairs_per_s",
+                       "extras_wall_s"}
+    assert ex["fp32_b1_fps"]["config"]["dtype"] == "fp32"
+    for k in ("b1_fps", "small_b1_fps_32it", "small_b1_fps_12it", "fp32_b1_fps", "train_pairs_per_s"):
         assert ex[k] is not None and ex[k]["value"] > 0, (k, r.stderr[-1500:])

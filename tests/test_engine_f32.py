@@ -343,3 +343,19 @@ def test_fp32_engine_matches_golden(factory, use_graph):
     assert out.shape == ref.shape
     err = (out - ref).norm(dim=-1).mean().item()
     assert err < 1e-3 * (1 + ref.norm(dim=-1).mean().item()), err
+
+
+@pytest.mark.gpu
+def test_fp32_engine_pipelined_equals_forward():
+    """Graph-pipelined steps (bench.py's batch-1 path) give forward()'s flows, bitwise."""
+    model = raft_small(seed=0)[0].eval().cuda()
+    eng = E.RaftEngine(model, torch.device("cuda", 0), precision="fp32")
+    ins = [_inputs(1, 128, 256, seed=s) for s in (5, 6, 7)]
+    with torch.no_grad():
+        ref = [eng.forward(a.cuda(), b.cuda(), 3) for a, b in ins]
+        outs = [eng.pipelined(a.cuda(), b.cuda(), 3) for a, b in ins]
+        outs.append(eng.flush())
+    torch.cuda.synchronize()
+    assert outs[0] is None
+    for r, o in zip(ref, outs[1:]):
+        assert torch.equal(r, o)
