@@ -297,13 +297,13 @@ extern "C" int jr_corr_pool_f32(const float* src, long M, int hl, int wl, float*
   return (int)hipGetLastError();
 }
 
-extern "C" int jr_corr_lookup_f32(const float* const* levels, int num_levels, int B, int h, int w, int radius,
-                                  const float* coords, float* out, int out_cstride, hipStream_t stream) {
+extern "C" int jr_corr_lookup_f32(const float* const* levels, int num_levels, int B, int h, int w, int nq,
+                                  int radius, const float* coords, float* out, int out_cstride, hipStream_t stream) {
   const int S = 2 * radius + 1;
   if (num_levels < 1 || num_levels > 4 || out_cstride < num_levels * S * S) return (int)hipErrorInvalidValue;
   Lv4 lv{};
   for (int l = 0; l < num_levels; ++l) lv.p[l] = levels[l];
-  const long total = (long)B * h * w;
+  const long total = (long)B * nq;
   const dim3 grid(nblk(total * num_levels * S, 256));
   switch (radius) {
     case 1: hipLaunchKernelGGL(lookup_f32<1>, grid, dim3(256), 0, stream, lv, num_levels, total, h, w, coords, out, out_cstride); break;

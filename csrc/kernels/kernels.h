@@ -315,8 +315,8 @@ int jr_upsample_convex_f32(const float* mask, int mask_cstride, const float* flo
 // 2x2 average pooling (floor) of per-query correlation maps: src [M][hl][wl] -> dst [M][hl/2][wl/2]
 int jr_corr_pool_f32(const float* src, long M, int hl, int wl, float* dst, hipStream_t stream);
 // Pyramid lookup with fp32 output (jr_corr_lookup's semantics and channel order;
-// row-major fp32 levels, no fused update): out [B*h*w][out_cstride]
-int jr_corr_lookup_f32(const float* const* levels, int num_levels, int B, int h, int w, int radius,
+// row-major fp32 levels [B*nq][h_l][w_l], no fused update): out [B*nq][out_cstride]
+int jr_corr_lookup_f32(const float* const* levels, int num_levels, int B, int h, int w, int nq, int radius,
                        const float* coords, float* out, int out_cstride, hipStream_t stream);
 // coords += delta (delta [M][dcs], channels 0, 1: the FlowHead output incl. its bias);
 // flow = coords - coords0 -> flow32 [M][2], hx / qx (channel offsets) and flow4 [M][4] (channels 0, 1)

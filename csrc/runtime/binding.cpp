@@ -1061,12 +1061,14 @@ static Launch make_corr_pool_f32(const TList& t, const IList& i, std::vector<at:
   return [=](hipStream_t s, int) { return jr_corr_pool_f32(ap, (long)M, hl, wl, bp, s); };
 }
 
-// t = [coords, out, l0, l1, l2, l3], i = [num_levels, B, h, w, radius]
+// t = [coords, out, l0, l1, l2, l3], i = [num_levels, B, h, w, radius(, nq: queries per image, default h*w)]
 static Launch make_lookup_f32(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
   at::Tensor coords = opt(t, 0), out = opt(t, 1);
   const int L = (int)i[0], B = (int)i[1], h = (int)i[2], w = (int)i[3], r = (int)i[4];
+  const int nq = i.size() > 5 ? (int)i[5] : h * w;
   const int S = 2 * r + 1;
-  const int64_t M = (int64_t)B * h * w;
+  TORCH_CHECK(nq >= 1, "lookup_f32: nq");
+  const int64_t M = (int64_t)B * nq;
   TORCH_CHECK(L >= 1 && L <= 4 && r >= 1 && r <= 4, "lookup_f32: levels 1..4, radius 1..4");
   check_f32_min(coords, "coords", M * 2);
   check_f32(out, "out");
@@ -1085,7 +1087,7 @@ static Launch make_lookup_f32(const TList& t, const IList& i, std::vector<at::Te
   const float* cp = coords.data_ptr<float>();
   float* op = out.data_ptr<float>();
   const int ocs = cs(out);
-  return [=](hipStream_t s, int) { return jr_corr_lookup_f32(lv.data(), L, B, h, w, r, cp, op, ocs, s); };
+  return [=](hipStream_t s, int) { return jr_corr_lookup_f32(lv.data(), L, B, h, w, nq, r, cp, op, ocs, s); };
 }
 
 // t = [delta ([M][dcs]), coords, flow32, hx, qx?, flow4?], i = [N, h, w, hx_off, qx_off]
@@ -1252,8 +1254,11 @@ class Plan : public torch::CustomClassHolder {
     if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
   }
 
+  // Segment 3 is the second half of the loop body (enqueued right after segment 1 in
+  // every iteration): a context-parallel engine runs the two halves separately, with
+  // the all-gather of the correlation features in between (run_segment).
   void set_segment(int64_t s) {
-    TORCH_CHECK(s >= 0 && s <= 2, "segment must be 0 (prologue), 1 (loop) or 2 (epilogue)");
+    TORCH_CHECK(s >= 0 && s <= 3, "segment must be 0 (prologue), 1 (loop), 2 (epilogue) or 3 (loop, second half)");
     seg_ = (int)s;
     defer_ = 0;
     reset_graph();
@@ -1326,6 +1331,12 @@ class Plan : public torch::CustomClassHolder {
 
   // Launch prologue, n_iters x loop body, epilogue (lane 0 = current stream).
   void run(int64_t n_iters) { JR_CHECK_OK(enqueue(cur_stream(), (int)n_iters)); }
+  // Launch one segment alone with iteration index `it` (eager; host-driven loops
+  // that interleave collectives with the segments, runtime/engine.py context parallelism).
+  void run_segment(int64_t seg, int64_t it) {
+    TORCH_CHECK(seg >= 0 && seg <= 3, "segment must be 0..3");
+    JR_CHECK_OK(enqueue(cur_stream(), (int)it, false, -1, (int)seg));
+  }
   // Enqueue into a stream that an outer capture is recording (e.g. a whole
   // training step captured by torch.cuda.graph): lane 0 is the caller's stream
   // itself, as in capture(), so the origin stream never holds only fork / join
@@ -1625,7 +1636,8 @@ class Plan : public torch::CustomClassHolder {
     }
   }
   // part: -1 = the whole forward, 0 = prologue only, 1 = loop + epilogue only.
-  int enqueue(hipStream_t s, int n_iters, bool capturing = false, int part = -1) {
+  // only_seg >= 0: just that segment, with iteration index n_iters.
+  int enqueue(hipStream_t s, int n_iters, bool capturing = false, int part = -1, int only_seg = -1) {
     if (int r = ensure_resources()) return r;
     check_ = std::getenv("JR_PLAN_CHECK") != nullptr && std::getenv("JR_PLAN_CHECK")[0] == '1';
     capturing_ = capturing;
@@ -1642,8 +1654,9 @@ class Plan : public torch::CustomClassHolder {
     // a loop-only capture, capture_part(1))
     bool used[kMaxLanes] = {};
     used[0] = true;
-    for (int sg = 0; sg < 3; ++sg) {
+    for (int sg = 0; sg < 4; ++sg) {
       if ((sg == 0 && part == 1) || (sg != 0 && part == 0)) continue;
+      if (only_seg >= 0 && sg != only_seg) continue;
       for (const auto& o : segs_[sg]) used[o.lane] = true;
     }
     if (int r = (int)hipEventRecord(fork_, s)) return r;
@@ -1657,6 +1670,10 @@ class Plan : public torch::CustomClassHolder {
     // enqueue of each phase: encoders + correlation pyramid, every refinement
     // iteration, the epilogue.
     RangeGuard all("raft.plan");
+    if (only_seg >= 0) {
+      RangeGuard r("raft.segment");
+      for (auto& o : segs_[only_seg]) if (int e = exec_op(o, st, n_iters, recorded)) return e;
+    } else {
     if (part != 1) {
       RangeGuard r("raft.prologue");
       for (auto& o : segs_[0]) if (int e = exec_op(o, st, 0, recorded)) return e;
@@ -1664,10 +1681,12 @@ class Plan : public torch::CustomClassHolder {
     for (int it = 0; part != 0 && it < n_iters; ++it) {
       RangeGuard r("raft.iteration");
       for (auto& o : segs_[1]) if (int e = exec_op(o, st, it, recorded)) return e;
+      for (auto& o : segs_[3]) if (int e = exec_op(o, st, it, recorded)) return e;
     }
     if (part != 0) {
       RangeGuard r("raft.epilogue");
       for (auto& o : segs_[2]) if (int e = exec_op(o, st, n_iters, recorded)) return e;
+    }
     }
     for (int l = l0; l < used_lanes_; ++l) {
       if (!used[l]) continue;
@@ -1676,7 +1695,7 @@ class Plan : public torch::CustomClassHolder {
     }
     return 0;
   }
-  std::vector<Op> segs_[3];
+  std::vector<Op> segs_[4];
   std::vector<at::Tensor> keep_;
   int seg_ = 0;
   int lane_ = 0;
@@ -1796,6 +1815,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("num_ops", &jr::Plan::num_ops)
       .def("op_names", &jr::Plan::op_names)
       .def("run", &jr::Plan::run)
+      .def("run_segment", &jr::Plan::run_segment)
       .def("run_inline", &jr::Plan::run_inline)
       .def("capture", &jr::Plan::capture)
       .def("captured_iters", &jr::Plan::captured_iters)

@@ -22,6 +22,15 @@ shards the volume over the ranks of a process group:
   deterministic kernels keep the recurrent state identical on every rank, so
   no further synchronisation is needed.
 
+On the GPU the wrapper runs the native engine in context-parallel mode
+(``RaftEngine(cp_group=...)``, runtime/engine.py): each rank's plan holds its
+slab's pyramid (the MFMA corr kernel with ``nq`` = slab pixels, row-major
+levels), segment 1 of every iteration runs the slab lookups, the engine
+all-gathers the features into the full map, and segment 3 runs the rest of the
+iteration -- all kernels launched from C++ (``Plan.run_segment``).  On the CPU
+(and as the executable specification) the module path below does the same with
+PyTorch ops.
+
 Inference only (``torch.no_grad``): training resolutions (368x496 crops) never
 need the volume sharded, and a CP backward would need the encoder gradients
 all-reduced over the query slabs.
@@ -90,9 +99,10 @@ class ContextParallelRAFT:
     ``cp(image1, image2, num_flow_updates)`` returns the same (N, B, H, W, 2)
     flows as ``model.apply`` on every rank."""
 
-    def __init__(self, model, group=None):
+    def __init__(self, model, group=None, **engine_kw):
         self.model = model
         self.group = group
+        self.engine_kw = engine_kw   # native engine options on the GPU (e.g. precision="fp32")
         if dist.is_available() and dist.is_initialized():
             self.rank = dist.get_rank(group)
             self.world = dist.get_world_size(group)
@@ -109,6 +119,9 @@ class ContextParallelRAFT:
         B, H, W, _ = image1.shape
         assert tuple(image2.shape) == tuple(image1.shape), "input images should have the same shape"
         assert H % 8 == 0 and W % 8 == 0, "input image H and W should be divisible by 8"
+        if image1.is_cuda:
+            eng = m.engine(image1.device, cp_group=True if self.group is None else self.group, **self.engine_kw)
+            return eng.forward(image1, image2, num_flow_updates, return_all_iters=return_all_iters)
         fmaps = m.feature_encoder(torch.cat([image1, image2], dim=0), False)
         fmap1, fmap2 = torch.chunk(fmaps, 2, dim=0)
         h, w = fmap1.shape[1], fmap1.shape[2]

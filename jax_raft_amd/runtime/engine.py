@@ -120,6 +120,8 @@ class _PlanState:
     out_slot: Optional[torch.Tensor] = None
     slot_ok: bool = True
     slot_ptr: int = 0
+    # context parallelism: {slabs, nq (padded slab pixels per image), local, corr} (see _gather_corr)
+    cp: Optional[dict] = None
 
 
 class RaftEngine:
@@ -154,6 +156,14 @@ class RaftEngine:
             leave idle.
         cfg_override: fixed tile configs per conv spec name (e.g. {"gru0.b": 27},
             tools/schedule_tune.py); ``JR_CFG_OVERRIDE="name=cfg,..."`` adds entries.
+        cp_group: context parallelism of the correlation volume:
+            a torch.distributed process group (``True``: the default group) whose
+            ranks each hold the pyramid of one slab of query rows
+            (``parallel/cp.py:row_slabs``) and all-gather the looked-up
+            correlation features every iteration (RCCL over xGMI); the rest of
+            the update block runs replicated.  Pyramid memory per rank / world.
+            One lane, eager from C++ (the collective sits between the two
+            halves of the loop body, ``Plan.run_segment``).
         precision: "bf16" (default: bf16 MFMA operands and activations, fp32
             accumulation, fp32 hidden state / flow / upsampled output) or "fp32"
             (the reference's own precision end to end on the f32 MFMA:
@@ -185,8 +195,9 @@ class RaftEngine:
     def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True,
                  corr_dtype: torch.dtype = torch.bfloat16, gate_dtype: torch.dtype = torch.bfloat16,
                  autotune: bool = True, streams="auto", split: int = 1,
-                 cfg_override: Optional[Dict[str, int]] = None, precision: str = "bf16"):
+                 cfg_override: Optional[Dict[str, int]] = None, precision: str = "bf16", cp_group=None):
         nat.require()
+        self._init_cp(cp_group)
         assert streams in (True, False, "auto"), streams
         self.streams_mode = streams
         self.streams = bool(streams)
@@ -539,6 +550,51 @@ class RaftEngine:
     # (raft_small) one lane measured 562 vs 528 pairs/s at batch 4.
     AUTO_STREAMS_MIN_BATCH = 4
 
+    def _init_cp(self, cp_group) -> None:
+        self.cp = cp_group is not None and cp_group is not False
+        self.cp_group = None if cp_group is True else cp_group
+        self.cp_rank, self.cp_world = 0, 1
+        if self.cp:
+            import torch.distributed as dist
+
+            if dist.is_available() and dist.is_initialized():
+                self.cp_rank = dist.get_rank(self.cp_group)
+                self.cp_world = dist.get_world_size(self.cp_group)
+
+    def _cp_slabs(self, h: int):
+        from ..parallel.cp import row_slabs
+
+        return row_slabs(h, self.cp_world)
+
+    def _gather_corr(self, st: _PlanState) -> None:
+        """All-gather every rank's looked-up correlation features ``local``
+        (B, nq, C) into the full-map ``corr`` (B*h*w, C) (stream-ordered with
+        the plan: the eager plan forks from / joins to the current stream)."""
+        cp = st.cp
+        local, corr, slabs, w = cp["local"], cp["corr"], cp["slabs"], cp["w"]
+        B = local.shape[0]
+        full = corr.view(B, -1, corr.shape[-1])
+        if self.cp_world == 1:
+            full[:, : local.shape[1]].copy_(local)
+            return
+        import torch.distributed as dist
+
+        parts = cp.get("parts")
+        if parts is None:
+            parts = cp["parts"] = [torch.empty_like(local) for _ in slabs]
+        dist.all_gather(parts, local, group=self.cp_group)
+        for (r0, r1), part in zip(slabs, parts):
+            full[:, r0 * w:r1 * w].copy_(part[:, : (r1 - r0) * w])
+
+    def _forward_cp(self, st: _PlanState, n_iters: int) -> None:
+        plan = st.plan
+        plan.run_segment(0, 0)
+        for it in range(n_iters):
+            plan.run_segment(1, it)
+            self._gather_corr(st)
+            plan.run_segment(3, it)
+        plan.run_segment(2, n_iters)
+
     def _lanes_ok(self, all_iters: bool) -> bool:
         """The lane schedule needs a mask head to overlap (every iteration
         upsampled) and the FlowHead taps epilogue (a 256-channel conv1)."""
@@ -551,7 +607,7 @@ class RaftEngine:
         (:meth:`pipelined`) measured faster only on one-lane plans: batch 1
         145 -> 157 pairs/s, raft_small batch 4 559 -> 602, final-only 326 -> 346;
         with lanes (raft_large batch 4) 319 -> 289 (profiles/r2_pipelined_graph_ab.txt)."""
-        if not self._lanes_ok(all_iters):
+        if self.cp or not self._lanes_ok(all_iters):
             return False
         if self.streams_mode != "auto":
             return bool(self.streams_mode)
@@ -569,7 +625,7 @@ class RaftEngine:
             f"Feature maps are too small to be down-sampled by the correlation pyramid: need >= {min_sz}, got {(h, w)}; "
             f"input images should be at least {8 * min_sz}.")
         dev = self.device
-        parts = self.split if (self.split > 1 and B % self.split == 0) else 1
+        parts = self.split if (self.split > 1 and B % self.split == 0 and not self.cp) else 1
         nb = B // parts
         # Each part is an independent forward with its own Plan; with use_graph
         # their captures are copied into ONE hipGraph (Plan.merge_*), so the
@@ -697,17 +753,27 @@ class RaftEngine:
             self._conv(plan, sp["fe.conv"], feat, 2 * B, h, w, fmap)
         # bf16 levels of /16-wide maps: levels 0 / 1 in the blocked layout (one
         # pyramid tile per block: whole-line writes, 2 x 2 blocks per lookup window)
-        blocked = int(self.corr_dtype == BF16 and w % 16 == 0 and (h * w) % 8 == 0)
+        blocked = int(self.corr_dtype == BF16 and w % 16 == 0 and (h * w) % 8 == 0 and not self.cp)
         self.corr_blocked = bool(blocked)
+        # context parallelism: this rank's pyramid holds the query rows [r0, r1) only
+        slabs = self._cp_slabs(h) if self.cp else [(0, h)]
+        r0, r1 = slabs[self.cp_rank]
+        nq = (r1 - r0) * w
         levels = []
         hl, wl = h, w
         for l in range(L):
-            shape = (M, -(-h // 8) * (8 >> l), -(-w // 16) * (16 >> l)) if blocked and l < 2 else (M, hl, wl)
+            shape = (M, -(-h // 8) * (8 >> l), -(-w // 16) * (16 >> l)) if blocked and l < 2 else (B * nq, hl, wl)
             levels.append(alloc(f"corr.l{l}", shape, self.corr_dtype))
             hl //= 2
             wl //= 2
-        plan.add_corr([fmap[:B], fmap[B:]] + levels + [None] * (4 - L), [B, h, w, self.fmap_ch, L, h * w, blocked],
-                      1.0 / float(self.fmap_ch) ** 0.5)
+        scale = 1.0 / float(self.fmap_ch) ** 0.5
+        if self.cp:
+            for b in range(B):
+                plan.add_corr([fmap[b, r0:r1], fmap[B + b]] + [v[b * nq:(b + 1) * nq] for v in levels] + [None] * (4 - L),
+                              [1, h, w, self.fmap_ch, L, nq, 0], scale)
+        else:
+            plan.add_corr([fmap[:B], fmap[B:]] + levels + [None] * (4 - L), [B, h, w, self.fmap_ch, L, h * w, blocked],
+                          scale)
         plan.add_wait(E_CTX)
 
         # ---------------- loop body: one refinement iteration (model.py:495-510)
@@ -719,7 +785,8 @@ class RaftEngine:
         c1 = alloc("c1", (M, cl[0])) if len(cl) == 2 else None
         taps = alloc("fh2.taps", (M, 24), F32)
         stride = st.out.shape[1] * H * W * 2  # one iteration of the full-batch output
-        split_mask = lanes_on   # mask predictor's 3x3 conv on the mask lane (else fused into FlowHead conv1)
+        # mask predictor's 3x3 conv on its own (mask lane / context parallel), else fused into FlowHead conv1
+        split_mask = lanes_on or self.cp
         # FlowHead conv1 of the loop: alone (lanes / final-only / no mask head) or
         # fused with the mask predictor's 3x3 conv (one lane, every iteration upsampled)
         s1 = sp["fh1"] if (self.has_mask and all_iters and not split_mask) else sp["fh1.flow"] if self.has_mask else sp["fh1"]
@@ -805,7 +872,28 @@ class RaftEngine:
                 self._conv(plan, sp[f"gru{gi}.b"], qx, B, h, w, hx, h32=h32, zbuf=zb, hidden=self.hidden,
                            epi=EPI_GRU_B, bmap=gbias[gi], bmap_coff=2 * self.hidden)
 
-        if lanes_on:
+        if self.cp:
+            # segment 1: this rank's lookups; the engine all-gathers them into `corr`
+            # (_gather_corr); segment 3: the rest of the iteration, replicated
+            hw = h * w
+            local = alloc("corr.local", (B, max(b_ - a_ for a_, b_ in slabs) * w, self.corr_cs))
+            plan.set_segment(1)
+            for b in range(B):
+                plan.add_lookup([coords[b * hw + r0 * w:b * hw + r1 * w], local[b]]
+                                + [v[b * nq:(b + 1) * nq] for v in levels] + [None] * (4 - L),
+                                [L, 1, h, w, self.radius, nq, 0])
+            plan.set_segment(3)
+            flow_features()
+            motion_and_gru(wait_flow=False, wait_mask=False)
+            flow_head()
+            flow_update()
+            if all_iters:
+                upsample(stride, mask_from_fm=False)
+            plan.set_segment(2)
+            if not all_iters:
+                upsample(0, mask_from_fm=False)
+            st.cp = dict(slabs=slabs, local=local, corr=corr, w=w)
+        elif lanes_on:
             # iteration 0's flow features (zero flow) run once in the prologue
             plan.set_segment(0)
             lane(main)
@@ -878,7 +966,9 @@ class RaftEngine:
         fresh = self.copy_output and st.slot_ok
         out = torch.empty_like(st.out) if fresh else st.out
         self._point_slot(st, out)
-        if len(st.plans) == 1 or not self.use_graph:
+        if st.cp is not None:
+            self._forward_cp(st, num_flow_updates)
+        elif len(st.plans) == 1 or not self.use_graph:
             for plan in st.plans:
                 self._launch(plan, num_flow_updates)
         else:
@@ -943,6 +1033,7 @@ class RaftEngine:
         B, H, W, C = image1.shape
         assert C == 3, "images must be NHWC with 3 channels"
         assert self.use_graph, "pipelined() replays captured graphs (use_graph=True)"
+        assert not self.cp, "pipelined(): not with context parallelism (a host-driven loop)"
         n = num_flow_updates
         key = (B, H, W, n, bool(return_all_iters))
         pp = self._pp

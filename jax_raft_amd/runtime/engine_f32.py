@@ -223,22 +223,26 @@ class RaftEngineF32(RaftEngine):
             gbias.append(gb)
         plan.add_init_coords([coords], [B, h, w])
         # correlation pyramid (model.py:418-446, 472-481): level 0 = fmap1 . fmap2^T / sqrt(C)
-        # per image on the fp32 MFMA GEMM, then 2x2 floor average pooling per level
+        # per image on the fp32 MFMA GEMM, then 2x2 floor average pooling per level; with
+        # context parallelism only this rank's query rows [r0, r1)
+        slabs = self._cp_slabs(h) if self.cp else [(0, h)]
+        r0, r1 = slabs[self.cp_rank]
+        nq = (r1 - r0) * w
         levels = []
         hl, wl = h, w
         for lv in range(L):
-            levels.append(alloc(f"corr.l{lv}", (M, hl, wl)))
+            levels.append(alloc(f"corr.l{lv}", (B * nq, hl, wl)))
             hl //= 2
             wl //= 2
         zero_b = alloc("corr.bias", (hw,))
         C = self.fmap_ch
         for b in range(B):
             wspec = nat.ConvSpecF32(fmap[B + b].reshape(hw, C), zero_b, 1, 1, 1, 1, 0, 0, C, C, hw)
-            self._conv(plan, wspec, fmap[b:b + 1], 1, h, w, levels[0][b * hw:(b + 1) * hw].view(hw, hw),
+            self._conv(plan, wspec, fmap[b, r0:r1], 1, r1 - r0, w, levels[0][b * nq:(b + 1) * nq].view(nq, hw),
                        alpha=1.0 / float(C) ** 0.5)
         hl, wl = h, w
         for lv in range(1, L):
-            plan.add_corr_pool_f32([levels[lv - 1], levels[lv]], [M, hl, wl])
+            plan.add_corr_pool_f32([levels[lv - 1], levels[lv]], [B * nq, hl, wl])
             hl //= 2
             wl //= 2
 
@@ -265,7 +269,18 @@ class RaftEngineF32(RaftEngine):
             plan.add_upsample_convex_f32([mask, flow32, st.out, st.out_slot], [B, h, w, stride, 0])
 
         plan.set_segment(1)
-        plan.add_lookup_f32([coords, corr] + levels + [None] * (4 - L), [L, B, h, w, self.radius])
+        if self.cp:
+            # this rank's lookups; the engine all-gathers them into `corr` (_gather_corr)
+            # before segment 3, the rest of the iteration (replicated)
+            local = alloc("corr.local", (B, max(b_ - a_ for a_, b_ in slabs) * w, self.corr_cs))
+            for b in range(B):
+                plan.add_lookup_f32([coords[b * hw + r0 * w:b * hw + r1 * w], local[b]]
+                                    + [v[b * nq:(b + 1) * nq] for v in levels] + [None] * (4 - L),
+                                    [L, 1, h, w, self.radius, nq])
+            st.cp = dict(slabs=slabs, local=local, corr=corr, w=w)
+            plan.set_segment(3)
+        else:
+            plan.add_lookup_f32([coords, corr] + levels + [None] * (4 - L), [L, B, h, w, self.radius])
         if c1 is not None:
             self._conv(plan, sp["me.convcorr1"], corr, B, h, w, c1, act=ACT_RELU)
             self._conv(plan, sp["me.convcorr2"], c1, B, h, w, cf, act=ACT_RELU)

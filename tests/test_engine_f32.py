@@ -73,7 +73,7 @@ class F32Interp:
     """Records a plan like the native Plan and executes it with PyTorch ops."""
 
     def __init__(self):
-        self.segs = {0: [], 1: [], 2: []}
+        self.segs = {0: [], 1: [], 2: [], 3: []}
         self.seg = 0
 
     def set_segment(self, s):
@@ -98,10 +98,14 @@ class F32Interp:
         for op, a in self.segs[0]:
             self._exec(op, a, 0)
         for it in range(n_iters):
-            for op, a in self.segs[1]:
+            for op, a in self.segs[1] + self.segs[3]:
                 self._exec(op, a, it)
         for op, a in self.segs[2]:
             self._exec(op, a, n_iters)
+
+    def run_segment(self, seg, it):
+        for op, a in self.segs[seg]:
+            self._exec(op, a, it)
 
     @staticmethod
     def _exec(op, a, it):
@@ -149,12 +153,14 @@ class F32Interp:
             ho, wo = hl // 2, wl // 2
             d.copy_(s[:, :2 * ho, :2 * wo].reshape(M, ho, 2, wo, 2).mean(dim=(2, 4)))
         elif op == "lookup_f32":
-            t, (L, B, h, w, r) = a
+            t, i = a
+            L, B, h, w, r = i[:5]
+            nq = i[5] if len(i) > 5 else h * w
             coords, out = t[0], t[1]
             lv = [v for v in t[2:2 + L]]
-            c = coords.reshape(B, h, w, 2)
-            o = R.index_pyramid(lv, c, r).reshape(B * h * w, -1)
-            out[:, :o.shape[1]] = o
+            c = coords.reshape(B, nq, 1, 2)
+            o = R.index_pyramid(lv, c, r).reshape(B * nq, -1)
+            out.view(-1, out.shape[-1])[:B * nq, :o.shape[1]] = o
         elif op == "flow_update_f32":
             (d, coords, f32, hx, qx, f4), (N, h, w, hx_off, qx_off) = a
             M = N * h * w
@@ -359,3 +365,54 @@ def test_fp32_engine_pipelined_equals_forward():
     assert outs[0] is None
     for r, o in zip(ref, outs[1:]):
         assert torch.equal(r, o)
+
+
+def _cp_worker(rank, world, port, arch, out):
+    import os
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(2)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    nat.require = lambda: None
+    nat.new_plan = F32Interp
+    tunedb.gpu_arch = lambda device=None: "cpu"
+    model = (raft_large if arch == "raft_large" else raft_small)(seed=0)[0].eval()
+    i1, i2 = _inputs(2, 128, 160, seed=7)
+    with torch.no_grad():
+        eng = E.RaftEngine(model, "cpu", precision="fp32", cp_group=True, copy_output=False)
+        flows = eng.forward(i1, i2, 2).clone()
+        st = next(iter(eng._states.values()))
+        assert st.cp is not None and st.plan.names(1) == ["lookup_f32"] * 2
+    parts = [torch.empty_like(flows) for _ in range(world)]
+    torch.distributed.all_gather(parts, flows)
+    if rank == 0:
+        torch.save(torch.stack(parts), out)
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("arch,world", [("raft_small", 2), ("raft_small", 3), ("raft_large", 2)])
+def test_engine_context_parallel_gloo(tmp_path, arch, world):
+    """Context parallelism on the native engine (cp_group): 16 query rows over 2 / 3
+    gloo ranks (3: uneven slabs), each rank's plan holding its slab's pyramid, the
+    looked-up features all-gathered between the two halves of every iteration; the
+    fp32 plans run by the interpreter reproduce the single-process golden forward."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "cp.pt")
+    mp.spawn(_cp_worker, args=(world, port, arch, out), nprocs=world, join=True)
+    got = torch.load(out, weights_only=True)
+    for r in range(1, world):
+        assert torch.equal(got[r], got[0])
+    model = (raft_large if arch == "raft_large" else raft_small)(seed=0)[0].eval()
+    i1, i2 = _inputs(2, 128, 160, seed=7)
+    with torch.no_grad():
+        ref = model(i1, i2, num_flow_updates=2)
+    err = (got[0] - ref).abs().max().item()
+    assert err < 2e-3 * (1 + ref.abs().max().item()), err

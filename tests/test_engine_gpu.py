@@ -328,3 +328,60 @@ def test_lane_schedule_graph_equals_eager_and_tracks_golden():
     mag = gold.norm(dim=-1).mean().item()
     for it in range(5):
         assert _epe(a[it].cpu(), gold[it]) < 0.05 * mag + 0.05, it
+
+
+def test_engine_context_parallel_single_slab():
+    """cp_group without a process group (one slab): the context-parallel schedule
+    (row-major pyramid, lookups in segment 1, the rest after the gather) vs the
+    default engine and the golden forward."""
+    torch.manual_seed(0)
+    model, variables = raft_large(seed=0)
+    i1, i2 = _inputs(2, 128, 256)
+    ref = model.apply(variables, i1, i2, train=False, num_flow_updates=3)
+    model = model.eval().cuda()
+    from jax_raft_amd.runtime.engine import RaftEngine
+
+    with torch.no_grad():
+        cp = RaftEngine(model, torch.device("cuda", 0), cp_group=True).forward(i1.cuda(), i2.cuda(), 3).cpu()
+        base = RaftEngine(model, torch.device("cuda", 0)).forward(i1.cuda(), i2.cuda(), 3).cpu()
+    torch.cuda.synchronize()
+    mag = ref.norm(dim=-1).mean().item()
+    assert _epe(cp[-1], ref[-1]) < 0.05 * mag + 0.05
+    assert _epe(cp[-1], base[-1]) < 0.02 * mag + 0.02
+
+
+def test_engine_context_parallel_two_ranks(tmp_path):
+    """Two context-parallel ranks sharing cuda:0 over gloo (JR_SHARE_GPU=1): both
+    ranks return the same flows, the fp32 engine's equal to the single-process
+    fp32 engine to rounding, the bf16 engine's within the engine tolerance of the
+    golden; final-only mode too."""
+    import os
+    import subprocess
+    import sys
+
+    from jax_raft_amd.runtime.engine import RaftEngine
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, JR_SHARE_GPU="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29637",
+           os.path.join(root, "tests", "_cp_gpu_worker.py"), str(tmp_path)]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    a = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    b = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    model, variables = raft_large(seed=0)
+    g = torch.Generator().manual_seed(11)
+    base = torch.rand(2, 136, 264, 3, generator=g) * 2 - 1
+    i1, i2 = base[:, 4:132, 4:260].contiguous(), base[:, 2:130, 6:262].contiguous()
+    ref = model.apply(variables, i1, i2, train=False, num_flow_updates=3)
+    mag = ref.norm(dim=-1).mean().item()
+    assert _epe(a["bf16"][-1], ref[-1]) < 0.05 * mag + 0.05
+    assert torch.equal(a["bf16_final"][0], a["bf16"][-1]) or _epe(a["bf16_final"][0], a["bf16"][-1]) < 1e-3
+    with torch.no_grad():
+        f32 = RaftEngine(model.eval().cuda(), torch.device("cuda", 0), precision="fp32").forward(
+            i1.cuda(), i2.cuda(), 3).cpu()
+    assert (a["fp32"] - f32).abs().max().item() < 1e-3
+    assert _epe(a["fp32"][-1], ref[-1]) < 1e-3 * (1 + mag)

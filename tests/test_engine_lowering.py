@@ -99,3 +99,24 @@ def test_engine_knobs_are_few(fake):
 
     params = [n for n in inspect.signature(E.RaftEngine.__init__).parameters if n not in ("self", "model", "device")]
     assert len(params) <= 10, params
+
+
+@pytest.mark.parametrize("factory", [raft_large, raft_small])
+def test_context_parallel_schedule(factory, fake):
+    """cp_group: the slab lookups (one per image) alone in loop segment 1, the rest
+    of the iteration in segment 3 (after the engine's all-gather), per-image slab
+    correlation in the prologue, no cross-lane events, no deferred ops."""
+    model = factory()[0].eval()
+    eng = E.RaftEngine(model, "cpu", autotune=False, cp_group=True)
+    st = eng._build(2, 128, 256, 3, True)
+    p = st.plan
+    assert st.cp is not None and not eng.uses_lanes(2)
+    assert p.names(1) == ["lookup", "lookup"]
+    seg3 = p.names(3)
+    assert "lookup" not in seg3 and seg3.count("flow_taps") == 1
+    assert seg3[-1] in ("convex_head", "upsample_bilinear", "upsample_convex")
+    assert p.names(0).count("corr") == 2
+    assert not any(op in ("record", "wait") for s, _, _, op, _ in p.ops if s in (1, 3))
+    assert all(d == 0 for s, _, d, _, _ in p.ops)
+    # one slab of every query row without a process group
+    assert st.cp["slabs"] == [(0, 16)]
