@@ -21,6 +21,12 @@ def _inputs(B, H, W, seed=0):
     return i1.contiguous(), i2.contiguous()
 
 
+# Measured on MI355X (tools/parity_probe.py): max over the 4 iterations of EPE / mean
+# |golden flow| = 0.0478-0.0486 (raft_small), 0.0134-0.0172 (raft_large); the bounds
+# leave 1.3x / 1.5x headroom (the bf16 drift at the headline size is tests/test_drift.py).
+REL_EPE = {"raft_small": 0.065, "raft_large": 0.026}
+
+
 @pytest.mark.parametrize("factory", [raft_small, raft_large])
 @pytest.mark.parametrize("use_graph", [False, True])
 @pytest.mark.parametrize("B,W", [(2, 160), (2, 256), (4, 256)])
@@ -42,7 +48,7 @@ def test_engine_matches_golden(factory, use_graph, B, W):
     mag = ref.norm(dim=-1).mean().item()
     for it in range(iters):
         e = _epe(out[it], ref[it])
-        assert e < 0.05 * mag + 0.05, (it, e, mag)
+        assert e < REL_EPE[factory.__name__] * mag, (it, e, mag)
 
 
 def test_graph_replay_equals_eager():
