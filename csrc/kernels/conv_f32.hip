@@ -6,9 +6,10 @@
 // own precision, and (as a 1x1 "conv" whose weight rows are fmap2's pixels) the
 // all-pairs correlation GEMM (:472-481).
 //
-// Design: 64 x 64 (output channel x pixel) block tile, 4 waves of 32 x 32
-// (2 x 2 MFMA tiles), 32-deep K stages double-buffered in LDS, global loads
-// one stage ahead in registers.  Weights are plain row-major [cout][K] with
+// Design: 4 waves (2 x 2) per block, 64 x 64 block tiles (output channel x
+// pixel; 2 x 2 MFMA tiles per wave), 32-deep K stages double-buffered in LDS,
+// global loads one stage ahead in registers; split-K with an ordered reduction
+// for grids of fewer than 4 blocks per CU.  Weights are plain row-major [cout][K] with
 // K = (kh, kw, cin4) -- no permutation, so the correlation uses fmap2 itself as
 // the weight matrix.  Activations are fp32 NHWC with a channel stride / offset,
 // channels padded to 4 (16-byte chunks).  The D fragment gives each lane 4
@@ -22,7 +23,7 @@
 
 namespace {
 
-constexpr int FB_CO = 64, FB_P = 64, FBK = 32, FPAD = 4;   // LDS rows of 36 floats: conflict-free b32 reads
+constexpr int FPAD = 4;   // LDS rows of FBK + 4 floats (36 / 20): conflict-free b32 fragment reads
 
 // 4 consecutive channels at p (nv < 4: the channel tail of a cout % 4 != 0 conv, scalar)
 JR_DEVICE void ld4(const float* p, int nv, float (&v)[4]) {
@@ -99,21 +100,29 @@ JR_DEVICE void f32_epilogue(const ConvF32Params& p, float (&v)[4], int m, int c0
   }
 }
 
-template <int EPI>
+// Block tile BCO x BP = (32 WM) x (32 WN) (output channels x pixels), 2 x 2
+// waves of (16 WM) x (16 WN) (WM x WN MFMA tiles: WM + WN LDS reads per WM x WN
+// MFMAs), FBK-deep K stages double-buffered in LDS, loads one stage ahead.
+// SPLIT: split-K over blockIdx.z (p.ksplit ranges of K stages); raw partial sums
+// go to p.part [ksplit][M][coutp] and conv_f32_reduce applies the epilogue.
+template <int EPI, bool SPLIT, int WM, int WN, int FBK>
 __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvF32Params p) {
-  __shared__ float sA[2][FB_CO][FBK + FPAD];
-  __shared__ float sB[2][FB_P][FBK + FPAD];
+  constexpr int BCO = 32 * WM, BP = 32 * WN;
+  constexpr int CPR = FBK / 4, RPP = 256 / CPR;       // 16-B chunks per row, rows per staging pass
+  constexpr int NA = BCO / RPP, NB = BP / RPP;        // staging passes of A / B
+  static_assert(NA >= 1 && NB >= 1 && BCO % RPP == 0 && BP % RPP == 0, "tile");
+  __shared__ float sA[2][BCO][FBK + FPAD];
+  __shared__ float sB[2][BP][FBK + FPAD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int p0 = blockIdx.x * FB_P, co0 = blockIdx.y * FB_CO;
+  const int p0 = blockIdx.x * BP, co0 = blockIdx.y * BCO;
   const int OHW = p.OH * p.OW;
-  // per-thread staging: 2 chunks (4 floats) of A and of B per stage: rows tid/8 and tid/8 + 32, k-chunk tid % 8
-  const int kc = tid & 7;
-  int ihb[2], iwb[2];
-  long xbase[2];
-  bool pok[2];
+  const int kc = tid % CPR, r0 = tid / CPR;
+  int ihb[NB], iwb[NB];
+  long xbase[NB];
+  bool pok[NB];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int m = p0 + (tid >> 3) + 32 * i;
+  for (int i = 0; i < NB; ++i) {
+    const int m = p0 + r0 + RPP * i;
     pok[i] = m < p.M;
     const int mm = pok[i] ? m : 0;
     const int n = mm / OHW, rem = mm - n * OHW, oh = rem / p.OW, ow = rem - oh * p.OW;
@@ -121,17 +130,25 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvF32Params p) {
     iwb[i] = ow * p.SW - p.PW;
     xbase[i] = (long)n * p.H * p.W * p.x_cs + p.x_coff;
   }
-  const int nks = (p.K + FBK - 1) / FBK;
-  float4 ra[2], rb[2];
+  const int nks_all = (p.K + FBK - 1) / FBK;
+  int ks_begin = 0, nks = nks_all;
+  if constexpr (SPLIT) {
+    ks_begin = (int)((long)nks_all * blockIdx.z / p.ksplit);
+    nks = (int)((long)nks_all * (blockIdx.z + 1) / p.ksplit) - ks_begin;
+  }
+  float4 ra[NA], rb[NB];
   auto load = [&](int ks) {
-    const int k = ks * FBK + kc * 4;
+    const int k = (ks_begin + ks) * FBK + kc * 4;
     const bool kok = k < p.K;
     const int tap = kok ? k / p.cin4 : 0, ci = k - tap * p.cin4;
     const int kh = tap / p.KW, kw = tap - kh * p.KW;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int co = co0 + (tid >> 3) + 32 * i;
+    for (int i = 0; i < NA; ++i) {
+      const int co = co0 + r0 + RPP * i;
       ra[i] = (kok && co < p.cout) ? *(const float4*)(p.w + (long)co * p.K + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
       const int ih = ihb[i] + kh, iw = iwb[i] + kw;
       const bool ok = kok && pok[i] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
       rb[i] = ok ? *(const float4*)(p.x + xbase[i] + ((long)ih * p.W + iw) * p.x_cs + ci) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -139,19 +156,17 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvF32Params p) {
   };
   auto store = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = (tid >> 3) + 32 * i;
-      *(float4*)&sA[buf][r][kc * 4] = ra[i];
-      *(float4*)&sB[buf][r][kc * 4] = rb[i];
-    }
+    for (int i = 0; i < NA; ++i) *(float4*)&sA[buf][r0 + RPP * i][kc * 4] = ra[i];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) *(float4*)&sB[buf][r0 + RPP * i][kc * 4] = rb[i];
   };
-  const int wco = (wave & 1) * 32, wp = (wave >> 1) * 32;
+  const int wco = (wave & 1) * 16 * WM, wp = (wave >> 1) * 16 * WN;
   const int li = lane & 15, lk = lane >> 4;
-  f32x4 acc[2][2];
+  f32x4 acc[WM][WN];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < WM; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < WN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   load(0);
   store(0);
   __syncthreads();
@@ -160,33 +175,72 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvF32Params p) {
     if (ks + 1 < nks) load(ks + 1);
 #pragma unroll
     for (int kk = 0; kk < FBK / 4; ++kk) {
-      float a[2], b[2];
+      float a[WM], b[WN];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        a[t] = sA[buf][wco + 16 * t + li][4 * kk + lk];
-        b[t] = sB[buf][wp + 16 * t + li][4 * kk + lk];
-      }
+      for (int t = 0; t < WM; ++t) a[t] = sA[buf][wco + 16 * t + li][4 * kk + lk];
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int u = 0; u < WN; ++u) b[u] = sB[buf][wp + 16 * u + li][4 * kk + lk];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[u], acc[t][u], 0, 0, 0);
+      for (int t = 0; t < WM; ++t)
+#pragma unroll
+        for (int u = 0; u < WN; ++u) acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[u], acc[t][u], 0, 0, 0);
     }
     if (ks + 1 < nks) store(buf ^ 1);
     __syncthreads();
   }
   // D: lane (col = pixel li, rows 4 lk .. 4 lk + 3) of tile (t, u)
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
+  for (int t = 0; t < WM; ++t) {
     const int c0 = co0 + wco + 16 * t + 4 * lk;
     if (c0 >= p.cout) continue;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < WN; ++u) {
       const int m = p0 + wp + 16 * u + li;
       if (m >= p.M) continue;
-      float v[4] = {acc[t][u][0], acc[t][u][1], acc[t][u][2], acc[t][u][3]};
-      f32_epilogue<EPI>(p, v, m, c0);
+      if constexpr (SPLIT) {
+        const int coutp = (p.cout + 3) & ~3;
+        *(f32x4*)(p.part + ((long)blockIdx.z * p.M + m) * coutp + c0) = acc[t][u];
+      } else {
+        float v[4] = {acc[t][u][0], acc[t][u][1], acc[t][u][2], acc[t][u][3]};
+        f32_epilogue<EPI>(p, v, m, c0);
+      }
     }
   }
+}
+
+// Split-K reduction: thread = (pixel, 4-channel chunk); partials summed in split
+// order (deterministic), then the conv's epilogue.
+template <int EPI>
+__global__ __launch_bounds__(256) void conv_f32_reduce(const ConvF32Params p) {
+  const int coutp = (p.cout + 3) & ~3, nc = coutp >> 2;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)p.M * nc) return;
+  const int m = (int)(idx / nc), c0 = (int)(idx - (long)m * nc) * 4;
+  f32x4 s = *(const f32x4*)(p.part + (long)m * coutp + c0);
+  for (int z = 1; z < p.ksplit; ++z) s += *(const f32x4*)(p.part + ((long)z * p.M + m) * coutp + c0);
+  float v[4] = {s[0], s[1], s[2], s[3]};
+  f32_epilogue<EPI>(p, v, m, c0);
+}
+
+template <int EPI, int WM, int WN, int FBK>
+int launch_tile(const ConvF32Params* p, hipStream_t stream) {
+  const unsigned gx = (p->M + 32 * WN - 1) / (32 * WN), gy = (p->cout + 32 * WM - 1) / (32 * WM);
+  if (p->ksplit > 1) {
+    hipLaunchKernelGGL((conv_f32_kernel<EPI, true, WM, WN, FBK>), dim3(gx, gy, p->ksplit), dim3(256), 0, stream, *p);
+    const long n = (long)p->M * ((p->cout + 3) / 4);
+    hipLaunchKernelGGL((conv_f32_reduce<EPI>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, *p);
+  } else {
+    hipLaunchKernelGGL((conv_f32_kernel<EPI, false, WM, WN, FBK>), dim3(gx, gy), dim3(256), 0, stream, *p);
+  }
+  return (int)hipGetLastError();
+}
+
+// 64 x 64 tiles (2 x 2 MFMA tiles per wave, 32-deep stages).  Measured at raft_large
+// 440x1024, 32 iterations, batch 1 (fp32 forward): 22.6 ms; 128 x 128 tiles (4 x 4 per
+// wave) with 16- / 32-deep stages 28.0 / 27.5 ms, 128 x 64 26.4 ms.
+template <int EPI>
+int launch_f32(const ConvF32Params* p, hipStream_t stream) {
+  return launch_tile<EPI, 2, 2, 32>(p, stream);
 }
 
 }  // namespace
@@ -200,12 +254,11 @@ extern "C" int jr_conv_f32(const ConvF32Params* p, int epi, hipStream_t stream) 
       (p->bmap && (p->bmap_cs % 4 || p->bmap_coff % 4)) || (p->h32 && p->hidden % 4) ||
       (gru && (p->hidden % 4 || !p->h32 || !p->zbuf || p->cout != (epi == 1 ? 2 : 1) * p->hidden)))
     return (int)hipErrorInvalidValue;
-  dim3 grid((p->M + FB_P - 1) / FB_P, (p->cout + FB_CO - 1) / FB_CO);
+  if (p->ksplit > 1 && (!p->part || p->ksplit > (p->K + 31) / 32)) return (int)hipErrorInvalidValue;
   switch (epi) {
-    case 0: hipLaunchKernelGGL(conv_f32_kernel<0>, grid, dim3(256), 0, stream, *p); break;
-    case 1: hipLaunchKernelGGL(conv_f32_kernel<1>, grid, dim3(256), 0, stream, *p); break;
-    case 2: hipLaunchKernelGGL(conv_f32_kernel<2>, grid, dim3(256), 0, stream, *p); break;
+    case 0: return launch_f32<0>(p, stream);
+    case 1: return launch_f32<1>(p, stream);
+    case 2: return launch_f32<2>(p, stream);
     default: return (int)hipErrorInvalidValue;
   }
-  return (int)hipGetLastError();
 }

@@ -300,6 +300,10 @@ struct ConvF32Params {
   const float* res; int res_cs, res_coff, res_post;
   float* h32; float* zbuf; int hidden;
   const float* bmap; int bmap_cs, bmap_coff;
+  // split-K (ksplit > 1): blockIdx.z takes 1/ksplit of the K stages and writes raw
+  // partial sums to part [ksplit][M][round_up(cout, 4)]; a second kernel adds them in
+  // order and applies the epilogue (the loop convs at batch 1 have 110-440 blocks)
+  int ksplit; float* part;
 };
 int jr_conv_f32(const ConvF32Params* p, int epi, hipStream_t stream);
 // jr_channel_stats / jr_norm_act / jr_prep_images / jr_copy_channels /

@@ -956,6 +956,26 @@ static Launch make_conv_f32(const TList& t, const IList& i, double alpha, std::v
   p.h32 = h32.defined() ? h32.data_ptr<float>() : nullptr;
   p.zbuf = zbuf.defined() ? zbuf.data_ptr<float>() : nullptr;
   p.bmap = bmap.defined() ? bmap.data_ptr<float>() : nullptr;
+  // split-K when the grid holds fewer than 4 blocks per CU (the batch-1 loop convs:
+  // 110-440 blocks on 256 CUs, one 4-wave block per CU leaves the f32 MFMA pipe ~half
+  // idle): aim at ~1536 blocks, >= 8 K stages per split.  JR_F32_KSPLIT=<n> forces n.
+  {
+    const long blocks = (long)((p.M + 63) / 64) * ((p.cout + 63) / 64);
+    const int nks = (p.K + 31) / 32;
+    int S = 1;
+    if (blocks < 1024) S = (int)std::min<long>({8L, (1536 + blocks - 1) / blocks, (long)std::max(1, nks / 8)});
+    if (const char* e = std::getenv("JR_F32_KSPLIT")) S = std::max(1, std::min(std::atoi(e), std::max(1, nks / 8)));
+    p.ksplit = S;
+    if (S > 1) {
+      at::Tensor part = at::empty({(int64_t)S * p.M * ((p.cout + 3) / 4 * 4)}, x.options());
+      p.part = part.data_ptr<float>();
+      if (keep) keep->push_back(part);
+      else {   // eager op: keep the workspace alive until the stream has used it
+        auto launch = [=](hipStream_t s, int) { return jr_conv_f32(&p, epi, s); };
+        return [launch, part](hipStream_t s, int it) { return launch(s, it); };
+      }
+    }
+  }
   if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, bmap}) if (v.defined()) keep->push_back(v);
   return [=](hipStream_t s, int) { return jr_conv_f32(&p, epi, s); };
 }

@@ -241,7 +241,11 @@ def test_precision_argument_is_validated():
     (2, 12, 16, 256, 256, 1, 5, 0, 256, 0),   # (1, 5) GRU-shaped, pad (0, 2) below
 ])
 @pytest.mark.parametrize("act", [0, 1, 4])
-def test_conv_f32_kernel(shape, act):
+@pytest.mark.parametrize("ksplit", [None, "1", "3"])
+def test_conv_f32_kernel(shape, act, ksplit, monkeypatch):
+    """vs the interpreter; ksplit: the automatic split-K choice, forced off, forced 3-way."""
+    if ksplit is not None:
+        monkeypatch.setenv("JR_F32_KSPLIT", ksplit)
     N, H, W, cin, cout, k, s, p, xcs, xoff = shape
     kh, kw = (k, k) if k != 1 or s != 5 else (1, 5)
     sh, sw = (s, s) if s != 5 else (1, 1)
@@ -268,8 +272,11 @@ def test_conv_f32_kernel(shape, act):
 
 
 @pytest.mark.gpu
-def test_conv_f32_gru_epilogues():
-    """GRU-A (z, r*h) and GRU-B (blend) epilogues with a bias map, vs the interpreter."""
+@pytest.mark.parametrize("ksplit", ["1", "4"])
+def test_conv_f32_gru_epilogues(ksplit, monkeypatch):
+    """GRU-A (z, r*h) and GRU-B (blend) epilogues with a bias map, vs the interpreter
+    (without / with split-K: the epilogue then runs in the reduction kernel)."""
+    monkeypatch.setenv("JR_F32_KSPLIT", ksplit)
     g = torch.Generator().manual_seed(2)
     N, H, W, hd, cs = 2, 8, 12, 64, 132
     M = N * H * W
