@@ -382,7 +382,7 @@ class FusedLoop:
         # backward
         self.gout = z(T, self.B, self.H, self.W, 2, dtype=F32)
         self.dmask = z(T, M, 576) if self.has_mask else None
-        self.utaps = z(M, 18, dtype=F32)
+        self.utaps = z(T * M, 18, dtype=F32)
         self.ddelta = z(T, M, 8)
         self.dfmm = z(T, M, self.fm_cs)
         self.dq = z(G, T, M, hd)
@@ -570,14 +570,14 @@ class FusedLoop:
         return self.packer.stale()
 
     # ----------------------------------------------------------- recording
-    def _conv(self, plan, name, x, y, *, x_coff=0, tx=None, ix=None, **kw):
-        record_conv(plan, self._specs[name], x, self.B, self.h, self.w, y, x_coff=x_coff, tx=tx, ix=ix, **kw)
+    def _conv(self, plan, name, x, y, *, x_coff=0, tx=None, ix=None, N=None, **kw):
+        record_conv(plan, self._specs[name], x, N or self.B, self.h, self.w, y, x_coff=x_coff, tx=tx, ix=ix, **kw)
 
-    def _bconv(self, plan, name, x, *, x_coff=0, split=0, s0=None, s1=None, **gru):
-        """Data-gradient conv with the EPI_BWD epilogue."""
+    def _bconv(self, plan, name, x, *, x_coff=0, split=0, s0=None, s1=None, N=None, **gru):
+        """Data-gradient conv with the EPI_BWD epilogue (N images, default the batch)."""
         tx, ix = _tx(s0=s0, s1=s1, **gru)
         y = (s1.out if s1 is not None and s1.out is not None else s0.out)
-        self._conv(plan, name, x, y, x_coff=x_coff, tx=tx, ix=ix, epi=EPI_BWD, hidden=split)
+        self._conv(plan, name, x, y, x_coff=x_coff, tx=tx, ix=ix, epi=EPI_BWD, hidden=split, N=N)
 
     def _build_fwd(self):
         P = nat.new_plan()
@@ -674,17 +674,23 @@ class FusedLoop:
         E_DM, E_ME = 0, 1
         for g_ in self.lv_grads:
             P.add_memset([g_])
+        # The output heads' backward of every iteration at once (T * B images): the x8
+        # upsampling, the mask conv and FlowHead conv2 data gradients depend only on that
+        # iteration's loss gradient and forward activations -- the coordinates are
+        # detached between iterations (model.py:498), so no gradient reaches delta_t
+        # through later iterations -- not on the recurrence, so they leave the serial
+        # per-iteration chain and run as T-stacked launches (M = T * B * h * w).
+        TB = T * B
+        if self.has_mask:
+            P.add_upsample_convex_bwd([self.mask, self.flow32, self.gout, self.dmask, self.utaps],
+                                      [TB, h, w], self.mp.multiplier)
+            P.add_flow_gather_bwd([self.utaps, self.ddelta], [TB, h, w])
+            self._bconv(P, "maskT", self.dmask, N=TB,
+                        s1=Seg(mask=self.fmm, mask_coff=self.fh_hidden, out=self.dfmm, out_coff=self.fh_hidden))
+        else:
+            P.add_upsample_bilinear_bwd([self.gout, self.ddelta], [TB, h, w])
+        self._bconv(P, "fh2T", self.ddelta, N=TB, s1=Seg(mask=self.fmm, out=self.dfmm))
         for t in reversed(range(T)):
-            fm = self.fmm[t]
-            if self.has_mask:
-                P.add_upsample_convex_bwd([self.mask[t], self.flow32[t], self.gout[t], self.dmask[t], self.utaps],
-                                          [B, h, w], self.mp.multiplier)
-                P.add_flow_gather_bwd([self.utaps, self.ddelta[t]], [B, h, w])
-                self._bconv(P, "maskT", self.dmask[t],
-                            s1=Seg(mask=fm, mask_coff=self.fh_hidden, out=self.dfmm[t], out_coff=self.fh_hidden))
-            else:
-                P.add_upsample_bilinear_bwd([self.gout[t], self.ddelta[t]], [B, h, w])
-            self._bconv(P, "fh2T", self.ddelta[t], s1=Seg(mask=fm, out=self.dfmm[t]))
             # flow head (+ mask) conv1 data gradient -> blend backward of the last GRU
             gl = G - 1
             self._bconv(P, "fh1T", self.dfmm[t], split=hd,
