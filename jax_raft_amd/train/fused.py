@@ -393,7 +393,7 @@ class FusedLoop:
         self.dm = z(T, M, self.mot_cs)
         self.dcf = z(T, M, self.cf_cs)
         self.dc1 = z(T, M, self.cl[0]) if len(self.cl) == 2 else None
-        self.dcorr = z(M, self.corr_cs)
+        self.dcorr = z(T, M, self.corr_cs)
         self.df1 = z(T, M, self.fl[0])
         self.dctx = z(M, self.ctx_cs, dtype=F32)
 
@@ -711,22 +711,26 @@ class FusedLoop:
                     self._bconv(P, "gAT0", self.dzr[0, t], split=hd, s0=Seg(gin=self.dh[0], out=self.dh_next),
                                 s1=Seg(gin=self.dmot, mask=self.hx[0, t], mask_coff=hd, valid=self.mot_out - 2,
                                        out=self.dm[t]))
-            # the motion encoder's backward (-> pyramid lookup scatter) only feeds the weight
-            # gradients: lane 1, overlapping the next (earlier) iteration's head / GRU backward
-            P.add_record(E_DM)
-            P.set_lane(self.lanes)
-            P.add_wait(E_DM)
-            self._bconv(P, "mcT", self.dm[t], s1=Seg(mask=self.cf[t], out=self.dcf[t]))
-            if len(cl) == 2:
-                self._bconv(P, "cc2T", self.dcf[t], s1=Seg(mask=self.c1[t], out=self.dc1[t]))
-                self._bconv(P, "cc1T", self.dc1[t], s1=Seg(out=self.dcorr, valid=self.corr_ch))
-            else:
-                self._bconv(P, "cc1T", self.dcf[t], s1=Seg(out=self.dcorr, valid=self.corr_ch))
-            P.add_lookup_bwd([self.coords[t], self.dcorr] + self.lv_grads + [None] * (4 - self.L),
+        # The motion encoder's backward (-> pyramid lookup scatter) only feeds the weight
+        # and pyramid gradients, never the recurrence: after the BPTT chain, as T-stacked
+        # launches (M = T * B * h * w), the lookup scatter per iteration (its level maps
+        # are per query pixel of one iteration).
+        TB = T * B
+        P.add_record(E_DM)
+        P.set_lane(self.lanes)
+        P.add_wait(E_DM)
+        self._bconv(P, "mcT", self.dm, N=TB, s1=Seg(mask=self.cf, out=self.dcf))
+        if len(cl) == 2:
+            self._bconv(P, "cc2T", self.dcf, N=TB, s1=Seg(mask=self.c1, out=self.dc1))
+            self._bconv(P, "cc1T", self.dc1, N=TB, s1=Seg(out=self.dcorr, valid=self.corr_ch))
+        else:
+            self._bconv(P, "cc1T", self.dcf, N=TB, s1=Seg(out=self.dcorr, valid=self.corr_ch))
+        self._bconv(P, "cf2T", self.dcf, N=TB, x_coff=cl[-1], s1=Seg(mask=self.f1, out=self.df1))
+        for t in reversed(range(T)):   # the BPTT chain's accumulation order
+            P.add_lookup_bwd([self.coords[t], self.dcorr[t]] + self.lv_grads + [None] * (4 - self.L),
                              [self.L, B, h, w, self.radius])
-            self._bconv(P, "cf2T", self.dcf[t], x_coff=cl[-1], s1=Seg(mask=self.f1[t], out=self.df1[t]))
-            P.add_record(E_ME)
-            P.set_lane(0)
+        P.add_record(E_ME)
+        P.set_lane(0)
         P.add_wait(E_ME)
         self._record_wgrads(P)
         return P
