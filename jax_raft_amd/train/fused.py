@@ -661,8 +661,15 @@ class FusedLoop:
                     P.add_record(E_FLOW)
                 mask_head(t)
                 P.set_lane(0)
+        if not fl:
+            # the output heads of every iteration (nothing in the recurrence reads them) as
+            # T-stacked launches after the loop (M = T * B * h * w)
+            TB = T * B
+            if self.has_mask:
+                self._conv(P, "mask", self.fmm, self.mask, x_coff=self.fh_hidden, alpha=self.mp.multiplier, N=TB)
+                P.add_upsample_convex([self.mask, self.flow32, self.out.view(TB, self.H, self.W, 2)], [TB, h, w, 0])
             else:
-                mask_head(t)
+                P.add_upsample_bilinear([self.flow32, self.out.view(TB, self.H, self.W, 2)], [TB, h, w, 0])
         return P
 
     def _build_bwd(self):
