@@ -1,0 +1,282 @@
+// Fused ConvGRU stage for the raft_large refinement loop (reference
+// jax_raft/model.py:301-312 ConvGRU, :315-329 RecurrentBlock: a 1x5 then a
+// 5x1 ConvGRU over [h | x], hidden 128, x = [motion | flow] 128 channels):
+//
+//   z, r = sigmoid(conv_zr([h | x]) + ctx_zr)      GEMM 1: 256 x 128 px, K = 5 x 256
+//   q    = tanh(conv_q([r h | x]) + ctx_q)         GEMM 2: 128 x 128 px, K = 5 x 256
+//   h'   = (1 - z) h + z q
+//
+// (ctx_* = the loop-invariant context-feature share + gate biases, a per-pixel
+// bias map computed once in the prologue, runtime/engine.py.)
+//
+// The unfused loop runs this as two implicit-GEMM launches (EPI_GRU_A /
+// EPI_GRU_B in conv_igemm.h) that hand z and r*h over through global memory.
+// Here one workgroup owns a tile whose pixels contain every tap neighbour of
+// every pixel: for the 1x5 stage a whole image row (W <= 128), for the 5x1
+// stage J whole image columns (J * H <= 128).  So r*h of the tile's pixels is
+// all GEMM 2 needs: it is written once into an LDS image (zero rows at both
+// ends of each run = the conv's zero padding) and GEMM 2 reads its B
+// fragments straight from that image, shifted by the tap.  z stays in the
+// registers of the waves that produced it: GEMM 1's 16 waves tile 4 x 64
+// channels x 4 x 32 pixels; waves 0-7 own the z channels and, in GEMM 2, the
+// same 64 x 32 (channel, pixel) tiles of q, so the blend is register-local.
+// Waves 8-15 (the r channels) write r*h, then only stage GEMM 2's operands.
+// No z / r*h global round trip, one launch instead of two, and nothing else
+// reads the tile's h while it is replaced (tap neighbours never leave the
+// tile), so h' is written in place.
+//
+// MFMA: v_mfma_f32_32x32x16_bf16, operands staged as in kernel M32
+// (conv_igemm.h: 64-deep K stages, register-staged global loads two stages
+// ahead, double-buffered LDS with the swzB swizzle, permuted weight rows from
+// ops/native.py:pack_weight so each lane owns 16 contiguous channels).
+#include "conv_igemm.h"
+
+namespace {
+
+constexpr int HD = 128;            // hidden channels
+constexpr int CIN = 256;           // [h | x] channels per tap
+constexpr int KPAD = 5 * CIN;      // packed K of both GEMMs
+constexpr int NSTG = KPAD / BK;    // 20 stages
+constexpr int TP = 128;            // pixel rows per tile
+constexpr int AROWS = 2 * HD;      // GEMM 1 rows
+constexpr int STAGE = (AROWS + TP) * BK;
+constexpr int RH_ROWS = 136;       // r*h image rows: J * (L + 4) <= 136
+constexpr unsigned OOB = 0x80000000u;
+
+// r*h image: rows of 128 channels (16 chunks of 16 B), chunk c of row R at c ^ (R & 15)
+JR_DEVICE int rh_off(int row, int chunk) { return row * HD + ((chunk ^ (row & 15)) << 3); }
+
+template <int NV>
+JR_DEVICE void load_map(const GruFusedParams& p, int m, int c, float* v) {
+  const long o = (long)m * p.bmap_cs + c;
+  if (p.bmap_bf16) load_bf16<NV>((const bf16*)p.bmap + o, v);
+  else load_f32<NV>((const float*)p.bmap + o, v);
+}
+
+__global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE + RH_ROWS * HD];
+  bf16* const rh = smem + 2 * STAGE;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wco = wave & 3, wp = wave >> 2;   // 64-channel group, 32-pixel group
+  const int rho = lane & 31, hh = lane >> 5;
+  const int tile = blockIdx.x;
+  const int n = tile / p.tiles_per_img, tt = tile - n * p.tiles_per_img;
+  const int npx = p.J * p.L;
+  auto pix = [&](int pl) -> int {   // tile pixel -> global pixel index (or -1)
+    if (pl >= npx) return -1;
+    const int j = pl / p.L, r = pl - j * p.L;
+    const int y = p.vertical ? r : tt;
+    const int x = p.vertical ? tt * p.J + j : r;
+    return (n * p.H + y) * p.W + x;
+  };
+
+  const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc((void*)p.hx, (short)0, (int)p.hx_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t was = __builtin_amdgcn_make_buffer_rsrc((void*)p.wa, (short)0, (int)p.wa_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wbs = __builtin_amdgcn_make_buffer_rsrc((void*)p.wb, (short)0, (int)p.wb_bytes, 0x00020000);
+
+  // zero rows of the r*h image (the conv's zero padding at both ends of each run)
+  if (tid < 4 * p.J * 16) {
+    const int q = tid >> 4, c = tid & 15, j = q >> 2, e = q & 3;
+    const int row = j * (p.L + 4) + (e < 2 ? e : p.L + e);
+    *(u32x4*)(rh + rh_off(row, c)) = u32x4{0u, 0u, 0u, 0u};
+  }
+
+  // loader: thread -> (pixel row lrow, 16-B chunk ch) of the B image, weight rows ar, ar + 128
+  const int lrow = tid >> 3, ch = tid & 7;
+  unsigned lbase = 0, lmask = 0;
+  {
+    const int lm = pix(lrow);
+    if (lm >= 0) {
+      lbase = (unsigned)lm * (unsigned)p.hx_cs * 2u + (unsigned)ch * 16u;
+      const int r = lrow % p.L;
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        if ((unsigned)(r + k - 2) < (unsigned)p.L) lmask |= 1u << k;
+    }
+  }
+  const int tapd = (p.vertical ? p.W : 1) * p.hx_cs * 2;   // bytes between tap neighbours
+  const unsigned aoff = (unsigned)(lrow * KPAD * 2 + ch * 16);
+
+  struct Regs { u32x4 a0, a1, b; };
+  auto xload = [&](int s) {   // B chunk of stage s from hx (channel block cb of tap s / 4)
+    const int tap = s >> 2, cb = s & 3;
+    const bool ok = s < NSTG && ((lmask >> tap) & 1u);
+    const unsigned off = lbase + (unsigned)((tap - 2) * tapd) + (unsigned)cb * 128u;
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xs, ok ? off : OOB, 0, 0));
+  };
+  auto kofs = [&](int s) { return (unsigned)((s >> 2) * CIN + (s & 3) * 64) * 2u; };
+  auto sA_of = [&](int buf) { return smem + buf * STAGE; };
+  auto sB_of = [&](int buf) { return smem + buf * STAGE + AROWS * BK; };
+  auto put = [&](bf16* base, int row, const u32x4& v) { *(u32x4*)(base + row * BK + ((ch ^ swzB(row)) << 3)) = v; };
+
+  // ---------------------------------------------------------------- GEMM 1
+  auto issue1 = [&](Regs& r, int s) {
+    const bool kin = s < NSTG;
+    r.a0 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(was, kin ? aoff + kofs(s) : OOB, 0, 0));
+    r.a1 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+        was, kin ? aoff + (unsigned)(128 * KPAD * 2) + kofs(s) : OOB, 0, 0));
+    r.b = xload(s);
+  };
+  auto store1 = [&](const Regs& r, int buf) {
+    put(sA_of(buf), lrow, r.a0);
+    put(sA_of(buf), lrow + 128, r.a1);
+    put(sB_of(buf), lrow, r.b);
+  };
+  f32x16 acc[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc[t][k] = 0.f;
+  const int prow = wp * 32 + rho;   // this lane's pixel row in the tile
+  auto mma_stage = [&](const bf16* sA, int arow0, auto&& bfrag) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int chunk = kk * 2 + hh;
+      const bf16x8 b = bfrag(chunk);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int row = arow0 + m32_arow(t, rho);
+        const bf16x8 a = *(const bf16x8*)(sA + row * BK + ((chunk ^ swzB(row)) << 3));
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[t], 0, 0, 0);
+      }
+    }
+  };
+  auto compute1 = [&](int buf) {
+    const bf16* sB = sB_of(buf);
+    mma_stage(sA_of(buf), wco * 64, [&](int chunk) {
+      return *(const bf16x8*)(sB + prow * BK + ((chunk ^ swzB(prow)) << 3));
+    });
+  };
+  {
+    Regs ra, rb;
+    issue1(ra, 0);
+    issue1(rb, 1);
+    store1(ra, 0);
+    __syncthreads();
+    for (int s = 0; s < NSTG; s += 2) {
+      issue1(ra, s + 2);
+      compute1(0);
+      store1(rb, 1);
+      __syncthreads();
+      issue1(rb, s + 3);
+      compute1(1);
+      store1(ra, 0);
+      __syncthreads();
+    }
+  }
+
+  // ------------------------------------------------------------ epilogue 1
+  // lane: channels c0 + [0, 16) (c0 = 64 wco + 32 t + 16 hh) of tile pixel prow
+  const int m = pix(prow);
+  const int jrun = prow / p.L;
+  const int rh_row = prow < npx ? jrun * (p.L + 4) + (prow - jrun * p.L) : 0;   // + tap = shifted row
+  bf16x8 z[2][2];   // z as bf16 (the unfused path's default gate storage, EPI_GRU_A z_bf16)
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int c0 = wco * 64 + 32 * t + 16 * hh;
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = acc[t][k];
+    if (m >= 0) {
+      float b[16];
+      load_map<16>(p, m, c0, b);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = sigmoidf_(v[k] + b[k]);
+    }
+    if (wco < 2) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        z[t][0][k] = f2bf(v[k]);
+        z[t][1][k] = f2bf(v[8 + k]);
+      }
+    } else if (m >= 0) {   // r * h (h from the bf16 loop buffer, as the unfused EPI_GRU_A) -> r*h image
+      float hv[16];
+      load_bf16<16>((const bf16*)p.hx + (long)m * p.hx_cs + (c0 - HD), hv);
+      bf16x8 o0, o1;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        o0[k] = f2bf(v[k] * hv[k]);
+        o1[k] = f2bf(v[8 + k] * hv[8 + k]);
+      }
+      const int chunk = (c0 - HD) >> 3;
+      *(bf16x8*)(rh + rh_off(rh_row + 2, chunk)) = o0;
+      *(bf16x8*)(rh + rh_off(rh_row + 2, chunk + 1)) = o1;
+    }
+  }
+  __syncthreads();   // r*h image complete; GEMM 1 staging free
+
+  // ---------------------------------------------------------------- GEMM 2
+  // stages s = (tap, cb): cb 0, 1 = the r*h channels (B from the image), cb 2, 3 = x (staged)
+  auto issue2 = [&](Regs& r, int s) {
+    const bool kin = s < NSTG;
+    r.a0 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wbs, kin ? aoff + kofs(s) : OOB, 0, 0));
+    if ((s & 3) >= 2) r.b = xload(s);
+  };
+  auto store2 = [&](const Regs& r, int buf, int s) {
+    put(sA_of(buf), lrow, r.a0);
+    if ((s & 3) >= 2) put(sB_of(buf), lrow, r.b);
+  };
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc[t][k] = 0.f;
+  auto compute2 = [&](int buf, int s) {
+    if (wco >= 2) return;   // waves 8-15 only stage operands
+    const int tap = s >> 2, cb = s & 3;
+    if (cb < 2) {
+      const int row = rh_row + tap;
+      mma_stage(sA_of(buf), wco * 64, [&](int chunk) { return *(const bf16x8*)(rh + rh_off(row, cb * 8 + chunk)); });
+    } else {
+      const bf16* sB = sB_of(buf);
+      mma_stage(sA_of(buf), wco * 64, [&](int chunk) {
+        return *(const bf16x8*)(sB + prow * BK + ((chunk ^ swzB(prow)) << 3));
+      });
+    }
+  };
+  {
+    Regs ra, rb;
+    issue2(ra, 0);
+    issue2(rb, 1);
+    store2(ra, 0, 0);
+    __syncthreads();
+    for (int s = 0; s < NSTG; s += 2) {
+      issue2(ra, s + 2);
+      compute2(0, s);
+      store2(rb, 1, s + 1);
+      __syncthreads();
+      issue2(rb, s + 3);
+      compute2(1, s + 1);
+      store2(ra, 0, s + 2);
+      __syncthreads();
+    }
+  }
+
+  // ------------------------------------------------------------ epilogue 2
+  if (wco >= 2 || m < 0) return;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int c0 = wco * 64 + 32 * t + 16 * hh;
+    float b[16], h[16], v[16];
+    load_map<16>(p, m, 2 * HD + c0, b);
+    float* hp = p.h32 + (long)m * HD + c0;
+    load_f32<16>(hp, h);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float q = tanhf_(acc[t][k] + b[k]);
+      const float zk = bf2f(z[t][k >> 3][k & 7]);
+      v[k] = (1.0f - zk) * h[k] + zk * q;
+    }
+    store_f32<16>(hp, v);
+    store_bf16<16>((bf16*)p.y + (long)m * p.y_cs + c0, v);
+    if (p.y2) store_bf16<16>((bf16*)p.y2 + (long)m * p.y2_cs + c0, v);
+  }
+}
+
+}  // namespace
+
+extern "C" int jr_gru_fused(const GruFusedParams* p, hipStream_t stream) {
+  if (p->ntiles <= 0) return 0;
+  hipLaunchKernelGGL(gru_fused_kernel, dim3(p->ntiles), dim3(1024), 0, stream, *p);
+  return (int)hipGetLastError();
+}

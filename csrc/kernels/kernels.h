@@ -327,4 +327,21 @@ int jr_corr_lookup_f32(const float* const* levels, int num_levels, int B, int h,
 int jr_flow_update_f32(const float* delta, int dcs, int N, int h, int w, float* coords, float* flow32, float* hx,
                        int hx_cs, int hx_off, float* qx, int qx_cs, int qx_off, float* flow4, hipStream_t stream);
 
+// Fused ConvGRU stage of raft_large (gru_fused.hip): z, r = sigmoid(conv_zr([h | x]) + bmap[z | r]),
+// q = tanh(conv_q([r h | x]) + bmap[q]), h' = (1 - z) h + z q, for one 1x5 (row tiles) or
+// 5x1 (column tiles) stage in ONE launch; r*h and z never leave the CU.
+struct GruFusedParams {
+  const void* hx; int hx_cs;          // bf16 [M][hx_cs]: [h (128) | x (128)]; hx_cs == 256
+  const void* wa; const void* wb;     // pack_weight of [z | r] ([256][1280]) and q ([128][1280])
+  const void* bmap; int bmap_cs; int bmap_bf16;   // [M][bmap_cs]: [z | r | q] context share + gate biases
+  float* h32;                         // fp32 hidden state [M][128], updated in place
+  void* y; int y_cs;                  // bf16 h' -> channels [0, 128) (the loop buffer hx)
+  void* y2; int y2_cs;                // optional second bf16 copy of h' (channels [0, 128))
+  int N, H, W;
+  int vertical;                       // 0: 1x5 taps along W, tiles = image rows; 1: 5x1, tiles = J columns
+  int L, J, tiles_per_img, ntiles;    // run length (W or H), runs per tile (J * L <= 128)
+  long hx_bytes, wa_bytes, wb_bytes;
+};
+int jr_gru_fused(const GruFusedParams* p, hipStream_t stream);
+
 }  // extern "C"

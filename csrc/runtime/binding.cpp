@@ -482,6 +482,55 @@ static Launch make_conv1x1(const TList& t, const IList& i, std::vector<at::Tenso
   };
 }
 
+bool gru_fused_fits(int64_t H, int64_t W, int64_t vertical) {
+  if (!vertical) return W >= 1 && W <= 128;
+  const int J = 2 * H <= 128 && W % 2 == 0 ? 2 : 1;
+  return H >= 1 && J * H <= 128 && J * (H + 4) <= 136 && W % J == 0;
+}
+
+// Fused ConvGRU stage (gru_fused.hip).  t = [hx (bf16 [M][256]: h | x), wa (pack_weight of [z | r],
+// [256][1280]), wb (pack_weight of q, [128][1280]), bmap ([M][>=384] fp32 / bf16: z | r | q context
+// share), h32 (fp32 [M][128], in place), y (bf16 [M][ycs], channels [0, 128)), y2 (optional copy)],
+// i = [N, H, W, vertical].  Tiles: a row (1x5, W <= 128) or J = 2 / 1 columns (5x1, J * H <= 128).
+static Launch make_gru_fused(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor hx = opt(t, 0), wa = opt(t, 1), wb = opt(t, 2), bmap = opt(t, 3), h32 = opt(t, 4), y = opt(t, 5),
+             y2 = opt(t, 6);
+  check_bf16(hx, "hx"); check_bf16(wa, "wa"); check_bf16(wb, "wb"); check_f32(h32, "h32"); check_bf16(y, "y");
+  TORCH_CHECK(i.size() == 4, "gru_fused: expected 4 ints");
+  GruFusedParams p{};
+  p.N = (int)i[0]; p.H = (int)i[1]; p.W = (int)i[2]; p.vertical = (int)i[3];
+  const int64_t M = (int64_t)p.N * p.H * p.W;
+  TORCH_CHECK(gru_fused_fits(p.H, p.W, p.vertical), "gru_fused: the tile geometry does not fit (", p.H, "x", p.W, ")");
+  TORCH_CHECK(cs(hx) == 256 && hx.numel() >= M * 256 && reinterpret_cast<uintptr_t>(hx.data_ptr()) % 16 == 0,
+              "gru_fused: hx must be [M][256] ([h 128 | x 128])");
+  TORCH_CHECK(wa.numel() == 256 * 1280 && wb.numel() == 128 * 1280 &&
+                  reinterpret_cast<uintptr_t>(wa.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(wb.data_ptr()) % 16 == 0,
+              "gru_fused: packed weights [256][1280] / [128][1280]");
+  TORCH_CHECK(bmap.defined() && bmap.is_cuda() && bmap.is_contiguous() &&
+                  (bmap.scalar_type() == at::kFloat || bmap.scalar_type() == at::kBFloat16) && cs(bmap) >= 384 &&
+                  cs(bmap) % 8 == 0 && bmap.numel() >= M * cs(bmap) && reinterpret_cast<uintptr_t>(bmap.data_ptr()) % 16 == 0,
+              "gru_fused: bias map [M][>=384] fp32 / bf16");
+  TORCH_CHECK(h32.numel() >= M * 128 && cs(h32) == 128 && reinterpret_cast<uintptr_t>(h32.data_ptr()) % 16 == 0,
+              "gru_fused: h32 [M][128]");
+  TORCH_CHECK(cs(y) % 8 == 0 && cs(y) >= 128 && y.numel() >= M * cs(y) && reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
+              "gru_fused: y [M][>=128]");
+  if (y2.defined()) {
+    check_bf16(y2, "y2");
+    TORCH_CHECK(cs(y2) % 8 == 0 && cs(y2) >= 128 && y2.numel() >= M * cs(y2) &&
+                    reinterpret_cast<uintptr_t>(y2.data_ptr()) % 16 == 0, "gru_fused: y2 [M][>=128]");
+  }
+  p.hx = hx.data_ptr(); p.hx_cs = 256; p.wa = wa.data_ptr(); p.wb = wb.data_ptr();
+  p.bmap = bmap.data_ptr(); p.bmap_cs = cs(bmap); p.bmap_bf16 = bmap.scalar_type() == at::kBFloat16;
+  p.h32 = h32.data_ptr<float>(); p.y = y.data_ptr(); p.y_cs = cs(y); p.y2 = ptr(y2); p.y2_cs = y2.defined() ? cs(y2) : 0;
+  if (!p.vertical) { p.L = p.W; p.J = 1; p.tiles_per_img = p.H; }
+  else { p.L = p.H; p.J = 2 * p.H <= 128 && p.W % 2 == 0 ? 2 : 1; p.tiles_per_img = p.W / p.J; }
+  p.ntiles = p.N * p.tiles_per_img;
+  p.hx_bytes = (long)hx.numel() * 2; p.wa_bytes = (long)wa.numel() * 2; p.wb_bytes = (long)wb.numel() * 2;
+  TORCH_CHECK(p.hx_bytes < (1LL << 31), "gru_fused: hx larger than 2 GiB");
+  if (keep) for (auto& v : {hx, wa, wb, bmap, h32, y, y2}) if (v.defined()) keep->push_back(v);
+  return [p](hipStream_t s, int) { return jr_gru_fused(&p, s); };
+}
+
 // t = [fm (bf16 [M][cs]), wpk (bf16, pack_taps), taps (fp32 [M][>=24])], i = [M, K, fcoff]
 static Launch make_taps_gemm(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
   at::Tensor fm = opt(t, 0), wpk = opt(t, 1), taps = opt(t, 2);
@@ -1197,6 +1246,7 @@ void lookup_bwd_op(const TList& t, IList i) { run_now(make_lookup_bwd(t, i, null
 void im2col_op(const TList& t, IList i) { run_now(make_im2col(t, i, nullptr)); }
 void flow_taps_op(const TList& t, IList i) { run_now(make_flow_taps(t, i, nullptr)); }
 void taps_gemm_op(const TList& t, IList i) { run_now(make_taps_gemm(t, i, nullptr)); }
+void gru_fused_op(const TList& t, IList i) { run_now(make_gru_fused(t, i, nullptr)); }
 void conv1x1_op(const TList& t, IList i) { run_now(make_conv1x1(t, i, nullptr)); }
 void conv_direct_op(const TList& t, IList i) { run_now(make_conv_direct(t, i, nullptr)); }
 void conv_train_op(const TList& t, IList i, double alpha, const TList& tx, IList ix) {
@@ -1315,6 +1365,7 @@ class Plan : public torch::CustomClassHolder {
   void add_copy_channels(TList t, IList i) { push(make_copy_channels(t, i, &keep_), "copy_channels"); }
   void add_flow_taps(TList t, IList i) { push(make_flow_taps(t, i, &keep_), "flow_taps"); }
   void add_taps_gemm(TList t, IList i) { push(make_taps_gemm(t, i, &keep_), "taps_gemm"); }
+  void add_gru_fused(TList t, IList i) { push(make_gru_fused(t, i, &keep_), "gru_fused"); }
   void add_conv1x1(TList t, IList i) { push(make_conv1x1(t, i, &keep_), "conv1x1"); }
   void add_conv_direct(TList t, IList i) { push(make_conv_direct(t, i, &keep_), "conv_direct"); }
   void add_conv_train(TList t, IList i, double alpha, TList tx, IList ix) {
@@ -1759,6 +1810,8 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("im2col(Tensor?[] t, int[] i) -> ()", &jr::im2col_op);
   m.def("flow_taps(Tensor?[] t, int[] i) -> ()", &jr::flow_taps_op);
   m.def("taps_gemm(Tensor?[] t, int[] i) -> ()", &jr::taps_gemm_op);
+  m.def("gru_fused(Tensor?[] t, int[] i) -> ()", &jr::gru_fused_op);
+  m.def("gru_fused_fits(int H, int W, int vertical) -> bool", &jr::gru_fused_fits);
   m.def("conv1x1(Tensor?[] t, int[] i) -> ()", &jr::conv1x1_op);
   m.def("conv_direct(Tensor?[] t, int[] i) -> ()", &jr::conv_direct_op);
   m.def("conv_train(Tensor?[] t, int[] i, float alpha, Tensor?[] tx, int[] ix) -> ()", &jr::conv_train_op);
@@ -1811,6 +1864,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_copy_channels", &jr::Plan::add_copy_channels)
       .def("add_flow_taps", &jr::Plan::add_flow_taps)
       .def("add_taps_gemm", &jr::Plan::add_taps_gemm)
+      .def("add_gru_fused", &jr::Plan::add_gru_fused)
       .def("add_conv1x1", &jr::Plan::add_conv1x1)
       .def("add_conv_direct", &jr::Plan::add_conv_direct)
       .def("add_conv_train", &jr::Plan::add_conv_train)

@@ -59,6 +59,16 @@ CFG_TILES.update({35: (256, 128), 36: (128, 128), 37: (128, 128), 38: (256, 128)
 TUNE_CFGS = (0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34,
              35, 38)
 NUM_CUS = 256
+def gru_fused_tiles(N: int, H: int, W: int, vertical: int) -> int:
+    """Workgroups of the fused ConvGRU stage (csrc/kernels/gru_fused.hip; mirrors
+    binding.cpp:gru_fused_fits): image rows (1x5, W <= 128) or pairs / singles of
+    image columns (5x1, J * H <= 128); 0 when the geometry does not fit a tile."""
+    if not vertical:
+        return N * H if 1 <= W <= 128 else 0
+    J = 2 if 2 * H <= 128 and W % 2 == 0 else 1
+    return N * (W // J) if 1 <= H and J * H <= 128 and J * (H + 4) <= 136 and W % J == 0 else 0
+
+
 def load(build_if_missing: bool = True) -> None:
     """Load ``_C.so`` (building it with hipcc first if it is missing)."""
     global _loaded, _load_error

@@ -601,6 +601,26 @@ class RaftEngine:
         return (all_iters and self.has_mask and self._taps_epi_w is not None and self._convex_w is not None
                 and self._specs["fh1.flow"].cout == 256)
 
+    def _gru_fused_ok(self, B: int, h: int, w: int) -> bool:
+        """The fused ConvGRU kernel (gru_fused.hip) serves raft_large's update block:
+        hidden 128, [h | motion | flow] = 256 loop channels, a 1x5 then a 5x1 stage,
+        and tiles (image rows / column pairs) that fit 128 pixels.  It launches one
+        workgroup per tile, so it is used when both stages have >= 3/4 as many tiles
+        as the GPU has CUs: measured on MI355X at 440x1024, batch 4 (220 / 256 tiles)
+        333-335 vs 320 pairs/s; batch 1 (55 / 64 tiles) 139 vs 158 FPS for the
+        two-launch implicit-GEMM path (profiles/r3_gru_fused_ab.txt).
+        ``JR_GRU_FUSED=0`` / ``=1`` force the two-launch path / the fused one."""
+        env = os.environ.get("JR_GRU_FUSED", "auto")
+        if env == "0":
+            return False
+        rb = self.model.update_block.recurrent_block
+        ks = [tuple(k) for k in rb.kernel_size]
+        if (self.hidden != 128 or self.hx_cs != 256 or self.gate_cs < 384 or ks != [(1, 5), (5, 1)]
+                or self.gate_dtype != torch.bfloat16):
+            return False
+        tiles = min(nat.gru_fused_tiles(B, h, w, 0), nat.gru_fused_tiles(B, h, w, 1))
+        return tiles > 0 and (env == "1" or tiles >= 3 * nat.NUM_CUS // 4)
+
     def uses_lanes(self, B: int, all_iters: bool = True) -> bool:
         """Whether the plan for batch ``B`` runs the model's branches on several
         lanes (``streams`` / its "auto" rule).  Graph-pipelined steps
@@ -796,6 +816,11 @@ class RaftEngine:
         mfeat = (alloc("mfeat", (M, round_up(sp["mask.convrelu"].cout, 8)))
                  if self.has_mask and (split_mask or not all_iters) else None)
         mask = alloc("mask", (M, 576)) if self.has_mask and self._convex_w is None else None
+        # fused ConvGRU stages (gru_fused.hip): one launch per stage, r*h / z stay in the CU
+        gru_f = self._gru_fused_ok(B, h, w) and not self.cp
+        # with the mask lane, the mask head reads h from its own copy `hm` (written by the last
+        # stage), so the first stage can replace h in hx while the mask lane still runs
+        hm = alloc("hm", (M, self.hidden)) if gru_f and lanes_on and self.has_mask else None
 
         def flow_features():
             if self._cf1_w is not None:
@@ -833,7 +858,7 @@ class RaftEngine:
             if mask_from_fm:
                 feat_, coff = fm, self.fh_hidden
             else:
-                self._conv(plan, sp["mask.convrelu"], hx, B, h, w, mfeat, act=ACT_RELU)
+                self._conv(plan, sp["mask.convrelu"], hm if hm is not None else hx, B, h, w, mfeat, act=ACT_RELU)
                 feat_, coff = mfeat, 0
             if self._convex_w is not None:
                 plan.add_convex_head([feat_, self._convex_w, self._convex_b, flow32, out, st.out_slot],
@@ -863,7 +888,16 @@ class RaftEngine:
                 plan.add_wait(E_FLOW)
             self._conv(plan, sp["me.conv"], cf, B, h, w, hx, y_coff=self.mot_off, act=ACT_RELU, y2=qx,
                        y2_coff=self.mot_off)
-            for gi in range(len(m.update_block.recurrent_block.kernel_size)):
+            ngru = len(m.update_block.recurrent_block.kernel_size)
+            for gi in range(ngru):
+                if gru_f:
+                    last = gi == ngru - 1
+                    if wait_mask and (last if hm is not None else gi == 0):
+                        plan.add_wait(E_MASK)  # the previous iteration's mask head has read hm / h (and flow32)
+                    ks = m.update_block.recurrent_block.kernel_size[gi]
+                    plan.add_gru_fused([hx, sp[f"gru{gi}.a"].w, sp[f"gru{gi}.b"].w, gbias[gi], h32, hx,
+                                        hm if last else None], [B, h, w, int(ks[0] > 1)])
+                    continue
                 # r*h from the bf16 h of the conv's own input hx (no fp32 state read)
                 self._conv(plan, sp[f"gru{gi}.a"], hx, B, h, w, qx, zbuf=zb, hidden=self.hidden,
                            epi=EPI_GRU_A, bmap=gbias[gi], bmap_coff=0)

@@ -71,6 +71,38 @@ def test_lane_schedule_raft_large(fake):
     assert ops.count("wait") == 3
 
 
+def test_lane_schedule_fused_gru(fake, monkeypatch):
+    """raft_large with the fused ConvGRU stages (gru_fused.hip, forced on at this small
+    size): one gru_fused op per stage on the critical lane, the mask lane's mask conv
+    reads its own h copy `hm` (written by the last stage), and the E_MASK wait moves
+    from the first stage to the last one (still three waits per iteration)."""
+    monkeypatch.setenv("JR_GRU_FUSED", "1")
+    eng, p = _plan(raft_large, 4)
+    loop = [(ln, d, op, a) for s, ln, d, op, a in p.ops if s == 1]
+    main = [op for ln, d, op, _ in loop if ln == 0]
+    assert [op for op in main if op not in ("record", "wait")] == \
+        ["lookup", "conv1x1", "conv", "conv", "gru_fused", "gru_fused", "conv"]
+    i1, i2 = [i for i, op in enumerate(main) if op == "gru_fused"]
+    assert main[i2 - 1] == "wait" and main[i1 - 1] != "wait"
+    assert [op for _, _, op, _ in loop].count("wait") == 3
+    g1, g2 = [a for _, _, op, a in loop if op == "gru_fused"]
+    assert g1[0][6] is None and g2[0][6] is not None           # only the last stage writes hm
+    assert g1[1][3] == 0 and g2[1][3] == 1                      # 1x5 (rows), then 5x1 (columns)
+    hm = g2[0][6]
+    mask_convs = [a for ln, d, op, a in loop if ln == 2 and op == "conv"]
+    assert any(t[0] is hm for t, *_ in mask_convs)             # the mask conv reads hm
+    assert not eng._gru_fused_ok(1, 55, 128) or eng._gru_fused_ok(4, 55, 128)
+    monkeypatch.setenv("JR_GRU_FUSED", "auto")
+    assert eng._gru_fused_ok(4, 55, 128) and not eng._gru_fused_ok(1, 55, 128)
+    assert not eng._gru_fused_ok(4, 55, 129)                    # a row wider than a tile
+
+
+def test_fused_gru_not_for_raft_small(fake, monkeypatch):
+    monkeypatch.setenv("JR_GRU_FUSED", "1")
+    _, p = _plan(raft_small, 4)
+    assert "gru_fused" not in p.names(1)
+
+
 @pytest.mark.parametrize("factory", [raft_large, raft_small])
 def test_one_lane_schedule(factory, fake):
     eng, p = _plan(factory, 1)

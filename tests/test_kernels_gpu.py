@@ -143,6 +143,53 @@ def test_gru_fused_epilogues(hidden, xin, ks, pad, cfg):
     assert (hx[:, :hidden].float().cpu() - ref.reshape(M, hidden)).abs().max().item() < 2.5e-2
 
 
+@pytest.mark.parametrize("map_dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("B,h,w,vertical", [(2, 7, 13, 0), (2, 7, 13, 1), (2, 9, 12, 1), (1, 55, 128, 0),
+                                            (1, 55, 128, 1), (3, 5, 3, 1), (1, 64, 20, 1), (1, 4, 128, 0)])
+def test_gru_stage_fused_kernel(B, h, w, vertical, map_dtype):
+    """gru_fused.hip (one launch per ConvGRU stage, r*h and z kept in the CU) vs the fp32
+    ConvGRU of the reference with the context share as a per-pixel bias map (model.py:301-312):
+    row tiles (1x5) and 1- / 2-column tiles (5x1), incl. the headline's 55 x 128 grid."""
+    nat = _nat()
+    torch.manual_seed(5)
+    hd, M = 128, B * h * w
+    ks = (5, 1) if vertical else (1, 5)
+    pad = (2, 0) if vertical else (0, 2)
+    hs = torch.tanh(torch.randn(B, h, w, hd))
+    xs = torch.randn(B, h, w, hd)
+    kz, kr, kq = [torch.randn(*ks, 2 * hd, hd) / math.sqrt(5 * 2 * hd) for _ in range(3)]
+    bm = torch.randn(B, h, w, 384) * 0.5
+    if map_dtype == torch.bfloat16:
+        bm = _bf(bm)
+    zero = torch.zeros(hd)
+    hxr = torch.cat([hs, xs], -1)
+    z = torch.sigmoid(R.conv2d_nhwc(_bf(hxr), _bf(kz), zero, (1, 1), pad) + bm[..., :hd])
+    r = torch.sigmoid(R.conv2d_nhwc(_bf(hxr), _bf(kr), zero, (1, 1), pad) + bm[..., hd:2 * hd])
+    q = torch.tanh(R.conv2d_nhwc(_bf(torch.cat([_bf(r * _bf(hs)), xs], -1)), _bf(kq), zero, (1, 1), pad)
+                   + bm[..., 2 * hd:])
+    ref = ((1 - z) * hs + z * q).reshape(M, hd)
+    hx = torch.cat([hs, xs], -1).reshape(M, 2 * hd).to(DEV, torch.bfloat16).contiguous()
+    h32 = hs.reshape(M, hd).to(DEV).contiguous()
+    sa = nat.make_spec(torch.cat([kz, kr], 3), torch.zeros(2 * hd), (1, 1), pad, cin8=256, device=DEV)
+    sb = nat.make_spec(kq, zero, (1, 1), pad, cin8=256, device=DEV)
+    assert nat.ops().gru_fused_fits(h, w, vertical)
+    hm = torch.full((M, hd), 7.0, dtype=torch.bfloat16, device=DEV)
+    bmg = bm.reshape(M, 384).to(DEV, map_dtype).contiguous()
+    nat.ops().gru_fused([hx, sa.w, sb.w, bmg, h32, hx, hm], [B, h, w, vertical])
+    torch.cuda.synchronize()
+    assert (h32.cpu() - ref).abs().max().item() < 2e-2
+    assert (hx[:, :hd].float().cpu() - ref).abs().max().item() < 2.5e-2
+    assert torch.equal(hm, hx[:, :hd])
+    assert torch.equal(hx[:, hd:].float().cpu(), _bf(xs.reshape(M, hd)))   # x untouched
+
+
+def test_gru_fused_fits():
+    nat = _nat()
+    assert nat.ops().gru_fused_fits(55, 128, 0) and nat.ops().gru_fused_fits(55, 128, 1)
+    assert not nat.ops().gru_fused_fits(55, 129, 0)      # a row wider than a tile
+    assert not nat.ops().gru_fused_fits(130, 64, 1)      # a column taller than a tile
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("h,w,C,L", [(16, 16, 64, 4), (23, 37, 128, 4), (55, 128, 256, 4), (17, 20, 64, 2),
                                      (13, 48, 64, 3)])
