@@ -29,6 +29,8 @@
 // (conv_igemm.h: 64-deep K stages, register-staged global loads two stages
 // ahead, double-buffered LDS with the swzB swizzle, permuted weight rows from
 // ops/native.py:pack_weight so each lane owns 16 contiguous channels).
+#include <cstdlib>
+
 #include "conv_igemm.h"
 
 namespace {
@@ -42,6 +44,8 @@ constexpr int AROWS = 2 * HD;      // GEMM 1 rows
 constexpr int STAGE = (AROWS + TP) * BK;
 constexpr int RH_ROWS = 136;       // r*h image rows: J * (L + 4) <= 136
 constexpr unsigned OOB = 0x80000000u;
+constexpr int G2ST = 2 * HD * BK;  // G2ALL: GEMM 2 staging buffer (128 weight + 128 pixel rows)
+static_assert(3 * G2ST <= 2 * STAGE, "G2ALL: two GEMM 2 buffers + the z image fit GEMM 1's staging");
 
 // r*h image: rows of 128 channels (16 chunks of 16 B), chunk c of row R at c ^ (R & 15)
 JR_DEVICE int rh_off(int row, int chunk) { return row * HD + ((chunk ^ (row & 15)) << 3); }
@@ -53,6 +57,7 @@ JR_DEVICE void load_map(const GruFusedParams& p, int m, int c, float* v) {
   else load_f32<NV>((const float*)p.bmap + o, v);
 }
 
+template <bool G2ALL>
 __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE + RH_ROWS * HD];
   bf16* const rh = smem + 2 * STAGE;
@@ -166,12 +171,24 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
     }
   }
 
+  // GEMM 2's first two stages (weights only: the r*h blocks of tap 0) load during epilogue 1
+  auto issue2 = [&](Regs& r, int s) {
+    const bool kin = s < NSTG;
+    r.a0 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wbs, kin ? aoff + kofs(s) : OOB, 0, 0));
+    if ((s & 3) >= 2) r.b = xload(s);
+  };
+  Regs ra2, rb2;
+  issue2(ra2, 0);
+  issue2(rb2, 1);
+
   // ------------------------------------------------------------ epilogue 1
   // lane: channels c0 + [0, 16) (c0 = 64 wco + 32 t + 16 hh) of tile pixel prow
   const int m = pix(prow);
   const int jrun = prow / p.L;
   const int rh_row = prow < npx ? jrun * (p.L + 4) + (prow - jrun * p.L) : 0;   // + tap = shifted row
-  bf16x8 z[2][2];   // z as bf16 (the unfused path's default gate storage, EPI_GRU_A z_bf16)
+  // G2ALL: z goes to an LDS image in the part of GEMM 1's staging that GEMM 2 leaves free
+  bf16* const zimg = smem + 2 * G2ST;
+  [[maybe_unused]] bf16x8 z[2][2];   // z as bf16 (the unfused path's default gate storage, EPI_GRU_A z_bf16)
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int c0 = wco * 64 + 32 * t + 16 * hh;
@@ -185,10 +202,18 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
       for (int k = 0; k < 16; ++k) v[k] = sigmoidf_(v[k] + b[k]);
     }
     if (wco < 2) {
+      bf16x8 o0, o1;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        z[t][0][k] = f2bf(v[k]);
-        z[t][1][k] = f2bf(v[8 + k]);
+        o0[k] = f2bf(v[k]);
+        o1[k] = f2bf(v[8 + k]);
+      }
+      if constexpr (G2ALL) {
+        *(bf16x8*)(zimg + rh_off(prow, c0 >> 3)) = o0;
+        *(bf16x8*)(zimg + rh_off(prow, (c0 >> 3) + 1)) = o1;
+      } else {
+        z[t][0] = o0;
+        z[t][1] = o1;
       }
     } else if (m >= 0) {   // r * h (h from the bf16 loop buffer, as the unfused EPI_GRU_A) -> r*h image
       float hv[16];
@@ -204,59 +229,73 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
       *(bf16x8*)(rh + rh_off(rh_row + 2, chunk + 1)) = o1;
     }
   }
-  __syncthreads();   // r*h image complete; GEMM 1 staging free
 
   // ---------------------------------------------------------------- GEMM 2
-  // stages s = (tap, cb): cb 0, 1 = the r*h channels (B from the image), cb 2, 3 = x (staged)
-  auto issue2 = [&](Regs& r, int s) {
-    const bool kin = s < NSTG;
-    r.a0 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wbs, kin ? aoff + kofs(s) : OOB, 0, 0));
-    if ((s & 3) >= 2) r.b = xload(s);
-  };
+  // stages s = (tap, cb): cb 0, 1 = the r*h channels (B from the image), cb 2, 3 = x (staged).
+  // G2ALL: all 16 waves, 32 x 32 (channel, pixel) tiles, staging buffers of 128 + 128 rows;
+  // else the 8 z waves keep GEMM 1's 64 x 32 tiles (z in registers), the others only stage.
+  auto sA2 = [&](int buf) { return G2ALL ? smem + buf * G2ST : sA_of(buf); };
+  auto sB2 = [&](int buf) { return G2ALL ? smem + buf * G2ST + HD * BK : sB_of(buf); };
   auto store2 = [&](const Regs& r, int buf, int s) {
-    put(sA_of(buf), lrow, r.a0);
-    if ((s & 3) >= 2) put(sB_of(buf), lrow, r.b);
+    put(sA2(buf), lrow, r.a0);
+    if ((s & 3) >= 2) put(sB2(buf), lrow, r.b);
   };
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int k = 0; k < 16; ++k) acc[t][k] = 0.f;
-  auto compute2 = [&](int buf, int s) {
-    if (wco >= 2) return;   // waves 8-15 only stage operands
-    const int tap = s >> 2, cb = s & 3;
-    if (cb < 2) {
-      const int row = rh_row + tap;
-      mma_stage(sA_of(buf), wco * 64, [&](int chunk) { return *(const bf16x8*)(rh + rh_off(row, cb * 8 + chunk)); });
-    } else {
-      const bf16* sB = sB_of(buf);
-      mma_stage(sA_of(buf), wco * 64, [&](int chunk) {
-        return *(const bf16x8*)(sB + prow * BK + ((chunk ^ swzB(prow)) << 3));
-      });
+  auto mma1 = [&](const bf16* sA, int arow, auto&& bfrag) {   // one 32-row A tile (G2ALL)
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int chunk = kk * 2 + hh;
+      const bf16x8 b = bfrag(chunk);
+      const bf16x8 a = *(const bf16x8*)(sA + arow * BK + ((chunk ^ swzB(arow)) << 3));
+      acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[0], 0, 0, 0);
     }
   };
-  {
-    Regs ra, rb;
-    issue2(ra, 0);
-    issue2(rb, 1);
-    store2(ra, 0, 0);
-    __syncthreads();
-    for (int s = 0; s < NSTG; s += 2) {
-      issue2(ra, s + 2);
-      compute2(0, s);
-      store2(rb, 1, s + 1);
-      __syncthreads();
-      issue2(rb, s + 3);
-      compute2(1, s + 1);
-      store2(ra, 0, s + 2);
-      __syncthreads();
+  const int arow2 = 64 * (wco >> 1) + m32_arow(wco & 1, rho);   // G2ALL: channels 32 wco + ..
+  auto compute2 = [&](int buf, int s) {
+    if (!G2ALL && wco >= 2) return;   // waves 8-15 only stage operands
+    const int tap = s >> 2, cb = s & 3;
+    const bf16* sB = sB2(buf);
+    auto from_rh = [&](int chunk) { return *(const bf16x8*)(rh + rh_off(rh_row + tap, cb * 8 + chunk)); };
+    auto from_st = [&](int chunk) { return *(const bf16x8*)(sB + prow * BK + ((chunk ^ swzB(prow)) << 3)); };
+    if constexpr (G2ALL) {
+      if (cb < 2) mma1(sA2(buf), arow2, from_rh);
+      else mma1(sA2(buf), arow2, from_st);
+    } else {
+      if (cb < 2) mma_stage(sA2(buf), wco * 64, from_rh);
+      else mma_stage(sA2(buf), wco * 64, from_st);
     }
+  };
+  __syncthreads();   // r*h (and z) images complete; GEMM 1 staging free
+  store2(ra2, 0, 0);
+  __syncthreads();
+  for (int s = 0; s < NSTG; s += 2) {
+    issue2(ra2, s + 2);
+    compute2(0, s);
+    store2(rb2, 1, s + 1);
+    __syncthreads();
+    issue2(rb2, s + 3);
+    compute2(1, s + 1);
+    store2(ra2, 0, s + 2);
+    __syncthreads();
   }
 
   // ------------------------------------------------------------ epilogue 2
-  if (wco >= 2 || m < 0) return;
+  if ((!G2ALL && wco >= 2) || m < 0) return;
+  constexpr int NT = G2ALL ? 1 : 2;
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int c0 = wco * 64 + 32 * t + 16 * hh;
+  for (int t = 0; t < NT; ++t) {
+    const int c0 = G2ALL ? 32 * wco + 16 * hh : wco * 64 + 32 * t + 16 * hh;
+    bf16x8 zz[2];
+    if constexpr (G2ALL) {
+      zz[0] = *(const bf16x8*)(zimg + rh_off(prow, c0 >> 3));
+      zz[1] = *(const bf16x8*)(zimg + rh_off(prow, (c0 >> 3) + 1));
+    } else {
+      zz[0] = z[t][0];
+      zz[1] = z[t][1];
+    }
     float b[16], h[16], v[16];
     load_map<16>(p, m, 2 * HD + c0, b);
     float* hp = p.h32 + (long)m * HD + c0;
@@ -264,7 +303,7 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const float q = tanhf_(acc[t][k] + b[k]);
-      const float zk = bf2f(z[t][k >> 3][k & 7]);
+      const float zk = bf2f(zz[k >> 3][k & 7]);
       v[k] = (1.0f - zk) * h[k] + zk * q;
     }
     store_f32<16>(hp, v);
@@ -277,6 +316,11 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
 
 extern "C" int jr_gru_fused(const GruFusedParams* p, hipStream_t stream) {
   if (p->ntiles <= 0) return 0;
-  hipLaunchKernelGGL(gru_fused_kernel, dim3(p->ntiles), dim3(1024), 0, stream, *p);
+  // GEMM 2 on all 16 waves with z through LDS (default; measured 334-341 vs 335 pairs/s at the
+  // headline, profiles/r3_gru_fused_ab.txt) or on the 8 z waves with z in registers (JR_GRU_G2=0)
+  const char* g2 = std::getenv("JR_GRU_G2");
+  const int g2all = g2 ? std::atoi(g2) : 1;
+  if (g2all) hipLaunchKernelGGL(gru_fused_kernel<true>, dim3(p->ntiles), dim3(1024), 0, stream, *p);
+  else hipLaunchKernelGGL(gru_fused_kernel<false>, dim3(p->ntiles), dim3(1024), 0, stream, *p);
   return (int)hipGetLastError();
 }

@@ -143,14 +143,16 @@ def test_gru_fused_epilogues(hidden, xin, ks, pad, cfg):
     assert (hx[:, :hidden].float().cpu() - ref.reshape(M, hidden)).abs().max().item() < 2.5e-2
 
 
+@pytest.mark.parametrize("g2", ["0", "1"])
 @pytest.mark.parametrize("map_dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("B,h,w,vertical", [(2, 7, 13, 0), (2, 7, 13, 1), (2, 9, 12, 1), (1, 55, 128, 0),
                                             (1, 55, 128, 1), (3, 5, 3, 1), (1, 64, 20, 1), (1, 4, 128, 0)])
-def test_gru_stage_fused_kernel(B, h, w, vertical, map_dtype):
+def test_gru_stage_fused_kernel(B, h, w, vertical, map_dtype, g2, monkeypatch):
     """gru_fused.hip (one launch per ConvGRU stage, r*h and z kept in the CU) vs the fp32
     ConvGRU of the reference with the context share as a per-pixel bias map (model.py:301-312):
     row tiles (1x5) and 1- / 2-column tiles (5x1), incl. the headline's 55 x 128 grid."""
     nat = _nat()
+    monkeypatch.setenv("JR_GRU_G2", g2)   # GEMM 2 on the 8 z waves (0) or all 16 waves (1)
     torch.manual_seed(5)
     hd, M = 128, B * h * w
     ks = (5, 1) if vertical else (1, 5)
