@@ -66,6 +66,10 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
   const int wco = wave & 3, wp = wave >> 2;   // 64-channel group, 32-pixel group
   const int rho = lane & 31, hh = lane >> 5;
   const int tile = blockIdx.x;
+  auto stamp = [&](int k) {
+    if (p.dbg && tid == 0) p.dbg[tile * 6 + k] = (long long)wall_clock64();
+  };
+  stamp(0);
   const int n = tile / p.tiles_per_img, tt = tile - n * p.tiles_per_img;
   const int npx = p.J * p.L;
   auto pix = [&](int pl) -> int {   // tile pixel -> global pixel index (or -1)
@@ -171,6 +175,7 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
     }
   }
 
+  stamp(1);
   // GEMM 2's first two stages (weights only: the r*h blocks of tap 0) load during epilogue 1
   auto issue2 = [&](Regs& r, int s) {
     const bool kin = s < NSTG;
@@ -269,6 +274,7 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
     }
   };
   __syncthreads();   // r*h (and z) images complete; GEMM 1 staging free
+  stamp(2);
   store2(ra2, 0, 0);
   __syncthreads();
   for (int s = 0; s < NSTG; s += 2) {
@@ -283,6 +289,7 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
   }
 
   // ------------------------------------------------------------ epilogue 2
+  stamp(3);
   if ((!G2ALL && wco >= 2) || m < 0) return;
   constexpr int NT = G2ALL ? 1 : 2;
 #pragma unroll
@@ -310,6 +317,7 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
     store_bf16<16>((bf16*)p.y + (long)m * p.y_cs + c0, v);
     if (p.y2) store_bf16<16>((bf16*)p.y2 + (long)m * p.y2_cs + c0, v);
   }
+  stamp(4);
 }
 
 }  // namespace

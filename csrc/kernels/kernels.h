@@ -341,6 +341,7 @@ struct GruFusedParams {
   int vertical;                       // 0: 1x5 taps along W, tiles = image rows; 1: 5x1, tiles = J columns
   int L, J, tiles_per_img, ntiles;    // run length (W or H), runs per tile (J * L <= 128)
   long hx_bytes, wa_bytes, wb_bytes;
+  long long* dbg;                     // optional [ntiles][6] phase timestamps (s_memrealtime, tools/gru_phases.py)
 };
 int jr_gru_fused(const GruFusedParams* p, hipStream_t stream);
 

@@ -494,7 +494,7 @@ bool gru_fused_fits(int64_t H, int64_t W, int64_t vertical) {
 // i = [N, H, W, vertical].  Tiles: a row (1x5, W <= 128) or J = 2 / 1 columns (5x1, J * H <= 128).
 static Launch make_gru_fused(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
   at::Tensor hx = opt(t, 0), wa = opt(t, 1), wb = opt(t, 2), bmap = opt(t, 3), h32 = opt(t, 4), y = opt(t, 5),
-             y2 = opt(t, 6);
+             y2 = opt(t, 6), dbg = opt(t, 7);
   check_bf16(hx, "hx"); check_bf16(wa, "wa"); check_bf16(wb, "wb"); check_f32(h32, "h32"); check_bf16(y, "y");
   TORCH_CHECK(i.size() == 4, "gru_fused: expected 4 ints");
   GruFusedParams p{};
@@ -525,6 +525,10 @@ static Launch make_gru_fused(const TList& t, const IList& i, std::vector<at::Ten
   if (!p.vertical) { p.L = p.W; p.J = 1; p.tiles_per_img = p.H; }
   else { p.L = p.H; p.J = 2 * p.H <= 128 && p.W % 2 == 0 ? 2 : 1; p.tiles_per_img = p.W / p.J; }
   p.ntiles = p.N * p.tiles_per_img;
+  if (dbg.defined()) {   // phase timestamps (tools/gru_phases.py)
+    TORCH_CHECK(dbg.is_cuda() && dbg.scalar_type() == at::kLong && dbg.numel() >= (int64_t)p.ntiles * 6, "gru_fused: dbg");
+    p.dbg = (long long*)dbg.data_ptr();
+  }
   p.hx_bytes = (long)hx.numel() * 2; p.wa_bytes = (long)wa.numel() * 2; p.wb_bytes = (long)wb.numel() * 2;
   TORCH_CHECK(p.hx_bytes < (1LL << 31), "gru_fused: hx larger than 2 GiB");
   if (keep) for (auto& v : {hx, wa, wb, bmap, h32, y, y2}) if (v.defined()) keep->push_back(v);
