@@ -241,6 +241,36 @@ __global__ void prep_images_kernel(const float* __restrict__ i1, const float* __
   *(bf16x8*)(out + idx * 8) = o;
 }
 
+// Space-to-depth image prep for the encoders' 7x7 / stride-2 stem (model.py:238-240):
+// out[n][Y][X][(sy * 2 + sx) * 3 + c] = img[n][2Y + sy][2X + sx][c] (bf16, channels 12..15 zero),
+// the input of the equivalent 4x4 / stride-1 conv (ops/native.py:s2d_stem_kernel): K = 16 x 16
+// instead of 49 x 8 (8-channel padded 3-channel taps).
+__global__ void prep_images_s2d_kernel(const float* __restrict__ i1, const float* __restrict__ i2, int B, int H, int W,
+                                       bf16* __restrict__ out) {
+  const int H2 = H >> 1, W2 = W >> 1;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long per = (long)H2 * W2;
+  if (idx >= 2L * B * per) return;
+  const long n = idx / per;
+  const int r = (int)(idx - n * per), Y = r / W2, X = r - (r / W2) * W2;
+  const float* img = n < B ? i1 + n * (long)H * W * 3 : i2 + (n - B) * (long)H * W * 3;
+  bf16x8 o0, o1;
+#pragma unroll
+  for (int sy = 0; sy < 2; ++sy) {
+    const float* row = img + ((long)(2 * Y + sy) * W + 2 * X) * 3;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {   // (sx, c) of this row: channels sy * 6 + k
+      const int ch = sy * 6 + k;
+      if (ch < 8) o0[ch] = f2bf(row[k]);
+      else o1[ch - 8] = f2bf(row[k]);
+    }
+  }
+#pragma unroll
+  for (int j = 4; j < 8; ++j) o1[j] = f2bf(0.f);
+  *(bf16x8*)(out + idx * 16) = o0;
+  *(bf16x8*)(out + idx * 16 + 8) = o1;
+}
+
 __global__ void init_coords_kernel(float* __restrict__ coords, int B, int h, int w) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long total = (long)B * h * w;
@@ -335,6 +365,15 @@ extern "C" int jr_prep_images(const float* img1, const float* img2, int B, int H
                               hipStream_t stream) {
   const long total = 2L * B * H * W;
   hipLaunchKernelGGL(prep_images_kernel, dim3(nblk(total, 256)), dim3(256), 0, stream, img1, img2, B, (long)H * W,
+                     (bf16*)out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jr_prep_images_s2d(const float* img1, const float* img2, int B, int H, int W, void* out,
+                                  hipStream_t stream) {
+  if ((H | W) & 1) return (int)hipErrorInvalidValue;
+  const long total = 2L * B * (H / 2) * (W / 2);
+  hipLaunchKernelGGL(prep_images_s2d_kernel, dim3(nblk(total, 256)), dim3(256), 0, stream, img1, img2, B, H, W,
                      (bf16*)out);
   return (int)hipGetLastError();
 }

@@ -138,6 +138,31 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
 #pragma unroll
     for (int k = 0; k < 16; ++k) acc[t][k] = 0.f;
   const int prow = wp * 32 + rho;   // this lane's pixel row in the tile
+  const int m = pix(prow);
+  const int jrun = prow / p.L;
+  const int rh_row = prow < npx ? jrun * (p.L + 4) + (prow - jrun * p.L) : 0;   // + tap = shifted row
+  // bf16 bias-map chunks of this lane's pixel, loaded during the last K stages of a GEMM
+  // (its epilogue then starts without a dependent global load)
+  // Unconditional loads (pixel clamped, an fp32 map read as bf16 chunks stays in bounds): a
+  // branch around them makes hipcc wait vmcnt(0) for them before the next LDS store of staged
+  // operands (measured +1-2.4 us per GEMM).
+  const int mld = m >= 0 ? m : 0;
+  auto pre_map = [&](u32x4 (&r)[2], int c) {
+    const u32x4* q = (const u32x4*)((const bf16*)p.bmap + (long)mld * p.bmap_cs + c);
+    r[0] = q[0];
+    r[1] = q[1];
+  };
+  auto map16 = [&](const u32x4 (&r)[2], int c, float* v) {   // bias map values: prefetched (bf16) or loaded
+    if (p.bmap_bf16) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v[k] = bf2f(__builtin_bit_cast(bf16x8, r[0])[k]);
+        v[8 + k] = bf2f(__builtin_bit_cast(bf16x8, r[1])[k]);
+      }
+    } else {
+      load_map<16>(p, m, c, v);
+    }
+  };
   auto mma_stage = [&](const bf16* sA, int arow0, auto&& bfrag) {
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
@@ -157,13 +182,14 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
       return *(const bf16x8*)(sB + prow * BK + ((chunk ^ swzB(prow)) << 3));
     });
   };
+  u32x4 bm1[2][2];
   {
     Regs ra, rb;
     issue1(ra, 0);
     issue1(rb, 1);
     store1(ra, 0);
     __syncthreads();
-    for (int s = 0; s < NSTG; s += 2) {
+    for (int s = 0; s < NSTG - 2; s += 2) {
       issue1(ra, s + 2);
       compute1(0);
       store1(rb, 1);
@@ -173,6 +199,14 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
       store1(ra, 0);
       __syncthreads();
     }
+    // last two stages: no operand loads left; the epilogue's bias-map chunks load instead
+#pragma unroll
+    for (int t = 0; t < 2; ++t) pre_map(bm1[t], wco * 64 + 32 * t + 16 * hh);
+    compute1(0);
+    store1(rb, 1);
+    __syncthreads();
+    compute1(1);
+    __syncthreads();   // GEMM 1 staging free (G2ALL writes the z image into it)
   }
 
   stamp(1);
@@ -188,9 +222,6 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
 
   // ------------------------------------------------------------ epilogue 1
   // lane: channels c0 + [0, 16) (c0 = 64 wco + 32 t + 16 hh) of tile pixel prow
-  const int m = pix(prow);
-  const int jrun = prow / p.L;
-  const int rh_row = prow < npx ? jrun * (p.L + 4) + (prow - jrun * p.L) : 0;   // + tap = shifted row
   // G2ALL: z goes to an LDS image in the part of GEMM 1's staging that GEMM 2 leaves free
   bf16* const zimg = smem + 2 * G2ST;
   [[maybe_unused]] bf16x8 z[2][2];   // z as bf16 (the unfused path's default gate storage, EPI_GRU_A z_bf16)
@@ -202,7 +233,7 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
     for (int k = 0; k < 16; ++k) v[k] = acc[t][k];
     if (m >= 0) {
       float b[16];
-      load_map<16>(p, m, c0, b);
+      map16(bm1[t], c0, b);
 #pragma unroll
       for (int k = 0; k < 16; ++k) v[k] = sigmoidf_(v[k] + b[k]);
     }
@@ -277,7 +308,7 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
   stamp(2);
   store2(ra2, 0, 0);
   __syncthreads();
-  for (int s = 0; s < NSTG; s += 2) {
+  for (int s = 0; s < NSTG - 2; s += 2) {
     issue2(ra2, s + 2);
     compute2(0, s);
     store2(rb2, 1, s + 1);
@@ -287,11 +318,28 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
     store2(ra2, 0, s + 2);
     __syncthreads();
   }
+  // last two stages: the epilogue's bias-map chunks and fp32 state load instead of operands
+  constexpr int NT = G2ALL ? 1 : 2;
+  u32x4 bm2[NT][2];
+  [[maybe_unused]] f32x4 h2[4];   // G2ALL: the fp32 state too (the 8-wave variant has no registers to spare)
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int c0 = G2ALL ? 32 * wco + 16 * hh : wco * 64 + 32 * t + 16 * hh;
+    pre_map(bm2[t], 2 * HD + c0);
+    if constexpr (G2ALL) {
+      const f32x4* hq = (const f32x4*)(p.h32 + (long)mld * HD + c0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) h2[k] = hq[k];
+    }
+  }
+  compute2(0, NSTG - 2);
+  store2(rb2, 1, NSTG - 1);
+  __syncthreads();
+  compute2(1, NSTG - 1);
 
   // ------------------------------------------------------------ epilogue 2
   stamp(3);
   if ((!G2ALL && wco >= 2) || m < 0) return;
-  constexpr int NT = G2ALL ? 1 : 2;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int c0 = G2ALL ? 32 * wco + 16 * hh : wco * 64 + 32 * t + 16 * hh;
@@ -304,9 +352,14 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
       zz[1] = z[t][1];
     }
     float b[16], h[16], v[16];
-    load_map<16>(p, m, 2 * HD + c0, b);
+    map16(bm2[t], 2 * HD + c0, b);
     float* hp = p.h32 + (long)m * HD + c0;
-    load_f32<16>(hp, h);
+    if constexpr (G2ALL) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) h[k] = h2[k >> 2][k & 3];
+    } else {
+      load_f32<16>(hp, h);
+    }
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const float q = tanhf_(acc[t][k] + b[k]);

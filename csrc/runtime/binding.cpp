@@ -843,12 +843,18 @@ static Launch make_prep(const TList& t, const IList& i, std::vector<at::Tensor>*
   at::Tensor a = opt(t, 0), b = opt(t, 1), out = opt(t, 2);
   check_f32(a, "img1"); check_f32(b, "img2"); check_bf16(out, "out");
   const int B = (int)i[0], H = (int)i[1], W = (int)i[2];
+  const bool s2d = i.size() > 3 && i[3];   // 2x2 space-to-depth layout for the s2d stem
   TORCH_CHECK(a.numel() == (int64_t)B * H * W * 3 && b.numel() == a.numel(), "prep: image shape");
-  TORCH_CHECK(out.numel() >= 2LL * B * H * W * 8 && cs(out) == 8, "prep: output");
+  if (s2d) {
+    TORCH_CHECK(H % 2 == 0 && W % 2 == 0 && out.numel() >= 2LL * B * H * W * 4 && cs(out) == 16, "prep: s2d output");
+  } else {
+    TORCH_CHECK(out.numel() >= 2LL * B * H * W * 8 && cs(out) == 8, "prep: output");
+  }
   if (keep) { keep->push_back(a); keep->push_back(b); keep->push_back(out); }
   const float* ap = a.data_ptr<float>();
   const float* bp = b.data_ptr<float>();
   void* op = out.data_ptr();
+  if (s2d) return [=](hipStream_t s, int) { return jr_prep_images_s2d(ap, bp, B, H, W, op, s); };
   return [=](hipStream_t s, int) { return jr_prep_images(ap, bp, B, H, W, op, s); };
 }
 

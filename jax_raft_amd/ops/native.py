@@ -208,6 +208,26 @@ def make_spec(kernel: torch.Tensor, bias: torch.Tensor, stride=(1, 1), padding=(
     return ConvSpec(w, b, kh, kw, stride[0], stride[1], padding[0], padding[1], cin, cin8, cout)
 
 
+def s2d_stem_kernel(kernel: torch.Tensor) -> torch.Tensor:
+    """A 7x7 / stride-2 / pad-3 conv over 3 channels (the encoders' stem, model.py:238-240)
+    as the equivalent 4x4 / stride-1 conv (top / left pad 2, output H/2 x W/2) over the 2x2
+    space-to-depth input (channel (sy * 2 + sx) * 3 + c, 16 with zero padding):
+    W'[ty][tx][(sy, sx, c)] = W[2 ty + sy - 1][2 tx + sx - 1][c] where that tap exists."""
+    kh, kw, cin, cout = kernel.shape
+    assert (kh, kw, cin) == (7, 7, 3), kernel.shape
+    k = kernel.detach().float()
+    out = torch.zeros(4, 4, 16, cout, dtype=k.dtype, device=k.device)
+    for ty in range(4):
+        for tx in range(4):
+            for sy in range(2):
+                for sx in range(2):
+                    a, b = 2 * ty + sy - 1, 2 * tx + sx - 1
+                    if 0 <= a < 7 and 0 <= b < 7:
+                        c0 = (sy * 2 + sx) * 3
+                        out[ty, tx, c0:c0 + 3] = k[a, b]
+    return out
+
+
 def pick_cfg(M: int, cout: int) -> int:
     """Tile-config heuristic: minimise (waves of blocks) x (tile cost), where a
     tile's per-FLOP cost rises as it shrinks; keeps >= one wave of blocks over
@@ -229,10 +249,10 @@ def conv_args(spec: ConvSpec, x: torch.Tensor, N: int, H: int, W: int, y: torch.
               y_coff: int = 0, act: int = ACT_NONE, split: int = 0, alpha: float = 1.0, y2=None, y2_coff: int = 0,
               res=None, res_coff: int = 0, res_post: int = 0, h32=None, zbuf=None, hidden: int = 0, coords=None,
               flow32=None, y3=None, y3_coff: int = 0, epi: int = EPI_STD, cfg: Optional[int] = None,
-              bmap=None, bmap_coff: int = 0, tapw=None):
+              bmap=None, bmap_coff: int = 0, tapw=None, out_hw: Optional[Tuple[int, int]] = None):
     """Build the (tensors, ints, alpha) argument triple of the ``conv`` op.
     ``bmap``: optional fp32 per-pixel bias map [M, C], channels from ``bmap_coff``."""
-    OH, OW = spec.out_hw(H, W)
+    OH, OW = out_hw if out_hw is not None else spec.out_hw(H, W)
     if cfg is None:
         cfg = pick_cfg(N * OH * OW, spec.cout)
     t = [x, spec.w, spec.b, y, y2, res, h32, zbuf, coords, flow32, y3, bmap]
@@ -240,8 +260,8 @@ def conv_args(spec: ConvSpec, x: torch.Tensor, N: int, H: int, W: int, y: torch.
         t.append(tapw)
     i = [N, H, W, x_coff, spec.cin8, spec.kh, spec.kw, spec.sh, spec.sw, spec.ph, spec.pw, spec.cout, act, split,
          y_coff, y2_coff, res_coff, hidden, y3_coff, epi, cfg, res_post]
-    if bmap is not None:
-        i += [0, 0, 0, 0, bmap_coff]
+    if bmap is not None or out_hw is not None:
+        i += [OH if out_hw is not None else 0, OW if out_hw is not None else 0, 0, 0, bmap_coff]
     return t, i, float(alpha)
 
 

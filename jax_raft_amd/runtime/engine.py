@@ -365,8 +365,18 @@ class RaftEngine:
         def conv_src(c, cin8=None):
             return lambda: (c.kernel.detach().float(), c.bias.detach().float(), c.stride, c.padding, cin8)
 
+        def s2d_src(cna: ConvNormActivation):
+            def f():
+                k, b = _fold_bn(cna)
+                return nat.s2d_stem_kernel(k), b, (1, 1), (2, 2), 16
+            return f
+
         for tag, enc in (("fe", m.feature_encoder), ("ce", m.context_encoder)):
             self._reg(f"{tag}.stem", cna_src(enc.convnormrelu, 8))
+            c0 = enc.convnormrelu.layers_0
+            if tuple(c0.kernel.shape[:3]) == (7, 7, 3) and tuple(c0.stride) == (2, 2) and tuple(c0.padding) == (3, 3):
+                # the stem as a 4x4 conv over the 2x2 space-to-depth input (ops/native.py:s2d_stem_kernel)
+                self._reg(f"{tag}.stem_s2d", s2d_src(enc.convnormrelu))
             for li in (1, 2, 3):
                 layer = getattr(enc, f"layer{li}")
                 for bi in range(layer.n):
@@ -442,7 +452,7 @@ class RaftEngine:
         if kw.get("epi") == EPI_TAPS and not self.autotune and kw.get("cfg") is None:
             kw = dict(kw, cfg=nat.TAPS_CFGS[0])
         if self.autotune and kw.get("cfg") is None:
-            OH, OW = spec.out_hw(H, W)
+            OH, OW = kw["out_hw"] if kw.get("out_hw") is not None else spec.out_hw(H, W)
             key = (N * OH * OW, spec.cout, spec.kh, spec.kw, spec.sh, spec.sw, spec.cin8, x.shape[-1],
                    kw.get("epi", EPI_STD), kw.get("bmap") is not None)
             cfg = _TUNE_CACHE.get(key + (str(self.device),))
@@ -478,12 +488,17 @@ class RaftEngine:
             bufs[bt + name] = t
             return t
 
-        def conv_raw(name, x, N, H, W, act=ACT_NONE, res=None, res_post=0):
+        def conv_raw(name, x, N, H, W, act=ACT_NONE, res=None, res_post=0, out_hw=None):
             s = sp[name]
-            OH, OW = s.out_hw(H, W)
+            OH, OW = out_hw if out_hw is not None else s.out_hw(H, W)
             y = alloc(name + ".y", (N, OH, OW, s.cout))
-            self._conv(plan, s, x, N, H, W, y, act=act, res=res, res_post=res_post)
+            self._conv(plan, s, x, N, H, W, y, act=act, res=res, res_post=res_post, out_hw=out_hw)
             return y, OH, OW
+
+        def stem(act=ACT_NONE):
+            if x.shape[-1] == 16:   # space-to-depth input (prep s2d): the 4x4 / stride-1 form of the stem
+                return conv_raw(f"{tag}.stem_s2d", x, N, H // 2, W // 2, act=act, out_hw=(H // 2, W // 2))
+            return conv_raw(f"{tag}.stem", x, N, H, W, act=act)
 
         def stats(name, y, N, HW, C):
             t = alloc(name + ".stats", (N, C, 2), F32)
@@ -499,10 +514,10 @@ class RaftEngine:
 
         # stem
         if inorm:
-            y, H, W = conv_raw(f"{tag}.stem", x, N, H, W)
+            y, H, W = stem()
             x = norm_act(f"{tag}.stem", y, stats(f"{tag}.stem", y, N, H * W, y.shape[-1]), relu=2)
         else:
-            x, H, W = conv_raw(f"{tag}.stem", x, N, H, W, act=ACT_RELU)
+            x, H, W = stem(act=ACT_RELU)
         for li in (1, 2, 3):
             layer = getattr(enc, f"layer{li}")
             for bi in range(layer.n):
@@ -728,8 +743,14 @@ class RaftEngine:
         flow32 = alloc("flow32", (M, 2), F32)
         for t in (hx, qx, flow8, flow32):
             plan.add_memset([t])
-        x0 = alloc("x0", (2 * B, H, W, 8))
-        plan.add_prep([inp1, inp2, x0], [B, H, W])
+        s2d = ("fe.stem_s2d" in sp and "ce.stem_s2d" in sp and H % 2 == 0 and W % 2 == 0
+               and os.environ.get("JR_NO_S2D", "0") != "1")
+        if s2d:   # 2x2 space-to-depth images for the 4x4 form of the 7x7 / stride-2 stems
+            x0 = alloc("x0", (2 * B, H // 2, W // 2, 16))
+            plan.add_prep([inp1, inp2, x0], [B, H, W, 1])
+        else:
+            x0 = alloc("x0", (2 * B, H, W, 8))
+            plan.add_prep([inp1, inp2, x0], [B, H, W])
         plan.add_record(E_PREP)
 
         lane(side)

@@ -69,8 +69,8 @@ class RaftEngineF32(RaftEngine):
         for name, fn in self._sources.items():
             if name in ("fh1", "fh2.taps") and self.has_mask:
                 continue   # bf16-engine fusions (FlowHead conv1 || mask conv, conv2 as taps)
-            if name == "fh2.taps":
-                continue
+            if name == "fh2.taps" or name.endswith(".stem_s2d"):
+                continue   # bf16-engine forms
             k, b, stride, pad, _ = fn()
             k = k.to(self.device)
             cin4 = self._cin4(name, k.shape[2])

@@ -617,3 +617,24 @@ def test_conv_taps_epilogue(cfg):
     out = taps.cpu()
     assert _rel(out[:, :18], ref) < 5e-3
     assert (out[:, 18:] == 7.0).all()
+
+
+@pytest.mark.parametrize("B,H,W", [(1, 16, 24), (2, 40, 56)])
+def test_s2d_stem_matches_7x7_stride2(B, H, W):
+    """Space-to-depth prep (elementwise.hip:prep_images_s2d_kernel) + the 4x4 / stride-1 form of
+    the 7x7 / stride-2 stem (ops/native.py:s2d_stem_kernel, top / left pad 2, output H/2 x W/2)
+    vs the fp32 7x7 conv of the reference (model.py:238-240)."""
+    nat = _nat()
+    torch.manual_seed(6)
+    i1, i2 = torch.rand(B, H, W, 3) * 2 - 1, torch.rand(B, H, W, 3) * 2 - 1
+    k = torch.randn(7, 7, 3, 64) / math.sqrt(147)
+    b = torch.randn(64) * 0.1
+    x0 = torch.zeros(2 * B, H // 2, W // 2, 16, dtype=torch.bfloat16, device=DEV)
+    nat.ops().prep([i1.to(DEV), i2.to(DEV), x0], [B, H, W, 1])
+    spec = nat.make_spec(nat.s2d_stem_kernel(k), b, (1, 1), (2, 2), cin8=16, device=DEV)
+    y = torch.empty(2 * B, H // 2, W // 2, 64, dtype=torch.float32, device=DEV)
+    nat.ops().conv(*nat.conv_args(spec, x0, 2 * B, H // 2, W // 2, y, out_hw=(H // 2, W // 2)))
+    torch.cuda.synchronize()
+    ref = R.conv2d_nhwc(_bf(torch.cat([i1, i2])), _bf(k), b, (2, 2), (3, 3))
+    assert y.shape == ref.shape
+    assert _rel(y.cpu(), ref) < 3e-3
