@@ -638,3 +638,27 @@ def test_s2d_stem_matches_7x7_stride2(B, H, W):
     ref = R.conv2d_nhwc(_bf(torch.cat([i1, i2])), _bf(k), b, (2, 2), (3, 3))
     assert y.shape == ref.shape
     assert _rel(y.cpu(), ref) < 3e-3
+
+
+@pytest.mark.parametrize("B,h,w,L", [(2, 12, 16, 4), (1, 9, 12, 3), (2, 16, 24, 4)])
+def test_pyr_bwd_dc(B, h, w, L):
+    """Correlation-pyramid backward, first half (train.hip: pyr_bwd_dc / pyr_bwd_dc8 for w % 8 == 0):
+    dC = s (g0 + sum_l nearest-upsampled g_l / 4^l) over the floor-pooled region, bf16."""
+    nat = _nat()
+    torch.manual_seed(7)
+    M = B * h * w
+    gs, hl, wl = [], h, w
+    for _ in range(L):
+        gs.append(torch.randn(M, hl, wl))
+        hl //= 2
+        wl //= 2
+    ref = gs[0].clone()
+    for l in range(1, L):
+        g = gs[l]
+        up = g.repeat_interleave(2 ** l, 1).repeat_interleave(2 ** l, 2) / 4 ** l
+        ref[:, :up.shape[1], :up.shape[2]] += up
+    ref *= 0.0625
+    dc = torch.empty(B, h * w, h * w, dtype=torch.bfloat16, device=DEV)
+    nat.ops().pyr_bwd_dc([dc] + [g.to(DEV) for g in gs] + [None] * (4 - L), [L, M, h, w], 0.0625)
+    torch.cuda.synchronize()
+    assert _rel(dc.float().cpu().reshape(M, h, w), ref) < 8e-3
