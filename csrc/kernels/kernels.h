@@ -346,5 +346,10 @@ struct GruFusedParams {
   long long* dbg;                     // optional [ntiles][6] phase timestamps (s_memrealtime, tools/gru_phases.py)
 };
 int jr_gru_fused(const GruFusedParams* p, hipStream_t stream);
+// Batched bf16 GEMM, fp32 accumulation (bgemm.hip): C[b] = alpha * op(A[b]) . B[b], B k-major [K][N],
+// A row-major [M][K] (a_kmajor 0) or k-major [K][M] (1); fp32 (C32) or bf16 (C16) output [M][ldc].
+// M, N multiples of 128, K of 64.
+int jr_bgemm(const void* A, long a_bs, int lda, int a_kmajor, const void* B, long b_bs, int ldb, int batch, int M,
+             int N, int K, float alpha, float* C32, void* C16, long c_bs, int ldc, hipStream_t stream);
 
 }  // extern "C"

@@ -1257,6 +1257,28 @@ void im2col_op(const TList& t, IList i) { run_now(make_im2col(t, i, nullptr)); }
 void flow_taps_op(const TList& t, IList i) { run_now(make_flow_taps(t, i, nullptr)); }
 void taps_gemm_op(const TList& t, IList i) { run_now(make_taps_gemm(t, i, nullptr)); }
 void gru_fused_op(const TList& t, IList i) { run_now(make_gru_fused(t, i, nullptr)); }
+
+// Batched GEMM (bgemm.hip).  t = [A (bf16 [batch][M][K] or [batch][K][M]), B (bf16 [batch][K][N]),
+// C (fp32 / bf16 [batch][M][N])], i = [M, N, K, a_kmajor]
+void bgemm_op(const TList& t, IList i, double alpha) {
+  at::Tensor a = opt(t, 0), b = opt(t, 1), c = opt(t, 2);
+  check_bf16(a, "A"); check_bf16(b, "B");
+  TORCH_CHECK(i.size() == 4, "bgemm: expected [M, N, K, a_kmajor]");
+  const int64_t M = i[0], N = i[1], K = i[2];
+  const int ak = (int)i[3];
+  TORCH_CHECK(c.defined() && c.is_cuda() && c.is_contiguous() &&
+                  (c.scalar_type() == at::kFloat || c.scalar_type() == at::kBFloat16), "bgemm: C fp32 / bf16 contiguous");
+  TORCH_CHECK(M % 128 == 0 && N % 128 == 0 && K % 64 == 0 && M > 0 && N > 0 && K > 0, "bgemm: M, N % 128, K % 64");
+  TORCH_CHECK(a.dim() == 3 && b.dim() == 3 && c.dim() == 3 && a.size(0) == b.size(0) && a.size(0) == c.size(0),
+              "bgemm: batched 3-d operands");
+  TORCH_CHECK((ak ? (a.size(1) == K && a.size(2) == M) : (a.size(1) == M && a.size(2) == K)) && b.size(1) == K &&
+                  b.size(2) == N && c.size(1) == M && c.size(2) == N, "bgemm: shapes");
+  TORCH_CHECK(M * K * 2 < (1LL << 31) && K * N * 2 < (1LL << 31), "bgemm: one batch's operand must stay below 2 GiB");
+  const bool f32 = c.scalar_type() == at::kFloat;
+  JR_CHECK_OK(jr_bgemm(a.data_ptr(), (long)(M * K), (int)(ak ? M : K), ak, b.data_ptr(), (long)(K * N), (int)N,
+                       (int)a.size(0), (int)M, (int)N, (int)K, (float)alpha, f32 ? c.data_ptr<float>() : nullptr,
+                       f32 ? nullptr : c.data_ptr(), (long)(M * N), (int)N, cur_stream()));
+}
 void conv1x1_op(const TList& t, IList i) { run_now(make_conv1x1(t, i, nullptr)); }
 void conv_direct_op(const TList& t, IList i) { run_now(make_conv_direct(t, i, nullptr)); }
 void conv_train_op(const TList& t, IList i, double alpha, const TList& tx, IList ix) {
@@ -1821,6 +1843,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("flow_taps(Tensor?[] t, int[] i) -> ()", &jr::flow_taps_op);
   m.def("taps_gemm(Tensor?[] t, int[] i) -> ()", &jr::taps_gemm_op);
   m.def("gru_fused(Tensor?[] t, int[] i) -> ()", &jr::gru_fused_op);
+  m.def("bgemm(Tensor?[] t, int[] i, float alpha) -> ()", &jr::bgemm_op);
   m.def("gru_fused_fits(int H, int W, int vertical) -> bool", &jr::gru_fused_fits);
   m.def("conv1x1(Tensor?[] t, int[] i) -> ()", &jr::conv1x1_op);
   m.def("conv_direct(Tensor?[] t, int[] i) -> ()", &jr::conv_direct_op);

@@ -42,6 +42,7 @@ KERNEL_SOURCES = [
     CSRC / "kernels" / "convex_head.hip",
     CSRC / "kernels" / "conv1x1.hip",
     CSRC / "kernels" / "gru_fused.hip",
+    CSRC / "kernels" / "bgemm.hip",
 ]
 HOST_SOURCES = [CSRC / "runtime" / "binding.cpp"]
 HEADERS = [CSRC / "kernels" / "common.h", CSRC / "kernels" / "kernels.h", CSRC / "kernels" / "conv_igemm.h"]

@@ -822,7 +822,10 @@ class FusedLoop:
         """Correlation pyramid backward: the pooling adjoints of all levels as one
         native pass to a bf16 volume gradient dC (with the 1/sqrt(C) scale), then
         dfmap1 = dC fmap2 and dfmap2 = dC^T fmap1 as batched bf16 GEMMs with fp32
-        accumulation (written straight into ``out1`` / ``out2`` when given)."""
+        accumulation (written straight into ``out1`` / ``out2`` when given): the native
+        batched MFMA GEMM (csrc/kernels/bgemm.hip, dC read row-major for dfmap1 and as
+        dC^T -- k-major -- for dfmap2, no transposed copy), torch.bmm only for shapes
+        outside its tiling (h*w or C not a multiple of 128)."""
         B, h, w, C = self.B, self.h, self.w, self.fmap_ch
         hw = h * w
         if getattr(self, "_dC", None) is None:
@@ -831,6 +834,13 @@ class FusedLoop:
                              1.0 / float(C) ** 0.5)
         f1 = self.fm1.reshape(B, hw, C)
         f2 = self.fm2.reshape(B, hw, C)
+        if hw % 128 == 0 and C % 128 == 0 and f1.is_contiguous() and f2.is_contiguous():
+            if out1 is None:
+                out1 = torch.empty(B, h, w, C, dtype=F32, device=self.device)
+                out2 = torch.empty(B, h, w, C, dtype=F32, device=self.device)
+            nat.ops().bgemm([self._dC, f2, out1.reshape(B, hw, C)], [hw, C, hw, 0], 1.0)   # dC . fmap2
+            nat.ops().bgemm([self._dC, f1, out2.reshape(B, hw, C)], [hw, C, hw, 1], 1.0)   # dC^T . fmap1
+            return out1, out2
         if out1 is not None:
             torch.bmm(self._dC, f2, out=out1.reshape(B, hw, C))
             torch.bmm(self._dC.transpose(1, 2), f1, out=out2.reshape(B, hw, C))

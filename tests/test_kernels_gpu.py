@@ -662,3 +662,22 @@ def test_pyr_bwd_dc(B, h, w, L):
     nat.ops().pyr_bwd_dc([dc] + [g.to(DEV) for g in gs] + [None] * (4 - L), [L, M, h, w], 0.0625)
     torch.cuda.synchronize()
     assert _rel(dc.float().cpu().reshape(M, h, w), ref) < 8e-3
+
+
+@pytest.mark.parametrize("a_kmajor", [0, 1])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("batch,M,N,K", [(2, 128, 256, 192), (3, 384, 128, 512), (1, 256, 256, 3072)])
+def test_bgemm(batch, M, N, K, a_kmajor, out_dtype):
+    """bgemm.hip (the pyramid backward's dfmap1 = dC . fmap2 / dfmap2 = dC^T . fmap1): batched
+    bf16 GEMM with A row-major or k-major vs fp32 matmul of the same bf16 operands."""
+    nat = _nat()
+    torch.manual_seed(8)
+    a = torch.randn(batch, M, K)
+    b = torch.randn(batch, K, N)
+    ref = torch.bmm(_bf(a), _bf(b)) * 0.5
+    ag = (a.transpose(1, 2) if a_kmajor else a).contiguous().to(DEV, torch.bfloat16)
+    c = torch.full((batch, M, N), float("nan"), dtype=out_dtype, device=DEV)
+    nat.ops().bgemm([ag, b.to(DEV, torch.bfloat16), c], [M, N, K, a_kmajor], 0.5)
+    torch.cuda.synchronize()
+    assert not torch.isnan(c.float()).any()
+    assert _rel(c.float().cpu(), ref) < (3e-3 if out_dtype == torch.float32 else 1e-2)
