@@ -218,7 +218,10 @@ def run_inference(ctx: Ctx, model, *, B: int, H: int, W: int, iters: int, steps:
     if copipe:
         eng.flush()   # the last prologue's batch (untimed)
         torch.cuda.synchronize(dev)
-    step_ms = sorted(events[i].elapsed_time(events[i + 1]) for i in range(steps))
+    step_ms = [events[i].elapsed_time(events[i + 1]) for i in range(steps)]
+    if os.environ.get("JR_BENCH_STEPS") == "1":   # per-step device times in order (diagnostics)
+        print("step_ms " + " ".join(f"{t:.2f}" for t in step_ms), file=sys.stderr, flush=True)
+    step_ms.sort()
     pct = lambda q: round(step_ms[min(len(step_ms) - 1, int(q * len(step_ms)))], 3)
     el = t1 - t0
     per_rank = [round(1000.0 * e / steps, 3) for e in ctx.all_values(el)]
