@@ -584,6 +584,59 @@ static Launch make_conv_direct(const TList& t, const IList& i, std::vector<at::T
   };
 }
 
+// The 7x7 flow conv (as make_conv_direct) merged with the DEFERRED x8 upsampling of the
+// previous iteration (merged.hip).  t = [x, w, bias, y, flow32, out, out_slot?(, feat, wpk, cbias)],
+// i = [N, H, W, 2, 7, 7, PH, PW, cout, relu, y_coff, mode (1 bilinear / 2 convex head), out_iter_stride,
+// out_slot_off, feat_coff].  Iteration 0 runs the flow conv alone (nothing to upsample yet); iteration
+// it > 0 upsamples iteration it - 1, as a deferred op would.
+static Launch make_flowin_dual(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep) {
+  Launch conv = make_conv_direct(t, IList(i.begin(), i.begin() + 11), keep);
+  TORCH_CHECK(i.size() == 15 && i[4] == 7 && i[5] == 7, "flowin_dual: expected 15 ints, a 7x7 flow conv");
+  at::Tensor x = opt(t, 0), w = opt(t, 1), bias = opt(t, 2), y = opt(t, 3), flow = opt(t, 4), out = opt(t, 5),
+             slot = opt(t, 6), feat = opt(t, 7), wpk = opt(t, 8), cb = opt(t, 9);
+  const int N = (int)i[0], H = (int)i[1], W = (int)i[2], PH = (int)i[6], PW = (int)i[7], cout = (int)i[8];
+  const int relu = (int)i[9], y_coff = (int)i[10], mode = (int)i[11], fcoff = (int)i[14];
+  const int64_t stride = i[12], slot_off = i[13];
+  check_f32(flow, "flow32");
+  TORCH_CHECK(mode == 1 || mode == 2, "flowin_dual: mode 1 (bilinear) or 2 (convex head)");
+  TORCH_CHECK(flow.numel() >= (int64_t)N * H * W * 2, "flowin_dual: flow [M][2]");
+  TORCH_CHECK(!slot.defined() || (slot.is_cuda() && slot.scalar_type() == at::kLong && slot.numel() == 1),
+              "flowin_dual: out_slot must be one device int64");
+  const int64_t cap = check_flow_out(out, N, H, W);
+  TORCH_CHECK(stride >= 0 && stride % 8 == 0, "flowin_dual: iteration stride");
+  int fcs = 0;
+  if (mode == 2) {
+    check_bf16(feat, "feat"); check_bf16(wpk, "wpk"); check_f32(cb, "cbias");
+    fcs = cs(feat);
+    TORCH_CHECK(fcs % 8 == 0 && fcoff % 8 == 0 && fcoff >= 0 && fcoff + 256 <= fcs &&
+                    feat.numel() >= (int64_t)N * H * W * fcs && reinterpret_cast<uintptr_t>(feat.data_ptr()) % 16 == 0,
+                "flowin_dual: feat [M][cs], 16-byte aligned 256-channel slice");
+    TORCH_CHECK(wpk.numel() == 576 * 256 && cb.numel() == 576 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 32 == 0,
+                "flowin_dual: convex head operands");
+  }
+  if (keep) for (auto& v : {flow, out, slot, feat, wpk, cb}) if (v.defined()) keep->push_back(v);
+  const void* xp = x.data_ptr();
+  const void* wp = w.data_ptr();
+  const float* bp = bias.data_ptr<float>();
+  void* yp = y.data_ptr();
+  const int xcs = cs(x), ycs = cs(y);
+  const float* fp = flow.data_ptr<float>();
+  float* op = out.data_ptr<float>();
+  const void* sp = slot.defined() ? slot.data_ptr() : nullptr;
+  const void* featp = ptr(feat);
+  const void* wpkp = ptr(wpk);
+  const float* cbp = cb.defined() ? cb.data_ptr<float>() : nullptr;
+  const float a = (float)alpha;
+  const int64_t per_iter = mode == 1 ? (int64_t)N * 64 * H * W * 2 : (int64_t)N * H * W * 128;
+  return [=](hipStream_t s, int it) {
+    if (it == 0) return conv(s, it);
+    const int64_t off = stride * (it - 1);
+    if (off + per_iter > cap) return (int)hipErrorInvalidValue;
+    return jr_flowin_dual(xp, xcs, N, H, W, PH, PW, wp, bp, cout, relu, yp, ycs, y_coff, mode, featp, fcs, fcoff, wpkp,
+                          cbp, a, fp, op + off, sp, (long)(slot_off + off), s);
+  };
+}
+
 // ------------------------------------------------------------------ flow head
 // t = [fm, wt (bf16 [2][9][cin]), bias (fp32 [2]), coords, flow32, hx, qx?, flow8?]
 // i = [N, h, w, cin, fm_coff, hx_off, qx_off]
@@ -1400,6 +1453,7 @@ class Plan : public torch::CustomClassHolder {
   void add_gru_fused(TList t, IList i) { push(make_gru_fused(t, i, &keep_), "gru_fused"); }
   void add_conv1x1(TList t, IList i) { push(make_conv1x1(t, i, &keep_), "conv1x1"); }
   void add_conv_direct(TList t, IList i) { push(make_conv_direct(t, i, &keep_), "conv_direct"); }
+  void add_flowin_dual(TList t, IList i, double alpha) { push(make_flowin_dual(t, i, alpha, &keep_), "flowin_dual"); }
   void add_conv_train(TList t, IList i, double alpha, TList tx, IList ix) {
     push(make_conv(t, i, alpha, &keep_, &tx, &ix), "conv_train");
   }
@@ -1898,6 +1952,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_flow_taps", &jr::Plan::add_flow_taps)
       .def("add_taps_gemm", &jr::Plan::add_taps_gemm)
       .def("add_gru_fused", &jr::Plan::add_gru_fused)
+      .def("add_flowin_dual", &jr::Plan::add_flowin_dual)
       .def("add_conv1x1", &jr::Plan::add_conv1x1)
       .def("add_conv_direct", &jr::Plan::add_conv_direct)
       .def("add_conv_train", &jr::Plan::add_conv_train)

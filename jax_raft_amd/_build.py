@@ -43,9 +43,11 @@ KERNEL_SOURCES = [
     CSRC / "kernels" / "conv1x1.hip",
     CSRC / "kernels" / "gru_fused.hip",
     CSRC / "kernels" / "bgemm.hip",
+    CSRC / "kernels" / "merged.hip",
 ]
 HOST_SOURCES = [CSRC / "runtime" / "binding.cpp"]
-HEADERS = [CSRC / "kernels" / "common.h", CSRC / "kernels" / "kernels.h", CSRC / "kernels" / "conv_igemm.h"]
+HEADERS = [CSRC / "kernels" / "common.h", CSRC / "kernels" / "kernels.h", CSRC / "kernels" / "conv_igemm.h",
+           CSRC / "kernels" / "conv_direct.h", CSRC / "kernels" / "convex_head.h", CSRC / "kernels" / "upsample.h"]
 
 
 def _torch_paths():

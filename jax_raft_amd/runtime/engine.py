@@ -843,6 +843,12 @@ class RaftEngine:
         # stage), so the first stage can replace h in hx while the mask lane still runs
         hm = alloc("hm", (M, self.hidden)) if gru_f and lanes_on and self.has_mask else None
 
+        # one-lane schedule: the flow conv + the previous iteration's upsampling as one grid (merged.hip)
+        c1k = me.convflow1.layers_0.kernel
+        merged_up = (self._cf1_w is not None and tuple(c1k.shape[:2]) == (7, 7) and not self.cp
+                     and (not self.has_mask or (self._convex_w is not None and fm is not None))
+                     and os.environ.get("JR_MERGED_UP", "1") != "0")
+
         def flow_features():
             if self._cf1_w is not None:
                 c = me.convflow1.layers_0
@@ -978,10 +984,25 @@ class RaftEngine:
             plan.set_segment(1)
             lane(main)
             lookup(with_update=True)
-            flow_features()
-            plan.set_defer(1)
-            upsample(stride, mask_from_fm=fm is not None and self.has_mask)   # iteration i-1
-            plan.set_defer(0)
+            if merged_up:
+                # the 7x7 flow conv and iteration i-1's x8 upsampling in ONE grid (merged.hip):
+                # both read the flow the lookup just updated, and at batch 1 neither fills the GPU
+                c = me.convflow1.layers_0
+                kh, kw_, _, co = c.kernel.shape
+                ints = [B, h, w, 2, kh, kw_, c.padding[0], c.padding[1], co, 1, 0]
+                if self.has_mask:
+                    plan.add_flowin_dual([flow8, self._cf1_w, self._cf1_b, f1, flow32, out, st.out_slot, fm,
+                                          self._convex_w, self._convex_b],
+                                         ints + [2, stride, out_off, self.fh_hidden], m.mask_predictor.multiplier)
+                else:
+                    plan.add_flowin_dual([flow8, self._cf1_w, self._cf1_b, f1, flow32, out, st.out_slot],
+                                         ints + [1, stride, out_off, 0], 1.0)
+                self._conv(plan, sp["me.convflow2"], f1, B, h, w, cf, y_coff=cl[-1], act=ACT_RELU)
+            else:
+                flow_features()
+                plan.set_defer(1)
+                upsample(stride, mask_from_fm=fm is not None and self.has_mask)   # iteration i-1
+                plan.set_defer(0)
             motion_and_gru(wait_flow=False, wait_mask=False)
             flow_head()
             plan.set_segment(2)

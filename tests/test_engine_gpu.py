@@ -419,3 +419,23 @@ def test_engine_context_parallel_two_ranks(tmp_path):
             i1.cuda(), i2.cuda(), 3).cpu()
     assert (a["fp32"] - f32).abs().max().item() < 1e-3
     assert _epe(a["fp32"][-1], ref[-1]) < 1e-3 * (1 + mag)
+
+
+@pytest.mark.parametrize("factory", [raft_small, raft_large])
+def test_merged_flow_conv_upsample_is_bitwise(factory, monkeypatch):
+    """One-lane schedule: the 7x7 flow conv merged with the previous iteration's x8 upsampling
+    (merged.hip, one grid) returns bitwise the flows of the separate launches."""
+    import copy
+
+    model, _ = factory()
+    i1, i2 = _inputs(1, 128, 192, seed=79)
+    i1, i2 = i1.cuda(), i2.cuda()
+    m0 = copy.deepcopy(model).cuda()
+    m1 = copy.deepcopy(model).cuda()
+    monkeypatch.setenv("JR_MERGED_UP", "0")
+    a = m0(i1, i2, num_flow_updates=4, streams=False)
+    monkeypatch.setenv("JR_MERGED_UP", "1")
+    b = m1(i1, i2, num_flow_updates=4, streams=False)
+    c = m1(i1, i2, num_flow_updates=4, streams=False, use_graph=False)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and torch.equal(b, c)

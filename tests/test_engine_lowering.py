@@ -103,8 +103,10 @@ def test_fused_gru_not_for_raft_small(fake, monkeypatch):
     assert "gru_fused" not in p.names(1)
 
 
+@pytest.mark.parametrize("merged", ["1", "0"])
 @pytest.mark.parametrize("factory", [raft_large, raft_small])
-def test_one_lane_schedule(factory, fake):
+def test_one_lane_schedule(factory, fake, merged, monkeypatch):
+    monkeypatch.setenv("JR_MERGED_UP", merged)
     eng, p = _plan(factory, 1)
     assert not eng.uses_lanes(1)
     loop = [(ln, d, op) for s, ln, d, op, _ in p.ops if s == 1]
@@ -112,7 +114,13 @@ def test_one_lane_schedule(factory, fake):
     ops = [op for _, _, op in loop]
     assert ops[0] == "lookup" and "flow_taps" not in ops   # the update runs inside the lookup
     up = "convex_head" if factory is raft_large else "upsample_bilinear"
-    assert ops.count(up) == 1 and [d for _, d, op in loop if op == up] == [1]
+    if merged == "1":   # flow conv + the previous iteration's upsampling in one grid (merged.hip)
+        assert ops[1] == "flowin_dual" and up not in ops and "conv_direct" not in ops
+        assert all(d == 0 for _, d, _ in loop)
+        mode = [a for s, ln, d, op, a in p.ops if s == 1 and op == "flowin_dual"][0][1][11]
+        assert mode == (2 if factory is raft_large else 1)
+    else:
+        assert ops.count(up) == 1 and [d for _, d, op in loop if op == up] == [1]
     assert "taps_gemm" in ops   # raft_large: fused 128 -> 512 FlowHead/mask conv + taps GEMM
     assert p.names(2) == ["flow_taps", up]
 
