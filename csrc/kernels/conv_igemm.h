@@ -468,8 +468,10 @@ struct FastStage {
   }
 };
 
+// Body of kernels R / P for the block tile (bx_, by_) (the grid mapping is the caller's:
+// conv_igemm_kernel below, or the grouped launch conv_igemm_grouped).
 template <int BCO, int BP, int WCO, int EPI, bool FAST, int NW = 4, int PIPE = 0>  // PIPE 1: kernel P
-__global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(const ConvParams p) {
+JR_DEVICE void conv_igemm_body(const ConvParams& p, const int bx_, const int by_) {
   constexpr int WP = NW / WCO;
   constexpr int RP = NW * 8;              // staging rows covered by one pass of the block (8 lanes per row)
   constexpr int WTCO = BCO / WCO;
@@ -490,8 +492,6 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(const ConvParams p)
   const int wave = tid >> 6;
   const int wco = wave % WCO;
   const int wp = wave / WCO;
-  int bx_, by_;
-  tile_of_block(p, bx_, by_);
   const int p0 = bx_ * BP;
   const int co0 = by_ * BCO;
   const int ch = tid & 7;
@@ -740,6 +740,13 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(const ConvParams p)
   }
 }
 
+template <int BCO, int BP, int WCO, int EPI, bool FAST, int NW = 4, int PIPE = 0>
+__global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(const ConvParams p) {
+  int bx, by;
+  tile_of_block(p, bx, by);
+  conv_igemm_body<BCO, BP, WCO, EPI, FAST, NW, PIPE>(p, bx, by);
+}
+
 // ---------------------------------------------------------------------------
 // Kernel M32: as kernel R (register-staged operands, 64-deep K stages,
 // 2-stage prefetch) but on v_mfma_f32_32x32x16_bf16: half the MFMA
@@ -756,7 +763,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 JR_DEVICE int m32_arow(int t, int rho) { return 16 * (rho >> 3) + 4 * (2 * t + ((rho >> 2) & 1)) + (rho & 3); }
 
 template <int BCO, int BP, int WCO, int EPI, bool FAST, int NW = 4>
-__global__ __launch_bounds__(NW * 64) void conv_m32_kernel(const ConvParams p) {
+JR_DEVICE void conv_m32_body(const ConvParams& p, const int bx_, const int by_) {
   constexpr int WP = NW / WCO;
   constexpr int RP = NW * 8;   // staging rows per block pass
   constexpr int WTCO = BCO / WCO;
@@ -776,8 +783,6 @@ __global__ __launch_bounds__(NW * 64) void conv_m32_kernel(const ConvParams p) {
   const int wave = tid >> 6;
   const int wco = wave % WCO;
   const int wp = wave / WCO;
-  int bx_, by_;
-  tile_of_block(p, bx_, by_);
   const int p0 = bx_ * BP;
   const int co0 = by_ * BCO;
   const int ch = tid & 7;
@@ -953,6 +958,47 @@ __global__ __launch_bounds__(NW * 64) void conv_m32_kernel(const ConvParams p) {
       epi_pixel<16, EPI>(p, v, m, cbase);
     }
   }
+}
+
+template <int BCO, int BP, int WCO, int EPI, bool FAST, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void conv_m32_kernel(const ConvParams p) {
+  int bx, by;
+  tile_of_block(p, bx, by);
+  conv_m32_body<BCO, BP, WCO, EPI, FAST, NW>(p, bx, by);
+}
+
+// Grouped launch (one-lane schedule): two independent convs with the same tile config in ONE
+// grid -- blocks [0, n1) are p1's tiles, the rest p2's (each in dispatch order) -- so at batch 1
+// their small grids run side by side without a cross-stream graph edge (runtime/engine.py).
+template <int BCO, int BP, int WCO, bool FAST, int NW, bool M32>
+__global__ __launch_bounds__(NW * 64) void conv_grouped_kernel(const ConvParams p1, const ConvParams p2, int n1,
+                                                               int gx1, int gx2) {
+  const int id = blockIdx.x;
+  const bool first = id < n1;
+  const ConvParams& p = first ? p1 : p2;
+  const int t = first ? id : id - n1, gx = first ? gx1 : gx2;
+  const int by = t / gx, bx = t - by * gx;
+  if constexpr (M32) conv_m32_body<BCO, BP, WCO, EPI_STD, FAST, NW>(p, bx, by);
+  else conv_igemm_body<BCO, BP, WCO, EPI_STD, FAST, NW, 0>(p, bx, by);
+}
+
+template <int BCO, int BP, int WCO, int NW, bool M32>
+int launch_grouped(const ConvParams* p1, const ConvParams* p2, hipStream_t s) {
+  if (p1->fast != p2->fast) return (int)hipErrorInvalidValue;
+  auto grid_of = [](const ConvParams* p, int& gx) {
+    const int rows = (p->cout + 63) / 64 * 64;
+    gx = (p->M + BP - 1) / BP;
+    return gx * ((rows + BCO - 1) / BCO);
+  };
+  int gx1, gx2;
+  const int n1 = grid_of(p1, gx1), n2 = grid_of(p2, gx2);
+  if (p1->fast)
+    hipLaunchKernelGGL((conv_grouped_kernel<BCO, BP, WCO, true, NW, M32>), dim3(n1 + n2), dim3(NW * 64), 0, s, *p1,
+                       *p2, n1, gx1, gx2);
+  else
+    hipLaunchKernelGGL((conv_grouped_kernel<BCO, BP, WCO, false, NW, M32>), dim3(n1 + n2), dim3(NW * 64), 0, s, *p1,
+                       *p2, n1, gx1, gx2);
+  return (int)hipGetLastError();
 }
 
 // LDS-DMA helpers (kernel D2)

@@ -352,6 +352,9 @@ struct GruFusedParams {
   long long* dbg;                     // optional [ntiles][6] phase timestamps (s_memrealtime, tools/gru_phases.py)
 };
 int jr_gru_fused(const GruFusedParams* p, hipStream_t stream);
+// Grouped launch of two EPI_STD convs with one tile config (conv_fam_grp.hip); ok: the configs it serves.
+int jr_conv_grouped(const ConvParams* p1, const ConvParams* p2, int cfg, hipStream_t stream);
+int jr_conv_grouped_ok(int cfg);
 // Batched bf16 GEMM, fp32 accumulation (bgemm.hip): C[b] = alpha * op(A[b]) . B[b], B k-major [K][N],
 // A row-major [M][K] (a_kmajor 0) or k-major [K][M] (1); fp32 (C32) or bf16 (C16) output [M][ldc].
 // M, N multiples of 128, K of 64.

@@ -72,8 +72,8 @@ static int64_t check_flow_out(const at::Tensor& out, int B, int h, int w);
 
 static void conv_train_extras(ConvParams& p, int epi, const TList& tx, const IList& ix, std::vector<at::Tensor>* keep);
 
-static Launch make_conv(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep,
-                        const TList* tx = nullptr, const IList* ix = nullptr) {
+static ConvParams build_conv(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep,
+                             const TList* tx, const IList* ix, int* epi_out, int* cfg_out) {
   TORCH_CHECK(i.size() == 22 || i.size() == 26 || i.size() == 27, "conv: expected 22, 26 or 27 ints");
   at::Tensor x = opt(t, 0), w = opt(t, 1), bias = opt(t, 2), y = opt(t, 3), y2 = opt(t, 4), res = opt(t, 5);
   at::Tensor h32 = opt(t, 6), zbuf = opt(t, 7), coords = opt(t, 8), flow32 = opt(t, 9), y3 = opt(t, 10);
@@ -194,7 +194,29 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   TORCH_CHECK(cfg >= 0 && cfg <= 43 && !(cfg >= 29 && cfg <= 32), "conv: unknown tile config ", cfg);
   if (tx) conv_train_extras(p, epi, *tx, *ix, keep);
   if (keep) for (auto& v : {x, w, bias, y, y2, res, h32, zbuf, coords, flow32, y3, bmap, tapw}) if (v.defined()) keep->push_back(v);
+  *epi_out = epi;
+  *cfg_out = cfg;
+  return p;
+}
+
+static Launch make_conv(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep,
+                        const TList* tx = nullptr, const IList* ix = nullptr) {
+  int epi = 0, cfg = 0;
+  const ConvParams p = build_conv(t, i, alpha, keep, tx, ix, &epi, &cfg);
   return [p, epi, cfg](hipStream_t s, int) { return jr_conv_forward(&p, cfg, epi, s); };
+}
+
+// Two independent EPI_STD convs with the same tile config as ONE grid (conv_igemm.h:
+// conv_grouped_kernel; configs of conv_fam_grp.hip), e.g. the one-lane loop's convcorr2 +
+// convflow2 at batch 1.
+static Launch make_conv_group(const TList& t1, const IList& i1, double a1, const TList& t2, const IList& i2,
+                              double a2, std::vector<at::Tensor>* keep) {
+  int e1 = 0, c1 = 0, e2 = 0, c2 = 0;
+  const ConvParams p1 = build_conv(t1, i1, a1, keep, nullptr, nullptr, &e1, &c1);
+  const ConvParams p2 = build_conv(t2, i2, a2, keep, nullptr, nullptr, &e2, &c2);
+  TORCH_CHECK(e1 == EPI_STD && e2 == EPI_STD && c1 == c2 && p1.fast == p2.fast && jr_conv_grouped_ok(c1),
+              "conv_group: two STD-epilogue convs with the same grouped-launch tile config and loader");
+  return [p1, p2, c1](hipStream_t s, int) { return jr_conv_grouped(&p1, &p2, c1, s); };
 }
 
 // Training operands of a conv (op conv_train / Plan.add_conv_train):
@@ -1310,6 +1332,7 @@ void im2col_op(const TList& t, IList i) { run_now(make_im2col(t, i, nullptr)); }
 void flow_taps_op(const TList& t, IList i) { run_now(make_flow_taps(t, i, nullptr)); }
 void taps_gemm_op(const TList& t, IList i) { run_now(make_taps_gemm(t, i, nullptr)); }
 void gru_fused_op(const TList& t, IList i) { run_now(make_gru_fused(t, i, nullptr)); }
+bool conv_grouped_ok_op(int64_t cfg) { return jr_conv_grouped_ok((int)cfg) != 0; }
 
 // Batched GEMM (bgemm.hip).  t = [A (bf16 [batch][M][K] or [batch][K][M]), B (bf16 [batch][K][N]),
 // C (fp32 / bf16 [batch][M][N])], i = [M, N, K, a_kmajor]
@@ -1436,6 +1459,9 @@ class Plan : public torch::CustomClassHolder {
   void add_record(int64_t ev) { push_sync(OP_RECORD, ev, "record"); }
   void add_wait(int64_t ev) { push_sync(OP_WAIT, ev, "wait"); }
   void add_conv(TList t, IList i, double alpha) { push(make_conv(t, i, alpha, &keep_), "conv"); }
+  void add_conv_group(TList t1, IList i1, double a1, TList t2, IList i2, double a2) {
+    push(make_conv_group(t1, i1, a1, t2, i2, a2, &keep_), "conv_group");
+  }
   void add_corr(TList t, IList i, double scale) { push(make_corr(t, i, scale, &keep_), "corr"); }
   void add_lookup(TList t, IList i) { push(make_lookup(t, i, &keep_), "lookup"); }
   void add_upsample_convex(TList t, IList i) { push(make_upsample_convex(t, i, &keep_), "upsample_convex"); }
@@ -1898,6 +1924,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("taps_gemm(Tensor?[] t, int[] i) -> ()", &jr::taps_gemm_op);
   m.def("gru_fused(Tensor?[] t, int[] i) -> ()", &jr::gru_fused_op);
   m.def("bgemm(Tensor?[] t, int[] i, float alpha) -> ()", &jr::bgemm_op);
+  m.def("conv_grouped_ok(int cfg) -> bool", &jr::conv_grouped_ok_op);
   m.def("gru_fused_fits(int H, int W, int vertical) -> bool", &jr::gru_fused_fits);
   m.def("conv1x1(Tensor?[] t, int[] i) -> ()", &jr::conv1x1_op);
   m.def("conv_direct(Tensor?[] t, int[] i) -> ()", &jr::conv_direct_op);
@@ -1953,6 +1980,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_taps_gemm", &jr::Plan::add_taps_gemm)
       .def("add_gru_fused", &jr::Plan::add_gru_fused)
       .def("add_flowin_dual", &jr::Plan::add_flowin_dual)
+      .def("add_conv_group", &jr::Plan::add_conv_group)
       .def("add_conv1x1", &jr::Plan::add_conv1x1)
       .def("add_conv_direct", &jr::Plan::add_conv_direct)
       .def("add_conv_train", &jr::Plan::add_conv_train)

@@ -44,6 +44,7 @@ KERNEL_SOURCES = [
     CSRC / "kernels" / "gru_fused.hip",
     CSRC / "kernels" / "bgemm.hip",
     CSRC / "kernels" / "merged.hip",
+    CSRC / "kernels" / "conv_fam_grp.hip",
 ]
 HOST_SOURCES = [CSRC / "runtime" / "binding.cpp"]
 HEADERS = [CSRC / "kernels" / "common.h", CSRC / "kernels" / "kernels.h", CSRC / "kernels" / "conv_igemm.h",

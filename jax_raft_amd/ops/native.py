@@ -59,6 +59,10 @@ CFG_TILES.update({35: (256, 128), 36: (128, 128), 37: (128, 128), 38: (256, 128)
 TUNE_CFGS = (0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34,
              35, 38)
 NUM_CUS = 256
+# tile configs served by the grouped two-conv launch (csrc/kernels/conv_fam_grp.hip)
+GROUPED_CFGS = frozenset((2, 4, 5, 23, 24, 12, 14, 15))
+
+
 def gru_fused_tiles(N: int, H: int, W: int, vertical: int) -> int:
     """Workgroups of the fused ConvGRU stage (csrc/kernels/gru_fused.hip; mirrors
     binding.cpp:gru_fused_fits): image rows (1x5, W <= 128) or pairs / singles of

@@ -445,6 +445,31 @@ class RaftEngine:
     # ------------------------------------------------------------- autotune
     def _conv(self, plan, spec: ConvSpec, x, N, H, W, y, **kw):
         """Append one conv to ``plan``, choosing its tile config (autotuned)."""
+        plan.add_conv(*conv_args(spec, x, N, H, W, y, **self._conv_kw(spec, x, N, H, W, y, kw)))
+
+    def _conv_group(self, plan, a: tuple, b: tuple) -> bool:
+        """Two independent STD-epilogue convs ``(spec, x, N, H, W, y, kw)`` as ONE grid
+        (conv_igemm.h:conv_grouped_kernel) in the tile config tuned for the first, when a
+        grouped launch serves that config; returns False (nothing added) otherwise."""
+        kwa = self._conv_kw(*a[:6], a[6])
+        cfg = kwa.get("cfg")
+        def fast(sp):   # binding.cpp build_conv: the FAST im2col loader (both convs must share it)
+            taps = sp.kh * sp.kw
+            return taps <= 32 and (taps == 1 or sp.cin8 % 64 == 0)
+
+        if cfg not in nat.GROUPED_CFGS or fast(a[0]) != fast(b[0]):
+            return False
+        kwb = dict(b[6], cfg=cfg)
+        name = next((k for k, v in self._specs.items() if v is b[0]), None)
+        if name is not None:
+            self.chosen_cfgs[name] = cfg
+        ta, ia, aa = conv_args(*a[:6], **kwa)
+        tb, ib, ab = conv_args(*b[:6], **kwb)
+        plan.add_conv_group(ta, ia, aa, tb, ib, ab)
+        return True
+
+    def _conv_kw(self, spec: ConvSpec, x, N, H, W, y, kw):
+        """``kw`` with the tile config of this conv (override / persisted / autotuned)."""
         if self.cfg_override and kw.get("cfg") is None:
             name = next((k for k, v in self._specs.items() if v is spec), None)
             if name in self.cfg_override:
@@ -466,7 +491,7 @@ class RaftEngine:
         name = next((k for k, v in self._specs.items() if v is spec), None)
         if name is not None:
             self.chosen_cfgs[name] = kw.get("cfg")
-        plan.add_conv(*conv_args(spec, x, N, H, W, y, **kw))
+        return kw
 
     # ------------------------------------------------------------- lowering
     def _encoder(self, st: _PlanState, plan, tag: str, enc: FeatureEncoder, x: torch.Tensor, N: int, H: int,
@@ -901,16 +926,24 @@ class RaftEngine:
             plan.add_lookup([coords, corr] + levels + [None] * (4 - L) + upd,
                             [L, B, h, w, self.radius, h * w, blocked] + extra)
 
-        def motion_and_gru(wait_flow: bool, wait_mask: bool):
+        def motion_and_gru(wait_flow: bool, wait_mask: bool, flow2: bool = False):
+            """``flow2``: convflow2 (the flow branch's second conv) is added here, as one grid
+            with the last correlation conv when a grouped launch serves its tile config
+            (conv_grouped_kernel; JR_CONV_GROUP=0 keeps them separate launches)."""
             if len(cl) == 2:
                 if self._cc1_w is not None:   # LDS-resident-weight 1x1 kernel (conv1x1.hip)
                     plan.add_conv1x1([corr, self._cc1_w, self._cc1_b, c1],
                                      [M, self.corr_cs, self._cc1_kpad, cl[0], ACT_RELU, 0])
                 else:
                     self._conv(plan, sp["me.convcorr1"], corr, B, h, w, c1, act=ACT_RELU)
-                self._conv(plan, sp["me.convcorr2"], c1, B, h, w, cf, act=ACT_RELU)
+                last = (sp["me.convcorr2"], c1, B, h, w, cf, dict(act=ACT_RELU))
             else:
-                self._conv(plan, sp["me.convcorr1"], corr, B, h, w, cf, act=ACT_RELU)
+                last = (sp["me.convcorr1"], corr, B, h, w, cf, dict(act=ACT_RELU))
+            fl2 = (sp["me.convflow2"], f1, B, h, w, cf, dict(y_coff=cl[-1], act=ACT_RELU))
+            if not (flow2 and os.environ.get("JR_CONV_GROUP", "1") != "0" and self._conv_group(plan, last, fl2)):
+                if flow2:
+                    self._conv(plan, *fl2[:6], **fl2[6])
+                self._conv(plan, *last[:6], **last[6])
             if wait_flow:
                 plan.add_wait(E_FLOW)
             self._conv(plan, sp["me.conv"], cf, B, h, w, hx, y_coff=self.mot_off, act=ACT_RELU, y2=qx,
@@ -997,13 +1030,12 @@ class RaftEngine:
                 else:
                     plan.add_flowin_dual([flow8, self._cf1_w, self._cf1_b, f1, flow32, out, st.out_slot],
                                          ints + [1, stride, out_off, 0], 1.0)
-                self._conv(plan, sp["me.convflow2"], f1, B, h, w, cf, y_coff=cl[-1], act=ACT_RELU)
             else:
                 flow_features()
                 plan.set_defer(1)
                 upsample(stride, mask_from_fm=fm is not None and self.has_mask)   # iteration i-1
                 plan.set_defer(0)
-            motion_and_gru(wait_flow=False, wait_mask=False)
+            motion_and_gru(wait_flow=False, wait_mask=False, flow2=merged_up)
             flow_head()
             plan.set_segment(2)
             flow_update()

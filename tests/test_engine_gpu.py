@@ -432,6 +432,7 @@ def test_merged_flow_conv_upsample_is_bitwise(factory, monkeypatch):
     i1, i2 = i1.cuda(), i2.cuda()
     m0 = copy.deepcopy(model).cuda()
     m1 = copy.deepcopy(model).cuda()
+    monkeypatch.setenv("JR_CONV_GROUP", "0")
     monkeypatch.setenv("JR_MERGED_UP", "0")
     a = m0(i1, i2, num_flow_updates=4, streams=False)
     monkeypatch.setenv("JR_MERGED_UP", "1")
@@ -439,3 +440,25 @@ def test_merged_flow_conv_upsample_is_bitwise(factory, monkeypatch):
     c = m1(i1, i2, num_flow_updates=4, streams=False, use_graph=False)
     torch.cuda.synchronize()
     assert torch.equal(a, b) and torch.equal(b, c)
+
+
+@pytest.mark.parametrize("factory,cfg", [(raft_large, 2), (raft_large, 12), (raft_small, 4), (raft_small, 15)])
+def test_grouped_corr_flow_conv_is_bitwise(factory, cfg, monkeypatch):
+    """One-lane schedule: the last correlation conv and convflow2 as one grid
+    (conv_igemm.h:conv_grouped_kernel) return bitwise the flows of the two launches in
+    the same tile config."""
+    import copy
+
+    last = "me.convcorr2" if factory is raft_large else "me.convcorr1"
+    monkeypatch.setenv("JR_CFG_OVERRIDE", f"{last}={cfg},me.convflow2={cfg}")
+    model, _ = factory()
+    i1, i2 = _inputs(1, 128, 192, seed=83)
+    i1, i2 = i1.cuda(), i2.cuda()
+    m0 = copy.deepcopy(model).cuda()
+    m1 = copy.deepcopy(model).cuda()
+    monkeypatch.setenv("JR_CONV_GROUP", "0")
+    a = m0(i1, i2, num_flow_updates=4, streams=False)
+    monkeypatch.setenv("JR_CONV_GROUP", "1")
+    b = m1(i1, i2, num_flow_updates=4, streams=False)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)

@@ -125,6 +125,28 @@ def test_one_lane_schedule(factory, fake, merged, monkeypatch):
     assert p.names(2) == ["flow_taps", up]
 
 
+@pytest.mark.parametrize("group", ["1", "0"])
+@pytest.mark.parametrize("factory", [raft_large, raft_small])
+def test_one_lane_grouped_corr_flow_conv(factory, fake, group, monkeypatch):
+    """One-lane schedule: the last correlation conv and convflow2 as one grid in the corr
+    conv's tile config (when a grouped launch serves it)."""
+    monkeypatch.setenv("JR_CONV_GROUP", group)
+    last = "me.convcorr2" if factory is raft_large else "me.convcorr1"
+    model = factory()[0].eval()
+    eng = E.RaftEngine(model, "cpu", autotune=False, cfg_override={last: 2})
+    p = eng._build(1, 128, 256, 3, True).plan
+    ops = p.names(1)
+    if group == "1":
+        g = [a for s, ln, d, op, a in p.ops if s == 1 and op == "conv_group"]
+        assert len(g) == 1 and ops.index("conv_group") > ops.index("flowin_dual")
+        t1, i1, _, t2, i2, _ = g[0]
+        assert t1[3] is t2[3] and eng.chosen_cfgs["me.convflow2"] == 2   # both write cf; one config
+    else:
+        assert "conv_group" not in ops
+    eng2 = E.RaftEngine(model, "cpu", autotune=False, cfg_override={last: 99})
+    assert "conv_group" not in eng2._build(1, 128, 256, 3, True).plan.names(1)   # no grouped variant
+
+
 @pytest.mark.parametrize("factory", [raft_large, raft_small])
 def test_final_only_schedule(factory, fake):
     eng, p = _plan(factory, 4, all_iters=False)
