@@ -37,13 +37,13 @@
 namespace {
 
 
-// one block (id) -- kernel body shared with the merged launches of merged.hip
+// one block (id) -- kernel body shared with the merged launches of merged.hip; sA: the caller's LDS
 template <int NC>  // pixel column tiles of 16 per wave (1 or 2)
 JR_DEVICE void convex_head_block(const bf16* __restrict__ feat, int fcs, int fcoff, const u32x4* __restrict__ wpk,
                                  const float* __restrict__ bias, float alpha, const float* __restrict__ flow, int B,
                                  int h, int w, float* __restrict__ out, const long long* __restrict__ out_slot,
-                                 long out_off, int nblk, int id) {
-  __shared__ u32x4 sA[8 * 9 * 64];  // this group's A fragments: [ks][tap][lane]
+                                 long out_off, int nblk, int id, u32x4* __restrict__ sA) {
+  // sA: 8 * 9 * 64 LDS entries for this group's A fragments ([ks][tap][lane])
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int g = (id >> 3) & 3, pb = (id >> 5) * 8 + (id & 7);
   if (pb >= nblk) return;  // whole block, before any barrier
@@ -142,6 +142,8 @@ __global__ __launch_bounds__(256, 2) void convex_head_kernel(const bf16* __restr
                                                              const float* __restrict__ flow, int B, int h, int w,
                                                              float* __restrict__ out, const long long* __restrict__ out_slot,
                                                              long out_off, int nblk) {
-  convex_head_block<NC>(feat, fcs, fcoff, wpk, bias, alpha, flow, B, h, w, out, out_slot, out_off, nblk, blockIdx.x);
+  __shared__ u32x4 sA[8 * 9 * 64];
+  convex_head_block<NC>(feat, fcs, fcoff, wpk, bias, alpha, flow, B, h, w, out, out_slot, out_off, nblk, blockIdx.x,
+                        sA);
 }
 }  // namespace

@@ -275,12 +275,19 @@ int jr_flow_taps(const float* t, int tcs, const float* bias, int N, int h, int w
 // MFMA A fragments [cout/16][NKC][64 lanes][8] (jax_raft_amd/ops/native.py:
 // pack_direct_weight); bias fp32 [cout]; y bf16 channels [y_coff, y_coff +
 // cout) of [N*H*W][y_cstride].  (KH, KW) in {(7, 7), (3, 3)}, cout % 32 == 0.
+// Operands of jr_conv1x1_lds as one struct (the optional third part of jr_flowin_dual).
+struct Conv1x1Args {
+  const void* x; int xcs, kvalid, kpad; const void* wpk; const float* bias; int act;
+  void* y; int ycs, ycoff, cout, M;
+};
 // The 7x7 flow conv of jr_conv_direct merged with the x8 upsampling of the previous iteration in one grid
-// (merged.hip): mode 1 = bilinear (flow -> out), mode 2 = the convex mask head (jr_convex_head operands).
+// (merged.hip): mode 1 = bilinear (flow -> out), mode 2 = the convex mask head (jr_convex_head operands;
+// out == nullptr: no upsampling part).  c1 (mode 2, kpad 352): jr_conv1x1_lds in the same grid.
 int jr_flowin_dual(const void* x, int x_cstride, int N, int H, int W, int PH, int PW, const void* w,
                    const float* fbias, int cout, int relu, void* y, int y_cstride, int y_coff, int mode,
                    const void* feat, int feat_cstride, int feat_coff, const void* wpk, const float* cbias, float alpha,
-                   const float* flow, float* out, const void* out_slot, long out_off, hipStream_t stream);
+                   const float* flow, float* out, const void* out_slot, long out_off, const Conv1x1Args* c1,
+                   hipStream_t stream);
 int jr_conv_direct(const void* x, int x_cstride, int N, int H, int W, int cin, int KH, int KW, int PH, int PW,
                    const void* w, const float* bias, int cout, int relu, void* y, int y_cstride, int y_coff,
                    hipStream_t stream);

@@ -611,9 +611,25 @@ static Launch make_conv_direct(const TList& t, const IList& i, std::vector<at::T
 // i = [N, H, W, 2, 7, 7, PH, PW, cout, relu, y_coff, mode (1 bilinear / 2 convex head), out_iter_stride,
 // out_slot_off, feat_coff].  Iteration 0 runs the flow conv alone (nothing to upsample yet); iteration
 // it > 0 upsamples iteration it - 1, as a deferred op would.
+// t = [x, w, bias, y, flow32, out, out_slot, feat?, wpk?, cbias?,  (c1x, c1w, c1b, c1y)?]
+// i = [conv_direct's 11 ints, mode, stride, slot_off, feat_coff,  (M, kvalid, kpad, cout, act, ycoff)?]
+// With the conv1x1 operands (mode 2): the correlation features' 1x1 conv runs in the same grid,
+// every iteration (iteration 0: with the flow conv alone).
 static Launch make_flowin_dual(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep) {
   Launch conv = make_conv_direct(t, IList(i.begin(), i.begin() + 11), keep);
-  TORCH_CHECK(i.size() == 15 && i[4] == 7 && i[5] == 7, "flowin_dual: expected 15 ints, a 7x7 flow conv");
+  TORCH_CHECK((i.size() == 15 || i.size() == 21) && i[4] == 7 && i[5] == 7,
+              "flowin_dual: expected 15 (+6) ints, a 7x7 flow conv");
+  const bool has_c1 = i.size() == 21;
+  Conv1x1Args c1a{};
+  if (has_c1) {
+    TORCH_CHECK(i[11] == 2 && i[17] == 352, "flowin_dual: the 1x1 conv part needs mode 2 and K padded to 352");
+    TList t1;
+    for (size_t k = 10; k < 14; ++k) t1.push_back(c10::optional<at::Tensor>(opt(t, k)));
+    (void)make_conv1x1(t1, IList(i.begin() + 15, i.end()), keep);   // validates (and keeps) the operands
+    at::Tensor x1 = opt(t, 10), w1 = opt(t, 11), b1 = opt(t, 12), y1 = opt(t, 13);
+    c1a = Conv1x1Args{x1.data_ptr(), (int)cs(x1), (int)i[16], (int)i[17], w1.data_ptr(), b1.data_ptr<float>(),
+                      (int)i[19], y1.data_ptr(), (int)cs(y1), (int)i[20], (int)i[18], (int)i[15]};
+  }
   at::Tensor x = opt(t, 0), w = opt(t, 1), bias = opt(t, 2), y = opt(t, 3), flow = opt(t, 4), out = opt(t, 5),
              slot = opt(t, 6), feat = opt(t, 7), wpk = opt(t, 8), cb = opt(t, 9);
   const int N = (int)i[0], H = (int)i[1], W = (int)i[2], PH = (int)i[6], PW = (int)i[7], cout = (int)i[8];
@@ -651,11 +667,14 @@ static Launch make_flowin_dual(const TList& t, const IList& i, double alpha, std
   const float a = (float)alpha;
   const int64_t per_iter = mode == 1 ? (int64_t)N * 64 * H * W * 2 : (int64_t)N * H * W * 128;
   return [=](hipStream_t s, int it) {
-    if (it == 0) return conv(s, it);
+    if (it == 0 && !has_c1) return conv(s, it);
+    if (it == 0)
+      return jr_flowin_dual(xp, xcs, N, H, W, PH, PW, wp, bp, cout, relu, yp, ycs, y_coff, mode, featp, fcs, fcoff,
+                            wpkp, cbp, a, fp, nullptr, nullptr, 0, &c1a, s);
     const int64_t off = stride * (it - 1);
     if (off + per_iter > cap) return (int)hipErrorInvalidValue;
     return jr_flowin_dual(xp, xcs, N, H, W, PH, PW, wp, bp, cout, relu, yp, ycs, y_coff, mode, featp, fcs, fcoff, wpkp,
-                          cbp, a, fp, op + off, sp, (long)(slot_off + off), s);
+                          cbp, a, fp, op + off, sp, (long)(slot_off + off), has_c1 ? &c1a : nullptr, s);
   };
 }
 

@@ -926,12 +926,18 @@ class RaftEngine:
             plan.add_lookup([coords, corr] + levels + [None] * (4 - L) + upd,
                             [L, B, h, w, self.radius, h * w, blocked] + extra)
 
+        # the one-lane merged grid also runs convcorr1 (1x1, K 324 -> 352; merged.hip); JR_MERGED_C1=0: own launch
+        c1_merged = (merged_up and self.has_mask and len(cl) == 2 and self._cc1_w is not None
+                     and self._cc1_kpad == 352 and os.environ.get("JR_MERGED_C1", "1") != "0")
+
         def motion_and_gru(wait_flow: bool, wait_mask: bool, flow2: bool = False):
             """``flow2``: convflow2 (the flow branch's second conv) is added here, as one grid
             with the last correlation conv when a grouped launch serves its tile config
             (conv_grouped_kernel; JR_CONV_GROUP=0 keeps them separate launches)."""
             if len(cl) == 2:
-                if self._cc1_w is not None:   # LDS-resident-weight 1x1 kernel (conv1x1.hip)
+                if flow2 and c1_merged:
+                    pass                      # ran in the flow conv's merged grid
+                elif self._cc1_w is not None:   # LDS-resident-weight 1x1 kernel (conv1x1.hip)
                     plan.add_conv1x1([corr, self._cc1_w, self._cc1_b, c1],
                                      [M, self.corr_cs, self._cc1_kpad, cl[0], ACT_RELU, 0])
                 else:
@@ -1024,9 +1030,13 @@ class RaftEngine:
                 kh, kw_, _, co = c.kernel.shape
                 ints = [B, h, w, 2, kh, kw_, c.padding[0], c.padding[1], co, 1, 0]
                 if self.has_mask:
-                    plan.add_flowin_dual([flow8, self._cf1_w, self._cf1_b, f1, flow32, out, st.out_slot, fm,
-                                          self._convex_w, self._convex_b],
-                                         ints + [2, stride, out_off, self.fh_hidden], m.mask_predictor.multiplier)
+                    t_ = [flow8, self._cf1_w, self._cf1_b, f1, flow32, out, st.out_slot, fm, self._convex_w,
+                          self._convex_b]
+                    i_ = ints + [2, stride, out_off, self.fh_hidden]
+                    if c1_merged:   # + convcorr1 (LDS-weight 1x1 kernel) in the same grid
+                        t_ += [corr, self._cc1_w, self._cc1_b, c1]
+                        i_ += [M, self.corr_cs, self._cc1_kpad, cl[0], ACT_RELU, 0]
+                    plan.add_flowin_dual(t_, i_, m.mask_predictor.multiplier)
                 else:
                     plan.add_flowin_dual([flow8, self._cf1_w, self._cf1_b, f1, flow32, out, st.out_slot],
                                          ints + [1, stride, out_off, 0], 1.0)

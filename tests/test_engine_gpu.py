@@ -424,7 +424,8 @@ def test_engine_context_parallel_two_ranks(tmp_path):
 @pytest.mark.parametrize("factory", [raft_small, raft_large])
 def test_merged_flow_conv_upsample_is_bitwise(factory, monkeypatch):
     """One-lane schedule: the 7x7 flow conv merged with the previous iteration's x8 upsampling
-    (merged.hip, one grid) returns bitwise the flows of the separate launches."""
+    (merged.hip, one grid; raft_large: + convcorr1's 1x1 conv) returns bitwise the flows of the
+    separate launches."""
     import copy
 
     model, _ = factory()

@@ -117,10 +117,13 @@ def test_one_lane_schedule(factory, fake, merged, monkeypatch):
     if merged == "1":   # flow conv + the previous iteration's upsampling in one grid (merged.hip)
         assert ops[1] == "flowin_dual" and up not in ops and "conv_direct" not in ops
         assert all(d == 0 for _, d, _ in loop)
-        mode = [a for s, ln, d, op, a in p.ops if s == 1 and op == "flowin_dual"][0][1][11]
-        assert mode == (2 if factory is raft_large else 1)
+        ints = [a for s, ln, d, op, a in p.ops if s == 1 and op == "flowin_dual"][0][1]
+        assert ints[11] == (2 if factory is raft_large else 1)
+        # raft_large: convcorr1 (the 1x1 LDS-weight conv) runs in the same merged grid
+        assert (len(ints) == 21 and "conv1x1" not in ops) if factory is raft_large else len(ints) == 15
     else:
         assert ops.count(up) == 1 and [d for _, d, op in loop if op == up] == [1]
+        assert ("conv1x1" in ops) == (factory is raft_large)
     assert "taps_gemm" in ops   # raft_large: fused 128 -> 512 FlowHead/mask conv + taps GEMM
     assert p.names(2) == ["flow_taps", up]
 
