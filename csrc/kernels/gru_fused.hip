@@ -325,7 +325,9 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int c0 = G2ALL ? 32 * wco + 16 * hh : wco * 64 + 32 * t + 16 * hh;
-    pre_map(bm2[t], 2 * HD + c0);
+    // 8-wave GEMM 2: waves wco >= 2 (c0 >= HD) have no epilogue 2 -- keep their (unused) load
+    // inside the map row: q channels 2 HD + c0 + 16 would pass the row's end (384)
+    pre_map(bm2[t], 2 * HD + (c0 < HD ? c0 : 0));
     if constexpr (G2ALL) {
       const f32x4* hq = (const f32x4*)(p.h32 + (long)mld * HD + c0);
 #pragma unroll
