@@ -969,7 +969,9 @@ __global__ __launch_bounds__(NW * 64) void conv_m32_kernel(const ConvParams p) {
 
 // Grouped launch (one-lane schedule): two independent convs with the same tile config in ONE
 // grid -- blocks [0, n1) are p1's tiles, the rest p2's (each in dispatch order) -- so at batch 1
-// their small grids run side by side without a cross-stream graph edge (runtime/engine.py).
+// their small grids run side by side without a cross-stream graph edge (runtime/engine.py:
+// _conv_group).  Used for the MotionEncoder's last correlation conv and its second flow conv
+// (reference jax_raft/model.py:279 / 285: independent branches until the concat at :287).
 template <int BCO, int BP, int WCO, bool FAST, int NW, bool M32>
 __global__ __launch_bounds__(NW * 64) void conv_grouped_kernel(const ConvParams p1, const ConvParams p2, int n1,
                                                                int gx1, int gx2) {
