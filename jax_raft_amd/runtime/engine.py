@@ -453,6 +453,19 @@ class RaftEngine:
         grouped launch serves that config; returns False (nothing added) otherwise."""
         kwa = self._conv_kw(*a[:6], a[6])
         cfg = kwa.get("cfg")
+        if a[6].get("cfg") is None and self.autotune:
+            # a measured config for the PAIR (tuned DB key "group" + both problems) beats the
+            # first conv's own: profiles/r3_grouped_cfg_ab.txt
+            (sa, xa, N, H, W, _), (sb, xb) = a[:6], b[:2]
+            gkey = ("group", N * H * W, sa.cout, sa.kh, sa.kw, sa.cin8, xa.shape[-1], sb.cout, sb.kh, sb.kw, sb.cin8,
+                    xb.shape[-1])
+            gcfg = tunedb.peek(self.arch, gkey)
+            name_a = next((k for k, v in self._specs.items() if v is sa), None)
+            if gcfg in nat.GROUPED_CFGS and name_a not in self.cfg_override:
+                cfg = gcfg
+                kwa = dict(kwa, cfg=cfg)
+                if name_a is not None:
+                    self.chosen_cfgs[name_a] = cfg
         def fast(sp):   # binding.cpp build_conv: the FAST im2col loader (both convs must share it)
             taps = sp.kh * sp.kw
             return taps <= 32 and (taps == 1 or sp.cin8 % 64 == 0)

@@ -65,6 +65,12 @@ def lookup(arch: str, key) -> Optional[int]:
     return cfg
 
 
+def peek(arch: str, key) -> Optional[int]:
+    """A persisted decision without counting a hit / miss (optional entries, e.g. the
+    tile config of a grouped two-conv launch, runtime/engine.py:_conv_group)."""
+    return _table(arch).get(_key(key))
+
+
 def record(arch: str, key, cfg: int) -> None:
     _table(arch)[_key(key)] = int(cfg)
 

@@ -185,3 +185,26 @@ def test_context_parallel_schedule(factory, fake):
     assert all(d == 0 for s, _, d, _, _ in p.ops)
     # one slab of every query row without a process group
     assert st.cp["slabs"] == [(0, 16)]
+
+
+def test_grouped_launch_uses_the_pair_config(fake, monkeypatch):
+    """A persisted decision for the PAIR (tuned DB key "group" + both problems) overrides the
+    first conv's own tile config in the grouped launch; without one the first conv's stays."""
+    model = raft_large()[0].eval()
+    seen = []
+
+    def peek(arch, key):
+        seen.append(key)
+        return 24 if key[0] == "group" else None
+
+    monkeypatch.setattr(tunedb, "peek", peek)
+    eng = E.RaftEngine(model, "cpu", autotune=True)
+    monkeypatch.setattr(eng, "_conv_kw", lambda spec, x, N, H, W, y, kw: dict(kw, cfg=23))
+    p = eng._build(1, 128, 256, 3, True).plan
+    g = [a for s, ln, d, op, a in p.ops if s == 1 and op == "conv_group"]
+    assert len(g) == 1 and g[0][1][20] == 24 and g[0][4][20] == 24       # ints[20] = cfg
+    assert seen and seen[0][:2] == ("group", 16 * 32)
+    monkeypatch.setattr(tunedb, "peek", lambda arch, key: None)
+    p = eng._build(1, 128, 256, 3, True).plan
+    g = [a for s, ln, d, op, a in p.ops if s == 1 and op == "conv_group"]
+    assert g[0][1][20] == 23 and g[0][4][20] == 23
