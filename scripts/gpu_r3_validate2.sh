@@ -2,7 +2,7 @@
 # Full GPU suite, smoke, headline bench with extras and its kernel trace (after the fused ConvGRU).
 set -o pipefail
 export TMPDIR=/tmp
-o=gpurun_out/r3v3
+o=gpurun_out/r3v4
 mkdir -p $o
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $o/gputests.log 2>&1 || { tail -30 $o/gputests.log; exit 1; }
 tail -1 $o/gputests.log
