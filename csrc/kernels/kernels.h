@@ -359,6 +359,32 @@ struct GruFusedParams {
   long long* dbg;                     // optional [ntiles][6] phase timestamps (s_memrealtime, tools/gru_phases.py)
 };
 int jr_gru_fused(const GruFusedParams* p, hipStream_t stream);
+
+// Halo-tiled fused ConvGRU stage (gru_halo.hip) for ANY /8 map size and both RAFT
+// recurrent blocks: raft_large's 1x5 / 5x1 stages (mode 0: a run of L pixels along the
+// tap axis, hd 128, cin 256) and raft_small's 3x3 GRU (mode 1: a TR x TC block, hd 96,
+// cin 192).  Each workgroup recomputes z / r on its tile's halo (+-2 / +-1 pixels) so
+// r*h never leaves the CU; the weights stream from L2 straight into MFMA A registers.
+// Reads [h | x] from hsrc (channels [0, hd)) and xsrc (channels [hd, cin)) and writes h'
+// to y (a DIFFERENT buffer than hsrc: neighbouring tiles read h of this tile's pixels).
+struct GruHaloParams {
+  const void* hsrc; const void* xsrc; int cs;   // bf16 [M][cs] loop buffers ([h | motion | flow | pad])
+  const void* wa; const void* wb;     // ops/native.py:pack_gru_halo of [z | r] and q: [cout/32][taps*cin/16][64][8]
+  const void* bmap; int bmap_cs;      // bf16 [M][bmap_cs]: [z | r | q] context share + gate biases
+  float* h32;                         // fp32 hidden state [M][hd], updated in place (own pixels only)
+  void* y; int y_cs;                  // bf16 h' -> channels [0, hd)
+  void* y2; int y2_cs;                // optional second bf16 copy of h'
+  int N, H, W;
+  int mode;                           // 0: 5-tap run (1x5 / 5x1), 1: 3x3 block
+  int axis;                           // mode 0: 0 = taps along W (1x5), 1 = along H (5x1)
+  int TR, TC;                         // output tile: mode 0 TR = 1, TC = run length L; mode 1 TR x TC
+  int tiles_y, tiles_x, ntiles;       // tiles per image = tiles_y * tiles_x (mode 0: lines x segments)
+  int nb1, nb2;                       // 32-pixel blocks of the halo region (GEMM 1) / the output tile
+  long src_bytes, wa_bytes, wb_bytes;
+};
+int jr_gru_halo(const GruHaloParams* p, hipStream_t stream);
+// LDS bytes of one workgroup (0: the configuration is not supported)
+int jr_gru_halo_lds(int hd, int mode, int TR, int TC, int nb1, int nb2);
 // Grouped launch of two EPI_STD convs with one tile config (conv_fam_grp.hip); ok: the configs it serves.
 int jr_conv_grouped(const ConvParams* p1, const ConvParams* p2, int cfg, hipStream_t stream);
 int jr_conv_grouped_ok(int cfg);

@@ -206,6 +206,21 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
   return [p, epi, cfg](hipStream_t s, int) { return jr_conv_forward(&p, cfg, epi, s); };
 }
 
+// A conv whose input on ODD loop iterations is x_alt (same shape as x): the reader of a state
+// that ping-pongs between two buffers (raft_small's FlowHead after the single-stage halo GRU).
+static Launch make_conv_alt(const TList& t, const IList& i, double alpha, const at::Tensor& x_alt,
+                            std::vector<at::Tensor>* keep) {
+  int epi = 0, cfg = 0;
+  const ConvParams p = build_conv(t, i, alpha, keep, nullptr, nullptr, &epi, &cfg);
+  const at::Tensor x = opt(t, 0);
+  check_bf16(x_alt, "x_alt");
+  TORCH_CHECK(x_alt.sizes() == x.sizes(), "conv_alt: x_alt must have x's shape");
+  ConvParams q = p;
+  q.x = x_alt.data_ptr();
+  if (keep) keep->push_back(x_alt);
+  return [p, q, epi, cfg](hipStream_t s, int it) { return jr_conv_forward((it & 1) ? &q : &p, cfg, epi, s); };
+}
+
 // Two independent EPI_STD convs with the same tile config as ONE grid (conv_igemm.h:
 // conv_grouped_kernel; configs of conv_fam_grp.hip), e.g. the one-lane loop's convcorr2 +
 // convflow2 at batch 1.
@@ -555,6 +570,90 @@ static Launch make_gru_fused(const TList& t, const IList& i, std::vector<at::Ten
   TORCH_CHECK(p.hx_bytes < (1LL << 31), "gru_fused: hx larger than 2 GiB");
   if (keep) for (auto& v : {hx, wa, wb, bmap, h32, y, y2}) if (v.defined()) keep->push_back(v);
   return [p](hipStream_t s, int) { return jr_gru_fused(&p, s); };
+}
+
+// Halo-tiled fused ConvGRU stage (gru_halo.hip).
+// t = [hsrc (bf16 [M][cs]: h = channels [0, hd)), xsrc (bf16 [M][cs]: x = [hd, cs)), wa, wb
+//      (ops/native.py:pack_gru_halo of [z | r] / q), bmap (bf16 [M][>= 3 hd]), h32 (fp32 [M][hd],
+//      in place), y (bf16 [M][ycs], h' -> channels [0, hd)), y2?],
+// i = [N, H, W, mode, axis, TR, TC, nb1, nb2].  cs = 2 hd (hd 128: mode 0 = a 5-tap run, TR = 1,
+// TC = run length; hd 96: mode 1 = a TR x TC block of the 3x3 GRU).
+bool gru_halo_geom_ok(int64_t hd, int64_t mode, int64_t TR, int64_t TC, int64_t nb1, int64_t nb2) {
+  if (TR < 1 || TC < 1) return false;
+  const int64_t nreg = mode == 0 ? TC + 4 : (TR + 2) * (TC + 2);
+  const int64_t nout = TR * TC;
+  if ((mode == 0 && (TR != 1 || hd != 128)) || (mode == 1 && hd != 96) || mode < 0 || mode > 1) return false;
+  if (nreg > 32 * nb1 || nout > 32 * nb2) return false;
+  return jr_gru_halo_lds((int)hd, (int)mode, (int)TR, (int)TC, (int)nb1, (int)nb2) > 0 &&
+         jr_gru_halo_lds((int)hd, (int)mode, (int)TR, (int)TC, (int)nb1, (int)nb2) <= 160 * 1024;
+}
+
+static Launch make_gru_halo(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor hs = opt(t, 0), xs = opt(t, 1), wa = opt(t, 2), wb = opt(t, 3), bmap = opt(t, 4), h32 = opt(t, 5),
+             y = opt(t, 6), y2 = opt(t, 7);
+  check_bf16(hs, "hsrc"); check_bf16(xs, "xsrc"); check_bf16(wa, "wa"); check_bf16(wb, "wb"); check_bf16(bmap, "bmap");
+  check_f32(h32, "h32"); check_bf16(y, "y");
+  TORCH_CHECK(i.size() == 9, "gru_halo: expected [N, H, W, mode, axis, TR, TC, nb1, nb2]");
+  GruHaloParams p{};
+  p.N = (int)i[0]; p.H = (int)i[1]; p.W = (int)i[2]; p.mode = (int)i[3]; p.axis = (int)i[4];
+  p.TR = (int)i[5]; p.TC = (int)i[6]; p.nb1 = (int)i[7]; p.nb2 = (int)i[8];
+  const int64_t M = (int64_t)p.N * p.H * p.W;
+  const int cs_ = cs(hs), hd = cs_ / 2;
+  const int taps = p.mode == 0 ? 5 : 9;
+  TORCH_CHECK(p.N >= 1 && p.H >= 1 && p.W >= 1 && M < (1LL << 31), "gru_halo: map size");
+  TORCH_CHECK(gru_halo_geom_ok(hd, p.mode, p.TR, p.TC, p.nb1, p.nb2), "gru_halo: unsupported tile (hd ", hd, ", mode ",
+              p.mode, ", ", p.TR, "x", p.TC, ", blocks ", p.nb1, "/", p.nb2, ")");
+  TORCH_CHECK(p.mode == 1 || p.axis == 0 || p.axis == 1, "gru_halo: axis must be 0 (1x5) or 1 (5x1)");
+  TORCH_CHECK(cs(xs) == cs_ && hs.numel() >= M * cs_ && xs.numel() >= M * cs_ && hs.numel() == xs.numel(),
+              "gru_halo: hsrc / xsrc must be [M][2 hd] with one shape");
+  TORCH_CHECK(hs.data_ptr() != y.data_ptr(), "gru_halo: y must not alias hsrc (neighbouring tiles read h)");
+  TORCH_CHECK(wa.numel() == (int64_t)2 * hd * taps * cs_ && wb.numel() == (int64_t)hd * taps * cs_,
+              "gru_halo: packed weights (pack_gru_halo) of [z | r] and q");
+  TORCH_CHECK(cs(bmap) >= 3 * hd && cs(bmap) % 8 == 0 && bmap.numel() >= M * cs(bmap), "gru_halo: bias map [M][>= 3 hd]");
+  TORCH_CHECK(cs(h32) == hd && h32.numel() >= M * hd, "gru_halo: h32 [M][hd]");
+  TORCH_CHECK(cs(y) % 8 == 0 && cs(y) >= hd && y.numel() >= M * cs(y), "gru_halo: y [M][>= hd]");
+  for (const at::Tensor* v : {&hs, &xs, &wa, &wb, &bmap, &h32, &y})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(v->data_ptr()) % 16 == 0, "gru_halo: operands must be 16-byte aligned");
+  if (y2.defined()) {
+    check_bf16(y2, "y2");
+    TORCH_CHECK(cs(y2) % 8 == 0 && cs(y2) >= hd && y2.numel() >= M * cs(y2) &&
+                    reinterpret_cast<uintptr_t>(y2.data_ptr()) % 16 == 0, "gru_halo: y2 [M][>= hd]");
+  }
+  p.hsrc = hs.data_ptr(); p.xsrc = xs.data_ptr(); p.cs = cs_;
+  p.wa = wa.data_ptr(); p.wb = wb.data_ptr();
+  p.bmap = bmap.data_ptr(); p.bmap_cs = cs(bmap);
+  p.h32 = h32.data_ptr<float>(); p.y = y.data_ptr(); p.y_cs = cs(y); p.y2 = ptr(y2); p.y2_cs = y2.defined() ? cs(y2) : 0;
+  if (p.mode == 0) {
+    const int len = p.axis ? p.H : p.W, lines = p.axis ? p.W : p.H;
+    p.tiles_y = lines;
+    p.tiles_x = (len + p.TC - 1) / p.TC;
+  } else {
+    p.tiles_y = (p.H + p.TR - 1) / p.TR;
+    p.tiles_x = (p.W + p.TC - 1) / p.TC;
+  }
+  const int64_t nt = (int64_t)p.N * p.tiles_y * p.tiles_x;
+  TORCH_CHECK(nt < (1LL << 31), "gru_halo: too many tiles");
+  p.ntiles = (int)nt;
+  p.src_bytes = (long)hs.numel() * 2; p.wa_bytes = (long)wa.numel() * 2; p.wb_bytes = (long)wb.numel() * 2;
+  TORCH_CHECK(p.src_bytes < (1LL << 31), "gru_halo: loop buffers larger than 2 GiB");
+  if (keep) for (auto& v : {hs, xs, wa, wb, bmap, h32, y, y2}) if (v.defined()) keep->push_back(v);
+  // optional t[8..10] = hsrc / xsrc / y of ODD loop iterations: a single-stage GRU (raft_small)
+  // ping-pongs h between two loop buffers (it cannot update h in place, see the kernel)
+  at::Tensor hs2 = opt(t, 8), xs2 = opt(t, 9), y_2 = opt(t, 10);
+  if (hs2.defined() || xs2.defined() || y_2.defined()) {
+    TORCH_CHECK(hs2.defined() && xs2.defined() && y_2.defined(), "gru_halo: odd-iteration operands: all three or none");
+    for (const at::Tensor* v : {&hs2, &xs2, &y_2}) {
+      check_bf16(*v, "odd-iteration operand");
+      TORCH_CHECK(v->sizes() == hs.sizes() && reinterpret_cast<uintptr_t>(v->data_ptr()) % 16 == 0,
+                  "gru_halo: odd-iteration operands must have the loop buffers' shape");
+    }
+    TORCH_CHECK(hs2.data_ptr() != y_2.data_ptr(), "gru_halo: odd-iteration y must not alias its hsrc");
+    GruHaloParams q = p;
+    q.hsrc = hs2.data_ptr(); q.xsrc = xs2.data_ptr(); q.y = y_2.data_ptr(); q.y_cs = cs(y_2);
+    if (keep) for (auto& v : {hs2, xs2, y_2}) keep->push_back(v);
+    return [p, q](hipStream_t s, int it) { return jr_gru_halo((it & 1) ? &q : &p, s); };
+  }
+  return [p](hipStream_t s, int) { return jr_gru_halo(&p, s); };
 }
 
 // t = [fm (bf16 [M][cs]), wpk (bf16, pack_taps), taps (fp32 [M][>=24])], i = [M, K, fcoff]
@@ -1351,6 +1450,7 @@ void im2col_op(const TList& t, IList i) { run_now(make_im2col(t, i, nullptr)); }
 void flow_taps_op(const TList& t, IList i) { run_now(make_flow_taps(t, i, nullptr)); }
 void taps_gemm_op(const TList& t, IList i) { run_now(make_taps_gemm(t, i, nullptr)); }
 void gru_fused_op(const TList& t, IList i) { run_now(make_gru_fused(t, i, nullptr)); }
+void gru_halo_op(const TList& t, IList i) { run_now(make_gru_halo(t, i, nullptr)); }
 bool conv_grouped_ok_op(int64_t cfg) { return jr_conv_grouped_ok((int)cfg) != 0; }
 
 // Batched GEMM (bgemm.hip).  t = [A (bf16 [batch][M][K] or [batch][K][M]), B (bf16 [batch][K][N]),
@@ -1478,6 +1578,9 @@ class Plan : public torch::CustomClassHolder {
   void add_record(int64_t ev) { push_sync(OP_RECORD, ev, "record"); }
   void add_wait(int64_t ev) { push_sync(OP_WAIT, ev, "wait"); }
   void add_conv(TList t, IList i, double alpha) { push(make_conv(t, i, alpha, &keep_), "conv"); }
+  void add_conv_alt(TList t, IList i, double alpha, at::Tensor x_alt) {
+    push(make_conv_alt(t, i, alpha, x_alt, &keep_), "conv");
+  }
   void add_conv_group(TList t1, IList i1, double a1, TList t2, IList i2, double a2) {
     push(make_conv_group(t1, i1, a1, t2, i2, a2, &keep_), "conv_group");
   }
@@ -1496,6 +1599,7 @@ class Plan : public torch::CustomClassHolder {
   void add_flow_taps(TList t, IList i) { push(make_flow_taps(t, i, &keep_), "flow_taps"); }
   void add_taps_gemm(TList t, IList i) { push(make_taps_gemm(t, i, &keep_), "taps_gemm"); }
   void add_gru_fused(TList t, IList i) { push(make_gru_fused(t, i, &keep_), "gru_fused"); }
+  void add_gru_halo(TList t, IList i) { push(make_gru_halo(t, i, &keep_), "gru_halo"); }
   void add_conv1x1(TList t, IList i) { push(make_conv1x1(t, i, &keep_), "conv1x1"); }
   void add_conv_direct(TList t, IList i) { push(make_conv_direct(t, i, &keep_), "conv_direct"); }
   void add_flowin_dual(TList t, IList i, double alpha) { push(make_flowin_dual(t, i, alpha, &keep_), "flowin_dual"); }
@@ -1945,6 +2049,8 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("bgemm(Tensor?[] t, int[] i, float alpha) -> ()", &jr::bgemm_op);
   m.def("conv_grouped_ok(int cfg) -> bool", &jr::conv_grouped_ok_op);
   m.def("gru_fused_fits(int H, int W, int vertical) -> bool", &jr::gru_fused_fits);
+  m.def("gru_halo(Tensor?[] t, int[] i) -> ()", &jr::gru_halo_op);
+  m.def("gru_halo_geom_ok(int hd, int mode, int TR, int TC, int nb1, int nb2) -> bool", &jr::gru_halo_geom_ok);
   m.def("conv1x1(Tensor?[] t, int[] i) -> ()", &jr::conv1x1_op);
   m.def("conv_direct(Tensor?[] t, int[] i) -> ()", &jr::conv_direct_op);
   m.def("conv_train(Tensor?[] t, int[] i, float alpha, Tensor?[] tx, int[] ix) -> ()", &jr::conv_train_op);
@@ -1983,6 +2089,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_wait", &jr::Plan::add_wait)
       .def("num_lanes", &jr::Plan::num_lanes)
       .def("add_conv", &jr::Plan::add_conv)
+      .def("add_conv_alt", &jr::Plan::add_conv_alt)
       .def("add_corr", &jr::Plan::add_corr)
       .def("add_lookup", &jr::Plan::add_lookup)
       .def("add_upsample_convex", &jr::Plan::add_upsample_convex)
@@ -1998,6 +2105,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_flow_taps", &jr::Plan::add_flow_taps)
       .def("add_taps_gemm", &jr::Plan::add_taps_gemm)
       .def("add_gru_fused", &jr::Plan::add_gru_fused)
+      .def("add_gru_halo", &jr::Plan::add_gru_halo)
       .def("add_flowin_dual", &jr::Plan::add_flowin_dual)
       .def("add_conv_group", &jr::Plan::add_conv_group)
       .def("add_conv1x1", &jr::Plan::add_conv1x1)

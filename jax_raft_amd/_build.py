@@ -42,13 +42,15 @@ KERNEL_SOURCES = [
     CSRC / "kernels" / "convex_head.hip",
     CSRC / "kernels" / "conv1x1.hip",
     CSRC / "kernels" / "gru_fused.hip",
+    CSRC / "kernels" / "gru_halo.hip",
     CSRC / "kernels" / "bgemm.hip",
     CSRC / "kernels" / "merged.hip",
     CSRC / "kernels" / "conv_fam_grp.hip",
 ]
 HOST_SOURCES = [CSRC / "runtime" / "binding.cpp"]
-HEADERS = [CSRC / "kernels" / "common.h", CSRC / "kernels" / "kernels.h", CSRC / "kernels" / "conv_igemm.h",
-           CSRC / "kernels" / "conv_direct.h", CSRC / "kernels" / "convex_head.h", CSRC / "kernels" / "upsample.h"]
+# every header of csrc/ is a dependency of every object (a missed header left stale objects in
+# _C.so before: conv1x1.h, round 3); the set is small, so a rebuild on any header edit is cheap
+HEADERS = sorted(CSRC.rglob("*.h"))
 
 
 def _torch_paths():

@@ -73,6 +73,92 @@ def gru_fused_tiles(N: int, H: int, W: int, vertical: int) -> int:
     return N * (W // J) if 1 <= H and J * H <= 128 and J * (H + 4) <= 136 and W % J == 0 else 0
 
 
+def _m32_chan(r: torch.Tensor) -> torch.Tensor:
+    """Channel held by row r of a 32-row MFMA A block whose accumulator register i of lane
+    half h is channel 16 h + i (row (i & 3) + 8 (i >> 2) + 4 h of the 32x32x16 tile)."""
+    return 16 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3)
+
+
+def pack_gru_halo(kernel: torch.Tensor, cin_pad: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """ConvGRU gate kernel (kh, kw, cin, cout) HWIO -> the weight stream of gru_halo.hip:
+    bf16 [cout/32][kh*kw*cin_pad/16][64][8], fragment (blk, s), lane l, element j holding
+    W[k = 16 s + 8 (l >> 5) + j][co = 32 blk + _m32_chan(l & 31)] with k = tap * cin_pad + ci
+    (tap row-major, input channels zero-padded to cin_pad): one contiguous 1 KB load per
+    MFMA A fragment."""
+    kh, kw, cin, cout = kernel.shape
+    assert cout % 32 == 0 and cin <= cin_pad and cin_pad % 16 == 0, (kernel.shape, cin_pad)
+    dev = kernel.device
+    k = torch.zeros(kh * kw, cin_pad, cout, dtype=torch.float32, device=dev)
+    k[:, :cin] = kernel.detach().float().reshape(kh * kw, cin, cout)
+    k = k.reshape(kh * kw * cin_pad, cout)
+    ks = kh * kw * cin_pad // 16
+    blk = torch.arange(cout // 32, device=dev).view(-1, 1, 1, 1)
+    s = torch.arange(ks, device=dev).view(1, -1, 1, 1)
+    l = torch.arange(64, device=dev).view(1, 1, 64, 1)
+    j = torch.arange(8, device=dev).view(1, 1, 1, 8)
+    kk = (16 * s + 8 * (l >> 5) + j).expand(cout // 32, ks, 64, 8)
+    co = (32 * blk + _m32_chan(l & 31)).expand(cout // 32, ks, 64, 8)
+    w = k[kk, co].to(torch.bfloat16).contiguous()
+    if out is not None:
+        assert out.shape == w.shape and out.dtype == torch.bfloat16
+        out.copy_(w)
+        return out
+    return w
+
+
+# (hd, mode) -> the (nb1, nb2) block counts gru_halo.hip instantiates (JR_HALO_CASES)
+GRU_HALO_BLOCKS = {(128, 0): ((1, 1), (2, 1), (2, 2), (3, 2)), (96, 1): ((2, 1), (2, 2), (3, 2))}
+
+
+def gru_halo_lds(hd: int, mode: int, TR: int, TC: int, nb1: int, nb2: int) -> int:
+    """LDS bytes of one gru_halo workgroup (mirrors gru_halo.hip:lds_bytes)."""
+    f_rows = TC + 8 if mode == 0 else (TR + 4) * (TC + 4)
+    f_elems = max(f_rows * 256, (hd // 32) * nb2 * 4 * 256 * 2)
+    return (round_up(f_elems, 8) + 32 * nb1 * 128) * 2
+
+
+def gru_halo_geom_ok(hd: int, mode: int, TR: int, TC: int, nb1: int, nb2: int) -> bool:
+    """Host-side mirror of binding.cpp:gru_halo_geom_ok (no library needed)."""
+    if (nb1, nb2) not in GRU_HALO_BLOCKS.get((hd, mode), ()) or TR < 1 or TC < 1:
+        return False
+    if mode == 0 and TR != 1:
+        return False
+    nreg = TC + 4 if mode == 0 else (TR + 2) * (TC + 2)
+    return nreg <= 32 * nb1 and TR * TC <= 32 * nb2 and gru_halo_lds(hd, mode, TR, TC, nb1, nb2) <= 160 * 1024
+
+
+def gru_halo_tiles(mode: int, axis: int, N: int, H: int, W: int, TR: int, TC: int) -> int:
+    """Workgroups of a gru_halo stage (binding.cpp:make_gru_halo)."""
+    if mode == 0:
+        length, lines = (H, W) if axis else (W, H)
+        return N * lines * -(-length // TC)
+    return N * -(-H // TR) * -(-W // TC)
+
+
+def gru_halo_candidates(hd: int, mode: int, axis: int, N: int, H: int, W: int) -> List[Tuple[int, int, int, int]]:
+    """(TR, TC, nb1, nb2) tilings of one gru_halo stage worth timing: per instantiated block
+    count, the largest tile that fits it, balanced so the last tile along the run / the
+    block grid is not a sliver (mode 0: runs of L = ceil(len / segments) pixels)."""
+    out = []
+    if mode == 0:
+        length = H if axis else W
+        for nb1, nb2 in ((1, 1), (2, 1), (2, 2), (3, 2)):
+            lmax = min(32 * nb1 - 4, 32 * nb2)
+            segs = -(-length // lmax)
+            L = -(-length // segs)
+            if (L + 4 > 32 * (nb1 - 1) or nb1 == 1) and (L > 32 * (nb2 - 1) or nb2 == 1):
+                out.append((1, L, nb1, nb2))
+    else:
+        for nb1, nb2, tr, tc in ((2, 1, 5, 6), (2, 1, 4, 8), (2, 2, 6, 6), (3, 2, 7, 8)):
+            out.append((min(tr, H), min(tc, W), nb1, nb2))
+    seen, res = set(), []
+    for c in out:
+        if c not in seen and gru_halo_geom_ok(hd, mode, *c):
+            seen.add(c)
+            res.append(c)
+    return res
+
+
 def load(build_if_missing: bool = True) -> None:
     """Load ``_C.so`` (building it with hipcc first if it is missing)."""
     global _loaded, _load_error

@@ -214,6 +214,7 @@ class RaftEngine:
         self._taps_w = None
         self._taps_epi_w = None
         self._cc1_w = self._cc1_b = None
+        self._halo_w: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}   # GRU gi -> gru_halo (wa, wb)
         self.model = model
         self.device = torch.device(device)
         self.use_graph = use_graph
@@ -341,6 +342,13 @@ class RaftEngine:
             else:
                 self._convex_w.copy_(wc)
                 self._convex_b.copy_(bc)
+        if self._halo_geom() is not None:   # the halo-tiled fused ConvGRU's weight streams
+            for gi in range(len(self.model.update_block.recurrent_block.kernel_size)):
+                ka = self._sources[f"gru{gi}.a"]()[0].to(self.device)
+                kb = self._sources[f"gru{gi}.b"]()[0].to(self.device)
+                old = self._halo_w.get(gi)
+                self._halo_w[gi] = (nat.pack_gru_halo(ka, self.hx_cs, out=old[0] if old else None),
+                                    nat.pack_gru_halo(kb, self.hx_cs, out=old[1] if old else None))
         cf1 = self.model.update_block.motion_encoder.convflow1.layers_0
         if nat.direct_conv_ok(cf1.kernel, cf1.stride):
             wd = nat.pack_direct_weight(cf1.kernel).to(self.device)
@@ -443,9 +451,14 @@ class RaftEngine:
         self._reg("fh2.taps", fh2_taps)
 
     # ------------------------------------------------------------- autotune
-    def _conv(self, plan, spec: ConvSpec, x, N, H, W, y, **kw):
-        """Append one conv to ``plan``, choosing its tile config (autotuned)."""
-        plan.add_conv(*conv_args(spec, x, N, H, W, y, **self._conv_kw(spec, x, N, H, W, y, kw)))
+    def _conv(self, plan, spec: ConvSpec, x, N, H, W, y, x_alt=None, **kw):
+        """Append one conv to ``plan``, choosing its tile config (autotuned).  ``x_alt``: the
+        input of odd loop iterations (a state that ping-pongs between two buffers)."""
+        args = conv_args(spec, x, N, H, W, y, **self._conv_kw(spec, x, N, H, W, y, kw))
+        if x_alt is not None:
+            plan.add_conv_alt(*args, x_alt)
+        else:
+            plan.add_conv(*args)
 
     def _conv_group(self, plan, a: tuple, b: tuple) -> bool:
         """Two independent STD-epilogue convs ``(spec, x, N, H, W, y, kw)`` as ONE grid
@@ -495,7 +508,8 @@ class RaftEngine:
                    kw.get("epi", EPI_STD), kw.get("bmap") is not None)
             cfg = _TUNE_CACHE.get(key + (str(self.device),))
             if cfg is None:
-                cfg = tunedb.lookup(self.arch, key)   # persisted decision (runtime/tunedb.py)
+                valid = nat.TAPS_CFGS if kw.get("epi") == EPI_TAPS else nat.TUNE_CFGS
+                cfg = tunedb.lookup(self.arch, key, valid)   # persisted decision (runtime/tunedb.py)
                 if cfg is None:
                     cfg = _tune(spec, x, N, H, W, y, kw)
                     tunedb.record(self.arch, key, cfg)
@@ -654,6 +668,70 @@ class RaftEngine:
         return (all_iters and self.has_mask and self._taps_epi_w is not None and self._convex_w is not None
                 and self._specs["fh1.flow"].cout == 256)
 
+    def _halo_geom(self):
+        """(hd, [(mode, axis) per ConvGRU stage]) when the halo-tiled fused ConvGRU
+        (gru_halo.hip) serves this update block, else None: raft_large's 1x5 + 5x1 stages
+        (hidden 128, [h | motion | flow] = 256 loop channels) or raft_small's single 3x3
+        GRU (hidden 96, 192 loop channels); bf16 bias map (``gate_dtype``)."""
+        rb = self.model.update_block.recurrent_block
+        ks = [tuple(k) for k in rb.kernel_size]
+        if self.gate_dtype != torch.bfloat16 or self.gate_cs < 3 * self.hidden:
+            return None
+        if self.hidden == 128 and self.hx_cs == 256 and ks == [(1, 5), (5, 1)]:
+            return 128, [(0, 0), (0, 1)]
+        if self.hidden == 96 and self.hx_cs == 192 and ks == [(3, 3)]:
+            return 96, [(1, 0)]
+        return None
+
+    def _gru_path(self, B: int, h: int, w: int) -> str:
+        """ConvGRU lowering of a plan: "halo" (gru_halo.hip: one launch per stage, any map
+        size and batch), "fused" (gru_fused.hip: whole-row tiles, raft_large at >= 3/4 of
+        the CUs' worth of rows) or "unfused" (two implicit-GEMM launches per stage).
+        ``JR_GRU=halo|fused|unfused`` forces one (where it applies)."""
+        env = os.environ.get("JR_GRU", "auto")
+        if env == "unfused":
+            return "unfused"
+        if env in ("auto", "halo") and self._halo_geom() is not None:
+            return "halo"
+        if env in ("auto", "fused") and self._gru_fused_ok(B, h, w):
+            return "fused"
+        return "unfused"
+
+    def _halo_tile(self, gi: int, mode: int, axis: int, B: int, h: int, w: int, ops_args) -> Tuple[int, int, int, int]:
+        """Tile of one gru_halo stage: the persisted decision (tuned DB key "gru_halo") or
+        the fastest candidate (ops/native.py:gru_halo_candidates) timed on the plan's own
+        buffers (the prologue re-initialises everything the trial launches write)."""
+        cands = nat.gru_halo_candidates(self.hidden, mode, axis, B, h, w)
+        enc = {c[0] * 1000000 + c[1] * 1000 + c[2] * 10 + c[3]: c for c in cands}
+        key = ("gru_halo", self.hidden, mode, axis, B, h, w)
+        forced = os.environ.get("JR_HALO_TILE")   # "TR,TC,nb1,nb2" (A/B measurements)
+        if forced:
+            return tuple(int(v) for v in forced.split(","))
+        if not self.autotune or len(cands) == 1 or self.device.type != "cuda":
+            return cands[0]
+        code = _TUNE_CACHE.get(key + (str(self.device),))
+        if code is None:
+            code = tunedb.lookup(self.arch, key, set(enc))
+        if code is None:
+            t, base = ops_args
+            best = None
+            for c, tile in enc.items():
+                nat.ops().gru_halo(t, base + list(tile))
+                s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s_.record()
+                for _ in range(5):
+                    nat.ops().gru_halo(t, base + list(tile))
+                e_.record()
+                e_.synchronize()
+                el = s_.elapsed_time(e_)
+                if best is None or el < best[0]:
+                    best = (el, c)
+            code = best[1]
+            tunedb.record(self.arch, key, code)
+        _TUNE_CACHE[key + (str(self.device),)] = code
+        self.chosen_cfgs[f"gru{gi}.halo"] = code
+        return enc[code]
+
     def _gru_fused_ok(self, B: int, h: int, w: int) -> bool:
         """The fused ConvGRU kernel (gru_fused.hip) serves raft_large's update block:
         hidden 128, [h | motion | flow] = 256 loop channels, a 1x5 then a 5x1 stage,
@@ -662,10 +740,8 @@ class RaftEngine:
         as the GPU has CUs: measured on MI355X at 440x1024, batch 4 (220 / 256 tiles)
         333-335 vs 320 pairs/s; batch 1 (55 / 64 tiles) 139 vs 158 FPS for the
         two-launch implicit-GEMM path (profiles/r3_gru_fused_ab.txt).
-        ``JR_GRU_FUSED=0`` / ``=1`` force the two-launch path / the fused one."""
-        env = os.environ.get("JR_GRU_FUSED", "auto")
-        if env == "0":
-            return False
+        ``JR_GRU=fused`` forces it where it fits."""
+        env = "1" if os.environ.get("JR_GRU") == "fused" else "auto"
         rb = self.model.update_block.recurrent_block
         ks = [tuple(k) for k in rb.kernel_size]
         if (self.hidden != 128 or self.hx_cs != 256 or self.gate_cs < 384 or ks != [(1, 5), (5, 1)]
@@ -875,11 +951,23 @@ class RaftEngine:
         mfeat = (alloc("mfeat", (M, round_up(sp["mask.convrelu"].cout, 8)))
                  if self.has_mask and (split_mask or not all_iters) else None)
         mask = alloc("mask", (M, 576)) if self.has_mask and self._convex_w is None else None
-        # fused ConvGRU stages (gru_fused.hip): one launch per stage, r*h / z stay in the CU
-        gru_f = self._gru_fused_ok(B, h, w) and not self.cp
+        # ConvGRU lowering: "halo" (gru_halo.hip, one launch per stage at any size / batch),
+        # "fused" (gru_fused.hip, whole-row tiles) or "unfused" (EPI_GRU_A / EPI_GRU_B convs)
+        gru_path = self._gru_path(B, h, w)
+        if gru_path == "fused" and self.cp:
+            gru_path = "unfused"
+        self.gru_path = gru_path
+        ngru = len(m.update_block.recurrent_block.kernel_size)
+        # the halo kernel cannot update h in place (neighbouring tiles read it): raft_large's
+        # stage 1 writes h' into qx, stage 2 reads it there and writes hx; raft_small's single
+        # stage ping-pongs h between hx (read on even iterations) and qx (odd), and its FlowHead
+        # reads the buffer the stage just wrote
+        halo_pp = gru_path == "halo" and ngru == 1
+        # qx's [motion | flow] part is read only by the unfused GRU-B and the ping-pong
+        qx_x = gru_path != "halo" or halo_pp
         # with the mask lane, the mask head reads h from its own copy `hm` (written by the last
         # stage), so the first stage can replace h in hx while the mask lane still runs
-        hm = alloc("hm", (M, self.hidden)) if gru_f and lanes_on and self.has_mask else None
+        hm = alloc("hm", (M, self.hidden)) if gru_path != "unfused" and lanes_on and self.has_mask else None
 
         # one-lane schedule: the flow conv + the previous iteration's upsampling as one grid (merged.hip)
         c1k = me.convflow1.layers_0.kernel
@@ -902,7 +990,10 @@ class RaftEngine:
             if taps_epi:
                 self._conv(plan, s1, hx, B, h, w, taps, act=ACT_RELU, epi=EPI_TAPS, tapw=self._taps_epi_w)
                 return
-            self._conv(plan, s1, hx, B, h, w, fm, act=ACT_RELU)
+            if halo_pp:   # h' of even iterations is in qx, of odd ones in hx
+                self._conv(plan, s1, qx, B, h, w, fm, x_alt=hx, act=ACT_RELU)
+            else:
+                self._conv(plan, s1, hx, B, h, w, fm, act=ACT_RELU)
             if self._taps_w is not None:   # skinny GEMM kernel (flowhead.hip), N = 18
                 plan.add_taps_gemm([fm, self._taps_w, taps], [M, self.fh_hidden, 0])
             else:
@@ -910,7 +1001,7 @@ class RaftEngine:
 
         def flow_update():
             """``coords1 += delta`` (model.py:505) from the taps; flow into hx / qx / flow8."""
-            plan.add_flow_taps([taps, self._fh2_b, coords, flow32, hx, qx, flow8],
+            plan.add_flow_taps([taps, self._fh2_b, coords, flow32, hx, qx if qx_x else None, flow8],
                                [B, h, w, self.flow_off, self.flow_off])
 
         def upsample(stride, mask_from_fm: bool):
@@ -934,7 +1025,7 @@ class RaftEngine:
                 plan.add_upsample_convex([mask, flow32, out], [B, h, w, stride])
 
         def lookup(with_update: bool):
-            upd = [taps, self._fh2_b, flow32, hx, qx, flow8] if with_update else []
+            upd = [taps, self._fh2_b, flow32, hx, qx if qx_x else None, flow8] if with_update else []
             extra = [self.flow_off, self.flow_off] if with_update else []
             plan.add_lookup([coords, corr] + levels + [None] * (4 - L) + upd,
                             [L, B, h, w, self.radius, h * w, blocked] + extra)
@@ -965,11 +1056,26 @@ class RaftEngine:
                 self._conv(plan, *last[:6], **last[6])
             if wait_flow:
                 plan.add_wait(E_FLOW)
-            self._conv(plan, sp["me.conv"], cf, B, h, w, hx, y_coff=self.mot_off, act=ACT_RELU, y2=qx,
-                       y2_coff=self.mot_off)
-            ngru = len(m.update_block.recurrent_block.kernel_size)
+            self._conv(plan, sp["me.conv"], cf, B, h, w, hx, y_coff=self.mot_off, act=ACT_RELU,
+                       y2=qx if qx_x else None, y2_coff=self.mot_off)
+            if gru_path == "halo":
+                _, stages = self._halo_geom()
+                for gi, (mode, axis) in enumerate(stages):
+                    wa_, wb_ = self._halo_w[gi]
+                    last = gi == ngru - 1
+                    if halo_pp:
+                        t = [hx, hx, wa_, wb_, gbias[gi], h32, qx, None, qx, qx, hx]
+                    else:
+                        t = [hx if gi == 0 else qx, hx, wa_, wb_, gbias[gi], h32, qx if gi == 0 else hx,
+                             hm if last else None]
+                    if wait_mask and last:
+                        plan.add_wait(E_MASK)  # the previous iteration's mask head has read hm (and flow32)
+                    base = [B, h, w, mode, axis]
+                    tile = self._halo_tile(gi, mode, axis, B, h, w, (t, base))
+                    plan.add_gru_halo(t, base + list(tile))
+                return
             for gi in range(ngru):
-                if gru_f:
+                if gru_path == "fused":
                     last = gi == ngru - 1
                     if wait_mask and (last if hm is not None else gi == 0):
                         plan.add_wait(E_MASK)  # the previous iteration's mask head has read hm / h (and flow32)

@@ -14,6 +14,12 @@ produced on the target hardware by ``tools/autotune_db.py``:
 
 ``JR_TUNE=fresh`` ignores the file (re-times every problem, e.g. to refresh
 it); ``JR_TUNE=db`` (default) uses it.
+
+The file records the ``kernel_set`` it was tuned against: when the compiled tile
+configs are renumbered or removed, :data:`KERNEL_SET` is bumped and an old file is
+ignored (re-timed) instead of handing out ids that no longer exist; and a caller
+passing ``valid=`` to :func:`lookup` gets a miss for a stored id outside its
+candidate set (e.g. an id from a retired config range).
 """
 from __future__ import annotations
 
@@ -24,6 +30,7 @@ from pathlib import Path
 from typing import Dict, Optional
 
 DB_DIR = Path(__file__).resolve().parent.parent / "tuned"
+KERNEL_SET = 1    # bump when tile-config ids are renumbered / removed (csrc/kernels/conv_igemm.hip)
 _lock = threading.Lock()
 _tables: Dict[str, Dict[str, int]] = {}
 _stats = {"hits": 0, "misses": 0}
@@ -54,13 +61,19 @@ def _table(arch: str) -> Dict[str, int]:
             p = path(arch)
             if os.environ.get("JR_TUNE", "db") != "fresh" and p.exists():
                 with open(p) as f:
-                    t = {k: int(v) for k, v in json.load(f).get("entries", {}).items()}
+                    d = json.load(f)
+                if int(d.get("kernel_set", 1)) == KERNEL_SET:
+                    t = {k: int(v) for k, v in d.get("entries", {}).items()}
             _tables[arch] = t
         return t
 
 
-def lookup(arch: str, key) -> Optional[int]:
+def lookup(arch: str, key, valid=None) -> Optional[int]:
+    """The stored decision for ``key`` (None: a miss).  ``valid``: the caller's candidate
+    ids; a stored id outside them is a miss (stale entry), not a launch failure."""
     cfg = _table(arch).get(_key(key))
+    if cfg is not None and valid is not None and cfg not in valid:
+        cfg = None
     _stats["hits" if cfg is not None else "misses"] += 1
     return cfg
 
@@ -79,13 +92,15 @@ def stats() -> Dict[str, int]:
     return dict(_stats)
 
 
-def save(arch: str) -> Path:
-    """Write this process's table (file entries + new decisions) for ``arch``."""
+def save(arch: str, target=None) -> Path:
+    """Write this process's table (file entries + new decisions) for ``arch`` to
+    ``target`` (default: the packaged ``tuned/<arch>.json``)."""
     t = _table(arch)
-    DB_DIR.mkdir(parents=True, exist_ok=True)
-    p = path(arch)
-    tmp = p.with_suffix(".json.tmp")
+    p = Path(target) if target is not None else path(arch)
+    p.parent.mkdir(parents=True, exist_ok=True)
+    tmp = p.with_name(p.name + ".tmp")
     with open(tmp, "w") as f:
-        json.dump({"version": 1, "arch": arch, "entries": dict(sorted(t.items()))}, f, indent=0)
+        json.dump({"version": 1, "kernel_set": KERNEL_SET, "arch": arch, "entries": dict(sorted(t.items()))}, f,
+                  indent=0)
     os.replace(tmp, p)
     return p

@@ -204,7 +204,7 @@ def record_conv(plan, spec, x, N, H, W, y, *, tx=None, ix=None, extra=None, **kw
            x.shape[-1], tuple(extra) if extra else None)
     cfg = _CFG_CACHE.get(key + (str(x.device),))
     if cfg is None:
-        cfg = tunedb.lookup(arch, key)   # persisted decision (runtime/tunedb.py)
+        cfg = tunedb.lookup(arch, key, nat.TUNE_CFGS)   # persisted decision (runtime/tunedb.py)
     ops = nat.ops()
     if cfg is None:
         scratch = torch.empty(N * OH * OW, round_up(spec.cout, 8), dtype=BF16, device=x.device)
@@ -834,7 +834,10 @@ class FusedLoop:
                              1.0 / float(C) ** 0.5)
         f1 = self.fm1.reshape(B, hw, C)
         f2 = self.fm2.reshape(B, hw, C)
-        if hw % 128 == 0 and C % 128 == 0 and f1.is_contiguous() and f2.is_contiguous():
+        # the GEMMs write through reshape views of out1 / out2: a non-contiguous output would make
+        # reshape return a copy and the gradient would be lost -- such outputs take the bmm path
+        outs_ok = out1 is None or (out1.is_contiguous() and out2.is_contiguous())
+        if hw % 128 == 0 and C % 128 == 0 and f1.is_contiguous() and f2.is_contiguous() and outs_ok:
             if out1 is None:
                 out1 = torch.empty(B, h, w, C, dtype=F32, device=self.device)
                 out2 = torch.empty(B, h, w, C, dtype=F32, device=self.device)
@@ -842,8 +845,10 @@ class FusedLoop:
             nat.ops().bgemm([self._dC, f1, out2.reshape(B, hw, C)], [hw, C, hw, 1], 1.0)   # dC^T . fmap1
             return out1, out2
         if out1 is not None:
-            torch.bmm(self._dC, f2, out=out1.reshape(B, hw, C))
-            torch.bmm(self._dC.transpose(1, 2), f1, out=out2.reshape(B, hw, C))
+            g1 = torch.bmm(self._dC, f2).float()
+            g2 = torch.bmm(self._dC.transpose(1, 2), f1).float()
+            out1.copy_(g1.reshape(out1.shape))
+            out2.copy_(g2.reshape(out2.shape))
             return out1, out2
         try:
             g1 = torch.bmm(self._dC, f2, out_dtype=F32)

@@ -21,7 +21,7 @@ def _inputs(B, H, W, seed=0):
     return i1.contiguous(), i2.contiguous()
 
 
-# Measured on MI355X (tools/parity_probe.py): max over the 4 iterations of EPE / mean
+# Measured on MI355X (dev/probes/parity_probe.py): max over the 4 iterations of EPE / mean
 # |golden flow| = 0.0478-0.0486 (raft_small), 0.0134-0.0172 (raft_large); the bounds
 # leave 1.3x / 1.5x headroom (the bf16 drift at the headline size is tests/test_drift.py).
 REL_EPE = {"raft_small": 0.065, "raft_large": 0.026}

@@ -53,15 +53,18 @@ def _plan(factory, B, all_iters=True, streams="auto", H=128, W=256):
     return eng, st.plan
 
 
-def test_lane_schedule_raft_large(fake):
+@pytest.mark.parametrize("gru", ["unfused", "halo"])
+def test_lane_schedule_raft_large(fake, gru, monkeypatch):
+    monkeypatch.setenv("JR_GRU", gru)
     eng, p = _plan(raft_large, 4)
     assert eng.uses_lanes(4) and not eng.uses_lanes(1) and not eng.uses_lanes(4, all_iters=False)
     loop = [(ln, d, op) for s, ln, d, op, _ in p.ops if s == 1]
     ops = [op for _, _, op in loop]
-    # critical lane: lookup (+ update) -> cc1 (LDS kernel) -> cc2 -> motion -> 2 x GRU(A, B) -> FlowHead taps
+    # critical lane: lookup (+ update) -> cc1 (LDS kernel) -> cc2 -> motion -> 2 x GRU -> FlowHead taps
     assert ops.count("lookup") == 1 and ops.count("flow_taps") == 0
+    stages = ["conv"] * 4 if gru == "unfused" else ["gru_halo"] * 2
     assert [op for ln, d, op in loop if ln == 0 and op not in ("record", "wait")] == \
-        ["lookup", "conv1x1", "conv", "conv", "conv", "conv", "conv", "conv", "conv"]
+        ["lookup", "conv1x1", "conv", "conv"] + stages + ["conv"]
     # mask lane: deferred flow features + mask conv + convex head of the previous iteration
     side = [op for ln, d, op in loop if ln == 2 and op not in ("record", "wait")]
     assert side == ["conv_direct", "conv", "conv", "convex_head"]
@@ -76,7 +79,7 @@ def test_lane_schedule_fused_gru(fake, monkeypatch):
     size): one gru_fused op per stage on the critical lane, the mask lane's mask conv
     reads its own h copy `hm` (written by the last stage), and the E_MASK wait moves
     from the first stage to the last one (still three waits per iteration)."""
-    monkeypatch.setenv("JR_GRU_FUSED", "1")
+    monkeypatch.setenv("JR_GRU", "fused")
     eng, p = _plan(raft_large, 4)
     loop = [(ln, d, op, a) for s, ln, d, op, a in p.ops if s == 1]
     main = [op for ln, d, op, _ in loop if ln == 0]
@@ -92,15 +95,50 @@ def test_lane_schedule_fused_gru(fake, monkeypatch):
     mask_convs = [a for ln, d, op, a in loop if ln == 2 and op == "conv"]
     assert any(t[0] is hm for t, *_ in mask_convs)             # the mask conv reads hm
     assert not eng._gru_fused_ok(1, 55, 128) or eng._gru_fused_ok(4, 55, 128)
-    monkeypatch.setenv("JR_GRU_FUSED", "auto")
+    monkeypatch.setenv("JR_GRU", "auto")
     assert eng._gru_fused_ok(4, 55, 128) and not eng._gru_fused_ok(1, 55, 128)
     assert not eng._gru_fused_ok(4, 55, 129)                    # a row wider than a tile
 
 
 def test_fused_gru_not_for_raft_small(fake, monkeypatch):
-    monkeypatch.setenv("JR_GRU_FUSED", "1")
+    monkeypatch.setenv("JR_GRU", "fused")
     _, p = _plan(raft_small, 4)
     assert "gru_fused" not in p.names(1)
+
+
+def test_halo_gru_raft_large_buffers(fake, monkeypatch):
+    """gru_halo lowering of raft_large (any batch): stage 1 (1x5 runs) reads [h | x] from hx
+    and writes h' into qx; stage 2 (5x1 runs) reads h' from qx, x from hx and writes hx (never
+    in place: neighbouring tiles read h); qx's [motion | flow] part is no longer written."""
+    monkeypatch.setenv("JR_GRU", "auto")
+    for B, lanes in ((1, False), (4, True)):
+        eng, p = _plan(raft_large, B)
+        assert eng.gru_path == "halo"
+        g = [a for s, ln, d, op, a in p.ops if s == 1 and op == "gru_halo"]
+        assert len(g) == 2
+        (t1, i1), (t2, i2) = g
+        hx, qx = t1[0], t1[6]
+        assert t1[1] is hx and t2[0] is qx and t2[1] is hx and t2[6] is hx and t1[6] is not hx
+        assert i1[3:5] == [0, 0] and i2[3:5] == [0, 1]                 # 1x5 along W, then 5x1 along H
+        assert nat.gru_halo_geom_ok(128, 0, *i1[5:]) and nat.gru_halo_geom_ok(128, 0, *i2[5:])
+        assert (t2[7] is not None) == lanes and t1[7] is None          # hm copy only for the mask lane
+        mc = [a for s, ln, d, op, a in p.ops if s == 1 and op == "conv" and a[0][0] is not None
+              and a[0][4] is not None and a[0][4] is qx]
+        assert not mc                                                  # me.conv no longer copies into qx
+
+
+def test_halo_gru_raft_small_ping_pong(fake, monkeypatch):
+    """raft_small's single 3x3 stage ping-pongs h between hx and qx: even iterations read hx
+    and write qx, odd ones the reverse, and the FlowHead conv reads the buffer just written."""
+    monkeypatch.setenv("JR_GRU", "auto")
+    eng, p = _plan(raft_small, 1)
+    assert eng.gru_path == "halo"
+    (t, i), = [a for s, ln, d, op, a in p.ops if s == 1 and op == "gru_halo"]
+    hx, qx = t[0], t[6]
+    assert t[1] is hx and t[8] is qx and t[9] is qx and t[10] is hx and qx is not hx
+    assert i[3] == 1 and nat.gru_halo_geom_ok(96, 1, *i[5:])
+    (fh,) = [a for s, ln, d, op, a in p.ops if s == 1 and op == "conv_alt"]
+    assert fh[0][0] is qx and fh[3] is hx
 
 
 @pytest.mark.parametrize("merged", ["1", "0"])
