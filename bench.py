@@ -18,12 +18,15 @@ untimed warmup steps, then exactly K steps bracketed by barrier + synchronize;
 the MAX over ranks is reported.
 
 After the headline, the secondary BASELINE configurations are measured the same
-way and added to the SAME JSON line (``extras``; each one's failure gives
-``null`` without losing the headline): raft_large batch 1 (the reference's
-FPS protocol), raft_small batch 1 at 32 and at 12 iterations (config 2), and
-training (config 5: raft_large, 384x512, 12 iterations, batch 6 per GPU,
-sequence loss + AdamW through the Trainer, RCCL gradient all-reduce for N>1,
-synthetic data generated inside each timed step).
+way and added to the SAME JSON line (``extras``; a failure in an extra's untimed
+set-up gives ``null`` on every rank without losing the headline): raft_large batch
+1 as a pipelined stream (``b1_fps``) and with the reference's synchronous per-pair
+protocol (``b1_sync``: H2D + forward + sync, 1 / mean latency,
+validate_sintel.py:185-188), raft_small batch 1 at 32 iterations (stream and
+sync) and at 12 iterations (config 2), the fp32 engine at batch 1, 1088x1920
+frames (``hires_b1``), and training (config 5: raft_large, 384x512, 12
+iterations, batch 6 per GPU, sequence loss + AdamW through the Trainer, RCCL
+gradient all-reduce for N>1, synthetic data generated inside each timed step).
 
 Weights are random-init (no network for checkpoints), data is synthetic, so
 EPE is not measurable here and is reported as null; the numerical drift of the
@@ -149,10 +152,31 @@ class FlowGather:
             self.inflight.pop(0).wait()
 
 
+class ExtraFailed(RuntimeError):
+    """An extra failed on some rank (every rank raises it together, so the ranks' collectives
+    stay paired and every rank reports the extra as null)."""
+
+
+def agree(ctx: Ctx, ok: bool, what: str) -> None:
+    """All ranks learn whether every rank got here without an error (MIN of a flag): a
+    failure on one rank must not leave the others waiting in a collective the failed rank
+    never enters (bench.py extras on N > 1)."""
+    if ctx.pg is None:
+        if not ok:
+            raise ExtraFailed(what)
+        return
+    t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=ctx._coll_dev())
+    ctx.pg.all_reduce(t, op=ctx.pg.ReduceOp.MIN)
+    if t.item() < 0.5:
+        raise ExtraFailed(what)
+
+
 def run_inference(ctx: Ctx, model, *, B: int, H: int, W: int, iters: int, steps: int, warmup: int,
                   final_only: bool, gather: bool, seed: int, engine_kw: dict, pipeline: str = "auto",
-                  h2d: bool = True, sync_h2d: bool = False) -> dict:
-    """Time ``steps`` inference steps of ``B`` pairs per rank; returns the run record."""
+                  h2d: bool = True, sync_h2d: bool = False, guarded: bool = False) -> dict:
+    """Time ``steps`` inference steps of ``B`` pairs per rank; returns the run record.
+    ``guarded``: the untimed part (engine, plan build, warmup: no collectives) may fail on
+    one rank; the ranks then agree on the failure before any collective (:func:`agree`)."""
     from jax_raft_amd.runtime.pipeline import InputPrefetcher
 
     dev = ctx.dev
@@ -164,15 +188,8 @@ def run_inference(ctx: Ctx, model, *, B: int, H: int, W: int, iters: int, steps:
     else:
         img1, img2 = img1.to(dev), img2.to(dev)
     pf = InputPrefetcher([(B, H, W, 3), (B, H, W, 3)], dev) if (h2d and not sync_h2d) else None
-    eng = model.engine(dev, **engine_kw)
-    mode = pipeline
-    if mode == "auto":
-        mode = "off" if (eng.uses_lanes(B, not final_only) or engine_kw.get("split", 1) > 1) else "graph"
-    copipe = mode == "graph" and engine_kw.get("use_graph", True)
     all_iters = not final_only
-    if copipe:   # fill the pipeline: the first batch's prologue (its loop runs in the first step)
-        eng.pipelined(img1.to(dev), img2.to(dev), iters, return_all_iters=all_iters)
-    gat = FlowGather(ctx, (B, H, W, 2)) if (gather and ctx.world > 1) else None
+    eng, mode, copipe, gat = None, pipeline, False, None
 
     def forward(a, b):
         if copipe:
@@ -199,12 +216,28 @@ def run_inference(ctx: Ctx, model, *, B: int, H: int, W: int, iters: int, steps:
                     pf.put(i + 1, [img1, img2])
         return out
 
-    out = run(warmup)
-    if gat is not None:
+    err, out = None, None
+    try:
+        eng = model.engine(dev, **engine_kw)
+        if mode == "auto":
+            mode = "off" if (eng.uses_lanes(B, not final_only) or engine_kw.get("split", 1) > 1) else "graph"
+        copipe = mode == "graph" and engine_kw.get("use_graph", True)
+        if copipe:   # fill the pipeline: the first batch's prologue (its loop runs in the first step)
+            eng.pipelined(img1.to(dev), img2.to(dev), iters, return_all_iters=all_iters)
+        out = run(warmup)              # gat is None: no collective in the warmup (see `guarded`)
+        torch.cuda.synchronize(dev)
+        if out is not None:
+            assert out.shape == ((iters if all_iters else 1), B, H, W, 2) and bool(torch.isfinite(out[-1]).all())
+    except Exception as e:  # noqa: BLE001
+        if not guarded:
+            raise
+        err = e
+    if guarded:
+        agree(ctx, err is None, f"{type(err).__name__}: {err}" if err is not None else "")
+    gat = FlowGather(ctx, (B, H, W, 2)) if (gather and ctx.world > 1) else None
+    if gat is not None:   # one untimed gather: the collective's first-use setup stays out of the timing
+        gat(out[-1] if out is not None else torch.zeros(B, H, W, 2, device=dev))
         gat.drain()
-    torch.cuda.synchronize(dev)
-    if out is not None:
-        assert out.shape == ((iters if all_iters else 1), B, H, W, 2) and bool(torch.isfinite(out[-1]).all())
     events = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     ctx.barrier()
     t0 = time.perf_counter()
@@ -235,6 +268,46 @@ def run_inference(ctx: Ctx, model, *, B: int, H: int, W: int, iters: int, steps:
         rec["gather_ms"] = round(_gather_ms(ctx, gat, out[-1] if out is not None else None, (B, H, W, 2)), 3)
     rec["tile_cfgs"] = dict(sorted(eng.chosen_cfgs.items()))
     return rec
+
+
+def run_sync_latency(ctx: Ctx, model, *, H: int, W: int, iters: int, steps: int, warmup: int, seed: int,
+                     engine_kw: dict) -> dict:
+    """The reference's own FPS protocol (validate_sintel.py:185-188,201-203), batch 1, one pair
+    at a time: host->device copy of the pair (from pageable host memory, like numpy inputs),
+    the forward with all ``iters`` upsampled predictions, then a synchronisation on the
+    result -- no overlap of consecutive pairs at all.  FPS = 1 / mean latency (x ranks for
+    N > 1, each rank timing its own pairs)."""
+    dev = ctx.dev
+    g = torch.Generator().manual_seed(seed + ctx.rank)
+    pairs = [(torch.rand(1, H, W, 3, generator=g) * 2 - 1, torch.rand(1, H, W, 3, generator=g) * 2 - 1)
+             for _ in range(4)]
+    err, lat = None, []
+    try:
+        eng = model.engine(dev, **dict(engine_kw, split=1))
+        for i in range(warmup):
+            a, b = pairs[i % 4]
+            eng.forward(a.to(dev), b.to(dev), iters)[-1]
+        torch.cuda.synchronize(dev)
+    except Exception as e:  # noqa: BLE001
+        err = e
+    agree(ctx, err is None, f"{type(err).__name__}: {err}" if err is not None else "")
+    ctx.barrier()
+    for i in range(steps):
+        a, b = pairs[i % 4]
+        t0 = time.perf_counter()
+        flow = eng.forward(a.to(dev), b.to(dev), iters)[-1]
+        torch.cuda.synchronize(dev)
+        lat.append(time.perf_counter() - t0)
+        assert flow.shape == (1, H, W, 2)
+    ctx.barrier()
+    mean = sum(lat) / len(lat)
+    mean_max = ctx.max_all(mean)
+    lat.sort()
+    return dict(value=round(ctx.world / mean_max, 3), latency_ms_mean=round(1000 * mean_max, 3),
+                latency_ms_p50=round(1000 * lat[len(lat) // 2], 3),
+                latency_ms_p99=round(1000 * lat[min(len(lat) - 1, int(0.99 * len(lat)))], 3),
+                steps=steps, warmup=warmup, protocol="per pair: H2D (pageable) + forward (all iterations "
+                "upsampled) + sync; no cross-pair overlap (validate_sintel.py:185-188)")
 
 
 def _gather_ms(ctx: Ctx, gat: FlowGather, flows, shape) -> float:
@@ -352,23 +425,38 @@ def main():
     if args.extras == "on" or (args.extras == "auto" and default_cfg):
         t_ex = time.perf_counter()
         ks, kw_ = args.extra_steps, max(3, args.warmup)
-        # fp32_b1_fps: the reference's own setting -- fp32 end to end, batch 1 (runtime/engine_f32.py)
-        plan = [("b1_fps", "raft_large", 32, BASELINE_FPS, "bf16"),
-                ("small_b1_fps_32it", "raft_small", 32, BASELINE_SMALL_FPS, "bf16"),
-                ("small_b1_fps_12it", "raft_small", 12, None, "bf16"),
-                ("fp32_b1_fps", "raft_large", 32, BASELINE_FPS, "fp32")]
-        for key, arch, it, base, prec in plan:
+        # *_b1_fps: batch-1 stream throughput (graph-pipelined: pair i's loop overlaps pair i+1's
+        # encoders); *_b1_sync: the reference's per-pair synchronous latency protocol (no overlap);
+        # fp32_b1_fps: the reference's own precision -- fp32 end to end (runtime/engine_f32.py);
+        # hires_b1: 1088x1920 frames (a 136x240 feature map), batch 1, 32 iterations
+        plan = [("b1_fps", "raft_large", 32, BASELINE_FPS, "bf16", "stream", (H, W)),
+                ("b1_sync", "raft_large", 32, BASELINE_FPS, "bf16", "sync", (H, W)),
+                ("small_b1_fps_32it", "raft_small", 32, BASELINE_SMALL_FPS, "bf16", "stream", (H, W)),
+                ("small_b1_sync_32it", "raft_small", 32, BASELINE_SMALL_FPS, "bf16", "sync", (H, W)),
+                ("small_b1_fps_12it", "raft_small", 12, None, "bf16", "stream", (H, W)),
+                ("fp32_b1_fps", "raft_large", 32, BASELINE_FPS, "fp32", "stream", (H, W)),
+                ("hires_b1", "raft_large", 32, None, "bf16", "stream", (1088, 1920))]
+        for key, arch, it, base, prec, proto, (eh, ew) in plan:
             try:
                 m = (raft_large if arch == "raft_large" else raft_small)(seed=0)[0].to(ctx.dev).eval()
-                r = run_inference(ctx, m, B=1, H=H, W=W, iters=it, steps=ks, warmup=kw_, final_only=False,
-                                  gather=not args.no_gather, seed=99,
-                                  engine_kw=dict(engine_kw, split=1, precision=prec))
-                r.pop("tile_cfgs", None)
-                r["config"] = dict(model=arch, per_gpu_batch=1, num_flow_updates=it, image_size=[H, W], dtype=prec)
+                if proto == "sync":
+                    r = run_sync_latency(ctx, m, H=eh, W=ew, iters=it, steps=ks, warmup=kw_, seed=99,
+                                         engine_kw=dict(engine_kw, precision=prec))
+                else:
+                    r = run_inference(ctx, m, B=1, H=eh, W=ew, iters=it, steps=ks, warmup=kw_, final_only=False,
+                                      gather=not args.no_gather, seed=99,
+                                      engine_kw=dict(engine_kw, split=1, precision=prec), guarded=True)
+                    r.pop("tile_cfgs", None)
+                r["config"] = dict(model=arch, per_gpu_batch=1, num_flow_updates=it, image_size=[eh, ew], dtype=prec)
                 r["vs_baseline"] = round(r["value"] / ctx.world / base, 3) if base else None
                 extras[key] = r
                 del m
-            except Exception as e:  # noqa: BLE001 -- a failed extra must not lose the headline
+            except ExtraFailed as e:   # failed on some rank; every rank lands here together
+                extras[key] = None
+                print(f"bench.py: extra {key} failed on a rank: {e}", file=sys.stderr)
+            except Exception as e:  # noqa: BLE001 -- single-rank: a failed extra must not lose the headline
+                if ctx.world > 1:
+                    raise   # a failure inside a timed (collective) phase cannot be isolated per rank
                 extras[key] = None
                 print(f"bench.py: extra {key} failed: {type(e).__name__}: {e}", file=sys.stderr)
             torch.cuda.empty_cache()
@@ -377,6 +465,8 @@ def main():
                                                        size=tuple(args.train_size), iters=12,
                                                        steps=max(2, ks // 2), warmup=3)
         except Exception as e:  # noqa: BLE001
+            if ctx.world > 1:
+                raise   # the DP step's gradient all-reduce cannot be left mid-way on one rank
             extras["train_pairs_per_s"] = None
             print(f"bench.py: extra train_pairs_per_s failed: {type(e).__name__}: {e}", file=sys.stderr)
         extras["extras_wall_s"] = round(time.perf_counter() - t_ex, 1)

@@ -118,21 +118,52 @@ class InstanceNorm(nn.Module):
 
 NORM_BATCH = "batch"
 NORM_INSTANCE = "instance"
+NORM_CUSTOM = "custom"
+
+
+def norm_kind(norm) -> Optional[str]:
+    """A norm given like the reference's ``norm_layer`` (``model.py:702-711``: a class or a
+    partial of one) or by name: "batch" / "instance" / None for the built-in Flax norms
+    (:class:`BatchNorm` / :class:`InstanceNorm` classes map to them), "custom" for any other
+    callable ``norm(channels) -> module`` (``module(x, train)`` or ``module(x)``), which runs
+    on the op-by-op path (the native engine lowers the built-in norms only)."""
+    if norm is None or norm in (NORM_BATCH, NORM_INSTANCE):
+        return norm
+    if norm is BatchNorm:
+        return NORM_BATCH
+    if norm is InstanceNorm:
+        return NORM_INSTANCE
+    if callable(norm):
+        return NORM_CUSTOM
+    raise ValueError(f"unknown norm layer {norm!r}")
+
+
+def _call_norm(m: nn.Module, x, train: bool):
+    import inspect
+
+    try:
+        n = len(inspect.signature(m.forward).parameters)
+    except (TypeError, ValueError):
+        n = 1
+    return m(x, train) if n >= 2 else m(x)
 
 
 class ConvNormActivation(nn.Module):
     """Conv -> optional norm -> optional relu; children ``layers_0``/``layers_1``.
-    Reference ``model.py:120-159``."""
+    Reference ``model.py:120-159``.  ``norm``: see :func:`norm_kind`."""
 
     def __init__(self, cin, cout, kernel_size=(3, 3), stride=(1, 1), padding=None,
-                 norm: Optional[str] = NORM_BATCH, relu: bool = True, gen=None):
+                 norm=NORM_BATCH, relu: bool = True, gen=None):
         super().__init__()
         self.layers_0 = Conv(cin, cout, kernel_size, stride, padding, init="kaiming", gen=gen)
-        self.norm = norm
-        if norm == NORM_BATCH:
+        kind = norm_kind(norm)
+        self.norm = kind
+        if kind == NORM_BATCH:
             self.layers_1 = BatchNorm(cout)
-        elif norm == NORM_INSTANCE:
+        elif kind == NORM_INSTANCE:
             self._in = InstanceNorm()
+        elif kind == NORM_CUSTOM:
+            self.layers_1 = norm(cout)
         self.relu = relu
 
     def forward(self, x, train: bool):
@@ -141,6 +172,8 @@ class ConvNormActivation(nn.Module):
             x = self.layers_1(x, train)
         elif self.norm == NORM_INSTANCE:
             x = self._in(x)
+        elif self.norm == NORM_CUSTOM:
+            x = _call_norm(self.layers_1, x, train)
         if self.relu:
             x = torch.relu(x)
         return x
@@ -189,6 +222,18 @@ class BottleneckBlock(nn.Module):
 BLOCKS = {"residual": ResidualBlock, "bottleneck": BottleneckBlock}
 
 
+def block_factory(block):
+    """A residual unit given like the reference's ``block`` (``model.py:702-711``: the class
+    itself) or by name ("residual" / "bottleneck"); any other callable
+    ``block(cin, cout, norm, stride, gen) -> module`` (``module(x, train)``) is accepted too
+    and runs on the op-by-op path."""
+    if isinstance(block, str):
+        return BLOCKS[block]
+    if callable(block):
+        return block
+    raise ValueError(f"unknown block {block!r}")
+
+
 class Sequential(nn.Module):
     """Registered sequential: children ``layers_0``, ``layers_1`` (``model.py:107-117``)."""
 
@@ -207,13 +252,14 @@ class Sequential(nn.Module):
 class FeatureEncoder(nn.Module):
     """Feature / context encoder, downsamples x8.  Reference ``model.py:219-257``."""
 
-    def __init__(self, block: str = "residual", layers=(64, 64, 96, 128, 256),
-                 strides=((2, 2), (1, 1), (2, 2), (2, 2)), norm: Optional[str] = NORM_BATCH, in_channels: int = 3,
+    def __init__(self, block="residual", layers=(64, 64, 96, 128, 256),
+                 strides=((2, 2), (1, 1), (2, 2), (2, 2)), norm=NORM_BATCH, in_channels: int = 3,
                  gen=None):
         super().__init__()
         assert len(layers) == 5
-        B = BLOCKS[block]
-        self.block, self.layers, self.strides, self.norm_kind = block, tuple(layers), tuple(strides), norm
+        B = block_factory(block)
+        self.block = next((k for k, v in BLOCKS.items() if v is B), "custom")
+        self.layers, self.strides, self.norm_kind = tuple(layers), tuple(strides), norm_kind(norm)
         self.convnormrelu = ConvNormActivation(in_channels, layers[0], (7, 7), strides[0], norm=norm, gen=gen)
         self.layer1 = Sequential(B(layers[0], layers[1], norm, strides[1], gen), B(layers[1], layers[1], norm, (1, 1), gen))
         self.layer2 = Sequential(B(layers[1], layers[2], norm, strides[2], gen), B(layers[2], layers[2], norm, (1, 1), gen))

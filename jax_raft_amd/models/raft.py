@@ -66,6 +66,7 @@ class RAFT(nn.Module):
         self.update_block = update_block
         self.mask_predictor = mask_predictor
         self._engines: Dict[Any, Any] = {}
+        self._lowering_error: Optional[str] = None
         self.arch: Optional[str] = None
 
     # ------------------------------------------------------------ API surface
@@ -89,9 +90,28 @@ class RAFT(nn.Module):
 
                 out = raft_forward_autograd(self, image1, image2, train, num_flow_updates, fused=fused)
                 return out if return_all_iters else out[-1:]
-            return self.engine(image1.device, **engine_kw).forward(image1, image2, num_flow_updates,
-                                                                   return_all_iters=return_all_iters)
+            eng = None if self._lowering_error is not None else self._try_engine(image1.device, engine_kw)
+            if eng is not None:
+                return eng.forward(image1, image2, num_flow_updates, return_all_iters=return_all_iters)
+            # a model the engine cannot lower (injected sub-modules, custom blocks / norms, channel
+            # counts outside the fused kernels' tiling): op by op on the same native kernels
+            # (convs, correlation pyramid, lookup: ops/functional.py), no graph
+            with torch.no_grad():
+                return self.forward_reference(image1, image2, False, num_flow_updates, return_all_iters)
         return self.forward_reference(image1, image2, train, num_flow_updates, return_all_iters)
+
+    def _try_engine(self, device, engine_kw):
+        """The native engine, or None (remembering why) when it cannot lower this model."""
+        try:
+            return self.engine(device, **engine_kw)
+        except NotImplementedError as e:
+            self._lowering_error = str(e)
+            return None
+
+    @property
+    def execution_path(self) -> str:
+        """"engine" (native plan / hipGraph) or "op-by-op: <why the engine cannot lower it>"."""
+        return "engine" if self._lowering_error is None else f"op-by-op: {self._lowering_error}"
 
     def apply(self, variables: Mapping[str, Any], image1, image2, train: bool = False, num_flow_updates: int = 12,
               mutable=False, **kw):
@@ -168,7 +188,16 @@ class RAFT(nn.Module):
 
     def _apply(self, fn, *args, **kwargs):  # drop engines when moved / cast
         self._engines = {}
+        self._lowering_error = None
         return super()._apply(fn, *args, **kwargs)
+
+    def __setattr__(self, name, value):
+        # a replaced sub-module may make the model lowerable again (or not): re-decide
+        if name in ("feature_encoder", "context_encoder", "corr_block", "update_block", "mask_predictor"):
+            self.__dict__["_lowering_error"] = None
+            if "_engines" in self.__dict__:
+                self.__dict__["_engines"] = {}
+        super().__setattr__(name, value)
 
 
 def _same_leaves(a: Mapping[str, Any], b: Mapping[str, Any]) -> bool:

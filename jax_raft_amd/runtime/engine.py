@@ -37,11 +37,18 @@ import torch
 
 from ..models.layers import (
     NORM_BATCH,
+    NORM_CUSTOM,
     NORM_INSTANCE,
     BottleneckBlock,
     ConvNormActivation,
+    CorrBlock,
     FeatureEncoder,
+    FlowHead,
+    MaskPredictor,
+    MotionEncoder,
+    RecurrentBlock,
     ResidualBlock,
+    UpdateBlock,
 )
 from ..ops import native as nat
 from . import tunedb
@@ -239,7 +246,16 @@ class RaftEngine:
         for enc in (fe, ce):
             if not isinstance(enc, FeatureEncoder):
                 raise NotImplementedError("native engine supports FeatureEncoder encoders only")
+            if enc.block == "custom" or enc.norm_kind == NORM_CUSTOM:
+                raise NotImplementedError("native engine lowers residual / bottleneck blocks with batch / "
+                                          "instance / no norm only")
         ub = m.update_block
+        if not (isinstance(ub, UpdateBlock) and isinstance(ub.motion_encoder, MotionEncoder)
+                and isinstance(ub.recurrent_block, RecurrentBlock) and isinstance(ub.flow_head, FlowHead)
+                and isinstance(m.corr_block, CorrBlock)
+                and (m.mask_predictor is None or isinstance(m.mask_predictor, MaskPredictor))):
+            raise NotImplementedError("native engine lowers the reference update block / correlation block / "
+                                      "mask predictor classes only")
         me, rb, fh = ub.motion_encoder, ub.recurrent_block, ub.flow_head
         self.hidden = rb.hidden_size
         self.ctx_ch = ce.out_channels - self.hidden

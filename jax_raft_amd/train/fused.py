@@ -243,6 +243,9 @@ def supported(model) -> bool:
     me, rb = ub.motion_encoder, ub.recurrent_block
     if not isinstance(model.feature_encoder, FeatureEncoder) or not isinstance(model.context_encoder, FeatureEncoder):
         return False
+    if any(e.block == "custom" or e.norm_kind not in (None, "batch", "instance")
+           for e in (model.feature_encoder, model.context_encoder)):
+        return False
     hd = rb.hidden_size
     ctx = model.context_encoder.out_channels - hd
     if hd % 16 or ctx <= 0 or me.out_channels < 3 or model.feature_encoder.out_channels % 64:

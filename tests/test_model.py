@@ -153,3 +153,33 @@ def test_apply_foreign_batch_stats_returned_not_written():
     assert np.array_equal(arr, snapshot)            # caller's arrays not written
     assert torch.equal(model.context_encoder.convnormrelu.layers_1.mean, own_before)
     assert not torch.allclose(upd.cpu(), torch.as_tensor(snapshot))
+
+
+def test_block_and_norm_as_classes_or_callables():
+    """Reference ``model.py:702-711`` passes the residual unit and the norm as classes: the
+    built-in classes map to the engine-lowerable kinds, any other callable is a custom
+    module (its parameters appear under ``layers_1`` like a Flax norm)."""
+    from torch import nn
+
+    from jax_raft_amd.models.layers import (BatchNorm, BottleneckBlock, FeatureEncoder, InstanceNorm,
+                                            ResidualBlock, norm_kind)
+
+    assert norm_kind(BatchNorm) == "batch" and norm_kind(InstanceNorm) == "instance" and norm_kind(None) is None
+
+    class Affine(nn.Module):
+        def __init__(self, c):
+            super().__init__()
+            self.scale = nn.Parameter(torch.ones(c))
+
+        def forward(self, x):
+            return x * self.scale
+
+    fe = FeatureEncoder(block=ResidualBlock, layers=(32, 32, 48, 64, 128), norm=InstanceNorm)
+    assert fe.block == "residual" and fe.norm_kind == "instance"
+    ce = FeatureEncoder(block=BottleneckBlock, layers=(32, 32, 64, 96, 160), norm=Affine)
+    assert ce.block == "bottleneck" and ce.norm_kind == "custom"
+    model, variables = raft_small(feature_encoder=fe, context_encoder=ce)
+    assert "layers_1" in variables["params"]["context_encoder"]["convnormrelu"]
+    x = torch.rand(1, 128, 128, 3) * 2 - 1
+    out = model(x, x, num_flow_updates=2)
+    assert out.shape == (2, 1, 128, 128, 2) and torch.isfinite(out).all()
