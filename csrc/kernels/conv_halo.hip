@@ -1,0 +1,248 @@
+// Halo 3x3 / stride-1 convolution: every 3x3 "same" conv of the reference RAFT
+// (jax_raft/model.py:120-159 ConvNormActivation inside the encoders' residual /
+// bottleneck blocks :162-216, the motion encoder :275-289, flow head :347-349, mask
+// predictor :389-390) as an alternative tile kernel to the implicit GEMM.
+//
+// The implicit GEMM (conv_igemm.h) re-derives an im2col row descriptor for every staged
+// row of every K stage; on the encoder shapes that per-tile address arithmetic, not MFMA
+// or memory, bounds it (~1400 VALU + 1050 SALU per wave for 72 MFMAs, profiles/
+// r3_encoder_conv_study.md).  Here a workgroup owns a TR x TC block of output pixels,
+// loads its (TR + 2) x (TC + 2) input footprint into LDS once (zero outside the image),
+// and reads the B fragment of tap (u, v) for output pixel (i, j) from footprint row
+// (i + u) * (TC + 2) + j + v: a constant offset per tap, no per-stage descriptors.  The
+// weights stream per wave from L2 in MFMA fragment order (ops/native.py:pack_gru_halo,
+// one contiguous 1 KB load per 32 x 16 fragment) through a register ring; each fragment
+// feeds TN 32-pixel blocks (A bytes per MFMA = 1 KB / TN).
+//
+// Waves: WCO x WPX; wave (wc, wp) computes output channels co0 + 32 wc + [0, 32) for the
+// pixel blocks wp * TN + [0, TN) of the tile.  Epilogue = EPI_STD of conv_igemm (bias,
+// residual pre / post, relu, bf16 store + copy), plus optional per-channel (sum, sumsq)
+// partials of the stored values for a following instance norm.
+#include "halo.h"
+
+namespace {
+
+// footprint image row pitch P chunks (16 B) for cin <= 8 P; XOR-swizzled so that the 16
+// lanes of a ds_read_b128 group (16 consecutive pixel rows, one chunk) hit 16 distinct
+// 16-B slots of the 256-B bank window
+template <int P>
+JR_DEVICE int fp_off(int row, int chunk) {
+  if constexpr (P == 8) return row * 64 + ((chunk ^ ((row >> 1) & 7)) << 3);
+  else if constexpr (P == 16) return row * 128 + (((chunk ^ row) & 15) << 3);
+  else return row * 256 + (((chunk & 16) | ((chunk ^ row) & 15)) << 3);
+}
+
+template <int CIN>
+constexpr int pitch_of() { return CIN <= 64 ? 8 : CIN <= 128 ? 16 : 32; }
+
+template <int CIN, int WCO, int WPX, int TN>
+__global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHaloParams p) {
+  constexpr int NT = 64 * WCO * WPX;
+  constexpr int P = pitch_of<CIN>();
+  constexpr int CC = CIN / 8;
+  constexpr int SPT = CIN / 16;           // k-steps per tap
+  constexpr int S = 9 * SPT;
+  constexpr int PD = S >= 16 ? 16 : S;
+  extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rho = lane & 31, hh = lane >> 5;
+  const int wc = wave % WCO, wp = wave / WCO;
+
+  const int per_img = p.tiles_y * p.tiles_x;
+  const int n = blockIdx.x / per_img;
+  const int rem = blockIdx.x - n * per_img;
+  const int ty = rem / p.tiles_x, tx = rem - ty * p.tiles_x;
+  const int y0 = ty * p.TR, x0 = tx * p.TC;
+  const int FW = p.TC + 2;
+  const int nfp = (p.TR + 2) * FW;
+  const int co_blk = blockIdx.y * WCO + wc;   // this wave's 32-channel output block
+
+  // weight ring first (its latency overlaps the footprint load)
+  const __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)p.w_bytes, 0x00020000);
+  const unsigned w_base = (unsigned)(co_blk * S * 64 + lane) * 16u;
+  bf16x8 ring[PD];
+#pragma unroll
+  for (int d = 0; d < PD; ++d) ring[d] = __builtin_bit_cast(bf16x8, bload(ws, w_base + (unsigned)d * 1024u));
+
+  // footprint -> LDS
+  {
+    const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
+    const int total = nfp * CC;
+    const int HW = p.H * p.W;
+    for (int base = 0; base < total; base += 4 * NT) {
+      u32x4 v[4];
+      int fr[4], ch[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int idx = base + k * NT + tid;
+        const int f = idx / CC, c = idx - f * CC;
+        const int fy = f / FW, fx = f - fy * FW;
+        const int y = y0 - 1 + fy, x = x0 - 1 + fx;
+        const bool in = idx < total && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
+        fr[k] = idx < total ? f : -1;
+        ch[k] = c;
+        const unsigned off = (unsigned)((n * HW + y * p.W + x) * p.xcs + p.xoff + 8 * c) * 2u;
+        v[k] = bload(xs, in ? off : HOOB);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (fr[k] >= 0) *(u32x4*)(lds + fp_off<P>(fr[k], ch[k])) = v[k];
+    }
+  }
+
+  // this lane's output pixels: footprint row of tap (0, 0), image pixel (-1: none)
+  int frow[TN], om[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int q = 32 * (wp * TN + b) + rho;
+    const int i = q / p.TC, j = q - i * p.TC;
+    const bool ok = i < p.TR && y0 + i < p.H && x0 + j < p.W;
+    frow[b] = ok ? i * FW + j : 0;
+    om[b] = ok ? (n * p.H + y0 + i) * p.W + x0 + j : -1;
+  }
+  __syncthreads();
+
+  f32x16 acc[TN];
+  pipe_gemm<TN, S, PD>(
+      acc, ring,
+      [&](int s) { return __builtin_bit_cast(bf16x8, bload(ws, w_base + (unsigned)s * 1024u)); },
+      [&](int s, int b) {
+        const int tap = s / SPT, kc = s - tap * SPT;
+        const int row = frow[b] + (tap / 3) * FW + tap % 3;
+        return *(const bf16x8*)(lds + fp_off<P>(row, 2 * kc + hh));
+      });
+
+  // epilogue: lane holds channels c0 .. c0 + 15 of pixel om[b]
+  const int c0 = 32 * co_blk + 16 * hh;
+  if (c0 >= p.cout) return;
+  const bool full = c0 + 16 <= p.cout;
+  float bv[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) bv[k] = c0 + k < p.cout ? p.bias[c0 + k] : 0.f;
+  float ssum[16], ssq[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) ssum[k] = ssq[k] = 0.f;
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int m = om[b];
+    if (m < 0) continue;
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = acc[b][k] + bv[k];
+    float r[16];
+    if (p.res) {
+      const bf16* rp = (const bf16*)p.res + (long)m * p.rcs + p.roff + c0;
+      if (full) load_bf16<16>(rp, r);
+      else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) r[k] = c0 + k < p.cout ? bf2f(rp[k]) : 0.f;
+      }
+      if (!p.res_post) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] += r[k];
+      }
+    }
+    if (p.act == ACT_RELU) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = fmaxf(v[k], 0.f);
+    }
+    if (p.res && p.res_post) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = fmaxf(v[k] + r[k], 0.f);
+    }
+    bf16* yp = (bf16*)p.y + (long)m * p.ycs + p.yoff + c0;
+    bf16* y2p = p.y2 ? (bf16*)p.y2 + (long)m * p.y2cs + p.y2off + c0 : nullptr;
+    if (full) {
+      store_bf16<16>(yp, v);
+      if (y2p) store_bf16<16>(y2p, v);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (c0 + k < p.cout) {
+          yp[k] = f2bf(v[k]);
+          if (y2p) y2p[k] = f2bf(v[k]);
+        }
+    }
+    if (p.stats_part) {   // statistics of the stored (bf16-rounded) values, as channel_stats reads them
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const float s = bf2f(f2bf(v[k]));
+        ssum[k] += s;
+        ssq[k] += s * s;
+      }
+    }
+  }
+  if (p.stats_part) {
+    // sum over the 32 pixel lanes of each lane half (channels 16 hh + k), then lane rho 0 writes
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) {
+        ssum[k] += __shfl_xor(ssum[k], o, 64);
+        ssq[k] += __shfl_xor(ssq[k], o, 64);
+      }
+    }
+    if (rho == 0) {
+      const int nb = per_img * WPX;
+      float* o = p.stats_part + (((long)n * nb + rem * WPX + wp) * p.cout + c0) * 2;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (c0 + k < p.cout) *(float2*)(o + 2 * k) = make_float2(ssum[k], ssq[k]);
+    }
+  }
+}
+
+struct HaloCfg {
+  int cin, wco, wpx, tn, tr, tc;
+};
+
+// tile configs (cfg id = index): encoder shapes (64 / 96 / 128 channels, large pixel tiles
+// sharing each weight fragment across 2-4 pixel blocks) and the refinement loop's 128 / 256-
+// channel convs at batch 1 (small tiles: 7040 pixels must still give >= 256 workgroups)
+constexpr HaloCfg kCfgs[] = {
+    {64, 2, 2, 4, 16, 16},  {64, 2, 2, 2, 8, 16},  {96, 3, 2, 2, 8, 16},  {96, 3, 1, 2, 4, 16},
+    {128, 4, 2, 2, 8, 16},  {128, 4, 1, 2, 4, 16}, {128, 2, 2, 2, 8, 16}, {128, 2, 1, 1, 4, 8},
+    {256, 2, 2, 2, 8, 16},  {256, 2, 1, 1, 4, 8},  {128, 4, 1, 1, 4, 8},  {256, 4, 1, 1, 4, 8},
+    {256, 2, 1, 2, 4, 16},
+};
+constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
+
+int lds_bytes(const HaloCfg& c) {
+  const int P = c.cin <= 64 ? 8 : c.cin <= 128 ? 16 : 32;
+  return (c.tr + 2) * (c.tc + 2) * P * 16;
+}
+
+template <int CIN, int WCO, int WPX, int TN>
+int launch(const ConvHaloParams& p, hipStream_t s, int lds) {
+  static const bool attr = hipFuncSetAttribute((const void*)conv_halo_kernel<CIN, WCO, WPX, TN>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  if (!attr) return (int)hipErrorInvalidValue;
+  const int cpad = (p.cout + 32 * WCO - 1) / (32 * WCO);
+  hipLaunchKernelGGL((conv_halo_kernel<CIN, WCO, WPX, TN>), dim3(p.ntiles, cpad), dim3(64 * WCO * WPX), lds, s, p);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int jr_conv_halo_cfg(int cfg, int* o) {
+  if (cfg < 0 || cfg >= kNumCfgs) return 0;
+  const HaloCfg& c = kCfgs[cfg];
+  o[0] = c.cin; o[1] = c.wco; o[2] = c.wpx; o[3] = c.tn; o[4] = c.tr; o[5] = c.tc;
+  return 1;
+}
+
+extern "C" int jr_conv_halo_lds(int cfg) { return cfg < 0 || cfg >= kNumCfgs ? 0 : lds_bytes(kCfgs[cfg]); }
+
+extern "C" int jr_conv_halo(const ConvHaloParams* p, int cfg, hipStream_t stream) {
+  if (cfg < 0 || cfg >= kNumCfgs || p->ntiles <= 0) return (int)hipErrorInvalidValue;
+  const HaloCfg& c = kCfgs[cfg];
+  const int lds = lds_bytes(c);
+#define JR_HALO_CONV(CIN_, WCO_, WPX_, TN_) \
+  if (c.cin == CIN_ && c.wco == WCO_ && c.wpx == WPX_ && c.tn == TN_) return launch<CIN_, WCO_, WPX_, TN_>(*p, stream, lds);
+  JR_HALO_CONV(64, 2, 2, 4) JR_HALO_CONV(64, 2, 2, 2) JR_HALO_CONV(96, 3, 2, 2) JR_HALO_CONV(96, 3, 1, 2)
+  JR_HALO_CONV(128, 4, 2, 2) JR_HALO_CONV(128, 4, 1, 2) JR_HALO_CONV(128, 2, 2, 2) JR_HALO_CONV(128, 2, 1, 1)
+  JR_HALO_CONV(256, 2, 2, 2) JR_HALO_CONV(256, 2, 1, 1) JR_HALO_CONV(128, 4, 1, 1) JR_HALO_CONV(256, 4, 1, 1)
+  JR_HALO_CONV(256, 2, 1, 2)
+#undef JR_HALO_CONV
+  return (int)hipErrorInvalidValue;
+}

@@ -326,6 +326,11 @@ extern "C" int jr_channel_stats(const void* x, int N, int HW, int C, float* stat
 
 extern "C" int jr_channel_stats_partials(int N, int HW) { return N * ((HW + STATS_ROWS - 1) / STATS_ROWS); }
 
+extern "C" int jr_channel_stats_final(const float* part, int N, int nb, int C, float* stats, hipStream_t stream) {
+  hipLaunchKernelGGL(channel_stats_final_kernel, dim3((2 * C + 63) / 64, N), dim3(256), 0, stream, part, N, nb, C, stats);
+  return (int)hipGetLastError();
+}
+
 extern "C" int jr_norm_act(const void* x, const float* sx, int mode_x, const float* gamma, const float* beta,
                            const void* res, const float* sr, int mode_r, const float* gamma_r, const float* beta_r,
                            void* y, int N, int HW, int C, float eps, int relu, hipStream_t stream) {

@@ -385,6 +385,32 @@ struct GruHaloParams {
 int jr_gru_halo(const GruHaloParams* p, hipStream_t stream);
 // LDS bytes of one workgroup (0: the configuration is not supported)
 int jr_gru_halo_lds(int hd, int mode, int TR, int TC, int nb1, int nb2);
+// Halo 3x3 / stride-1 conv (conv_halo.hip): a TR x TC tile of output pixels per workgroup,
+// its (TR + 2) x (TC + 2) input footprint loaded into LDS once, B fragments read from it
+// shifted by the tap (no im2col address arithmetic), weights streamed in MFMA fragment order
+// (ops/native.py:pack_gru_halo).  EPI_STD semantics of conv_igemm (bias, residual pre / post,
+// relu, bf16 output + copy) plus an optional per-channel statistics output.
+struct ConvHaloParams {
+  const void* x; int xcs, xoff;        // bf16 NHWC input [N][H][W][xcs], channels xoff .. xoff + cin
+  int N, H, W, cin;
+  const void* w; long w_bytes;         // pack_gru_halo(kernel (3, 3, cin, cout_pad), cin)
+  const float* bias; int cout;         // real output channels
+  int act;                             // ACT_NONE / ACT_RELU
+  void* y; int ycs, yoff;              // bf16 output
+  void* y2; int y2cs, y2off;           // optional bf16 copy
+  const void* res; int rcs, roff, res_post;   // optional bf16 residual (0: act(v + r), 1: relu(act(v) + r))
+  float* stats_part;                   // optional [N][tiles_per_img * WPX][cout][2] (sum, sumsq) partials
+  int TR, TC, tiles_y, tiles_x, ntiles;
+  long x_bytes;
+};
+// cfg: index into the halo tile-config table (conv_halo.hip); 0 on success
+int jr_conv_halo(const ConvHaloParams* p, int cfg, hipStream_t stream);
+// table entry: {cin, WCO, WPX, TN, TR, TC} (returns 0 for an unknown cfg); LDS bytes
+int jr_conv_halo_cfg(int cfg, int* out6);
+int jr_conv_halo_lds(int cfg);
+// per-channel stats [N][C][2] from partials [N][nb][C][2] (channel_stats_final_kernel)
+int jr_channel_stats_final(const float* part, int N, int nb, int C, float* stats, hipStream_t stream);
+
 // Grouped launch of two EPI_STD convs with one tile config (conv_fam_grp.hip); ok: the configs it serves.
 int jr_conv_grouped(const ConvParams* p1, const ConvParams* p2, int cfg, hipStream_t stream);
 int jr_conv_grouped_ok(int cfg);

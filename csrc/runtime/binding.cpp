@@ -199,8 +199,76 @@ static ConvParams build_conv(const TList& t, const IList& i, double alpha, std::
   return p;
 }
 
+// Tile configs >= kHaloCfg0 select the halo 3x3 kernel (conv_halo.hip, table index cfg - kHaloCfg0)
+// for an EPI_STD 3x3 / stride-1 / pad-1 conv; its weights (ops/native.py:pack_gru_halo of the
+// kernel, cout padded to 32) come as t[12].  Optional t[13]: per-channel statistics partials.
+constexpr int kHaloCfg0 = 100;
+
+bool conv_halo_ok_cfg(int64_t cfg, int64_t cin8, int64_t cout) {
+  int c[6];
+  if (!jr_conv_halo_cfg((int)(cfg - kHaloCfg0), c)) return false;
+  return c[0] == cin8 && cout <= 512 && jr_conv_halo_lds((int)(cfg - kHaloCfg0)) <= 160 * 1024;
+}
+
+static Launch make_conv_halo(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep) {
+  TORCH_CHECK(i.size() >= 22, "conv: expected >= 22 ints");
+  const int cfg = (int)i[20] - kHaloCfg0;
+  int c[6];
+  TORCH_CHECK(jr_conv_halo_cfg(cfg, c), "conv_halo: unknown tile config ", i[20]);
+  at::Tensor x = opt(t, 0), bias = opt(t, 2), y = opt(t, 3), y2 = opt(t, 4), res = opt(t, 5), wh = opt(t, 12),
+             part = opt(t, 13);
+  check_bf16(x, "x"); check_f32(bias, "bias"); check_bf16(y, "y"); check_bf16(wh, "halo weights");
+  const int N = (int)i[0], H = (int)i[1], W = (int)i[2], xoff = (int)i[3], cin8 = (int)i[4];
+  const int KH = (int)i[5], KW = (int)i[6], SH = (int)i[7], SW = (int)i[8], PH = (int)i[9], PW = (int)i[10];
+  const int cout = (int)i[11], act = (int)i[12], epi = (int)i[19];
+  TORCH_CHECK(KH == 3 && KW == 3 && SH == 1 && SW == 1 && PH == 1 && PW == 1 && epi == EPI_STD &&
+                  (act == 0 || act == 1) && alpha == 1.0 && !opt(t, 11).defined() &&   // ACT_NONE / ACT_RELU
+                  !opt(t, 6).defined() && (i.size() < 26 || (i[22] <= 0 && i[23] <= 0 && i[24] == 0 && i[25] == 0)),
+              "conv_halo: a 3x3 / stride-1 / pad-1 EPI_STD conv (relu / none, no alpha / bias map / state)");
+  TORCH_CHECK(c[0] == cin8 && cin8 % 16 == 0, "conv_halo: config ", i[20], " is for ", c[0], " input channels, got ", cin8);
+  const int cpad = (cout + 31) / 32 * 32;
+  TORCH_CHECK(wh.numel() == (int64_t)cpad * 9 * cin8, "conv_halo: halo weights (pack_gru_halo, cout padded to 32)");
+  TORCH_CHECK(cs(x) % 8 == 0 && xoff % 8 == 0 && xoff + cin8 <= cs(x) && x.numel() >= (int64_t)N * H * W * cs(x),
+              "conv_halo: input channel slice");
+  const int64_t M = (int64_t)N * H * W;
+  TORCH_CHECK(cs(y) % 8 == 0 && (int)i[14] % 8 == 0 && (int)i[14] + cout <= cs(y) && y.numel() >= M * cs(y), "conv_halo: y");
+  ConvHaloParams p{};
+  p.x = x.data_ptr(); p.xcs = cs(x); p.xoff = xoff; p.N = N; p.H = H; p.W = W; p.cin = cin8;
+  p.w = wh.data_ptr(); p.w_bytes = (long)wh.numel() * 2;
+  p.bias = bias.data_ptr<float>(); p.cout = cout; p.act = act;
+  p.y = y.data_ptr(); p.ycs = cs(y); p.yoff = (int)i[14];
+  if (y2.defined()) {
+    check_bf16(y2, "y2");
+    TORCH_CHECK(cs(y2) % 8 == 0 && (int)i[15] % 8 == 0 && (int)i[15] + cout <= cs(y2) && y2.numel() >= M * cs(y2), "conv_halo: y2");
+    p.y2 = y2.data_ptr(); p.y2cs = cs(y2); p.y2off = (int)i[15];
+  }
+  if (res.defined()) {
+    check_bf16(res, "res");
+    TORCH_CHECK(cs(res) % 8 == 0 && (int)i[16] % 8 == 0 && (int)i[16] + cout <= cs(res) && res.numel() >= M * cs(res),
+                "conv_halo: residual");
+    p.res = res.data_ptr(); p.rcs = cs(res); p.roff = (int)i[16]; p.res_post = (int)i[21];
+  }
+  p.TR = c[4]; p.TC = c[5];
+  p.tiles_y = (H + p.TR - 1) / p.TR; p.tiles_x = (W + p.TC - 1) / p.TC;
+  const int64_t nt = (int64_t)N * p.tiles_y * p.tiles_x;
+  TORCH_CHECK(nt < (1LL << 31), "conv_halo: too many tiles");
+  p.ntiles = (int)nt;
+  if (part.defined()) {
+    check_f32(part, "stats partials");
+    TORCH_CHECK(part.numel() >= (int64_t)N * p.tiles_y * p.tiles_x * c[2] * cout * 2, "conv_halo: stats partials too small");
+    p.stats_part = part.data_ptr<float>();
+  }
+  p.x_bytes = (long)x.numel() * 2;
+  TORCH_CHECK(p.x_bytes < (1LL << 31), "conv_halo: input larger than 2 GiB");
+  for (const at::Tensor* v : {&x, &wh, &y})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(v->data_ptr()) % 16 == 0, "conv_halo: 16-byte aligned operands");
+  if (keep) for (auto& v : {x, bias, y, y2, res, wh, part}) if (v.defined()) keep->push_back(v);
+  return [p, cfg](hipStream_t s, int) { return jr_conv_halo(&p, cfg, s); };
+}
+
 static Launch make_conv(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep,
                         const TList* tx = nullptr, const IList* ix = nullptr) {
+  if (i.size() >= 22 && i[20] >= kHaloCfg0 && tx == nullptr) return make_conv_halo(t, i, alpha, keep);
   int epi = 0, cfg = 0;
   const ConvParams p = build_conv(t, i, alpha, keep, tx, ix, &epi, &cfg);
   return [p, epi, cfg](hipStream_t s, int) { return jr_conv_forward(&p, cfg, epi, s); };
@@ -210,6 +278,12 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
 // that ping-pongs between two buffers (raft_small's FlowHead after the single-stage halo GRU).
 static Launch make_conv_alt(const TList& t, const IList& i, double alpha, const at::Tensor& x_alt,
                             std::vector<at::Tensor>* keep) {
+  if (i.size() >= 22 && i[20] >= kHaloCfg0) {   // halo kernel: two launch closures
+    TList t2 = t.copy();
+    t2.set(0, c10::optional<at::Tensor>(x_alt));
+    Launch a = make_conv_halo(t, i, alpha, keep), b = make_conv_halo(t2, i, alpha, keep);
+    return [a, b](hipStream_t s, int it) { return (it & 1) ? b(s, it) : a(s, it); };
+  }
   int epi = 0, cfg = 0;
   const ConvParams p = build_conv(t, i, alpha, keep, nullptr, nullptr, &epi, &cfg);
   const at::Tensor x = opt(t, 0);
@@ -1451,6 +1525,25 @@ void flow_taps_op(const TList& t, IList i) { run_now(make_flow_taps(t, i, nullpt
 void taps_gemm_op(const TList& t, IList i) { run_now(make_taps_gemm(t, i, nullptr)); }
 void gru_fused_op(const TList& t, IList i) { run_now(make_gru_fused(t, i, nullptr)); }
 void gru_halo_op(const TList& t, IList i) { run_now(make_gru_halo(t, i, nullptr)); }
+bool conv_halo_ok_op(int64_t cfg, int64_t cin8, int64_t cout) { return conv_halo_ok_cfg(cfg, cin8, cout); }
+// t = [part (fp32 [N][nb][C][2]), stats (fp32 [N][C][2])], i = [N, nb, C]
+static Launch make_stats_final(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor part = opt(t, 0), st = opt(t, 1);
+  check_f32(part, "partials"); check_f32(st, "stats");
+  TORCH_CHECK(i.size() == 3, "stats_final: expected [N, nb, C]");
+  const int N = (int)i[0], nb = (int)i[1], C = (int)i[2];
+  TORCH_CHECK(part.numel() >= (int64_t)N * nb * C * 2 && st.numel() >= (int64_t)N * C * 2, "stats_final: sizes");
+  if (keep) { keep->push_back(part); keep->push_back(st); }
+  const float* pp = part.data_ptr<float>();
+  float* sp = st.data_ptr<float>();
+  return [=](hipStream_t s, int) { return jr_channel_stats_final(pp, N, nb, C, sp, s); };
+}
+void stats_final_op(const TList& t, IList i) { run_now(make_stats_final(t, i, nullptr)); }
+std::vector<int64_t> conv_halo_cfg_op(int64_t cfg) {
+  int c[6];
+  if (!jr_conv_halo_cfg((int)(cfg - kHaloCfg0), c)) return {};
+  return {c[0], c[1], c[2], c[3], c[4], c[5]};
+}
 bool conv_grouped_ok_op(int64_t cfg) { return jr_conv_grouped_ok((int)cfg) != 0; }
 
 // Batched GEMM (bgemm.hip).  t = [A (bf16 [batch][M][K] or [batch][K][M]), B (bf16 [batch][K][N]),
@@ -1600,6 +1693,7 @@ class Plan : public torch::CustomClassHolder {
   void add_taps_gemm(TList t, IList i) { push(make_taps_gemm(t, i, &keep_), "taps_gemm"); }
   void add_gru_fused(TList t, IList i) { push(make_gru_fused(t, i, &keep_), "gru_fused"); }
   void add_gru_halo(TList t, IList i) { push(make_gru_halo(t, i, &keep_), "gru_halo"); }
+  void add_stats_final(TList t, IList i) { push(make_stats_final(t, i, &keep_), "stats_final"); }
   void add_conv1x1(TList t, IList i) { push(make_conv1x1(t, i, &keep_), "conv1x1"); }
   void add_conv_direct(TList t, IList i) { push(make_conv_direct(t, i, &keep_), "conv_direct"); }
   void add_flowin_dual(TList t, IList i, double alpha) { push(make_flowin_dual(t, i, alpha, &keep_), "flowin_dual"); }
@@ -2050,6 +2144,9 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("conv_grouped_ok(int cfg) -> bool", &jr::conv_grouped_ok_op);
   m.def("gru_fused_fits(int H, int W, int vertical) -> bool", &jr::gru_fused_fits);
   m.def("gru_halo(Tensor?[] t, int[] i) -> ()", &jr::gru_halo_op);
+  m.def("conv_halo_ok(int cfg, int cin8, int cout) -> bool", &jr::conv_halo_ok_op);
+  m.def("stats_final(Tensor?[] t, int[] i) -> ()", &jr::stats_final_op);
+  m.def("conv_halo_cfg(int cfg) -> int[]", &jr::conv_halo_cfg_op);
   m.def("gru_halo_geom_ok(int hd, int mode, int TR, int TC, int nb1, int nb2) -> bool", &jr::gru_halo_geom_ok);
   m.def("conv1x1(Tensor?[] t, int[] i) -> ()", &jr::conv1x1_op);
   m.def("conv_direct(Tensor?[] t, int[] i) -> ()", &jr::conv_direct_op);
@@ -2106,6 +2203,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_taps_gemm", &jr::Plan::add_taps_gemm)
       .def("add_gru_fused", &jr::Plan::add_gru_fused)
       .def("add_gru_halo", &jr::Plan::add_gru_halo)
+      .def("add_stats_final", &jr::Plan::add_stats_final)
       .def("add_flowin_dual", &jr::Plan::add_flowin_dual)
       .def("add_conv_group", &jr::Plan::add_conv_group)
       .def("add_conv1x1", &jr::Plan::add_conv1x1)

@@ -174,6 +174,28 @@ def conv2d_nhwc(
     return y.permute(0, 2, 3, 1)
 
 
+def conv2d_nhwc_gemm(
+    x: torch.Tensor,
+    kernel: torch.Tensor,
+    bias: Optional[torch.Tensor],
+    stride: Tuple[int, int] = (1, 1),
+    padding: Tuple[int, int] = (0, 0),
+) -> torch.Tensor:
+    """:func:`conv2d_nhwc` as explicit im2col + one fp32 GEMM (the same sum, no
+    convolution library): the golden conv of GPU-side references (ops/functional.py
+    ``golden_ops``), which must not depend on a conv library's algorithm search."""
+    N, H, W, C = x.shape
+    kh, kw, _, co = kernel.shape
+    cols = F.unfold(x.permute(0, 3, 1, 2), (kh, kw), padding=padding, stride=stride)   # (N, C*kh*kw, L)
+    OH = (H + 2 * padding[0] - kh) // stride[0] + 1
+    OW = (W + 2 * padding[1] - kw) // stride[1] + 1
+    w = kernel.permute(2, 0, 1, 3).reshape(C * kh * kw, co)          # unfold order: (c, i, j)
+    y = torch.matmul(cols.transpose(1, 2), w)                        # (N, L, co)
+    if bias is not None:
+        y = y + bias
+    return y.reshape(N, OH, OW, co)
+
+
 def instance_norm_nhwc(x: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
     """Flax ``nn.InstanceNorm(epsilon=1e-5, use_bias=False, use_scale=False)``
     (``model.py:706-707``): per (n, c) over H, W, biased variance.  Statistics

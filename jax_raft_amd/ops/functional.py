@@ -7,23 +7,45 @@ no silent fallback: if the native library is missing, GPU calls raise.
 """
 from __future__ import annotations
 
+import threading
+from contextlib import contextmanager
 from typing import List, Sequence
 
 import torch
 
 from ..models import reference as R
 
+_mode = threading.local()
+
+
+@contextmanager
+def golden_ops():
+    """Run the module forwards on the golden PyTorch ops on ANY device (a plain fp32
+    reference on the GPU, e.g. for engine-vs-golden tests at sizes the CPU cannot afford)."""
+    prev = getattr(_mode, "golden", False)
+    _mode.golden = True
+    try:
+        yield
+    finally:
+        _mode.golden = prev
+
+
+def _native(x: torch.Tensor) -> bool:
+    return x.is_cuda and not getattr(_mode, "golden", False)
+
 
 def conv2d_nhwc(x: torch.Tensor, kernel: torch.Tensor, bias, stride=(1, 1), padding=(0, 0)) -> torch.Tensor:
-    if x.is_cuda:
+    if _native(x):
         from .autograd import conv2d_nhwc as native_conv
 
         return native_conv(x, kernel, bias, stride, padding)
+    if x.is_cuda:   # golden_ops on the GPU: im2col + GEMM (no convolution-library search)
+        return R.conv2d_nhwc_gemm(x, kernel, bias, stride, padding)
     return R.conv2d_nhwc(x, kernel, bias, stride, padding)
 
 
 def build_pyramid(fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int) -> List[torch.Tensor]:
-    if fmap1.is_cuda:
+    if _native(fmap1):
         from .autograd import build_pyramid as native_pyr
 
         B, h, w, _ = fmap1.shape
@@ -38,7 +60,7 @@ def build_pyramid(fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int) -> 
 def build_pyramid_queries(fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int) -> List[torch.Tensor]:
     """Pyramid of a subset of query pixels ``fmap1`` (B, hq, wq, C) against all of
     ``fmap2`` (B, h, w, C): levels (B*hq*wq, h_l, w_l) (context parallelism)."""
-    if fmap1.is_cuda:
+    if _native(fmap1):
         from .autograd import build_pyramid as native_pyr
 
         return native_pyr(fmap1, fmap2, num_levels)
@@ -46,7 +68,7 @@ def build_pyramid_queries(fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: 
 
 
 def index_pyramid(pyramid: Sequence[torch.Tensor], coords: torch.Tensor, radius: int) -> torch.Tensor:
-    if coords.is_cuda:
+    if _native(coords):
         from .autograd import index_pyramid as native_lookup
 
         return native_lookup(pyramid, coords, radius)

@@ -217,7 +217,9 @@ class ConvSpec:
     """A packed convolution ready for the implicit-GEMM kernel.
 
     ``w``: bf16 [cout_pad, kpad], K ordered (kh, kw, cin8) with the input
-    channels zero-padded to ``cin8``; ``b``: fp32 [cout]."""
+    channels zero-padded to ``cin8``; ``b``: fp32 [cout]; ``wh``: for a 3x3 /
+    stride-1 / pad-1 conv with cin8 % 16 == 0, the weights of the halo kernel
+    (conv_halo.hip; :func:`pack_halo_conv`), else None."""
 
     w: torch.Tensor
     b: torch.Tensor
@@ -230,9 +232,46 @@ class ConvSpec:
     cin: int
     cin8: int
     cout: int
+    wh: Optional[torch.Tensor] = None
 
     def out_hw(self, H: int, W: int) -> Tuple[int, int]:
         return (H + 2 * self.ph - self.kh) // self.sh + 1, (W + 2 * self.pw - self.kw) // self.sw + 1
+
+    @property
+    def halo_shape(self) -> bool:
+        return (self.kh, self.kw, self.sh, self.sw, self.ph, self.pw) == (3, 3, 1, 1, 1, 1) and self.cin8 % 16 == 0
+
+
+# halo 3x3 conv tile configs (csrc/kernels/conv_halo.hip kCfgs; conv op cfg id = HALO_CFG0 + index):
+# (cin, waves along cout, waves along pixels, 32-pixel blocks per wave, tile rows, tile cols)
+HALO_CFG0 = 100
+HALO_CFGS = ((64, 2, 2, 4, 16, 16), (64, 2, 2, 2, 8, 16), (96, 3, 2, 2, 8, 16), (96, 3, 1, 2, 4, 16),
+             (128, 4, 2, 2, 8, 16), (128, 4, 1, 2, 4, 16), (128, 2, 2, 2, 8, 16), (128, 2, 1, 1, 4, 8),
+             (256, 2, 2, 2, 8, 16), (256, 2, 1, 1, 4, 8), (128, 4, 1, 1, 4, 8), (256, 4, 1, 1, 4, 8),
+             (256, 2, 1, 2, 4, 16))
+
+
+def pack_halo_conv(kernel: torch.Tensor, cin8: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """(3, 3, cin, cout) HWIO -> the halo conv's weight stream: :func:`pack_gru_halo` with the
+    input channels padded to cin8 and the output channels to a multiple of 32."""
+    kh, kw, cin, cout = kernel.shape
+    k = kernel.detach().float()
+    if cout % 32:
+        k = torch.cat([k, torch.zeros(kh, kw, cin, round_up(cout, 32) - cout, device=k.device)], dim=3)
+    return pack_gru_halo(k, cin8, out=out)
+
+
+def halo_cfgs_for(spec: "ConvSpec", kw: dict) -> Tuple[int, ...]:
+    """Halo conv configs that can run this conv (shape, epilogue, channel count)."""
+    if spec.wh is None or not spec.halo_shape:
+        return ()
+    if kw.get("epi", EPI_STD) != EPI_STD or kw.get("act", ACT_NONE) not in (ACT_NONE, ACT_RELU):
+        return ()
+    if kw.get("alpha", 1.0) != 1.0 or kw.get("bmap") is not None or kw.get("h32") is not None:
+        return ()
+    if kw.get("out_hw") is not None or kw.get("y") is not None and kw["y"].dtype != torch.bfloat16:
+        return ()
+    return tuple(HALO_CFG0 + i for i, c in enumerate(HALO_CFGS) if c[0] == spec.cin8 and spec.cout <= 512)
 
 
 def _row_perm(cout_pad: int) -> torch.Tensor:
@@ -293,9 +332,13 @@ def make_spec(kernel: torch.Tensor, bias: torch.Tensor, stride=(1, 1), padding=(
               device=None) -> ConvSpec:
     kh, kw, cin, cout = kernel.shape
     cin8 = cin8 or round_up(cin, 8)
-    w = pack_weight(kernel.to(device) if device is not None else kernel, cin8)
+    k = kernel.to(device) if device is not None else kernel
+    w = pack_weight(k, cin8)
     b = bias.detach().float().to(w.device).contiguous()
-    return ConvSpec(w, b, kh, kw, stride[0], stride[1], padding[0], padding[1], cin, cin8, cout)
+    spec = ConvSpec(w, b, kh, kw, stride[0], stride[1], padding[0], padding[1], cin, cin8, cout)
+    if spec.halo_shape and any(c[0] == cin8 for c in HALO_CFGS):
+        spec.wh = pack_halo_conv(k, cin8)
+    return spec
 
 
 def s2d_stem_kernel(kernel: torch.Tensor) -> torch.Tensor:
@@ -348,6 +391,9 @@ def conv_args(spec: ConvSpec, x: torch.Tensor, N: int, H: int, W: int, y: torch.
     t = [x, spec.w, spec.b, y, y2, res, h32, zbuf, coords, flow32, y3, bmap]
     if tapw is not None:
         t.append(tapw)
+    elif cfg >= HALO_CFG0:   # the halo 3x3 kernel (conv_halo.hip): its own weight stream
+        assert spec.wh is not None, "halo tile config for a conv without halo weights"
+        t.append(spec.wh)
     i = [N, H, W, x_coff, spec.cin8, spec.kh, spec.kw, spec.sh, spec.sw, spec.ph, spec.pw, spec.cout, act, split,
          y_coff, y2_coff, res_coff, hidden, y3_coff, epi, cfg, res_post]
     if bmap is not None or out_hw is not None:

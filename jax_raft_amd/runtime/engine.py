@@ -75,7 +75,7 @@ def _tune(spec: ConvSpec, x, N, H, W, y, kw, reps: int = 5) -> int:
     """Time every tile config of one conv problem; return the fastest."""
     ops = nat.ops()
     best, best_t = None, None
-    cfgs = nat.TAPS_CFGS if kw.get("epi") == nat.EPI_TAPS else nat.TUNE_CFGS
+    cfgs = nat.TAPS_CFGS if kw.get("epi") == nat.EPI_TAPS else nat.TUNE_CFGS + nat.halo_cfgs_for(spec, dict(kw, y=y))
     for cfg in cfgs:
         args = conv_args(spec, x, N, H, W, y, **dict(kw, cfg=cfg))
         ops.conv(*args)  # warm (and JIT-free: all configs are precompiled)
@@ -318,6 +318,8 @@ class RaftEngine:
             if name in self._specs:
                 sp = self._specs[name]
                 nat.pack_weight(k, sp.cin8, out=sp.w)
+                if sp.wh is not None:
+                    nat.pack_halo_conv(k, sp.cin8, out=sp.wh)
                 sp.b.copy_(b.float().to(self.device))
             else:
                 self._specs[name] = nat.make_spec(k, b.to(self.device), stride, pad, cin8=cin8, device=self.device)
@@ -524,7 +526,8 @@ class RaftEngine:
                    kw.get("epi", EPI_STD), kw.get("bmap") is not None)
             cfg = _TUNE_CACHE.get(key + (str(self.device),))
             if cfg is None:
-                valid = nat.TAPS_CFGS if kw.get("epi") == EPI_TAPS else nat.TUNE_CFGS
+                valid = (nat.TAPS_CFGS if kw.get("epi") == EPI_TAPS
+                         else nat.TUNE_CFGS + nat.halo_cfgs_for(spec, dict(kw, y=y)))
                 cfg = tunedb.lookup(self.arch, key, valid)   # persisted decision (runtime/tunedb.py)
                 if cfg is None:
                     cfg = _tune(spec, x, N, H, W, y, kw)

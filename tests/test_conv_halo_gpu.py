@@ -1,0 +1,92 @@
+"""conv_halo.hip (the halo 3x3 / stride-1 conv: LDS input footprint, tap-shifted B
+fragments, streamed weights) against the fp32 golden conv (reference.conv2d_nhwc) with
+bf16-rounded operands, for every tile config: map sizes that are not multiples of the tile,
+a partial last channel block (126 = the motion encoder's conv), channel slices of wider
+buffers, the residual epilogue (pre / post), the output copy and the statistics partials."""
+import math
+
+import pytest
+import torch
+
+from jax_raft_amd.models import reference as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+def _nat():
+    from jax_raft_amd.ops import native
+
+    native.require()
+    return native
+
+
+def _rel(a, b):
+    return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
+
+
+@pytest.mark.parametrize("idx", range(13))
+def test_conv_halo_matches_reference(idx):
+    nat = _nat()
+    cfg = nat.HALO_CFG0 + idx
+    cin = nat.HALO_CFGS[idx][0]
+    torch.manual_seed(idx)
+    for (N, H, W, cout) in ((1, 19, 37, 64 if cin != 256 else 192), (2, 9, 20, 126)):
+        x = torch.randn(N, H, W, cin)
+        k = torch.randn(3, 3, cin, cout) / math.sqrt(9 * cin)
+        b = torch.randn(cout) * 0.1
+        ref = R.conv2d_nhwc(_bf(x), _bf(k), b, (1, 1), (1, 1))
+        spec = nat.make_spec(k, b, (1, 1), (1, 1), device=DEV)
+        assert spec.wh is not None and cfg in nat.halo_cfgs_for(spec, {})
+        # input as a channel slice of a wider buffer (offset 8)
+        xg = torch.zeros(N, H, W, cin + 16, dtype=torch.bfloat16, device=DEV)
+        xg[..., 8:8 + cin] = x.to(DEV, torch.bfloat16)
+        y = torch.full((N * H * W, nat.round_up(cout, 8) + 16), 5.0, dtype=torch.bfloat16, device=DEV)
+        t, i, a = nat.conv_args(spec, xg, N, H, W, y, x_coff=8, y_coff=0, cfg=cfg)
+        nat.ops().conv(t, i, a)
+        torch.cuda.synchronize()
+        got = y[:, :cout].float().cpu().reshape(N, H, W, cout)
+        assert _rel(got, ref) < 1e-2, (cfg, N, H, W, cout)
+        assert (y[:, cout:] == 5.0).all()
+        # relu + residual (pre / post) + copy
+        res = torch.randn(N, H, W, cout)
+        rg = torch.zeros(N * H * W, nat.round_up(cout, 8) + 8, dtype=torch.bfloat16, device=DEV)
+        rg[:, :cout] = res.reshape(-1, cout).to(DEV, torch.bfloat16)
+        for post in (0, 1):
+            y2 = torch.zeros(N * H * W, nat.round_up(cout, 8), dtype=torch.bfloat16, device=DEV)
+            t, i, a = nat.conv_args(spec, xg, N, H, W, y, x_coff=8, act=nat.ACT_RELU, res=rg, res_post=post,
+                                    y2=y2, cfg=cfg)
+            nat.ops().conv(t, i, a)
+            torch.cuda.synchronize()
+            want = torch.relu(torch.relu(ref) + _bf(res)) if post else torch.relu(ref + _bf(res))
+            assert _rel(y[:, :cout].float().cpu().reshape(N, H, W, cout), want) < 1e-2, (cfg, post)
+            assert torch.equal(y2[:, :cout], y[:, :cout])
+
+
+@pytest.mark.parametrize("idx", [0, 2, 4, 8])
+def test_conv_halo_stats_partials(idx):
+    """Per-channel (sum, sumsq) of the stored outputs, per tile, reduced by the stats final
+    kernel: equals the statistics of the output tensor (what channel_stats computes)."""
+    nat = _nat()
+    cfg = nat.HALO_CFG0 + idx
+    cin, wco, wpx, tn, tr, tc = nat.HALO_CFGS[idx]
+    torch.manual_seed(3)
+    N, H, W, cout = 2, 21, 35, 96 if cin == 96 else 64
+    x = torch.randn(N, H, W, cin).to(DEV, torch.bfloat16)
+    k = torch.randn(3, 3, cin, cout) / math.sqrt(9 * cin)
+    spec = nat.make_spec(k, torch.randn(cout) * 0.1, (1, 1), (1, 1), device=DEV)
+    y = torch.empty(N * H * W, cout, dtype=torch.bfloat16, device=DEV)
+    nb = -(-H // tr) * -(-W // tc) * wpx
+    part = torch.full((N, nb, cout, 2), float("nan"), device=DEV)
+    stats = torch.empty(N, cout, 2, device=DEV)
+    t, i, a = nat.conv_args(spec, x, N, H, W, y, cfg=cfg)
+    nat.ops().conv(t + [part], i, a)
+    nat.ops().stats_final([part, stats], [N, nb, cout])
+    torch.cuda.synchronize()
+    yf = y.float().reshape(N, H * W, cout)
+    want = torch.stack([yf.sum(1), (yf * yf).sum(1)], -1)
+    assert torch.allclose(stats, want, rtol=1e-4, atol=1e-2), (stats - want).abs().max()

@@ -139,3 +139,16 @@ def test_instance_norm_closed_form_backward():
     v = (x2 * x2).mean(dim=(1, 2), keepdim=True) - m * m
     ((x2 - m) * torch.rsqrt(v + 1e-5) * g).sum().backward()
     assert (ga - x2.grad).abs().max() < 1e-5
+
+
+def test_conv_gemm_equals_conv():
+    """The GEMM-form golden conv (GPU-side references) is the same operator."""
+    torch.manual_seed(0)
+    for (kh, kw), s, p in (((3, 3), (1, 1), (1, 1)), ((7, 7), (2, 2), (3, 3)), ((1, 5), (1, 1), (0, 2)),
+                           ((1, 1), (2, 2), (0, 0))):
+        x = torch.randn(2, 11, 14, 6)
+        k = torch.randn(kh, kw, 6, 5)
+        b = torch.randn(5)
+        a = R.conv2d_nhwc(x, k, b, s, p)
+        g = R.conv2d_nhwc_gemm(x, k, b, s, p)
+        assert a.shape == g.shape and torch.allclose(a, g, atol=1e-4, rtol=1e-4)

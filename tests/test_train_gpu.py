@@ -49,28 +49,37 @@ def test_dp_grads_equal_full_batch(tmp_path):
     assert (tmp_path / "rank0.txt").read_text() != (tmp_path / "rank1.txt").read_text()   # own data per rank
     for n in g0:
         assert torch.equal(g0[n], g1[n]), n
-    # single process, the two samples as one batch, same init (seed 0), same device data
-    model = raft_small(seed=0)[0].cuda().train()
     ds = SyntheticFlow(size=(128, 160), seed=0, device="cuda")
     parts = [ds.batch([0]), ds.batch([1])]
-    img1, img2, flow, valid = (torch.cat([p[k] for p in parts]) for k in range(4))
-    preds = model(img1, img2, train=True, num_flow_updates=2, autograd=True)
-    loss, _ = sequence_loss(preds, flow, valid, 0.8, 400.0)
-    loss.backward()
-    torch.cuda.synchronize()
-    full = {n: p.grad.detach().float().cpu() for n, p in model.named_parameters()}
-    scale = max(v.norm().item() for v in full.values())
-    cos = []
-    for n, v in full.items():
-        if v.norm().item() < 1e-4 * scale:
-            continue
-        c = (torch.dot(v.flatten(), g0[n].flatten()) / (v.norm() * g0[n].norm() + 1e-12)).item()
-        cos.append(c)
-        assert c > 0.9 and 0.8 < g0[n].norm().item() / v.norm().item() < 1.25, (n, c)
-    assert torch.tensor(cos).median() > 0.99, cos
-    tot = torch.cat([v.flatten() for v in full.values()])
-    dp = torch.cat([g0[n].flatten() for n in full])
-    assert ((dp - tot).norm() / tot.norm()).item() < 5e-2
+
+    def grads(batch):
+        model = raft_small(seed=0)[0].cuda().train()
+        img1, img2, flow, valid = batch
+        preds = model(img1, img2, train=True, num_flow_updates=2, autograd=True)
+        loss, _ = sequence_loss(preds, flow, valid, 0.8, 400.0)
+        loss.backward()
+        torch.cuda.synchronize()
+        return {n: p.grad.detach().float().cpu() for n, p in model.named_parameters()}
+
+    def rel(a, b):   # global relative L2 error over every parameter
+        x = torch.cat([a[n].flatten() for n in b])
+        y = torch.cat([v.flatten() for v in b.values()])
+        return ((x - y).norm() / y.norm()).item()
+
+    # (1) the communication itself: the DP result must be the mean of the same two per-sample
+    # gradients computed in this process (same batch-1 kernels; the only difference is the
+    # fp32 all-reduce summation and tile-config choices if the tuned DB misses)
+    s0, s1 = grads(parts[0]), grads(parts[1])
+    mean = {n: 0.5 * (s0[n] + s1[n]) for n in s0}
+    e_comm = rel(g0, mean)
+    # (2) the semantics: the two samples as ONE batch in one process (batch-2 kernels: other
+    # tile configs / summation orders in bf16)
+    full = grads(tuple(torch.cat([p[k] for p in parts]) for k in range(4)))
+    e_full = rel(g0, full)
+    print(f"DP vs per-sample mean: {e_comm:.3e}; DP vs full batch: {e_full:.3e}")
+    # measured on MI355X (round 4): see profiles/r4_dp_grad_error.txt
+    assert e_comm < 1e-3, e_comm
+    assert e_full < 2e-2, e_full
 
 
 def test_gpu_nonfinite_step_dropped_without_host_sync():
