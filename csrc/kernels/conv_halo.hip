@@ -64,11 +64,26 @@ __global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHal
 #pragma unroll
   for (int d = 0; d < PD; ++d) ring[d] = __builtin_bit_cast(bf16x8, bload(ws, w_base + (unsigned)d * 1024u));
 
+  // input instance norm: per-channel scale / shift of image n, a table after the footprint
+  float* const nrm = (float*)(lds + (p.TR + 2) * (p.TC + 2) * P * 8);
+  if (p.in_stats) {
+    for (int c = tid; c < CIN; c += NT) {
+      const float inv = 1.0f / (float)p.in_hw;
+      const float m = p.in_stats[((long)n * CIN + c) * 2] * inv;
+      const float var = fmaxf(p.in_stats[((long)n * CIN + c) * 2 + 1] * inv - m * m, 0.f);
+      const float a = rsqrtf(var + p.in_eps);
+      nrm[2 * c] = a;
+      nrm[2 * c + 1] = -m * a;
+    }
+    __syncthreads();
+  }
+
   // footprint -> LDS
   {
     const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
     const int total = nfp * CC;
     const int HW = p.H * p.W;
+    const bool norm = p.in_stats != nullptr;
     for (int base = 0; base < total; base += 4 * NT) {
       u32x4 v[4];
       int fr[4], ch[4];
@@ -83,10 +98,29 @@ __global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHal
         ch[k] = c;
         const unsigned off = (unsigned)((n * HW + y * p.W + x) * p.xcs + p.xoff + 8 * c) * 2u;
         v[k] = bload(xs, in ? off : HOOB);
+        if (!in) ch[k] |= 1 << 30;   // padding: stays zero through the norm
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (fr[k] >= 0) *(u32x4*)(lds + fp_off<P>(fr[k], ch[k])) = v[k];
+      for (int k = 0; k < 4; ++k) {
+        if (fr[k] < 0) continue;
+        const int c = ch[k] & 0xffff;
+        if (norm && !(ch[k] >> 30)) {
+          bf16x8 e = __builtin_bit_cast(bf16x8, v[k]);
+          const f32x4* ab = (const f32x4*)(nrm + 16 * c);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x4 t = ab[q];   // (a, b) of channels 8c + 2q, 8c + 2q + 1
+#pragma unroll
+            for (int h2 = 0; h2 < 2; ++h2) {
+              float f = bf2f(e[2 * q + h2]) * t[2 * h2] + t[2 * h2 + 1];
+              if (p.in_relu) f = fmaxf(f, 0.f);
+              e[2 * q + h2] = f2bf(f);
+            }
+          }
+          v[k] = __builtin_bit_cast(u32x4, e);
+        }
+        *(u32x4*)(lds + fp_off<P>(fr[k], c)) = v[k];
+      }
     }
   }
 
@@ -209,7 +243,7 @@ constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
 int lds_bytes(const HaloCfg& c) {
   const int P = c.cin <= 64 ? 8 : c.cin <= 128 ? 16 : 32;
-  return (c.tr + 2) * (c.tc + 2) * P * 16;
+  return (c.tr + 2) * (c.tc + 2) * P * 16 + c.cin * 8;   // footprint + input-norm table
 }
 
 template <int CIN, int WCO, int WPX, int TN>

@@ -400,6 +400,10 @@ struct ConvHaloParams {
   void* y2; int y2cs, y2off;           // optional bf16 copy
   const void* res; int rcs, roff, res_post;   // optional bf16 residual (0: act(v + r), 1: relu(act(v) + r))
   float* stats_part;                   // optional [N][tiles_per_img * WPX][cout][2] (sum, sumsq) partials
+  // optional instance norm (+ relu) of the INPUT, applied while the footprint is loaded:
+  // x' = act((x - mean[n][c]) * rsqrt(var[n][c] + eps)) from in_stats [N][cin][2] (sum, sumsq
+  // over in_hw pixels; jr_norm_act mode 1 semantics), zero padding stays zero
+  const float* in_stats; int in_hw; float in_eps; int in_relu;
   int TR, TC, tiles_y, tiles_x, ntiles;
   long x_bytes;
 };

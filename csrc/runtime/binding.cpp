@@ -258,6 +258,16 @@ static Launch make_conv_halo(const TList& t, const IList& i, double alpha, std::
     TORCH_CHECK(part.numel() >= (int64_t)N * p.tiles_y * p.tiles_x * c[2] * cout * 2, "conv_halo: stats partials too small");
     p.stats_part = part.data_ptr<float>();
   }
+  // optional t[14]: stats of the input ([N][cin][2] sums) -> instance norm (+ relu) on load;
+  // i[27..28] (after the 27-int form): in_relu, in_hw; eps 1e-5 (the encoders' InstanceNorm)
+  at::Tensor ist = opt(t, 14);
+  if (ist.defined()) {
+    check_f32(ist, "input stats");
+    TORCH_CHECK(i.size() >= 29, "conv_halo: the input norm needs [.., in_relu, in_hw]");
+    TORCH_CHECK(ist.numel() >= (int64_t)N * cin8 * 2 && i[28] > 0, "conv_halo: input stats [N][cin][2]");
+    p.in_stats = ist.data_ptr<float>(); p.in_relu = (int)i[27]; p.in_hw = (int)i[28]; p.in_eps = 1e-5f;
+    if (keep) keep->push_back(ist);
+  }
   p.x_bytes = (long)x.numel() * 2;
   TORCH_CHECK(p.x_bytes < (1LL << 31), "conv_halo: input larger than 2 GiB");
   for (const at::Tensor* v : {&x, &wh, &y})

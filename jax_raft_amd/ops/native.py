@@ -382,9 +382,13 @@ def conv_args(spec: ConvSpec, x: torch.Tensor, N: int, H: int, W: int, y: torch.
               y_coff: int = 0, act: int = ACT_NONE, split: int = 0, alpha: float = 1.0, y2=None, y2_coff: int = 0,
               res=None, res_coff: int = 0, res_post: int = 0, h32=None, zbuf=None, hidden: int = 0, coords=None,
               flow32=None, y3=None, y3_coff: int = 0, epi: int = EPI_STD, cfg: Optional[int] = None,
-              bmap=None, bmap_coff: int = 0, tapw=None, out_hw: Optional[Tuple[int, int]] = None):
+              bmap=None, bmap_coff: int = 0, tapw=None, out_hw: Optional[Tuple[int, int]] = None,
+              stats_part=None, in_stats=None, in_relu: int = 0, in_hw: int = 0):
     """Build the (tensors, ints, alpha) argument triple of the ``conv`` op.
-    ``bmap``: optional fp32 per-pixel bias map [M, C], channels from ``bmap_coff``."""
+    ``bmap``: optional fp32 per-pixel bias map [M, C], channels from ``bmap_coff``.
+    Halo tile configs only (cfg >= HALO_CFG0): ``stats_part`` receives per-tile channel
+    (sum, sumsq) partials of the output; ``in_stats`` ([N][cin][2] sums over ``in_hw``
+    pixels) normalises the input (instance norm, + relu if ``in_relu``) as it is loaded."""
     OH, OW = out_hw if out_hw is not None else spec.out_hw(H, W)
     if cfg is None:
         cfg = pick_cfg(N * OH * OW, spec.cout)
@@ -394,10 +398,15 @@ def conv_args(spec: ConvSpec, x: torch.Tensor, N: int, H: int, W: int, y: torch.
     elif cfg >= HALO_CFG0:   # the halo 3x3 kernel (conv_halo.hip): its own weight stream
         assert spec.wh is not None, "halo tile config for a conv without halo weights"
         t.append(spec.wh)
+        if stats_part is not None or in_stats is not None:
+            t += [stats_part, in_stats]
+    assert (stats_part is None and in_stats is None) or cfg >= HALO_CFG0, "stats / input norm need a halo config"
     i = [N, H, W, x_coff, spec.cin8, spec.kh, spec.kw, spec.sh, spec.sw, spec.ph, spec.pw, spec.cout, act, split,
          y_coff, y2_coff, res_coff, hidden, y3_coff, epi, cfg, res_post]
-    if bmap is not None or out_hw is not None:
+    if bmap is not None or out_hw is not None or in_stats is not None:
         i += [OH if out_hw is not None else 0, OW if out_hw is not None else 0, 0, 0, bmap_coff]
+    if in_stats is not None:
+        i += [int(in_relu), int(in_hw)]
     return t, i, float(alpha)
 
 

@@ -75,8 +75,7 @@ def _tune(spec: ConvSpec, x, N, H, W, y, kw, reps: int = 5) -> int:
     """Time every tile config of one conv problem; return the fastest."""
     ops = nat.ops()
     best, best_t = None, None
-    cfgs = nat.TAPS_CFGS if kw.get("epi") == nat.EPI_TAPS else nat.TUNE_CFGS + nat.halo_cfgs_for(spec, dict(kw, y=y))
-    for cfg in cfgs:
+    for cfg in _candidates(spec, kw, y):
         args = conv_args(spec, x, N, H, W, y, **dict(kw, cfg=cfg))
         ops.conv(*args)  # warm (and JIT-free: all configs are precompiled)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -89,6 +88,21 @@ def _tune(spec: ConvSpec, x, N, H, W, y, kw, reps: int = 5) -> int:
         if best_t is None or t < best_t:
             best, best_t = cfg, t
     return best
+
+
+def _fused_norm(kw) -> bool:
+    """The conv writes channel-statistics partials or normalises its input on load: only the
+    halo kernel (conv_halo.hip) does either."""
+    return kw.get("stats_part") is not None or kw.get("in_stats") is not None
+
+
+def _candidates(spec: ConvSpec, kw, y) -> Tuple[int, ...]:
+    """Tile configs that can run this conv: the taps-epilogue configs, or the implicit-GEMM
+    autotune set plus the halo 3x3 configs (halo only when a norm is fused into the conv)."""
+    if kw.get("epi") == nat.EPI_TAPS:
+        return nat.TAPS_CFGS
+    halo = nat.halo_cfgs_for(spec, dict(kw, y=y))
+    return halo if _fused_norm(kw) else nat.TUNE_CFGS + halo
 
 
 def _fold_bn(cna: ConvNormActivation) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -208,6 +222,10 @@ class RaftEngine:
         assert streams in (True, False, "auto"), streams
         self.streams_mode = streams
         self.streams = bool(streams)
+        # instance norms of the encoders fused into halo 3x3 convs (statistics partials in the
+        # producer's epilogue, normalise + relu in the consumer's footprint load);
+        # JR_HALO_NORM=0: the separate statistics / norm_act passes
+        self.halo_norm = os.environ.get("JR_HALO_NORM", "1") != "0"
         self.mask_head = "split"      # per plan: "split" (mask lane) | "fused" (one lane, 128 -> 512 conv)
         self.gate_dtype = gate_dtype
         self.split = split
@@ -520,14 +538,19 @@ class RaftEngine:
                 kw = dict(kw, cfg=self.cfg_override[name])
         if kw.get("epi") == EPI_TAPS and not self.autotune and kw.get("cfg") is None:
             kw = dict(kw, cfg=nat.TAPS_CFGS[0])
+        if _fused_norm(kw) and not self.autotune and kw.get("cfg") is None:
+            kw = dict(kw, cfg=_candidates(spec, kw, y)[0])
         if self.autotune and kw.get("cfg") is None:
             OH, OW = kw["out_hw"] if kw.get("out_hw") is not None else spec.out_hw(H, W)
+            valid = _candidates(spec, kw, y)
             key = (N * OH * OW, spec.cout, spec.kh, spec.kw, spec.sh, spec.sw, spec.cin8, x.shape[-1],
                    kw.get("epi", EPI_STD), kw.get("bmap") is not None)
+            # problems the halo kernel can run are keyed apart (decisions made before it existed
+            # never timed it); a fused norm restricts the choice to the halo configs
+            if any(c >= nat.HALO_CFG0 for c in valid):
+                key = key + ("halo-norm" if _fused_norm(kw) else "halo",)
             cfg = _TUNE_CACHE.get(key + (str(self.device),))
             if cfg is None:
-                valid = (nat.TAPS_CFGS if kw.get("epi") == EPI_TAPS
-                         else nat.TUNE_CFGS + nat.halo_cfgs_for(spec, dict(kw, y=y)))
                 cfg = tunedb.lookup(self.arch, key, valid)   # persisted decision (runtime/tunedb.py)
                 if cfg is None:
                     cfg = _tune(spec, x, N, H, W, y, kw)
@@ -566,6 +589,29 @@ class RaftEngine:
             self._conv(plan, s, x, N, H, W, y, act=act, res=res, res_post=res_post, out_hw=out_hw)
             return y, OH, OW
 
+        def halo_fusable(name) -> bool:
+            return self.halo_norm and bool(nat.halo_cfgs_for(sp[name], {}))
+
+        def conv_stats(name, x, N, H, W, in_stats=None):
+            """A halo 3x3 conv that writes its output's channel-statistics partials (reduced
+            by one small launch) and, given ``in_stats``, instance-normalises + relus its raw
+            input as it loads it (no channel_stats pass over the output, no norm_act pass
+            over the input)."""
+            s = sp[name]
+            y = alloc(name + ".y", (N, H, W, s.cout))
+            nb_max = max(-(-H // c[4]) * -(-W // c[5]) * c[2] for c in nat.HALO_CFGS if c[0] == s.cin8)
+            part = alloc(name + ".part", (N, nb_max, s.cout, 2), F32)
+            kw = dict(stats_part=part, in_stats=in_stats, in_relu=1, in_hw=H * W)
+            kw = self._conv_kw(s, x, N, H, W, y, kw)
+            if kw.get("cfg") is None or kw["cfg"] < nat.HALO_CFG0:   # an override chose another kernel
+                return None
+            plan.add_conv(*conv_args(s, x, N, H, W, y, **kw))
+            c = nat.HALO_CFGS[kw["cfg"] - nat.HALO_CFG0]
+            nb = -(-H // c[4]) * -(-W // c[5]) * c[2]
+            st_ = alloc(name + ".stats", (N, s.cout, 2), F32)
+            plan.add_stats_final([part, st_], [N, nb, s.cout])
+            return y, st_
+
         def stem(act=ACT_NONE):
             if x.shape[-1] == 16:   # space-to-depth input (prep s2d): the 4x4 / stride-1 form of the stem
                 return conv_raw(f"{tag}.stem_s2d", x, N, H // 2, W // 2, act=act, out_hw=(H // 2, W // 2))
@@ -598,12 +644,21 @@ class RaftEngine:
                 has_ds = blk.stride != (1, 1)
                 if inorm:
                     h_, w_ = H, W
-                    y = x
+                    y, ys = x, None   # ys: stats of a raw conv output y still to be normalised
                     for j, nm in enumerate(names):
-                        yr, h_, w_ = conv_raw(f"{pre}.{nm}", y, N, h_, w_)
-                        s = stats(f"{pre}.{nm}", yr, N, h_ * w_, yr.shape[-1])
+                        cname = f"{pre}.{nm}"
+                        fused = None
+                        if halo_fusable(cname) and sp[cname].out_hw(h_, w_) == (h_, w_):
+                            fused = conv_stats(cname, y, N, h_, w_, in_stats=ys)
+                        if fused is not None:
+                            yr, s = fused
+                        else:
+                            if ys is not None:
+                                y = norm_act(f"{pre}.{names[j - 1]}", y, ys, relu=2)
+                            yr, h_, w_ = conv_raw(cname, y, N, h_, w_)
+                            s = stats(cname, yr, N, h_ * w_, yr.shape[-1])
                         if j + 1 < len(names):
-                            y = norm_act(f"{pre}.{nm}", yr, s, relu=2)
+                            y, ys = yr, s
                         else:
                             last, last_s = yr, s
                     if has_ds:

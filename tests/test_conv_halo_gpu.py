@@ -90,3 +90,30 @@ def test_conv_halo_stats_partials(idx):
     yf = y.float().reshape(N, H * W, cout)
     want = torch.stack([yf.sum(1), (yf * yf).sum(1)], -1)
     assert torch.allclose(stats, want, rtol=1e-4, atol=1e-2), (stats - want).abs().max()
+
+
+@pytest.mark.parametrize("idx", [0, 2, 4])
+def test_conv_halo_input_instance_norm(idx):
+    """The producer's instance norm + relu applied while the footprint is loaded equals
+    norm_act (jr_norm_act mode 1, relu) followed by the conv; padding stays zero."""
+    nat = _nat()
+    cfg = nat.HALO_CFG0 + idx
+    cin = nat.HALO_CFGS[idx][0]
+    torch.manual_seed(4)
+    N, H, W, cout = 2, 13, 30, 64
+    x = (torch.randn(N, H, W, cin) * 2 + 0.5).to(DEV, torch.bfloat16)
+    stats = torch.empty(N, cin, 2, device=DEV)
+    xf = x.float().reshape(N, H * W, cin)
+    stats.copy_(torch.stack([xf.sum(1), (xf * xf).sum(1)], -1))
+    k = torch.randn(3, 3, cin, cout) / math.sqrt(9 * cin)
+    b = torch.randn(cout) * 0.1
+    spec = nat.make_spec(k, b, (1, 1), (1, 1), device=DEV)
+    mean = xf.mean(1, keepdim=True)
+    var = (xf * xf).mean(1, keepdim=True) - mean * mean
+    xn = torch.relu((xf - mean) * torch.rsqrt(var.clamp_min(0) + 1e-5)).reshape(N, H, W, cin)
+    ref = R.conv2d_nhwc(_bf(xn.cpu()), _bf(k), b, (1, 1), (1, 1))
+    y = torch.empty(N * H * W, cout, dtype=torch.bfloat16, device=DEV)
+    t, i, a = nat.conv_args(spec, x, N, H, W, y, cfg=cfg, in_stats=stats, in_relu=1, in_hw=H * W)
+    nat.ops().conv(t, i, a)
+    torch.cuda.synchronize()
+    assert _rel(y.float().cpu().reshape(N, H, W, cout), ref) < 1.5e-2

@@ -336,12 +336,13 @@ def test_lane_schedule_graph_equals_eager_and_tracks_golden():
         assert _epe(a[it].cpu(), gold[it]) < 0.05 * mag + 0.05, it
 
 
+@pytest.mark.parametrize("gru", ["fused", "halo"])
 @pytest.mark.parametrize("B,H,W", [(4, 128, 160), (3, 136, 264)])
-def test_fused_gru_lane_schedule(monkeypatch, B, H, W):
-    """The fused ConvGRU stages (gru_fused.hip) forced on at a small size, with the lane
-    schedule (mask lane on the hm parity halves / flowp copy, two waits per iteration):
-    graph == eager bitwise, tracks the golden at every iteration and stays close to the
-    two-launch path."""
+def test_fused_gru_lane_schedule(monkeypatch, B, H, W, gru):
+    """The fused ConvGRU stages -- whole-row tiles (gru_fused.hip) or halo tiles
+    (gru_halo.hip) -- with the lane schedule (the mask lane reads the last stage's h copy
+    hm): graph == eager bitwise, tracks the golden at every iteration and stays close to
+    the two-launch path."""
     import copy
 
     model, variables = raft_large()
@@ -350,13 +351,13 @@ def test_fused_gru_lane_schedule(monkeypatch, B, H, W):
     m0 = copy.deepcopy(model).cuda()
     m1 = copy.deepcopy(model).cuda()
     i1, i2 = i1.cuda(), i2.cuda()
-    monkeypatch.setenv("JR_GRU_FUSED", "0")
+    monkeypatch.setenv("JR_GRU", "unfused")
     c = m0(i1, i2, num_flow_updates=5, streams=True)
-    monkeypatch.setenv("JR_GRU_FUSED", "1")
+    monkeypatch.setenv("JR_GRU", gru)
     a = m1(i1, i2, num_flow_updates=5, streams=True)
     b = m1(i1, i2, num_flow_updates=5, streams=True, use_graph=False)
     torch.cuda.synchronize()
-    assert m1.engine(torch.device("cuda", 0))._gru_fused_ok(B, H // 8, W // 8)
+    assert m1.engine(torch.device("cuda", 0), streams=True).gru_path == gru
     assert torch.equal(a, b)
     mag = gold.norm(dim=-1).mean().item()
     for it in range(5):

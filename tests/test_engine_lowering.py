@@ -246,3 +246,24 @@ def test_grouped_launch_uses_the_pair_config(fake, monkeypatch):
     p = eng._build(1, 128, 256, 3, True).plan
     g = [a for s, ln, d, op, a in p.ops if s == 1 and op == "conv_group"]
     assert g[0][1][20] == 23 and g[0][4][20] == 23
+
+
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_encoder_instance_norm_fused_into_halo_convs(fake, monkeypatch, fuse):
+    """raft_large's feature encoder (instance norm): with JR_HALO_NORM=1 every 3x3 / stride-1
+    conv runs on a halo config that writes its statistics partials (one stats_final each, no
+    channel_stats pass) and the conv after it normalises on load (the block-internal norm_act
+    passes disappear); block outputs are still materialised by norm_act."""
+    monkeypatch.setenv("JR_HALO_NORM", fuse)
+    eng, p = _plan(raft_large, 1)
+    pro = p.names(0)
+    fe_ops = [(op, a) for s, ln, d, op, a in p.ops if s == 0]
+    halo_convs = [a for op, a in fe_ops if op == "conv" and a[1][20] >= nat.HALO_CFG0]
+    if fuse == "1":
+        # per encoder image set: 10 stride-1 3x3 convs (4 in layer 1, 3 in layers 2 and 3)
+        assert pro.count("stats_final") == 10 and len(halo_convs) == 10
+        with_norm = [a for a in halo_convs if len(a[0]) > 14 and a[0][14] is not None]
+        assert len(with_norm) == 6            # the second conv of each of the 6 residual blocks
+        assert pro.count("norm_act") == 1 + 6  # stem + block outputs
+    else:
+        assert "stats_final" not in pro and pro.count("norm_act") == 1 + 6 + 6
