@@ -56,8 +56,10 @@ struct Halo {
   static constexpr int KS = TAPS * SPT;         // k-steps of both packed weights
   static constexpr int SRH = HD / 16;           // GEMM 2 k-steps per tap: r*h part
   static constexpr int SX = (CIN - HD) / 16;    //                          x part
-  static constexpr int PD1 = 16;                // weight ring depths (k-steps in flight per wave)
-  static constexpr int PD2 = SRH;
+  // weight ring depths (k-steps = 1 KB loads in flight per wave): the stream from L2 is this
+  // kernel's bound at batch 1 (Little's law: bytes in flight / L2 latency under load)
+  static constexpr int PD1 = NB1 + NB2 <= 3 ? 24 : 16;
+  static constexpr int PD2 = NB2 >= 2 ? (HD == 96 ? 8 : 12) : 16;
   static_assert(CIN % 16 == 0 && HD % 32 == 0 && CC <= 32 && HC <= 16 && SRH == SX, "geometry");
 };
 

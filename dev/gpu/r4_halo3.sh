@@ -8,10 +8,10 @@ timeout -k 10 400 python -u -m pytest tests/test_conv_halo_gpu.py tests/test_eng
 rc=$?
 tail -15 $o/engine.log
 [ $rc -eq 0 ] || exit $rc
-run() {  # tag, env..., -- bench args
-  local tag=$1; shift
-  env "$@" > /dev/null 2>&1
-}
+for args in "--arch raft_large --batch 1" "--arch raft_small --batch 1"; do
+  timeout -k 10 240 python -u tools/gru_bench.py $args 2>&1 | grep -v amdgpu.ids >> $o/gru_bench.log || { tail -20 $o/gru_bench.log; exit 1; }
+done
+grep -E "stage|halo" $o/gru_bench.log
 for g in halo unfused; do
   for hn in 1 0; do
     export JR_GRU=$g JR_HALO_NORM=$hn

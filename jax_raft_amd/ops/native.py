@@ -262,8 +262,9 @@ def pack_halo_conv(kernel: torch.Tensor, cin8: int, out: Optional[torch.Tensor] 
 
 
 def halo_cfgs_for(spec: "ConvSpec", kw: dict) -> Tuple[int, ...]:
-    """Halo conv configs that can run this conv (shape, epilogue, channel count)."""
-    if spec.wh is None or not spec.halo_shape:
+    """Halo conv configs that can run this conv (shape, epilogue, channel count).
+    ``JR_CONV_HALO=0`` removes them from every candidate set (A/B measurements)."""
+    if spec.wh is None or not spec.halo_shape or os.environ.get("JR_CONV_HALO", "1") == "0":
         return ()
     if kw.get("epi", EPI_STD) != EPI_STD or kw.get("act", ACT_NONE) not in (ACT_NONE, ACT_RELU):
         return ()

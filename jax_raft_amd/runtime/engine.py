@@ -765,10 +765,14 @@ class RaftEngine:
         env = os.environ.get("JR_GRU", "auto")
         if env == "unfused":
             return "unfused"
-        if env in ("auto", "halo") and self._halo_geom() is not None:
-            return "halo"
+        # auto: the whole-row kernel where it fills the GPU (its own >= 3/4-of-the-CUs rule:
+        # raft_large at batch >= 4 on Sintel frames, measured 339 vs 317-334 pairs/s for the
+        # halo kernel in the lane schedule, profiles/r4_gru_lowering_ab.txt), the halo kernel
+        # everywhere else (batch 1: 215 vs 191 FPS; raft_small; any map size)
         if env in ("auto", "fused") and self._gru_fused_ok(B, h, w):
             return "fused"
+        if env in ("auto", "halo") and self._halo_geom() is not None:
+            return "halo"
         return "unfused"
 
     def _halo_tile(self, gi: int, mode: int, axis: int, B: int, h: int, w: int, ops_args) -> Tuple[int, int, int, int]:

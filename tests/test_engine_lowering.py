@@ -110,7 +110,7 @@ def test_halo_gru_raft_large_buffers(fake, monkeypatch):
     """gru_halo lowering of raft_large (any batch): stage 1 (1x5 runs) reads [h | x] from hx
     and writes h' into qx; stage 2 (5x1 runs) reads h' from qx, x from hx and writes hx (never
     in place: neighbouring tiles read h); qx's [motion | flow] part is no longer written."""
-    monkeypatch.setenv("JR_GRU", "auto")
+    monkeypatch.setenv("JR_GRU", "halo")
     for B, lanes in ((1, False), (4, True)):
         eng, p = _plan(raft_large, B)
         assert eng.gru_path == "halo"
