@@ -22,20 +22,25 @@
 
 namespace {
 
-// footprint image row pitch P chunks (16 B) for cin <= 8 P; XOR-swizzled so that the 16
-// lanes of a ds_read_b128 group (16 consecutive pixel rows, one chunk) hit 16 distinct
-// 16-B slots of the 256-B bank window
+// Footprint image: pixel row r = fy * (TC + 2) + fx holds CIN channels in P 16-B chunks
+// (P = 8 / 16 / 32 for CIN <= 64 / 128 / 256).  Chunk c of pixel (fy, fx) sits in slot
+// c ^ kx(key) of its row, key = (fx + TC * fy) & 15: the 16 lanes of one ds_read_b128 lane
+// group read 16 pixels of consecutive keys (lane_px below), so for every tap (a constant shift
+// of fx / fy) they hit 16 distinct 16-B slots of the 256-B bank window.  With P = 8 two rows
+// share a window: the row parity (fx & 1, TC + 2 even) picks the half, key >> 1 the slot.
 template <int P>
-JR_DEVICE int fp_off(int row, int chunk) {
-  if constexpr (P == 8) return row * 64 + ((chunk ^ ((row >> 1) & 7)) << 3);
-  else if constexpr (P == 16) return row * 128 + (((chunk ^ row) & 15) << 3);
-  else return row * 256 + (((chunk & 16) | ((chunk ^ row) & 15)) << 3);
+JR_DEVICE constexpr int key_x(int key) { return P == 8 ? (key >> 1) & 7 : key & 15; }
+
+// position of lane rho (0..31) in its 32-pixel block: the ds_read_b128 lane groups
+// {0-3, 12-15, 20-27} and {4-11, 16-19, 28-31} get pixels 0..15 and 16..31 (guide: LDS table)
+JR_DEVICE int lane_px(int rho) {
+  return rho < 4 ? rho : rho < 12 ? rho + 12 : rho < 16 ? rho - 8 : rho < 20 ? rho + 8 : rho < 28 ? rho - 12 : rho;
 }
 
 template <int CIN>
 constexpr int pitch_of() { return CIN <= 64 ? 8 : CIN <= 128 ? 16 : 32; }
 
-template <int CIN, int WCO, int WPX, int TN>
+template <int CIN, int WCO, int WPX, int TN, int TR, int TC>
 __global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHaloParams p) {
   constexpr int NT = 64 * WCO * WPX;
   constexpr int P = pitch_of<CIN>();
@@ -43,7 +48,12 @@ __global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHal
   constexpr int SPT = CIN / 16;           // k-steps per tap
   constexpr int S = 9 * SPT;
   constexpr int PD = S >= 16 ? 16 : S;
+  constexpr int FW = TC + 2;
+  constexpr int NFP = (TR + 2) * FW;
+  constexpr int RB = P * 16;              // footprint row bytes
+  static_assert(TR * TC <= 32 * WPX * TN && (TC == 16 || TC == 8), "tile");
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
+  char* const lds_b = (char*)lds;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rho = lane & 31, hh = lane >> 5;
   const int wc = wave % WCO, wp = wave / WCO;
@@ -52,9 +62,7 @@ __global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHal
   const int n = blockIdx.x / per_img;
   const int rem = blockIdx.x - n * per_img;
   const int ty = rem / p.tiles_x, tx = rem - ty * p.tiles_x;
-  const int y0 = ty * p.TR, x0 = tx * p.TC;
-  const int FW = p.TC + 2;
-  const int nfp = (p.TR + 2) * FW;
+  const int y0 = ty * TR, x0 = tx * TC;
   const int co_blk = blockIdx.y * WCO + wc;   // this wave's 32-channel output block
 
   // weight ring first (its latency overlaps the footprint load)
@@ -64,47 +72,48 @@ __global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHal
 #pragma unroll
   for (int d = 0; d < PD; ++d) ring[d] = __builtin_bit_cast(bf16x8, bload(ws, w_base + (unsigned)d * 1024u));
 
-  // input instance norm: per-channel scale / shift of image n, a table after the footprint
-  float* const nrm = (float*)(lds + (p.TR + 2) * (p.TC + 2) * P * 8);
-  if (p.in_stats) {
-    for (int c = tid; c < CIN; c += NT) {
-      const float inv = 1.0f / (float)p.in_hw;
-      const float m = p.in_stats[((long)n * CIN + c) * 2] * inv;
-      const float var = fmaxf(p.in_stats[((long)n * CIN + c) * 2 + 1] * inv - m * m, 0.f);
-      const float a = rsqrtf(var + p.in_eps);
-      nrm[2 * c] = a;
-      nrm[2 * c + 1] = -m * a;
-    }
-    __syncthreads();
-  }
-
-  // footprint -> LDS
+  // footprint -> LDS: batches of up to 16 loads per thread in flight; the input instance norm
+  // (per-channel scale / shift of image n, a table after the footprint) is applied on the way
   {
+    float* const nrm = (float*)(lds_b + NFP * RB);
     const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
-    const int total = nfp * CC;
-    const int HW = p.H * p.W;
+    constexpr int TOTAL = NFP * CC;
+    constexpr int NL = (TOTAL + NT - 1) / NT;
+    constexpr int NBAT = NL < 16 ? NL : 16;
     const bool norm = p.in_stats != nullptr;
-    for (int base = 0; base < total; base += 4 * NT) {
-      u32x4 v[4];
-      int fr[4], ch[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int idx = base + k * NT + tid;
+    for (int l0 = 0; l0 < NL; l0 += NBAT) {
+      u32x4 v[NBAT];
+      int dst[NBAT];
+#pragma unroll
+      for (int k = 0; k < NBAT; ++k) {
+        const int idx = (l0 + k) * NT + tid;
         const int f = idx / CC, c = idx - f * CC;
         const int fy = f / FW, fx = f - fy * FW;
         const int y = y0 - 1 + fy, x = x0 - 1 + fx;
-        const bool in = idx < total && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
-        fr[k] = idx < total ? f : -1;
-        ch[k] = c;
-        const unsigned off = (unsigned)((n * HW + y * p.W + x) * p.xcs + p.xoff + 8 * c) * 2u;
+        const bool live = l0 + k < NL && idx < TOTAL;
+        const bool in = live && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
+        const unsigned off = (unsigned)((n * p.H + y) * p.W + x) * (unsigned)p.xcs * 2u + (unsigned)(p.xoff + 8 * c) * 2u;
         v[k] = bload(xs, in ? off : HOOB);
-        if (!in) ch[k] |= 1 << 30;   // padding: stays zero through the norm
+        // destination byte offset; bit 30: padding (stays zero through the norm), -1: none
+        dst[k] = !live ? -1 : (f * RB + ((c ^ key_x<P>(fx + TC * fy)) << 4)) | (in ? 0 : 1 << 30) | (c << 20);
+      }
+      if (l0 == 0 && norm) {
+        for (int c = tid; c < CIN; c += NT) {
+          const float inv = 1.0f / (float)p.in_hw;
+          const float m = p.in_stats[((long)n * CIN + c) * 2] * inv;
+          const float var = fmaxf(p.in_stats[((long)n * CIN + c) * 2 + 1] * inv - m * m, 0.f);
+          const float a = rsqrtf(var + p.in_eps);
+          nrm[2 * c] = a;
+          nrm[2 * c + 1] = -m * a;
+        }
+        __syncthreads();
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (fr[k] < 0) continue;
-        const int c = ch[k] & 0xffff;
-        if (norm && !(ch[k] >> 30)) {
+      for (int k = 0; k < NBAT; ++k) {
+        if (dst[k] < 0) continue;
+        if (norm && !(dst[k] >> 30)) {
+          const int c = (dst[k] >> 20) & 63;
           bf16x8 e = __builtin_bit_cast(bf16x8, v[k]);
           const f32x4* ab = (const f32x4*)(nrm + 16 * c);
 #pragma unroll
@@ -112,26 +121,27 @@ __global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHal
             const f32x4 t = ab[q];   // (a, b) of channels 8c + 2q, 8c + 2q + 1
 #pragma unroll
             for (int h2 = 0; h2 < 2; ++h2) {
-              float f = bf2f(e[2 * q + h2]) * t[2 * h2] + t[2 * h2 + 1];
-              if (p.in_relu) f = fmaxf(f, 0.f);
-              e[2 * q + h2] = f2bf(f);
+              float fv = bf2f(e[2 * q + h2]) * t[2 * h2] + t[2 * h2 + 1];
+              if (p.in_relu) fv = fmaxf(fv, 0.f);
+              e[2 * q + h2] = f2bf(fv);
             }
           }
           v[k] = __builtin_bit_cast(u32x4, e);
         }
-        *(u32x4*)(lds + fp_off<P>(fr[k], c)) = v[k];
+        *(u32x4*)(lds_b + (dst[k] & 0xfffff)) = v[k];
       }
     }
   }
 
-  // this lane's output pixels: footprint row of tap (0, 0), image pixel (-1: none)
-  int frow[TN], om[TN];
+  // this lane's output pixels: byte offset of footprint row of tap (0, 0), its key, image pixel
+  int rb0[TN], key0[TN], om[TN];
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
-    const int q = 32 * (wp * TN + b) + rho;
-    const int i = q / p.TC, j = q - i * p.TC;
-    const bool ok = i < p.TR && y0 + i < p.H && x0 + j < p.W;
-    frow[b] = ok ? i * FW + j : 0;
+    const int q = 32 * (wp * TN + b) + lane_px(rho);
+    const int i = q / TC, j = q - i * TC;
+    const bool ok = i < TR && y0 + i < p.H && x0 + j < p.W;
+    rb0[b] = ok ? (i * FW + j) * RB : 0;
+    key0[b] = ok ? j + TC * i : 0;
     om[b] = ok ? (n * p.H + y0 + i) * p.W + x0 + j : -1;
   }
   __syncthreads();
@@ -142,10 +152,11 @@ __global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHal
       [&](int s) { return __builtin_bit_cast(bf16x8, bload(ws, w_base + (unsigned)s * 1024u)); },
       [&](int s, int b) {
         const int tap = s / SPT, kc = s - tap * SPT;
-        const int row = frow[b] + (tap / 3) * FW + tap % 3;
-        return *(const bf16x8*)(lds + fp_off<P>(row, 2 * kc + hh));
+        const int u = tap / 3, v = tap % 3;
+        // slot of chunk 2 kc + hh: (2 kc) ^ (kx ^ hh); the tap's row shift is an immediate offset
+        const int kxh = (key_x<P>(key0[b] + v + TC * u) ^ hh) << 4;
+        return *(const bf16x8*)(lds_b + (rb0[b] + (((2 * kc) << 4) ^ kxh)) + (u * FW + v) * RB);
       });
-
   // epilogue: lane holds channels c0 .. c0 + 15 of pixel om[b]
   const int c0 = 32 * co_blk + 16 * hh;
   if (c0 >= p.cout) return;
@@ -246,13 +257,14 @@ int lds_bytes(const HaloCfg& c) {
   return (c.tr + 2) * (c.tc + 2) * P * 16 + c.cin * 8;   // footprint + input-norm table
 }
 
-template <int CIN, int WCO, int WPX, int TN>
+template <int CIN, int WCO, int WPX, int TN, int TR, int TC>
 int launch(const ConvHaloParams& p, hipStream_t s, int lds) {
-  static const bool attr = hipFuncSetAttribute((const void*)conv_halo_kernel<CIN, WCO, WPX, TN>,
+  if (p.TR != TR || p.TC != TC) return (int)hipErrorInvalidValue;
+  static const bool attr = hipFuncSetAttribute((const void*)conv_halo_kernel<CIN, WCO, WPX, TN, TR, TC>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   if (!attr) return (int)hipErrorInvalidValue;
   const int cpad = (p.cout + 32 * WCO - 1) / (32 * WCO);
-  hipLaunchKernelGGL((conv_halo_kernel<CIN, WCO, WPX, TN>), dim3(p.ntiles, cpad), dim3(64 * WCO * WPX), lds, s, p);
+  hipLaunchKernelGGL((conv_halo_kernel<CIN, WCO, WPX, TN, TR, TC>), dim3(p.ntiles, cpad), dim3(64 * WCO * WPX), lds, s, p);
   return (int)hipGetLastError();
 }
 
@@ -271,12 +283,14 @@ extern "C" int jr_conv_halo(const ConvHaloParams* p, int cfg, hipStream_t stream
   if (cfg < 0 || cfg >= kNumCfgs || p->ntiles <= 0) return (int)hipErrorInvalidValue;
   const HaloCfg& c = kCfgs[cfg];
   const int lds = lds_bytes(c);
-#define JR_HALO_CONV(CIN_, WCO_, WPX_, TN_) \
-  if (c.cin == CIN_ && c.wco == WCO_ && c.wpx == WPX_ && c.tn == TN_) return launch<CIN_, WCO_, WPX_, TN_>(*p, stream, lds);
-  JR_HALO_CONV(64, 2, 2, 4) JR_HALO_CONV(64, 2, 2, 2) JR_HALO_CONV(96, 3, 2, 2) JR_HALO_CONV(96, 3, 1, 2)
-  JR_HALO_CONV(128, 4, 2, 2) JR_HALO_CONV(128, 4, 1, 2) JR_HALO_CONV(128, 2, 2, 2) JR_HALO_CONV(128, 2, 1, 1)
-  JR_HALO_CONV(256, 2, 2, 2) JR_HALO_CONV(256, 2, 1, 1) JR_HALO_CONV(128, 4, 1, 1) JR_HALO_CONV(256, 4, 1, 1)
-  JR_HALO_CONV(256, 2, 1, 2)
+#define JR_HALO_CONV(CIN_, WCO_, WPX_, TN_, TR_, TC_) \
+  if (c.cin == CIN_ && c.wco == WCO_ && c.wpx == WPX_ && c.tn == TN_ && c.tr == TR_ && c.tc == TC_) \
+    return launch<CIN_, WCO_, WPX_, TN_, TR_, TC_>(*p, stream, lds);
+  JR_HALO_CONV(64, 2, 2, 4, 16, 16) JR_HALO_CONV(64, 2, 2, 2, 8, 16) JR_HALO_CONV(96, 3, 2, 2, 8, 16)
+  JR_HALO_CONV(96, 3, 1, 2, 4, 16) JR_HALO_CONV(128, 4, 2, 2, 8, 16) JR_HALO_CONV(128, 4, 1, 2, 4, 16)
+  JR_HALO_CONV(128, 2, 2, 2, 8, 16) JR_HALO_CONV(128, 2, 1, 1, 4, 8) JR_HALO_CONV(256, 2, 2, 2, 8, 16)
+  JR_HALO_CONV(256, 2, 1, 1, 4, 8) JR_HALO_CONV(128, 4, 1, 1, 4, 8) JR_HALO_CONV(256, 4, 1, 1, 4, 8)
+  JR_HALO_CONV(256, 2, 1, 2, 4, 16)
 #undef JR_HALO_CONV
   return (int)hipErrorInvalidValue;
 }
