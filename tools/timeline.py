@@ -23,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--iter", type=int, default=10)
+    ap.add_argument("--prologue", action="store_true", help="list the prologue kernels instead")
     a = ap.parse_args()
     rows = sorted(((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in _load(a.trace)),
                   key=lambda r: r[1])
@@ -42,7 +43,7 @@ def main():
     lk = [i for i, r in enumerate(seg) if "corr_lookup" in r[0]]
     print(f"prologue {(seg[lk[0]][1] - seg[0][1]) / 1e6:.3f} ms; loop {(seg[-1][2] - seg[lk[0]][1]) / 1e6:.3f} ms; "
           f"per iteration {(seg[lk[-1]][1] - seg[lk[0]][1]) / 1e3 / (len(lk) - 1):.1f} us")
-    it = seg[lk[a.iter]:lk[a.iter + 1] + 1]
+    it = seg[:lk[0] + 1] if a.prologue else seg[lk[a.iter]:lk[a.iter + 1] + 1]
     t0 = it[0][1]
     for n, s, e in it:
         print(f"{(s - t0) / 1e3:7.1f} {(e - t0) / 1e3:7.1f} {(e - s) / 1e3:6.1f}  {short(n)}")
