@@ -1808,9 +1808,17 @@ class Plan : public torch::CustomClassHolder {
     // in order on one stream, measured 264 vs 289 pairs/s at batch 4.)
     const char* pm = std::getenv("JR_PIPE_PROLOGUE");
     const bool pro_first = pm && std::string(pm) == "first";
-    if (pro_first) append_graph(g, next->pgraph_[0]);
-    append_graph(g, pgraph_[1]);
-    if (!pro_first) append_graph(g, next->pgraph_[0]);
+    // One empty root node ahead of both branches: the executor forks a node's successors
+    // onto parallel streams, but runs disconnected components in creation order on the
+    // launch stream (measured: 21.6 us of a 3.2 ms raft_small batch-1 step concurrent,
+    // profiles/r4_pipeline_fork_ab.txt).  JR_PIPE_FORK=0: no root (A/B).
+    hipGraphNode_t root = nullptr;
+    const char* fk = std::getenv("JR_PIPE_FORK");
+    if (!(fk && std::string(fk) == "0"))
+      TORCH_CHECK(hipGraphAddEmptyNode(&root, g, nullptr, 0) == hipSuccess, "graph root");
+    if (pro_first) append_graph(g, next->pgraph_[0], root);
+    append_graph(g, pgraph_[1], root);
+    if (!pro_first) append_graph(g, next->pgraph_[0], root);
     hipError_t e3 = hipGraphInstantiate(&pipe_exec_, g, nullptr, nullptr, 0);
     if (debug_) fprintf(stderr, "[plan] pipelined instantiate %d\n", (int)e3);
     TORCH_CHECK(e3 == hipSuccess, "graph instantiate failed: ", hipGetErrorString(e3));
@@ -1819,7 +1827,7 @@ class Plan : public torch::CustomClassHolder {
   }
   // Copy every node of src (kernel / empty nodes: what a plan capture holds)
   // into dst in dependency order, keeping src's edges.
-  static void append_graph(hipGraph_t dst, hipGraph_t src) {
+  static void append_graph(hipGraph_t dst, hipGraph_t src, hipGraphNode_t root = nullptr) {
     size_t n = 0;
     TORCH_CHECK(hipGraphGetNodes(src, nullptr, &n) == hipSuccess, "graph nodes");
     std::vector<hipGraphNode_t> nodes(n);
@@ -1853,6 +1861,7 @@ class Plan : public torch::CustomClassHolder {
       ready.erase(it);
       std::vector<hipGraphNode_t> d;
       for (size_t j : deps[i]) d.push_back(copy[j]);
+      if (d.empty() && root) d.push_back(root);
       hipGraphNodeType type;
       TORCH_CHECK(hipGraphNodeGetType(nodes[i], &type) == hipSuccess, "node type");
       hipError_t e = hipSuccess;
@@ -1880,6 +1889,9 @@ class Plan : public torch::CustomClassHolder {
   void merge_reset() {
     reset_pipe();
     TORCH_CHECK(hipGraphCreate(&pipe_graph_, 0) == hipSuccess, "graph create");
+    const char* fk = std::getenv("JR_PIPE_FORK");   // one root: the parts fork (capture_pipelined)
+    if (!(fk && std::string(fk) == "0"))
+      TORCH_CHECK(hipGraphAddEmptyNode(&pipe_root_, pipe_graph_, nullptr, 0) == hipSuccess, "graph root");
   }
   void merge_add(c10::intrusive_ptr<Plan> part, int64_t n_iters) {
     TORCH_CHECK(pipe_graph_ != nullptr && pipe_exec_ == nullptr, "merge_add: call merge_reset() first");
@@ -1890,7 +1902,7 @@ class Plan : public torch::CustomClassHolder {
       part->capture(n_iters);
       pipe_graph_ = merging;
     }
-    append_graph(pipe_graph_, part->graph_);
+    append_graph(pipe_graph_, part->graph_, pipe_root_);
   }
   void merge_finish(int64_t n_iters) {
     TORCH_CHECK(pipe_graph_ != nullptr && pipe_exec_ == nullptr, "merge_finish: call merge_reset() first");
@@ -1915,6 +1927,7 @@ class Plan : public torch::CustomClassHolder {
   void reset_pipe() {
     if (pipe_exec_) { (void)hipGraphExecDestroy(pipe_exec_); pipe_exec_ = nullptr; }
     if (pipe_graph_) { (void)hipGraphDestroy(pipe_graph_); pipe_graph_ = nullptr; }
+    pipe_root_ = nullptr;
     pipe_iters_ = -1;
     pipe_next_ = nullptr;
   }
@@ -2123,6 +2136,7 @@ class Plan : public torch::CustomClassHolder {
   hipGraphExec_t pexec_[2] = {};
   int64_t pcaptured_[2] = {-1, -1};
   hipGraph_t pipe_graph_ = nullptr;
+  hipGraphNode_t pipe_root_ = nullptr;
   hipGraphExec_t pipe_exec_ = nullptr;
   int64_t pipe_iters_ = -1;
   const Plan* pipe_next_ = nullptr;

@@ -918,12 +918,22 @@ class RaftEngine:
         E_PREP, E_CTX, E_FLOW, E_FH, E_MASK, E_FE2 = range(ev0, ev0 + 6)
         main, side, side2 = lanes
         lanes_on = main != side
+        # the prologue's branches (context encoder, feature encoder of each image) run on
+        # their own lanes even when the loop runs on one, up to Sintel-size batch 4 worth of
+        # pixels: there its ~100 kernels are small and latency-bound.  Measured at batch 1
+        # (profiles/r4_prologue_lanes_ab.txt): raft_small 12 iterations 667 -> 861 pairs/s,
+        # per-pair sync latency -1..-2 %; 1088x1920 frames 67.6 -> 63.7 (so: off there).
+        # JR_PRO_LANES=0: never, =1: always (A/B).
+        pl = os.environ.get("JR_PRO_LANES", "auto")
+        pro_on = pl == "1" or (pl == "auto" and B * h * w <= 4 * 55 * 128)
+        p_main, p_side, p_side2 = lanes if lanes_on or self.cp or not pro_on else (main, 1, 2)
+        p_on = p_main != p_side
 
         def lane(l):
             plan.set_lane(l)
 
         plan.set_segment(0)
-        lane(main)
+        lane(p_main)
         hx = alloc("hx", (M, self.hx_cs))
         qx = alloc("qx", (M, self.hx_cs))
         h32 = alloc("h32", (M, self.hidden), F32)
@@ -945,7 +955,7 @@ class RaftEngine:
             plan.add_prep([inp1, inp2, x0], [B, H, W])
         plan.add_record(E_PREP)
 
-        lane(side)
+        lane(p_side)
         plan.add_wait(E_PREP)
         ctxf, ch_, cw_ = self._encoder(st, plan, "ce", m.context_encoder, x0[:B], B, H, W, bt=pt)
         assert (ch_, cw_) == (h, w), "The context encoder should downsample H and W by 8"
@@ -964,23 +974,23 @@ class RaftEngine:
         plan.add_record(E_CTX)
 
         fmap = alloc("fmap", (2 * B, h, w, self.fmap_ch))
-        if lanes_on:
+        if p_on:
             # the feature encoder of image2 on a third lane, concurrent with image1's
             # (and the context encoder): per-image instance norms, so the halves are
             # exact, and the sequential encoder chain that gates the correlation
             # pyramid is half as long
-            lane(side2)
+            lane(p_side2)
             plan.add_wait(E_PREP)
             featb, _, _ = self._encoder(st, plan, "fe", m.feature_encoder, x0[B:], B, H, W, bt=pt + "fe2.")
             self._conv(plan, sp["fe.conv"], featb, B, h, w, fmap[B:])
             plan.add_record(E_FE2)
-            lane(main)
+            lane(p_main)
             feat, fh_, fw_ = self._encoder(st, plan, "fe", m.feature_encoder, x0[:B], B, H, W, bt=pt)
             assert (fh_, fw_) == (h, w), "The feature encoder should downsample H and W by 8"
             self._conv(plan, sp["fe.conv"], feat, B, h, w, fmap[:B])
             plan.add_wait(E_FE2)
         else:
-            lane(main)
+            lane(p_main)
             feat, fh_, fw_ = self._encoder(st, plan, "fe", m.feature_encoder, x0, 2 * B, H, W, bt=pt)
             assert (fh_, fw_) == (h, w), "The feature encoder should downsample H and W by 8"
             self._conv(plan, sp["fe.conv"], feat, 2 * B, h, w, fmap)

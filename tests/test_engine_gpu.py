@@ -286,7 +286,9 @@ def test_streams_auto_matches_lanes_and_single_lane(factory):
             assert _epe(a, b if B >= 4 else c) < 1e-4 and _epe(b, c) < 1e-2 * mag + 1e-2
         eng = model.engine(torch.device("cuda", 0), streams="auto")
         st = eng._states[(B, 128, 128, 3, True)]
-        assert (st.plan.num_lanes() > 1) == (B >= eng.AUTO_STREAMS_MIN_BATCH and eng.has_mask)
+        # loop lanes (the prologue's branches run on lanes at every batch, JR_PRO_LANES)
+        assert eng.uses_lanes(B) == (B >= eng.AUTO_STREAMS_MIN_BATCH and eng.has_mask)
+        assert st.plan.num_lanes() > 1
         # final-only (serving) mode: "auto" keeps one lane at every batch
         d = model(i1, i2, num_flow_updates=3, streams="auto", return_all_iters=False)
         torch.cuda.synchronize()
@@ -294,7 +296,7 @@ def test_streams_auto_matches_lanes_and_single_lane(factory):
             assert (d[-1] - c[-1]).abs().max().item() < 1e-3
         else:
             assert _epe(d[-1], c[-1]) < 1e-2 * c[-1].norm(dim=-1).mean().item() + 1e-2
-        assert eng._states[(B, 128, 128, 3, False)].plan.num_lanes() == 1
+        assert not eng.uses_lanes(B, all_iters=False)
 
 
 def test_engine_split_parts_match_single():

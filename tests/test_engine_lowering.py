@@ -255,6 +255,7 @@ def test_encoder_instance_norm_fused_into_halo_convs(fake, monkeypatch, fuse):
     channel_stats pass) and the conv after it normalises on load (the block-internal norm_act
     passes disappear); block outputs are still materialised by norm_act."""
     monkeypatch.setenv("JR_HALO_NORM", fuse)
+    monkeypatch.setenv("JR_PRO_LANES", "0")   # one feature-encoder pass over both images
     eng, p = _plan(raft_large, 1)
     pro = p.names(0)
     fe_ops = [(op, a) for s, ln, d, op, a in p.ops if s == 0]
@@ -267,3 +268,17 @@ def test_encoder_instance_norm_fused_into_halo_convs(fake, monkeypatch, fuse):
         assert pro.count("norm_act") == 1 + 6  # stem + block outputs
     else:
         assert "stats_final" not in pro and pro.count("norm_act") == 1 + 6 + 6
+
+
+@pytest.mark.parametrize("arch", [raft_large, raft_small])
+def test_prologue_lanes_at_batch_one(fake, monkeypatch, arch):
+    """At batch 1 the loop runs on one lane, the prologue on three: context encoder (lane 1),
+    feature encoder of image 2 (lane 2), image 1 + pyramid (lane 0); JR_PRO_LANES=0 keeps the
+    whole forward on lane 0."""
+    eng, p = _plan(arch, 1)
+    pro_lanes = {ln for s, ln, d, op, a in p.ops if s == 0}
+    loop_lanes = {ln for s, ln, d, op, a in p.ops if s == 1}
+    assert pro_lanes == {0, 1, 2} and loop_lanes == {0}
+    monkeypatch.setenv("JR_PRO_LANES", "0")
+    eng, p = _plan(arch, 1)
+    assert {ln for s, ln, d, op, a in p.ops} == {0}
