@@ -20,6 +20,8 @@
 // shuffle.  Output channels follow the reference order
 // l*(2r+1)^2 + i*(2r+1) + j (x-offset i-r is the slow index), staged in LDS
 // and written as 16-B vectors, zero-padded to the consumer's channel stride.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -651,6 +653,11 @@ extern "C" int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int
   void* lv[4] = {lvl0, lvl1, lvl2, lvl3};
   for (int l = 0; l < num_levels; ++l) wide = wide && reinterpret_cast<uintptr_t>(lv[l]) % 16 == 0;
   if (blocked && !wide) return (int)hipErrorInvalidValue;   // the blocked layout is written by the wide epilogue only
+  static const bool tile_pyr = getenv("JR_PYR_TILE") != nullptr;   // A/B: the tile kernel below
+  if (blocked && nq == h * w && !tile_pyr) {
+    const int e = jr_corr_pyramid_blocked(f1, f2, B, h, w, C, cs, lvl0, lvl1, lvl2, lvl3, num_levels, scale, stream);
+    if (e != (int)hipErrorNotSupported) return e;
+  }
   if (wide)
     hipLaunchKernelGGL((corr_pyramid_kernel<bf16, true>), grid, dim3(256), 0, stream, (const bf16*)f1, (const bf16*)f2,
                        h, w, nq, C, cs, (bf16*)lvl0, (bf16*)lvl1, (bf16*)lvl2, (bf16*)lvl3, num_levels, scale, blocked);

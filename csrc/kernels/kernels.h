@@ -129,6 +129,9 @@ int jr_norm_act(const void* x, const float* sx, int mode_x, const float* gamma, 
 // levels[l]: fp32 or bf16 [B][nq][h_l][w_l]; blocked (bf16, w % 16 == 0):
 // levels 0 and 1 as [B][nq][ceil(h/8)][ceil(w/16)] blocks of (8>>l) x (16>>l)
 // (the pyramid kernel's tiles; corr.hip LvGeom), levels 2 and 3 row-major.
+// persistent blocked-layout (bf16) pyramid build, corr_pyr.hip; hipErrorNotSupported = shape not handled
+int jr_corr_pyramid_blocked(const void* f1, const void* f2, int B, int h, int w, int C, int cs, void* l0, void* l1,
+                            void* l2, void* l3, int nlev, float scale, hipStream_t stream);
 int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int w, int nq, int C, int cs,
                     void* lvl0, void* lvl1, void* lvl2, void* lvl3, int num_levels, float scale, int out_bf16,
                     int blocked, hipStream_t stream);

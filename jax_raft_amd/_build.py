@@ -32,6 +32,7 @@ KERNEL_SOURCES = [
     CSRC / "kernels" / "conv_fam_d2.hip",
     CSRC / "kernels" / "conv_fam_g.hip",
     CSRC / "kernels" / "corr.hip",
+    CSRC / "kernels" / "corr_pyr.hip",
     CSRC / "kernels" / "elementwise.hip",
     CSRC / "kernels" / "conv_f32.hip",
     CSRC / "kernels" / "f32.hip",

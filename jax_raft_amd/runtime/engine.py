@@ -555,6 +555,7 @@ class RaftEngine:
                 if cfg is None:
                     cfg = _tune(spec, x, N, H, W, y, kw)
                     tunedb.record(self.arch, key, cfg)
+                cfg = self._agree(cfg)
                 _TUNE_CACHE[key + (str(self.device),)] = cfg
             kw = dict(kw, cfg=cfg)
         name = next((k for k, v in self._specs.items() if v is spec), None)
@@ -702,6 +703,21 @@ class RaftEngine:
                 self.cp_rank = dist.get_rank(self.cp_group)
                 self.cp_world = dist.get_world_size(self.cp_group)
 
+    def _agree(self, v: int) -> int:
+        """Context-parallel ranks build the same plan, so every tuning decision is taken
+        from rank 0: ranks timing the candidates themselves (on a shared GPU, or on GPUs
+        of different clocks) could pick different tile configs, i.e. flows that differ in
+        bf16 rounding between ranks."""
+        if not self.cp or self.cp_world == 1:
+            return v
+        import torch.distributed as dist
+
+        dev = self.device if dist.get_backend(self.cp_group) == "nccl" else torch.device("cpu")
+        t = torch.tensor([int(v)], dtype=torch.int64, device=dev)
+        src = dist.get_global_rank(self.cp_group, 0) if self.cp_group is not None else 0
+        dist.broadcast(t, src=src, group=self.cp_group)
+        return int(t.item())
+
     def _cp_slabs(self, h: int):
         from ..parallel.cp import row_slabs
 
@@ -806,6 +822,7 @@ class RaftEngine:
                     best = (el, c)
             code = best[1]
             tunedb.record(self.arch, key, code)
+        code = self._agree(code)
         _TUNE_CACHE[key + (str(self.device),)] = code
         self.chosen_cfgs[f"gru{gi}.halo"] = code
         return enc[code]

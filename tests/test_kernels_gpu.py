@@ -461,15 +461,19 @@ def test_conv_direct(kh, cout, xcs, ycs, ycoff):
     assert _rel(got[:, ycoff:ycoff + cout], ref.reshape(-1, cout)) < 1e-2
 
 
-@pytest.mark.parametrize("h,w,L,radius", [(55, 128, 4, 4), (13, 48, 3, 3), (16, 32, 2, 4)])
-def test_corr_blocked_layout_pyramid_and_lookup(h, w, L, radius):
+@pytest.mark.parametrize("h,w,L,radius,C", [(55, 128, 4, 4, 64), (13, 48, 3, 3, 64), (16, 32, 2, 4, 64),
+                                             (55, 128, 4, 4, 256), (13, 48, 3, 3, 128), (21, 32, 4, 4, 256),
+                                             (8, 16, 1, 2, 128)])
+def test_corr_blocked_layout_pyramid_and_lookup(h, w, L, radius, C):
     """Blocked level layout (levels 0 / 1 stored as the pyramid kernel's 8x16
     tiles): the pyramid written blocked equals the row-major reference once
     un-blocked, and the lookup on it (wide and per-lane kernels) matches the
-    reference lookup of the row-major pyramid."""
+    reference lookup of the row-major pyramid.  C = 128 / 256: the persistent
+    kernel of corr_pyr.hip (partial query tiles at 13 x 48, 21 x 32); C = 64: the
+    tile kernel of corr.hip."""
     nat = _nat()
     torch.manual_seed(9)
-    B, C = 2, 64
+    B = 2
     f1 = torch.randn(B, h, w, C)
     f2 = torch.randn(B, h, w, C)
     ref = R.build_pyramid(_bf(f1), _bf(f2), L)
