@@ -653,8 +653,11 @@ extern "C" int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int
   void* lv[4] = {lvl0, lvl1, lvl2, lvl3};
   for (int l = 0; l < num_levels; ++l) wide = wide && reinterpret_cast<uintptr_t>(lv[l]) % 16 == 0;
   if (blocked && !wide) return (int)hipErrorInvalidValue;   // the blocked layout is written by the wide epilogue only
-  static const bool tile_pyr = getenv("JR_PYR_TILE") != nullptr;   // A/B: the tile kernel below
-  if (blocked && nq == h * w && !tile_pyr) {
+  // the persistent kernel (corr_pyr.hip) holds every CU for the whole build: at batch 1 the
+  // pipelined graph runs the previous pair's loop concurrently, and the short-lived tiles of
+  // the kernel below interleave with it (measured b1 stream 227 vs 200-204 FPS)
+  static const bool tile_pyr = getenv("JR_PYR_TILE") != nullptr;   // A/B: always the tile kernel
+  if (blocked && nq == h * w && B >= 2 && !tile_pyr) {
     const int e = jr_corr_pyramid_blocked(f1, f2, B, h, w, C, cs, lvl0, lvl1, lvl2, lvl3, num_levels, scale, stream);
     if (e != (int)hipErrorNotSupported) return e;
   }

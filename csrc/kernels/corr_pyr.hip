@@ -44,8 +44,8 @@ __global__ __launch_bounds__(256, OCC) void corr_pyr_blocked_kernel(const bf16* 
                                                                   const bf16* __restrict__ f2, int h, int w, int cs,
                                                                   bf16* __restrict__ l0, bf16* __restrict__ l1,
                                                                   bf16* __restrict__ l2, bf16* __restrict__ l3,
-                                                                  int nlev, float scale, long items, int nwg,
-                                                                  int acc23, int qtmajor) {
+                                                                  int nlev, float scale, int items, int nwg,
+                                                                  int acc23, int qtmajor, int dbg) {
   constexpr int C = 16 * KS;
   constexpr int RB = 2 * C;               // bytes of one target row in the B tile
   constexpr int CPR = C / 8;              // 16-B chunks per target row
@@ -59,14 +59,12 @@ __global__ __launch_bounds__(256, OCC) void corr_pyr_blocked_kernel(const bf16* 
   const long qs0 = (long)ntt * 128, qs1 = (long)ntt * 32;   // per-query blocked level sizes
   // XCD-contiguous logical id: block g runs on XCD g % 8
   const int g = blockIdx.x, lid = (g & 7) * (nwg >> 3) + (g >> 3);
-  const long i0 = items * lid / nwg, i1 = items * (lid + 1) / nwg;
+  const int i0 = (int)((long)items * lid / nwg), i1 = (int)((long)items * (lid + 1) / nwg);
   if (i0 >= i1) return;
 
   u32x4 bst[NLD];
-  auto load_b = [&](long it) {   // B tile of item `it` -> registers
-    const int tt = (int)(it % ntt);
-    const int b = (int)(it / ((long)ntt * nqt));
-    const int ty0 = (tt / ntx) * 8, tx0 = (tt % ntx) * 16;
+  auto load_b = [&](int b, int ty_t, int tx_t) {   // B tile of an item -> registers
+    const int ty0 = ty_t * 8, tx0 = tx_t * 16;
     const bf16* base = f2 + (long)b * P * cs;
 #pragma unroll
     for (int k = 0; k < NLD; ++k) {
@@ -85,13 +83,21 @@ __global__ __launch_bounds__(256, OCC) void corr_pyr_blocked_kernel(const bf16* 
 
   bf16x8 qf[KS];   // this lane's query features (MFMA B operand): channels 16 ks + 8 hh ..
   int cur_q = -1;
-  load_b(i0);
+  // item coordinates, advanced incrementally (image b, query tile qt, target tile row / column)
+  int b = i0 / (ntt * nqt), qt = (i0 / ntt) % nqt, ty_t = (i0 % ntt) / ntx, tx_t = i0 % ntx;
+  load_b(b, ty_t, tx_t);
   store_b();
   __syncthreads();
-  for (long it = i0; it < i1; ++it) {
-    const int tt = (int)(it % ntt);
-    const int qt = (int)((it / ntt) % nqt);
-    const int b = (int)(it / ((long)ntt * nqt));
+  for (int it = i0; it < i1; ++it) {
+    int nb = b, nq_t = qt, nty_t = ty_t, ntx_t = tx_t + 1;
+    if (ntx_t == ntx) {
+      ntx_t = 0;
+      if (++nty_t == nty) {
+        nty_t = 0;
+        if (++nq_t == nqt) { nq_t = 0; ++nb; }
+      }
+    }
+    const int tt = ty_t * ntx + tx_t;
     const int qtile = b * nqt + qt;
     if (qtile != cur_q) {
       cur_q = qtile;
@@ -100,7 +106,7 @@ __global__ __launch_bounds__(256, OCC) void corr_pyr_blocked_kernel(const bf16* 
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) qf[ks] = *(const bf16x8*)(qp + 16 * ks);
     }
-    if (it + 1 < i1) load_b(it + 1);   // in flight during the MFMAs
+    if (it + 1 < i1) load_b(nb, nty_t, ntx_t);   // in flight during the MFMAs
 
     // D[target 32 n + m][query] over 4 target blocks
     f32x16 acc[4];
@@ -117,10 +123,10 @@ __global__ __launch_bounds__(256, OCC) void corr_pyr_blocked_kernel(const bf16* 
         a[n] = *(const bf16x8*)(sm + tr * RB + ((c ^ (tr & 15)) << 4));
       }
 #pragma unroll
-      for (int n = 0; n < 4; ++n) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[n], qf[ks], acc[n], 0, 0, 0);
+      for (int n = 0; n < 4; ++n)
+        if (!(dbg & 2)) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[n], qf[ks], acc[n], 0, 0, 0);
     }
 
-    const int ty_t = tt / ntx, tx_t = tt % ntx;
     const int qi = wave * 32 + rho;          // query within the tile
     const int q = qt * 128 + qi;
     const bool qok = q < P;
@@ -193,7 +199,7 @@ __global__ __launch_bounds__(256, OCC) void corr_pyr_blocked_kernel(const bf16* 
         u32x4 v = *(const u32x4*)(st0 + qj * 256 + ((c ^ (s >> 1)) << 4));
         if (s & 1) v = u32x4{v[2], v[3], v[0], v[1]};
         const long o0 = qtmajor ? ((((long)b * nqt + qt) * ntt + tt) * 128 + qj) * 128 : (qrow + qj) * qs0 + (long)tt * 128;
-        if (qt * 128 + qj < P) *(u32x4*)(l0 + o0 + 8 * c) = v;
+        if (qt * 128 + qj < P && !(dbg & 1)) *(u32x4*)(l0 + o0 + 8 * c) = v;
       }
       if (nlev >= 2) {
 #pragma unroll
@@ -204,12 +210,12 @@ __global__ __launch_bounds__(256, OCC) void corr_pyr_blocked_kernel(const bf16* 
 #pragma unroll
           for (int i = 0; i < 4; ++i) e[i] = *(const unsigned*)(st1 + qj * 64 + (((4 * c + i) ^ s) << 2));
           const long o1 = qtmajor ? ((((long)b * nqt + qt) * ntt + tt) * 128 + qj) * 32 : (qrow + qj) * qs1 + (long)tt * 32;
-          if (qt * 128 + qj < P) *(u32x4*)(l1 + o1 + 8 * c) = u32x4{e[0], e[1], e[2], e[3]};
+          if (qt * 128 + qj < P && !(dbg & 1)) *(u32x4*)(l1 + o1 + 8 * c) = u32x4{e[0], e[1], e[2], e[3]};
         }
       }
       if (acc23 && nlev >= 3 && (tx_t == ntx - 1 || it + 1 == i1)) {
         // this WG's run of tile row ty_t ends: tiles tx_lo .. tx_t of it are in LDS
-        const int tx_lo = tx_t - (int)(it - (it - tx_t > i0 ? it - tx_t : i0));
+        const int tx_lo = tx_t - (it - (it - tx_t > i0 ? it - tx_t : i0));
         const int nt = tx_t - tx_lo + 1;
         for (int idx = tid; idx < 128 * 2 * nt; idx += 256) {
           const int qj = idx / (2 * nt), r = idx - qj * 2 * nt, m = r / nt, t = tx_lo + r - m * nt;
@@ -227,6 +233,7 @@ __global__ __launch_bounds__(256, OCC) void corr_pyr_blocked_kernel(const bf16* 
       }
     }
     lds_sync();   // B(it + 1) in place; staging reads done
+    b = nb; qt = nq_t; ty_t = nty_t; tx_t = ntx_t;
   }
 }
 
@@ -240,9 +247,12 @@ extern "C" int jr_corr_pyramid_blocked(const void* f1, const void* f2, int B, in
   for (void* p : {l0, l1, l2, l3})
     if (reinterpret_cast<uintptr_t>(p) % 16) return (int)hipErrorNotSupported;
   const long P = (long)h * w, nqt = (P + 127) / 128, ntt = (long)(w / 16) * ((h + 7) / 8);
-  const long items = (long)B * nqt * ntt;
+  const long items_l = (long)B * nqt * ntt;
+  if (items_l >= (1L << 31)) return (int)hipErrorNotSupported;
+  const int items = (int)items_l;
   const int occ = 1;
   static const int qtm = getenv("JR_PYR_QT") != nullptr;   // experiment: query-tile-major levels 0 / 1
+  static const int dbg = getenv("JR_PYR_DBG") ? atoi(getenv("JR_PYR_DBG")) : 0;   // 1: no L0/L1 stores, 2: no MFMA
   int nwg = occ * 256;
   if (items < nwg) nwg = (int)((items + 7) / 8 * 8);
   // the B tile, the level 0 / 1 staging (40 KB), the level 2 / 3 rows (w <= 256)
@@ -257,7 +267,7 @@ extern "C" int jr_corr_pyramid_blocked(const void* f1, const void* f2, int B, in
     if (!attr) return (int)hipErrorInvalidValue;                                                                 \
     hipLaunchKernelGGL((corr_pyr_blocked_kernel<KS_, OCC_>), dim3(nwg), dim3(256), lds, stream, (const bf16*)f1,        \
                        (const bf16*)f2, h, w, cs, (bf16*)l0, (bf16*)l1, (bf16*)l2, (bf16*)l3, nlev, scale, items,  \
-                       nwg, acc23, qtm);                                                                            \
+                       nwg, acc23, qtm, dbg);                                                                            \
   }
   if (C == 256) JR_PYR(16, 1) else JR_PYR(8, 1)
 #undef JR_PYR

@@ -448,16 +448,25 @@ __global__ __launch_bounds__(256) void pack_pieces_kernel(const PackPiece* __res
     const long co = pc.co0 + r / taps;
     const long sco = co - pc.co0 + pc.so_co, sci = ci - pc.ci0 + pc.so_ci;
     float v;
-    if (pc.mode == 0) {          // forward: W[tap][ci][co]
+    if (pc.mode == 0 || pc.mode == 4) {          // forward: W[tap][ci][co]
       v = src[(tap * pc.cin_s + sci) * pc.cout_s + sco];
-    } else if (pc.mode == 1) {   // data gradient: W[flipped tap][src in = co][src out = ci]
+    } else if (pc.mode == 1 || pc.mode == 5) {   // data gradient: W[flipped tap][src in = co][src out = ci]
       const long th = tap / pc.kw, tw = tap % pc.kw;
       const long ft = (pc.kh - 1 - th) * pc.kw + (pc.kw - 1 - tw);
       v = src[(ft * pc.cin_s + sco) * pc.cout_s + sci];
     } else {                     // flow-head taps: dst (1,1,cin,18), co = 2 * src tap + c
       v = src[((co >> 1) * pc.cin_s + sci) * pc.cout_s + (co & 1)];
     }
-    ((bf16*)pc.dst)[packed_row(co) * pc.kpad + tap * pc.cin8 + ci] = f2bf(v);
+    if (pc.mode >= 4) {
+      // halo weight stream (conv_halo.hip, ops/native.py:pack_gru_halo): fragment (co / 32,
+      // k / 16), lane 32 ((k >> 3) & 1) + r with _m32_chan(r) = co % 32, element k & 7
+      const long k = tap * pc.cin8 + ci, c = co & 31;
+      const long r = ((c >> 2) & 3) * 8 + ((c >> 4) & 1) * 4 + (c & 3);
+      const long ks = taps * pc.cin8 / 16;
+      ((bf16*)pc.dst)[(((co >> 5) * ks + (k >> 4)) * 64 + ((k >> 3) & 1) * 32 + r) * 8 + (k & 7)] = f2bf(v);
+    } else {
+      ((bf16*)pc.dst)[packed_row(co) * pc.kpad + tap * pc.cin8 + ci] = f2bf(v);
+    }
   }
 }
 

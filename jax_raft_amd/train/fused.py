@@ -164,11 +164,13 @@ class Packer:
 
     def piece(self, src, spec, mode: int, co, ci, so_co: int = 0, so_ci: int = 0):
         """dst output channels co = (co0, co1), input channels ci = (ci0, ci1) of
-        ``spec`` from ``src`` (mode 0 forward, 1 data gradient, 2 flow-head taps)."""
+        ``spec`` from ``src`` (mode 0 forward, 1 data gradient, 2 flow-head taps; 4 / 5: the
+        forward / data-gradient weights in the halo conv's stream layout, ``spec.wh``)."""
         src = self._src(src.data)
         kh, kw = spec.kh, spec.kw
-        self.dsts.append(spec.w)
-        self.rows.append([src.data_ptr(), spec.w.data_ptr(), kh, kw, src.shape[2], src.shape[3], spec.cin8,
+        dst = spec.wh if mode >= 4 else spec.w
+        self.dsts.append(dst)
+        self.rows.append([src.data_ptr(), dst.data_ptr(), kh, kw, src.shape[2], src.shape[3], spec.cin8,
                           spec.w.shape[1], co[0], co[1], ci[0], ci[1], so_co, so_ci, mode, 0])
 
     def bias(self, src, dst: torch.Tensor, co, so: int = 0):
@@ -202,14 +204,20 @@ def record_conv(plan, spec, x, N, H, W, y, *, tx=None, ix=None, extra=None, **kw
     arch = tunedb.gpu_arch(x.device)
     key = ("train", N, H, W, OH, OW, spec.kh, spec.kw, spec.sh, spec.sw, spec.ph, spec.pw, spec.cin8, spec.cout,
            x.shape[-1], tuple(extra) if extra else None)
+    # plain-epilogue 3x3 convs may also run on the halo kernel (conv_halo.hip); keyed apart from
+    # decisions made before it was a candidate
+    halo = nat.halo_cfgs_for(spec, dict(kw, y=y)) if tx is None and not extra and x_coff == 0 else ()
+    cands = tuple(nat.TUNE_CFGS) + tuple(halo)
+    if halo:
+        key = key + ("halo",)
     cfg = _CFG_CACHE.get(key + (str(x.device),))
     if cfg is None:
-        cfg = tunedb.lookup(arch, key, nat.TUNE_CFGS)   # persisted decision (runtime/tunedb.py)
+        cfg = tunedb.lookup(arch, key, cands)   # persisted decision (runtime/tunedb.py)
     ops = nat.ops()
     if cfg is None:
         scratch = torch.empty(N * OH * OW, round_up(spec.cout, 8), dtype=BF16, device=x.device)
         best = None
-        for c in nat.TUNE_CFGS:
+        for c in cands:
             t, i, a = nat.conv_args(spec, x, N, H, W, scratch, x_coff=x_coff, cfg=c)
             if extra:
                 i = i + list(extra)

@@ -140,9 +140,14 @@ class EncoderTrain:
         pk = Packer()
         for c in self._convs():
             kh, kw, cin, cout = c.kernel.shape
-            pk.piece(c.kernel, self._specs[id(c)], 0, (0, cout), (0, cin))
-            pk.bias(c.bias, self._specs[id(c)].b, (0, cout))
-            pk.piece(c.kernel, self._tspecs[id(c)], 1, (0, cin), (0, cout))
+            sp, tp = self._specs[id(c)], self._tspecs[id(c)]
+            pk.piece(c.kernel, sp, 0, (0, cout), (0, cin))
+            pk.bias(c.bias, sp.b, (0, cout))
+            pk.piece(c.kernel, tp, 1, (0, cin), (0, cout))
+            if sp.wh is not None:   # halo-kernel weight streams of the stride-1 3x3 convs
+                pk.piece(c.kernel, sp, 4, (0, cout), (0, cin))
+            if tp.wh is not None and c.stride == (1, 1):
+                pk.piece(c.kernel, tp, 5, (0, cin), (0, cout))
         return pk
 
     def _affine(self, unit):
@@ -228,6 +233,10 @@ class EncoderTrain:
 
         tp = self._tspecs[id(u.conv)]
         s = u.conv.stride
+        if gin is None and s == (1, 1) and out.dtype == BF16:
+            # nothing to accumulate: a plain conv over the flipped weights (halo-kernel candidate)
+            self.tuner(self.plan_b, tp, dy, u.N, u.OH, u.OW, out, act=ACT_NONE)
+            return
         tx, ix = _tx(s1=Seg(gin=gin, out=out))
         extra = None if s == (1, 1) else [u.H, u.W, _log2(s[0]), _log2(s[1])]
         self.tuner(self.plan_b, tp, dy, u.N, u.OH, u.OW, out, tx=tx, ix=ix, epi=EPI_BWD, hidden=0, extra=extra)

@@ -117,3 +117,35 @@ def test_conv_halo_input_instance_norm(idx):
     nat.ops().conv(t, i, a)
     torch.cuda.synchronize()
     assert _rel(y.float().cpu().reshape(N, H, W, cout), ref) < 1.5e-2
+
+
+@pytest.mark.parametrize("cin,cout", [(64, 64), (96, 96), (128, 192), (256, 126)])
+def test_training_repack_of_halo_weights(cin, cout):
+    """The training step's one-launch weight repack (train.hip:pack_pieces_kernel, modes 4 / 5)
+    writes the halo conv's weight stream of a conv and of its data gradient exactly as
+    ops/native.py:pack_halo_conv does from the (flipped, transposed) kernel."""
+    from jax_raft_amd.ops import native as nat
+    from jax_raft_amd.train.fused import Packer, _flip_t
+
+    torch.manual_seed(cin + cout)
+    k = torch.randn(3, 3, cin, cout, device=DEV)
+    b = torch.zeros(cout, device=DEV)
+    sp = nat.make_spec(k, b, (1, 1), (1, 1), device=DEV)
+    kt = _flip_t(k)
+    tp = nat.make_spec(kt, torch.zeros(cin, device=DEV), (1, 1), (1, 1), cin8=nat.round_up(cout, 8), device=DEV)
+    assert sp.wh is not None
+    want_f = sp.wh.clone()
+    want_t = tp.wh.clone() if tp.wh is not None else None
+    sp.wh.zero_()
+    if tp.wh is not None:
+        tp.wh.zero_()
+    k2 = k.clone().contiguous()
+    pk = Packer()
+    pk.piece(k2, sp, 4, (0, cout), (0, cin))
+    if tp.wh is not None:
+        pk.piece(k2, tp, 5, (0, cin), (0, cout))
+    pk.record(None)
+    torch.cuda.synchronize()
+    assert torch.equal(sp.wh, want_f)
+    if want_t is not None:
+        assert torch.equal(tp.wh, want_t)
