@@ -40,7 +40,9 @@ JR_DEVICE int lane_px(int rho) {
 template <int CIN>
 constexpr int pitch_of() { return CIN <= 64 ? 8 : CIN <= 128 ? 16 : 32; }
 
-template <int CIN, int WCO, int WPX, int TN, int TR, int TC>
+// INN: the input is normalised (+ residual) while loading (p.in_stats set); a separate
+// instantiation so the plain convs keep their register budget
+template <int CIN, int WCO, int WPX, int TN, int TR, int TC, bool INN>
 __global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHaloParams p) {
   constexpr int NT = 64 * WCO * WPX;
   constexpr int P = pitch_of<CIN>();
@@ -73,18 +75,22 @@ __global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHal
   for (int d = 0; d < PD; ++d) ring[d] = __builtin_bit_cast(bf16x8, bload(ws, w_base + (unsigned)d * 1024u));
 
   // footprint -> LDS: batches of up to 16 loads per thread in flight; the input instance norm
-  // (per-channel scale / shift of image n, a table after the footprint) is applied on the way
+  // (per-channel scale / shift of image n, tables after the footprint) and the optional
+  // residual are applied on the way, the tile's own pixels optionally written back (xn)
   {
-    float* const nrm = (float*)(lds_b + NFP * RB);
+    float* const nrm = (float*)(lds_b + NFP * RB);   // [CIN][2] input, [CIN][2] residual
     const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)p.in_res, (short)0, (int)p.x_bytes, 0x00020000);
     constexpr int TOTAL = NFP * CC;
     constexpr int NL = (TOTAL + NT - 1) / NT;
-    constexpr int NBAT = NL < 16 ? NL : 16;
-    const bool norm = p.in_stats != nullptr;
+    constexpr int NBMAX = INN ? 8 : 16;   // the normalising loader holds the residual chunks too
+    constexpr int NBAT = NL < NBMAX ? NL : NBMAX;
+    constexpr bool norm = INN;
+    const bool resid = INN && p.in_res != nullptr;
 #pragma unroll
     for (int l0 = 0; l0 < NL; l0 += NBAT) {
-      u32x4 v[NBAT];
-      int dst[NBAT];
+      u32x4 v[NBAT], vr[NBAT];
+      int dst[NBAT], pix[NBAT];
 #pragma unroll
       for (int k = 0; k < NBAT; ++k) {
         const int idx = (l0 + k) * NT + tid;
@@ -93,19 +99,26 @@ __global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHal
         const int y = y0 - 1 + fy, x = x0 - 1 + fx;
         const bool live = l0 + k < NL && idx < TOTAL;
         const bool in = live && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
-        const unsigned off = (unsigned)((n * p.H + y) * p.W + x) * (unsigned)p.xcs * 2u + (unsigned)(p.xoff + 8 * c) * 2u;
+        const int m = (n * p.H + y) * p.W + x;
+        const unsigned off = (unsigned)m * (unsigned)p.xcs * 2u + (unsigned)(p.xoff + 8 * c) * 2u;
         v[k] = bload(xs, in ? off : HOOB);
+        if (resid) vr[k] = bload(rs, in ? (unsigned)m * (unsigned)p.in_rcs * 2u + (unsigned)(16 * c) : HOOB);
         // destination byte offset; bit 30: padding (stays zero through the norm), -1: none
         dst[k] = !live ? -1 : (f * RB + ((c ^ key_x<P>(fx + TC * fy)) << 4)) | (in ? 0 : 1 << 30) | (c << 20);
+        // image pixel of a tile-own footprint pixel (xn write-back), else -1
+        pix[k] = in && fy >= 1 && fy <= TR && fx >= 1 && fx <= TC ? m : -1;
       }
-      if (l0 == 0 && norm) {
-        for (int c = tid; c < CIN; c += NT) {
+      if (l0 == 0 && INN) {
+        for (int c = tid; c < 2 * CIN; c += NT) {
+          const float* stt = c < CIN ? p.in_stats : p.in_res_stats;
+          const int cc = c < CIN ? c : c - CIN;
+          if (stt == nullptr) continue;
           const float inv = 1.0f / (float)p.in_hw;
-          const float m = p.in_stats[((long)n * CIN + c) * 2] * inv;
-          const float var = fmaxf(p.in_stats[((long)n * CIN + c) * 2 + 1] * inv - m * m, 0.f);
+          const float mu = stt[((long)n * CIN + cc) * 2] * inv;
+          const float var = fmaxf(stt[((long)n * CIN + cc) * 2 + 1] * inv - mu * mu, 0.f);
           const float a = rsqrtf(var + p.in_eps);
           nrm[2 * c] = a;
-          nrm[2 * c + 1] = -m * a;
+          nrm[2 * c + 1] = -mu * a;
         }
         __syncthreads();
       }
@@ -115,18 +128,24 @@ __global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHal
         if (norm && !(dst[k] >> 30)) {
           const int c = (dst[k] >> 20) & 63;
           bf16x8 e = __builtin_bit_cast(bf16x8, v[k]);
+          const bf16x8 er = __builtin_bit_cast(bf16x8, resid ? vr[k] : u32x4{0u, 0u, 0u, 0u});
           const f32x4* ab = (const f32x4*)(nrm + 16 * c);
+          const f32x4* abr = (const f32x4*)(nrm + 2 * CIN + 16 * c);
+          const bool rn = resid && p.in_res_stats != nullptr;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const f32x4 t = ab[q];   // (a, b) of channels 8c + 2q, 8c + 2q + 1
+            const f32x4 tr = rn ? abr[q] : f32x4{1.f, 0.f, 1.f, 0.f};
 #pragma unroll
             for (int h2 = 0; h2 < 2; ++h2) {
               float fv = bf2f(e[2 * q + h2]) * t[2 * h2] + t[2 * h2 + 1];
+              if (resid) fv += bf2f(er[2 * q + h2]) * tr[2 * h2] + tr[2 * h2 + 1];
               if (p.in_relu) fv = fmaxf(fv, 0.f);
               e[2 * q + h2] = f2bf(fv);
             }
           }
           v[k] = __builtin_bit_cast(u32x4, e);
+          if (p.xn && pix[k] >= 0) *(u32x4*)((bf16*)p.xn + (long)pix[k] * p.xncs + 8 * c) = v[k];
         }
         *(u32x4*)(lds_b + (dst[k] & 0xfffff)) = v[k];
       }
@@ -254,18 +273,25 @@ constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
 int lds_bytes(const HaloCfg& c) {
   const int P = c.cin <= 64 ? 8 : c.cin <= 128 ? 16 : 32;
-  return (c.tr + 2) * (c.tc + 2) * P * 16 + c.cin * 8;   // footprint + input-norm table
+  return (c.tr + 2) * (c.tc + 2) * P * 16 + c.cin * 16;   // footprint + input / residual norm tables
+}
+
+template <int CIN, int WCO, int WPX, int TN, int TR, int TC, bool INN>
+int launch_v(const ConvHaloParams& p, hipStream_t s, int lds) {
+  static const bool attr = hipFuncSetAttribute((const void*)conv_halo_kernel<CIN, WCO, WPX, TN, TR, TC, INN>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  if (!attr) return (int)hipErrorInvalidValue;
+  const int cpad = (p.cout + 32 * WCO - 1) / (32 * WCO);
+  hipLaunchKernelGGL((conv_halo_kernel<CIN, WCO, WPX, TN, TR, TC, INN>), dim3(p.ntiles, cpad), dim3(64 * WCO * WPX), lds,
+                     s, p);
+  return (int)hipGetLastError();
 }
 
 template <int CIN, int WCO, int WPX, int TN, int TR, int TC>
 int launch(const ConvHaloParams& p, hipStream_t s, int lds) {
   if (p.TR != TR || p.TC != TC) return (int)hipErrorInvalidValue;
-  static const bool attr = hipFuncSetAttribute((const void*)conv_halo_kernel<CIN, WCO, WPX, TN, TR, TC>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-  if (!attr) return (int)hipErrorInvalidValue;
-  const int cpad = (p.cout + 32 * WCO - 1) / (32 * WCO);
-  hipLaunchKernelGGL((conv_halo_kernel<CIN, WCO, WPX, TN, TR, TC>), dim3(p.ntiles, cpad), dim3(64 * WCO * WPX), lds, s, p);
-  return (int)hipGetLastError();
+  return p.in_stats ? launch_v<CIN, WCO, WPX, TN, TR, TC, true>(p, s, lds)
+                    : launch_v<CIN, WCO, WPX, TN, TR, TC, false>(p, s, lds);
 }
 
 }  // namespace

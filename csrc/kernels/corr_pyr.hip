@@ -5,14 +5,14 @@
 // The volume (533 MB at raft_large batch 4) is the only traffic that has to reach HBM; the
 // tile kernel of corr.hip re-read both feature maps per 128 x 128 tile (1.6 GB of L2 reads,
 // 382 MB past L2: profiles/r4_corr_study.md).  Here:
-//   * one workgroup per CU walks a contiguous run of (image, query tile, target tile) items,
+//   * one workgroup (8 waves) per CU walks a contiguous run of (image, query tile, target tile) items,
 //     target tile fastest; runs are XCD-contiguous, so an XCD's CUs read one image's f2;
 //   * a wave keeps its 32 queries' features in registers (the MFMA B operand) for the whole
-//     run; only the 128-target tile (8 x 16 pixels, the MFMA A operand) is staged in LDS,
+//     run (two waves per query group, each for half the target tile); only the 128-target tile (8 x 16 pixels, the MFMA A operand) is staged in LDS,
 //     its loads for item k + 1 in flight during item k's MFMAs;
 //   * D[target][query]: a lane holds 16 targets of ONE query (rows 2n, 2n+1 of the tile,
-//     4 consecutive x twice), so the 2x2 / 4x4 pools are in-lane sums and the 8x8 one needs
-//     one lane^32 exchange;
+//     4 consecutive x twice), so the 2x2 pools are in-lane sums, the 4x4 ones need one
+//     lane^32 exchange and the 8x8 ones combine the two waves' exact level-2 cells in LDS;
 //   * levels 0 / 1 are transposed through an LDS staging area into whole 256 / 64-byte
 //     per-query blocks and written with coalesced 16-B stores; levels 2 / 3 are gathered per
 //     tile row in LDS and written as whole lines;
@@ -32,28 +32,33 @@ JR_DEVICE unsigned pack_bf16x2(float a, float b) {
   return (unsigned)__builtin_bit_cast(unsigned short, f2bf(a)) | ((unsigned)__builtin_bit_cast(unsigned short, f2bf(b)) << 16);
 }
 
-// KS = C / 16 feature-channel k-steps; OCC workgroups per CU (the 256-channel variant needs
-// 64 query + 64 accumulator + 64 staging registers per lane: one workgroup per CU)
 // LDS-only barrier: the global stores and the next tile's loads stay in flight
-// (__syncthreads() would drain vmcnt, i.e. wait for every store of the item: measured
-// 270 us at batch 4 with it)
+// (__syncthreads() would drain vmcnt, i.e. wait for every store of the item)
 JR_DEVICE void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int KS, int OCC>
-__global__ __launch_bounds__(256, OCC) void corr_pyr_blocked_kernel(const bf16* __restrict__ f1,
-                                                                  const bf16* __restrict__ f2, int h, int w, int cs,
-                                                                  bf16* __restrict__ l0, bf16* __restrict__ l1,
-                                                                  bf16* __restrict__ l2, bf16* __restrict__ l3,
-                                                                  int nlev, float scale, int items, int nwg,
-                                                                  int acc23, int qtmajor, int dbg) {
+// KS = C / 16 feature-channel k-steps.  8 waves, one workgroup per CU: wave (qg, th) holds
+// queries 32 qg .. of the tile (64 registers of features) and computes target blocks 2 th,
+// 2 th + 1 (tile rows 4 th .. 4 th + 3): two waves per SIMD hide each other's LDS / epilogue
+// latency (the 4-wave form measured 255 us at batch 4, one wave per SIMD).
+template <int KS>
+__global__ __launch_bounds__(512, 1) void corr_pyr_blocked_kernel(const bf16* __restrict__ f1,
+                                                                 const bf16* __restrict__ f2, int h, int w, int cs,
+                                                                 bf16* __restrict__ l0, bf16* __restrict__ l1,
+                                                                 bf16* __restrict__ l2, bf16* __restrict__ l3,
+                                                                 int nlev, float scale, int items, int nwg,
+                                                                 int acc23) {
   constexpr int C = 16 * KS;
+  constexpr int NT = 512;
   constexpr int RB = 2 * C;               // bytes of one target row in the B tile
   constexpr int CPR = C / 8;              // 16-B chunks per target row
-  constexpr int NLD = 128 * CPR / 256;    // B-tile chunks per thread
-  constexpr int BT = 128 * RB;            // LDS: [B tile | level 0 / 1 staging (40 KB) | level 2 / 3 rows]
+  constexpr int NLD = 128 * CPR / NT;     // B-tile chunks per thread
+  constexpr int BT = 128 * RB;
+  // LDS: [B tile | level 0 staging 32 KB | level 1 staging 8 KB | level 2 cells of the item
+  //       (fp32, 4 KB) | level 2 rows (bf16, 128 q x 2 x w2) | level 3 row (bf16, 128 q x w3)]
   extern __shared__ __attribute__((aligned(16))) char sm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rho = lane & 31, hh = lane >> 5;
+  const int qg = wave & 3, th = wave >> 2;
   const int P = h * w, ntx = w >> 4, nty = (h + 7) >> 3, ntt = ntx * nty, nqt = (P + 127) >> 7;
   const int h1 = h >> 1, h2 = h1 >> 1, w2 = (w >> 1) >> 1, h3 = h2 >> 1, w3 = w2 >> 1;
   const long qs0 = (long)ntt * 128, qs1 = (long)ntt * 32;   // per-query blocked level sizes
@@ -61,6 +66,11 @@ __global__ __launch_bounds__(256, OCC) void corr_pyr_blocked_kernel(const bf16* 
   const int g = blockIdx.x, lid = (g & 7) * (nwg >> 3) + (g >> 3);
   const int i0 = (int)((long)items * lid / nwg), i1 = (int)((long)items * (lid + 1) / nwg);
   if (i0 >= i1) return;
+  char* st0 = sm + BT;
+  char* st1 = st0 + 128 * 256;
+  float* l2c = (float*)(st1 + 128 * 64);   // [128 q][2 rows][4 cells]
+  char* a2 = (char*)(l2c + 128 * 8);
+  char* a3 = a2 + 128 * 2 * w2 * 2;
 
   u32x4 bst[NLD];
   auto load_b = [&](int b, int ty_t, int tx_t) {   // B tile of an item -> registers
@@ -68,7 +78,7 @@ __global__ __launch_bounds__(256, OCC) void corr_pyr_blocked_kernel(const bf16* 
     const bf16* base = f2 + (long)b * P * cs;
 #pragma unroll
     for (int k = 0; k < NLD; ++k) {
-      const int idx = k * 256 + tid, tr = idx / CPR, c = idx % CPR;
+      const int idx = k * NT + tid, tr = idx / CPR, c = idx % CPR;
       const int ty = min(ty0 + (tr >> 4), h - 1), tx = tx0 + (tr & 15);
       bst[k] = *(const u32x4*)(base + (long)(ty * w + tx) * cs + 8 * c);
     }
@@ -76,9 +86,14 @@ __global__ __launch_bounds__(256, OCC) void corr_pyr_blocked_kernel(const bf16* 
   auto store_b = [&]() {          // registers -> LDS, chunk c of target row tr in slot c ^ (tr & 15)
 #pragma unroll
     for (int k = 0; k < NLD; ++k) {
-      const int idx = k * 256 + tid, tr = idx / CPR, c = idx % CPR;
+      const int idx = k * NT + tid, tr = idx / CPR, c = idx % CPR;
       *(u32x4*)(sm + tr * RB + ((c ^ (tr & 15)) << 4)) = bst[k];
     }
+  };
+  // level-3 cell pair (x3 = 2 tx + 0 / 1) of tile query qj from its exact level-2 cells
+  auto l3_of = [&](int qj) {
+    const float* c = l2c + qj * 8;
+    return pack_bf16x2(0.25f * (c[0] + c[1] + c[4] + c[5]), 0.25f * (c[2] + c[3] + c[6] + c[7]));
   };
 
   bf16x8 qf[KS];   // this lane's query features (MFMA B operand): channels 16 ks + 8 hh ..
@@ -101,48 +116,56 @@ __global__ __launch_bounds__(256, OCC) void corr_pyr_blocked_kernel(const bf16* 
     const int qtile = b * nqt + qt;
     if (qtile != cur_q) {
       cur_q = qtile;
-      const int q = min(qt * 128 + wave * 32 + rho, P - 1);
+      const int q = min(qt * 128 + qg * 32 + rho, P - 1);
       const bf16* qp = f1 + ((long)b * P + q) * cs + 8 * hh;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) qf[ks] = *(const bf16x8*)(qp + 16 * ks);
     }
     if (it + 1 < i1) load_b(nb, nty_t, ntx_t);   // in flight during the MFMAs
 
-    // D[target 32 n + m][query] over 4 target blocks
-    f32x16 acc[4];
+    // D[target 32 n + m][query], n = 2 th + nn
+    f32x16 acc[2];
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int nn = 0; nn < 2; ++nn)
 #pragma unroll
-      for (int k = 0; k < 16; ++k) acc[n][k] = 0.f;
+      for (int k = 0; k < 16; ++k) acc[nn][k] = 0.f;
+    {   // A fragments one k-step ahead (all of them in flight at once would spill)
+      auto read_a = [&](int ks, bf16x8 (&a)[2]) {
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      bf16x8 a[4];
+        for (int nn = 0; nn < 2; ++nn) {
+          const int tr = 32 * (2 * th + nn) + rho, c = 2 * ks + hh;
+          a[nn] = *(const bf16x8*)(sm + tr * RB + ((c ^ (tr & 15)) << 4));
+        }
+      };
+      bf16x8 acur[2], anxt[2];
+      read_a(0, acur);
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int tr = 32 * n + rho, c = 2 * ks + hh;
-        a[n] = *(const bf16x8*)(sm + tr * RB + ((c ^ (tr & 15)) << 4));
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + 1 < KS) read_a(ks + 1, anxt);
+#pragma unroll
+        for (int nn = 0; nn < 2; ++nn)
+          acc[nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[nn], qf[ks], acc[nn], 0, 0, 0);
+#pragma unroll
+        for (int nn = 0; nn < 2; ++nn) acur[nn] = anxt[nn];
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_barrier(0);
       }
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-        if (!(dbg & 2)) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[n], qf[ks], acc[n], 0, 0, 0);
     }
 
-    const int qi = wave * 32 + rho;          // query within the tile
-    const int q = qt * 128 + qi;
-    const bool qok = q < P;
+    const int qi = qg * 32 + rho;            // query within the tile
     const int sw0 = qi & 15, sw1 = (qi >> 1) & 15;
-    char* st0 = sm + BT;                     // level 0: [128 q][32 units of 8 B]
-    char* st1 = st0 + 128 * 256;             // level 1: [128 q][16 units of 4 B]
-    float s2[2][2] = {{0.f, 0.f}, {0.f, 0.f}}, s3[2] = {0.f, 0.f};
+    float s2[2] = {0.f, 0.f};
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
+    for (int nn = 0; nn < 2; ++nn) {
+      const int n = 2 * th + nn;
 #pragma unroll
       for (int xg = 0; xg < 2; ++xg) {
         float v[2][4];
 #pragma unroll
         for (int rr = 0; rr < 2; ++rr)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[rr][i] = acc[n][rr * 8 + xg * 4 + i] * scale;
+          for (int i = 0; i < 4; ++i) v[rr][i] = acc[nn][rr * 8 + xg * 4 + i] * scale;
 #pragma unroll
         for (int rr = 0; rr < 2; ++rr) {   // level 0: row 2n + rr, x = 8 xg + 4 hh .. + 3
           const int u = (2 * n + rr) * 4 + 2 * xg + hh;
@@ -155,80 +178,67 @@ __global__ __launch_bounds__(256, OCC) void corr_pyr_blocked_kernel(const bf16* 
           const int u = n * 4 + 2 * xg + hh;
           *(unsigned*)(st1 + qi * 64 + ((u ^ sw1) << 2)) = pack_bf16x2(p0, p1);
         }
-        s2[n >> 1][xg] += p0 + p1;
-        s3[xg] += p0 + p1;
+        s2[xg] += p0 + p1;
       }
     }
-    // level 2 (rows 2 ty_t + m, x2 = 4 tx_t + 2 xg + hh): lane hh = m writes row m
-    // levels 2 / 3 of a target tile are 4 / 2 cells of a query row: gathered in LDS (acc23,
-    // 128 q x 2 rows x w2 + 128 q x w3 cells) and written once the WG's run of the tile row ends,
-    // as whole lines (8 tiles x 8 B per query row); else straight out
-    char* a2 = st1 + 128 * 64;
-    char* a3 = a2 + 128 * 2 * w2 * 2;
-    if (nlev >= 3) {   // level 2 (rows 2 ty_t + m, x2 = 4 tx_t + 2 xg + hh): lane hh = m takes row m
-      const float snd0 = hh ? s2[0][0] : s2[1][0], snd1 = hh ? s2[0][1] : s2[1][1];
-      const float r0 = __shfl_xor(snd0, 32), r1 = __shfl_xor(snd1, 32);
-      const float own0 = hh ? s2[1][0] : s2[0][0], own1 = hh ? s2[1][1] : s2[0][1];
-      // x2 order: (hh 0, xg 0), (hh 1, xg 0), (hh 0, xg 1), (hh 1, xg 1); s2 holds 4 level-1 cells
-      const float c0 = 0.25f * (hh ? r0 : own0), c1 = 0.25f * (hh ? own0 : r0);
-      const float c2 = 0.25f * (hh ? r1 : own1), c3 = 0.25f * (hh ? own1 : r1);
-      const u32x2 v2 = u32x2{pack_bf16x2(c0, c1), pack_bf16x2(c2, c3)};
-      const int Y2 = 2 * ty_t + hh;
-      if (acc23)
-        *(u32x2*)(a2 + ((qi * 2 + hh) * w2 + 4 * tx_t) * 2) = v2;
-      else if (qok && Y2 < h2)
-        *(u32x2*)(l2 + (((long)b * P + q) * h2 + Y2) * w2 + 4 * tx_t) = v2;
-    }
-    if (nlev >= 4) {   // level 3: one cell pair per query, x3 = 2 tx_t + xg
-      const float t0 = s3[0] + __shfl_xor(s3[0], 32), t1 = s3[1] + __shfl_xor(s3[1], 32);
-      const unsigned v3 = pack_bf16x2(t0 * 0.0625f, t1 * 0.0625f);
-      if (acc23) {
-        if (hh == 0) *(unsigned*)(a3 + (qi * w3 + 2 * tx_t) * 2) = v3;
-      } else if (qok && hh == 0 && ty_t < h3) {
-        *(unsigned*)(l3 + (((long)b * P + q) * h3 + ty_t) * w3 + 2 * tx_t) = v3;
+    if (nlev >= 3) {   // level 2: row th of the tile's two, x2 = 2 xg + hh
+      const float r0 = __shfl_xor(s2[0], 32), r1 = __shfl_xor(s2[1], 32);
+      if (hh == 0) {
+        const float c0 = 0.25f * s2[0], c1 = 0.25f * r0, c2 = 0.25f * s2[1], c3 = 0.25f * r1;
+        *(f32x4*)(l2c + qi * 8 + th * 4) = f32x4{c0, c1, c2, c3};
+        const u32x2 v2 = u32x2{pack_bf16x2(c0, c1), pack_bf16x2(c2, c3)};
+        const int q = qt * 128 + qi, Y2 = 2 * ty_t + th;
+        if (acc23)
+          *(u32x2*)(a2 + ((qi * 2 + th) * w2 + 4 * tx_t) * 2) = v2;
+        else if (q < P && Y2 < h2)
+          *(u32x2*)(l2 + (((long)b * P + q) * h2 + Y2) * w2 + 4 * tx_t) = v2;
       }
     }
     lds_sync();   // the B tile is consumed, the outputs staged
     if (it + 1 < i1) store_b();   // (waits for its loads: issued after the previous item's stores)
+    const long qrow = (long)b * P + qt * 128;
     // levels 0 / 1: whole per-query blocks, 16 threads per query row of 256 B
-    {
-      const long qrow = (long)b * P + qt * 128;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int idx = k * 256 + tid, qj = idx >> 4, c = idx & 15, s = qj & 15;
-        u32x4 v = *(const u32x4*)(st0 + qj * 256 + ((c ^ (s >> 1)) << 4));
-        if (s & 1) v = u32x4{v[2], v[3], v[0], v[1]};
-        const long o0 = qtmajor ? ((((long)b * nqt + qt) * ntt + tt) * 128 + qj) * 128 : (qrow + qj) * qs0 + (long)tt * 128;
-        if (qt * 128 + qj < P && !(dbg & 1)) *(u32x4*)(l0 + o0 + 8 * c) = v;
+    for (int k = 0; k < 4; ++k) {
+      const int idx = k * NT + tid, qj = idx >> 4, c = idx & 15, s = qj & 15;
+      u32x4 v = *(const u32x4*)(st0 + qj * 256 + ((c ^ (s >> 1)) << 4));
+      if (s & 1) v = u32x4{v[2], v[3], v[0], v[1]};
+      if (qt * 128 + qj < P) *(u32x4*)(l0 + (qrow + qj) * qs0 + (long)tt * 128 + 8 * c) = v;
+    }
+    if (nlev >= 2) {
+      const int qj = tid >> 2, c = tid & 3, s = (qj >> 1) & 15;
+      // 16-B chunk c = 4-B units 4c .. 4c + 3, stored at slots (4c + i) ^ s
+      unsigned e[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) e[i] = *(const unsigned*)(st1 + qj * 64 + (((4 * c + i) ^ s) << 2));
+      if (qt * 128 + qj < P) *(u32x4*)(l1 + (qrow + qj) * qs1 + (long)tt * 32 + 8 * c) = u32x4{e[0], e[1], e[2], e[3]};
+    }
+    const bool row_end = tx_t == ntx - 1 || it + 1 == i1;
+    if (nlev >= 4 && tid < 128) {   // level 3 of this tile: into the row buffer, or straight out
+      const int q = qt * 128 + tid;
+      if (acc23) {
+        if (!row_end) *(unsigned*)(a3 + (tid * w3 + 2 * tx_t) * 2) = l3_of(tid);
+      } else if (q < P && ty_t < h3) {
+        *(unsigned*)(l3 + ((qrow + tid) * h3 + ty_t) * w3 + 2 * tx_t) = l3_of(tid);
       }
-      if (nlev >= 2) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const int idx = k * 256 + tid, qj = idx >> 2, c = idx & 3, s = (qj >> 1) & 15;
-          // 16-B chunk c = 4-B units 4c .. 4c + 3, stored at slots (4c + i) ^ s
-          unsigned e[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) e[i] = *(const unsigned*)(st1 + qj * 64 + (((4 * c + i) ^ s) << 2));
-          const long o1 = qtmajor ? ((((long)b * nqt + qt) * ntt + tt) * 128 + qj) * 32 : (qrow + qj) * qs1 + (long)tt * 32;
-          if (qt * 128 + qj < P && !(dbg & 1)) *(u32x4*)(l1 + o1 + 8 * c) = u32x4{e[0], e[1], e[2], e[3]};
-        }
+    }
+    if (acc23 && nlev >= 3 && row_end) {
+      // this WG's run of tile row ty_t ends: tiles tx_lo .. tx_t of it are in LDS (the level-3
+      // cells of tile tx_t straight from the level-2 cells of this item)
+      const int tx_lo = tx_t - (it - (it - tx_t > i0 ? it - tx_t : i0));
+      const int nt = tx_t - tx_lo + 1;
+      for (int idx = tid; idx < 128 * 2 * nt; idx += NT) {
+        const int qj = idx / (2 * nt), r = idx - qj * 2 * nt, m = r / nt, t = tx_lo + r - m * nt;
+        const int Y2 = 2 * ty_t + m;
+        if (qt * 128 + qj < P && Y2 < h2)
+          *(u32x2*)(l2 + ((qrow + qj) * h2 + Y2) * w2 + 4 * t) = *(const u32x2*)(a2 + ((qj * 2 + m) * w2 + 4 * t) * 2);
       }
-      if (acc23 && nlev >= 3 && (tx_t == ntx - 1 || it + 1 == i1)) {
-        // this WG's run of tile row ty_t ends: tiles tx_lo .. tx_t of it are in LDS
-        const int tx_lo = tx_t - (it - (it - tx_t > i0 ? it - tx_t : i0));
-        const int nt = tx_t - tx_lo + 1;
-        for (int idx = tid; idx < 128 * 2 * nt; idx += 256) {
-          const int qj = idx / (2 * nt), r = idx - qj * 2 * nt, m = r / nt, t = tx_lo + r - m * nt;
-          const int Y2 = 2 * ty_t + m;
-          if (qt * 128 + qj < P && Y2 < h2)
-            *(u32x2*)(l2 + ((qrow + qj) * h2 + Y2) * w2 + 4 * t) = *(const u32x2*)(a2 + ((qj * 2 + m) * w2 + 4 * t) * 2);
-        }
-        if (nlev >= 4 && ty_t < h3) {
-          for (int idx = tid; idx < 128 * nt; idx += 256) {
-            const int qj = idx / nt, t = tx_lo + idx - qj * nt;
-            if (qt * 128 + qj < P)
-              *(unsigned*)(l3 + ((qrow + qj) * h3 + ty_t) * w3 + 2 * t) = *(const unsigned*)(a3 + (qj * w3 + 2 * t) * 2);
-          }
+      if (nlev >= 4 && ty_t < h3) {
+        for (int idx = tid; idx < 128 * nt; idx += NT) {
+          const int qj = idx / nt, t = tx_lo + idx - qj * nt;
+          if (qt * 128 + qj < P)
+            *(unsigned*)(l3 + ((qrow + qj) * h3 + ty_t) * w3 + 2 * t) =
+                t == tx_t ? l3_of(qj) : *(const unsigned*)(a3 + (qj * w3 + 2 * t) * 2);
         }
       }
     }
@@ -250,26 +260,23 @@ extern "C" int jr_corr_pyramid_blocked(const void* f1, const void* f2, int B, in
   const long items_l = (long)B * nqt * ntt;
   if (items_l >= (1L << 31)) return (int)hipErrorNotSupported;
   const int items = (int)items_l;
-  const int occ = 1;
-  static const int qtm = getenv("JR_PYR_QT") != nullptr;   // experiment: query-tile-major levels 0 / 1
-  static const int dbg = getenv("JR_PYR_DBG") ? atoi(getenv("JR_PYR_DBG")) : 0;   // 1: no L0/L1 stores, 2: no MFMA
-  int nwg = occ * 256;
+  int nwg = 256;
   if (items < nwg) nwg = (int)((items + 7) / 8 * 8);
-  // the B tile, the level 0 / 1 staging (40 KB), the level 2 / 3 rows (w <= 256)
+  // B tile, level 0 / 1 staging (40 KB), the item's level-2 cells (4 KB), the level 2 / 3 rows (w <= 256)
   const int w2 = w / 4, w3 = w / 8;
   const int acc23 = w <= 256 && nlev >= 3;
-  const int lds = 128 * 2 * C + 128 * (256 + 64) + (acc23 ? 128 * (2 * w2 + w3) * 2 : 0);
-  if (lds > 160 * 1024 / occ) return (int)hipErrorNotSupported;
-#define JR_PYR(KS_, OCC_)                                                                                        \
+  const int lds = 128 * 2 * C + 128 * (256 + 64 + 32) + (acc23 ? 128 * (2 * w2 + w3) * 2 : 0);
+  if (lds > 160 * 1024) return (int)hipErrorNotSupported;
+#define JR_PYR(KS_)                                                                                              \
   {                                                                                                              \
-    static const bool attr = hipFuncSetAttribute((const void*)corr_pyr_blocked_kernel<KS_, OCC_>,               \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 / OCC_) == hipSuccess; \
+    static const bool attr = hipFuncSetAttribute((const void*)corr_pyr_blocked_kernel<KS_>,                     \
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess; \
     if (!attr) return (int)hipErrorInvalidValue;                                                                 \
-    hipLaunchKernelGGL((corr_pyr_blocked_kernel<KS_, OCC_>), dim3(nwg), dim3(256), lds, stream, (const bf16*)f1,        \
+    hipLaunchKernelGGL((corr_pyr_blocked_kernel<KS_>), dim3(nwg), dim3(512), lds, stream, (const bf16*)f1,       \
                        (const bf16*)f2, h, w, cs, (bf16*)l0, (bf16*)l1, (bf16*)l2, (bf16*)l3, nlev, scale, items,  \
-                       nwg, acc23, qtm, dbg);                                                                            \
+                       nwg, acc23);                                                                              \
   }
-  if (C == 256) JR_PYR(16, 1) else JR_PYR(8, 1)
+  if (C == 256) JR_PYR(16) else JR_PYR(8)
 #undef JR_PYR
   return (int)hipGetLastError();
 }

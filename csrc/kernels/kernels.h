@@ -407,6 +407,12 @@ struct ConvHaloParams {
   // x' = act((x - mean[n][c]) * rsqrt(var[n][c] + eps)) from in_stats [N][cin][2] (sum, sumsq
   // over in_hw pixels; jr_norm_act mode 1 semantics), zero padding stays zero
   const float* in_stats; int in_hw; float in_eps; int in_relu;
+  // optional residual of that input (a residual block's output, built while loading):
+  // x' = act(norm(x) + r) with r = in_res (bf16, channel stride in_rcs), itself instance-
+  // normalised by in_res_stats if given; xn (channel stride xncs) receives x' of the tile's
+  // own pixels (the block output, needed again as the next block's residual)
+  const void* in_res; int in_rcs; const float* in_res_stats;
+  void* xn; int xncs;
   int TR, TC, tiles_y, tiles_x, ntiles;
   long x_bytes;
 };

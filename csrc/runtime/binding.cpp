@@ -268,6 +268,35 @@ static Launch make_conv_halo(const TList& t, const IList& i, double alpha, std::
     p.in_stats = ist.data_ptr<float>(); p.in_relu = (int)i[27]; p.in_hw = (int)i[28]; p.in_eps = 1e-5f;
     if (keep) keep->push_back(ist);
   }
+  // optional t[15..17]: the input's residual (bf16 [N][H][W][>= cin], channel offset 0), its
+  // stats ([N][cin][2], instance-normalised if given), the write-back of the built input
+  at::Tensor ires = opt(t, 15), irst = opt(t, 16), xn = opt(t, 17);
+  if (ires.defined() || irst.defined() || xn.defined()) {
+    TORCH_CHECK(ist.defined(), "conv_halo: an input residual / write-back needs the input norm");
+    const int64_t M = (int64_t)N * H * W;
+    if (ires.defined()) {
+      check_bf16(ires, "input residual");
+      TORCH_CHECK(cs(ires) % 8 == 0 && cs(ires) >= cin8 && ires.numel() >= M * cs(ires) &&
+                  (int64_t)ires.numel() * 2 <= (1LL << 31), "conv_halo: input residual [N][H][W][>= cin]");
+      p.in_res = ires.data_ptr(); p.in_rcs = cs(ires);
+      if (keep) keep->push_back(ires);
+    }
+    if (irst.defined()) {
+      TORCH_CHECK(ires.defined(), "conv_halo: residual stats without a residual");
+      check_f32(irst, "residual stats");
+      TORCH_CHECK(irst.numel() >= (int64_t)N * cin8 * 2, "conv_halo: residual stats [N][cin][2]");
+      p.in_res_stats = irst.data_ptr<float>();
+      if (keep) keep->push_back(irst);
+    }
+    if (xn.defined()) {
+      check_bf16(xn, "input write-back");
+      TORCH_CHECK(cs(xn) % 8 == 0 && cs(xn) >= cin8 && xn.numel() >= M * cs(xn), "conv_halo: xn [N][H][W][>= cin]");
+      TORCH_CHECK(!(xn.data_ptr() == x.data_ptr()) && !(ires.defined() && xn.data_ptr() == ires.data_ptr()),
+                  "conv_halo: xn must not alias the input or its residual (neighbouring tiles read them)");
+      p.xn = xn.data_ptr(); p.xncs = cs(xn);
+      if (keep) keep->push_back(xn);
+    }
+  }
   p.x_bytes = (long)x.numel() * 2;
   TORCH_CHECK(p.x_bytes < (1LL << 31), "conv_halo: input larger than 2 GiB");
   for (const at::Tensor* v : {&x, &wh, &y})

@@ -384,12 +384,15 @@ def conv_args(spec: ConvSpec, x: torch.Tensor, N: int, H: int, W: int, y: torch.
               res=None, res_coff: int = 0, res_post: int = 0, h32=None, zbuf=None, hidden: int = 0, coords=None,
               flow32=None, y3=None, y3_coff: int = 0, epi: int = EPI_STD, cfg: Optional[int] = None,
               bmap=None, bmap_coff: int = 0, tapw=None, out_hw: Optional[Tuple[int, int]] = None,
-              stats_part=None, in_stats=None, in_relu: int = 0, in_hw: int = 0):
+              stats_part=None, in_stats=None, in_relu: int = 0, in_hw: int = 0, in_res=None, in_res_stats=None,
+              xn=None):
     """Build the (tensors, ints, alpha) argument triple of the ``conv`` op.
     ``bmap``: optional fp32 per-pixel bias map [M, C], channels from ``bmap_coff``.
     Halo tile configs only (cfg >= HALO_CFG0): ``stats_part`` receives per-tile channel
     (sum, sumsq) partials of the output; ``in_stats`` ([N][cin][2] sums over ``in_hw``
-    pixels) normalises the input (instance norm, + relu if ``in_relu``) as it is loaded."""
+    pixels) normalises the input (instance norm, + relu if ``in_relu``) as it is loaded;
+    ``in_res`` (+ ``in_res_stats``: normalised too) is added before the relu (a residual
+    block's output built on the fly) and ``xn`` receives the built input."""
     OH, OW = out_hw if out_hw is not None else spec.out_hw(H, W)
     if cfg is None:
         cfg = pick_cfg(N * OH * OW, spec.cout)
@@ -399,9 +402,12 @@ def conv_args(spec: ConvSpec, x: torch.Tensor, N: int, H: int, W: int, y: torch.
     elif cfg >= HALO_CFG0:   # the halo 3x3 kernel (conv_halo.hip): its own weight stream
         assert spec.wh is not None, "halo tile config for a conv without halo weights"
         t.append(spec.wh)
-        if stats_part is not None or in_stats is not None:
+        if in_res is not None or in_res_stats is not None or xn is not None:
+            t += [stats_part, in_stats, in_res, in_res_stats, xn]
+        elif stats_part is not None or in_stats is not None:
             t += [stats_part, in_stats]
-    assert (stats_part is None and in_stats is None) or cfg >= HALO_CFG0, "stats / input norm need a halo config"
+    assert (stats_part is None and in_stats is None and in_res is None and xn is None) or cfg >= HALO_CFG0, \
+        "stats / input norm need a halo config"
     i = [N, H, W, x_coff, spec.cin8, spec.kh, spec.kw, spec.sh, spec.sw, spec.ph, spec.pw, spec.cout, act, split,
          y_coff, y2_coff, res_coff, hidden, y3_coff, epi, cfg, res_post]
     if bmap is not None or out_hw is not None or in_stats is not None:

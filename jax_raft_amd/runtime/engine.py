@@ -593,16 +593,18 @@ class RaftEngine:
         def halo_fusable(name) -> bool:
             return self.halo_norm and bool(nat.halo_cfgs_for(sp[name], {}))
 
-        def conv_stats(name, x, N, H, W, in_stats=None):
+        def conv_stats(name, x, N, H, W, in_stats=None, in_res=None, in_res_stats=None, xn=None):
             """A halo 3x3 conv that writes its output's channel-statistics partials (reduced
             by one small launch) and, given ``in_stats``, instance-normalises + relus its raw
             input as it loads it (no channel_stats pass over the output, no norm_act pass
-            over the input)."""
+            over the input); with ``in_res`` (+ its stats) the input is a residual block's
+            output relu(IN(x) + [IN](res)), built on the fly and written to ``xn``."""
             s = sp[name]
             y = alloc(name + ".y", (N, H, W, s.cout))
             nb_max = max(-(-H // c[4]) * -(-W // c[5]) * c[2] for c in nat.HALO_CFGS if c[0] == s.cin8)
             part = alloc(name + ".part", (N, nb_max, s.cout, 2), F32)
-            kw = dict(stats_part=part, in_stats=in_stats, in_relu=1, in_hw=H * W)
+            kw = dict(stats_part=part, in_stats=in_stats, in_relu=1, in_hw=H * W, in_res=in_res,
+                      in_res_stats=in_res_stats, xn=xn)
             kw = self._conv_kw(s, x, N, H, W, y, kw)
             if kw.get("cfg") is None or kw["cfg"] < nat.HALO_CFG0:   # an override chose another kernel
                 return None
@@ -630,10 +632,20 @@ class RaftEngine:
                               [1, mode_r, N_, H_ * W_, C, relu], 1e-5)
             return y
 
-        # stem
+        # Instance-norm encoders keep a block's output lazy -- (raw, stats, residual, its stats)
+        # -- and build it inside the next block's first conv when that is a stride-1 halo conv
+        # (which also writes it out for the next residual); otherwise one norm_act pass
+        # materialises it (JR_HALO_NORM=0: always).
+        pend = None
+
+        def materialise(p_):
+            return norm_act(p_["name"], p_["raw"], p_["s"], res=p_["res"], sr=p_["rs"],
+                            mode_r=1 if p_["rs"] is not None else 0, relu=3 if p_["res"] is not None else 2)
+
         if inorm:
             y, H, W = stem()
-            x = norm_act(f"{tag}.stem", y, stats(f"{tag}.stem", y, N, H * W, y.shape[-1]), relu=2)
+            pend = dict(name=f"{tag}.stem", raw=y, s=stats(f"{tag}.stem", y, N, H * W, y.shape[-1]), res=None, rs=None)
+            x = None
         else:
             x, H, W = stem(act=ACT_RELU)
         for li in (1, 2, 3):
@@ -646,7 +658,21 @@ class RaftEngine:
                 if inorm:
                     h_, w_ = H, W
                     y, ys = x, None   # ys: stats of a raw conv output y still to be normalised
-                    for j, nm in enumerate(names):
+                    j0 = 0
+                    c1 = f"{pre}.{names[0]}"
+                    if (pend is not None and not has_ds and halo_fusable(c1) and sp[c1].out_hw(h_, w_) == (h_, w_)
+                            and pend["raw"].shape[-1] == sp[c1].cin8):
+                        xb = alloc(f"{pre}.x", tuple(pend["raw"].shape))
+                        fused = conv_stats(c1, pend["raw"], N, h_, w_, in_stats=pend["s"], in_res=pend["res"],
+                                           in_res_stats=pend["rs"], xn=xb)
+                        if fused is not None:
+                            x, pend = xb, None
+                            (y, ys), j0 = fused, 1
+                    if pend is not None:
+                        x, pend = materialise(pend), None
+                        y = x
+                    for j in range(j0, len(names)):
+                        nm = names[j]
                         cname = f"{pre}.{nm}"
                         fused = None
                         if halo_fusable(cname) and sp[cname].out_hw(h_, w_) == (h_, w_):
@@ -665,9 +691,12 @@ class RaftEngine:
                     if has_ds:
                         dr, _, _ = conv_raw(f"{pre}.downsample", x, N, H, W)
                         ds = stats(f"{pre}.downsample", dr, N, h_ * w_, dr.shape[-1])
-                        x = norm_act(f"{pre}.out", last, last_s, res=dr, sr=ds, mode_r=1, relu=3)
+                        pend = dict(name=f"{pre}.out", raw=last, s=last_s, res=dr, rs=ds)
                     else:
-                        x = norm_act(f"{pre}.out", last, last_s, res=x, mode_r=0, relu=3)
+                        pend = dict(name=f"{pre}.out", raw=last, s=last_s, res=x, rs=None)
+                    x = None
+                    if not self.halo_norm:
+                        x, pend = materialise(pend), None
                     H, W = h_, w_
                 else:
                     res = x
@@ -681,6 +710,8 @@ class RaftEngine:
                         else:
                             y, h_, w_ = conv_raw(f"{pre}.{nm}", y, N, h_, w_, act=ACT_RELU, res=res, res_post=1)
                     x, H, W = y, h_, w_
+        if pend is not None:
+            x = materialise(pend)
         return x, H, W
 
     # lanes pay off once the per-iteration kernels fill the chip: measured on

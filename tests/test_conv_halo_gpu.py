@@ -119,6 +119,45 @@ def test_conv_halo_input_instance_norm(idx):
     assert _rel(y.float().cpu().reshape(N, H, W, cout), ref) < 1.5e-2
 
 
+@pytest.mark.parametrize("idx,res_norm", [(0, False), (1, True), (2, True), (4, False), (6, True)])
+def test_conv_halo_builds_residual_block_output(idx, res_norm):
+    """A residual block's output relu(IN(x) + r) -- r the identity input or an instance-
+    normalised downsample output -- built while the footprint is loaded equals norm_act +
+    the conv, and the tile-own pixels of it are written out (xn) exactly once."""
+    nat = _nat()
+    cfg = nat.HALO_CFG0 + idx
+    cin = nat.HALO_CFGS[idx][0]
+    torch.manual_seed(5 + idx)
+    N, H, W, cout = 2, 13, 30, 64
+    x = (torch.randn(N, H, W, cin) * 2 + 0.5).to(DEV, torch.bfloat16)
+    r = (torch.randn(N, H, W, cin) * 1.5 - 0.2).to(DEV, torch.bfloat16)
+
+    def st(t):
+        f = t.float().reshape(N, H * W, cin)
+        return torch.stack([f.sum(1), (f * f).sum(1)], -1).contiguous()
+
+    def inorm(t):
+        f = t.float().reshape(N, H * W, cin)
+        m = f.mean(1, keepdim=True)
+        v = (f * f).mean(1, keepdim=True) - m * m
+        return ((f - m) * torch.rsqrt(v.clamp_min(0) + 1e-5)).reshape(N, H, W, cin)
+
+    built = torch.relu(inorm(x) + (inorm(r) if res_norm else r.float()))
+    k = torch.randn(3, 3, cin, cout) / math.sqrt(9 * cin)
+    b = torch.randn(cout) * 0.1
+    spec = nat.make_spec(k, b, (1, 1), (1, 1), device=DEV)
+    ref = R.conv2d_nhwc(_bf(built.cpu()), _bf(k), b, (1, 1), (1, 1))
+    y = torch.empty(N * H * W, cout, dtype=torch.bfloat16, device=DEV)
+    xn = torch.full((N, H, W, cin), float("nan"), dtype=torch.bfloat16, device=DEV)
+    t, i, a = nat.conv_args(spec, x, N, H, W, y, cfg=cfg, in_stats=st(x), in_relu=1, in_hw=H * W, in_res=r,
+                            in_res_stats=st(r) if res_norm else None, xn=xn)
+    nat.ops().conv(t, i, a)
+    torch.cuda.synchronize()
+    assert _rel(y.float().cpu().reshape(N, H, W, cout), ref) < 1.5e-2
+    assert not torch.isnan(xn.float()).any()
+    assert _rel(xn.float(), built) < 1e-2
+
+
 @pytest.mark.parametrize("cin,cout", [(64, 64), (96, 96), (128, 192), (256, 126)])
 def test_training_repack_of_halo_weights(cin, cout):
     """The training step's one-launch weight repack (train.hip:pack_pieces_kernel, modes 4 / 5)

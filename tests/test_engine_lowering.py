@@ -253,7 +253,9 @@ def test_encoder_instance_norm_fused_into_halo_convs(fake, monkeypatch, fuse):
     """raft_large's feature encoder (instance norm): with JR_HALO_NORM=1 every 3x3 / stride-1
     conv runs on a halo config that writes its statistics partials (one stats_final each, no
     channel_stats pass) and the conv after it normalises on load (the block-internal norm_act
-    passes disappear); block outputs are still materialised by norm_act."""
+    passes disappear); a block output (or the stem's) is built inside the next block's first
+    conv when that is a stride-1 halo conv, which writes it out for the residual; only the
+    outputs feeding a stride-2 block or the final 1x1 conv are materialised by norm_act."""
     monkeypatch.setenv("JR_HALO_NORM", fuse)
     monkeypatch.setenv("JR_PRO_LANES", "0")   # one feature-encoder pass over both images
     eng, p = _plan(raft_large, 1)
@@ -264,8 +266,12 @@ def test_encoder_instance_norm_fused_into_halo_convs(fake, monkeypatch, fuse):
         # per encoder image set: 10 stride-1 3x3 convs (4 in layer 1, 3 in layers 2 and 3)
         assert pro.count("stats_final") == 10 and len(halo_convs) == 10
         with_norm = [a for a in halo_convs if len(a[0]) > 14 and a[0][14] is not None]
-        assert len(with_norm) == 6            # the second conv of each of the 6 residual blocks
-        assert pro.count("norm_act") == 1 + 6  # stem + block outputs
+        assert len(with_norm) == 10           # every halo conv builds its input
+        with_res = [a for a in with_norm if len(a[0]) > 17 and a[0][15] is not None]
+        assert len(with_res) == 3 and all(a[0][17] is not None for a in with_res)   # L1B1, L2B1, L3B1 conv1
+        ds_res = [a for a in with_res if a[0][16] is not None]
+        assert len(ds_res) == 2               # layers 2 / 3 block 1: the residual is block 0's downsample
+        assert pro.count("norm_act") == 3     # outputs of L1B1 / L2B1 (before stride-2 blocks), L3B1
     else:
         assert "stats_final" not in pro and pro.count("norm_act") == 1 + 6 + 6
 
