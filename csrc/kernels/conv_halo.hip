@@ -49,7 +49,10 @@ __global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHal
   constexpr int CC = CIN / 8;
   constexpr int SPT = CIN / 16;           // k-steps per tap
   constexpr int S = 9 * SPT;
-  constexpr int PD = S >= 16 ? 16 : S;
+  // weight ring depth: 16 fragments, 8 for the 4-block waves at 2 waves / SIMD (256 VGPRs; each
+  // fragment there feeds 4 MFMAs, so 8 in flight still cover ~1000 cycles of L2 latency)
+  constexpr bool WIDE = TN >= 4 && WCO * WPX > 4;
+  constexpr int PD = S >= 16 ? (WIDE ? 8 : 16) : S;
   constexpr int FW = TC + 2;
   constexpr int NFP = (TR + 2) * FW;
   constexpr int RB = P * 16;              // footprint row bytes
@@ -83,7 +86,7 @@ __global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHal
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)p.in_res, (short)0, (int)p.x_bytes, 0x00020000);
     constexpr int TOTAL = NFP * CC;
     constexpr int NL = (TOTAL + NT - 1) / NT;
-    constexpr int NBMAX = INN ? 8 : 16;   // the normalising loader holds the residual chunks too
+    constexpr int NBMAX = INN || WIDE ? 8 : 16;   // the normalising loader holds the residual chunks too
     constexpr int NBAT = NL < NBMAX ? NL : NBMAX;
     constexpr bool norm = INN;
     const bool resid = INN && p.in_res != nullptr;
@@ -268,6 +271,15 @@ constexpr HaloCfg kCfgs[] = {
     {128, 4, 2, 2, 8, 16},  {128, 4, 1, 2, 4, 16}, {128, 2, 2, 2, 8, 16}, {128, 2, 1, 1, 4, 8},
     {256, 2, 2, 2, 8, 16},  {256, 2, 1, 1, 4, 8},  {128, 4, 1, 1, 4, 8},  {256, 4, 1, 1, 4, 8},
     {256, 2, 1, 2, 4, 16},
+    // all output channels of a loop conv in one workgroup, 128-pixel tiles (batch >= 4): the
+    // footprint is loaded once for every channel and each 1 KB weight fragment feeds 4 MFMAs, so
+    // the per-CU weight stream from L2 (the bound of the 64-pixel / 64-channel tiles) is 1/4 of it
+    {256, 6, 1, 4, 8, 16},  {256, 4, 1, 4, 8, 16},  {128, 8, 1, 4, 8, 16},  {128, 2, 1, 4, 8, 16},
+    {256, 6, 1, 2, 4, 16},  {256, 4, 1, 2, 4, 16},
+    // one 32-channel block per workgroup, 128-pixel tiles (batch 1): a CU streams 1/6 - 1/8 of the
+    // weights a whole-cout tile needs (the per-CU L2 stream bounds the 7040-pixel loop convs), the
+    // footprint is re-read per channel block from L2 instead
+    {256, 1, 2, 2, 8, 16},  {256, 1, 4, 1, 8, 16},  {128, 1, 2, 2, 8, 16},  {128, 1, 4, 1, 8, 16},
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -316,7 +328,10 @@ extern "C" int jr_conv_halo(const ConvHaloParams* p, int cfg, hipStream_t stream
   JR_HALO_CONV(96, 3, 1, 2, 4, 16) JR_HALO_CONV(128, 4, 2, 2, 8, 16) JR_HALO_CONV(128, 4, 1, 2, 4, 16)
   JR_HALO_CONV(128, 2, 2, 2, 8, 16) JR_HALO_CONV(128, 2, 1, 1, 4, 8) JR_HALO_CONV(256, 2, 2, 2, 8, 16)
   JR_HALO_CONV(256, 2, 1, 1, 4, 8) JR_HALO_CONV(128, 4, 1, 1, 4, 8) JR_HALO_CONV(256, 4, 1, 1, 4, 8)
-  JR_HALO_CONV(256, 2, 1, 2, 4, 16)
+  JR_HALO_CONV(256, 2, 1, 2, 4, 16) JR_HALO_CONV(256, 6, 1, 4, 8, 16) JR_HALO_CONV(256, 4, 1, 4, 8, 16)
+  JR_HALO_CONV(128, 8, 1, 4, 8, 16) JR_HALO_CONV(128, 2, 1, 4, 8, 16) JR_HALO_CONV(256, 6, 1, 2, 4, 16)
+  JR_HALO_CONV(256, 4, 1, 2, 4, 16) JR_HALO_CONV(256, 1, 2, 2, 8, 16) JR_HALO_CONV(256, 1, 4, 1, 8, 16)
+  JR_HALO_CONV(128, 1, 2, 2, 8, 16) JR_HALO_CONV(128, 1, 4, 1, 8, 16)
 #undef JR_HALO_CONV
   return (int)hipErrorInvalidValue;
 }

@@ -42,26 +42,36 @@ struct WgParams {
   const void* x; int xcs, xoff, N, H, W, cin8, KH, KW, SH, SW, PH, PW;
   const void* dy; int ycs, yoff, OH, OW, cout;
   int K, M, px_split;
+  int gx, gy, S, per;               // k tiles, cout tiles, pixel splits; workgroups per XCD
   float* part; int cout_pad, kpad;  // [S][cout_pad][kpad]
   float* bpart;                     // [S][cout_pad] (bias partials) or null
   long x_bytes, y_bytes;
 };
 
-template <int BCO, int BKK>
-__global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
+template <int BCO, int BKK, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const WgParams p) {
+  constexpr int NT = 64 * WM * WN;                 // threads: WM x WN waves over the output tile
   constexpr int UA = BCO / 4, UB = BKK / 4;        // 8-B units per LDS row
   constexpr int A_EL = WPX * BCO, B_EL = WPX * BKK;
   constexpr int CA = BCO / 8, CB = BKK / 8;        // 16-B chunks per pixel row
-  constexpr int NA = WPX * CA / 256, NB = WPX * CB / 256;  // chunks per thread
-  constexpr int TM = BCO / 32, TN = BKK / 32;      // 16x16 tiles per wave (2x2 waves)
+  constexpr int NA = WPX * CA / NT, NB = WPX * CB / NT;    // chunks per thread
+  constexpr int TM = BCO / WM / 16, TN = BKK / WN / 16;    // 16x16 tiles per wave
   static_assert(NA >= 1 && NB >= 1, "tile");
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (A_EL + B_EL)];
+  extern __shared__ __attribute__((aligned(16))) bf16 smem[];   // 2 x (A_EL + B_EL)
   constexpr unsigned OOB = 0x80000000u;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int k0 = blockIdx.x * BKK, co0 = blockIdx.y * BCO;
-  const int m_begin = blockIdx.z * p.px_split;
+  const int wr = wave / WN, wc = wave % WN;
+  // XCD-aware order: hardware block L runs on XCD L % 8, so logical workgroup (L % 8) * per + L / 8
+  // puts the gx * gy tiles of one pixel split -- which read the same dY rows and (tap-shifted) the
+  // same X rows -- on one L2, dispatched back to back.  Padding blocks (logical id past the grid) exit.
+  const int lid = (int)(blockIdx.x & 7) * p.per + (int)(blockIdx.x >> 3);
+  const int tps = p.gx * p.gy;
+  if (lid >= tps * p.S) return;
+  const int bz = lid / tps, bt = lid - bz * tps;
+  const int by = bt / p.gx, bx = bt - by * p.gx;
+  const int k0 = bx * BKK, co0 = by * BCO;
+  const int m_begin = bz * p.px_split;
   const int m_end = min(p.M, m_begin + p.px_split);
   const int OHW = p.OH * p.OW;
   const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
@@ -82,14 +92,14 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
   float bsum[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
-  const bool do_bias = p.bpart != nullptr && blockIdx.x == 0;
+  const bool do_bias = p.bpart != nullptr && bx == 0;
 
   // X rows of this thread: pixels m = stage base + rB + (256 / CB) i, tracked incrementally as
   // (n, oh, ow) (no integer division in the loop); every issue() advances them by one stage
   int xn[NB], xoh[NB], xow[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
-    const int m = m_begin + rB + (256 / CB) * i;
+    const int m = m_begin + rB + (NT / CB) * i;
     xn[i] = m / OHW;
     const int rem = m - xn[i] * OHW;
     xoh[i] = rem / p.OW;
@@ -101,14 +111,14 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
     const int mb = mb_next;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int m = mb + rA + (256 / CA) * i;
+      const int m = mb + rA + (NT / CA) * i;
       const bool ok = a_ok && m < m_end;
       const unsigned off = (unsigned)(((long)m * p.ycs + p.yoff + co0 + 8 * cA) * 2);
       r.a[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ys, ok ? off : OOB, 0, 0));
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int m = mb + rB + (256 / CB) * i;
+      const int m = mb + rB + (NT / CB) * i;
       const int ih = xoh[i] * p.SH - p.PH + kh, iw = xow[i] * p.SW - p.PW + kw;
       const bool ok = b_tap && m < m_end && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
       const unsigned off = (unsigned)(((((long)xn[i] * p.H + ih) * p.W + iw) * p.xcs + p.xoff + ci) * 2);
@@ -126,7 +136,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
     bf16* sB = sA + A_EL;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int row = rA + (256 / CA) * i;
+      const int row = rA + (NT / CA) * i;
       const int u = (2 * cA) ^ swz<UA>(row);
       *(u32x4*)(sA + row * BCO + 4 * u) = r.a[i];
       if (do_bias) {
@@ -137,7 +147,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int row = rB + (256 / CB) * i;
+      const int row = rB + (NT / CB) * i;
       const int u = (2 * cB) ^ swz<UB>(row);
       *(u32x4*)(sB + row * BKK + 4 * u) = r.b[i];
     }
@@ -165,13 +175,13 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
-        const int cb = wr * (BCO / 2) + 16 * tm;
+        const int cb = wr * (BCO / WM) + 16 * tm;
         const s16x4 lo = tr(sA, UA, BCO, r0, cb), hi = tr(sA, UA, BCO, r0 + 4, cb);
         af[tm] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {
-        const int cb = wc * (BKK / 2) + 16 * tn;
+        const int cb = wc * (BKK / WN) + 16 * tn;
         const s16x4 lo = tr(sB, UB, BKK, r0, cb), hi = tr(sB, UB, BKK, r0 + 4, cb);
         bfr[tn] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
@@ -200,15 +210,15 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
   }
 
   // partial tile -> part[z][co][k]
-  float* out = p.part + (long)blockIdx.z * p.cout_pad * p.kpad;
+  float* out = p.part + (long)bz * p.cout_pad * p.kpad;
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int co = co0 + wr * (BCO / 2) + 16 * tm + 4 * g + j;
-        const int k = k0 + wc * (BKK / 2) + 16 * tn + (lane & 15);
+        const int co = co0 + wr * (BCO / WM) + 16 * tm + 4 * g + j;
+        const int k = k0 + wc * (BKK / WN) + 16 * tn + (lane & 15);
         out[(long)co * p.kpad + k] = acc[tm][tn][j];
       }
   if (do_bias) {
@@ -221,8 +231,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
     if (tid < BCO) {
       const int c8 = tid >> 3, j = tid & 7;
       float s = 0.f;
-      for (int t = c8; t < 256; t += CA) s += red[t * 8 + j];
-      p.bpart[(long)blockIdx.z * p.cout_pad + co0 + tid] = s;
+      for (int t = c8; t < NT; t += CA) s += red[t * 8 + j];
+      p.bpart[(long)bz * p.cout_pad + co0 + tid] = s;
     }
   }
 }
@@ -270,21 +280,41 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   }
 }
 
-template <int BCO, int BKK>
+template <int BCO, int BKK, int WM = 2, int WN = 2>
 int launch(const WgParams& p, int S, hipStream_t st) {
-  dim3 grid((p.K + BKK - 1) / BKK, (p.cout + BCO - 1) / BCO, S);
-  hipLaunchKernelGGL((wgrad_kernel<BCO, BKK>), grid, dim3(256), 0, st, p);
+  constexpr int lds = 2 * WPX * (BCO + BKK) * 2;
+  static const bool attr = hipFuncSetAttribute((const void*)wgrad_kernel<BCO, BKK, WM, WN>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+  if (!attr) return (int)hipErrorInvalidValue;
+  WgParams q = p;
+  q.gx = (p.K + BKK - 1) / BKK;
+  q.gy = (p.cout + BCO - 1) / BCO;
+  q.S = S;
+  q.per = (q.gx * q.gy * S + 7) / 8;
+  hipLaunchKernelGGL((wgrad_kernel<BCO, BKK, WM, WN>), dim3(8 * q.per), dim3(64 * WM * WN), lds, st, q);
   return (int)hipGetLastError();
+}
+
+// Tile of one wgrad problem.  256 x 256 for the refinement loop's wide convs (cout >= 192, K >= 1024):
+// 128 FLOP per staged byte (vs 64 for 128 x 128), which the per-CU operand stream from L2 / MALL bounds,
+// at one resident workgroup per CU (128 KB of LDS, the accumulators in AGPRs).
+inline void wgrad_tile(int K, int cout, int* bco, int* bkk, int* slots) {
+  if (cout >= 192 && K >= 1024) {
+    *bco = 256; *bkk = 256; *slots = 256;
+  } else {
+    *bco = cout > 64 ? 128 : 64; *bkk = K > 64 ? 128 : 64; *slots = 512;
+  }
 }
 
 }  // namespace
 
 extern "C" int jr_wgrad_plan(int M, int K, int cout, int* S, int* cout_pad, int* kpad) {
-  const int bco = cout > 64 ? 128 : 64, bkk = K > 64 ? 128 : 64;
+  int bco, bkk, slots;
+  wgrad_tile(K, cout, &bco, &bkk, &slots);
   const int tiles = ((K + bkk - 1) / bkk) * ((cout + bco - 1) / bco);
-  // one round of 2 resident workgroups per CU (64 KB of LDS each): S = floor(512 / tiles)
+  // one round of resident workgroups (2 per CU at 64 KB of LDS, 1 at 128 KB): S = floor(slots / tiles)
   // (rounding up left a few workgroups for a second round), >= 4 stages of pixels per split
-  int s = std::max(1, std::min(512 / tiles, (M + 4 * WPX - 1) / (4 * WPX)));
+  int s = std::max(1, std::min(slots / tiles, (M + 4 * WPX - 1) / (4 * WPX)));
   *S = s;
   *cout_pad = (cout + bco - 1) / bco * bco;
   *kpad = (K + bkk - 1) / bkk * bkk;
@@ -311,9 +341,12 @@ extern "C" int jr_wgrad(const void* x, int xcs, int xoff, int N, int H, int W, i
   S = (p.M + p.px_split - 1) / p.px_split;
   p.part = part; p.cout_pad = cp; p.kpad = kp; p.bpart = db ? bpart : nullptr;
   p.x_bytes = x_bytes; p.y_bytes = y_bytes;
+  int bco, bkk, slots;
+  wgrad_tile(p.K, cout, &bco, &bkk, &slots);
   const bool bc = cout > 64, bk = p.K > 64;
   int r;
-  if (bc && bk) r = launch<128, 128>(p, S, stream);
+  if (bco == 256) r = launch<256, 256, 2, 4>(p, S, stream);
+  else if (bc && bk) r = launch<128, 128>(p, S, stream);
   else if (bc) r = launch<128, 64>(p, S, stream);
   else if (bk) r = launch<64, 128>(p, S, stream);
   else r = launch<64, 64>(p, S, stream);

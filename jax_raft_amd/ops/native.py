@@ -248,7 +248,9 @@ HALO_CFG0 = 100
 HALO_CFGS = ((64, 2, 2, 4, 16, 16), (64, 2, 2, 2, 8, 16), (96, 3, 2, 2, 8, 16), (96, 3, 1, 2, 4, 16),
              (128, 4, 2, 2, 8, 16), (128, 4, 1, 2, 4, 16), (128, 2, 2, 2, 8, 16), (128, 2, 1, 1, 4, 8),
              (256, 2, 2, 2, 8, 16), (256, 2, 1, 1, 4, 8), (128, 4, 1, 1, 4, 8), (256, 4, 1, 1, 4, 8),
-             (256, 2, 1, 2, 4, 16))
+             (256, 2, 1, 2, 4, 16), (256, 6, 1, 4, 8, 16), (256, 4, 1, 4, 8, 16), (128, 8, 1, 4, 8, 16),
+             (128, 2, 1, 4, 8, 16), (256, 6, 1, 2, 4, 16), (256, 4, 1, 2, 4, 16), (256, 1, 2, 2, 8, 16),
+             (256, 1, 4, 1, 8, 16), (128, 1, 2, 2, 8, 16), (128, 1, 4, 1, 8, 16))
 
 
 def pack_halo_conv(kernel: torch.Tensor, cin8: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -226,6 +226,9 @@ class RaftEngine:
         # producer's epilogue, normalise + relu in the consumer's footprint load);
         # JR_HALO_NORM=0: the separate statistics / norm_act passes
         self.halo_norm = os.environ.get("JR_HALO_NORM", "1") != "0"
+        # JR_HALO_RES=0: a residual block's output is materialised by one norm_act pass instead of
+        # being built (residual + its norm) inside the next block's first halo conv
+        self.halo_res = self.halo_norm and os.environ.get("JR_HALO_RES", "1") != "0"
         self.mask_head = "split"      # per plan: "split" (mask lane) | "fused" (one lane, 128 -> 512 conv)
         self.gate_dtype = gate_dtype
         self.split = split
@@ -660,7 +663,7 @@ class RaftEngine:
                     y, ys = x, None   # ys: stats of a raw conv output y still to be normalised
                     j0 = 0
                     c1 = f"{pre}.{names[0]}"
-                    if (pend is not None and not has_ds and halo_fusable(c1) and sp[c1].out_hw(h_, w_) == (h_, w_)
+                    if (pend is not None and self.halo_res and not has_ds and halo_fusable(c1) and sp[c1].out_hw(h_, w_) == (h_, w_)
                             and pend["raw"].shape[-1] == sp[c1].cin8):
                         xb = alloc(f"{pre}.x", tuple(pend["raw"].shape))
                         fused = conv_stats(c1, pend["raw"], N, h_, w_, in_stats=pend["s"], in_res=pend["res"],

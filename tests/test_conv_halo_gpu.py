@@ -9,6 +9,7 @@ import pytest
 import torch
 
 from jax_raft_amd.models import reference as R
+from jax_raft_amd.ops.native import HALO_CFGS as _HALO
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -29,7 +30,7 @@ def _rel(a, b):
     return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
 
 
-@pytest.mark.parametrize("idx", range(13))
+@pytest.mark.parametrize("idx", range(len(_HALO)))
 def test_conv_halo_matches_reference(idx):
     nat = _nat()
     cfg = nat.HALO_CFG0 + idx

@@ -319,6 +319,10 @@ WG_CASES = [
     (2, 11, 9, 256, 0, 256, 256, 126, 128, 0, 3, 3, 1, (1, 1)),
     (2, 11, 9, 512, 256, 256, 256, 64, 256, 192, 3, 3, 1, (1, 1)),
     (3, 16, 20, 96, 0, 96, 96, 80, 88, 0, 3, 3, 1, (1, 1)),
+    # 256 x 256 tiles (cout >= 192, K >= 1024): a partial cout tile, gradient slices at an offset
+    (2, 7, 9, 256, 0, 256, 256, 192, 200, 8, 3, 3, 1, (1, 1)),
+    (2, 10, 13, 128, 0, 128, 128, 320, 320, 0, 3, 3, 1, (1, 1)),
+    (3, 5, 66, 264, 8, 256, 256, 256, 256, 0, 5, 1, 1, (2, 0)),
 ]
 
 
