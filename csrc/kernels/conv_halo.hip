@@ -142,8 +142,11 @@ __global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHal
 #pragma unroll
             for (int h2 = 0; h2 < 2; ++h2) {
               float fv = bf2f(e[2 * q + h2]) * t[2 * h2] + t[2 * h2 + 1];
+              // in_relu bit 1: the relu of the block's last ConvNormActivation, before the residual
+              // add (model.py:171-180: relu(x + relu(IN(conv2)))); bit 0: the relu after it
+              if (p.in_relu & 2) fv = fmaxf(fv, 0.f);
               if (resid) fv += bf2f(er[2 * q + h2]) * tr[2 * h2] + tr[2 * h2 + 1];
-              if (p.in_relu) fv = fmaxf(fv, 0.f);
+              if (p.in_relu & 1) fv = fmaxf(fv, 0.f);
               e[2 * q + h2] = f2bf(fv);
             }
           }

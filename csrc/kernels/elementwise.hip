@@ -109,22 +109,35 @@ __global__ __launch_bounds__(256) void channel_stats_partial_kernel(const bf16* 
 // flight), then the 4 lanes combine through LDS in a fixed order.
 __global__ __launch_bounds__(256) void channel_stats_final_kernel(const float* __restrict__ part, int N, int nb, int C,
                                                                    float* __restrict__ stats) {
-  __shared__ float red[4][64];
+  // block = 8 values (lane v) x 32 partial groups (g): thread (v, g) sums partials g, g + 32, ... with
+  // 8 loads in flight per round trip (the loop is latency-bound: a few MB of partials), then the 32
+  // groups combine in a fixed order (deterministic)
+  __shared__ float red_[32][9];
   const int n = blockIdx.y;
-  const int vi = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int lb = threadIdx.x >> 6;
+  const int v = threadIdx.x & 7, g = threadIdx.x >> 3;
+  const int vi = blockIdx.x * 8 + v;
   const int nv = 2 * C;
-  float acc = 0.f;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
   if (vi < nv) {
     const float* p = part + (long)n * nb * nv + vi;
-#pragma unroll 8
-    for (int b = lb; b < nb; b += 4) acc += p[(long)b * nv];
+    for (int b = g; b < nb; b += 32 * 8) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int bb = b + 32 * u;
+        t[u] = bb < nb ? p[(long)bb * nv] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u & 3] += t[u];
+    }
   }
-  red[lb][threadIdx.x & 63] = acc;
+  red_[g][v] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   __syncthreads();
-  if (lb == 0 && vi < nv) {
-    const int t = threadIdx.x;
-    stats[(long)n * nv + vi] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+  if (g == 0 && vi < nv) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) t += red_[k][v];
+    stats[(long)n * nv + vi] = t;
   }
 }
 
@@ -319,7 +332,7 @@ extern "C" int jr_channel_stats(const void* x, int N, int HW, int C, float* stat
   if (C % 8 != 0 || (C / 8) > 256) return (int)hipErrorInvalidValue;
   const int nb = (HW + STATS_ROWS - 1) / STATS_ROWS;
   hipLaunchKernelGGL(channel_stats_partial_kernel, dim3(nb, N), dim3(256), 0, stream, (const bf16*)x, HW, C, partial);
-  hipLaunchKernelGGL(channel_stats_final_kernel, dim3((2 * C + 63) / 64, N), dim3(256), 0, stream, partial, N, nb, C,
+  hipLaunchKernelGGL(channel_stats_final_kernel, dim3((2 * C + 7) / 8, N), dim3(256), 0, stream, partial, N, nb, C,
                      stats);
   return (int)hipGetLastError();
 }
@@ -327,7 +340,7 @@ extern "C" int jr_channel_stats(const void* x, int N, int HW, int C, float* stat
 extern "C" int jr_channel_stats_partials(int N, int HW) { return N * ((HW + STATS_ROWS - 1) / STATS_ROWS); }
 
 extern "C" int jr_channel_stats_final(const float* part, int N, int nb, int C, float* stats, hipStream_t stream) {
-  hipLaunchKernelGGL(channel_stats_final_kernel, dim3((2 * C + 63) / 64, N), dim3(256), 0, stream, part, N, nb, C, stats);
+  hipLaunchKernelGGL(channel_stats_final_kernel, dim3((2 * C + 7) / 8, N), dim3(256), 0, stream, part, N, nb, C, stats);
   return (int)hipGetLastError();
 }
 

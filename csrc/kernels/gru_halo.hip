@@ -58,8 +58,9 @@ struct Halo {
   static constexpr int SX = (CIN - HD) / 16;    //                          x part
   // weight ring depths (k-steps = 1 KB loads in flight per wave): the stream from L2 is this
   // kernel's bound at batch 1 (Little's law: bytes in flight / L2 latency under load)
-  static constexpr int PD1 = NB1 + NB2 <= 3 ? 24 : 16;
-  static constexpr int PD2 = NB2 >= 2 ? (HD == 96 ? 8 : 12) : 16;
+  // (4-block outputs at 2 waves / SIMD: shallower rings keep the 256-VGPR budget without spills)
+  static constexpr int PD1 = NB1 + NB2 <= 3 ? 24 : NB1 >= 5 ? 6 : NB2 >= 4 ? 8 : 16;
+  static constexpr int PD2 = NB2 >= 4 ? 6 : NB2 >= 2 ? (HD == 96 ? 8 : 12) : 16;
   static_assert(CIN % 16 == 0 && HD % 32 == 0 && CC <= 32 && HC <= 16 && SRH == SX, "geometry");
 };
 
@@ -311,12 +312,13 @@ __global__ __launch_bounds__(4 * HD) void gru_halo_kernel(const GruHaloParams p)
   // epilogue 2 operands of the z waves, loaded ahead of GEMM 2: the q bias map, and (NB2 <= 2)
   // the fp32 state of the output pixels
   constexpr bool PRE_H = NB2 <= 2;
-  u32x4 bq[NB2][2];
+  constexpr bool PRE_Q = NB2 <= 3;   // 4-block tiles: the q bias map is read in the epilogue (VGPRs)
+  u32x4 bq[PRE_Q ? NB2 : 1][2];
   f32x4 hpre[PRE_H ? NB2 : 1][4];
   if (zwave) {
 #pragma unroll
     for (int b = 0; b < NB2; ++b) {
-      map_pre(om[b], 2 * HD + c0, bq[b]);
+      if constexpr (PRE_Q) map_pre(om[b], 2 * HD + c0, bq[b]);
       if constexpr (PRE_H) {
         const f32x4* hq = (const f32x4*)(p.h32 + (long)(om[b] >= 0 ? om[b] : 0) * HD + c0);
 #pragma unroll
@@ -364,7 +366,13 @@ __global__ __launch_bounds__(4 * HD) void gru_halo_kernel(const GruHaloParams p)
     const int m = om[b];
     if (m < 0) continue;
     float bv[16], h[16], v[16];
-    map_f(bq[b], bv);
+    if constexpr (PRE_Q) {
+      map_f(bq[b], bv);
+    } else {
+      u32x4 bqe[2];
+      map_pre(m, 2 * HD + c0, bqe);
+      map_f(bqe, bv);
+    }
     float* hp = p.h32 + (long)m * HD + c0;
     if constexpr (PRE_H) {
 #pragma unroll
@@ -416,9 +424,9 @@ int launch(const GruHaloParams& p, hipStream_t s) {
 }
 
 // the instantiated (hd, mode, nb1, nb2) set: raft_large's 5-tap runs and raft_small's 3x3 blocks
-// (4-block outputs need > 256 VGPRs with the ring / z / GEMM 2 accumulators live: not built)
+// (4-block outputs: whole 128-pixel rows of the 1x5 stage at batch >= 4, one workgroup per CU)
 #define JR_HALO_CASES(X)                                                                     \
-  X(128, 0, 1, 1) X(128, 0, 2, 1) X(128, 0, 2, 2) X(128, 0, 3, 2)                            \
+  X(128, 0, 1, 1) X(128, 0, 2, 1) X(128, 0, 2, 2) X(128, 0, 3, 2) X(128, 0, 3, 3) X(128, 0, 5, 4) \
   X(96, 1, 2, 1) X(96, 1, 2, 2) X(96, 1, 3, 2)
 
 }  // namespace

@@ -343,21 +343,35 @@ __global__ __launch_bounds__(256) void norm_bwd_partial_kernel(const bf16* __res
 
 __global__ __launch_bounds__(256) void norm_bwd_final_kernel(const float* __restrict__ part, int nb, int C,
                                                              float* __restrict__ red) {
-  __shared__ float sm[4][64];
+  // block = 8 values (lane v) x 32 partial groups (g): thread (v, g) sums partials g, g + 32, ... with
+  // 8 loads in flight per round trip (the loop is latency-bound: a few MB of partials), then the 32
+  // groups combine in a fixed order (deterministic)
+  __shared__ float red_[32][9];
   const int n = blockIdx.y;
-  const int vi = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int lb = threadIdx.x >> 6;
+  const int v = threadIdx.x & 7, g = threadIdx.x >> 3;
+  const int vi = blockIdx.x * 8 + v;
   const int nv = 2 * C;
-  float acc = 0.f;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
   if (vi < nv) {
     const float* p = part + (long)n * nb * nv + vi;
-    for (int b = lb; b < nb; b += 4) acc += p[(long)b * nv];
+    for (int b = g; b < nb; b += 32 * 8) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int bb = b + 32 * u;
+        t[u] = bb < nb ? p[(long)bb * nv] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u & 3] += t[u];
+    }
   }
-  sm[lb][threadIdx.x & 63] = acc;
+  red_[g][v] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   __syncthreads();
-  if (lb == 0 && vi < nv) {
-    const int t = threadIdx.x;
-    red[(long)n * nv + vi] = ((sm[0][t] + sm[1][t]) + sm[2][t]) + sm[3][t];
+  if (g == 0 && vi < nv) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) t += red_[k][v];
+    red[(long)n * nv + vi] = t;
   }
 }
 
@@ -612,7 +626,7 @@ extern "C" int jr_norm_bwd(const void* gout, const void* om, const void* y, cons
     const int nb = (HW + NB_ROWS - 1) / NB_ROWS;
     hipLaunchKernelGGL(norm_bwd_partial_kernel, dim3(nb, N), dim3(256), 0, stream, (const bf16*)gout,
                        (const bf16*)om, (const bf16*)y, stats, mode, gamma, beta, relu, N, HW, C, eps, partial);
-    hipLaunchKernelGGL(norm_bwd_final_kernel, dim3((2 * C + 63) / 64, N), dim3(256), 0, stream, partial, nb, C, red);
+    hipLaunchKernelGGL(norm_bwd_final_kernel, dim3((2 * C + 7) / 8, N), dim3(256), 0, stream, partial, nb, C, red);
   }
   const int nrg = 256 / (C / 8);
   const long want = ((long)N * HW + 2047) / 2048;

@@ -107,7 +107,7 @@ def pack_gru_halo(kernel: torch.Tensor, cin_pad: int, out: Optional[torch.Tensor
 
 
 # (hd, mode) -> the (nb1, nb2) block counts gru_halo.hip instantiates (JR_HALO_CASES)
-GRU_HALO_BLOCKS = {(128, 0): ((1, 1), (2, 1), (2, 2), (3, 2)), (96, 1): ((2, 1), (2, 2), (3, 2))}
+GRU_HALO_BLOCKS = {(128, 0): ((1, 1), (2, 1), (2, 2), (3, 2), (3, 3), (5, 4)), (96, 1): ((2, 1), (2, 2), (3, 2))}
 
 
 def gru_halo_lds(hd: int, mode: int, TR: int, TC: int, nb1: int, nb2: int) -> int:
@@ -142,7 +142,7 @@ def gru_halo_candidates(hd: int, mode: int, axis: int, N: int, H: int, W: int) -
     out = []
     if mode == 0:
         length = H if axis else W
-        for nb1, nb2 in ((1, 1), (2, 1), (2, 2), (3, 2)):
+        for nb1, nb2 in ((1, 1), (2, 1), (2, 2), (3, 2), (3, 3), (5, 4)):
             lmax = min(32 * nb1 - 4, 32 * nb2)
             segs = -(-length // lmax)
             L = -(-length // segs)
@@ -392,7 +392,8 @@ def conv_args(spec: ConvSpec, x: torch.Tensor, N: int, H: int, W: int, y: torch.
     ``bmap``: optional fp32 per-pixel bias map [M, C], channels from ``bmap_coff``.
     Halo tile configs only (cfg >= HALO_CFG0): ``stats_part`` receives per-tile channel
     (sum, sumsq) partials of the output; ``in_stats`` ([N][cin][2] sums over ``in_hw``
-    pixels) normalises the input (instance norm, + relu if ``in_relu``) as it is loaded;
+    pixels) normalises the input (instance norm; ``in_relu`` bit 0: relu, bit 1: relu before the
+    residual add) as it is loaded;
     ``in_res`` (+ ``in_res_stats``: normalised too) is added before the relu (a residual
     block's output built on the fly) and ``xn`` receives the built input."""
     OH, OW = out_hw if out_hw is not None else spec.out_hw(H, W)

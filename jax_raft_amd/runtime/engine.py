@@ -606,8 +606,9 @@ class RaftEngine:
             y = alloc(name + ".y", (N, H, W, s.cout))
             nb_max = max(-(-H // c[4]) * -(-W // c[5]) * c[2] for c in nat.HALO_CFGS if c[0] == s.cin8)
             part = alloc(name + ".part", (N, nb_max, s.cout, 2), F32)
-            kw = dict(stats_part=part, in_stats=in_stats, in_relu=1, in_hw=H * W, in_res=in_res,
-                      in_res_stats=in_res_stats, xn=xn)
+            # a residual block's output: relu(res + relu(IN(raw))) (model.py:171-180), in_relu bits 0 + 1
+            kw = dict(stats_part=part, in_stats=in_stats, in_relu=3 if in_res is not None else 1, in_hw=H * W,
+                      in_res=in_res, in_res_stats=in_res_stats, xn=xn)
             kw = self._conv_kw(s, x, N, H, W, y, kw)
             if kw.get("cfg") is None or kw["cfg"] < nat.HALO_CFG0:   # an override chose another kernel
                 return None

@@ -68,7 +68,7 @@ def test_conv_halo_matches_reference(idx):
             assert torch.equal(y2[:, :cout], y[:, :cout])
 
 
-@pytest.mark.parametrize("idx", [0, 2, 4, 8])
+@pytest.mark.parametrize("idx", range(len(_HALO)))
 def test_conv_halo_stats_partials(idx):
     """Per-channel (sum, sumsq) of the stored outputs, per tile, reduced by the stats final
     kernel: equals the statistics of the output tensor (what channel_stats computes)."""
@@ -93,7 +93,7 @@ def test_conv_halo_stats_partials(idx):
     assert torch.allclose(stats, want, rtol=1e-4, atol=1e-2), (stats - want).abs().max()
 
 
-@pytest.mark.parametrize("idx", [0, 2, 4])
+@pytest.mark.parametrize("idx", range(len(_HALO)))
 def test_conv_halo_input_instance_norm(idx):
     """The producer's instance norm + relu applied while the footprint is loaded equals
     norm_act (jr_norm_act mode 1, relu) followed by the conv; padding stays zero."""
@@ -120,11 +120,12 @@ def test_conv_halo_input_instance_norm(idx):
     assert _rel(y.float().cpu().reshape(N, H, W, cout), ref) < 1.5e-2
 
 
-@pytest.mark.parametrize("idx,res_norm", [(0, False), (1, True), (2, True), (4, False), (6, True)])
+@pytest.mark.parametrize("idx,res_norm", [(i, rn) for i in range(len(_HALO)) for rn in (False, True)])
 def test_conv_halo_builds_residual_block_output(idx, res_norm):
-    """A residual block's output relu(IN(x) + r) -- r the identity input or an instance-
-    normalised downsample output -- built while the footprint is loaded equals norm_act +
-    the conv, and the tile-own pixels of it are written out (xn) exactly once."""
+    """A residual block's output relu(relu(IN(x)) + r) (model.py:171-180; r the identity input
+    or an instance-normalised downsample output) built while the footprint is loaded
+    (in_relu = 3) equals norm_act + the conv, and the tile-own pixels of it are written out
+    (xn) exactly once."""
     nat = _nat()
     cfg = nat.HALO_CFG0 + idx
     cin = nat.HALO_CFGS[idx][0]
@@ -143,14 +144,14 @@ def test_conv_halo_builds_residual_block_output(idx, res_norm):
         v = (f * f).mean(1, keepdim=True) - m * m
         return ((f - m) * torch.rsqrt(v.clamp_min(0) + 1e-5)).reshape(N, H, W, cin)
 
-    built = torch.relu(inorm(x) + (inorm(r) if res_norm else r.float()))
+    built = torch.relu(torch.relu(inorm(x)) + (inorm(r) if res_norm else r.float()))
     k = torch.randn(3, 3, cin, cout) / math.sqrt(9 * cin)
     b = torch.randn(cout) * 0.1
     spec = nat.make_spec(k, b, (1, 1), (1, 1), device=DEV)
     ref = R.conv2d_nhwc(_bf(built.cpu()), _bf(k), b, (1, 1), (1, 1))
     y = torch.empty(N * H * W, cout, dtype=torch.bfloat16, device=DEV)
     xn = torch.full((N, H, W, cin), float("nan"), dtype=torch.bfloat16, device=DEV)
-    t, i, a = nat.conv_args(spec, x, N, H, W, y, cfg=cfg, in_stats=st(x), in_relu=1, in_hw=H * W, in_res=r,
+    t, i, a = nat.conv_args(spec, x, N, H, W, y, cfg=cfg, in_stats=st(x), in_relu=3, in_hw=H * W, in_res=r,
                             in_res_stats=st(r) if res_norm else None, xn=xn)
     nat.ops().conv(t, i, a)
     torch.cuda.synchronize()
