@@ -43,7 +43,7 @@ constexpr int pitch_of() { return CIN <= 64 ? 8 : CIN <= 128 ? 16 : 32; }
 // INN: the input is normalised (+ residual) while loading (p.in_stats set); a separate
 // instantiation so the plain convs keep their register budget
 template <int CIN, int WCO, int WPX, int TN, int TR, int TC, bool INN>
-__global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHaloParams p) {
+__global__ __launch_bounds__(64 * WCO * WPX, (INN && CIN <= 64 && TN <= 2) ? 3 : 1) void conv_halo_kernel(const ConvHaloParams p) {
   constexpr int NT = 64 * WCO * WPX;
   constexpr int P = pitch_of<CIN>();
   constexpr int CC = CIN / 8;
@@ -52,7 +52,7 @@ __global__ __launch_bounds__(64 * WCO * WPX) void conv_halo_kernel(const ConvHal
   // weight ring depth: 16 fragments, 8 for the 4-block waves at 2 waves / SIMD (256 VGPRs; each
   // fragment there feeds 4 MFMAs, so 8 in flight still cover ~1000 cycles of L2 latency)
   constexpr bool WIDE = TN >= 4 && WCO * WPX > 4;
-  constexpr int PD = S >= 16 ? (WIDE ? 8 : 16) : S;
+  constexpr int PD = S >= 16 ? ((WIDE || (INN && CIN <= 64)) ? 8 : 16) : S;   // (INN, 64 ch: 3 waves / SIMD)
   constexpr int FW = TC + 2;
   constexpr int NFP = (TR + 2) * FW;
   constexpr int RB = P * 16;              // footprint row bytes

@@ -218,6 +218,9 @@ int jr_pack_pieces(const void* table, int n, long max_elems, hipStream_t stream)
 // dY (bf16 [N][OH][OW][ycs], channels yoff.. yoff+cout).  part / bpart: split-K workspaces of
 // S * cout_pad * kpad and S * cout_pad floats from jr_wgrad_plan (S <= 0: the planned S).
 int jr_wgrad_plan(int M, int K, int cout, int* S, int* cout_pad, int* kpad);
+// the workspace plan of one conv's weight gradient (the 3x3 / stride-1 halo path or the im2col tiles)
+int jr_wgrad_plan_geom(int N, int H, int W, int cin8, int KH, int KW, int SH, int SW, int PH, int PW, int OH, int OW,
+                       int cout, int* S, int* cout_pad, int* kpad);
 int jr_wgrad(const void* x, int xcs, int xoff, int N, int H, int W, int cin8, int KH, int KW, int SH, int SW, int PH,
              int PW, const void* dy, int ycs, int yoff, int OH, int OW, int cout, int cin, float* part, float* bpart,
              int S, float* dw, float* db, long x_bytes, long y_bytes, hipStream_t stream);

@@ -306,6 +306,208 @@ inline void wgrad_tile(int K, int cout, int* bco, int* bkk, int* slots) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Halo weight gradient of a 3x3 / stride-1 / pad-1 conv (every 3x3 conv of the encoders' residual
+// blocks, the motion encoder, flow head and mask head; model.py:120-159, 275-289, 347-349, 389-390).
+//
+// The im2col kernel above re-gathers the input for every K tile: 9 shifted copies of each pixel
+// row per 3x3 tap.  Here a workgroup owns a (64 output x 64 input channel) block of dW (all 9 taps:
+// a 64 x 576 output tile) and walks a contiguous range of 8 x 16 pixel tiles: per tile it stages the
+// tile's dY rows [128 px][64 co] and the input footprint [10 x 18 px][64 ci] in LDS once, and reads
+// the B fragment of tap (u, v) from the footprint shifted by a constant -- 39 KB staged per 9.4
+// MFLOP (241 FLOP per byte, vs 64 for the 128 x 128 im2col tile).
+//
+// MFMA v_mfma_f32_16x16x32_bf16, K = pixels: both operands are transposed LDS reads
+// (ds_read_b64_tr_b16) of images whose rows are pixels, as in wgrad_kernel; each lane addresses its
+// own pixel row, so the footprint rows of a tap are just (pixel row + tap offset).  Wave w computes
+// the 64 co x (9 taps x 16 ci at 16 w) block: 4 x 9 accumulators (one wave per SIMD, ~480 registers).  Partials go to the same
+// [split][cout_pad][kpad] layout as wgrad_kernel (k = tap * cin8 + ci), reduced by wgrad_reduce_kernel.
+// ---------------------------------------------------------------------------------------------
+constexpr int HTR = 8, HTC = 16, HFW = HTC + 2, HNF = (HTR + 2) * HFW;   // tile, footprint
+constexpr int HPX = HTR * HTC;                                          // 128 pixels per tile
+constexpr int HA_EL = HPX * 64, HB_EL = (HNF + 4) * 64;                 // LDS image elements
+constexpr int HNT = 256;                                                // 4 waves, one per SIMD
+constexpr int HNA = HPX * 8 / HNT, HNB = (HNF * 8 + HNT - 1) / HNT;     // 16-B chunks per thread
+
+struct WgHaloParams {
+  const void* x; int xcs, xoff, N, H, W, cin8;
+  const void* dy; int ycs, yoff, cout;
+  int tiles_x, tiles_y, ntiles, nco, nci, S, per, tps;   // tps: tiles per split
+  float* part; int cout_pad, kpad;
+  float* bpart;
+  long x_bytes, y_bytes;
+};
+
+JR_DEVICE int hswz(int r) { return 4 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)); }   // 64-col image
+
+__global__ __launch_bounds__(256, 1) void wgrad_halo_kernel(const WgHaloParams p) {
+  extern __shared__ __attribute__((aligned(16))) bf16 smem[];   // 2 x (A image + B image)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lid = (int)(blockIdx.x & 7) * p.per + (int)(blockIdx.x >> 3);   // XCD-aware (wgrad_kernel)
+  const int ncb = p.nco * p.nci;
+  if (lid >= ncb * p.S) return;
+  const int z = lid / ncb, cb = lid - z * ncb;
+  const int cob = cb / p.nci, cib = cb - cob * p.nci;
+  const int co0 = cob * 64, ci0 = cib * 64;
+  const int t_begin = z * p.tps, t_end = min(p.ntiles, t_begin + p.tps);
+  const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, (short)0, (int)p.y_bytes, 0x00020000);
+  constexpr unsigned OOB = 0x80000000u;
+  const bool do_bias = p.bpart != nullptr && cib == 0;
+
+  struct Regs { u32x4 a[HNA]; u32x4 b[HNB]; };
+  Regs ra;
+  float bsum[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
+  const int ch = tid & 7;          // 16-B chunk (8 channels) of every row this thread stages
+  const bool a_ok = co0 + 8 * ch < p.cout;
+  const bool b_ok = ci0 + 8 * ch < p.cin8;
+
+  auto issue = [&](Regs& r, int t) {
+    const int per_img = p.tiles_x * p.tiles_y;
+    const int n = t / per_img, rem = t - n * per_img;
+    const int ty = rem / p.tiles_x, tx = rem - ty * p.tiles_x;
+    const int y0 = ty * HTR, x0 = tx * HTC;
+#pragma unroll
+    for (int i = 0; i < HNA; ++i) {
+      const int row = (tid >> 3) + (HNT / 8) * i;   // pixel of the tile
+      const int yy = y0 + (row >> 4), xx = x0 + (row & 15);
+      const bool ok = a_ok && yy < p.H && xx < p.W;
+      const unsigned off = (unsigned)(((long)((n * p.H + yy) * p.W + xx) * p.ycs + p.yoff + co0 + 8 * ch) * 2);
+      r.a[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ys, ok ? off : OOB, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < HNB; ++i) {
+      const int f = (tid >> 3) + (HNT / 8) * i;     // footprint pixel
+      const int fy = f / HFW, fx = f - fy * HFW;
+      const int yy = y0 - 1 + fy, xx = x0 - 1 + fx;
+      const bool ok = b_ok && f < HNF && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+      const unsigned off = (unsigned)(((long)((n * p.H + yy) * p.W + xx) * p.xcs + p.xoff + ci0 + 8 * ch) * 2);
+      r.b[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xs, ok ? off : OOB, 0, 0));
+    }
+  };
+  auto store = [&](const Regs& r, int buf) {
+    bf16* sA = smem + buf * (HA_EL + HB_EL);
+    bf16* sB = sA + HA_EL;
+#pragma unroll
+    for (int i = 0; i < HNA; ++i) {
+      const int row = (tid >> 3) + (HNT / 8) * i;
+      *(u32x4*)(sA + row * 64 + 4 * ((2 * ch) ^ hswz(row))) = r.a[i];
+      if (do_bias) {
+        const bf16x8 v = __builtin_bit_cast(bf16x8, r.a[i]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bsum[j] += bf2f(v[j]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < HNB; ++i) {
+      const int f = (tid >> 3) + (HNT / 8) * i;
+      if (f < HNF) *(u32x4*)(sB + f * 64 + 4 * ((2 * ch) ^ hswz(f))) = r.b[i];
+    }
+  };
+
+  // wave w: all 64 output channels x input channels ci0 + 16 w + [0, 16), all taps (measured: 8 waves of
+  // 32 x 144 -- two per SIMD, B fragments read twice -- were 20-30 % slower)
+  const int wco = 0, wci = wave;
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 9; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  // transposed read of the 4 x 16 block at image row r (this lane's row), columns cb + 4 pp
+  auto tr = [&](const bf16* img, int r, int cbase) -> s16x4 {
+    const int u = cbase / 4 + pp;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + r * 64 + 4 * (u ^ hswz(r))));
+  };
+  auto fpr = [](int px) { return (px >> 4) * HFW + (px & 15); };   // footprint row of pixel (tap (0, 0))
+  auto compute = [&](int buf) {
+    const bf16* sA = smem + buf * (HA_EL + HB_EL);
+    const bf16* sB = sA + HA_EL;
+#pragma unroll
+    for (int ks = 0; ks < HPX / 32; ++ks) {
+      const int p0 = 32 * ks + 8 * g + q;           // this lane's pixels: p0 (low half), p0 + 4 (high)
+      bf16x8 af[4];
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm) {
+        const s16x4 lo = tr(sA, p0, 32 * wco + 16 * tm), hi = tr(sA, p0 + 4, 32 * wco + 16 * tm);
+        af[tm] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+      const int f0 = fpr(p0), f1 = fpr(p0 + 4);
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int to = (tap / 3) * HFW + tap % 3;
+        const s16x4 lo = tr(sB, f0 + to, 16 * wci), hi = tr(sB, f1 + to, 16 * wci);
+        const bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+        for (int tm = 0; tm < 4; ++tm) acc[tm][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tm], bfr, acc[tm][tap], 0, 0, 0);
+      }
+    }
+  };
+
+  if (t_begin < t_end) {
+    issue(ra, t_begin);
+    store(ra, 0);
+    __syncthreads();
+    for (int t = t_begin; t < t_end; ++t) {
+      const int buf = (t - t_begin) & 1;
+      if (t + 1 < t_end) issue(ra, t + 1);
+      compute(buf);
+      if (t + 1 < t_end) store(ra, buf ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // partial tile -> part[z][co][tap * cin8 + ci]
+  float* out = p.part + (long)z * p.cout_pad * p.kpad;
+#pragma unroll
+  for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ci = ci0 + 16 * wci + (lane & 15);
+      if (ci >= p.cin8) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int co = co0 + 32 * wco + 16 * tm + 4 * g + j;
+        out[(long)co * p.kpad + tap * p.cin8 + ci] = acc[tm][tap][j];
+      }
+    }
+  if (do_bias) {
+    // threads with the same chunk ch hold partial sums of the same 8 channels
+    __syncthreads();
+    float* red = (float*)smem;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = bsum[j];
+    __syncthreads();
+    if (tid < 64) {
+      const int c8 = tid >> 3, j = tid & 7;
+      float s = 0.f;
+      for (int t = c8; t < HNT; t += 8) s += red[t * 8 + j];
+      p.bpart[(long)z * p.cout_pad + co0 + tid] = s;
+    }
+  }
+}
+
+// the halo path serves 3x3 / stride-1 / pad-1 convs; S: splits of the pixel tiles so that the
+// (split x channel block) grid is about one round of resident workgroups (one per CU: ~480 registers)
+inline bool wgrad_halo_ok(int KH, int KW, int SH, int SW, int PH, int PW) {
+  static const bool off = std::getenv("JR_WGRAD_HALO") != nullptr && std::getenv("JR_WGRAD_HALO")[0] == '0';
+  return !off && KH == 3 && KW == 3 && SH == 1 && SW == 1 && PH == 1 && PW == 1;
+}
+inline void wgrad_halo_geom(int N, int H, int W, int cin8, int cout, int* ntiles, int* nco, int* nci, int* S, int* tps) {
+  const int tx = (W + HTC - 1) / HTC, ty = (H + HTR - 1) / HTR;
+  *ntiles = N * tx * ty;
+  *nco = (cout + 63) / 64;
+  *nci = (cin8 + 63) / 64;
+  const int cbs = *nco * *nci;
+  int s = std::max(1, std::min(256 / cbs, (*ntiles + 3) / 4));   // one workgroup per CU, >= 4 tiles per split
+  *tps = (*ntiles + s - 1) / s;
+  *S = (*ntiles + *tps - 1) / *tps;
+}
+
 }  // namespace
 
 extern "C" int jr_wgrad_plan(int M, int K, int cout, int* S, int* cout_pad, int* kpad) {
@@ -321,6 +523,18 @@ extern "C" int jr_wgrad_plan(int M, int K, int cout, int* S, int* cout_pad, int*
   return 0;
 }
 
+extern "C" int jr_wgrad_plan_geom(int N, int H, int W, int cin8, int KH, int KW, int SH, int SW, int PH, int PW,
+                                  int OH, int OW, int cout, int* S, int* cout_pad, int* kpad) {
+  jr_wgrad_plan(N * OH * OW, KH * KW * cin8, cout, S, cout_pad, kpad);
+  if (wgrad_halo_ok(KH, KW, SH, SW, PH, PW)) {
+    int nt, nco, nci, s, tps;
+    wgrad_halo_geom(N, H, W, cin8, cout, &nt, &nco, &nci, &s, &tps);
+    *S = s;
+    *cout_pad = std::max(*cout_pad, nco * 64);
+  }
+  return 0;
+}
+
 extern "C" int jr_wgrad(const void* x, int xcs, int xoff, int N, int H, int W, int cin8, int KH, int KW, int SH,
                         int SW, int PH, int PW, const void* dy, int ycs, int yoff, int OH, int OW, int cout, int cin,
                         float* part, float* bpart, int S, float* dw, float* db, long x_bytes, long y_bytes,
@@ -333,8 +547,30 @@ extern "C" int jr_wgrad(const void* x, int xcs, int xoff, int N, int H, int W, i
   p.K = KH * KW * cin8;
   p.M = N * OH * OW;
   int s_, cp, kp;
-  jr_wgrad_plan(p.M, p.K, cout, &s_, &cp, &kp);
+  jr_wgrad_plan_geom(N, H, W, cin8, KH, KW, SH, SW, PH, PW, OH, OW, cout, &s_, &cp, &kp);
   if (S <= 0) S = s_;
+  if (wgrad_halo_ok(KH, KW, SH, SW, PH, PW)) {
+    WgHaloParams h{};
+    h.x = x; h.xcs = xcs; h.xoff = xoff; h.N = N; h.H = H; h.W = W; h.cin8 = cin8;
+    h.dy = dy; h.ycs = ycs; h.yoff = yoff; h.cout = cout;
+    h.tiles_x = (W + HTC - 1) / HTC; h.tiles_y = (H + HTR - 1) / HTR;
+    int s;
+    wgrad_halo_geom(N, H, W, cin8, cout, &h.ntiles, &h.nco, &h.nci, &s, &h.tps);
+    if (S < s) return (int)hipErrorInvalidValue;   // workspace planned for another geometry
+    h.S = s;
+    h.per = (h.nco * h.nci * s + 7) / 8;
+    h.part = part; h.cout_pad = cp; h.kpad = kp; h.bpart = db ? bpart : nullptr;
+    h.x_bytes = x_bytes; h.y_bytes = y_bytes;
+    constexpr int lds = 2 * (HA_EL + HB_EL) * 2;
+    static const bool attr = hipFuncSetAttribute((const void*)wgrad_halo_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 lds) == hipSuccess;
+    if (!attr) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(wgrad_halo_kernel, dim3(8 * h.per), dim3(HNT), lds, stream, h);
+    if (const int e = (int)hipGetLastError()) return e;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((p.K + 31) / 32), (unsigned)cout), dim3(256), 0, stream, part,
+                       h.bpart, s, cp, kp, KH, KW, cin8, cin, cout, dw, db);
+    return (int)hipGetLastError();
+  }
   if (const char* e = std::getenv("JR_WGRAD_S")) S = std::max(1, std::min(S, atoi(e)));  // tuning probe (<= planned S)
   const int per = (p.M + S - 1) / S;
   p.px_split = (per + WPX - 1) / WPX * WPX;

@@ -513,7 +513,7 @@ static Launch make_wgrad(const TList& t, const IList& i, std::vector<at::Tensor>
   if (db.defined()) { check_f32(db, "db"); TORCH_CHECK(db.numel() == cout, "wgrad: db"); }
   int S, cp, kp;
   const int64_t M = (int64_t)N * OH * OW;
-  jr_wgrad_plan((int)M, KH * KW * cin8, cout, &S, &cp, &kp);
+  jr_wgrad_plan_geom(N, H, W, cin8, KH, KW, SH, SW, PH, PW, OH, OW, cout, &S, &cp, &kp);
   if (!part.defined()) part = at::empty({(int64_t)S * cp * kp}, dw.options());
   if (!bpart.defined()) bpart = at::empty({(int64_t)S * cp}, dw.options());
   check_f32(part, "part"); check_f32(bpart, "bpart");

@@ -13,7 +13,7 @@ produced on the target hardware by ``tools/autotune_db.py``:
   the process; ``save()`` writes the merged table back.
 
 ``JR_TUNE=fresh`` ignores the file (re-times every problem, e.g. to refresh
-it); ``JR_TUNE=db`` (default) uses it.
+it); ``JR_TUNE=db`` (default) uses it; ``JR_TUNE_DB=<file>`` reads another table.
 
 The file records the ``kernel_set`` it was tuned against: when the compiled tile
 configs are renumbered or removed, :data:`KERNEL_SET` is bumped and an old file is
@@ -45,7 +45,11 @@ def gpu_arch(device=None) -> str:
 
 
 def path(arch: str) -> Path:
-    return DB_DIR / f"{arch}.json"
+    """The table file: the packaged ``tuned/<arch>.json``, or ``JR_TUNE_DB`` (a table another
+    process saved: e.g. tools/race_check.py hands its decisions to its child processes so that
+    they compare kernels, not autotune outcomes)."""
+    o = os.environ.get("JR_TUNE_DB")
+    return Path(o) if o else DB_DIR / f"{arch}.json"
 
 
 def _key(key) -> str:

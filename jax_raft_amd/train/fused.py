@@ -750,7 +750,12 @@ class FusedLoop:
         P.add_record(E_ME)
         P.set_lane(0)
         P.add_wait(E_ME)
-        self._record_wgrads(P)
+        # the stacked weight gradients: their own plan, replayed on a side stream so that they
+        # overlap the pyramid and encoder backward (independent of them; joined by _finish_weights)
+        self.plan_w = nat.new_plan()
+        self.plan_w.set_segment(0)
+        self.plan_w.set_lane(0)
+        self._record_wgrads(self.plan_w)
         return P
 
     def _record_wgrads(self, P):
@@ -819,7 +824,10 @@ class FusedLoop:
         self.gen += 1
         return self.out.clone()
 
-    def backward(self, gout: torch.Tensor, gen: int, fe_dy=None):
+    def backward(self, gout: torch.Tensor, gen: int, fe_dy=None, defer_weights: bool = False):
+        """The loop's backward: (dfmap1, dfmap2, d context-encoder output, parameter
+        gradients); ``defer_weights``: the parameter gradients are None here and come from
+        :meth:`finish_weights` (their kernels overlap whatever the caller enqueues meanwhile)."""
         if gen != self.gen or self.done_gen == gen:
             raise RuntimeError("fused refinement loop: this backward's saved activations were overwritten by a "
                                "later forward of the same loop (run backward before the next forward) or it "
@@ -827,7 +835,49 @@ class FusedLoop:
         self.done_gen = gen
         self.gout.copy_(gout)
         self._run(self.plan_b)
-        return self._finish(fe_dy)
+        cur = torch.cuda.current_stream(self.device)
+        if defer_weights:   # the stacked weight gradients overlap the caller's encoder backward
+            if getattr(self, "_wstream", None) is None:
+                self._wstream = torch.cuda.Stream(device=self.device)
+            self._wstream.wait_stream(cur)
+            with torch.cuda.stream(self._wstream):
+                self._run(self.plan_w)
+            self._w_pending = True
+            return self._finish_data(fe_dy) + (None,)
+        self._run(self.plan_w)
+        self._w_pending = False
+        return self._finish_data(fe_dy) + (self.finish_weights(),)
+
+    def finish_weights(self):
+        """Join the weight-gradient stream and assemble the gate / flow-head kernels into
+        the gradient arena: the loop parameters' gradients (after :meth:`backward`)."""
+        if self._w_pending:
+            torch.cuda.current_stream(self.device).wait_stream(self._wstream)
+            self._w_pending = False
+        A = self.arena
+        hd, C, fh, mp = self.hd, self.ctx_ch, self.fh, self.mp
+        mot = self.mot_out
+        for g, gru in enumerate(self.grus):
+            gC, db = self._gC[g]
+            for j, conv in enumerate((gru.convz, gru.convr, gru.convq)):
+                full = A.of(conv, "kernel")
+                src = self.gAw[g][..., j * hd:(j + 1) * hd] if j < 2 else self.gBw[g]
+                full[:, :, :hd] = src[:, :, :hd]
+                full[:, :, hd + C:] = src[:, :, hd: hd + mot]
+                full[:, :, hd:hd + C] = gC[..., j * hd:(j + 1) * hd]
+                A.of(conv, "bias").copy_(db[j * hd:(j + 1) * hd])
+        fhn, mh = self.fh_hidden, self.mask_hidden
+        A.of(fh.conv1, "kernel").copy_(self.fh1w[..., :fhn])
+        A.of(fh.conv1, "bias").copy_(self.fh1b[:fhn])
+        if self.has_mask:
+            mr = mp.convrelu.layers_0
+            A.of(mr, "kernel").copy_(self.fh1w[..., fhn:fhn + mh])
+            A.of(mr, "bias").copy_(self.fh1b[fhn:fhn + mh])
+        A.of(fh.conv2, "kernel").copy_(torch.flip(self.fh2w, dims=(0, 1)).permute(0, 1, 3, 2))
+        A.of(fh.conv2, "bias").copy_(self.ddelta.reshape(-1, 8)[:, :2].sum(0, dtype=F32))
+        grads = A.snapshot()
+        self.last_snapshot = A.last_snapshot
+        return [grads[id(p)] for p in self.params]
 
     def _pyramid_backward(self, out1=None, out2=None):
         """Correlation pyramid backward: the pooling adjoints of all levels as one
@@ -870,14 +920,13 @@ class FusedLoop:
         return g1.reshape(B, h, w, C), g2.reshape(B, h, w, C)
 
     # ---------------------------------------------------- weight gradients
-    def _finish(self, fe_dy=None):
-        """After the backward plan (data gradients + stacked weight gradients):
-        the context share of the ConvGRU gates (iteration sums), the assembly of
-        the gate / flow-head kernels, the pyramid and context-encoder input
-        gradients."""
+    def _finish_data(self, fe_dy=None):
+        """After the backward plan: the context share of the ConvGRU gates (iteration sums,
+        weight gradient kept for :meth:`finish_weights`), the pyramid and context-encoder
+        input gradients."""
         T, G, M, hd, C = self.T, self.G, self.M, self.hd, self.ctx_ch
-        fh, mp, A = self.fh, self.mp, self.arena
         dctx = self.dctx
+        self._gC = []
         for g, gru in enumerate(self.grus):
             kh, kw = gru.convz.kernel.shape[:2]
             S = torch.cat([self.dzr[g].sum(0, dtype=F32), self.dq[g].sum(0, dtype=F32)], dim=1)  # (M, 3 hd)
@@ -886,26 +935,10 @@ class FusedLoop:
             db = torch.empty(3 * hd, device=self.device)
             record_wgrad(None, self.ctx_in, self.B, self.h, self.w, 0, self.ctx_cs, tuple(gC.shape), (1, 1),
                          gru.padding, Sb, 0, gC, db)
-            mot = self.mot_out
-            for j, conv in enumerate((gru.convz, gru.convr, gru.convq)):
-                full = A.of(conv, "kernel")
-                src = self.gAw[g][..., j * hd:(j + 1) * hd] if j < 2 else self.gBw[g]
-                full[:, :, :hd] = src[:, :, :hd]
-                full[:, :, hd + C:] = src[:, :, hd: hd + mot]
-                full[:, :, hd:hd + C] = gC[..., j * hd:(j + 1) * hd]
-                A.of(conv, "bias").copy_(db[j * hd:(j + 1) * hd])
+            self._gC.append((gC, db))
             # context data gradient of this GRU's gates (accumulated over the GRUs)
             tx, ix = _tx(s1=Seg(gin=dctx if g > 0 else None, out=dctx))
             self._conv(None, f"gCT{g}", Sb, dctx, tx=tx, ix=ix, epi=EPI_BWD, hidden=0)
-        fhn, mh = self.fh_hidden, self.mask_hidden
-        A.of(fh.conv1, "kernel").copy_(self.fh1w[..., :fhn])
-        A.of(fh.conv1, "bias").copy_(self.fh1b[:fhn])
-        if self.has_mask:
-            mr = mp.convrelu.layers_0
-            A.of(mr, "kernel").copy_(self.fh1w[..., fhn:fhn + mh])
-            A.of(mr, "bias").copy_(self.fh1b[fhn:fhn + mh])
-        A.of(fh.conv2, "kernel").copy_(torch.flip(self.fh2w, dims=(0, 1)).permute(0, 1, 3, 2))
-        A.of(fh.conv2, "bias").copy_(self.ddelta.reshape(-1, 8)[:, :2].sum(0, dtype=F32))
         if fe_dy is not None:   # whole-model path: straight into the feature encoder's bf16 output gradient
             g1, g2 = self._pyramid_backward(fe_dy[: self.B], fe_dy[self.B:])
         else:
@@ -915,9 +948,7 @@ class FusedLoop:
         dc = torch.empty(M, hd + C, device=self.device, dtype=F32)
         dc[:, :hd] = self.dh_next * (1 - h0 * h0)
         dc[:, hd:] = dctx[:, :C] * (self.ctx_in[:, :C] > 0)
-        grads = A.snapshot()
-        self.last_snapshot = A.last_snapshot
-        return g1, g2, dc.reshape(self.B, self.h, self.w, hd + C), [grads[id(p)] for p in self.params]
+        return g1, g2, dc.reshape(self.B, self.h, self.w, hd + C)
 
 
 class FusedRefine(torch.autograd.Function):
@@ -986,15 +1017,18 @@ class FusedModel:
 
     def backward(self, gout, gen: int):
         comm = _ACTIVE_COMM.get(id(self.model))
-        _, _, dctx, pgrads = self.loop.backward(gout, gen, fe_dy=self.fe.dy_out)
-        if comm is not None:   # data parallel: the loop's gradients reduce while the encoders run backward
-            comm.start(self.loop.last_snapshot)
+        # the loop's stacked weight gradients run on their own stream, overlapping the encoders'
+        # backward (bandwidth-bound norm passes next to MFMA-bound GEMMs)
+        _, _, dctx, _ = self.loop.backward(gout, gen, fe_dy=self.fe.dy_out, defer_weights=True)
         self.ce.dy_out.copy_(dctx)
         cur, side = torch.cuda.current_stream(self.loop.device), self._side()
         side.wait_stream(cur)
         with torch.cuda.stream(side):
             self.ce.run_backward()
         self.fe.run_backward()
+        pgrads = self.loop.finish_weights()
+        if comm is not None:   # data parallel: the loop's gradients reduce while the encoders' snapshot
+            comm.start(self.loop.last_snapshot)
         cur.wait_stream(side)
         grads = {id(p): g for p, g in zip(self.loop.params, pgrads)}
         for enc in (self.fe, self.ce):

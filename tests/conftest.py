@@ -26,3 +26,28 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _release_gpu_state(request):
+    """After every GPU test: collect the test's engines / plans (their hipGraphs, events,
+    lane streams and buffers) and return cached device memory, so that one process can run
+    the whole GPU suite without the native state of earlier tests accumulating."""
+    yield
+    if "gpu" not in request.keywords:
+        return
+    import gc
+
+    import torch
+
+    if not torch.cuda.is_initialized():
+        return
+    try:
+        from jax_raft_amd.train import fused as _fused
+
+        _fused._LOOPS.clear()
+    except Exception:  # pragma: no cover
+        pass
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()

@@ -78,6 +78,8 @@ def main():
         torch.save(compute(a.size, a.iters), a.child)
         return 0
     ref = compute(a.size, a.iters)
+    from jax_raft_amd.runtime import tunedb
+
     bad = []
     for k1, k2 in (("infer_graph", "infer_graph_2"), ("infer_graph", "infer_eager"),
                    ("lanes_graph", "lanes_graph_2"), ("lanes_graph", "lanes_eager"),
@@ -85,9 +87,13 @@ def main():
         if not torch.equal(ref[k1], ref[k2]):
             bad.append(f"{k1} != {k2} (max |diff| {(ref[k1] - ref[k2]).abs().max().item():.3g})")
     with tempfile.TemporaryDirectory() as d:
+        # the children reuse this process's tile-config decisions (problems missing from the packaged
+        # table are timed here; a child timing them again could pick another config, whose different
+        # partial-sum layout changes the rounding -- an autotune outcome, not a race)
+        db = str(tunedb.save(tunedb.gpu_arch(), os.path.join(d, "tuned.json")))
         for name, env in (("serialised", {"AMD_SERIALIZE_KERNEL": "3"}), ("plan-check", {"JR_PLAN_CHECK": "1"})):
             path = os.path.join(d, name + ".pt")
-            e = dict(os.environ, **env)
+            e = dict(os.environ, JR_TUNE_DB=db, **env)
             if name == "plan-check":
                 e["JR_FUSED_GRAPH"] = "0"   # eager plans: the per-op check runs outside graph capture
             r = subprocess.run([sys.executable, __file__, "--size", *map(str, a.size), "--iters", str(a.iters),

@@ -25,9 +25,10 @@ def main():
     ap.add_argument("--size", type=int, nargs=2, default=[384, 512])
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--graph-step", action="store_true", help="replay the whole step as one captured graph")
     a = ap.parse_args()
     cfg = TrainConfig(arch=a.arch, steps=a.steps + a.warmup, batch=a.batch, iters=a.iters, size=tuple(a.size),
-                      log_every=10 ** 9)
+                      log_every=10 ** 9, graph_step=a.graph_step)
     tr = Trainer(cfg)
     batches = [tr.batch_for(i) for i in range(2)]
     for i in range(a.warmup):
