@@ -235,6 +235,7 @@ __global__ __launch_bounds__(4 * HD) void gru_halo_kernel(const GruHaloParams p)
       map_f(bm[b], bv);
 #pragma unroll
       for (int k = 0; k < 16; ++k) zreg[b][k] = sigmoidf_(acc[b][k] + bv[k]);
+      if (p.zo && om[b] >= 0) store_bf16<16>((bf16*)p.zo + (long)om[b] * HD + c0, zreg[b]);   // training: z
     }
   };
   // epilogue 1 of the r waves: r*h (h = the bf16 loop state of the footprint) -> R, zero outside
@@ -262,6 +263,22 @@ __global__ __launch_bounds__(4 * HD) void gru_halo_kernel(const GruHaloParams p)
       }
       *(bf16x8*)(R + r_off(g, c0 >> 3)) = o0;
       *(bf16x8*)(R + r_off(g, (c0 >> 3) + 1)) = o1;
+      if (p.ro && in) {   // training: r and r*h of the tile's own pixels (the region minus the halo)
+        const bool own = MODE == 0 ? (g >= 2 && g - 2 < t.nout)
+                                   : (g / t.RW >= 1 && g / t.RW <= p.TR && g % t.RW >= 1 && g % t.RW <= p.TC);
+        if (own) {
+          float rv[16];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            rv[k] = sigmoidf_(acc[b][k] + bv[k]);
+            rv[8 + k] = sigmoidf_(acc[b][8 + k] + bv[8 + k]);
+          }
+          store_bf16<16>((bf16*)p.ro + (long)rm[b] * HD + c0, rv);
+          bf16* rp = (bf16*)p.rh + (long)rm[b] * p.rh_cs + c0;
+          *(bf16x8*)rp = o0;
+          *(bf16x8*)(rp + 8) = o1;
+        }
+      }
     }
   };
   if constexpr (NB1 == NB2) {
@@ -320,7 +337,7 @@ __global__ __launch_bounds__(4 * HD) void gru_halo_kernel(const GruHaloParams p)
     for (int b = 0; b < NB2; ++b) {
       if constexpr (PRE_Q) map_pre(om[b], 2 * HD + c0, bq[b]);
       if constexpr (PRE_H) {
-        const f32x4* hq = (const f32x4*)(p.h32 + (long)(om[b] >= 0 ? om[b] : 0) * HD + c0);
+        const f32x4* hq = (const f32x4*)((p.h32in ? p.h32in : p.h32) + (long)(om[b] >= 0 ? om[b] : 0) * HD + c0);
 #pragma unroll
         for (int k = 0; k < 4; ++k) hpre[b][k] = hq[k];
       }
@@ -378,8 +395,9 @@ __global__ __launch_bounds__(4 * HD) void gru_halo_kernel(const GruHaloParams p)
 #pragma unroll
       for (int k = 0; k < 16; ++k) h[k] = hpre[b][k >> 2][k & 3];
     } else {
-      load_f32<16>(hp, h);
+      load_f32<16>(p.h32in ? p.h32in + (long)m * HD + c0 : hp, h);
     }
+    float qv[16];
 #pragma unroll
     for (int q4 = 0; q4 < 4; ++q4) {
       const f32x4 o = *(const f32x4*)(P + (((qb * NB2 + b) * 4 + q4) * 64 + lane) * 4);
@@ -388,9 +406,11 @@ __global__ __launch_bounds__(4 * HD) void gru_halo_kernel(const GruHaloParams p)
         const int k = 4 * q4 + e;
         const float q = tanhf_(acc2[b][k] + o[e] + bv[k]);
         const float z = zreg[b][k];
+        qv[k] = q;
         v[k] = (1.0f - z) * h[k] + z * q;
       }
     }
+    if (p.qo) store_bf16<16>((bf16*)p.qo + (long)m * HD + c0, qv);   // training: q
     store_f32<16>(hp, v);
     store_bf16<16>((bf16*)p.y + (long)m * p.y_cs + c0, v);
     if (p.y2) store_bf16<16>((bf16*)p.y2 + (long)m * p.y2_cs + c0, v);

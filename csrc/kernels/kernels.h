@@ -218,6 +218,8 @@ int jr_pack_pieces(const void* table, int n, long max_elems, hipStream_t stream)
 // dY (bf16 [N][OH][OW][ycs], channels yoff.. yoff+cout).  part / bpart: split-K workspaces of
 // S * cout_pad * kpad and S * cout_pad floats from jr_wgrad_plan (S <= 0: the planned S).
 int jr_wgrad_plan(int M, int K, int cout, int* S, int* cout_pad, int* kpad);
+// out[m] = [sum_t a[t][m] | sum_t b[t][m]] (bf16 in / out, fp32 sums; train/fused.py gate context share)
+int jr_sum_iters(const void* a, const void* b, int T, long M, int Ca, int Cb, void* out, hipStream_t stream);
 // the workspace plan of one conv's weight gradient (the 3x3 / stride-1 halo path or the im2col tiles)
 int jr_wgrad_plan_geom(int N, int H, int W, int cin8, int KH, int KW, int SH, int SW, int PH, int PW, int OH, int OW,
                        int cout, int* S, int* cout_pad, int* kpad);
@@ -387,6 +389,11 @@ struct GruHaloParams {
   int tiles_y, tiles_x, ntiles;       // tiles per image = tiles_y * tiles_x (mode 0: lines x segments)
   int nb1, nb2;                       // 32-pixel blocks of the halo region (GEMM 1) / the output tile
   long src_bytes, wa_bytes, wb_bytes;
+  // training forward (train/fused.py): h read from h32in (null: h32, in place) and h' written to h32;
+  // the gates saved for the backward, bf16 [M][hd] each (null: not stored): z, r, q, and r*h into
+  // rh (channel stride rh_cs, the q conv's input buffer)
+  const float* h32in;
+  void* zo; void* ro; void* qo; void* rh; int rh_cs;
 };
 int jr_gru_halo(const GruHaloParams* p, hipStream_t stream);
 // LDS bytes of one workgroup (0: the configuration is not supported)

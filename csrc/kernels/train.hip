@@ -616,6 +616,44 @@ extern "C" int jr_pack_pieces(const void* table, int n, long max_elems, hipStrea
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Iteration sums of the ConvGRU gate gradients (the loop-invariant context share of the gates,
+// train/fused.py:_finish_data): out[m][c] = sum_t a[t][m][c] (c < Ca), then b (c >= Ca), bf16 in,
+// fp32 sums, one bf16 rounding -- one pass instead of two strided framework reductions + cat + cast.
+// Thread = 8 channels of one pixel (16-B loads), T loads in flight.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sum_iters_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b, int T,
+                                                        long M, int Ca, int Cb, bf16* __restrict__ out) {
+  const int cg = (Ca + Cb) >> 3;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= M * cg) return;
+  const long m = idx / cg;
+  const int c = (int)(idx - m * cg) * 8;
+  const bool fa = c < Ca;
+  const bf16* src = fa ? a + m * Ca + c : b + m * Cb + (c - Ca);
+  const long tstride = fa ? M * Ca : M * Cb;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const bf16x8 v = *(const bf16x8*)(src + (long)t * tstride);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[j]);
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
+  *(bf16x8*)(out + m * (Ca + Cb) + c) = o;
+}
+
+extern "C" int jr_sum_iters(const void* a, const void* b, int T, long M, int Ca, int Cb, void* out, hipStream_t stream) {
+  if (Ca % 8 || Cb % 8 || T < 1) return (int)hipErrorInvalidValue;
+  const long n = M * ((Ca + Cb) / 8);
+  hipLaunchKernelGGL(sum_iters_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const bf16*)a,
+                     (const bf16*)b, T, M, Ca, Cb, (bf16*)out);
+  return (int)hipGetLastError();
+}
+
 extern "C" int jr_norm_bwd_partials(int N, int HW) { return N * ((HW + NB_ROWS - 1) / NB_ROWS); }
 
 extern "C" int jr_norm_bwd(const void* gout, const void* om, const void* y, const float* stats, int mode,

@@ -750,6 +750,33 @@ static Launch make_gru_halo(const TList& t, const IList& i, std::vector<at::Tens
   p.src_bytes = (long)hs.numel() * 2; p.wa_bytes = (long)wa.numel() * 2; p.wb_bytes = (long)wb.numel() * 2;
   TORCH_CHECK(p.src_bytes < (1LL << 31), "gru_halo: loop buffers larger than 2 GiB");
   if (keep) for (auto& v : {hs, xs, wa, wb, bmap, h32, y, y2}) if (v.defined()) keep->push_back(v);
+  // optional t[11..15] (training forward, train/fused.py): h32in (fp32 [M][hd]: h is read there and
+  // h' written to h32), and the saved gates zo / ro / qo (bf16 [M][hd]) + r*h into rh (bf16 [M][>= hd])
+  {
+    at::Tensor h32in = opt(t, 11), zo = opt(t, 12), ro = opt(t, 13), qo = opt(t, 14), rh = opt(t, 15);
+    if (h32in.defined()) {
+      check_f32(h32in, "h32in");
+      TORCH_CHECK(cs(h32in) == hd && h32in.numel() >= M * hd && h32in.data_ptr() != h32.data_ptr() &&
+                      reinterpret_cast<uintptr_t>(h32in.data_ptr()) % 16 == 0, "gru_halo: h32in [M][hd], not h32");
+      p.h32in = h32in.data_ptr<float>();
+      if (keep) keep->push_back(h32in);
+    }
+    const bool any = zo.defined() || ro.defined() || qo.defined() || rh.defined();
+    if (any) {
+      TORCH_CHECK(zo.defined() && ro.defined() && qo.defined() && rh.defined(), "gru_halo: saved gates: all four or none");
+      for (const at::Tensor* v : {&zo, &ro, &qo}) {
+        check_bf16(*v, "saved gate");
+        TORCH_CHECK(cs(*v) == hd && v->numel() >= M * hd && reinterpret_cast<uintptr_t>(v->data_ptr()) % 16 == 0,
+                    "gru_halo: saved gates are bf16 [M][hd]");
+      }
+      check_bf16(rh, "rh");
+      TORCH_CHECK(cs(rh) % 8 == 0 && cs(rh) >= hd && rh.numel() >= M * cs(rh) &&
+                      reinterpret_cast<uintptr_t>(rh.data_ptr()) % 16 == 0 && rh.data_ptr() != hs.data_ptr() &&
+                      rh.data_ptr() != xs.data_ptr(), "gru_halo: rh [M][>= hd], not a source");
+      p.zo = zo.data_ptr(); p.ro = ro.data_ptr(); p.qo = qo.data_ptr(); p.rh = rh.data_ptr(); p.rh_cs = cs(rh);
+      if (keep) for (auto& v : {zo, ro, qo, rh}) keep->push_back(v);
+    }
+  }
   // optional t[8..10] = hsrc / xsrc / y of ODD loop iterations: a single-stage GRU (raft_small)
   // ping-pongs h between two loop buffers (it cannot update h in place, see the kernel)
   at::Tensor hs2 = opt(t, 8), xs2 = opt(t, 9), y_2 = opt(t, 10);
@@ -1212,6 +1239,22 @@ static Launch make_copy_channels(const TList& t, const IList& i, std::vector<at:
   return [=](hipStream_t s, int) { return jr_copy_channels(ap, acs, so, bp, bcs, dof, M, C, s); };
 }
 
+// t = [a (bf16 [T][M][Ca]), b (bf16 [T][M][Cb]), out (bf16 [M][Ca + Cb])], i = [T, M]
+static Launch make_sum_iters(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor a = opt(t, 0), b = opt(t, 1), o = opt(t, 2);
+  check_bf16(a, "a"); check_bf16(b, "b"); check_bf16(o, "out");
+  const int T = (int)i[0];
+  const int64_t M = i[1];
+  const int Ca = cs(a), Cb = cs(b);
+  TORCH_CHECK(T >= 1 && a.numel() == T * M * Ca && b.numel() == T * M * Cb && o.numel() == M * (Ca + Cb) &&
+                  Ca % 8 == 0 && Cb % 8 == 0,
+              "sum_iters: shapes");
+  if (keep) for (auto& v : {a, b, o}) keep->push_back(v);
+  const void *ap = a.data_ptr(), *bp = b.data_ptr();
+  void* op = o.data_ptr();
+  return [=](hipStream_t s, int) { return jr_sum_iters(ap, bp, T, (long)M, Ca, Cb, op, s); };
+}
+
 // t = [coords, gout, dl0, dl1, dl2, dl3], i = [num_levels, B, h, w, radius]
 static Launch make_lookup_bwd(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
   at::Tensor coords = opt(t, 0), g = opt(t, 1);
@@ -1558,6 +1601,7 @@ void norm_act_op(const TList& t, IList i, double eps) { run_now(make_norm_act(t,
 void prep_op(const TList& t, IList i) { run_now(make_prep(t, i, nullptr)); }
 void init_coords_op(const TList& t, IList i) { run_now(make_init_coords(t, i, nullptr)); }
 void copy_channels_op(const TList& t, IList i) { run_now(make_copy_channels(t, i, nullptr)); }
+void sum_iters_op(const TList& t, IList i) { run_now(make_sum_iters(t, i, nullptr)); }
 void lookup_bwd_op(const TList& t, IList i) { run_now(make_lookup_bwd(t, i, nullptr)); }
 void im2col_op(const TList& t, IList i) { run_now(make_im2col(t, i, nullptr)); }
 void flow_taps_op(const TList& t, IList i) { run_now(make_flow_taps(t, i, nullptr)); }
@@ -2188,6 +2232,7 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("prep(Tensor?[] t, int[] i) -> ()", &jr::prep_op);
   m.def("init_coords(Tensor?[] t, int[] i) -> ()", &jr::init_coords_op);
   m.def("copy_channels(Tensor?[] t, int[] i) -> ()", &jr::copy_channels_op);
+  m.def("sum_iters(Tensor?[] t, int[] i) -> ()", &jr::sum_iters_op);
   m.def("lookup_bwd(Tensor?[] t, int[] i) -> ()", &jr::lookup_bwd_op);
   m.def("im2col(Tensor?[] t, int[] i) -> ()", &jr::im2col_op);
   m.def("flow_taps(Tensor?[] t, int[] i) -> ()", &jr::flow_taps_op);

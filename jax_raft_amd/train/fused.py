@@ -294,6 +294,7 @@ class FusedLoop:
         self._pack()
         self.packer = self._pieces()
         self.arena = GradArena(self.params, self.device, model=self.model)
+        self._halo_tiles = [self._halo_tile(g) for g in range(self.G)] if self.gru_halo else None
         self.plan_f = self._build_fwd()
         self.plan_b = self._build_bwd()
 
@@ -327,6 +328,11 @@ class FusedLoop:
         self.fm_cs = round_up(self.fh_hidden + self.mask_hidden, 8)
         self.gate_cs = round_up(3 * self.hd, 8)
         self.fmap_ch = m.feature_encoder.out_channels
+        # the forward's ConvGRU stages on gru_halo.hip (one launch per stage instead of EPI_GRU_A / B):
+        # raft_large's 1x5 / 5x1 stages over [h | motion | flow] = 2 hd loop channels.  JR_TRAIN_GRU_HALO=0: off
+        ks = [tuple(g.convz.kernel.shape[:2]) for g in self.grus]
+        self.gru_halo = (self.device.type == "cuda" and os.environ.get("JR_TRAIN_GRU_HALO", "1") != "0"
+                         and self.hd == 128 and self.hx_cs == 2 * self.hd and ks == [(1, 5), (5, 1)])
 
     def _params(self):
         me, fh, mp = self.me, self.fh, self.mp
@@ -356,6 +362,7 @@ class FusedLoop:
         self.fm1, self.fm2 = self.fm[: self.B], self.fm[self.B:]
         self.ctx_raw = z(self.B, h, w, self.hd + self.ctx_ch)  # context-encoder output (full-model path)
         self.gbias = [z(M, self.gate_cs, dtype=F32) for _ in range(G)]
+        self.gbias_bf = [z(M, self.gate_cs) for _ in range(G)] if self.gru_halo else None
         # [g][t]: GRU g's inputs at iteration t; hx[0][t + 1] / hf[0][t + 1] = output of the last GRU
         self.hx = z(G, T + 1, M, self.hx_cs)
         self.qx = z(G, T + 1, M, self.hx_cs)
@@ -505,10 +512,15 @@ class FusedLoop:
             k = k.to(self.device)
             sp = self._specs.get(name)
             if sp is None:
-                self._specs[name] = nat.make_spec(k, b.to(self.device), (1, 1), tuple(pad), cin8=cin8, device=self.device)
+                sp = self._specs[name] = nat.make_spec(k, b.to(self.device), (1, 1), tuple(pad), cin8=cin8,
+                                                       device=self.device)
+                if self.gru_halo and name[:2] in ("gA", "gB") and name[2:].isdigit():
+                    sp.wh = nat.pack_gru_halo(k, sp.cin8)   # gru_halo.hip weight stream (repacked by the plan)
             else:
                 nat.pack_weight(k, sp.cin8, out=sp.w)
                 sp.b.copy_(b)
+                if sp.wh is not None and name[:2] in ("gA", "gB") and name[2:].isdigit():
+                    nat.pack_gru_halo(k, sp.cin8, out=sp.wh)
         fb = self.fh.conv2.bias.detach().float().to(self.device)
         if not hasattr(self, "_fh2_bias"):
             self._fh2_bias = fb.contiguous()
@@ -544,13 +556,15 @@ class FusedLoop:
         for g, gru in enumerate(self.grus):
             for j, c in enumerate((gru.convz, gru.convr)):   # loop part [h | motion] of the z / r gates
                 co = (j * hd, (j + 1) * hd)
-                pk.piece(c.kernel, sp[f"gA{g}"], 0, co, (0, hd))
-                pk.piece(c.kernel, sp[f"gA{g}"], 0, co, (hd, hd + mot), so_ci=hd + C)
+                for mode in ((0, 4) if sp[f"gA{g}"].wh is not None else (0,)):   # 4: the gru_halo stream
+                    pk.piece(c.kernel, sp[f"gA{g}"], mode, co, (0, hd))
+                    pk.piece(c.kernel, sp[f"gA{g}"], mode, co, (hd, hd + mot), so_ci=hd + C)
                 pk.piece(c.kernel, sp[f"gAT{g}"], 1, (0, hd), co)
                 pk.piece(c.kernel, sp[f"gAT{g}"], 1, (hd, hd + mot), co, so_co=hd + C)
             q = gru.convq
-            pk.piece(q.kernel, sp[f"gB{g}"], 0, (0, hd), (0, hd))
-            pk.piece(q.kernel, sp[f"gB{g}"], 0, (0, hd), (hd, hd + mot), so_ci=hd + C)
+            for mode in ((0, 4) if sp[f"gB{g}"].wh is not None else (0,)):
+                pk.piece(q.kernel, sp[f"gB{g}"], mode, (0, hd), (0, hd))
+                pk.piece(q.kernel, sp[f"gB{g}"], mode, (0, hd), (hd, hd + mot), so_ci=hd + C)
             pk.piece(q.kernel, sp[f"gBT{g}"], 1, (0, hd), (0, hd))
             pk.piece(q.kernel, sp[f"gBT{g}"], 1, (hd, hd + mot), (0, hd), so_co=hd + C)
             for j, c in enumerate((gru.convz, gru.convr, gru.convq)):   # context share + gate biases
@@ -579,6 +593,32 @@ class FusedLoop:
 
     def stale(self) -> bool:
         return self.packer.stale()
+
+    def _halo_tile(self, g: int):
+        """(mode, axis, tile) of GRU stage g on gru_halo: the fastest of the candidate tilings
+        (ops/native.py:gru_halo_candidates), timed once on this loop's own buffers (the first
+        forward overwrites everything the trial launches write)."""
+        axis = 0 if tuple(self.grus[g].convz.kernel.shape[:2]) == (1, 5) else 1
+        cands = nat.gru_halo_candidates(self.hd, 0, axis, self.B, self.h, self.w)
+        if len(cands) == 1:
+            return 0, axis, cands[0]
+        t = [self.hx[g, 0], self.hx[g, 0], self._specs[f"gA{g}"].wh, self._specs[f"gB{g}"].wh, self.gbias_bf[g],
+             self.hf[g, 1] if g + 1 < self.G else self.hf[0, 1], self.hx[g + 1, 0] if g + 1 < self.G else self.hx[0, 1],
+             None, None, None, None, self.hf[g, 0], self.zg[g, 0], self.rg[g, 0], self.qg[g, 0], self.qx[g, 0]]
+        base = [self.B, self.h, self.w, 0, axis]
+        best = None
+        for tile in cands:
+            nat.ops().gru_halo(t, base + list(tile))
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(3):
+                nat.ops().gru_halo(t, base + list(tile))
+            e1.record()
+            e1.synchronize()
+            el = e0.elapsed_time(e1)
+            if best is None or el < best[0]:
+                best = (el, tile)
+        return 0, axis, best[1]
 
     # ----------------------------------------------------------- recording
     def _conv(self, plan, name, x, y, *, x_coff=0, tx=None, ix=None, N=None, **kw):
@@ -609,8 +649,8 @@ class FusedLoop:
                    [B, h, w, self.fmap_ch, self.L, h * w, self.blocked],
                    1.0 / float(self.fmap_ch) ** 0.5)
         P.add_record(E_PACK)
-        for g in range(G):  # loop-invariant context share of every gate (+ biases), fp32
-            self._conv(P, f"gC{g}", self.ctx_in, self.gbias[g])
+        for g in range(G):  # loop-invariant context share of every gate (+ biases), fp32 (+ bf16 for gru_halo)
+            self._conv(P, f"gC{g}", self.ctx_in, self.gbias[g], y2=self.gbias_bf[g] if self.gru_halo else None)
 
         def flow_features(t):
             self._conv(P, "cf1", self.flow8[t], self.f1[t], act=ACT_RELU)
@@ -648,12 +688,21 @@ class FusedLoop:
                 P.add_copy_channels([hx0, self.hx[g, t]], [hd, hd, self.M, self.mot_cs])
                 P.add_copy_channels([hx0, self.qx[g, t]], [hd, hd, self.M, self.mot_cs])
             for g in range(G):
-                tx, ix = _tx(rbuf=self.rg[g, t])
-                self._conv(P, f"gA{g}", self.hx[g, t], self.qx[g, t], zbuf=self.zg[g, t], h32=self.hf[g, t],
-                           hidden=hd, epi=EPI_GRU_A, bmap=self.gbias[g], bmap_coff=0, tx=tx, ix=ix)
                 last = g + 1 == G
                 nh = self.hx[0, t + 1] if last else self.hx[g + 1, t]
                 nhf = self.hf[0, t + 1] if last else self.hf[g + 1, t]
+                if self.gru_halo:
+                    # one gru_halo launch per stage (csrc/kernels/gru_halo.hip), saving z, r, q and r*h
+                    # for the backward; h read from hf[g, t], h' written to the next state buffers
+                    mode, axis, tile = self._halo_tiles[g]
+                    P.add_gru_halo([self.hx[g, t], self.hx[g, t], self._specs[f"gA{g}"].wh, self._specs[f"gB{g}"].wh,
+                                    self.gbias_bf[g], nhf, nh, None, None, None, None, self.hf[g, t], self.zg[g, t],
+                                    self.rg[g, t], self.qg[g, t], self.qx[g, t]],
+                                   [B, h, w, mode, axis] + list(tile))
+                    continue
+                tx, ix = _tx(rbuf=self.rg[g, t])
+                self._conv(P, f"gA{g}", self.hx[g, t], self.qx[g, t], zbuf=self.zg[g, t], h32=self.hf[g, t],
+                           hidden=hd, epi=EPI_GRU_A, bmap=self.gbias[g], bmap_coff=0, tx=tx, ix=ix)
                 tx, ix = _tx(qbuf=self.qg[g, t], h32o=nhf)
                 self._conv(P, f"gB{g}", self.qx[g, t], nh, zbuf=self.zg[g, t], h32=self.hf[g, t], hidden=hd,
                            epi=EPI_GRU_B, bmap=self.gbias[g], bmap_coff=2 * hd, tx=tx, ix=ix)
@@ -929,8 +978,9 @@ class FusedLoop:
         self._gC = []
         for g, gru in enumerate(self.grus):
             kh, kw = gru.convz.kernel.shape[:2]
-            S = torch.cat([self.dzr[g].sum(0, dtype=F32), self.dq[g].sum(0, dtype=F32)], dim=1)  # (M, 3 hd)
-            Sb = S.to(BF16)
+            # iteration sums of [dzr | dq] (M, 3 hd), fp32 accumulation, one bf16 rounding (train.hip)
+            Sb = torch.empty(M, 3 * hd, dtype=BF16, device=self.device)
+            nat.ops().sum_iters([self.dzr[g], self.dq[g], Sb], [T, M])
             gC = torch.empty(kh, kw, C, 3 * hd, device=self.device)
             db = torch.empty(3 * hd, device=self.device)
             record_wgrad(None, self.ctx_in, self.B, self.h, self.w, 0, self.ctx_cs, tuple(gC.shape), (1, 1),
