@@ -598,8 +598,17 @@ static Launch make_flow_taps(const TList& t, const IList& i, std::vector<at::Ten
   void* qp = ptr(qx);
   void* f8p = ptr(f8);
   const int tcs = cs(tp), hcs = cs(hx), qcs = qx.defined() ? cs(qx) : 0, f8cs = f8.defined() ? cs(f8) : 0;
-  return [=](hipStream_t s, int) {
-    return jr_flow_taps(tpp, tcs, bp, N, h, w, cp, f32p, hp, hcs, hx_off, qp, qcs, qx_off, f8p, f8cs, s);
+  // optional t[7]: flow32 of ODD iterations (parity-buffered, see make_lookup)
+  float* f32b = nullptr;
+  if (at::Tensor fb = opt(t, 7); fb.defined()) {
+    check_f32(fb, "flow32 (odd)");
+    TORCH_CHECK(fb.numel() >= 2 * M, "flow_taps: odd-iteration flow32 [M][2]");
+    f32b = fb.data_ptr<float>();
+    if (keep) keep->push_back(fb);
+  }
+  return [=](hipStream_t s, int it) {
+    float* f = (f32b && (it & 1)) ? f32b : f32p;
+    return jr_flow_taps(tpp, tcs, bp, N, h, w, cp, f, hp, hcs, hx_off, qp, qcs, qx_off, f8p, f8cs, s);
   };
 }
 
@@ -682,6 +691,19 @@ static Launch make_gru_fused(const TList& t, const IList& i, std::vector<at::Ten
   p.hx_bytes = (long)hx.numel() * 2; p.wa_bytes = (long)wa.numel() * 2; p.wb_bytes = (long)wb.numel() * 2;
   TORCH_CHECK(p.hx_bytes < (1LL << 31), "gru_fused: hx larger than 2 GiB");
   if (keep) for (auto& v : {hx, wa, wb, bmap, h32, y, y2}) if (v.defined()) keep->push_back(v);
+  // optional t[8]: the y2 copy of ODD loop iterations (a parity-buffered h copy for the mask lane,
+  // runtime/engine.py: the lane reads iteration i's copy while iteration i+1 writes the other one)
+  at::Tensor y2b = opt(t, 8);
+  if (y2b.defined()) {
+    TORCH_CHECK(y2.defined(), "gru_fused: an odd-iteration y2 needs y2");
+    check_bf16(y2b, "y2 (odd)");
+    TORCH_CHECK(y2b.sizes() == y2.sizes() && reinterpret_cast<uintptr_t>(y2b.data_ptr()) % 16 == 0,
+                "gru_fused: odd-iteration y2 must have y2's shape");
+    GruFusedParams q = p;
+    q.y2 = y2b.data_ptr();
+    if (keep) keep->push_back(y2b);
+    return [p, q](hipStream_t s, int it) { return jr_gru_fused((it & 1) ? &q : &p, s); };
+  }
   return [p](hipStream_t s, int) { return jr_gru_fused(&p, s); };
 }
 
@@ -1018,9 +1040,19 @@ static Launch make_lookup(const TList& t, const IList& i, std::vector<at::Tensor
                   hx.data_ptr(), cs(hx), hx_off, ptr(qx), cs(qx), qx_off, ptr(f8), cs(f8), 1};
     if (keep) for (auto& v : {tp, bias, f32, hx, qx, f8}) if (v.defined()) keep->push_back(v);
   }
+  // optional t[12]: flow32 of ODD iterations (parity-buffered for the mask lane's convex head)
+  float* f32b = nullptr;
+  if (at::Tensor fb = opt(t, 12); fb.defined()) {
+    TORCH_CHECK(upd.on, "lookup: an odd-iteration flow32 needs the fused update");
+    check_f32(fb, "flow32 (odd)");
+    TORCH_CHECK(fb.numel() >= (int64_t)B * nq * 2, "lookup: odd-iteration flow32 [M][2]");
+    f32b = fb.data_ptr<float>();
+    if (keep) keep->push_back(fb);
+  }
   return [=](hipStream_t s, int it) {
     TapsUpd u = upd;
     u.on = upd.on && it > 0;
+    if (f32b && (it & 1)) u.flow32 = f32b;
     return jr_corr_lookup(lv.data(), L, B, h, w, nq, r, cp, op, ocs, lbf, blocked, s, &u);
   };
 }
@@ -1094,10 +1126,20 @@ static Launch make_convex_head(const TList& t, const IList& i, double alpha, std
   const float* flp = flow.data_ptr<float>();
   float* op = out.data_ptr<float>();
   const float a = (float)alpha;
+  // optional t[6]: the parity-buffered flow (runtime/engine.py): the flow of iteration it was written by
+  // the update of iteration it + 1 (lookup / flow_taps), into t[6] when it + 1 is odd, else into t[3]
+  const float* flb = nullptr;
+  if (at::Tensor fb = opt(t, 6); fb.defined()) {
+    check_f32(fb, "flow (odd)");
+    TORCH_CHECK(fb.numel() >= 2 * M, "convex_head: odd flow [M][2]");
+    flb = fb.data_ptr<float>();
+    if (keep) keep->push_back(fb);
+  }
   return [=](hipStream_t s, int it) {
     const int64_t off = stride * it;
     if (off + M * 128 > cap) return (int)hipErrorInvalidValue;
-    return jr_convex_head(fp, fcs, coff, wp, bp, a, flp, B, h, w, op + off, sp, (long)(slot_off + off), tiles, s);
+    const float* f = (flb && ((it + 1) & 1)) ? flb : flp;
+    return jr_convex_head(fp, fcs, coff, wp, bp, a, f, B, h, w, op + off, sp, (long)(slot_off + off), tiles, s);
   };
 }
 

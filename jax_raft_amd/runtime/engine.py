@@ -1108,6 +1108,17 @@ class RaftEngine:
         # with the mask lane, the mask head reads h from its own copy `hm` (written by the last
         # stage), so the first stage can replace h in hx while the mask lane still runs
         hm = alloc("hm", (M, self.hidden)) if gru_path != "unfused" and lanes_on and self.has_mask else None
+        # Parity-buffered mask-lane operands (gru_fused + convex head, JR_MASK_PARITY=1: on): the last
+        # GRU stage writes h into hm / hm2 and the update writes the flow into flow32 / flow32b by
+        # iteration parity, so iteration i+1 never overwrites what the lane still reads for iteration
+        # i; the lane's next read of a buffer is ordered by the E_FLOW join of the iteration after,
+        # and the per-iteration E_MASK join (a ~10 us cross-stream graph edge) goes away.  Measured
+        # slower at batch 4 (359-365 vs 372 pairs/s, profiles/r4_mask_parity_ab.txt): unjoined, the
+        # mask head overlaps the ConvGRU stages (48 -> 54-56 us each) instead of the motion encoder.
+        parity = (hm is not None and gru_path == "fused" and self._convex_w is not None
+                  and os.environ.get("JR_MASK_PARITY", "0") == "1")
+        hm2 = alloc("hm2", (M, self.hidden)) if parity else None
+        flow32b = alloc("flow32b", (M, 2), F32) if parity else None
 
         # one-lane schedule: the flow conv + the previous iteration's upsampling as one grid (merged.hip)
         c1k = me.convflow1.layers_0.kernel
@@ -1141,8 +1152,8 @@ class RaftEngine:
 
         def flow_update():
             """``coords1 += delta`` (model.py:505) from the taps; flow into hx / qx / flow8."""
-            plan.add_flow_taps([taps, self._fh2_b, coords, flow32, hx, qx if qx_x else None, flow8],
-                               [B, h, w, self.flow_off, self.flow_off])
+            plan.add_flow_taps([taps, self._fh2_b, coords, flow32, hx, qx if qx_x else None, flow8]
+                               + ([flow32b] if parity else []), [B, h, w, self.flow_off, self.flow_off])
 
         def upsample(stride, mask_from_fm: bool):
             """x8 upsampling of flow32 into the output (model.py:508): convex with
@@ -1154,10 +1165,12 @@ class RaftEngine:
             if mask_from_fm:
                 feat_, coff = fm, self.fh_hidden
             else:
-                self._conv(plan, sp["mask.convrelu"], hm if hm is not None else hx, B, h, w, mfeat, act=ACT_RELU)
+                self._conv(plan, sp["mask.convrelu"], hm if hm is not None else hx, B, h, w, mfeat, act=ACT_RELU,
+                           x_alt=hm2)
                 feat_, coff = mfeat, 0
             if self._convex_w is not None:
-                plan.add_convex_head([feat_, self._convex_w, self._convex_b, flow32, out, st.out_slot],
+                plan.add_convex_head([feat_, self._convex_w, self._convex_b, flow32, out, st.out_slot]
+                                     + ([flow32b] if parity else []),
                                      [B, h, w, coff, stride, 0, out_off], m.mask_predictor.multiplier)
             else:   # generic mask head (an injected MaskPredictor): 1x1 conv + convex upsampling
                 st.slot_ok = False
@@ -1166,6 +1179,8 @@ class RaftEngine:
 
         def lookup(with_update: bool):
             upd = [taps, self._fh2_b, flow32, hx, qx if qx_x else None, flow8] if with_update else []
+            if with_update and parity:
+                upd.append(flow32b)   # t[12]: the odd iterations' flow
             extra = [self.flow_off, self.flow_off] if with_update else []
             plan.add_lookup([coords, corr] + levels + [None] * (4 - L) + upd,
                             [L, B, h, w, self.radius, h * w, blocked] + extra)
@@ -1217,11 +1232,12 @@ class RaftEngine:
             for gi in range(ngru):
                 if gru_path == "fused":
                     last = gi == ngru - 1
-                    if wait_mask and (last if hm is not None else gi == 0):
+                    if wait_mask and not parity and (last if hm is not None else gi == 0):
                         plan.add_wait(E_MASK)  # the previous iteration's mask head has read hm / h (and flow32)
                     ks = m.update_block.recurrent_block.kernel_size[gi]
                     plan.add_gru_fused([hx, sp[f"gru{gi}.a"].w, sp[f"gru{gi}.b"].w, gbias[gi], h32, hx,
-                                        hm if last else None], [B, h, w, int(ks[0] > 1)])
+                                        hm if last else None] + ([None, hm2] if last and parity else []),
+                                       [B, h, w, int(ks[0] > 1)])
                     continue
                 # r*h from the bf16 h of the conv's own input hx (no fp32 state read)
                 self._conv(plan, sp[f"gru{gi}.a"], hx, B, h, w, qx, zbuf=zb, hidden=self.hidden,

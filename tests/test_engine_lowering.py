@@ -74,11 +74,42 @@ def test_lane_schedule_raft_large(fake, gru, monkeypatch):
     assert ops.count("wait") == 3
 
 
+def test_lane_schedule_fused_gru_parity(fake, monkeypatch):
+    """Default lane schedule with the fused ConvGRU: the last stage writes the mask lane's h
+    copy into hm / hm2 by iteration parity, the update writes the flow into flow32 / flow32b,
+    the lane's mask conv and convex head read the matching buffer -- and the E_MASK join is
+    gone (two waits per iteration: the lane's E_FH fork and the E_FLOW join).  Opt-in
+    (JR_MASK_PARITY=1): measured slower on MI355X."""
+    monkeypatch.setenv("JR_GRU", "fused")
+    monkeypatch.setenv("JR_MASK_PARITY", "1")
+    eng, p = _plan(raft_large, 4)
+    loop = [(ln, d, op, a) for s, ln, d, op, a in p.ops if s == 1]
+    main = [op for ln, d, op, _ in loop if ln == 0]
+    assert [op for op in main if op not in ("record", "wait")] == \
+        ["lookup", "conv1x1", "conv", "conv", "gru_fused", "gru_fused", "conv"]
+    assert [op for _, _, op, _ in loop].count("wait") == 2
+    i1, i2 = [i for i, op in enumerate(main) if op == "gru_fused"]
+    assert main[i1 - 1] != "wait" and main[i2 - 1] != "wait"
+    g1, g2 = [a for _, _, op, a in loop if op == "gru_fused"]
+    hm, hm2 = g2[0][6], g2[0][8]
+    assert g1[0][6] is None and len(g1[0]) == 7 and hm is not None and hm2 is not None and hm2 is not hm
+    side = [(d, op, a) for ln, d, op, a in loop if ln == 2]
+    alt = [a for d, op, a in side if op == "conv_alt"]
+    assert len(alt) == 1 and alt[0][0][0] is hm and alt[0][-1] is hm2   # mask conv: hm (even) / hm2 (odd)
+    lk = [a for _, _, op, a in loop if op == "lookup"][0]
+    cx = [a for d, op, a in side if op == "convex_head"][0]
+    assert lk[0][12] is cx[0][6] and lk[0][8] is cx[0][3]               # flow32 / flow32b pair
+    epi = [(op, a) for s, ln, d, op, a in p.ops if s == 2]
+    ft = [a for op, a in epi if op == "flow_taps"][0]
+    assert ft[0][7] is cx[0][6]
+
+
 def test_lane_schedule_fused_gru(fake, monkeypatch):
     """raft_large with the fused ConvGRU stages (gru_fused.hip, forced on at this small
-    size): one gru_fused op per stage on the critical lane, the mask lane's mask conv
-    reads its own h copy `hm` (written by the last stage), and the E_MASK wait moves
-    from the first stage to the last one (still three waits per iteration)."""
+    size), the default schedule (no parity buffers): one gru_fused op per stage on the
+    critical lane, the mask lane's mask conv reads its own h copy `hm` (written by the last
+    stage), and the E_MASK wait moves from the first stage to the last one (three waits per
+    iteration)."""
     monkeypatch.setenv("JR_GRU", "fused")
     eng, p = _plan(raft_large, 4)
     loop = [(ln, d, op, a) for s, ln, d, op, a in p.ops if s == 1]
