@@ -37,6 +37,21 @@
 namespace {
 
 
+// group g's A fragments -> LDS (global_load_lds, no VGPR staging; completion: the caller's barrier)
+JR_DEVICE void convex_head_load_a(const u32x4* __restrict__ wpk, int g, u32x4* __restrict__ sA) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int f = wave; f < 72; f += 4)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(wpk + (f * 4 + g) * 64 + lane),
+                                     (__attribute__((address_space(3))) void*)(sA + f * 64), 16, 0, 0);
+}
+
+// pixel block pb of group g (A fragments already in sA, or in flight when `sync`: then the block
+// barrier after the B loads completes them)
+template <int NC>
+JR_DEVICE void convex_head_tile(const bf16* __restrict__ feat, int fcs, int fcoff, const float* __restrict__ bias,
+                                float alpha, const float* __restrict__ flow, int B, int h, int w,
+                                float* __restrict__ out, int g, int pb, bool sync, const u32x4* __restrict__ sA);
+
 // one block (id) -- kernel body shared with the merged launches of merged.hip; sA: the caller's LDS
 template <int NC>  // pixel column tiles of 16 per wave (1 or 2)
 JR_DEVICE void convex_head_block(const bf16* __restrict__ feat, int fcs, int fcoff, const u32x4* __restrict__ wpk,
@@ -44,14 +59,19 @@ JR_DEVICE void convex_head_block(const bf16* __restrict__ feat, int fcs, int fco
                                  int h, int w, float* __restrict__ out, const long long* __restrict__ out_slot,
                                  long out_off, int nblk, int id, u32x4* __restrict__ sA) {
   // sA: 8 * 9 * 64 LDS entries for this group's A fragments ([ks][tap][lane])
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int g = (id >> 3) & 3, pb = (id >> 5) * 8 + (id & 7);
   if (pb >= nblk) return;  // whole block, before any barrier
   if (out_slot) out = (float*)(*out_slot) + out_off;  // output address supplied at run time (fresh tensor per call)
+  convex_head_load_a(wpk, g, sA);
+  convex_head_tile<NC>(feat, fcs, fcoff, bias, alpha, flow, B, h, w, out, g, pb, true, sA);
+}
+
+template <int NC>
+JR_DEVICE void convex_head_tile(const bf16* __restrict__ feat, int fcs, int fcoff, const float* __restrict__ bias,
+                                float alpha, const float* __restrict__ flow, int B, int h, int w,
+                                float* __restrict__ out, int g, int pb, bool sync, const u32x4* __restrict__ sA) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int HW = h * w, M = B * HW;
-  for (int f = wave; f < 72; f += 4)
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(wpk + (f * 4 + g) * 64 + lane),
-                                     (__attribute__((address_space(3))) void*)(sA + f * 64), 16, 0, 0);
   const int col = lane & 15, q = lane >> 4;
   const int p0 = (pb * 4 + wave) * 16 * NC;  // first pixel of this wave
   u32x4 b[NC][8];
@@ -67,7 +87,7 @@ JR_DEVICE void convex_head_block(const bf16* __restrict__ feat, int fcs, int fco
   for (int k = 0; k < 9; ++k)
 #pragma unroll
     for (int c = 0; c < NC; ++c) acc[k][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  __syncthreads();  // waits for the LDS copies (and the B loads) of every wave
+  if (sync) __syncthreads();  // waits for the LDS copies (and the B loads) of every wave
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) {
 #pragma unroll
@@ -85,9 +105,11 @@ JR_DEVICE void convex_head_block(const bf16* __restrict__ feat, int fcs, int fco
   // Softmax in base 2: log2(e) folded into the scale, v_exp_f32 directly.
   const float a2 = alpha * 1.4426950408889634f;
   float bv[9][4];
+  const float* bias_ = bias;
+  asm volatile("" : "+s"(bias_));   // the persistent kernel's tile loop must not hoist these 36 VGPRs
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
-    const float4 t = *(const float4*)(bias + k * 64 + 16 * g + 4 * q);
+    const float4 t = *(const float4*)(bias_ + k * 64 + 16 * g + 4 * q);
     bv[k][0] = t.x * a2; bv[k][1] = t.y * a2; bv[k][2] = t.z * a2; bv[k][3] = t.w * a2;
   }
   const int sy = 2 * g + (q >> 1), sx0 = 4 * (q & 1);
@@ -134,6 +156,30 @@ JR_DEVICE void convex_head_block(const bf16* __restrict__ feat, int fcs, int fco
   }
 }
 
+
+// Persistent form: 4 x nslot blocks (2 per CU); block (group g, slot) loads its group's 72 KB of A
+// fragments ONCE and walks pixel blocks slot, slot + nslot, ... (the per-block weight copy, ~1/3 of
+// the bytes the short-lived blocks move, is paid once per block instead of once per pixel block).
+template <int NC>
+__global__ __launch_bounds__(256, 2) void convex_head_persist_kernel(const bf16* __restrict__ feat, int fcs, int fcoff,
+                                                                     const u32x4* __restrict__ wpk,
+                                                                     const float* __restrict__ bias, float alpha,
+                                                                     const float* __restrict__ flow, int B, int h,
+                                                                     int w, float* __restrict__ out,
+                                                                     const long long* __restrict__ out_slot,
+                                                                     long out_off, int nblk, int nslot) {
+  __shared__ u32x4 sA[8 * 9 * 64];
+  const int id = blockIdx.x;
+  const int g = (id >> 3) & 3, slot = (id >> 5) * 8 + (id & 7);
+  if (slot >= nslot || slot >= nblk) return;
+  if (out_slot) out = (float*)(*out_slot) + out_off;
+  convex_head_load_a(wpk, g, sA);
+  bool first = true;
+  for (int pb = slot; pb < nblk; pb += nslot) {
+    convex_head_tile<NC>(feat, fcs, fcoff, bias, alpha, flow, B, h, w, out, g, pb, first, sA);
+    first = false;
+  }
+}
 
 template <int NC>
 __global__ __launch_bounds__(256, 2) void convex_head_kernel(const bf16* __restrict__ feat, int fcs, int fcoff,

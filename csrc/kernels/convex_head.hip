@@ -1,4 +1,6 @@
 // Launcher of the inference mask head (kernel: convex_head.h).
+#include <cstdlib>
+
 #include "convex_head.h"
 
 
@@ -11,6 +13,23 @@ extern "C" int jr_convex_head(const void* feat, int feat_cstride, int feat_coff,
   auto blocks = [M](int nc) { return (M + 64 * nc - 1) / (64 * nc); };
   const int nc = tiles == 1 || tiles == 2 ? tiles : blocks(2) * 4 >= 384 ? 2 : 1;
   const int nblk = blocks(nc);
+  // the persistent form when the grid would take more than one round (128 slots x 4 groups = 2 blocks
+  // per CU): 23.3 -> 20.3 us at raft_large batch 4 (profiles/r4_convex_persist_ab.txt);
+  // JR_CONVEX_PERSIST=0: always the one-pixel-block-per-workgroup form
+  static const bool persist = getenv("JR_CONVEX_PERSIST") == nullptr || getenv("JR_CONVEX_PERSIST")[0] != '0';
+  if (persist && nblk > 128) {
+    const int nslot = 128;
+    const dim3 pg(nslot / 8 * 32);
+    if (nc == 2)
+      hipLaunchKernelGGL(convex_head_persist_kernel<2>, pg, dim3(256), 0, stream, (const bf16*)feat, feat_cstride,
+                         feat_coff, (const u32x4*)wpk, bias, alpha, flow, B, h, w, out, (const long long*)out_slot,
+                         out_off, nblk, nslot);
+    else
+      hipLaunchKernelGGL(convex_head_persist_kernel<1>, pg, dim3(256), 0, stream, (const bf16*)feat, feat_cstride,
+                         feat_coff, (const u32x4*)wpk, bias, alpha, flow, B, h, w, out, (const long long*)out_slot,
+                         out_off, nblk, nslot);
+    return (int)hipGetLastError();
+  }
   const dim3 grid((nblk + 7) / 8 * 32);
   if (nc == 2)
     hipLaunchKernelGGL(convex_head_kernel<2>, grid, dim3(256), 0, stream, (const bf16*)feat, feat_cstride, feat_coff,
