@@ -95,8 +95,19 @@ JR_DEVICE void epi_bwd(const ConvParams& p, float (&v)[NV], int m, int cbase) {
   const int lc = cbase - (s ? p.hidden : 0);
   const int n = min(NV, p.cout - cbase);  // valid channels of this group
   const bool full = n == NV;
-  if (g.gin) {
-    const float* gp = g.gin + (long)m * g.gin_cs + g.gin_coff + lc;
+  if (g.gin && g.gin_bf16) {   // bf16 gradient input (exact when it is a masked bf16 gradient)
+    const bf16* gp = (const bf16*)g.gin + (long)m * g.gin_cs + g.gin_coff + lc;
+    if (full) {
+      float gi[NV];
+      load_bf16<NV>(gp, gi);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v[j] += gi[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) if (j < n) v[j] += bf2f(gp[j]);
+    }
+  } else if (g.gin) {
+    const float* gp = (const float*)g.gin + (long)m * g.gin_cs + g.gin_coff + lc;
     if (full) {
       float gi[NV];
       load_f32<NV>(gp, gi);

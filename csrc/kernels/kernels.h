@@ -32,7 +32,7 @@ enum ConvEpi : int {
 //           gdzr[hidden + lc] = acc h r (1-r) ; out (fp32) += acc r
 struct BwdSeg {
   int mode;
-  const float* gin; int gin_cs, gin_coff;
+  const void* gin; int gin_cs, gin_coff, gin_bf16;   // gradient input: fp32, or bf16 (gin_bf16)
   const void* mask; int mask_cs, mask_coff;
   int valid;
   void* out; int out_cs, out_coff, out_f32;
@@ -199,7 +199,7 @@ int jr_flow_gather_bwd(const float* taps, int tcs, int N, int h, int w, void* df
 int jr_norm_bwd_partials(int N, int HW);
 int jr_norm_bwd(const void* gout, const void* om, const void* y, const float* stats, int mode, const float* gamma,
                 const float* beta, int relu, int N, int HW, int C, float eps, float* red, float* partial, void* dy,
-                float* gres, hipStream_t stream);
+                void* gres, int gres_bf16, hipStream_t stream);
 // Batched weight packing (training): one rectangular piece of one packed conv weight
 // (bf16 [cout_pad][kpad], rows permuted, ops/native.py:pack_weight) from an fp32 HWIO source
 // [kh][kw][cin_s][cout_s].  For dst output channel co in [co0, co1), tap, input channel ci

@@ -380,7 +380,8 @@ __global__ __launch_bounds__(256) void norm_bwd_apply_kernel(const bf16* __restr
                                                              int mode, const float* __restrict__ gam,
                                                              const float* __restrict__ bet, int relu,
                                                              const float* __restrict__ red, int N, int HW, int C,
-                                                             float eps, bf16* __restrict__ dy, float* __restrict__ gres,
+                                                             float eps, bf16* __restrict__ dy, void* __restrict__ gres,
+                                                             int gres_bf16,
                                                              int rows) {
   const int n = blockIdx.y;
   const int cg = C >> 3;
@@ -425,8 +426,15 @@ __global__ __launch_bounds__(256) void norm_bwd_apply_kernel(const bf16* __restr
       float r[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) r[j] = (om && !(bf2f(ov[j]) > 0.f)) ? 0.f : bf2f(gv[j]);
-      *(f32x4*)(gres + off) = f32x4{r[0], r[1], r[2], r[3]};
-      *(f32x4*)(gres + off + 4) = f32x4{r[4], r[5], r[6], r[7]};
+      if (gres_bf16) {   // exact: a masked bf16 gradient
+        bf16x8 rb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rb[j] = f2bf(r[j]);
+        *(bf16x8*)((bf16*)gres + off) = rb;
+      } else {
+        *(f32x4*)((float*)gres + off) = f32x4{r[0], r[1], r[2], r[3]};
+        *(f32x4*)((float*)gres + off + 4) = f32x4{r[4], r[5], r[6], r[7]};
+      }
     }
   }
 }
@@ -658,7 +666,7 @@ extern "C" int jr_norm_bwd_partials(int N, int HW) { return N * ((HW + NB_ROWS -
 
 extern "C" int jr_norm_bwd(const void* gout, const void* om, const void* y, const float* stats, int mode,
                            const float* gamma, const float* beta, int relu, int N, int HW, int C, float eps,
-                           float* red, float* partial, void* dy, float* gres, hipStream_t stream) {
+                           float* red, float* partial, void* dy, void* gres, int gres_bf16, hipStream_t stream) {
   if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
   if (mode != 0) {
     const int nb = (HW + NB_ROWS - 1) / NB_ROWS;
@@ -671,7 +679,7 @@ extern "C" int jr_norm_bwd(const void* gout, const void* om, const void* y, cons
   const int rows = (int)std::max<long>(nrg, (want + nrg - 1) / nrg * nrg);
   const unsigned nbk = (unsigned)((HW + rows - 1) / rows);
   hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(nbk, N), dim3(256), 0, stream, (const bf16*)gout, (const bf16*)om,
-                     (const bf16*)y, stats, mode, gamma, beta, relu, red, N, HW, C, eps, (bf16*)dy, gres, rows);
+                     (const bf16*)y, stats, mode, gamma, beta, relu, red, N, HW, C, eps, (bf16*)dy, gres, gres_bf16, rows);
   return (int)hipGetLastError();
 }
 

@@ -390,9 +390,12 @@ static void conv_train_extras(ConvParams& p, int epi, const TList& tx, const ILi
       TORCH_CHECK(g.out_cs % 8 == 0 && g.out_coff % 8 == 0 && g.out_coff + width <= g.out_cs &&
                       out.numel() >= M * g.out_cs, "conv_train: segment output slice");
       if (gin.defined()) {
-        need_f32(gin, 0, "gin");
-        g.gin = gin.data_ptr<float>(); g.gin_cs = cs(gin); g.gin_coff = (int)ix[b + 1];
-        TORCH_CHECK(g.gin_cs % 4 == 0 && g.gin_coff % 4 == 0 && g.gin_coff + width <= g.gin_cs &&
+        g.gin_bf16 = gin.scalar_type() == at::kBFloat16;
+        if (g.gin_bf16) check_bf16(gin, "gin");
+        else need_f32(gin, 0, "gin");
+        g.gin = gin.data_ptr(); g.gin_cs = cs(gin); g.gin_coff = (int)ix[b + 1];
+        const int ga = g.gin_bf16 ? 8 : 4;   // 16-byte vector loads
+        TORCH_CHECK(g.gin_cs % ga == 0 && g.gin_coff % ga == 0 && g.gin_coff + width <= g.gin_cs &&
                         gin.numel() >= M * g.gin_cs, "conv_train: segment gradient-input slice");
       }
       if (mask.defined()) {
@@ -457,7 +460,11 @@ static Launch make_norm_bwd(const TList& t, const IList& i, double eps, std::vec
   TORCH_CHECK(g.numel() >= n && y.numel() >= n && dy.numel() >= n && cs(g) == C && cs(y) == C && cs(dy) == C,
               "norm_bwd: [N][HW][C] tensors");
   if (om.defined()) { check_bf16(om, "om"); TORCH_CHECK(om.numel() >= n && cs(om) == C, "norm_bwd: om"); }
-  if (gres.defined()) { check_f32(gres, "gres"); TORCH_CHECK(gres.numel() >= n && cs(gres) == C, "norm_bwd: gres"); }
+  if (gres.defined()) {   // fp32, or bf16 (the masked gradient gout * [om > 0] is exact in bf16)
+    TORCH_CHECK(gres.is_cuda() && gres.is_contiguous() &&
+                    (gres.scalar_type() == at::kFloat || gres.scalar_type() == at::kBFloat16), "norm_bwd: gres dtype");
+    TORCH_CHECK(gres.numel() >= n && cs(gres) == C, "norm_bwd: gres");
+  }
   if (mode) {
     check_f32(st, "stats");
     TORCH_CHECK(st.numel() >= (int64_t)N * C * 2, "norm_bwd: stats");
@@ -473,11 +480,13 @@ static Launch make_norm_bwd(const TList& t, const IList& i, double eps, std::vec
   auto fp = [](const at::Tensor& v) -> float* { return v.defined() ? v.data_ptr<float>() : nullptr; };
   const void *gp = g.data_ptr(), *op = ptr(om), *yp = y.data_ptr();
   const float *sp = fp(st), *gmp = fp(gam), *btp = fp(bet);
-  float *rp = fp(red), *pp = fp(part), *grp = fp(gres);
+  float *rp = fp(red), *pp = fp(part);
+  void* grp = gres.defined() ? gres.data_ptr() : nullptr;
+  const int gbf = gres.defined() && gres.scalar_type() == at::kBFloat16;
   void* dp = dy.data_ptr();
   const float e = (float)eps;
   return [=](hipStream_t s, int) {
-    return jr_norm_bwd(gp, op, yp, sp, mode, gmp, btp, relu, N, HW, C, e, rp, pp, dp, grp, s);
+    return jr_norm_bwd(gp, op, yp, sp, mode, gmp, btp, relu, N, HW, C, e, rp, pp, dp, grp, gbf, s);
   };
 }
 

@@ -757,6 +757,16 @@ class FusedLoop:
         else:
             P.add_upsample_bilinear_bwd([self.gout, self.ddelta], [TB, h, w])
         self._bconv(P, "fh2T", self.ddelta, N=TB, s1=Seg(mask=self.fmm, out=self.dfmm))
+        # the heads' weight gradients need only what ran so far: their own plan, replayed on the
+        # weight-gradient stream while the (latency-bound) BPTT chain runs (see backward)
+        self.plan_b1 = P
+        self.plan_w1 = nat.new_plan()
+        self.plan_w1.set_segment(0)
+        self.plan_w1.set_lane(0)
+        self._record_head_wgrads(self.plan_w1)
+        P = nat.new_plan()
+        P.set_segment(0)
+        P.set_lane(0)
         for t in reversed(range(T)):
             # flow head (+ mask) conv1 data gradient -> blend backward of the last GRU
             gl = G - 1
@@ -837,6 +847,15 @@ class FusedLoop:
             record_wgrad(P, self.qx[g], nT, h, w, 0, self.hx_cs, tuple(gb.shape), (1, 1), gru.padding, self.dq[g], 0, gb)
             self.gAw.append(ga)
             self.gBw.append(gb)
+
+    def _record_head_wgrads(self, P):
+        """Weight gradients of the output heads (FlowHead conv1 + the mask head's 3x3 conv,
+        FlowHead conv2, the mask 1x1 conv): inputs from the forward, output gradients from
+        the heads' backward -- nothing from the BPTT chain."""
+        T, hd, B, h, w = self.T, self.hd, self.B, self.h, self.w
+        nT = T * B
+        mp, A = self.mp, self.arena
+        dev = self.device
         fm_out = self.fh_hidden + self.mask_hidden
         self.fh1w = torch.zeros(3, 3, hd, fm_out, device=dev)
         self.fh1b = torch.zeros(fm_out, device=dev)
@@ -847,7 +866,8 @@ class FusedLoop:
         self.fh2w = torch.zeros(3, 3, 2, self.fh_hidden, device=dev)
         record_wgrad(P, self.ddelta, nT, h, w, 0, 8, tuple(self.fh2w.shape), (1, 1), (1, 1), self.fmm, 0, self.fh2w)
         if self.has_mask:
-            wb(mp.conv, self.fmm, self.fh_hidden, self.mask_hidden, self.dmask)
+            record_wgrad(P, self.fmm, nT, h, w, self.fh_hidden, self.mask_hidden, tuple(mp.conv.kernel.shape), (1, 1),
+                         mp.conv.padding, self.dmask, 0, A.of(mp.conv, "kernel"), A.of(mp.conv, "bias"))
 
     def _run(self, plan):
         _run_plan(plan, self.use_graph)
@@ -883,18 +903,22 @@ class FusedLoop:
                                "already ran (retain_graph is not supported by the fused loop)")
         self.done_gen = gen
         self.gout.copy_(gout)
-        self._run(self.plan_b)
         cur = torch.cuda.current_stream(self.device)
-        if defer_weights:   # the stacked weight gradients overlap the caller's encoder backward
-            if getattr(self, "_wstream", None) is None:
-                self._wstream = torch.cuda.Stream(device=self.device)
-            self._wstream.wait_stream(cur)
-            with torch.cuda.stream(self._wstream):
-                self._run(self.plan_w)
-            self._w_pending = True
+        if getattr(self, "_wstream", None) is None:
+            self._wstream = torch.cuda.Stream(device=self.device)
+        ws = self._wstream
+        # the heads' backward, then their weight gradients on the side stream next to the BPTT chain
+        self._run(self.plan_b1)
+        ws.wait_stream(cur)
+        with torch.cuda.stream(ws):
+            self._run(self.plan_w1)
+        self._run(self.plan_b)
+        ws.wait_stream(cur)
+        with torch.cuda.stream(ws):   # the stacked weight gradients: they overlap the caller's encoder backward
+            self._run(self.plan_w)
+        self._w_pending = True
+        if defer_weights:
             return self._finish_data(fe_dy) + (None,)
-        self._run(self.plan_w)
-        self._w_pending = False
         return self._finish_data(fe_dy) + (self.finish_weights(),)
 
     def finish_weights(self):

@@ -268,7 +268,8 @@ class EncoderTrain:
             last.dy = self._z(*last.y.shape)
             res_g = None
             if ds is None:
-                res_g = self._z(*blk["x"].shape, dtype=F32)  # dL/dx through the identity shortcut
+                # dL/dx through the identity shortcut: gout * [block output > 0], exact in bf16
+                res_g = self._z(*blk["x"].shape)
                 self._norm_bwd(last, dout, last.dy, om=blk["out"], relu=1, gres=res_g)
             else:
                 self._norm_bwd(last, dout, last.dy, om=blk["out"], relu=1)
