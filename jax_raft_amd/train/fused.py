@@ -287,6 +287,7 @@ class FusedLoop:
         self.fwd_lanes = 1 if os.environ.get("JR_FUSED_FWD_LANES", "0") == "1" else 0
         self.gen = 0            # forward generation (a backward must match the latest forward)
         self.done_gen = -1
+        self._w_pending = False  # weight-gradient plans in flight on the side stream (finish_weights joins)
         self._analyse()
         self._params()
         self._alloc()
