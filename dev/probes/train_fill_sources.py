@@ -21,9 +21,12 @@ def main():
     for _ in range(3):
         tr.train_step(b)
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True, record_shapes=True,
+                 experimental_config=torch._C._profiler._ExperimentalConfig(verbose=True)) as prof:
         tr.train_step(b)
         torch.cuda.synchronize()
+    print(prof.key_averages(group_by_stack_n=6).table(sort_by="count", row_limit=25, max_name_column_width=40,
+                                                       max_src_column_width=90))
     agg = collections.Counter()
     for ev in prof.events():
         if ev.device_type != torch.autograd.DeviceType.CPU or not ev.stack:

@@ -918,16 +918,29 @@ class FusedLoop:
         with torch.cuda.stream(ws):   # the stacked weight gradients: they overlap the caller's encoder backward
             self._run(self.plan_w)
         self._w_pending = True
+        data = self._finish_data(fe_dy)
+        # the gate / flow-head kernel assembly (~30 small copies) on the weight-gradient stream too,
+        # after the context-share weight gradients of _finish_data: off the critical path
+        with torch.cuda.stream(ws):
+            ws.wait_event(self._ev_gc)
+            self._assemble()
         if defer_weights:
-            return self._finish_data(fe_dy) + (None,)
-        return self._finish_data(fe_dy) + (self.finish_weights(),)
+            return data + (None,)
+        return data + (self.finish_weights(),)
 
     def finish_weights(self):
-        """Join the weight-gradient stream and assemble the gate / flow-head kernels into
-        the gradient arena: the loop parameters' gradients (after :meth:`backward`)."""
+        """Join the weight-gradient stream (stacked weight gradients + the kernel assembly):
+        the loop parameters' gradients (after :meth:`backward`)."""
         if self._w_pending:
             torch.cuda.current_stream(self.device).wait_stream(self._wstream)
             self._w_pending = False
+        grads = self.arena.snapshot()
+        self.last_snapshot = self.arena.last_snapshot
+        return [grads[id(p)] for p in self.params]
+
+    def _assemble(self):
+        """The gate kernels ([h | context | motion] from the loop-part and context-share
+        weight gradients) and the flow-head / mask kernels into the gradient arena."""
         A = self.arena
         hd, C, fh, mp = self.hd, self.ctx_ch, self.fh, self.mp
         mot = self.mot_out
@@ -949,9 +962,6 @@ class FusedLoop:
             A.of(mr, "bias").copy_(self.fh1b[fhn:fhn + mh])
         A.of(fh.conv2, "kernel").copy_(torch.flip(self.fh2w, dims=(0, 1)).permute(0, 1, 3, 2))
         A.of(fh.conv2, "bias").copy_(self.ddelta.reshape(-1, 8)[:, :2].sum(0, dtype=F32))
-        grads = A.snapshot()
-        self.last_snapshot = A.last_snapshot
-        return [grads[id(p)] for p in self.params]
 
     def _pyramid_backward(self, out1=None, out2=None):
         """Correlation pyramid backward: the pooling adjoints of all levels as one
@@ -1014,6 +1024,8 @@ class FusedLoop:
             # context data gradient of this GRU's gates (accumulated over the GRUs)
             tx, ix = _tx(s1=Seg(gin=dctx if g > 0 else None, out=dctx))
             self._conv(None, f"gCT{g}", Sb, dctx, tx=tx, ix=ix, epi=EPI_BWD, hidden=0)
+        self._ev_gc = torch.cuda.Event()   # the context-share weight gradients are done (_assemble)
+        self._ev_gc.record()
         if fe_dy is not None:   # whole-model path: straight into the feature encoder's bf16 output gradient
             g1, g2 = self._pyramid_backward(fe_dy[: self.B], fe_dy[self.B:])
         else:
