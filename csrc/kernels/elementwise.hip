@@ -7,6 +7,8 @@
 //   InstanceNorm / BatchNorm (Flax)                         model.py:147,157,706-711
 //   make_coords_grid                                        model.py:37-40
 //   image normalisation / NHWC staging                      scripts/validate_sintel.py:177-183
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 #include "upsample.h"
@@ -63,7 +65,7 @@ __global__ void upsample_bilinear_kernel(const float* __restrict__ flow, int B, 
 constexpr int STATS_ROWS = 1024;
 
 __global__ __launch_bounds__(256) void channel_stats_partial_kernel(const bf16* __restrict__ x, int HW, int C,
-                                                                    float* __restrict__ part) {
+                                                                    float* __restrict__ part, int rows) {
   __shared__ float red[256][17];
   const int n = blockIdx.y;
   const int cg = C >> 3;
@@ -71,8 +73,8 @@ __global__ __launch_bounds__(256) void channel_stats_partial_kernel(const bf16* 
   const int g = tid % cg;
   const int rg = tid / cg;
   const int nrg = 256 / cg;
-  const int r0 = blockIdx.x * STATS_ROWS;
-  const int r1 = min(r0 + STATS_ROWS, HW);
+  const int r0 = blockIdx.x * rows;
+  const int r1 = min(r0 + rows, HW);
   float s[8], q[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
@@ -327,17 +329,32 @@ extern "C" int jr_upsample_bilinear(const float* flow, int B, int h, int w, floa
   return (int)hipGetLastError();
 }
 
+// rows per partial block: >= ~1024 blocks over the batch (the deep layers' small maps are otherwise
+// latency-bound on a few dozen blocks), at most STATS_ROWS, a multiple of the row groups
+static int stats_rows(int N, int HW, int C) {
+  const int nrg = 256 / (C / 8);
+  const int nb = std::max(1, (1024 + N - 1) / N);
+  const int r = (HW + nb - 1) / nb;
+  return std::min(STATS_ROWS, std::max(nrg, (r + nrg - 1) / nrg * nrg));
+}
+
 extern "C" int jr_channel_stats(const void* x, int N, int HW, int C, float* stats, float* partial,
                                 hipStream_t stream) {
   if (C % 8 != 0 || (C / 8) > 256) return (int)hipErrorInvalidValue;
-  const int nb = (HW + STATS_ROWS - 1) / STATS_ROWS;
-  hipLaunchKernelGGL(channel_stats_partial_kernel, dim3(nb, N), dim3(256), 0, stream, (const bf16*)x, HW, C, partial);
+  const int rows = stats_rows(N, HW, C);
+  const int nb = (HW + rows - 1) / rows;
+  hipLaunchKernelGGL(channel_stats_partial_kernel, dim3(nb, N), dim3(256), 0, stream, (const bf16*)x, HW, C, partial,
+                     rows);
   hipLaunchKernelGGL(channel_stats_final_kernel, dim3((2 * C + 7) / 8, N), dim3(256), 0, stream, partial, N, nb, C,
                      stats);
   return (int)hipGetLastError();
 }
 
-extern "C" int jr_channel_stats_partials(int N, int HW) { return N * ((HW + STATS_ROWS - 1) / STATS_ROWS); }
+// an upper bound for both the bf16 path (adaptive rows) and jr_channel_stats_f32 (STATS_ROWS rows)
+extern "C" int jr_channel_stats_partials(int N, int HW, int C) {
+  if (C % 8 != 0 || C / 8 > 256) return N * ((HW + 3) / 4);
+  return N * ((HW + stats_rows(N, HW, C) - 1) / stats_rows(N, HW, C));
+}
 
 extern "C" int jr_channel_stats_final(const float* part, int N, int nb, int C, float* stats, hipStream_t stream) {
   hipLaunchKernelGGL(channel_stats_final_kernel, dim3((2 * C + 7) / 8, N), dim3(256), 0, stream, part, N, nb, C, stats);

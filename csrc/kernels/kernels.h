@@ -111,9 +111,9 @@ int jr_conv_forward(const ConvParams* p, int cfg, int epi, hipStream_t stream);
 // Instance/batch-norm statistics and normalisation.
 // ---------------------------------------------------------------------------
 // stats[n][c][2] = (sum, sumsq) over pixels of x (bf16 NHWC, C channels, contiguous), deterministic
-// two-pass reduction; `partial` must hold jr_channel_stats_partials(N, HW) * C * 2 floats.
+// two-pass reduction; `partial` must hold jr_channel_stats_partials(N, HW, C) * C * 2 floats.
 int jr_channel_stats(const void* x, int N, int HW, int C, float* stats, float* partial, hipStream_t stream);
-int jr_channel_stats_partials(int N, int HW);
+int jr_channel_stats_partials(int N, int HW, int C);
 // y = post( pre(xn) + rn ), xn = (x - mean_x) * rstd_x * gamma + beta (mode_x), rn likewise for res.
 // mode: 0 = identity, 1 = instance (stats per n), 2 = batch (stats summed over n).
 // relu bit 0: relu on xn before the residual add; bit 1: relu on the sum.
@@ -195,8 +195,8 @@ int jr_flow_gather_bwd(const float* taps, int tcs, int N, int h, int w, void* df
 // optional) -> relu (relu & 1)" whose output gradient is gout * [om > 0] (om optional: the
 // ReLU'd residual-block output): dy bf16, gres fp32 (optional) = gout * [om > 0]; red fp32
 // [N][C][2] = per-(n, c) (sum g, sum g*xhat) (the BN affine gradients), partial: workspace of
-// jr_norm_bwd_partials(N, HW) * C * 2 floats.  y / gout / om / dy / gres are [N][HW][C] dense.
-int jr_norm_bwd_partials(int N, int HW);
+// jr_norm_bwd_partials(N, HW, C) * C * 2 floats.  y / gout / om / dy / gres are [N][HW][C] dense.
+int jr_norm_bwd_partials(int N, int HW, int C);
 int jr_norm_bwd(const void* gout, const void* om, const void* y, const float* stats, int mode, const float* gamma,
                 const float* beta, int relu, int N, int HW, int C, float eps, float* red, float* partial, void* dy,
                 void* gres, int gres_bf16, hipStream_t stream);

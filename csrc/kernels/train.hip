@@ -304,14 +304,14 @@ __global__ __launch_bounds__(256) void norm_bwd_partial_kernel(const bf16* __res
                                                                const bf16* __restrict__ y, const float* __restrict__ st,
                                                                int mode, const float* __restrict__ gam,
                                                                const float* __restrict__ bet, int relu, int N, int HW,
-                                                               int C, float eps, float* __restrict__ part) {
+                                                               int C, float eps, float* __restrict__ part, int rows) {
   __shared__ float red[256][17];
   const int n = blockIdx.y;
   const int cg = C >> 3;
   const int tid = threadIdx.x;
   const int g8 = tid % cg, rg = tid / cg, nrg = 256 / cg;
-  const int r0 = blockIdx.x * NB_ROWS;
-  const int r1 = min(r0 + NB_ROWS, HW);
+  const int r0 = blockIdx.x * rows;
+  const int r1 = min(r0 + rows, HW);
   float s[8], q[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
@@ -662,16 +662,28 @@ extern "C" int jr_sum_iters(const void* a, const void* b, int T, long M, int Ca,
   return (int)hipGetLastError();
 }
 
-extern "C" int jr_norm_bwd_partials(int N, int HW) { return N * ((HW + NB_ROWS - 1) / NB_ROWS); }
+// rows per partial-reduction block: enough blocks (>= ~1024 over the batch) that the small deep-layer
+// maps are not latency-bound on a few dozen blocks, at most NB_ROWS, a multiple of the row groups
+static int norm_bwd_rows(int N, int HW, int C) {
+  const int nrg = 256 / (C / 8);
+  const int nb = std::max(1, (1024 + N - 1) / N);
+  const int r = (HW + nb - 1) / nb;
+  return std::min(NB_ROWS, std::max(nrg, (r + nrg - 1) / nrg * nrg));
+}
+
+extern "C" int jr_norm_bwd_partials(int N, int HW, int C) {
+  return N * ((HW + norm_bwd_rows(N, HW, C) - 1) / norm_bwd_rows(N, HW, C));
+}
 
 extern "C" int jr_norm_bwd(const void* gout, const void* om, const void* y, const float* stats, int mode,
                            const float* gamma, const float* beta, int relu, int N, int HW, int C, float eps,
                            float* red, float* partial, void* dy, void* gres, int gres_bf16, hipStream_t stream) {
   if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
   if (mode != 0) {
-    const int nb = (HW + NB_ROWS - 1) / NB_ROWS;
+    const int prow = norm_bwd_rows(N, HW, C);
+    const int nb = (HW + prow - 1) / prow;
     hipLaunchKernelGGL(norm_bwd_partial_kernel, dim3(nb, N), dim3(256), 0, stream, (const bf16*)gout,
-                       (const bf16*)om, (const bf16*)y, stats, mode, gamma, beta, relu, N, HW, C, eps, partial);
+                       (const bf16*)om, (const bf16*)y, stats, mode, gamma, beta, relu, N, HW, C, eps, partial, prow);
     hipLaunchKernelGGL(norm_bwd_final_kernel, dim3((2 * C + 7) / 8, N), dim3(256), 0, stream, partial, nb, C, red);
   }
   const int nrg = 256 / (C / 8);

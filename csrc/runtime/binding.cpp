@@ -470,7 +470,7 @@ static Launch make_norm_bwd(const TList& t, const IList& i, double eps, std::vec
     TORCH_CHECK(st.numel() >= (int64_t)N * C * 2, "norm_bwd: stats");
     check_f32(red, "red");
     TORCH_CHECK(red.numel() >= (int64_t)N * C * 2, "norm_bwd: red");
-    const int64_t need = (int64_t)jr_norm_bwd_partials(N, HW) * C * 2;
+    const int64_t need = (int64_t)jr_norm_bwd_partials(N, HW, C) * C * 2;
     if (!part.defined()) part = at::empty({need}, st.options());
     check_f32(part, "partial");
     TORCH_CHECK(part.numel() >= need, "norm_bwd: partial workspace too small");
@@ -1183,7 +1183,7 @@ static Launch make_stats(const TList& t, const IList& i, std::vector<at::Tensor>
   const int N = (int)i[0], HW = (int)i[1], C = (int)i[2];
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && cs(x) == C && x.numel() >= (int64_t)N * HW * C, "stats: shape");
   TORCH_CHECK(st.numel() >= (int64_t)N * C * 2, "stats: buffer too small");
-  const int64_t need = (int64_t)jr_channel_stats_partials(N, HW) * C * 2;
+  const int64_t need = (int64_t)jr_channel_stats_partials(N, HW, C) * C * 2;
   // (A one-launch form -- the last block per image reducing the partials behind
   // an integer ticket -- measured 0.9 ms/step SLOWER at raft_large batch 4: the
   // device-scope release fence before each block's ticket writes back the
@@ -1446,7 +1446,7 @@ static Launch make_stats_f32(const TList& t, const IList& i, std::vector<at::Ten
   check_f32(x, "x");
   TORCH_CHECK(C % 4 == 0 && C <= 1024 && cs(x) == C && x.numel() >= (int64_t)N * HW * C, "stats_f32: shape");
   check_f32_min(st, "stats", (int64_t)N * C * 2);
-  const int64_t need = (int64_t)jr_channel_stats_partials(N, HW) * C * 2;
+  const int64_t need = (int64_t)jr_channel_stats_partials(N, HW, C) * C * 2;
   if (!part.defined()) part = at::empty({need}, st.options());
   check_f32_min(part, "partial", need);
   if (keep) for (auto& v : {x, st, part}) keep->push_back(v);
