@@ -2,7 +2,7 @@
 # Round 4 rehearsal of the driver's round-end checks: the whole GPU suite in one process, smoke(), bench.py
 set -o pipefail
 export TMPDIR=/tmp
-o=gpurun_out/r4_final
+o=gpurun_out/${OUT:-r4_final}
 mkdir -p $o
 timeout -k 10 1500 python -u -m pytest tests/ -x -q -m gpu --timeout 600 --timeout-method thread > $o/gpu_tests.txt 2>&1 || { tail -30 $o/gpu_tests.txt; exit 1; }
 tail -2 $o/gpu_tests.txt
