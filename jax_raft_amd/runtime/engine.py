@@ -247,6 +247,13 @@ class RaftEngine:
         self.device = torch.device(device)
         self.use_graph = use_graph
         self.copy_output = copy_output
+        # host gate: a graph replay is launched only after the previous call's work has finished
+        # (the host waits on its completion event).  Replays enqueued behind a still-running
+        # one-lane forward start measurably later on this ROCm: batch-1 raft_large 193 -> 220-226
+        # pairs/s for back-to-back forwards, 205 -> 228 pipelined; no change at batch 4 (lanes).
+        # profiles/r4_host_gate.txt.  JR_HOST_GATE=0 disables it.
+        self.host_gate = os.environ.get("JR_HOST_GATE", "1") != "0"
+        self._done_ev: Optional[torch.cuda.Event] = None
         self.corr_dtype = corr_dtype
         self.autotune = autotune
         self._specs: Dict[str, ConvSpec] = {}
@@ -1354,6 +1361,7 @@ class RaftEngine:
         if st is None:
             st = self._build(B, H, W, num_flow_updates, bool(return_all_iters))
             self._states[key] = st
+        self._gate()
         st.inp1.copy_(image1)
         st.inp2.copy_(image2)
         fresh = self.copy_output and st.slot_ok
@@ -1374,9 +1382,21 @@ class RaftEngine:
                     p0.merge_add(plan, num_flow_updates)
                 p0.merge_finish(num_flow_updates)
             p0.replay_pipelined()
+        self._mark()
         if fresh:
             return out
         return st.out.clone() if self.copy_output else st.out
+
+    def _gate(self) -> None:
+        """Wait (host) for the previous forward / pipelined call (see ``host_gate``)."""
+        if self.host_gate and self._done_ev is not None:
+            self._done_ev.synchronize()
+
+    def _mark(self) -> None:
+        if self.host_gate and self.device.type == "cuda":
+            if self._done_ev is None:
+                self._done_ev = torch.cuda.Event()
+            self._done_ev.record()
 
     @staticmethod
     def _point_slot(st: _PlanState, out: torch.Tensor) -> None:
@@ -1436,6 +1456,7 @@ class RaftEngine:
             pp = self._pp = dict(key=key, n=0, pending=None)
         slot = pp["n"] & 1
         st = self._slot_state(key, slot)
+        self._gate()
         st.inp1.copy_(image1)
         st.inp2.copy_(image2)
         prev = pp["pending"]
@@ -1453,6 +1474,7 @@ class RaftEngine:
                 pst.plan.capture_pipelined(st.plan, n)
             pst.plan.replay_pipelined()
             result = out if fresh else (pst.out.clone() if self.copy_output else pst.out)
+        self._mark()
         pp["pending"] = slot
         pp["n"] += 1
         return result
