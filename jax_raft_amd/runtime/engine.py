@@ -247,11 +247,13 @@ class RaftEngine:
         self.device = torch.device(device)
         self.use_graph = use_graph
         self.copy_output = copy_output
-        # host gate: a graph replay is launched only after the previous call's work has finished
-        # (the host waits on its completion event).  Replays enqueued behind a still-running
-        # one-lane forward start measurably later on this ROCm: batch-1 raft_large 193 -> 220-226
-        # pairs/s for back-to-back forwards, 205 -> 228 pipelined; no change at batch 4 (lanes).
-        # profiles/r4_host_gate.txt.  JR_HOST_GATE=0 disables it.
+        # host gate: the graph replay of a forward with >= GATE_MIN_ITERS iterations is launched
+        # only after the previous call's work has finished (the host waits on its completion
+        # event).  A long replay enqueued behind a still-running one runs slower on this ROCm:
+        # batch 1 raft_large 32 it 208-213 -> 261 pairs/s, raft_small 32 it 334-337 -> 435-436,
+        # batch 4 387-393 -> 401-402; short forwards lose (raft_small 12 it 713-754 -> 646-698),
+        # where the exposed host launch is a larger share.  profiles/r4_host_gate.txt;
+        # JR_HOST_GATE=0 disables it.
         self.host_gate = os.environ.get("JR_HOST_GATE", "1") != "0"
         self._done_ev: Optional[torch.cuda.Event] = None
         self.corr_dtype = corr_dtype
@@ -1361,12 +1363,12 @@ class RaftEngine:
         if st is None:
             st = self._build(B, H, W, num_flow_updates, bool(return_all_iters))
             self._states[key] = st
-        self._gate()
         st.inp1.copy_(image1)
         st.inp2.copy_(image2)
         fresh = self.copy_output and st.slot_ok
         out = torch.empty_like(st.out) if fresh else st.out
         self._point_slot(st, out)
+        self._gate(num_flow_updates)   # after the host-side preparation: only the launch waits
         if st.cp is not None:
             self._forward_cp(st, num_flow_updates)
         elif len(st.plans) == 1 or not self.use_graph:
@@ -1387,9 +1389,11 @@ class RaftEngine:
             return out
         return st.out.clone() if self.copy_output else st.out
 
-    def _gate(self) -> None:
+    GATE_MIN_ITERS = 20
+
+    def _gate(self, n_iters: int) -> None:
         """Wait (host) for the previous forward / pipelined call (see ``host_gate``)."""
-        if self.host_gate and self._done_ev is not None:
+        if self.host_gate and self._done_ev is not None and n_iters >= self.GATE_MIN_ITERS:
             self._done_ev.synchronize()
 
     def _mark(self) -> None:
@@ -1456,7 +1460,6 @@ class RaftEngine:
             pp = self._pp = dict(key=key, n=0, pending=None)
         slot = pp["n"] & 1
         st = self._slot_state(key, slot)
-        self._gate()
         st.inp1.copy_(image1)
         st.inp2.copy_(image2)
         prev = pp["pending"]
@@ -1464,6 +1467,7 @@ class RaftEngine:
         if prev is None:
             if st.plan.captured_part_iters(0) != n:
                 st.plan.capture_part(0, n)
+            self._gate(n)
             st.plan.replay_part(0)
         else:
             pst = self._slot_state(key, prev)
@@ -1472,6 +1476,7 @@ class RaftEngine:
             self._point_slot(pst, out)
             if pst.plan.pipelined_iters(st.plan) != n:
                 pst.plan.capture_pipelined(st.plan, n)
+            self._gate(n)
             pst.plan.replay_pipelined()
             result = out if fresh else (pst.out.clone() if self.copy_output else pst.out)
         self._mark()

@@ -466,3 +466,30 @@ def test_grouped_corr_flow_conv_is_bitwise(factory, cfg, monkeypatch):
     b = m1(i1, i2, num_flow_updates=4, streams=False)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_host_gate_keeps_results(pipelined):
+    """The engine's host gate (launch a long forward's replay only after the previous call
+    finished, engine.py:_gate) changes timing only: back-to-back gated calls return the
+    flows of ungated calls bitwise, and every returned tensor stays intact."""
+    model, _ = raft_small()
+    model = model.cuda().eval()
+    pairs = [tuple(t.cuda() for t in _inputs(1, 128, 128, seed=s)) for s in (5, 6, 7)]
+    n = 24   # >= RaftEngine.GATE_MIN_ITERS: the gate is active
+    outs = {}
+    for gate in (True, False):
+        eng = model.engine(torch.device("cuda"))
+        eng.host_gate = gate
+        assert n >= eng.GATE_MIN_ITERS
+        if pipelined:
+            res = [eng.pipelined(a, b, n) for a, b in pairs]
+            res = res[1:] + [eng.flush()]
+        else:
+            res = [eng.forward(a, b, n) for a, b in pairs]
+        torch.cuda.synchronize()
+        outs[gate] = res
+    for x, y in zip(outs[True], outs[False]):
+        assert x.shape == (n, 1, 128, 128, 2)
+        assert torch.equal(x, y)
+    assert not torch.equal(outs[True][0], outs[True][1])
