@@ -1336,6 +1336,25 @@ class RaftEngine:
             plan.set_defer(1)
             upsample(stride, mask_from_fm=fm is not None and self.has_mask)
             plan.set_defer(0)
+        elif (self._cf1_w is not None and tuple(c1k.shape[:2]) == (7, 7) and B < self.AUTO_STREAMS_MIN_BATCH
+              and os.environ.get("JR_FO_MERGED", "1") != "0"):
+            # final-only below batch 4, the one-lane order of the all-iterations loop: the flow update
+            # fused into the next lookup, the 7x7 flow conv in the merged grid (its bilinear half
+            # writes the single output slot every iteration; the epilogue's upsampling overwrites
+            # it), convflow2 grouped with convcorr2.  Batch 1: 239.5 -> 244.6 pairs/s; batch 4
+            # loses (414.8 -> 402.7), keeps the order below (profiles/r4_host_gate.txt)
+            plan.set_segment(1)
+            lane(main)
+            lookup(with_update=True)
+            c = me.convflow1.layers_0
+            kh, kw_, _, co = c.kernel.shape
+            plan.add_flowin_dual([flow8, self._cf1_w, self._cf1_b, f1, flow32, out, st.out_slot],
+                                 [B, h, w, 2, kh, kw_, c.padding[0], c.padding[1], co, 1, 0, 1, 0, out_off, 0], 1.0)
+            motion_and_gru(wait_flow=False, wait_mask=False, flow2=True)
+            flow_head()
+            plan.set_segment(2)           # epilogue: the last update, then the final flow upsampled once
+            flow_update()
+            upsample(0, mask_from_fm=False)
         else:
             plan.set_segment(1)
             lane(main)
