@@ -319,3 +319,18 @@ def test_prologue_lanes_at_batch_one(fake, monkeypatch, arch):
     monkeypatch.setenv("JR_PRO_LANES", "0")
     eng, p = _plan(arch, 1)
     assert {ln for s, ln, d, op, a in p.ops} == {0}
+
+
+@pytest.mark.parametrize("factory", [raft_large, raft_small])
+def test_final_only_schedule_batch1(factory, fake):
+    """Final-only below batch 4: the all-iterations one-lane order -- the update inside the
+    lookup, the 7x7 flow conv in the merged grid whose bilinear half writes the single output
+    slot (iteration stride 0), the last update + the one upsampling in the epilogue."""
+    eng, p = _plan(factory, 1, all_iters=False)
+    ops = p.names(1)
+    assert ops[0] == "lookup" and ops[1] == "flowin_dual" and "flow_taps" not in ops
+    assert "convex_head" not in ops and "conv_direct" not in ops
+    ints = [a for s, ln, d, op, a in p.ops if s == 1 and op == "flowin_dual"][0][1]
+    assert len(ints) == 15 and ints[11] == 1 and ints[12] == 0   # bilinear, iteration stride 0
+    ep = p.names(2)   # (raft_large: + the mask head's 3x3 conv before the convex head)
+    assert ep[0] == "flow_taps" and ep[-1] == ("convex_head" if factory is raft_large else "upsample_bilinear")
