@@ -271,22 +271,30 @@ def run_inference(ctx: Ctx, model, *, B: int, H: int, W: int, iters: int, steps:
 
 
 def run_sync_latency(ctx: Ctx, model, *, H: int, W: int, iters: int, steps: int, warmup: int, seed: int,
-                     engine_kw: dict) -> dict:
+                     engine_kw: dict, raw: bool = False) -> dict:
     """The reference's own FPS protocol (validate_sintel.py:185-188,201-203), batch 1, one pair
     at a time: host->device copy of the pair (from pageable host memory, like numpy inputs),
     the forward with all ``iters`` upsampled predictions, then a synchronisation on the
     result -- no overlap of consecutive pairs at all.  FPS = 1 / mean latency (x ranks for
-    N > 1, each rank timing its own pairs)."""
+    N > 1, each rank timing its own pairs).  ``raw``: the pair is raw uint8 H x W frames (any
+    size: Sintel's 436 x 1024), normalised and replicate-padded to /8 on the device by the
+    engine's prep kernel, the flows cropped back (validate_sintel.py:177-191 on the device)."""
     dev = ctx.dev
     g = torch.Generator().manual_seed(seed + ctx.rank)
-    pairs = [(torch.rand(1, H, W, 3, generator=g) * 2 - 1, torch.rand(1, H, W, 3, generator=g) * 2 - 1)
-             for _ in range(4)]
+    if raw:
+        pairs = [(torch.randint(0, 256, (1, H, W, 3), generator=g, dtype=torch.uint8),
+                  torch.randint(0, 256, (1, H, W, 3), generator=g, dtype=torch.uint8)) for _ in range(4)]
+        h2d = lambda x: x   # noqa: E731 -- the engine copies host frames straight into its plan input
+    else:
+        pairs = [(torch.rand(1, H, W, 3, generator=g) * 2 - 1, torch.rand(1, H, W, 3, generator=g) * 2 - 1)
+                 for _ in range(4)]
+        h2d = lambda x: x.to(dev)   # noqa: E731
     err, lat = None, []
     try:
         eng = model.engine(dev, **dict(engine_kw, split=1))
         for i in range(warmup):
             a, b = pairs[i % 4]
-            eng.forward(a.to(dev), b.to(dev), iters)[-1]
+            eng.forward(h2d(a), h2d(b), iters)[-1]
         torch.cuda.synchronize(dev)
     except Exception as e:  # noqa: BLE001
         err = e
@@ -295,7 +303,7 @@ def run_sync_latency(ctx: Ctx, model, *, H: int, W: int, iters: int, steps: int,
     for i in range(steps):
         a, b = pairs[i % 4]
         t0 = time.perf_counter()
-        flow = eng.forward(a.to(dev), b.to(dev), iters)[-1]
+        flow = eng.forward(h2d(a), h2d(b), iters)[-1]
         torch.cuda.synchronize(dev)
         lat.append(time.perf_counter() - t0)
         assert flow.shape == (1, H, W, 2)
@@ -303,11 +311,14 @@ def run_sync_latency(ctx: Ctx, model, *, H: int, W: int, iters: int, steps: int,
     mean = sum(lat) / len(lat)
     mean_max = ctx.max_all(mean)
     lat.sort()
+    proto = ("per pair: raw uint8 frames H2D (pageable) + on-device normalise / replicate pad to /8 + forward "
+             "(all iterations upsampled) + crop + sync; no cross-pair overlap (validate_sintel.py:177-191)" if raw else
+             "per pair: H2D (pageable) + forward (all iterations upsampled) + sync; no cross-pair overlap "
+             "(validate_sintel.py:185-188)")
     return dict(value=round(ctx.world / mean_max, 3), latency_ms_mean=round(1000 * mean_max, 3),
                 latency_ms_p50=round(1000 * lat[len(lat) // 2], 3),
                 latency_ms_p99=round(1000 * lat[min(len(lat) - 1, int(0.99 * len(lat)))], 3),
-                steps=steps, warmup=warmup, protocol="per pair: H2D (pageable) + forward (all iterations "
-                "upsampled) + sync; no cross-pair overlap (validate_sintel.py:185-188)")
+                steps=steps, warmup=warmup, protocol=proto)
 
 
 def _gather_ms(ctx: Ctx, gat: FlowGather, flows, shape) -> float:
@@ -431,6 +442,8 @@ def main():
         # hires_b1: 1088x1920 frames (a 136x240 feature map), batch 1, 32 iterations
         plan = [("b1_fps", "raft_large", 32, BASELINE_FPS, "bf16", "stream", (H, W)),
                 ("b1_sync", "raft_large", 32, BASELINE_FPS, "bf16", "sync", (H, W)),
+                # raw 436 x 1024 uint8 Sintel-size frames, prepared on the device
+                ("b1_sync_u8", "raft_large", 32, BASELINE_FPS, "bf16", "sync_u8", (H - 4, W)),
                 ("small_b1_fps_32it", "raft_small", 32, BASELINE_SMALL_FPS, "bf16", "stream", (H, W)),
                 ("small_b1_sync_32it", "raft_small", 32, BASELINE_SMALL_FPS, "bf16", "sync", (H, W)),
                 ("small_b1_fps_12it", "raft_small", 12, None, "bf16", "stream", (H, W)),
@@ -442,9 +455,9 @@ def main():
             mul = 3 if arch == "raft_small" else 1
             try:
                 m = (raft_large if arch == "raft_large" else raft_small)(seed=0)[0].to(ctx.dev).eval()
-                if proto == "sync":
+                if proto in ("sync", "sync_u8"):
                     r = run_sync_latency(ctx, m, H=eh, W=ew, iters=it, steps=ks * mul, warmup=kw_ * mul,
-                                         seed=99, engine_kw=dict(engine_kw, precision=prec))
+                                         seed=99, engine_kw=dict(engine_kw, precision=prec), raw=proto == "sync_u8")
                 else:
                     r = run_inference(ctx, m, B=1, H=eh, W=ew, iters=it, steps=ks * mul, warmup=kw_ * mul,
                                       final_only=False, gather=not args.no_gather, seed=99,

@@ -266,6 +266,60 @@ __global__ void prep_images_s2d_kernel(const float* __restrict__ i1, const float
   *(bf16x8*)(out + idx * 16 + 8) = o1;
 }
 
+// Device-side input preparation of raw frames (the host protocol of the reference is
+// validate_sintel.py:177-183 -- x / 255 * 2 - 1, InputPadder('sintel') replicate padding to /8,
+// NCHW -> NHWC -- and demo.py:7-10): uint8 NHWC frames of any size H0 x W0 are normalised through
+// a 256-entry fp32 table (computed on the host by the reference's own expression, so the values
+// are bitwise those of the host path) and replicate-padded to the plan's H x W (pt / pl rows /
+// columns before the frame: source pixel = clamp(y - pt, 0, H0 - 1), clamp(x - pl, 0, W0 - 1)),
+// then written in the layout of prep_images(_s2d)_kernel above.  One thread per output pixel
+// (S2D: per 2 x 2 block); the table is staged in LDS.
+template <bool S2D>
+__global__ void prep_u8_kernel(const unsigned char* __restrict__ i1, const unsigned char* __restrict__ i2,
+                               const float* __restrict__ lut, int B, int H0, int W0, int H, int W, int pt, int pl,
+                               bf16* __restrict__ out) {
+  __shared__ float tab[256];
+  tab[threadIdx.x] = lut[threadIdx.x];   // blockDim.x == 256
+  __syncthreads();
+  constexpr int R = S2D ? 2 : 1;
+  const int Hq = H / R, Wq = W / R;
+  const long per = (long)Hq * Wq;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= 2L * B * per) return;
+  const long n = idx / per;
+  const int r = (int)(idx - n * per), Y = r / Wq, X = r - (r / Wq) * Wq;
+  const unsigned char* img = n < B ? i1 + n * (long)H0 * W0 * 3 : i2 + (n - B) * (long)H0 * W0 * 3;
+  float v[12];
+#pragma unroll
+  for (int sy = 0; sy < R; ++sy) {
+    const int y = min(max(R * Y + sy - pt, 0), H0 - 1);
+#pragma unroll
+    for (int sx = 0; sx < R; ++sx) {
+      const int x = min(max(R * X + sx - pl, 0), W0 - 1);
+      const unsigned char* px = img + ((long)y * W0 + x) * 3;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[(sy * R + sx) * 3 + c] = tab[px[c]];
+    }
+  }
+  if (S2D) {
+    bf16x8 o0, o1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o0[k] = f2bf(v[k]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o1[k] = f2bf(v[8 + k]);
+#pragma unroll
+    for (int k = 4; k < 8; ++k) o1[k] = f2bf(0.f);
+    *(bf16x8*)(out + idx * 16) = o0;
+    *(bf16x8*)(out + idx * 16 + 8) = o1;
+  } else {
+    bf16x8 o;
+    o[0] = f2bf(v[0]); o[1] = f2bf(v[1]); o[2] = f2bf(v[2]);
+#pragma unroll
+    for (int k = 3; k < 8; ++k) o[k] = f2bf(0.f);
+    *(bf16x8*)(out + idx * 8) = o;
+  }
+}
+
 __global__ void init_coords_kernel(float* __restrict__ coords, int B, int h, int w) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long total = (long)B * h * w;
@@ -390,6 +444,21 @@ extern "C" int jr_prep_images_s2d(const float* img1, const float* img2, int B, i
   const long total = 2L * B * (H / 2) * (W / 2);
   hipLaunchKernelGGL(prep_images_s2d_kernel, dim3(nblk(total, 256)), dim3(256), 0, stream, img1, img2, B, H, W,
                      (bf16*)out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jr_prep_u8(const void* img1, const void* img2, const float* lut, int B, int H0, int W0, int H, int W,
+                          int pt, int pl, int s2d, void* out, hipStream_t stream) {
+  if (H0 < 1 || W0 < 1 || H < H0 || W < W0 || pt < 0 || pl < 0 || (s2d && ((H | W) & 1))) return (int)hipErrorInvalidValue;
+  const long total = 2L * B * (s2d ? (long)(H / 2) * (W / 2) : (long)H * W);
+  const auto* a = (const unsigned char*)img1;
+  const auto* b = (const unsigned char*)img2;
+  if (s2d)
+    hipLaunchKernelGGL(prep_u8_kernel<true>, dim3(nblk(total, 256)), dim3(256), 0, stream, a, b, lut, B, H0, W0, H, W,
+                       pt, pl, (bf16*)out);
+  else
+    hipLaunchKernelGGL(prep_u8_kernel<false>, dim3(nblk(total, 256)), dim3(256), 0, stream, a, b, lut, B, H0, W0, H,
+                       W, pt, pl, (bf16*)out);
   return (int)hipGetLastError();
 }
 

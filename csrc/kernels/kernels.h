@@ -256,6 +256,9 @@ int jr_seq_loss_bwd(const float* pred, const float* gt, const float* valid, long
 int jr_prep_images(const float* img1, const float* img2, int B, int H, int W, void* out, hipStream_t stream);
 // 2x2 space-to-depth prep: out bf16 [2B][H/2][W/2][16] (see elementwise.hip:prep_images_s2d_kernel)
 int jr_prep_images_s2d(const float* img1, const float* img2, int B, int H, int W, void* out, hipStream_t stream);
+// uint8 NHWC frames (any size) -> normalised, replicate-padded bf16 encoder input (elementwise.hip)
+int jr_prep_u8(const void* img1, const void* img2, const float* lut, int B, int H0, int W0, int H, int W, int pt,
+               int pl, int s2d, void* out, hipStream_t stream);
 // coords[b][y][x] = (x, y); flow32 = 0
 int jr_init_coords(float* coords, int B, int h, int w, hipStream_t stream);
 // im2col of x (bf16 NHWC, channel slice) into col [N*OH*OW][kpad] in the packed-weight K order

@@ -1223,7 +1223,34 @@ static Launch make_norm_act(const TList& t, const IList& i, double eps, std::vec
 
 // ---------------------------------------------------------------------- misc
 // t = [img1, img2, out], i = [B, H, W]
+// uint8 frames: t = [img1, img2 (uint8 [B][H0][W0][3]), out, lut (fp32 [256])],
+// i = [B, H, W, s2d, H0, W0, pt, pl] (K14: normalise + replicate pad + layout, jr_prep_u8)
+static Launch make_prep_u8(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  at::Tensor a = opt(t, 0), b = opt(t, 1), out = opt(t, 2), lut = opt(t, 3);
+  TORCH_CHECK(a.defined() && b.defined() && a.scalar_type() == at::kByte && b.scalar_type() == at::kByte &&
+                  a.is_cuda() && b.is_cuda() && a.is_contiguous() && b.is_contiguous(), "prep: uint8 frames");
+  check_bf16(out, "out"); check_f32(lut, "lut");
+  TORCH_CHECK(i.size() == 8 && lut.numel() == 256, "prep: uint8 frames need [B, H, W, s2d, H0, W0, pt, pl] and a 256 table");
+  const int B = (int)i[0], H = (int)i[1], W = (int)i[2], s2d = (int)i[3], H0 = (int)i[4], W0 = (int)i[5];
+  const int pt = (int)i[6], pl = (int)i[7];
+  TORCH_CHECK(H0 >= 1 && W0 >= 1 && H >= H0 && W >= W0 && pt >= 0 && pl >= 0 && pt <= H - H0 && pl <= W - W0,
+              "prep: padded size / offsets");
+  TORCH_CHECK(a.numel() == (int64_t)B * H0 * W0 * 3 && b.numel() == a.numel(), "prep: uint8 frame shape");
+  if (s2d) {
+    TORCH_CHECK(H % 2 == 0 && W % 2 == 0 && out.numel() >= 2LL * B * H * W * 4 && cs(out) == 16, "prep: s2d output");
+  } else {
+    TORCH_CHECK(out.numel() >= 2LL * B * H * W * 8 && cs(out) == 8, "prep: output");
+  }
+  if (keep) for (auto& v : {a, b, out, lut}) keep->push_back(v);
+  const void* ap = a.data_ptr();
+  const void* bp = b.data_ptr();
+  const float* lp = lut.data_ptr<float>();
+  void* op = out.data_ptr();
+  return [=](hipStream_t s, int) { return jr_prep_u8(ap, bp, lp, B, H0, W0, H, W, pt, pl, s2d, op, s); };
+}
+
 static Launch make_prep(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
+  if (opt(t, 0).defined() && opt(t, 0).scalar_type() == at::kByte) return make_prep_u8(t, i, keep);
   at::Tensor a = opt(t, 0), b = opt(t, 1), out = opt(t, 2);
   check_f32(a, "img1"); check_f32(b, "img2"); check_bf16(out, "out");
   const int B = (int)i[0], H = (int)i[1], W = (int)i[2];

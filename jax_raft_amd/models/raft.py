@@ -51,6 +51,9 @@ _MODELS_URLS = {
 def _as_tensor(x) -> torch.Tensor:
     if isinstance(x, torch.Tensor):
         return x
+    a = np.asarray(x)
+    if a.dtype == np.uint8:   # raw frames (normalised + padded by the engine / forward)
+        return torch.from_numpy(np.ascontiguousarray(a))
     return torch.as_tensor(np.asarray(x, dtype=np.float32))
 
 
@@ -81,7 +84,12 @@ class RAFT(nn.Module):
         image1, image2 = _as_tensor(image1), _as_tensor(image2)
         B, H, W, _ = image1.shape
         assert (H, W) == tuple(image2.shape[-3:-1]), "input images should have the same shape"
+        if image1.dtype == torch.uint8:
+            return self._forward_u8(image1, image2, train, num_flow_updates, return_all_iters, engine_kw)
         assert (H % 8 == 0) and (W % 8 == 0), "input image H and W should be divisible by 8"
+        dev = self._param_device()
+        if dev.type == "cuda" and not image1.is_cuda:   # host arrays / tensors for a model on the GPU
+            image1, image2 = image1.to(dev), image2.to(dev)
         autograd = engine_kw.pop("autograd", False)
         fused = engine_kw.pop("fused", None)
         if image1.is_cuda:
@@ -99,6 +107,37 @@ class RAFT(nn.Module):
             with torch.no_grad():
                 return self.forward_reference(image1, image2, False, num_flow_updates, return_all_iters)
         return self.forward_reference(image1, image2, train, num_flow_updates, return_all_iters)
+
+    def _forward_u8(self, image1, image2, train, num_flow_updates, return_all_iters, engine_kw):
+        """Raw uint8 NHWC frames of any size: the reference's input protocol
+        (``scripts/validate_sintel.py:177-191``: x / 255 * 2 - 1, InputPadder('sintel') replicate
+        padding to /8, unpad of the flows) -- on the GPU inside the engine's prep kernel, elsewhere
+        (CPU golden path, training, models the engine cannot lower) with framework ops."""
+        dev = self._param_device()
+        if dev.type == "cuda" and not (train or engine_kw.get("autograd")) and self._lowering_error is None:
+            # host frames go straight into the plan's uint8 input buffers (one H2D copy of 1/4 the
+            # bytes of normalised fp32 frames)
+            eng = self._try_engine(dev, {k: v for k, v in engine_kw.items() if k not in ("autograd", "fused")})
+            if eng is not None:
+                return eng.forward(image1, image2, num_flow_updates, return_all_iters=return_all_iters)
+        if dev.type == "cuda" and not image1.is_cuda:
+            image1, image2 = image1.to(dev), image2.to(dev)
+        from ..runtime.engine import sintel_pad, u8_table
+
+        H0, W0 = image1.shape[1:3]
+        pt, pb, pl, pr = sintel_pad(H0, W0)
+        lut = u8_table(image1.device)
+
+        def prep(x):
+            x = lut[x.long()].permute(0, 3, 1, 2)
+            return torch.nn.functional.pad(x, [pl, pr, pt, pb], mode="replicate").permute(0, 2, 3, 1).contiguous()
+
+        out = self.forward(prep(image1), prep(image2), train, num_flow_updates, return_all_iters, **engine_kw)
+        return out[:, :, pt:pt + H0, pl:pl + W0]
+
+    def _param_device(self) -> torch.device:
+        p = next(self.parameters(), None)
+        return p.device if p is not None else torch.device("cpu")
 
     def _try_engine(self, device, engine_kw):
         """The native engine, or None (remembering why) when it cannot lower this model."""
@@ -183,6 +222,7 @@ class RAFT(nn.Module):
         eng = self._engines.get(key)
         if eng is None:
             eng = RaftEngine(self, device, **kw)
+            eng._hold_model_weakly()   # no model <-> engine cycle: the plans die with the model
             self._engines[key] = eng
         return eng
 

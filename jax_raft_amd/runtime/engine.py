@@ -30,6 +30,8 @@ iteration: K = 5 x 256 instead of 5 x 384 for raft_large.
 from __future__ import annotations
 
 import os
+import weakref
+from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -143,6 +145,29 @@ class _PlanState:
     slot_ptr: int = 0
     # context parallelism: {slabs, nq (padded slab pixels per image), local, corr} (see _gather_corr)
     cp: Optional[dict] = None
+    # raw uint8 frames (K14): (H0, W0, pt, pl) of the frames inside the padded plan size, else None
+    src: Optional[Tuple[int, int, int, int]] = None
+
+
+def sintel_pad(H0: int, W0: int) -> Tuple[int, int, int, int]:
+    """InputPadder('sintel') of the reference (``scripts/validate_sintel.py:23-31``): the rows /
+    columns (top, bottom, left, right) that replicate-pad an H0 x W0 frame to multiples of 8."""
+    ph = (((H0 // 8) + 1) * 8 - H0) % 8
+    pw = (((W0 // 8) + 1) * 8 - W0) % 8
+    return ph // 2, ph - ph // 2, pw // 2, pw - pw // 2
+
+
+_U8_LUT: Dict[str, torch.Tensor] = {}
+
+
+def u8_table(device) -> torch.Tensor:
+    """x / 255 * 2 - 1 for x = 0..255, evaluated on the host in fp32 exactly as the reference's
+    input protocol (validate_sintel.py:177-178, demo.py:9) -- the device kernel looks values up."""
+    key = str(device)
+    t = _U8_LUT.get(key)
+    if t is None:
+        t = _U8_LUT[key] = (torch.arange(256, dtype=torch.float32) / 255.0 * 2.0 - 1.0).to(device)
+    return t
 
 
 class RaftEngine:
@@ -243,7 +268,12 @@ class RaftEngine:
         self._taps_epi_w = None
         self._cc1_w = self._cc1_b = None
         self._halo_w: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}   # GRU gi -> gru_halo (wa, wb)
-        self.model = model
+        # the model: held strongly by an engine built directly, weakly by one the model caches itself
+        # (RAFT.engine -> _hold_model_weakly): model._engines -> engine -> model would be a reference
+        # cycle, and every plan of a cycle-held engine (hipGraphs, 64 events, lane streams, pyramid
+        # buffers) would outlive the model until a full garbage collection
+        self._model_strong = model
+        self._model_ref = None
         self.device = torch.device(device)
         self.use_graph = use_graph
         self.copy_output = copy_output
@@ -262,12 +292,124 @@ class RaftEngine:
         self.arch = tunedb.gpu_arch(self.device)
         self.chosen_cfgs: Dict[str, Optional[int]] = {}   # conv spec name -> tile config of the last plan built
         self._sources: Dict[str, callable] = {}
-        self._states: Dict[Tuple[int, int, int, int], _PlanState] = {}
+        # built plans, least recently used first; at most max_plans key groups (a forward's plan and
+        # its pipelined() slots are one group) -- a long-lived serving / eval process over many input
+        # shapes keeps a bounded set; release() drops them all
+        self._states: "OrderedDict[tuple, _PlanState]" = OrderedDict()
         self._sig = None
         self._sig_modules = None
         self._pp = None   # pipelined(): {key, n, pending slot}
         self._analyse()
         self._pack()
+
+    @property
+    def model(self):
+        m = self._model_strong if self._model_strong is not None else self._model_ref()
+        if m is None:
+            raise ReferenceError("RaftEngine: its model has been garbage-collected")
+        return m
+
+    def _hold_model_weakly(self) -> None:
+        """Called by the model that caches this engine (``RAFT.engine``): keep a weak reference."""
+        if self._model_strong is not None:
+            self._model_ref = weakref.ref(self._model_strong)
+            self._model_strong = None
+
+    # ------------------------------------------------------------ plan cache
+    max_plans = 8   # key groups kept (an instance attribute may lower / raise it)
+
+    @staticmethod
+    def _group(key: tuple) -> tuple:
+        return key[:-2] if len(key) > 2 and key[-2] == "pslot" else key
+
+    # raw uint8 frames are prepared on the device by the plan's prep kernel (an engine without that
+    # path normalises + pads them with framework ops first: the fp32 engine)
+    _native_u8 = True
+
+    def _key(self, image1: torch.Tensor, image2: torch.Tensor, n_iters: int, all_iters: bool) -> tuple:
+        """Plan key of one call: (B, H, W, n, all) for float NHWC images in [-1, 1] with H, W % 8 == 0;
+        + ("u8", H0, W0, pt, pl) for uint8 NHWC frames of any size, whose plan runs at the padded
+        size (InputPadder 'sintel' semantics) and returns the flows cropped back to H0 x W0."""
+        B, H, W, C = image1.shape
+        assert C == 3, "images must be NHWC with 3 channels"
+        assert tuple(image2.shape) == tuple(image1.shape), "input images should have the same shape"
+        if image1.dtype == torch.uint8:
+            assert image2.dtype == torch.uint8, "both frames must be uint8"
+            pt, pb, pl, pr = sintel_pad(H, W)
+            return (B, H + pt + pb, W + pl + pr, n_iters, bool(all_iters), "u8", H, W, pt, pl)
+        assert H % 8 == 0 and W % 8 == 0, "input image H and W should be divisible by 8"
+        return (B, H, W, n_iters, bool(all_iters))
+
+    def _build_key(self, key: tuple) -> _PlanState:
+        src = tuple(key[6:10]) if len(key) >= 10 and key[5] == "u8" else None
+        return self._build(*key[:5], src=src)
+
+    @staticmethod
+    def _crop(st: _PlanState, out: torch.Tensor) -> torch.Tensor:
+        if st.src is None:
+            return out
+        H0, W0, pt, pl = st.src
+        return out[:, :, pt:pt + H0, pl:pl + W0]
+
+    def _host_u8(self, image1, image2):
+        """uint8 frames -> float [-1, 1], replicate-padded to /8 with framework ops on the device
+        (engines without the native u8 prep); returns (img1, img2, crop)."""
+        B, H0, W0, _ = image1.shape
+        pt, pb, pl, pr = sintel_pad(H0, W0)
+        lut = u8_table(self.device)
+
+        def one(x):
+            x = lut[x.to(self.device).long()].permute(0, 3, 1, 2)
+            return torch.nn.functional.pad(x, [pl, pr, pt, pb], mode="replicate").permute(0, 2, 3, 1).contiguous()
+
+        return one(image1), one(image2), (H0, W0, pt, pl)
+
+    def _plan_state(self, key: tuple, build) -> _PlanState:
+        """The plan of ``key`` (built by ``build()`` on a miss), marked most recently used; a miss
+        first evicts the least recently used key groups beyond ``max_plans`` (never the group of a
+        batch :meth:`pipelined` left pending)."""
+        st = self._states.get(key)
+        if st is not None:
+            for k in [k for k in self._states if self._group(k) == self._group(key)]:
+                self._states.move_to_end(k)
+            return st
+        self._evict(self._group(key))
+        st = build()
+        self._states[key] = st
+        return st
+
+    def _evict(self, incoming: tuple) -> None:
+        groups = list(OrderedDict.fromkeys(self._group(k) for k in self._states))
+        pend = self._pp["key"] if self._pp is not None and self._pp["pending"] is not None else None
+        n = len(groups) + (incoming not in groups)
+        cap = max(1, int(self.max_plans))
+        for g in groups:
+            if n <= cap:
+                break
+            if g == incoming or g == pend:
+                continue
+            self._drop_group(g)
+            n -= 1
+
+    def _drop_group(self, g: tuple) -> None:
+        # a plan's pipelined graph holds the other slot's kernel nodes (its buffers): the whole
+        # group goes at once
+        for k in [k for k in self._states if self._group(k) == g]:
+            del self._states[k]
+        if self._pp is not None and self._pp["key"] == g:
+            self._pp = None
+
+    def release(self) -> None:
+        """Drop every built plan: their hipGraphs, events, lane streams and device buffers are freed
+        now (the next forward rebuilds).  Not while a :meth:`pipelined` batch is pending."""
+        if self._pp is not None and self._pp["pending"] is not None:
+            raise RuntimeError("release(): flush() the pending pipelined batch first")
+        self._states.clear()
+        self._pp = None
+        self._done_ev = None
+
+    def num_plans(self) -> int:
+        return len(self._states)
 
     # ----------------------------------------------------------- structure
     def _analyse(self):
@@ -319,9 +461,10 @@ class RaftEngine:
         module list cached at the last repack instead of Module.parameters()
         (its recursive generators cost ~0.7 ms per call, on every forward)."""
         mods = self._sig_modules
-        if mods is None:
-            mods = self._sig_modules = [m for _, m in self.model.named_modules()]
-        sig = []
+        root = self.model
+        if mods is None:   # the root itself is left out (a weakly held model stays collectable)
+            mods = self._sig_modules = [m for n, m in root.named_modules() if n]
+        sig = [tuple(id(c) for c in root._modules.values())]
         for mod in mods:
             for t in mod._parameters.values():
                 if t is not None:
@@ -451,6 +594,7 @@ class RaftEngine:
         self._reg("me.convflow1", cna_src(me.convflow1, 8))
         self._reg("me.convflow2", cna_src(me.convflow2))
         self._reg("me.conv", cna_src(me.conv))
+        hx_cs = self.hx_cs   # the sources below must not capture the engine (no self-cycle: plans die by refcount)
         for gi in range(len(rb.kernel_size)):
             gru = getattr(rb, f"convgru{gi + 1}")
 
@@ -462,10 +606,10 @@ class RaftEngine:
 
             def gru_a(gru=gru):
                 k = torch.cat([loop_part(gru.convz.kernel), loop_part(gru.convr.kernel)], dim=3)
-                return k, torch.zeros(2 * H_), (1, 1), gru.padding, self.hx_cs
+                return k, torch.zeros(2 * H_), (1, 1), gru.padding, hx_cs
 
             def gru_b(gru=gru):
-                return loop_part(gru.convq.kernel), torch.zeros(H_), (1, 1), gru.padding, self.hx_cs
+                return loop_part(gru.convq.kernel), torch.zeros(H_), (1, 1), gru.padding, hx_cs
 
             def gru_ctx(gru=gru):  # context share of [z | r | q] + the gate biases (prologue, once)
                 k = torch.cat([c.kernel.detach()[:, :, H_:H_ + C_] for c in (gru.convz, gru.convr, gru.convq)], dim=3)
@@ -902,7 +1046,8 @@ class RaftEngine:
         nb = B // self.split if (self.split > 1 and B % self.split == 0) else B
         return nb >= self.AUTO_STREAMS_MIN_BATCH
 
-    def _build(self, B: int, H: int, W: int, n_iters: int, all_iters: bool = True) -> _PlanState:
+    def _build(self, B: int, H: int, W: int, n_iters: int, all_iters: bool = True,
+               src: Optional[Tuple[int, int, int, int]] = None) -> _PlanState:
         on = self.uses_lanes(B, all_iters)
         self.streams = on
         self.mask_head = "split" if on else "fused"
@@ -919,9 +1064,13 @@ class RaftEngine:
         # their captures are copied into ONE hipGraph (Plan.merge_*), so the
         # parts' kernels fill each other's idle CUs.
         plans = [nat.new_plan() for _ in range(parts)]
-        st = _PlanState(plan=plans[0], plans=plans, n_iters=n_iters)
-        st.inp1 = torch.zeros((B, H, W, 3), dtype=F32, device=dev)
-        st.inp2 = torch.zeros((B, H, W, 3), dtype=F32, device=dev)
+        st = _PlanState(plan=plans[0], plans=plans, n_iters=n_iters, src=src)
+        if src is not None:   # raw frames: the prep kernel normalises + pads them (K14)
+            st.inp1 = torch.zeros((B, src[0], src[1], 3), dtype=torch.uint8, device=dev)
+            st.inp2 = torch.zeros((B, src[0], src[1], 3), dtype=torch.uint8, device=dev)
+        else:
+            st.inp1 = torch.zeros((B, H, W, 3), dtype=F32, device=dev)
+            st.inp2 = torch.zeros((B, H, W, 3), dtype=F32, device=dev)
         st.out = torch.zeros((n_iters if all_iters else 1, B, H, W, 2), dtype=F32, device=dev)
         st.slot_ptr = st.out.data_ptr()
         st.out_slot = torch.tensor([st.slot_ptr], dtype=torch.int64, device=dev)
@@ -1008,11 +1157,13 @@ class RaftEngine:
             plan.add_memset([t])
         s2d = ("fe.stem_s2d" in sp and "ce.stem_s2d" in sp and H % 2 == 0 and W % 2 == 0
                and os.environ.get("JR_NO_S2D", "0") != "1")
-        if s2d:   # 2x2 space-to-depth images for the 4x4 form of the 7x7 / stride-2 stems
-            x0 = alloc("x0", (2 * B, H // 2, W // 2, 16))
+        x0 = alloc("x0", (2 * B, H // 2, W // 2, 16) if s2d else (2 * B, H, W, 8))
+        if st.src is not None:   # uint8 frames: normalise + replicate pad + layout in one kernel (K14)
+            H0, W0, pt, pl = st.src
+            plan.add_prep([inp1, inp2, x0, u8_table(dev)], [B, H, W, int(s2d), H0, W0, pt, pl])
+        elif s2d:   # 2x2 space-to-depth images for the 4x4 form of the 7x7 / stride-2 stems
             plan.add_prep([inp1, inp2, x0], [B, H, W, 1])
         else:
-            x0 = alloc("x0", (2 * B, H, W, 8))
             plan.add_prep([inp1, inp2, x0], [B, H, W])
         plan.add_record(E_PREP)
 
@@ -1116,7 +1267,11 @@ class RaftEngine:
         qx_x = gru_path != "halo" or halo_pp
         # with the mask lane, the mask head reads h from its own copy `hm` (written by the last
         # stage), so the first stage can replace h in hx while the mask lane still runs
-        hm = alloc("hm", (M, self.hidden)) if gru_path != "unfused" and lanes_on and self.has_mask else None
+        # raft_small's ping-pong stage with a mask head (an injected MaskPredictor) also writes the copy:
+        # its h' alternates between qx and hx, so the mask head (final-only epilogue, context parallel,
+        # mask lane) reads hm instead of a buffer that holds h' only on every other iteration
+        hm = (alloc("hm", (M, self.hidden))
+              if gru_path != "unfused" and self.has_mask and (lanes_on or halo_pp) else None)
         # Parity-buffered mask-lane operands (gru_fused + convex head, JR_MASK_PARITY=1: on): the last
         # GRU stage writes h into hm / hm2 and the update writes the flow into flow32 / flow32b by
         # iteration parity, so iteration i+1 never overwrites what the lane still reads for iteration
@@ -1228,7 +1383,7 @@ class RaftEngine:
                     wa_, wb_ = self._halo_w[gi]
                     last = gi == ngru - 1
                     if halo_pp:
-                        t = [hx, hx, wa_, wb_, gbias[gi], h32, qx, None, qx, qx, hx]
+                        t = [hx, hx, wa_, wb_, gbias[gi], h32, qx, hm, qx, qx, hx]
                     else:
                         t = [hx if gi == 0 else qx, hx, wa_, wb_, gbias[gi], h32, qx if gi == 0 else hx,
                              hm if last else None]
@@ -1375,13 +1530,13 @@ class RaftEngine:
         returns; ``return_all_iters=False`` returns only the final one, (1, B, H, W, 2)."""
         if self._signature() != self._sig:
             self._pack()
-        B, H, W, C = image1.shape
-        assert C == 3, "images must be NHWC with 3 channels"
-        key = (B, H, W, num_flow_updates, bool(return_all_iters))
-        st = self._states.get(key)
-        if st is None:
-            st = self._build(B, H, W, num_flow_updates, bool(return_all_iters))
-            self._states[key] = st
+        if image1.dtype == torch.uint8 and not self._native_u8:
+            a, b, src = self._host_u8(image1, image2)
+            out = self.forward(a, b, num_flow_updates, return_all_iters)
+            H0, W0, pt, pl = src
+            return out[:, :, pt:pt + H0, pl:pl + W0]
+        key = self._key(image1, image2, num_flow_updates, return_all_iters)
+        st = self._plan_state(key, lambda: self._build_key(key))
         st.inp1.copy_(image1)
         st.inp2.copy_(image2)
         fresh = self.copy_output and st.slot_ok
@@ -1405,8 +1560,8 @@ class RaftEngine:
             p0.replay_pipelined()
         self._mark()
         if fresh:
-            return out
-        return st.out.clone() if self.copy_output else st.out
+            return self._crop(st, out)
+        return self._crop(st, st.out.clone() if self.copy_output else st.out)
 
     GATE_MIN_ITERS = 20
 
@@ -1431,16 +1586,14 @@ class RaftEngine:
 
     # ------------------------------------- software-pipelined graphs (throughput)
     def _slot_state(self, key, slot: int) -> _PlanState:
-        skey = key + ("pslot", slot)
-        st = self._states.get(skey)
-        if st is None:
+        def build():
             saved, self.split = self.split, 1
             try:
-                st = self._build(*key)
+                return self._build_key(key)
             finally:
                 self.split = saved
-            self._states[skey] = st
-        return st
+
+        return self._plan_state(key + ("pslot", slot), build)
 
     @torch.no_grad()
     def pipelined(self, image1: torch.Tensor, image2: torch.Tensor, num_flow_updates: int = 12,
@@ -1466,12 +1619,14 @@ class RaftEngine:
                 # would run with the new ones (a result matching neither forward)
                 raise RuntimeError("pipelined(): the weights changed while a batch is pending; flush() it first")
             self._pack()
-        B, H, W, C = image1.shape
-        assert C == 3, "images must be NHWC with 3 channels"
         assert self.use_graph, "pipelined() replays captured graphs (use_graph=True)"
         assert not self.cp, "pipelined(): not with context parallelism (a host-driven loop)"
+        if image1.dtype == torch.uint8 and not self._native_u8:
+            a, b, src = self._host_u8(image1, image2)
+            r = self.pipelined(a, b, num_flow_updates, return_all_iters)
+            return None if r is None else r[:, :, src[2]:src[2] + src[0], src[3]:src[3] + src[1]]
         n = num_flow_updates
-        key = (B, H, W, n, bool(return_all_iters))
+        key = self._key(image1, image2, n, return_all_iters)
         pp = self._pp
         if pp is not None and pp["key"] != key and pp["pending"] is not None:
             raise RuntimeError("pipelined(): flush() the pending batch before changing the input shape / iterations")
@@ -1497,7 +1652,7 @@ class RaftEngine:
                 pst.plan.capture_pipelined(st.plan, n)
             self._gate(n)
             pst.plan.replay_pipelined()
-            result = out if fresh else (pst.out.clone() if self.copy_output else pst.out)
+            result = self._crop(pst, out if fresh else (pst.out.clone() if self.copy_output else pst.out))
         self._mark()
         pp["pending"] = slot
         pp["n"] += 1
@@ -1521,7 +1676,7 @@ class RaftEngine:
         st.plan.replay_part(1)
         pp["pending"] = None
         pp["n"] = 0
-        return out if fresh else (st.out.clone() if self.copy_output else st.out)
+        return self._crop(st, out if fresh else (st.out.clone() if self.copy_output else st.out))
 
     def _launch(self, plan, n_iters: int) -> None:
         if self.use_graph:
@@ -1532,5 +1687,6 @@ class RaftEngine:
             plan.run(n_iters)
 
     def op_names(self, B: int, H: int, W: int, n_iters: int, return_all_iters: bool = True):
-        st = self._states.get((B, H, W, n_iters, return_all_iters)) or self._build(B, H, W, n_iters, return_all_iters)
+        st = self._plan_state((B, H, W, n_iters, return_all_iters),
+                              lambda: self._build(B, H, W, n_iters, return_all_iters))
         return [st.plan.op_names(s) for s in range(3)]

@@ -38,6 +38,7 @@ class RaftEngineF32(RaftEngine):
     ``autotune`` / ``corr_dtype`` / ``gate_dtype`` do not apply."""
 
     precision = "fp32"
+    _native_u8 = False   # uint8 frames: normalised + padded by framework ops, then the fp32 prep
 
     def _analyse(self):
         super()._analyse()
@@ -161,7 +162,8 @@ class RaftEngineF32(RaftEngine):
                 H, W = h_, w_
         return x, H, W
 
-    def _build(self, B: int, H: int, W: int, n_iters: int, all_iters: bool = True) -> _PlanState:
+    def _build(self, B: int, H: int, W: int, n_iters: int, all_iters: bool = True, src=None) -> _PlanState:
+        assert src is None, "fp32 engine: uint8 frames are prepared by RaftEngine._host_u8"
         m = self.model
         dev = self.device
         sp = self._specs

@@ -39,6 +39,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import weakref
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -272,7 +273,7 @@ class FusedLoop:
 
     def __init__(self, model, B: int, H: int, W: int, T: int, device, use_graph: bool = True):
         nat.require()
-        self.model = model
+        self._model_ref = weakref.ref(model)   # weak: the plan cache (_LOOPS) must not keep the model alive
         self.B, self.H, self.W, self.T = B, H, W, T
         self.h, self.w = H // 8, W // 8
         self.M = B * self.h * self.w
@@ -591,6 +592,13 @@ class FusedLoop:
         pk.piece(fh.conv2.kernel, sp["fh2T"], 1, (0, self.fh_hidden), (0, 2))
         pk.bias(fh.conv2.bias, self._fh2_bias, (0, 2))
         return pk
+
+    @property
+    def model(self):
+        m = self._model_ref()
+        if m is None:
+            raise ReferenceError("FusedLoop: its model has been garbage-collected")
+        return m
 
     def stale(self) -> bool:
         return self.packer.stale()
@@ -1068,7 +1076,7 @@ class FusedModel:
     def __init__(self, model, B: int, H: int, W: int, T: int, device, use_graph: bool = True):
         from .fused_encoder import EncoderTrain
 
-        self.model = model
+        self._model_ref = weakref.ref(model)
         self.B, self.H, self.W = B, H, W
         self.loop = FusedLoop(model, B, H, W, T, device, use_graph)
         dev = self.loop.device
@@ -1078,6 +1086,13 @@ class FusedModel:
         self.fe = EncoderTrain(model.feature_encoder, self.x0, self.loop.fm, record_conv, use_graph)
         self.ce = EncoderTrain(model.context_encoder, self.x0[:B], self.loop.ctx_raw, record_conv, use_graph)
         self.params = [p for p in model.parameters()]
+
+    @property
+    def model(self):
+        m = self._model_ref()
+        if m is None:
+            raise ReferenceError("FusedModel: its model has been garbage-collected")
+        return m
 
     def stale(self) -> bool:
         """Parameters re-allocated (e.g. moved) since the plans were recorded."""
@@ -1144,7 +1159,10 @@ class FusedRAFT(torch.autograd.Function):
         return (None, None, None, None) + tuple(grads)
 
 
-_LOOPS: Dict[tuple, object] = {}
+# Native training plans per model: model -> {(kind, B, H, W, T, device): FusedLoop / FusedModel}.
+# Weakly keyed, and the plans hold their model weakly, so a model's plans (hipGraphs, events,
+# streams, arenas, activation buffers) are freed with the model instead of living for the process.
+_LOOPS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 # Gradient communicators of the models whose Trainer step is running: set only
 # inside :func:`grad_comm` (around one step's backward), keyed by the model, so a
 # backward outside a training step, or of another model, never starts a collective.
@@ -1219,16 +1237,18 @@ def _tensor_sig(model) -> tuple:
 
 
 def _cached(kind, model, B, H, W, T, device):
-    key = (kind, id(model), B, H, W, T, str(device))
-    obj = _LOOPS.get(key)
+    key = (kind, B, H, W, T, str(device))
+    plans = _LOOPS.get(model)
+    obj = plans.get(key) if plans is not None else None
     sig = _tensor_sig(model)
-    if obj is None or obj.model is not model or getattr(obj, "_sig", None) != sig or obj.stale():
-        for k in [k for k, v in _LOOPS.items() if k[1] == id(model)]:
-            del _LOOPS[k]   # one plan set per model: drop other shapes / kinds
+    if obj is None or getattr(obj, "_sig", None) != sig or obj.stale():
+        # one plan set per model: drop other shapes / kinds first (their buffers), then build
+        _LOOPS.pop(model, None)
+        obj = None
         g = os.environ.get("JR_FUSED_GRAPH", "1") != "0"
         obj = (FusedModel if kind == "model" else FusedLoop)(model, B, H, W, T, device, use_graph=g)
         obj._sig = sig
-        _LOOPS[key] = obj
+        _LOOPS[model] = {key: obj}
     return obj
 
 

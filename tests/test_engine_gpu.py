@@ -113,9 +113,14 @@ def test_engine_fp32_pyramid_closer_to_golden():
     model = model.cuda()
     out32 = model(i1.cuda(), i2.cuda(), num_flow_updates=3, corr_dtype=torch.float32).cpu()
     out16 = model(i1.cuda(), i2.cuda(), num_flow_updates=3).cpu()
+    # relative bounds (mean |golden flow| is ~0.01-0.05 px at these sizes with random weights: an
+    # absolute term would let an all-zero output pass); the fp32 pyramid removes the bf16 rounding
+    # of the correlation volume / lookup, so it must not be further from the golden than bf16
     mag = ref.norm(dim=-1).mean().item()
-    assert _epe(out32[-1], ref[-1]) < 0.05 * mag + 0.05
-    assert _epe(out16[-1], ref[-1]) < 0.05 * mag + 0.05
+    e32, e16 = _epe(out32[-1], ref[-1]), _epe(out16[-1], ref[-1])
+    assert e32 < REL_EPE["raft_large"] * mag, (e32, mag)
+    assert e16 < REL_EPE["raft_large"] * mag, (e16, mag)
+    assert e32 <= e16, (e32, e16)
 
 
 def test_input_prefetcher_pipeline_matches_direct():
@@ -161,7 +166,7 @@ def test_final_only_mode_equals_last_iteration(factory, use_graph):
     mag = full[-1].norm(dim=-1).mean().item()
     if factory is raft_small:   # same kernels, same order
         assert (last[0] - full[-1]).abs().max().item() < 1e-4
-    assert _epe(last[0], full[-1]) < 1e-2 * mag + 1e-2
+    assert _epe(last[0], full[-1]) < 0.5 * REL_EPE["raft_large"] * mag
 
 
 @pytest.mark.parametrize("factory,B", [(raft_large, 4), (raft_large, 1), (raft_small, 2)])
@@ -209,7 +214,7 @@ def test_split_mask_head_matches_fused():
     torch.cuda.synchronize()
     mag = b.norm(dim=-1).mean().item()
     for it in range(6):
-        assert _epe(a[it], b[it]) < 0.02 * mag + 0.02, it
+        assert _epe(a[it], b[it]) < 0.5 * REL_EPE["raft_large"] * mag, it
     assert torch.equal(a, c)
 
 
@@ -232,7 +237,33 @@ def test_generic_mask_head_matches_golden(final_only):
     assert a.shape == ref.shape
     mag = ref.norm(dim=-1).mean().item()
     for it in range(a.shape[0]):
-        assert _epe(a[it].cpu(), ref[it]) < 0.05 * mag + 0.05, it
+        assert _epe(a[it].cpu(), ref[it]) < REL_EPE["raft_large"] * mag, it
+
+
+@pytest.mark.parametrize("B", [1, 4])
+@pytest.mark.parametrize("final_only", [False, True])
+def test_small_with_mask_predictor_matches_golden(B, final_only):
+    """raft_small with an injected 256 -> 576 MaskPredictor (model.py:665 pops the kwarg for either
+    arch): its single 3x3 ConvGRU stage ping-pongs h' between qx (even iterations) and hx (odd),
+    so the mask head must read the stage's copy hm.  An odd iteration count puts the final h' in
+    qx: reading hx there would upsample with the previous iteration's mask."""
+    from jax_raft_amd.models.layers import MaskPredictor
+
+    mp = MaskPredictor(96, hidden_size=256, multiplier=0.25, gen=torch.Generator().manual_seed(9))
+    model, variables = raft_small(mask_predictor=mp)
+    i1, i2 = _inputs(B, 128, 256, seed=41 + B)
+    iters = 3
+    ref = model.apply(variables, i1, i2, num_flow_updates=iters, return_all_iters=not final_only)
+    model = model.cuda()
+    out = model(i1.cuda(), i2.cuda(), num_flow_updates=iters, return_all_iters=not final_only)
+    eng = model.engine(torch.device("cuda", 0))
+    torch.cuda.synchronize()
+    assert eng.gru_path == "halo" and eng._convex_w is not None
+    assert out.shape == ref.shape
+    out = out.cpu()
+    for it in range(out.shape[0]):
+        mag = ref[it].norm(dim=-1).mean().item()
+        assert _epe(out[it], ref[it]) < REL_EPE["raft_small"] * mag, (it, _epe(out[it], ref[it]), mag)
 
 
 @pytest.mark.parametrize("tiles", [0, 1, 2])
@@ -283,7 +314,7 @@ def test_streams_auto_matches_lanes_and_single_lane(factory):
             assert (a - b).abs().max().item() < 1e-3 and (a - c).abs().max().item() < 1e-3
         else:   # lanes: split mask head + FlowHead taps epilogue (bf16-level differences)
             mag = c.norm(dim=-1).mean().item()
-            assert _epe(a, b if B >= 4 else c) < 1e-4 and _epe(b, c) < 1e-2 * mag + 1e-2
+            assert _epe(a, b if B >= 4 else c) < 1e-4 and _epe(b, c) < 0.5 * REL_EPE["raft_large"] * mag
         eng = model.engine(torch.device("cuda", 0), streams="auto")
         st = eng._states[(B, 128, 128, 3, True)]
         # loop lanes (the prologue's branches run on lanes at every batch, JR_PRO_LANES)
@@ -295,7 +326,7 @@ def test_streams_auto_matches_lanes_and_single_lane(factory):
         if factory is raft_small:
             assert (d[-1] - c[-1]).abs().max().item() < 1e-3
         else:
-            assert _epe(d[-1], c[-1]) < 1e-2 * c[-1].norm(dim=-1).mean().item() + 1e-2
+            assert _epe(d[-1], c[-1]) < 0.5 * REL_EPE["raft_large"] * c[-1].norm(dim=-1).mean().item()
         assert not eng.uses_lanes(B, all_iters=False)
 
 
@@ -335,7 +366,7 @@ def test_lane_schedule_graph_equals_eager_and_tracks_golden():
     assert torch.equal(a, b)
     mag = gold.norm(dim=-1).mean().item()
     for it in range(5):
-        assert _epe(a[it].cpu(), gold[it]) < 0.05 * mag + 0.05, it
+        assert _epe(a[it].cpu(), gold[it]) < REL_EPE["raft_large"] * mag, it
 
 
 @pytest.mark.parametrize("gru", ["fused", "halo"])
@@ -383,8 +414,8 @@ def test_engine_context_parallel_single_slab():
         base = RaftEngine(model, torch.device("cuda", 0)).forward(i1.cuda(), i2.cuda(), 3).cpu()
     torch.cuda.synchronize()
     mag = ref.norm(dim=-1).mean().item()
-    assert _epe(cp[-1], ref[-1]) < 0.05 * mag + 0.05
-    assert _epe(cp[-1], base[-1]) < 0.02 * mag + 0.02
+    assert _epe(cp[-1], ref[-1]) < REL_EPE["raft_large"] * mag
+    assert _epe(cp[-1], base[-1]) < 0.5 * REL_EPE["raft_large"] * mag
 
 
 def test_engine_context_parallel_two_ranks(tmp_path):
@@ -415,7 +446,7 @@ def test_engine_context_parallel_two_ranks(tmp_path):
     i1, i2 = base[:, 4:132, 4:260].contiguous(), base[:, 2:130, 6:262].contiguous()
     ref = model.apply(variables, i1, i2, train=False, num_flow_updates=3)
     mag = ref.norm(dim=-1).mean().item()
-    assert _epe(a["bf16"][-1], ref[-1]) < 0.05 * mag + 0.05
+    assert _epe(a["bf16"][-1], ref[-1]) < REL_EPE["raft_large"] * mag
     assert torch.equal(a["bf16_final"][0], a["bf16"][-1]) or _epe(a["bf16_final"][0], a["bf16"][-1]) < 1e-3
     with torch.no_grad():
         f32 = RaftEngine(model.eval().cuda(), torch.device("cuda", 0), precision="fp32").forward(
