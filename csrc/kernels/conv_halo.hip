@@ -83,7 +83,7 @@ __global__ __launch_bounds__(64 * WCO * WPX, (INN && CIN <= 64 && TN <= 2) ? 3 :
   {
     float* const nrm = (float*)(lds_b + NFP * RB);   // [CIN][2] input, [CIN][2] residual
     const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)p.in_res, (short)0, (int)p.x_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)p.in_res, (short)0, (int)p.in_res_bytes, 0x00020000);
     constexpr int TOTAL = NFP * CC;
     constexpr int NL = (TOTAL + NT - 1) / NT;
     constexpr int NBMAX = INN || WIDE ? 8 : 16;   // the normalising loader holds the residual chunks too

@@ -27,7 +27,8 @@
 //   8 k-steps of a wave's tiles are loaded at once (64 VGPRs at 2 tiles): one
 //   memory round trip per block instead of one per k-step, which is what
 //   bounded the k-step-pipelined variants (~25 us at raft_large batch 4:
-//   waves lived the whole kernel waiting on loads; profiles/r2_convex_head.md).
+//   waves lived the whole kernel waiting on loads; measured in round 2, the study file was never
+//   committed -- the current kernel's numbers: profiles/r4_convex_persist_ab.txt).
 //   Block order is XCD-aware: the 4 groups of one pixel block get block ids
 //   equal mod 8, so they run on one XCD and share its L2 copy of the features.
 #pragma once

@@ -4,7 +4,7 @@
 //
 // The volume (533 MB at raft_large batch 4) is the only traffic that has to reach HBM; the
 // tile kernel of corr.hip re-read both feature maps per 128 x 128 tile (1.6 GB of L2 reads,
-// 382 MB past L2: profiles/r4_corr_study.md).  Here:
+// 382 MB past L2 in round 4; the current kernels' traffic: profiles/r5_corr_study.md).  Here:
 //   * one workgroup (8 waves) per CU walks a contiguous run of (image, query tile, target tile) items,
 //     target tile fastest; runs are XCD-contiguous, so an XCD's CUs read one image's f2;
 //   * a wave keeps its 32 queries' features in registers (the MFMA B operand) for the whole

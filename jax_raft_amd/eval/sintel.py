@@ -62,6 +62,11 @@ class MpiSintel:
         return a, b, flow
 
 
+
+def _finite_mean(rates) -> float:
+    ok = [r for r in rates if np.isfinite(r)]
+    return float(np.mean(ok)) if ok else float("nan")
+
 def epe_metrics(epe_all: np.ndarray) -> Dict[str, float]:
     return {
         "epe": float(np.mean(epe_all)),
@@ -132,7 +137,10 @@ def validate_sintel(model, data_root: str, iters: int = 32, dstypes: Sequence[st
             rates = [float(r.item()) for r in rt]
         cnt = max(sums[4], 1)
         res = {"epe": sums[0] / cnt, "1px": sums[1] / cnt, "3px": sums[2] / cnt, "5px": sums[3] / cnt,
-               "fps": float(np.mean(rates)), "fps_aggregate": float(np.sum(rates)), "world": world,
+               # ranks without a timed batch (a short shard: every batch the first of its shape) report nan
+               # and are left out, so one such rank cannot turn the job's rate into nan
+               "fps": _finite_mean(rates), "fps_aggregate": float(np.sum([r for r in rates if np.isfinite(r)])),
+               "world": world,
                "pairs": int(n), "batch_size": bs}
         results[dstype] = res
         if verbose and rank == 0:

@@ -1159,8 +1159,8 @@ class RaftEngine:
                and os.environ.get("JR_NO_S2D", "0") != "1")
         x0 = alloc("x0", (2 * B, H // 2, W // 2, 16) if s2d else (2 * B, H, W, 8))
         if st.src is not None:   # uint8 frames: normalise + replicate pad + layout in one kernel (K14)
-            H0, W0, pt, pl = st.src
-            plan.add_prep([inp1, inp2, x0, u8_table(dev)], [B, H, W, int(s2d), H0, W0, pt, pl])
+            H0, W0, pad_t, pad_l = st.src   # (pt is this part's buffer prefix)
+            plan.add_prep([inp1, inp2, x0, u8_table(dev)], [B, H, W, int(s2d), H0, W0, pad_t, pad_l])
         elif s2d:   # 2x2 space-to-depth images for the 4x4 form of the 7x7 / stride-2 stems
             plan.add_prep([inp1, inp2, x0], [B, H, W, 1])
         else:

@@ -424,6 +424,9 @@ class FusedLoop:
         (flipped, in/out-swapped kernels, padding k-1-p, zero bias, output
         channels padded to the buffer they are written into)."""
         me, fh, mp, hd, C = self.me, self.fh, self.mp, self.hd, self.ctx_ch
+        # the sources are kept (self._src): they must not capture self, or every FusedLoop would be
+        # a reference cycle that only a full garbage collection frees (with its device buffers)
+        dev, hx_cs, ctx_cs = self.device, self.hx_cs, self.ctx_cs
         src = {}
 
         def kb(c):
@@ -456,7 +459,7 @@ class FusedLoop:
         def loop_part(k):  # input channels [h | context | motion] -> [h | motion] (hx layout, padded)
             k = k.detach().float()
             kk = torch.cat([k[:, :, :hd], k[:, :, hd + C:]], dim=2)
-            out = k.new_zeros(k.shape[:2] + (self.hx_cs, k.shape[3]))
+            out = k.new_zeros(k.shape[:2] + (hx_cs, k.shape[3]))
             out[:, :, : kk.shape[2]] = kk
             return out
 
@@ -476,9 +479,9 @@ class FusedLoop:
             def gcb(gru=gru):
                 return torch.cat([c.bias.detach() for c in (gru.convz, gru.convr, gru.convq)]).float()
 
-            src[f"gA{g}"] = (lambda ga=ga, pad=pad: (ga(), torch.zeros(2 * hd, device=self.device), pad, self.hx_cs))
-            src[f"gB{g}"] = (lambda gb=gb, pad=pad: (gb(), torch.zeros(hd, device=self.device), pad, self.hx_cs))
-            src[f"gC{g}"] = (lambda gc=gc, gcb=gcb, pad=pad: (gc(), gcb(), pad, self.ctx_cs))
+            src[f"gA{g}"] = (lambda ga=ga, pad=pad: (ga(), torch.zeros(2 * hd, device=dev), pad, hx_cs))
+            src[f"gB{g}"] = (lambda gb=gb, pad=pad: (gb(), torch.zeros(hd, device=dev), pad, hx_cs))
+            src[f"gC{g}"] = (lambda gc=gc, gcb=gcb, pad=pad: (gc(), gcb(), pad, ctx_cs))
             src[f"gAT{g}"] = bwd(ga, pad, 2 * hd, self.hx_cs)
             src[f"gBT{g}"] = bwd(gb, pad, hd, self.hx_cs)
             src[f"gCT{g}"] = bwd(gc, pad, 3 * hd, self.ctx_cs)
@@ -501,7 +504,7 @@ class FusedLoop:
             cin = k.shape[2]
             return k.reshape(9, cin, 2).permute(1, 0, 2).reshape(1, 1, cin, 18)
 
-        src["fh2t"] = lambda: (taps(), torch.zeros(18, device=self.device), (0, 0), None)
+        src["fh2t"] = lambda: (taps(), torch.zeros(18, device=dev), (0, 0), None)
         src["fh2T"] = bwd(lambda: fh.conv2.kernel.detach().float(), (1, 1), 8, self.fh_hidden)
         return src
 

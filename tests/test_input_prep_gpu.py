@@ -93,7 +93,7 @@ def test_engine_u8_pipelined_and_fp32():
     for r, o in zip(refs, outs):
         assert torch.equal(r, o)
     e32 = RaftEngine(model, torch.device("cuda", 0), precision="fp32")
-    x, y = frames[0]
+    x, y = (torch.from_numpy(v).cuda() for v in _frames(1, 125, 250, seed=9))   # fp32 engine: h * w % 4 == 0
     f1, f2, p = _host(x.cpu().numpy(), y.cpu().numpy())
     a = e32.forward(x, y, 2)
     b = e32.forward(f1.cuda(), f2.cuda(), 2)

@@ -8,7 +8,9 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("arch", ["raft_small", "raft_large"])
-def test_gpu_train_steps_reduce_loss(arch):
+def test_gpu_train_steps_stay_finite(arch):
+    """Six logged steps through Trainer.fit: finite losses and weights (the loss decrease itself:
+    test_gpu_train_overfits_one_batch)."""
     cfg = TrainConfig(arch=arch, steps=6, batch=2, iters=3, size=(128, 160), log_every=1, lr=2e-4)
     tr = Trainer(cfg)
     assert tr.device.type == "cuda"
@@ -91,9 +93,9 @@ def test_dp_grads_equal_full_batch(tmp_path):
     full = grads(tuple(torch.cat([p[k] for p in parts]) for k in range(4)))
     e_full = rel(g0, full)
     print(f"DP vs per-sample mean: {e_comm:.3e}; DP vs full batch: {e_full:.3e}")
-    # measured on MI355X (round 4): see profiles/r4_dp_grad_error.txt
-    assert e_comm < 1e-3, e_comm
-    assert e_full < 2e-2, e_full
+    # measured on MI355X (round 5, profiles/r5_dp_grad_error.txt): 0 and 7.9e-8
+    assert e_comm < 1e-5, e_comm
+    assert e_full < 1e-3, e_full
 
 
 def test_gpu_nonfinite_step_dropped_without_host_sync():
