@@ -33,6 +33,12 @@ namespace {
 constexpr int BK = 64;
 
 JR_DEVICE int swzB(int row) { return (row >> 1) & 7; }
+// A (weight) images read with the 32x32x16 row order m32_arow: a ds_read_b128 lane group
+// ({0-3, 12-15, 20-27} / {4-11, 16-19, 28-31}) reads 4 row pairs 16 or 32 rows apart, which
+// swzB maps two-by-two onto the same 16-B slots (2-way conflicts: profiles/r5_pmc_b4.txt,
+// gru_fused 29 % / conv_m32 17-19 % of LDS cycles); xoring bit 4 of the pair index into the
+// slot's top bit separates them (rows of a 64-row group; groups start at multiples of 64)
+JR_DEVICE int swzA(int row) { return ((row >> 1) ^ ((row >> 5) << 2)) & 7; }
 
 template <int NV>
 JR_DEVICE void store_bf16(bf16* dst, const float* v) {
@@ -893,7 +899,7 @@ JR_DEVICE void conv_m32_body(const ConvParams& p, const int bx_, const int by_) 
 #pragma unroll
     for (int i = 0; i < WR; ++i) {
       const int rr = (tid >> 3) + RP * i;
-      *(u32x4*)(sA + rr * BK + ((ch ^ swzB(rr)) << 3)) = r.w[i];
+      *(u32x4*)(sA + rr * BK + ((ch ^ swzA(rr)) << 3)) = r.w[i];
     }
   };
 
@@ -920,7 +926,7 @@ JR_DEVICE void conv_m32_body(const ConvParams& p, const int bx_, const int by_) 
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
         const int row = gbase + 64 * ((tabs0 + tm) >> 1) + m32_arow((tabs0 + tm) & 1, rho);  // 128-row wave tiles span two groups
-        af[tm] = *(const bf16x8*)(sA + row * BK + ((chunk ^ swzB(row)) << 3));
+        af[tm] = *(const bf16x8*)(sA + row * BK + ((chunk ^ swzA(row)) << 3));
       }
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {

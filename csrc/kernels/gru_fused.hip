@@ -118,6 +118,7 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
   auto sA_of = [&](int buf) { return smem + buf * STAGE; };
   auto sB_of = [&](int buf) { return smem + buf * STAGE + AROWS * BK; };
   auto put = [&](bf16* base, int row, const u32x4& v) { *(u32x4*)(base + row * BK + ((ch ^ swzB(row)) << 3)) = v; };
+  auto putA = [&](bf16* base, int row, const u32x4& v) { *(u32x4*)(base + row * BK + ((ch ^ swzA(row)) << 3)) = v; };
 
   // ---------------------------------------------------------------- GEMM 1
   auto issue1 = [&](Regs& r, int s) {
@@ -128,8 +129,8 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
     r.b = xload(s);
   };
   auto store1 = [&](const Regs& r, int buf) {
-    put(sA_of(buf), lrow, r.a0);
-    put(sA_of(buf), lrow + 128, r.a1);
+    putA(sA_of(buf), lrow, r.a0);
+    putA(sA_of(buf), lrow + 128, r.a1);
     put(sB_of(buf), lrow, r.b);
   };
   f32x16 acc[2];
@@ -171,7 +172,7 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int row = arow0 + m32_arow(t, rho);
-        const bf16x8 a = *(const bf16x8*)(sA + row * BK + ((chunk ^ swzB(row)) << 3));
+        const bf16x8 a = *(const bf16x8*)(sA + row * BK + ((chunk ^ swzA(row)) << 3));
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[t], 0, 0, 0);
       }
     }
@@ -273,7 +274,7 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
   auto sA2 = [&](int buf) { return G2ALL ? smem + buf * G2ST : sA_of(buf); };
   auto sB2 = [&](int buf) { return G2ALL ? smem + buf * G2ST + HD * BK : sB_of(buf); };
   auto store2 = [&](const Regs& r, int buf, int s) {
-    put(sA2(buf), lrow, r.a0);
+    putA(sA2(buf), lrow, r.a0);
     if ((s & 3) >= 2) put(sB2(buf), lrow, r.b);
   };
 #pragma unroll
@@ -285,7 +286,7 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
     for (int kk = 0; kk < 4; ++kk) {
       const int chunk = kk * 2 + hh;
       const bf16x8 b = bfrag(chunk);
-      const bf16x8 a = *(const bf16x8*)(sA + arow * BK + ((chunk ^ swzB(arow)) << 3));
+      const bf16x8 a = *(const bf16x8*)(sA + arow * BK + ((chunk ^ swzA(arow)) << 3));
       acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[0], 0, 0, 0);
     }
   };

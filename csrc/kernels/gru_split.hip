@@ -55,6 +55,10 @@ struct SplitCfg {
   static_assert(2 * BUF <= 160 * 1024, "LDS");
 };
 
+// LDS-only workgroup barrier: __syncthreads() would also wait for every outstanding global load
+// (vmcnt(0)), i.e. drain the next slabs' prefetch at every slab boundary
+JR_DEVICE void split_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // byte offset of chunk c of footprint row f: the 16 consecutive rows a b128 lane group reads
 // (one logical chunk) land in 16 distinct 16-B slots of the 256-B bank window
 template <int KC>
@@ -80,6 +84,10 @@ __global__ __launch_bounds__(64 * (CB / CBW) * (PB / PBW)) void gru_split_kernel
     ctile = q - (q / p.ctiles) * p.ctiles;
     if (ptile >= p.ptiles) return;
   }
+  auto stamp = [&](int k) {
+    if (p.dbg && tid == 0) p.dbg[blockIdx.x * 12 + k] = (long long)wall_clock64();
+  };
+  stamp(0);
   const int line_len = p.axis ? p.H : p.W;
   const int HW = p.H * p.W;
   auto line_pix = [&](int j, int pos_in_line) -> int {   // image pixel of position pos of run j's line, -1 outside
@@ -121,21 +129,25 @@ __global__ __launch_bounds__(64 * (CB / CBW) * (PB / PBW)) void gru_split_kernel
     foff[k] = v;
   }
   const unsigned wbase = (unsigned)((ctile * C::NSLAB) * C::A_BYTES) + (unsigned)tid * 16u;
-  u32x4 sa[NA], sf[NF];
-  auto issue = [&](int s) {
+  // the loads of slab s are issued DEPTH slabs before it is computed: two register sets when the
+  // per-thread staging is small (8-wave tiles), so ~2 slabs of compute cover the L2 / HBM latency
+  constexpr int DEPTH = NA + NF <= 12 ? 2 : 1;
+  u32x4 sa[DEPTH][NA], sf[DEPTH][NF];
+  auto issue = [&](int s, int r) {
 #pragma unroll
-    for (int k = 0; k < NA; ++k) sa[k] = bload(wrs, wbase + (unsigned)(s * C::A_BYTES + k * C::NT * 16));
+    for (int k = 0; k < NA; ++k) sa[r][k] = bload(wrs, wbase + (unsigned)(s * C::A_BYTES + k * C::NT * 16));
 #pragma unroll
-    for (int k = 0; k < NF; ++k) sf[k] = bload(srs, foff[k] >= 0 ? (unsigned)foff[k] + (unsigned)(s * KC * 2) : HOOB);
+    for (int k = 0; k < NF; ++k)
+      sf[r][k] = bload(srs, foff[k] >= 0 ? (unsigned)foff[k] + (unsigned)(s * KC * 2) : HOOB);
   };
-  auto commit = [&](int buf) {
+  auto commit = [&](int buf, int r) {
     char* const base = lds + buf * C::BUF;
 #pragma unroll
-    for (int k = 0; k < NA; ++k) *(u32x4*)(base + (k * C::NT + tid) * 16) = sa[k];
+    for (int k = 0; k < NA; ++k) *(u32x4*)(base + (k * C::NT + tid) * 16) = sa[r][k];
 #pragma unroll
     for (int k = 0; k < NF; ++k) {
       const int e = k * C::NT + tid;
-      if (foff[k] != -2) *(u32x4*)(base + C::A_BYTES + fslot<KC>(e / C::CPR, e % C::CPR)) = sf[k];
+      if (foff[k] != -2) *(u32x4*)(base + C::A_BYTES + fslot<KC>(e / C::CPR, e % C::CPR)) = sf[r][k];
     }
   };
 
@@ -159,34 +171,79 @@ __global__ __launch_bounds__(64 * (CB / CBW) * (PB / PBW)) void gru_split_kernel
 #pragma unroll
       for (int k = 0; k < 16; ++k) acc[a][b][k] = 0.f;
 
-  issue(0);
-  commit(0);
-  __syncthreads();
-  for (int s = 0; s < C::NSLAB; ++s) {
-    if (s + 1 < C::NSLAB) issue(s + 1);
-    const char* const A = lds + (s & 1) * C::BUF;
-    const char* const F = A + C::A_BYTES;
+  // epilogue operands (independent of the GEMM): loaded during the last slab's MFMAs
+  constexpr bool EPRE = CBW * PBW <= 2;
+  u32x4 ep0[EPRE ? CBW * PBW : 1][2], ep1[EPRE ? CBW * PBW : 1][2];
+  f32x4 ep2[EPRE ? CBW * PBW : 1][4];
+  auto epi_pre = [&]() {
 #pragma unroll
-    for (int tap = 0; tap < STAPS; ++tap) {
+    for (int a = 0; a < CBW; ++a) {
+      const int co = 32 * (ctile * CB + wc * CBW + a) + 16 * hh;
 #pragma unroll
-      for (int kk = 0; kk < C::KK; ++kk) {
-        bf16x8 af[CBW], bfr[PBW];
+      for (int b = 0; b < PBW; ++b) {
+        const long m = opix[b] >= 0 ? opix[b] : 0;   // unconditional (clamped): no branch around the loads
+        const int e = a * PBW + b;
+        const u32x4* q = (const u32x4*)((const bf16*)p.bmap + m * p.bmap_cs + (MODE == 0 ? co : 2 * SHD + co));
+        ep0[e][0] = q[0];
+        ep0[e][1] = q[1];
+        if (MODE == 0) {
+          const u32x4* hq = (const u32x4*)((const bf16*)p.src + m * p.src_cs + (co >= SHD ? co - SHD : 0));
+          ep1[e][0] = hq[0];
+          ep1[e][1] = hq[1];
+        } else {
+          const u32x4* zq = (const u32x4*)((const bf16*)p.zb + m * SHD + co);
+          ep1[e][0] = zq[0];
+          ep1[e][1] = zq[1];
+          const f32x4* hq = (const f32x4*)(p.h32 + m * SHD + co);
 #pragma unroll
-        for (int a = 0; a < CBW; ++a)
-          af[a] = *(const bf16x8*)(A + ((tap * C::KK + kk) * CB + wc * CBW + a) * 1024 + lane * 16);
-#pragma unroll
-        for (int b = 0; b < PBW; ++b) {
-          const int f = frow[b] + tap;
-          bfr[b] = *(const bf16x8*)(F + fslot<KC>(f, 2 * kk + hh));
+          for (int k = 0; k < 4; ++k) ep2[e][k] = hq[k];
         }
-#pragma unroll
-        for (int a = 0; a < CBW; ++a)
-#pragma unroll
-          for (int b = 0; b < PBW; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
       }
     }
-    if (s + 1 < C::NSLAB) commit((s + 1) & 1);
-    __syncthreads();
+  };
+
+  issue(0, 0);
+  if (DEPTH == 2 && C::NSLAB > 1) issue(1, 1);
+  commit(0, 0);
+  split_lds_sync();
+  stamp(1);
+  for (int s = 0; s < C::NSLAB; ++s) {
+    if (DEPTH == 1 && s + 1 < C::NSLAB) issue(s + 1, 0);
+    if (DEPTH == 2 && s + 2 < C::NSLAB) issue(s + 2, s & 1);   // set s & 1 was committed (slab s)
+    if (EPRE && s == C::NSLAB - 1) epi_pre();
+    const char* const A = lds + (s & 1) * C::BUF;
+    const char* const F = A + C::A_BYTES;
+    // k-step st = (tap, kk); the fragments of step st + 1 are read from LDS while step st's MFMAs
+    // run (one wave per SIMD: nothing else would hide the LDS latency)
+    constexpr int S = STAPS * C::KK;
+    auto rd = [&](int st, bf16x8 (&af)[CBW], bf16x8 (&bfr)[PBW]) {
+      const int tap = st / C::KK, kk = st - tap * C::KK;
+#pragma unroll
+      for (int a = 0; a < CBW; ++a)
+        af[a] = *(const bf16x8*)(A + ((tap * C::KK + kk) * CB + wc * CBW + a) * 1024 + lane * 16);
+#pragma unroll
+      for (int b = 0; b < PBW; ++b) bfr[b] = *(const bf16x8*)(F + fslot<KC>(frow[b] + tap, 2 * kk + hh));
+    };
+    bf16x8 af0[CBW], bf0[PBW], af1[CBW], bf1[PBW];
+    rd(0, af0, bf0);
+#pragma unroll
+    for (int st = 0; st < S; ++st) {
+      bf16x8 (&ac)[CBW] = (st & 1) ? af1 : af0;
+      bf16x8 (&bc)[PBW] = (st & 1) ? bf1 : bf0;
+      bf16x8 (&an)[CBW] = (st & 1) ? af0 : af1;
+      bf16x8 (&bn)[PBW] = (st & 1) ? bf0 : bf1;
+      if (st + 1 < S) rd(st + 1, an, bn);
+#pragma unroll
+      for (int a = 0; a < CBW; ++a)
+#pragma unroll
+        for (int b = 0; b < PBW; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ac[a], bc[b], acc[a][b], 0, 0, 0);
+      if (st + 1 < S) __builtin_amdgcn_sched_group_barrier(0x100, CBW + PBW, 0);   // next step's DS reads first
+      __builtin_amdgcn_sched_group_barrier(0x008, CBW * PBW, 0);                    // then this step's MFMAs
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (s + 1 < C::NSLAB) commit((s + 1) & 1, DEPTH == 2 ? (s + 1) & 1 : 0);
+    split_lds_sync();
+    if (s < 8) stamp(2 + s);
   }
 
   // ---------------------------------------------------------------- epilogues
@@ -200,7 +257,16 @@ __global__ __launch_bounds__(64 * (CB / CBW) * (PB / PBW)) void gru_split_kernel
       const int m = opix[b];
       if (m < 0) continue;
       float bv[16], v[16];
-      load_bf16<16>((const bf16*)p.bmap + (long)m * p.bmap_cs + (MODE == 0 ? co : 2 * SHD + co), bv);
+      const int e = a * PBW + b;
+      auto unpack = [](const u32x4 (&r)[2], float* o) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          o[k] = bf2f(__builtin_bit_cast(bf16x8, r[0])[k]);
+          o[8 + k] = bf2f(__builtin_bit_cast(bf16x8, r[1])[k]);
+        }
+      };
+      if constexpr (EPRE) unpack(ep0[e], bv);
+      else load_bf16<16>((const bf16*)p.bmap + (long)m * p.bmap_cs + (MODE == 0 ? co : 2 * SHD + co), bv);
       if (MODE == 0) {
         if (co < SHD) {   // z
 #pragma unroll
@@ -209,16 +275,23 @@ __global__ __launch_bounds__(64 * (CB / CBW) * (PB / PBW)) void gru_split_kernel
         } else {          // r * h (h: the bf16 loop state the conv read)
           const int c = co - SHD;
           float h[16];
-          load_bf16<16>((const bf16*)p.src + (long)m * p.src_cs + c, h);
+          if constexpr (EPRE) unpack(ep1[e], h);
+          else load_bf16<16>((const bf16*)p.src + (long)m * p.src_cs + c, h);
 #pragma unroll
           for (int k = 0; k < 16; ++k) v[k] = sigmoidf_(acc[a][b][k] + bv[k]) * h[k];
           store_bf16<16>((bf16*)p.rh + (long)m * p.rh_cs + c, v);
         }
       } else {            // q, blend: h' = (1 - z) h + z q (fp32 state)
         float z[16], h[16];
-        load_bf16<16>((const bf16*)p.zb + (long)m * SHD + co, z);
         float* hp = p.h32 + (long)m * SHD + co;
-        load_f32<16>(hp, h);
+        if constexpr (EPRE) {
+          unpack(ep1[e], z);
+#pragma unroll
+          for (int k = 0; k < 16; ++k) h[k] = ep2[e][k >> 2][k & 3];
+        } else {
+          load_bf16<16>((const bf16*)p.zb + (long)m * SHD + co, z);
+          load_f32<16>(hp, h);
+        }
 #pragma unroll
         for (int k = 0; k < 16; ++k) v[k] = (1.0f - z[k]) * h[k] + z[k] * tanhf_(acc[a][b][k] + bv[k]);
         store_f32<16>(hp, v);
@@ -227,6 +300,7 @@ __global__ __launch_bounds__(64 * (CB / CBW) * (PB / PBW)) void gru_split_kernel
       }
     }
   }
+  stamp(10);
 }
 
 struct SplitCfgId {
@@ -240,6 +314,8 @@ constexpr SplitCfgId kSplitCfgs[] = {
     {4, 1, 64, 1, 1},   // 3: 128 px x 32 ch, 4 waves
     {2, 2, 64, 1, 1},   // 4: 64 px x 64 ch, 4 waves
     {8, 1, 64, 1, 2},   // 5: 256 px x 32 ch, 4 waves
+    {8, 2, 64, 1, 2},   // 6: 256 px x 64 ch, 8 waves (two per SIMD: each hides the other's latencies)
+    {4, 2, 64, 1, 1},   // 7: 128 px x 64 ch, 8 waves
 };
 constexpr int kNumSplitCfgs = sizeof(kSplitCfgs) / sizeof(kSplitCfgs[0]);
 
@@ -273,7 +349,7 @@ extern "C" int jr_gru_split(const GruSplitParams* p, int cfg, hipStream_t stream
     return p->mode ? launch_split<PB_, CB_, KC_, CBW_, PBW_, 1>(*p, stream)                            \
                    : launch_split<PB_, CB_, KC_, CBW_, PBW_, 0>(*p, stream);
   JR_SPLIT(8, 2, 64, 2, 2) JR_SPLIT(8, 4, 32, 2, 2) JR_SPLIT(4, 2, 64, 2, 1) JR_SPLIT(4, 1, 64, 1, 1)
-  JR_SPLIT(2, 2, 64, 1, 1) JR_SPLIT(8, 1, 64, 1, 2)
+  JR_SPLIT(2, 2, 64, 1, 1) JR_SPLIT(8, 1, 64, 1, 2) JR_SPLIT(8, 2, 64, 1, 2) JR_SPLIT(4, 2, 64, 1, 1)
 #undef JR_SPLIT
   return (int)hipErrorInvalidValue;
 }

@@ -415,6 +415,7 @@ struct GruSplitParams {
   float* h32;                                     // B: fp32 [M][128] hidden state, updated in place
   void* y; int y_cs;                              // B: bf16 h' -> channels [0, 128)
   void* y2; int y2_cs;                            // B: optional second copy
+  long long* dbg;                                 // optional [grid][12] phase stamps (s_memrealtime, tools/gru_split_phases.py)
 };
 int jr_gru_split(const GruSplitParams* p, int cfg, hipStream_t stream);
 // table entry {pb, cb, kc, cbw, pbw} of a gru_split config (0: unknown)

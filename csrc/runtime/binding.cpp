@@ -886,7 +886,13 @@ static Launch make_gru_split(const TList& t, const IList& i, std::vector<at::Ten
   const int64_t runs = (int64_t)p.lines * p.rpl;
   p.ptiles = (int)((runs + p.J - 1) / p.J);
   p.ctiles = nout / (32 * CB);
-  if (keep) for (auto& v : {src, w, bmap, zb, rh, h32, y, y2}) if (v.defined()) keep->push_back(v);
+  at::Tensor dbg = opt(t, 8);   // optional phase stamps (int64 [grid][12])
+  if (dbg.defined()) {
+    TORCH_CHECK(dbg.scalar_type() == at::kLong && dbg.is_cuda() &&
+                    dbg.numel() >= (int64_t)((p.ptiles + 7) / 8 * 8) * p.ctiles * 12, "gru_split: dbg [grid][12] int64");
+    p.dbg = (long long*)dbg.data_ptr();
+  }
+  if (keep) for (auto& v : {src, w, bmap, zb, rh, h32, y, y2, dbg}) if (v.defined()) keep->push_back(v);
   return [p, cfg](hipStream_t s, int) { return jr_gru_split(&p, cfg, s); };
 }
 

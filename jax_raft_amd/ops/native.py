@@ -160,7 +160,7 @@ def gru_halo_candidates(hd: int, mode: int, axis: int, N: int, H: int, W: int) -
 
 
 # gru_split.hip tile configs (cfg id = index): (pixel blocks PB, channel blocks CB, slab channels KC)
-GRU_SPLIT_CFGS = ((8, 2, 64), (8, 4, 32), (4, 2, 64), (4, 1, 64), (2, 2, 64), (8, 1, 64))
+GRU_SPLIT_CFGS = ((8, 2, 64), (8, 4, 32), (4, 2, 64), (4, 1, 64), (2, 2, 64), (8, 1, 64), (8, 2, 64), (4, 2, 64))
 
 
 def pack_gru_split(kernel: torch.Tensor, cb: int, kc: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
