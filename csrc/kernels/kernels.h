@@ -400,26 +400,6 @@ struct GruHaloParams {
 };
 int jr_gru_halo(const GruHaloParams* p, hipStream_t stream);
 
-// Channel-split ConvGRU stage (gru_split.hip): raft_large's 1x5 / 5x1 stages as two launches,
-// mode 0 (A): z -> zb, r*h -> rh from src = hx; mode 1 (B): q + blend from src = qx ([r*h | x]).
-// A tile = J runs of up to L pixels along the tap axis; ptiles x ctiles workgroups.
-struct GruSplitParams {
-  const void* src; int src_cs; long src_bytes;   // bf16 [M][src_cs] (256 loop channels)
-  const void* w; long w_bytes;                    // ops/native.py:pack_gru_split
-  const void* bmap; int bmap_cs;                  // bf16 [M][bmap_cs]: [z | r | q] context share + biases
-  int N, H, W, axis;                              // axis 0: 1x5 (taps along W), 1: 5x1
-  int L, J, rpl, lines, ptiles, ctiles;           // run length, runs per tile, runs per line, lines
-  int mode;                                       // 0: A, 1: B
-  void* zb;                                       // bf16 [M][128] z (A writes, B reads)
-  void* rh; int rh_cs;                            // A: bf16 r*h -> channels [0, 128)
-  float* h32;                                     // B: fp32 [M][128] hidden state, updated in place
-  void* y; int y_cs;                              // B: bf16 h' -> channels [0, 128)
-  void* y2; int y2_cs;                            // B: optional second copy
-  long long* dbg;                                 // optional [grid][12] phase stamps (s_memrealtime, tools/gru_split_phases.py)
-};
-int jr_gru_split(const GruSplitParams* p, int cfg, hipStream_t stream);
-// table entry {pb, cb, kc, cbw, pbw} of a gru_split config (0: unknown)
-int jr_gru_split_cfg(int cfg, int* out5);
 // LDS bytes of one workgroup (0: the configuration is not supported)
 int jr_gru_halo_lds(int hd, int mode, int TR, int TC, int nb1, int nb2);
 // Halo 3x3 / stride-1 conv (conv_halo.hip): a TR x TC tile of output pixels per workgroup,

@@ -827,75 +827,6 @@ static Launch make_gru_halo(const TList& t, const IList& i, std::vector<at::Tens
   return [p](hipStream_t s, int) { return jr_gru_halo(&p, s); };
 }
 
-// Channel-split ConvGRU stage launch (gru_split.hip).
-// t = [src (bf16 [M][256]: hx for mode 0, qx = [r*h | x] for mode 1), w (pack_gru_split of the mode's
-//      weights), bmap (bf16 [M][>= 384]), zb (bf16 [M][128]), rh (mode 0: bf16 [M][>= 128], r*h ->
-//      channels [0, 128)), h32 (mode 1: fp32 [M][128]), y (mode 1: bf16 [M][>= 128]), y2?],
-// i = [N, H, W, axis, mode, L, J, cfg]
-static Launch make_gru_split(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
-  at::Tensor src = opt(t, 0), w = opt(t, 1), bmap = opt(t, 2), zb = opt(t, 3), rh = opt(t, 4), h32 = opt(t, 5),
-             y = opt(t, 6), y2 = opt(t, 7);
-  TORCH_CHECK(i.size() == 8, "gru_split: expected [N, H, W, axis, mode, L, J, cfg]");
-  check_bf16(src, "src"); check_bf16(w, "w"); check_bf16(bmap, "bmap"); check_bf16(zb, "zb");
-  GruSplitParams p{};
-  p.N = (int)i[0]; p.H = (int)i[1]; p.W = (int)i[2]; p.axis = (int)i[3]; p.mode = (int)i[4];
-  p.L = (int)i[5]; p.J = (int)i[6];
-  const int cfg = (int)i[7];
-  int c5[5];
-  TORCH_CHECK(jr_gru_split_cfg(cfg, c5), "gru_split: unknown config ", cfg);
-  const int PB = c5[0], CB = c5[1];
-  const int64_t M = (int64_t)p.N * p.H * p.W;
-  TORCH_CHECK(p.N >= 1 && p.H >= 1 && p.W >= 1 && M < (1LL << 31), "gru_split: map size");
-  TORCH_CHECK(p.axis == 0 || p.axis == 1, "gru_split: axis must be 0 (1x5) or 1 (5x1)");
-  TORCH_CHECK(p.mode == 0 || p.mode == 1, "gru_split: mode must be 0 (z, r*h) or 1 (q, blend)");
-  const int len = p.axis ? p.H : p.W;
-  TORCH_CHECK(p.L >= 1 && p.L <= len && p.J >= 1 && p.J * p.L <= 32 * PB && p.J * (p.L + 4) <= 36 * PB,
-              "gru_split: tile of ", p.J, " runs x ", p.L, " pixels does not fit config ", cfg);
-  TORCH_CHECK(cs(src) == 256 && src.numel() >= M * 256, "gru_split: src [M][256]");
-  const int nout = p.mode ? 128 : 256;
-  TORCH_CHECK(nout % (32 * CB) == 0, "gru_split: channel tile");
-  TORCH_CHECK(w.numel() == (int64_t)nout * 5 * 256, "gru_split: packed weights (pack_gru_split) of ", nout, " channels");
-  TORCH_CHECK(cs(bmap) >= 384 && cs(bmap) % 8 == 0 && bmap.numel() >= M * cs(bmap), "gru_split: bias map [M][>= 384]");
-  TORCH_CHECK(cs(zb) == 128 && zb.numel() >= M * 128, "gru_split: zb [M][128]");
-  if (p.mode == 0) {
-    check_bf16(rh, "rh");
-    TORCH_CHECK(cs(rh) % 8 == 0 && cs(rh) >= 128 && rh.numel() >= M * cs(rh) && rh.data_ptr() != src.data_ptr(),
-                "gru_split: rh [M][>= 128], not the source");
-    p.rh = rh.data_ptr(); p.rh_cs = cs(rh);
-  } else {
-    check_f32(h32, "h32"); check_bf16(y, "y");
-    TORCH_CHECK(cs(h32) == 128 && h32.numel() >= M * 128, "gru_split: h32 [M][128]");
-    TORCH_CHECK(cs(y) % 8 == 0 && cs(y) >= 128 && y.numel() >= M * cs(y) && y.data_ptr() != src.data_ptr(),
-                "gru_split: y [M][>= 128], not the source");
-    p.h32 = h32.data_ptr<float>(); p.y = y.data_ptr(); p.y_cs = cs(y);
-    if (y2.defined()) {
-      check_bf16(y2, "y2");
-      TORCH_CHECK(cs(y2) % 8 == 0 && cs(y2) >= 128 && y2.numel() >= M * cs(y2), "gru_split: y2 [M][>= 128]");
-      p.y2 = y2.data_ptr(); p.y2_cs = cs(y2);
-    }
-  }
-  for (const at::Tensor* v : {&src, &w, &bmap, &zb, &rh, &h32, &y, &y2})
-    if (v->defined()) TORCH_CHECK(reinterpret_cast<uintptr_t>(v->data_ptr()) % 16 == 0, "gru_split: 16-byte aligned operands");
-  p.src = src.data_ptr(); p.src_cs = 256; p.src_bytes = (long)src.numel() * 2;
-  p.w = w.data_ptr(); p.w_bytes = (long)w.numel() * 2;
-  p.bmap = bmap.data_ptr(); p.bmap_cs = cs(bmap);
-  p.zb = zb.data_ptr();
-  TORCH_CHECK(p.src_bytes < (1LL << 31) && p.w_bytes < (1LL << 31), "gru_split: buffers larger than 2 GiB");
-  p.rpl = (len + p.L - 1) / p.L;
-  p.lines = p.N * (p.axis ? p.W : p.H);
-  const int64_t runs = (int64_t)p.lines * p.rpl;
-  p.ptiles = (int)((runs + p.J - 1) / p.J);
-  p.ctiles = nout / (32 * CB);
-  at::Tensor dbg = opt(t, 8);   // optional phase stamps (int64 [grid][12])
-  if (dbg.defined()) {
-    TORCH_CHECK(dbg.scalar_type() == at::kLong && dbg.is_cuda() &&
-                    dbg.numel() >= (int64_t)((p.ptiles + 7) / 8 * 8) * p.ctiles * 12, "gru_split: dbg [grid][12] int64");
-    p.dbg = (long long*)dbg.data_ptr();
-  }
-  if (keep) for (auto& v : {src, w, bmap, zb, rh, h32, y, y2, dbg}) if (v.defined()) keep->push_back(v);
-  return [p, cfg](hipStream_t s, int) { return jr_gru_split(&p, cfg, s); };
-}
-
 // t = [fm (bf16 [M][cs]), wpk (bf16, pack_taps), taps (fp32 [M][>=24])], i = [M, K, fcoff]
 static Launch make_taps_gemm(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
   at::Tensor fm = opt(t, 0), wpk = opt(t, 1), taps = opt(t, 2);
@@ -1755,7 +1686,6 @@ void flow_taps_op(const TList& t, IList i) { run_now(make_flow_taps(t, i, nullpt
 void taps_gemm_op(const TList& t, IList i) { run_now(make_taps_gemm(t, i, nullptr)); }
 void gru_fused_op(const TList& t, IList i) { run_now(make_gru_fused(t, i, nullptr)); }
 void gru_halo_op(const TList& t, IList i) { run_now(make_gru_halo(t, i, nullptr)); }
-void gru_split_op(const TList& t, IList i) { run_now(make_gru_split(t, i, nullptr)); }
 bool conv_halo_ok_op(int64_t cfg, int64_t cin8, int64_t cout) { return conv_halo_ok_cfg(cfg, cin8, cout); }
 // t = [part (fp32 [N][nb][C][2]), stats (fp32 [N][C][2])], i = [N, nb, C]
 static Launch make_stats_final(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
@@ -1924,7 +1854,6 @@ class Plan : public torch::CustomClassHolder {
   void add_taps_gemm(TList t, IList i) { push(make_taps_gemm(t, i, &keep_), "taps_gemm"); }
   void add_gru_fused(TList t, IList i) { push(make_gru_fused(t, i, &keep_), "gru_fused"); }
   void add_gru_halo(TList t, IList i) { push(make_gru_halo(t, i, &keep_), "gru_halo"); }
-  void add_gru_split(TList t, IList i) { push(make_gru_split(t, i, &keep_), "gru_split"); }
   void add_stats_final(TList t, IList i) { push(make_stats_final(t, i, &keep_), "stats_final"); }
   void add_conv1x1(TList t, IList i) { push(make_conv1x1(t, i, &keep_), "conv1x1"); }
   void add_conv_direct(TList t, IList i) { push(make_conv_direct(t, i, &keep_), "conv_direct"); }
@@ -2391,7 +2320,6 @@ TORCH_LIBRARY(jax_raft_amd, m) {
   m.def("conv_grouped_ok(int cfg) -> bool", &jr::conv_grouped_ok_op);
   m.def("gru_fused_fits(int H, int W, int vertical) -> bool", &jr::gru_fused_fits);
   m.def("gru_halo(Tensor?[] t, int[] i) -> ()", &jr::gru_halo_op);
-  m.def("gru_split(Tensor?[] t, int[] i) -> ()", &jr::gru_split_op);
   m.def("conv_halo_ok(int cfg, int cin8, int cout) -> bool", &jr::conv_halo_ok_op);
   m.def("stats_final(Tensor?[] t, int[] i) -> ()", &jr::stats_final_op);
   m.def("conv_halo_cfg(int cfg) -> int[]", &jr::conv_halo_cfg_op);
@@ -2451,7 +2379,6 @@ TORCH_LIBRARY(jax_raft_amd, m) {
       .def("add_taps_gemm", &jr::Plan::add_taps_gemm)
       .def("add_gru_fused", &jr::Plan::add_gru_fused)
       .def("add_gru_halo", &jr::Plan::add_gru_halo)
-      .def("add_gru_split", &jr::Plan::add_gru_split)
       .def("add_stats_final", &jr::Plan::add_stats_final)
       .def("add_flowin_dual", &jr::Plan::add_flowin_dual)
       .def("add_conv_group", &jr::Plan::add_conv_group)

@@ -44,7 +44,6 @@ KERNEL_SOURCES = [
     CSRC / "kernels" / "conv1x1.hip",
     CSRC / "kernels" / "gru_fused.hip",
     CSRC / "kernels" / "gru_halo.hip",
-    CSRC / "kernels" / "gru_split.hip",
     CSRC / "kernels" / "conv_halo.hip",
     CSRC / "kernels" / "bgemm.hip",
     CSRC / "kernels" / "merged.hip",

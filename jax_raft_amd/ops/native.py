@@ -159,60 +159,6 @@ def gru_halo_candidates(hd: int, mode: int, axis: int, N: int, H: int, W: int) -
     return res
 
 
-# gru_split.hip tile configs (cfg id = index): (pixel blocks PB, channel blocks CB, slab channels KC)
-GRU_SPLIT_CFGS = ((8, 2, 64), (8, 4, 32), (4, 2, 64), (4, 1, 64), (2, 2, 64), (8, 1, 64), (8, 2, 64), (4, 2, 64))
-
-
-def pack_gru_split(kernel: torch.Tensor, cb: int, kc: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """ConvGRU gate kernel (1, 5, 256, cout) / (5, 1, 256, cout) HWIO -> gru_split.hip's weight
-    layout: bf16 [cout / (32 cb)][256 / kc][5 taps][kc / 16][cb][64][8] -- per channel tile, one
-    contiguous block per kc-channel slab holding every fragment of that slab in MFMA order (the
-    fragments of pack_gru_halo, regrouped: lane l, element j = W[tap, 16 s + 8 (l >> 5) + j,
-    co = 32 blk + _m32_chan(l & 31)])."""
-    kh, kw, cin, cout = kernel.shape
-    assert kh * kw == 5 and cin <= 256 and cout % (32 * cb) == 0 and 256 % kc == 0, (kernel.shape, cb, kc)
-    w = pack_gru_halo(kernel, 256)                       # [cout/32][5 * 16][64][8]
-    ct, ns, kk = cout // (32 * cb), 256 // kc, kc // 16
-    w = w.view(ct, cb, 5, ns, kk, 64, 8).permute(0, 3, 2, 4, 1, 5, 6).contiguous()
-    if out is not None:
-        assert out.shape == w.shape and out.dtype == torch.bfloat16
-        out.copy_(w)
-        return out
-    return w
-
-
-def gru_split_tile(cfg: int, axis: int, N: int, H: int, W: int) -> Tuple[int, int]:
-    """(L, J) of a gru_split config: runs of L <= 32 PB pixels along the tap axis (balanced
-    segments of a longer line), J runs per tile within the config's pixel blocks and footprint."""
-    pb = GRU_SPLIT_CFGS[cfg][0]
-    length = H if axis else W
-    segs = -(-length // (32 * pb))
-    L = -(-length // segs)
-    J = max(1, min((32 * pb) // L, (36 * pb) // (L + 4)))
-    return L, J
-
-
-def gru_split_candidates(mode: int, axis: int, N: int, H: int, W: int) -> List[Tuple[int, int, int]]:
-    """(cfg, L, J) of the gru_split configs worth timing for one launch (mode 0: the 256 z / r
-    channels, 1: the 128 q channels): those whose workgroup count fills at least half the CUs."""
-    nout = 256 if mode == 0 else 128
-    out = []
-    for cfg, (pb, cb, kc) in enumerate(GRU_SPLIT_CFGS):
-        if nout % (32 * cb):
-            continue
-        L, J = gru_split_tile(cfg, axis, N, H, W)
-        length = H if axis else W
-        lines = N * (W if axis else H)
-        runs = lines * -(-length // L)
-        wgs = -(-runs // J) * (nout // (32 * cb))
-        if wgs >= NUM_CUS // 2:
-            out.append((cfg, L, J))
-    if not out:   # tiny maps: the smallest tiles
-        cfg = 4 if mode == 0 else 3
-        out.append((cfg,) + gru_split_tile(cfg, axis, N, H, W))
-    return out
-
-
 def load(build_if_missing: bool = True) -> None:
     """Load ``_C.so`` (building it with hipcc first if it is missing)."""
     global _loaded, _load_error

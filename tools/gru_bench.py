@@ -91,24 +91,6 @@ def main():
                 continue
             bestb = tb if bestb is None else min(bestb, tb)
         print(f"  two-launch GEMM path (best tile configs): {best:7.2f} + {bestb:7.2f} = {best + bestb:7.2f} us")
-        if large:   # channel-split two-launch kernel (gru_split.hip): every config of each launch
-            qx = torch.randn(M, cs, device=dev).to(torch.bfloat16)
-            ta = {}
-            for cfg, L, J in nat.gru_split_candidates(0, axis, B, h, w):
-                pc = nat.GRU_SPLIT_CFGS[cfg]
-                wsa = nat.pack_gru_split(kzr, pc[1], pc[2])
-                ta[cfg] = graph_time(lambda: nat.ops().gru_split([src, wsa, bm, zb, qx, None, None, None],
-                                                                 [B, h, w, axis, 0, L, J, cfg]), a.reps)
-            tb = {}
-            for cfg, L, J in nat.gru_split_candidates(1, axis, B, h, w):
-                pc = nat.GRU_SPLIT_CFGS[cfg]
-                wsb = nat.pack_gru_split(kq, pc[1], pc[2])
-                tb[cfg] = graph_time(lambda: nat.ops().gru_split([qx, wsb, bm, zb, None, h32, dst, None],
-                                                                 [B, h, w, axis, 1, L, J, cfg]), a.reps)
-            fa, fb = min(ta, key=ta.get), min(tb, key=tb.get)
-            print("  gru_split A: " + " ".join(f"cfg{c}={t:.2f}" for c, t in ta.items())
-                  + "  B: " + " ".join(f"cfg{c}={t:.2f}" for c, t in tb.items())
-                  + f"  best {ta[fa]:.2f} + {tb[fb]:.2f} = {ta[fa] + tb[fb]:.2f} us")
         if large and nat.ops().gru_fused_fits(h, w, axis):
             wpa, wpb = sa.w, sb.w
             t = graph_time(lambda: nat.ops().gru_fused([src, wpa, wpb, bm, h32, src, None], [B, h, w, axis]), a.reps)
