@@ -58,16 +58,18 @@ GROUPS["none"] = lambda n: False
 
 
 @contextlib.contextmanager
-def emulate(model, pred, corr_bf16: bool, parts: str = "xwy"):
-    """parts: which operands of the selected convs are bf16 -- x (input), w (kernel), y (output)."""
+def emulate(model, pred, corr_bf16: bool, parts="xwy"):
+    """parts: which operands of the selected convs are bf16 -- x (input), w (kernel), y (output);
+    a callable name -> parts string gives per-conv choices."""
     names = {id(m): n for n, m in model.named_modules()}
     orig_conv = L.Conv.forward
-    orig_pyr = R.build_pyramid if hasattr(R, "build_pyramid") else None
+    parts_of = parts if callable(parts) else (lambda n, _p=parts: _p)
 
     def fwd(self, x):
         n = names.get(id(self), "")
         if not pred(n):
             return orig_conv(self, x)
+        parts = parts_of(n)
         y = R.conv2d_nhwc(rb(x) if "x" in parts else x, rb(self.kernel) if "w" in parts else self.kernel, self.bias,
                           self.stride, self.padding)
         # the GRU gates / flow-head output feed fp32 state in the engine: keep those fp32
@@ -116,6 +118,29 @@ def main():
         for v in a.variants.split(","):
             # variant: groups joined by '&' (a '!' prefix: everything BUT that group), then optional
             # '+corr' (bf16 pyramid) and '+parts=xw' (only those operands rounded)
+            if ";" in v:   # per-group parts: "fe=xy;!fe=xwy[+corr]"
+                corr = v.endswith("+corr")
+                specs = []
+                for tok in v.replace("+corr", "").split(";"):
+                    g, pp = tok.split("=")
+                    neg = g.startswith("!")
+                    specs.append((GROUPS[g.lstrip("!")], neg, pp))
+
+                def parts_of(n, specs=specs):
+                    for f, neg, pp in specs:
+                        if f(n) != neg:
+                            return pp
+                    return ""
+
+                with emulate(model, lambda n: True, corr, parts_of):
+                    t = time.time()
+                    o = model(i1, i2, num_flow_updates=a.iters)
+                rel = [drift.epe(o[k], ref[k]) / mags[k].item() for k in range(a.iters)]
+                out[v] = rel
+                pick = [0, 1, 3, 7, 11, 15, 23, 31]
+                print(f"{v:24s} rel EPE " + " ".join(f"it{k + 1}={rel[k]:.2e}" for k in pick if k < a.iters)
+                      + f"  ({time.time() - t:.1f} s)", flush=True)
+                continue
             toks = v.split("+")
             groups, corr = toks[0], "corr" in toks[1:]
             parts = next((t.split("=")[1] for t in toks[1:] if t.startswith("parts=")), "xwy")
