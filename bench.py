@@ -75,6 +75,7 @@ class Ctx:
         local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         ndev = torch.cuda.device_count()
         self.gloo = args.dist_backend == "gloo"
+        self.step_times = bool(getattr(args, "step_times", False))
         idx = local_rank % ndev if self.gloo else local_rank
         torch.cuda.set_device(idx)
         self.dev = torch.device("cuda", idx)
@@ -252,7 +253,7 @@ def run_inference(ctx: Ctx, model, *, B: int, H: int, W: int, iters: int, steps:
         eng.flush()   # the last prologue's batch (untimed)
         torch.cuda.synchronize(dev)
     step_ms = [events[i].elapsed_time(events[i + 1]) for i in range(steps)]
-    if os.environ.get("JR_BENCH_STEPS") == "1":   # per-step device times in order (diagnostics)
+    if ctx.step_times:   # per-step device times in order (diagnostics)
         print("step_ms " + " ".join(f"{t:.2f}" for t in step_ms), file=sys.stderr, flush=True)
     step_ms.sort()
     pct = lambda q: round(step_ms[min(len(step_ms) - 1, int(q * len(step_ms)))], 3)
@@ -397,6 +398,7 @@ def main():
     ap.add_argument("--extras", default="auto", choices=["auto", "on", "off"],
                     help="secondary configs after the headline (auto: on for the default headline config)")
     ap.add_argument("--extra-steps", type=int, default=20)
+    ap.add_argument("--step-times", action="store_true", help="print every timed step's device time (stderr)")
     ap.add_argument("--train-batch", type=int, default=6, help="extras: training batch per GPU (config 5: 6)")
     ap.add_argument("--train-size", type=int, nargs=2, default=[384, 512], help="extras: training image size")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],

@@ -14,10 +14,8 @@ extern "C" int jr_convex_head(const void* feat, int feat_cstride, int feat_coff,
   const int nc = tiles == 1 || tiles == 2 ? tiles : blocks(2) * 4 >= 384 ? 2 : 1;
   const int nblk = blocks(nc);
   // the persistent form when the grid would take more than one round (128 slots x 4 groups = 2 blocks
-  // per CU): 23.3 -> 20.3 us at raft_large batch 4 (profiles/r4_convex_persist_ab.txt);
-  // JR_CONVEX_PERSIST=0: always the one-pixel-block-per-workgroup form
-  static const bool persist = getenv("JR_CONVEX_PERSIST") == nullptr || getenv("JR_CONVEX_PERSIST")[0] != '0';
-  if (persist && nblk > 128) {
+  // per CU): 23.3 -> 20.3 us at raft_large batch 4 (profiles/r4_convex_persist_ab.txt)
+  if (nblk > 128) {
     const int nslot = 128;
     const dim3 pg(nslot / 8 * 32);
     if (nc == 2)

@@ -656,8 +656,7 @@ extern "C" int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int
   // the persistent kernel (corr_pyr.hip) holds every CU for the whole build: at batch 1 the
   // pipelined graph runs the previous pair's loop concurrently, and the short-lived tiles of
   // the kernel below interleave with it (measured b1 stream 227 vs 200-204 FPS)
-  static const bool tile_pyr = getenv("JR_PYR_TILE") != nullptr;   // A/B: always the tile kernel
-  if (blocked && nq == h * w && B >= 2 && !tile_pyr) {
+  if (blocked && nq == h * w && B >= 2) {
     const int e = jr_corr_pyramid_blocked(f1, f2, B, h, w, C, cs, lvl0, lvl1, lvl2, lvl3, num_levels, scale, stream);
     if (e != (int)hipErrorNotSupported) return e;
   }

@@ -380,13 +380,9 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
 
 extern "C" int jr_gru_fused(const GruFusedParams* p, hipStream_t stream) {
   if (p->ntiles <= 0) return 0;
-  // GEMM 2 on all 16 waves with z through LDS (default; measured 334-341 vs 335 pairs/s at the
-  // headline, profiles/r3_gru_fused_ab.txt) or on the 8 z waves with z in registers (JR_GRU_G2=0)
-  static const int g2all = [] {   // read once per process, not on every (graph-captured) launch
-    const char* g2 = std::getenv("JR_GRU_G2");
-    return g2 ? std::atoi(g2) : 1;
-  }();
-  if (g2all) hipLaunchKernelGGL(gru_fused_kernel<true>, dim3(p->ntiles), dim3(1024), 0, stream, *p);
+  // GEMM 2 on all 16 waves with z through LDS (the engine's choice) or on the 8 z waves with z
+  // in registers (p->g2all = 0; profiles/r3_gru_fused_ab.txt)
+  if (p->g2all) hipLaunchKernelGGL(gru_fused_kernel<true>, dim3(p->ntiles), dim3(1024), 0, stream, *p);
   else hipLaunchKernelGGL(gru_fused_kernel<false>, dim3(p->ntiles), dim3(1024), 0, stream, *p);
   return (int)hipGetLastError();
 }

@@ -366,6 +366,7 @@ struct GruFusedParams {
   int N, H, W;
   int vertical;                       // 0: 1x5 taps along W, tiles = image rows; 1: 5x1, tiles = J columns
   int L, J, tiles_per_img, ntiles;    // run length (W or H), runs per tile (J * L <= 128)
+  int g2all;                          // 1: GEMM 2 on all 16 waves (z through LDS); 0: on the 8 z waves
   long hx_bytes, wa_bytes, wb_bytes;
   long long* dbg;                     // optional [ntiles][6] phase timestamps (s_memrealtime, tools/gru_phases.py)
 };

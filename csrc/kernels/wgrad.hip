@@ -494,8 +494,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_halo_kernel(const WgHaloParams p
 // the halo path serves 3x3 / stride-1 / pad-1 convs; S: splits of the pixel tiles so that the
 // (split x channel block) grid is about one round of resident workgroups (one per CU: ~480 registers)
 inline bool wgrad_halo_ok(int KH, int KW, int SH, int SW, int PH, int PW) {
-  static const bool off = std::getenv("JR_WGRAD_HALO") != nullptr && std::getenv("JR_WGRAD_HALO")[0] == '0';
-  return !off && KH == 3 && KW == 3 && SH == 1 && SW == 1 && PH == 1 && PW == 1;
+  return KH == 3 && KW == 3 && SH == 1 && SW == 1 && PH == 1 && PW == 1;
 }
 inline void wgrad_halo_geom(int N, int H, int W, int cin8, int cout, int* ntiles, int* nco, int* nci, int* S, int* tps) {
   const int tx = (W + HTC - 1) / HTC, ty = (H + HTR - 1) / HTR;
@@ -571,7 +570,6 @@ extern "C" int jr_wgrad(const void* x, int xcs, int xoff, int N, int H, int W, i
                        h.bpart, s, cp, kp, KH, KW, cin8, cin, cout, dw, db);
     return (int)hipGetLastError();
   }
-  if (const char* e = std::getenv("JR_WGRAD_S")) S = std::max(1, std::min(S, atoi(e)));  // tuning probe (<= planned S)
   const int per = (p.M + S - 1) / S;
   p.px_split = (per + WPX - 1) / WPX * WPX;
   S = (p.M + p.px_split - 1) / p.px_split;

@@ -126,16 +126,20 @@ static ConvParams build_conv(const TList& t, const IList& i, double alpha, std::
   const int epi = (int)i[19];
   {
     const int taps = p.KH * p.KW;
-    p.fast = p.dsh == 0 && p.dsw == 0 && taps <= 32 && (taps == 1 || p.cin8 % 64 == 0) && !std::getenv("JR_CONV_NO_FAST");
-    p.xcd_remap = std::getenv("JR_CONV_XCD") ? 1 : 0;  // measured: -0.5..1.4 % on the RAFT convs (inputs MALL-resident)
+    p.fast = p.dsh == 0 && p.dsw == 0 && taps <= 32 && (taps == 1 || p.cin8 % 64 == 0);
   }
   int cfg = (int)i[20];
   // Timing-only ablation (tools/microbench.py --ablate): cfg bits 8/9 give the
   // X / W buffer descriptors zero records, so every load through them is
   // dropped by the range check while the instruction stream stays the same.
+  // Lowering variants (same results; tests and microbench A/B): bit 10 = XCD-aware tile
+  // order (conv_igemm.h:tile_of_block; measured -0.5..1.4 % on the RAFT convs, whose inputs
+  // are MALL-resident, so off by default), bit 11 = the generic im2col loader instead of FAST.
   if (cfg >> 8) {
     if ((cfg >> 8) & 1) p.x_bytes = 0;
     if ((cfg >> 8) & 2) p.w_bytes = 0;
+    p.xcd_remap = (cfg >> 10) & 1;
+    if ((cfg >> 11) & 1) p.fast = 0;
     cfg &= 255;
   }
   // Shape / alignment contract of conv_igemm.hip.
@@ -659,14 +663,17 @@ bool gru_fused_fits(int64_t H, int64_t W, int64_t vertical) {
 // Fused ConvGRU stage (gru_fused.hip).  t = [hx (bf16 [M][256]: h | x), wa (pack_weight of [z | r],
 // [256][1280]), wb (pack_weight of q, [128][1280]), bmap ([M][>=384] fp32 / bf16: z | r | q context
 // share), h32 (fp32 [M][128], in place), y (bf16 [M][ycs], channels [0, 128)), y2 (optional copy)],
-// i = [N, H, W, vertical].  Tiles: a row (1x5, W <= 128) or J = 2 / 1 columns (5x1, J * H <= 128).
+// i = [N, H, W, vertical(, g2all)].  Tiles: a row (1x5, W <= 128) or J = 2 / 1 columns (5x1, J * H <= 128).
+// g2all (default 1): GEMM 2 on all 16 waves with z through LDS; 0: on the 8 z waves, z in registers
+// (measured 334-341 vs 335 pairs/s at the headline, profiles/r3_gru_fused_ab.txt; kept for the tests).
 static Launch make_gru_fused(const TList& t, const IList& i, std::vector<at::Tensor>* keep) {
   at::Tensor hx = opt(t, 0), wa = opt(t, 1), wb = opt(t, 2), bmap = opt(t, 3), h32 = opt(t, 4), y = opt(t, 5),
              y2 = opt(t, 6), dbg = opt(t, 7);
   check_bf16(hx, "hx"); check_bf16(wa, "wa"); check_bf16(wb, "wb"); check_f32(h32, "h32"); check_bf16(y, "y");
-  TORCH_CHECK(i.size() == 4, "gru_fused: expected 4 ints");
+  TORCH_CHECK(i.size() == 4 || i.size() == 5, "gru_fused: expected 4 or 5 ints");
   GruFusedParams p{};
   p.N = (int)i[0]; p.H = (int)i[1]; p.W = (int)i[2]; p.vertical = (int)i[3];
+  p.g2all = i.size() == 5 ? (int)(i[4] != 0) : 1;
   const int64_t M = (int64_t)p.N * p.H * p.W;
   TORCH_CHECK(gru_fused_fits(p.H, p.W, p.vertical), "gru_fused: the tile geometry does not fit (", p.H, "x", p.W, ")");
   TORCH_CHECK(cs(hx) == 256 && hx.numel() >= M * 256 && reinterpret_cast<uintptr_t>(hx.data_ptr()) % 16 == 0,
@@ -1391,9 +1398,9 @@ static void check_f32_min(const at::Tensor& t, const char* name, int64_t n) {
 
 // t = [x, w ([cout][K] fp32), bias, y, y2, res, h32, zbuf, bmap]
 // i = [N, H, W, x_coff, cin4, KH, KW, SH, SW, PH, PW, cout, act, split, y_coff, y2_coff, res_coff, res_post,
-//      hidden, bmap_coff, epi]
+//      hidden, bmap_coff, epi, ksplit (0: automatic, n > 0: forced n-way split-K)]
 static Launch make_conv_f32(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep) {
-  TORCH_CHECK(i.size() == 21, "conv_f32: expected 21 ints");
+  TORCH_CHECK(i.size() == 22, "conv_f32: expected 22 ints");
   at::Tensor x = opt(t, 0), w = opt(t, 1), bias = opt(t, 2), y = opt(t, 3), y2 = opt(t, 4), res = opt(t, 5);
   at::Tensor h32 = opt(t, 6), zbuf = opt(t, 7), bmap = opt(t, 8);
   ConvF32Params p{};
@@ -1444,13 +1451,13 @@ static Launch make_conv_f32(const TList& t, const IList& i, double alpha, std::v
   p.bmap = bmap.defined() ? bmap.data_ptr<float>() : nullptr;
   // split-K when the grid holds fewer than 4 blocks per CU (the batch-1 loop convs:
   // 110-440 blocks on 256 CUs, one 4-wave block per CU leaves the f32 MFMA pipe ~half
-  // idle): aim at ~1536 blocks, >= 8 K stages per split.  JR_F32_KSPLIT=<n> forces n.
+  // idle): aim at ~1536 blocks, >= 8 K stages per split.  i[21] = n > 0 forces n (tests).
   {
     const long blocks = (long)((p.M + 63) / 64) * ((p.cout + 63) / 64);
     const int nks = (p.K + 31) / 32;
     int S = 1;
     if (blocks < 1024) S = (int)std::min<long>({8L, (1536 + blocks - 1) / blocks, (long)std::max(1, nks / 8)});
-    if (const char* e = std::getenv("JR_F32_KSPLIT")) S = std::max(1, std::min(std::atoi(e), std::max(1, nks / 8)));
+    if (i[21] > 0) S = std::max(1, std::min((int)i[21], std::max(1, nks / 8)));
     p.ksplit = S;
     if (S > 1) {
       at::Tensor part = at::empty({(int64_t)S * p.M * ((p.cout + 3) / 4 * 4)}, x.options());
@@ -1953,23 +1960,18 @@ class Plan : public torch::CustomClassHolder {
     hipGraph_t g = nullptr;
     TORCH_CHECK(hipGraphCreate(&g, 0) == hipSuccess, "graph create");
     pipe_graph_ = g;
-    // loop nodes first (the executor launches in creation order); JR_PIPE_PROLOGUE=first
-    // creates the prologue's first (A/B: batch 1 157 -> 78 pairs/s, the two phases then
-    // run one after the other).  (The prologue as one child-graph node, i.e. its nodes
-    // in order on one stream, measured 264 vs 289 pairs/s at batch 4.)
-    const char* pm = std::getenv("JR_PIPE_PROLOGUE");
-    const bool pro_first = pm && std::string(pm) == "first";
+    // loop nodes first (the executor launches in creation order; the prologue's first
+    // measured batch 1 157 -> 78 pairs/s, the two phases then run one after the other).
+    // (The prologue as one child-graph node, i.e. its nodes in order on one stream,
+    // measured 264 vs 289 pairs/s at batch 4.)
     // One empty root node ahead of both branches: the executor forks a node's successors
     // onto parallel streams, but runs disconnected components in creation order on the
-    // launch stream (measured: 21.6 us of a 3.2 ms raft_small batch-1 step concurrent,
-    // profiles/r5_pipeline_fork_ab.txt: raft_small b1 12 it 788 vs 713 pairs/s).  JR_PIPE_FORK=0: no root (A/B).
+    // launch stream (measured: 21.6 us of a 3.2 ms raft_small batch-1 step concurrent;
+    // with the root raft_small b1 12 it 788 vs 713 pairs/s, profiles/r5_pipeline_fork_ab.txt).
     hipGraphNode_t root = nullptr;
-    const char* fk = std::getenv("JR_PIPE_FORK");
-    if (!(fk && std::string(fk) == "0"))
-      TORCH_CHECK(hipGraphAddEmptyNode(&root, g, nullptr, 0) == hipSuccess, "graph root");
-    if (pro_first) append_graph(g, next->pgraph_[0], root);
+    TORCH_CHECK(hipGraphAddEmptyNode(&root, g, nullptr, 0) == hipSuccess, "graph root");
     append_graph(g, pgraph_[1], root);
-    if (!pro_first) append_graph(g, next->pgraph_[0], root);
+    append_graph(g, next->pgraph_[0], root);
     hipError_t e3 = hipGraphInstantiate(&pipe_exec_, g, nullptr, nullptr, 0);
     if (debug_) fprintf(stderr, "[plan] pipelined instantiate %d\n", (int)e3);
     TORCH_CHECK(e3 == hipSuccess, "graph instantiate failed: ", hipGetErrorString(e3));
@@ -2040,9 +2042,8 @@ class Plan : public torch::CustomClassHolder {
   void merge_reset() {
     reset_pipe();
     TORCH_CHECK(hipGraphCreate(&pipe_graph_, 0) == hipSuccess, "graph create");
-    const char* fk = std::getenv("JR_PIPE_FORK");   // one root: the parts fork (capture_pipelined)
-    if (!(fk && std::string(fk) == "0"))
-      TORCH_CHECK(hipGraphAddEmptyNode(&pipe_root_, pipe_graph_, nullptr, 0) == hipSuccess, "graph root");
+    // one root: the parts fork (capture_pipelined)
+    TORCH_CHECK(hipGraphAddEmptyNode(&pipe_root_, pipe_graph_, nullptr, 0) == hipSuccess, "graph root");
   }
   void merge_add(c10::intrusive_ptr<Plan> part, int64_t n_iters) {
     TORCH_CHECK(pipe_graph_ != nullptr && pipe_exec_ == nullptr, "merge_add: call merge_reset() first");
@@ -2086,7 +2087,6 @@ class Plan : public torch::CustomClassHolder {
     if (!cap_stream_) {
       int least = 0, greatest = 0;
       TORCH_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess, "priority range");
-      if (!use_priority()) greatest = 0;
       TORCH_CHECK(hipStreamCreateWithPriority(&cap_stream_, hipStreamNonBlocking, greatest) == hipSuccess, "stream");
     }
     return cap_stream_;
@@ -2150,11 +2150,6 @@ class Plan : public torch::CustomClassHolder {
     segs_[seg_].push_back(Op{Launch(), lane_, kind, (int)ev, std::string(name) + std::to_string(ev), defer_});
     reset_graph();
   }
-  // JR_LANE_PRIORITY=0 disables the lane priorities (A/B measurements)
-  static bool use_priority() {
-    const char* v = std::getenv("JR_LANE_PRIORITY");
-    return !(v && v[0] == '0');
-  }
   static int create_event(hipEvent_t* e) {
     return (int)hipEventCreateWithFlags(e, hipEventDisableTiming);
   }
@@ -2166,7 +2161,6 @@ class Plan : public torch::CustomClassHolder {
     if (!fork_) if (int r = create_event(&fork_)) return r;
     int least = 0, greatest = 0;
     if (int r = (int)hipDeviceGetStreamPriorityRange(&least, &greatest)) return r;
-    if (!use_priority()) least = greatest = 0;
     if (!lanes_[0]) if (int r = (int)hipStreamCreateWithPriority(&lanes_[0], hipStreamNonBlocking, greatest)) return r;
     if (!join_[0]) if (int r = create_event(&join_[0])) return r;
     for (int l = 1; l < used_lanes_; ++l) {

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Device time of the inference convex mask head (csrc/kernels/convex_head.h) at raft_large
-batch 4 (55 x 128 maps), as a captured graph of 30 launches; run twice with
-JR_CONVEX_PERSIST=0 / 1 (read once per process) to compare the two forms."""
+batch 4 (55 x 128 maps), as a captured graph of 30 launches (the persistent form above 128
+pixel blocks; the round-4 A/B of the two forms: profiles/r4_convex_persist_ab.txt)."""
 import os
 import sys
 
@@ -40,7 +40,7 @@ def main():
         e.synchronize()
         t = s.elapsed_time(e) * 1000 / 30
         best = t if best is None else min(best, t)
-    print(f"convex_head B={B} persist={os.environ.get('JR_CONVEX_PERSIST', '0')}: {best:.1f} us, "
+    print(f"convex_head B={B}: {best:.1f} us, "
           f"checksum {out.double().abs().sum().item():.6e}")
 
 

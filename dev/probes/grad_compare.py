@@ -46,9 +46,9 @@ def main():
     ref = grads(model, i1, i2, target, a.iters)
     model = model.cuda()
     res = {}
-    for name, env, kw in (("unfused", {}, dict(fused=False)), ("loop", {"JR_FUSED_ENCODERS": "0"}, dict(fused=True)),
-                          ("whole", {"JR_FUSED_ENCODERS": "1"}, dict(fused=True))):
-        os.environ.update(env)
+    for name, enc, kw in (("unfused", True, dict(fused=False)), ("loop", False, dict(fused=True)),
+                          ("whole", True, dict(fused=True))):
+        F.FUSED_ENCODERS = enc
         F._LOOPS.clear()
         model.load_state_dict(state)
         res[name] = grads(model, i1.cuda(), i2.cuda(), target, a.iters, **kw)

@@ -19,7 +19,7 @@ REPO = PKG_DIR.parent
 CSRC = REPO / "csrc"
 BUILD = REPO / "build" / "native"
 SO_PATH = PKG_DIR / "_C.so"
-ARCH = os.environ.get("JR_OFFLOAD_ARCH", "gfx950")
+ARCH = os.environ.get("JR_OFFLOAD_ARCH") or "gfx950"   # (documented in knobs.py; _build imports nothing)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 

@@ -17,7 +17,6 @@ is PyTorch glue on the framework layer.  ``coords`` never receive a gradient
 from __future__ import annotations
 
 import math
-import os
 import weakref
 from typing import List, Sequence, Tuple
 
@@ -76,18 +75,7 @@ def _cached_spec(kernel: torch.Tensor, bias, stride, padding, cin8: int, transpo
     return spec
 
 
-def _env_pos_int(name: str, default: int) -> int:
-    raw = os.environ.get(name, str(default))
-    try:
-        v = int(raw)
-    except ValueError:
-        raise ValueError(f"{name} must be a positive integer, got {raw!r}") from None
-    if v < 1:
-        raise ValueError(f"{name} must be >= 1, got {v}")
-    return v
-
-
-_WGRAD_TILES_PER_CU = _env_pos_int("JR_WGRAD_TILES_PER_CU", 2)
+_WGRAD_TILES_PER_CU = 2   # split-K target of the weight-gradient GEMMs: ~2 tiles per CU
 
 
 def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:

@@ -8,7 +8,6 @@ PyTorch ops.
 from __future__ import annotations
 
 import math
-import os
 import threading
 from dataclasses import dataclass
 from pathlib import Path
@@ -16,11 +15,12 @@ from typing import List, Optional, Sequence, Tuple
 
 import torch
 
+from .. import knobs
 from .._build import SO_PATH as _DEFAULT_SO
 
 # JR_NATIVE_SO: load another build of the library (e.g. the host-sanitizer
 # build _C_san.so, jax_raft_amd/_build.py --sanitize); default: the in-tree _C.so
-SO_PATH = Path(os.environ["JR_NATIVE_SO"]).resolve() if os.environ.get("JR_NATIVE_SO") else _DEFAULT_SO
+SO_PATH = Path(knobs.get("JR_NATIVE_SO")).resolve() if knobs.get("JR_NATIVE_SO") else _DEFAULT_SO
 
 _lock = threading.Lock()
 _loaded = False
@@ -265,8 +265,8 @@ def pack_halo_conv(kernel: torch.Tensor, cin8: int, out: Optional[torch.Tensor] 
 
 def halo_cfgs_for(spec: "ConvSpec", kw: dict) -> Tuple[int, ...]:
     """Halo conv configs that can run this conv (shape, epilogue, channel count).
-    ``JR_CONV_HALO=0`` removes them from every candidate set (A/B measurements)."""
-    if spec.wh is None or not spec.halo_shape or os.environ.get("JR_CONV_HALO", "1") == "0":
+    """
+    if spec.wh is None or not spec.halo_shape:
         return ()
     if kw.get("epi", EPI_STD) != EPI_STD or kw.get("act", ACT_NONE) not in (ACT_NONE, ACT_RELU):
         return ()
@@ -576,11 +576,12 @@ def make_spec_f32(kernel: torch.Tensor, bias: torch.Tensor, stride=(1, 1), paddi
 def conv_f32_args(spec: ConvSpecF32, x: torch.Tensor, N: int, H: int, W: int, y: torch.Tensor, *, x_coff: int = 0,
                   y_coff: int = 0, act: int = ACT_NONE, split: int = 0, alpha: float = 1.0, y2=None, y2_coff: int = 0,
                   res=None, res_coff: int = 0, res_post: int = 0, h32=None, zbuf=None, hidden: int = 0, bmap=None,
-                  bmap_coff: int = 0, epi: int = EPI_STD):
-    """(tensors, ints, alpha) of the ``conv_f32`` op / ``Plan.add_conv_f32``."""
+                  bmap_coff: int = 0, epi: int = EPI_STD, ksplit: int = 0):
+    """(tensors, ints, alpha) of the ``conv_f32`` op / ``Plan.add_conv_f32``; ``ksplit`` > 0 forces
+    an n-way split-K (0: the kernel's own choice)."""
     t = [x, spec.w, spec.b, y, y2, res, h32, zbuf, bmap]
     i = [N, H, W, x_coff, spec.cin4, spec.kh, spec.kw, spec.sh, spec.sw, spec.ph, spec.pw, spec.cout, act, split,
-         y_coff, y2_coff, res_coff, res_post, hidden, bmap_coff, epi]
+         y_coff, y2_coff, res_coff, res_post, hidden, bmap_coff, epi, ksplit]
     return t, i, float(alpha)
 
 

@@ -26,6 +26,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from .. import knobs
+
 
 def is_dist() -> bool:
     return dist.is_available() and dist.is_initialized()
@@ -46,10 +48,10 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> Tup
     WORLD_SIZE) return ``(0, 1, device)`` without creating a group."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    backend = backend or os.environ.get("JR_DIST_BACKEND") or None
+    backend = backend or knobs.get("JR_DIST_BACKEND")
     # JR_SHARE_GPU=1: ranks share the visible GPUs round-robin over gloo (a
     # rehearsal of >1 rank on a 1-GPU box; RCCL refuses two ranks per GPU)
-    share = os.environ.get("JR_SHARE_GPU") == "1" and torch.cuda.is_available()
+    share = knobs.flag("JR_SHARE_GPU") and torch.cuda.is_available()
     use_gpu = torch.cuda.is_available() and (backend != "gloo" or share)
     if share:
         backend = "gloo"

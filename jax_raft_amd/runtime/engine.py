@@ -29,7 +29,6 @@ iteration: K = 5 x 256 instead of 5 x 384 for raft_large.
 """
 from __future__ import annotations
 
-import os
 import weakref
 from collections import OrderedDict
 from dataclasses import dataclass, field
@@ -52,6 +51,7 @@ from ..models.layers import (
     ResidualBlock,
     UpdateBlock,
 )
+from .. import knobs
 from ..ops import native as nat
 from . import tunedb
 from ..ops.native import (
@@ -238,6 +238,18 @@ class RaftEngine:
 
     precision = "bf16"
 
+    # Lowering choices.  Each is the measured winner of an A/B (the profile is cited where the
+    # choice is used); they are class attributes rather than environment switches so that tests
+    # can cover the alternative lowering against the same oracle (monkeypatch.setattr on the
+    # class, before the plan is built).  Operational environment variables: jax_raft_amd/knobs.py.
+    GRU = "auto"          # ConvGRU stage lowering: "auto" | "halo" | "fused" | "unfused" (_gru_path)
+    PRO_LANES = "auto"    # prologue branches on lanes at one-lane loops: "auto" | "on" | "off"
+    HALO_NORM = True      # encoder instance norms fused into the halo 3x3 convs
+    MERGED_UP = True      # one-lane loop: 7x7 flow conv merged with the x8 upsampling (merged.hip)
+    CONV_GROUP = True     # one-lane loop: last correlation conv + convflow2 as one grouped grid
+    MASK_PARITY = False   # lane schedule: parity-buffered h copy for the mask lane (slower at b4)
+    HOST_GATE = True      # host gate of long replays (see GATE_MIN_ITERS)
+
     def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True,
                  corr_dtype: torch.dtype = torch.bfloat16, gate_dtype: torch.dtype = torch.bfloat16,
                  autotune: bool = True, streams="auto", split: int = 1,
@@ -248,19 +260,16 @@ class RaftEngine:
         self.streams_mode = streams
         self.streams = bool(streams)
         # instance norms of the encoders fused into halo 3x3 convs (statistics partials in the
-        # producer's epilogue, normalise + relu in the consumer's footprint load);
-        # JR_HALO_NORM=0: the separate statistics / norm_act passes
-        self.halo_norm = os.environ.get("JR_HALO_NORM", "1") != "0"
-        # JR_HALO_RES=0: a residual block's output is materialised by one norm_act pass instead of
-        # being built (residual + its norm) inside the next block's first halo conv
-        self.halo_res = self.halo_norm and os.environ.get("JR_HALO_RES", "1") != "0"
+        # producer's epilogue, normalise + relu in the consumer's footprint load; a residual
+        # block's output built -- residual + its norm -- inside the next block's first halo conv;
+        # profiles/r4_in_fusion_ab.txt); HALO_NORM = False: the separate statistics / norm_act passes
+        self.halo_norm = bool(self.HALO_NORM)
+        self.halo_res = self.halo_norm
         self.mask_head = "split"      # per plan: "split" (mask lane) | "fused" (one lane, 128 -> 512 conv)
         self.gate_dtype = gate_dtype
         self.split = split
         self.cfg_override = dict(cfg_override or {})
-        for item in filter(None, os.environ.get("JR_CFG_OVERRIDE", "").split(",")):
-            k, v = item.split("=")
-            self.cfg_override[k.strip()] = int(v)
+        self.cfg_override.update(knobs.cfg_override())
         self._cf1_w = self._cf1_b = None
         self._fh2_b = None
         self._convex_w = self._convex_b = None
@@ -282,9 +291,8 @@ class RaftEngine:
         # event).  A long replay enqueued behind a still-running one runs slower on this ROCm:
         # batch 1 raft_large 32 it 208-213 -> 261 pairs/s, raft_small 32 it 334-337 -> 435-436,
         # batch 4 387-393 -> 401-402; short forwards lose (raft_small 12 it 713-754 -> 646-698),
-        # where the exposed host launch is a larger share.  profiles/r4_host_gate.txt;
-        # JR_HOST_GATE=0 disables it.
-        self.host_gate = os.environ.get("JR_HOST_GATE", "1") != "0"
+        # where the exposed host launch is a larger share.  profiles/r4_host_gate.txt
+        self.host_gate = bool(self.HOST_GATE)
         self._done_ev: Optional[torch.cuda.Event] = None
         self.corr_dtype = corr_dtype
         self.autotune = autotune
@@ -965,8 +973,9 @@ class RaftEngine:
         """ConvGRU lowering of a plan: "halo" (gru_halo.hip: one launch per stage, any map
         size and batch), "fused" (gru_fused.hip: whole-row tiles, raft_large at >= 3/4 of
         the CUs' worth of rows) or "unfused" (two implicit-GEMM launches per stage).
-        ``JR_GRU=halo|fused|unfused`` forces one (where it applies)."""
-        env = os.environ.get("JR_GRU", "auto")
+        The class attribute ``GRU = "halo" | "fused" | "unfused"`` forces one (where it applies)."""
+        env = self.GRU
+        assert env in ("auto", "halo", "fused", "unfused"), env
         if env == "unfused":
             return "unfused"
         # auto: the whole-row kernel where it fills the GPU (its own >= 3/4-of-the-CUs rule:
@@ -986,9 +995,6 @@ class RaftEngine:
         cands = nat.gru_halo_candidates(self.hidden, mode, axis, B, h, w)
         enc = {c[0] * 1000000 + c[1] * 1000 + c[2] * 10 + c[3]: c for c in cands}
         key = ("gru_halo", self.hidden, mode, axis, B, h, w)
-        forced = os.environ.get("JR_HALO_TILE")   # "TR,TC,nb1,nb2" (A/B measurements)
-        if forced:
-            return tuple(int(v) for v in forced.split(","))
         if not self.autotune or len(cands) == 1 or self.device.type != "cuda":
             return cands[0]
         code = _TUNE_CACHE.get(key + (str(self.device),))
@@ -1023,8 +1029,8 @@ class RaftEngine:
         as the GPU has CUs: measured on MI355X at 440x1024, batch 4 (220 / 256 tiles)
         333-335 vs 320 pairs/s; batch 1 (55 / 64 tiles) 139 vs 158 FPS for the
         two-launch implicit-GEMM path (profiles/r3_gru_fused_ab.txt).
-        ``JR_GRU=fused`` forces it where it fits."""
-        env = "1" if os.environ.get("JR_GRU") == "fused" else "auto"
+        ``GRU = "fused"`` forces it where it fits."""
+        env = "1" if self.GRU == "fused" else "auto"
         rb = self.model.update_block.recurrent_block
         ks = [tuple(k) for k in rb.kernel_size]
         if (self.hidden != 128 or self.hx_cs != 256 or self.gate_cs < 384 or ks != [(1, 5), (5, 1)]
@@ -1133,9 +1139,10 @@ class RaftEngine:
         # pixels: there its ~100 kernels are small and latency-bound.  Measured at batch 1
         # (profiles/r4_prologue_lanes_ab.txt): raft_small 12 iterations 667 -> 861 pairs/s,
         # per-pair sync latency -1..-2 %; 1088x1920 frames 67.6 -> 63.7 (so: off there).
-        # JR_PRO_LANES=0: never, =1: always (A/B).
-        pl = os.environ.get("JR_PRO_LANES", "auto")
-        pro_on = pl == "1" or (pl == "auto" and B * h * w <= 4 * 55 * 128)
+        # PRO_LANES = "off": never, "on": always.
+        pl = self.PRO_LANES
+        assert pl in ("auto", "on", "off"), pl
+        pro_on = pl == "on" or (pl == "auto" and B * h * w <= 4 * 55 * 128)
         p_main, p_side, p_side2 = lanes if lanes_on or self.cp or not pro_on else (main, 1, 2)
         p_on = p_main != p_side
 
@@ -1155,8 +1162,7 @@ class RaftEngine:
         flow32 = alloc("flow32", (M, 2), F32)
         for t in (hx, qx, flow8, flow32):
             plan.add_memset([t])
-        s2d = ("fe.stem_s2d" in sp and "ce.stem_s2d" in sp and H % 2 == 0 and W % 2 == 0
-               and os.environ.get("JR_NO_S2D", "0") != "1")
+        s2d = "fe.stem_s2d" in sp and "ce.stem_s2d" in sp and H % 2 == 0 and W % 2 == 0
         x0 = alloc("x0", (2 * B, H // 2, W // 2, 16) if s2d else (2 * B, H, W, 8))
         if st.src is not None:   # uint8 frames: normalise + replicate pad + layout in one kernel (K14)
             H0, W0, pad_t, pad_l = st.src   # (pt is this part's buffer prefix)
@@ -1272,7 +1278,7 @@ class RaftEngine:
         # mask lane) reads hm instead of a buffer that holds h' only on every other iteration
         hm = (alloc("hm", (M, self.hidden))
               if gru_path != "unfused" and self.has_mask and (lanes_on or halo_pp) else None)
-        # Parity-buffered mask-lane operands (gru_fused + convex head, JR_MASK_PARITY=1: on): the last
+        # Parity-buffered mask-lane operands (gru_fused + convex head, MASK_PARITY = True): the last
         # GRU stage writes h into hm / hm2 and the update writes the flow into flow32 / flow32b by
         # iteration parity, so iteration i+1 never overwrites what the lane still reads for iteration
         # i; the lane's next read of a buffer is ordered by the E_FLOW join of the iteration after,
@@ -1280,7 +1286,7 @@ class RaftEngine:
         # slower at batch 4 (359-365 vs 372 pairs/s, profiles/r4_mask_parity_ab.txt): unjoined, the
         # mask head overlaps the ConvGRU stages (48 -> 54-56 us each) instead of the motion encoder.
         parity = (hm is not None and gru_path == "fused" and self._convex_w is not None
-                  and os.environ.get("JR_MASK_PARITY", "0") == "1")
+                  and self.MASK_PARITY)
         hm2 = alloc("hm2", (M, self.hidden)) if parity else None
         flow32b = alloc("flow32b", (M, 2), F32) if parity else None
 
@@ -1288,7 +1294,7 @@ class RaftEngine:
         c1k = me.convflow1.layers_0.kernel
         merged_up = (self._cf1_w is not None and tuple(c1k.shape[:2]) == (7, 7) and not self.cp
                      and (not self.has_mask or (self._convex_w is not None and fm is not None))
-                     and os.environ.get("JR_MERGED_UP", "1") != "0")
+                     and self.MERGED_UP)
 
         def flow_features():
             if self._cf1_w is not None:
@@ -1349,14 +1355,14 @@ class RaftEngine:
             plan.add_lookup([coords, corr] + levels + [None] * (4 - L) + upd,
                             [L, B, h, w, self.radius, h * w, blocked] + extra)
 
-        # the one-lane merged grid also runs convcorr1 (1x1, K 324 -> 352; merged.hip); JR_MERGED_C1=0: own launch
+        # the one-lane merged grid also runs convcorr1 (1x1, K 324 -> 352; merged.hip)
         c1_merged = (merged_up and self.has_mask and len(cl) == 2 and self._cc1_w is not None
-                     and self._cc1_kpad == 352 and os.environ.get("JR_MERGED_C1", "1") != "0")
+                     and self._cc1_kpad == 352)
 
         def motion_and_gru(wait_flow: bool, wait_mask: bool, flow2: bool = False):
             """``flow2``: convflow2 (the flow branch's second conv) is added here, as one grid
             with the last correlation conv when a grouped launch serves its tile config
-            (conv_grouped_kernel; JR_CONV_GROUP=0 keeps them separate launches)."""
+            (conv_grouped_kernel; CONV_GROUP = False keeps them separate launches)."""
             if len(cl) == 2:
                 if flow2 and c1_merged:
                     pass                      # ran in the flow conv's merged grid
@@ -1369,7 +1375,7 @@ class RaftEngine:
             else:
                 last = (sp["me.convcorr1"], corr, B, h, w, cf, dict(act=ACT_RELU))
             fl2 = (sp["me.convflow2"], f1, B, h, w, cf, dict(y_coff=cl[-1], act=ACT_RELU))
-            if not (flow2 and os.environ.get("JR_CONV_GROUP", "1") != "0" and self._conv_group(plan, last, fl2)):
+            if not (flow2 and self.CONV_GROUP and self._conv_group(plan, last, fl2)):
                 if flow2:
                     self._conv(plan, *fl2[:6], **fl2[6])
                 self._conv(plan, *last[:6], **last[6])
@@ -1491,8 +1497,7 @@ class RaftEngine:
             plan.set_defer(1)
             upsample(stride, mask_from_fm=fm is not None and self.has_mask)
             plan.set_defer(0)
-        elif (self._cf1_w is not None and tuple(c1k.shape[:2]) == (7, 7) and B < self.AUTO_STREAMS_MIN_BATCH
-              and os.environ.get("JR_FO_MERGED", "1") != "0"):
+        elif self._cf1_w is not None and tuple(c1k.shape[:2]) == (7, 7) and B < self.AUTO_STREAMS_MIN_BATCH:
             # final-only below batch 4, the one-lane order of the all-iterations loop: the flow update
             # fused into the next lookup, the 7x7 flow conv in the merged grid (its bilinear half
             # writes the single output slot every iteration; the epilogue's upsampling overwrites

@@ -29,6 +29,8 @@ import threading
 from pathlib import Path
 from typing import Dict, Optional
 
+from .. import knobs
+
 DB_DIR = Path(__file__).resolve().parent.parent / "tuned"
 KERNEL_SET = 1    # bump when tile-config ids are renumbered / removed (csrc/kernels/conv_igemm.hip)
 _lock = threading.Lock()
@@ -48,7 +50,7 @@ def path(arch: str) -> Path:
     """The table file: the packaged ``tuned/<arch>.json``, or ``JR_TUNE_DB`` (a table another
     process saved: e.g. tools/race_check.py hands its decisions to its child processes so that
     they compare kernels, not autotune outcomes)."""
-    o = os.environ.get("JR_TUNE_DB")
+    o = knobs.get("JR_TUNE_DB")
     return Path(o) if o else DB_DIR / f"{arch}.json"
 
 
@@ -63,7 +65,7 @@ def _table(arch: str) -> Dict[str, int]:
         if t is None:
             t = {}
             p = path(arch)
-            if os.environ.get("JR_TUNE", "db") != "fresh" and p.exists():
+            if knobs.get("JR_TUNE", "db") != "fresh" and p.exists():
                 with open(p) as f:
                     d = json.load(f)
                 if int(d.get("kernel_set", 1)) == KERNEL_SET:

@@ -38,7 +38,6 @@ followed by its backward before the next forward of the same loop (checked).
 from __future__ import annotations
 
 import contextlib
-import os
 import weakref
 from dataclasses import dataclass
 from typing import Dict, List, Optional
@@ -46,6 +45,7 @@ from typing import Dict, List, Optional
 import torch
 
 from ..models.layers import FeatureEncoder
+from .. import knobs
 from ..ops import native as nat
 from ..ops.native import ACT_NONE, ACT_RELU, EPI_GRU_A, EPI_GRU_B, EPI_STD, round_up
 from ..runtime import tunedb
@@ -271,6 +271,9 @@ class FusedLoop:
     """Native forward/backward of ``num_flow_updates`` refinement iterations for
     one model at one (batch, image size); see the module docstring."""
 
+    LANES = False       # motion-encoder backward on a side lane (slower, see __init__)
+    FWD_LANES = False   # the forward's flow-feature / mask-head lane (slower, see __init__)
+
     def __init__(self, model, B: int, H: int, W: int, T: int, device, use_graph: bool = True):
         nat.require()
         self._model_ref = weakref.ref(model)   # weak: the plan cache (_LOOPS) must not keep the model alive
@@ -279,13 +282,13 @@ class FusedLoop:
         self.M = B * self.h * self.w
         self.device = torch.device(device)
         self.use_graph = use_graph
-        # side lanes of the plans: opt-in.  JR_FUSED_LANES=1: the motion encoder's backward
-        # on a side lane (183 pairs/s vs 267 on one in-order stream, config 5);
-        # JR_FUSED_FWD_LANES=1: the forward's two-edge flow-feature / mask-head lane (189-196
-        # vs 288, although the same schedule speeds up the inference engine by 4 %: in the
-        # training step the multi-lane graphs' replays stall the launch queue around them)
-        self.lanes = 1 if os.environ.get("JR_FUSED_LANES", "0") == "1" else 0
-        self.fwd_lanes = 1 if os.environ.get("JR_FUSED_FWD_LANES", "0") == "1" else 0
+        # side lanes of the plans (LANES / FWD_LANES class attributes, off): the motion encoder's
+        # backward on a side lane measured 183 pairs/s vs 267 on one in-order stream (config 5);
+        # the forward's two-edge flow-feature / mask-head lane 189-196 vs 288, although the same
+        # schedule speeds up the inference engine by 4 %: in the training step the multi-lane
+        # graphs' replays stall the launch queue around them
+        self.lanes = 1 if self.LANES else 0
+        self.fwd_lanes = 1 if self.FWD_LANES else 0
         self.gen = 0            # forward generation (a backward must match the latest forward)
         self.done_gen = -1
         self._w_pending = False  # weight-gradient plans in flight on the side stream (finish_weights joins)
@@ -331,10 +334,10 @@ class FusedLoop:
         self.gate_cs = round_up(3 * self.hd, 8)
         self.fmap_ch = m.feature_encoder.out_channels
         # the forward's ConvGRU stages on gru_halo.hip (one launch per stage instead of EPI_GRU_A / B):
-        # raft_large's 1x5 / 5x1 stages over [h | motion | flow] = 2 hd loop channels.  JR_TRAIN_GRU_HALO=0: off
+        # raft_large's 1x5 / 5x1 stages over [h | motion | flow] = 2 hd loop channels
+        # (profiles/r4_train_bench.txt)
         ks = [tuple(g.convz.kernel.shape[:2]) for g in self.grus]
-        self.gru_halo = (self.device.type == "cuda" and os.environ.get("JR_TRAIN_GRU_HALO", "1") != "0"
-                         and self.hd == 128 and self.hx_cs == 2 * self.hd and ks == [(1, 5), (5, 1)])
+        self.gru_halo = (self.device.type == "cuda" and self.hd == 128 and self.hx_cs == 2 * self.hd and ks == [(1, 5), (5, 1)])
 
     def _params(self):
         me, fh, mp = self.me, self.fh, self.mp
@@ -1206,8 +1209,14 @@ def grad_comm(model, comm):
             _ACTIVE_COMM[id(model)] = prev
 
 
+# Module switches (measured choices; tests flip them with monkeypatch.setattr -- see knobs.py):
+FUSED_TRAIN = True      # native fused loop / model nodes (False: the per-op autograd path)
+FUSED_ENCODERS = True   # the whole-model node (encoders + pyramid + loop); False: only the loop
+FUSED_GRAPH = True      # replay the fused plans as hipGraphs (JR_PLAN_CHECK=1 forces eager plans)
+
+
 def enabled() -> bool:
-    return os.environ.get("JR_FUSED_TRAIN", "1") != "0"
+    return FUSED_TRAIN
 
 
 def full_model_ok(model, train: bool) -> bool:
@@ -1218,7 +1227,7 @@ def full_model_ok(model, train: bool) -> bool:
     bns = [m for m in model.modules() if isinstance(m, BatchNorm)]
     if bns and (not train or any(b.sync_group is not None for b in bns)):
         return False
-    return os.environ.get("JR_FUSED_ENCODERS", "1") != "0"
+    return FUSED_ENCODERS
 
 
 def _tensor_sig(model) -> tuple:
@@ -1248,7 +1257,7 @@ def _cached(kind, model, B, H, W, T, device):
         # one plan set per model: drop other shapes / kinds first (their buffers), then build
         _LOOPS.pop(model, None)
         obj = None
-        g = os.environ.get("JR_FUSED_GRAPH", "1") != "0"
+        g = FUSED_GRAPH and not knobs.flag("JR_PLAN_CHECK")
         obj = (FusedModel if kind == "model" else FusedLoop)(model, B, H, W, T, device, use_graph=g)
         obj._sig = sig
         _LOOPS[model] = {key: obj}

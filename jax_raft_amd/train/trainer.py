@@ -99,8 +99,7 @@ class Trainer:
             dp.convert_sync_batchnorm(self.model)
         self.flat_comm = dp.FlatGradComm() if self.world > 1 else None
         self.sync = dp.GradAllReducer(self.model, bucket_mb=cfg.bucket_mb, flat_comm=self.flat_comm)
-        self._graph_ok = (cfg.graph_step and self.device.type == "cuda" and self.world == 1
-                          and os.environ.get("JR_GRAPH_STEP", "1") != "0")
+        self._graph_ok = cfg.graph_step and self.device.type == "cuda" and self.world == 1
         self.opt = _adamw(self.model.parameters(), cfg, self.device, capturable=self._graph_ok)
         self._graph = None         # captured whole-step graph (see _graph_step)
         self.sched = torch.optim.lr_scheduler.OneCycleLR(

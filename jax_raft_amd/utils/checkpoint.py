@@ -24,6 +24,8 @@ import msgpack
 import numpy as np
 import torch
 
+from .. import knobs
+
 _EXT_NDARRAY = 1
 _EXT_NATIVE_COMPLEX = 2
 _EXT_NPSCALAR = 3
@@ -298,7 +300,7 @@ def resolve_pretrained(arch: str, url: str, weights: Optional[str] = None) -> by
         with open(weights, "rb") as f:
             return f.read()
     fname = url.rsplit("/", 1)[-1]
-    for d in (os.environ.get("JAX_RAFT_AMD_WEIGHTS"), os.path.expanduser("~/.cache/jax_raft_amd")):
+    for d in (knobs.get("JAX_RAFT_AMD_WEIGHTS"), os.path.expanduser("~/.cache/jax_raft_amd")):
         if d and os.path.exists(os.path.join(d, fname)):
             with open(os.path.join(d, fname), "rb") as f:
                 return f.read()

@@ -29,7 +29,7 @@ def conv_f32_ref(t, i, alpha):
     """PyTorch semantics of the conv_f32 op (kernels.h: ConvF32Params)."""
     x, w, bias, y, y2, res, h32, zbuf, bmap = t
     (N, H, W, x_coff, cin4, KH, KW, SH, SW, PH, PW, cout, act, split, y_coff, y2_coff, res_coff, res_post,
-     hidden, bmap_coff, epi) = i
+     hidden, bmap_coff, epi, _ksplit) = i
     xin = x.reshape(N, H, W, x.shape[-1])[..., x_coff:x_coff + cin4].permute(0, 3, 1, 2)
     k = w.reshape(cout, KH, KW, cin4).permute(0, 3, 1, 2)
     v = F.conv2d(xin, k, None, stride=(SH, SW), padding=(PH, PW)).permute(0, 2, 3, 1)
@@ -241,11 +241,9 @@ def test_precision_argument_is_validated():
     (2, 12, 16, 256, 256, 1, 5, 0, 256, 0),   # (1, 5) GRU-shaped, pad (0, 2) below
 ])
 @pytest.mark.parametrize("act", [0, 1, 4])
-@pytest.mark.parametrize("ksplit", [None, "1", "3"])
-def test_conv_f32_kernel(shape, act, ksplit, monkeypatch):
-    """vs the interpreter; ksplit: the automatic split-K choice, forced off, forced 3-way."""
-    if ksplit is not None:
-        monkeypatch.setenv("JR_F32_KSPLIT", ksplit)
+@pytest.mark.parametrize("ksplit", [0, 1, 3])
+def test_conv_f32_kernel(shape, act, ksplit):
+    """vs the interpreter; ksplit: the automatic split-K choice (0), forced off, forced 3-way."""
     N, H, W, cin, cout, k, s, p, xcs, xoff = shape
     kh, kw = (k, k) if k != 1 or s != 5 else (1, 5)
     sh, sw = (s, s) if s != 5 else (1, 1)
@@ -265,18 +263,17 @@ def test_conv_f32_kernel(shape, act, ksplit, monkeypatch):
     sg = nat.make_spec_f32(kern, b, (sh, sw), (ph, pw), device=dev)
     yg = torch.zeros(N, OH, OW, ycs, device=dev)
     nat.ops().conv_f32(*nat.conv_f32_args(sg, x.to(dev), N, H, W, yg, x_coff=xoff, act=act, split=cout // 2,
-                                          alpha=0.5, res=None if res is None else res.to(dev)))
+                                          alpha=0.5, res=None if res is None else res.to(dev), ksplit=ksplit))
     torch.cuda.synchronize()
     assert (yg.cpu() - yr).abs().max().item() < 1e-4 * (1 + yr.abs().max().item())
     assert not yg[..., cout:].any()
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ksplit", ["1", "4"])
-def test_conv_f32_gru_epilogues(ksplit, monkeypatch):
+@pytest.mark.parametrize("ksplit", [1, 4])
+def test_conv_f32_gru_epilogues(ksplit):
     """GRU-A (z, r*h) and GRU-B (blend) epilogues with a bias map, vs the interpreter
     (without / with split-K: the epilogue then runs in the reduction kernel)."""
-    monkeypatch.setenv("JR_F32_KSPLIT", ksplit)
     g = torch.Generator().manual_seed(2)
     N, H, W, hd, cs = 2, 8, 12, 64, 132
     M = N * H * W
@@ -294,9 +291,10 @@ def test_conv_f32_gru_epilogues(ksplit, monkeypatch):
         z = torch.zeros(M, hd, device=d)
         q = torch.zeros(M, cs, device=d)
         y = torch.zeros(M, cs, device=d)
-        a1 = nat.conv_f32_args(sa, xx, N, H, W, q, zbuf=z, h32=hh, hidden=hd, epi=nat.EPI_GRU_A, bmap=bm)
+        a1 = nat.conv_f32_args(sa, xx, N, H, W, q, zbuf=z, h32=hh, hidden=hd, epi=nat.EPI_GRU_A, bmap=bm,
+                               ksplit=ksplit)
         a2 = nat.conv_f32_args(sb, xx, N, H, W, y, zbuf=z, h32=hh, hidden=hd, epi=nat.EPI_GRU_B, bmap=bm,
-                               bmap_coff=2 * hd)
+                               bmap_coff=2 * hd, ksplit=ksplit)
         for a in (a1, a2):
             if devname == "cpu":
                 conv_f32_ref(*a)

@@ -4,6 +4,7 @@ import pytest
 import torch
 
 from jax_raft_amd import raft_large, raft_small
+from jax_raft_amd.runtime.engine import RaftEngine
 
 pytestmark = pytest.mark.gpu
 
@@ -317,7 +318,7 @@ def test_streams_auto_matches_lanes_and_single_lane(factory):
             assert _epe(a, b if B >= 4 else c) < 1e-4 and _epe(b, c) < 0.5 * REL_EPE["raft_large"] * mag
         eng = model.engine(torch.device("cuda", 0), streams="auto")
         st = eng._states[(B, 128, 128, 3, True)]
-        # loop lanes (the prologue's branches run on lanes at every batch, JR_PRO_LANES)
+        # loop lanes (the prologue's branches run on lanes at every batch, RaftEngine.PRO_LANES)
         assert eng.uses_lanes(B) == (B >= eng.AUTO_STREAMS_MIN_BATCH and eng.has_mask)
         assert st.plan.num_lanes() > 1
         # final-only (serving) mode: "auto" keeps one lane at every batch
@@ -384,9 +385,9 @@ def test_fused_gru_lane_schedule(monkeypatch, B, H, W, gru):
     m0 = copy.deepcopy(model).cuda()
     m1 = copy.deepcopy(model).cuda()
     i1, i2 = i1.cuda(), i2.cuda()
-    monkeypatch.setenv("JR_GRU", "unfused")
+    monkeypatch.setattr(RaftEngine, "GRU", "unfused")
     c = m0(i1, i2, num_flow_updates=5, streams=True)
-    monkeypatch.setenv("JR_GRU", gru)
+    monkeypatch.setattr(RaftEngine, "GRU", gru)
     a = m1(i1, i2, num_flow_updates=5, streams=True)
     b = m1(i1, i2, num_flow_updates=5, streams=True, use_graph=False)
     torch.cuda.synchronize()
@@ -467,10 +468,10 @@ def test_merged_flow_conv_upsample_is_bitwise(factory, monkeypatch):
     i1, i2 = i1.cuda(), i2.cuda()
     m0 = copy.deepcopy(model).cuda()
     m1 = copy.deepcopy(model).cuda()
-    monkeypatch.setenv("JR_CONV_GROUP", "0")
-    monkeypatch.setenv("JR_MERGED_UP", "0")
+    monkeypatch.setattr(RaftEngine, "CONV_GROUP", False)
+    monkeypatch.setattr(RaftEngine, "MERGED_UP", False)
     a = m0(i1, i2, num_flow_updates=4, streams=False)
-    monkeypatch.setenv("JR_MERGED_UP", "1")
+    monkeypatch.setattr(RaftEngine, "MERGED_UP", True)
     b = m1(i1, i2, num_flow_updates=4, streams=False)
     c = m1(i1, i2, num_flow_updates=4, streams=False, use_graph=False)
     torch.cuda.synchronize()
@@ -491,9 +492,9 @@ def test_grouped_corr_flow_conv_is_bitwise(factory, cfg, monkeypatch):
     i1, i2 = i1.cuda(), i2.cuda()
     m0 = copy.deepcopy(model).cuda()
     m1 = copy.deepcopy(model).cuda()
-    monkeypatch.setenv("JR_CONV_GROUP", "0")
+    monkeypatch.setattr(RaftEngine, "CONV_GROUP", False)
     a = m0(i1, i2, num_flow_updates=4, streams=False)
-    monkeypatch.setenv("JR_CONV_GROUP", "1")
+    monkeypatch.setattr(RaftEngine, "CONV_GROUP", True)
     b = m1(i1, i2, num_flow_updates=4, streams=False)
     torch.cuda.synchronize()
     assert torch.equal(a, b)

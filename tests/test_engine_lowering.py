@@ -55,7 +55,7 @@ def _plan(factory, B, all_iters=True, streams="auto", H=128, W=256):
 
 @pytest.mark.parametrize("gru", ["unfused", "halo"])
 def test_lane_schedule_raft_large(fake, gru, monkeypatch):
-    monkeypatch.setenv("JR_GRU", gru)
+    monkeypatch.setattr(E.RaftEngine, "GRU", gru)
     eng, p = _plan(raft_large, 4)
     assert eng.uses_lanes(4) and not eng.uses_lanes(1) and not eng.uses_lanes(4, all_iters=False)
     loop = [(ln, d, op) for s, ln, d, op, _ in p.ops if s == 1]
@@ -80,8 +80,8 @@ def test_lane_schedule_fused_gru_parity(fake, monkeypatch):
     the lane's mask conv and convex head read the matching buffer -- and the E_MASK join is
     gone (two waits per iteration: the lane's E_FH fork and the E_FLOW join).  Opt-in
     (JR_MASK_PARITY=1): measured slower on MI355X."""
-    monkeypatch.setenv("JR_GRU", "fused")
-    monkeypatch.setenv("JR_MASK_PARITY", "1")
+    monkeypatch.setattr(E.RaftEngine, "GRU", "fused")
+    monkeypatch.setattr(E.RaftEngine, "MASK_PARITY", True)
     eng, p = _plan(raft_large, 4)
     loop = [(ln, d, op, a) for s, ln, d, op, a in p.ops if s == 1]
     main = [op for ln, d, op, _ in loop if ln == 0]
@@ -110,7 +110,7 @@ def test_lane_schedule_fused_gru(fake, monkeypatch):
     critical lane, the mask lane's mask conv reads its own h copy `hm` (written by the last
     stage), and the E_MASK wait moves from the first stage to the last one (three waits per
     iteration)."""
-    monkeypatch.setenv("JR_GRU", "fused")
+    monkeypatch.setattr(E.RaftEngine, "GRU", "fused")
     eng, p = _plan(raft_large, 4)
     loop = [(ln, d, op, a) for s, ln, d, op, a in p.ops if s == 1]
     main = [op for ln, d, op, _ in loop if ln == 0]
@@ -126,13 +126,13 @@ def test_lane_schedule_fused_gru(fake, monkeypatch):
     mask_convs = [a for ln, d, op, a in loop if ln == 2 and op == "conv"]
     assert any(t[0] is hm for t, *_ in mask_convs)             # the mask conv reads hm
     assert not eng._gru_fused_ok(1, 55, 128) or eng._gru_fused_ok(4, 55, 128)
-    monkeypatch.setenv("JR_GRU", "auto")
+    monkeypatch.setattr(E.RaftEngine, "GRU", "auto")
     assert eng._gru_fused_ok(4, 55, 128) and not eng._gru_fused_ok(1, 55, 128)
     assert not eng._gru_fused_ok(4, 55, 129)                    # a row wider than a tile
 
 
 def test_fused_gru_not_for_raft_small(fake, monkeypatch):
-    monkeypatch.setenv("JR_GRU", "fused")
+    monkeypatch.setattr(E.RaftEngine, "GRU", "fused")
     _, p = _plan(raft_small, 4)
     assert "gru_fused" not in p.names(1)
 
@@ -141,7 +141,7 @@ def test_halo_gru_raft_large_buffers(fake, monkeypatch):
     """gru_halo lowering of raft_large (any batch): stage 1 (1x5 runs) reads [h | x] from hx
     and writes h' into qx; stage 2 (5x1 runs) reads h' from qx, x from hx and writes hx (never
     in place: neighbouring tiles read h); qx's [motion | flow] part is no longer written."""
-    monkeypatch.setenv("JR_GRU", "halo")
+    monkeypatch.setattr(E.RaftEngine, "GRU", "halo")
     for B, lanes in ((1, False), (4, True)):
         eng, p = _plan(raft_large, B)
         assert eng.gru_path == "halo"
@@ -161,7 +161,7 @@ def test_halo_gru_raft_large_buffers(fake, monkeypatch):
 def test_halo_gru_raft_small_ping_pong(fake, monkeypatch):
     """raft_small's single 3x3 stage ping-pongs h between hx and qx: even iterations read hx
     and write qx, odd ones the reverse, and the FlowHead conv reads the buffer just written."""
-    monkeypatch.setenv("JR_GRU", "auto")
+    monkeypatch.setattr(E.RaftEngine, "GRU", "auto")
     eng, p = _plan(raft_small, 1)
     assert eng.gru_path == "halo"
     (t, i), = [a for s, ln, d, op, a in p.ops if s == 1 and op == "gru_halo"]
@@ -175,7 +175,7 @@ def test_halo_gru_raft_small_ping_pong(fake, monkeypatch):
 @pytest.mark.parametrize("merged", ["1", "0"])
 @pytest.mark.parametrize("factory", [raft_large, raft_small])
 def test_one_lane_schedule(factory, fake, merged, monkeypatch):
-    monkeypatch.setenv("JR_MERGED_UP", merged)
+    monkeypatch.setattr(E.RaftEngine, "MERGED_UP", merged == "1")
     eng, p = _plan(factory, 1)
     assert not eng.uses_lanes(1)
     loop = [(ln, d, op) for s, ln, d, op, _ in p.ops if s == 1]
@@ -202,7 +202,7 @@ def test_one_lane_schedule(factory, fake, merged, monkeypatch):
 def test_one_lane_grouped_corr_flow_conv(factory, fake, group, monkeypatch):
     """One-lane schedule: the last correlation conv and convflow2 as one grid in the corr
     conv's tile config (when a grouped launch serves it)."""
-    monkeypatch.setenv("JR_CONV_GROUP", group)
+    monkeypatch.setattr(E.RaftEngine, "CONV_GROUP", group == "1")
     last = "me.convcorr2" if factory is raft_large else "me.convcorr1"
     model = factory()[0].eval()
     eng = E.RaftEngine(model, "cpu", autotune=False, cfg_override={last: 2})
@@ -287,8 +287,8 @@ def test_encoder_instance_norm_fused_into_halo_convs(fake, monkeypatch, fuse):
     passes disappear); a block output (or the stem's) is built inside the next block's first
     conv when that is a stride-1 halo conv, which writes it out for the residual; only the
     outputs feeding a stride-2 block or the final 1x1 conv are materialised by norm_act."""
-    monkeypatch.setenv("JR_HALO_NORM", fuse)
-    monkeypatch.setenv("JR_PRO_LANES", "0")   # one feature-encoder pass over both images
+    monkeypatch.setattr(E.RaftEngine, "HALO_NORM", fuse == "1")
+    monkeypatch.setattr(E.RaftEngine, "PRO_LANES", "off")   # one feature-encoder pass over both images
     eng, p = _plan(raft_large, 1)
     pro = p.names(0)
     fe_ops = [(op, a) for s, ln, d, op, a in p.ops if s == 0]
@@ -316,7 +316,7 @@ def test_prologue_lanes_at_batch_one(fake, monkeypatch, arch):
     pro_lanes = {ln for s, ln, d, op, a in p.ops if s == 0}
     loop_lanes = {ln for s, ln, d, op, a in p.ops if s == 1}
     assert pro_lanes == {0, 1, 2} and loop_lanes == {0}
-    monkeypatch.setenv("JR_PRO_LANES", "0")
+    monkeypatch.setattr(E.RaftEngine, "PRO_LANES", "off")
     eng, p = _plan(arch, 1)
     assert {ln for s, ln, d, op, a in p.ops} == {0}
 

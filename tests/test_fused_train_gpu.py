@@ -90,7 +90,7 @@ def test_fused_matches_unfused(factory, encoders, monkeypatch):
     early encoder layers, cos ~0.97, so they are not compared directly)."""
     from jax_raft_amd.train import fused as F
 
-    monkeypatch.setenv("JR_FUSED_ENCODERS", "1" if encoders else "0")
+    monkeypatch.setattr(F, "FUSED_ENCODERS", encoders)
     F._LOOPS.clear()
     model, i1, i2, target = _setup(factory)
     state = {k: v.clone() for k, v in model.state_dict().items()}
@@ -153,10 +153,10 @@ def test_fused_graph_equals_eager(monkeypatch):
 
     model, i1, i2, target = _setup(raft_large, seed=7)
     state = {k: v.clone() for k, v in model.state_dict().items()}
-    monkeypatch.setenv("JR_FUSED_GRAPH", "0")
+    monkeypatch.setattr(F, "FUSED_GRAPH", False)
     F._LOOPS.clear()
     out_e, g_e = _run(model, i1, i2, target, 2, fused=True)
-    monkeypatch.setenv("JR_FUSED_GRAPH", "1")
+    monkeypatch.setattr(F, "FUSED_GRAPH", True)
     F._LOOPS.clear()
     model.load_state_dict(state)
     out_g, g_g = _run(model, i1, i2, target, 2, fused=True)

@@ -69,6 +69,33 @@ def test_conv_matches_reference(case, cfg):
     assert err < 2e-3, err
 
 
+@pytest.mark.parametrize("case", [CONV_CASES[0], CONV_CASES[4], CONV_CASES[6], CONV_CASES[8]])
+@pytest.mark.parametrize("cfg", [2, 12, 24])
+def test_conv_lowering_variants_are_bitwise(case, cfg):
+    """The conv's lowering variants (cfg bit 10: XCD-aware tile order, conv_igemm.h:tile_of_block;
+    bit 11: the generic im2col loader instead of FAST) change only where / how tiles load, so the
+    outputs are bitwise those of the default lowering (binding.cpp:build_conv)."""
+    nat = _nat()
+    N, H, W, cin, cout, kh, kw, s, p = case
+    pad = p if isinstance(p, tuple) else (p, p)
+    torch.manual_seed(1)
+    k = torch.randn(kh, kw, cin, cout) / math.sqrt(kh * kw * cin)
+    spec = nat.make_spec(k, torch.randn(cout) * 0.1, (s, s), pad, device=DEV)
+    xg = torch.zeros(N, H, W, spec.cin8, dtype=torch.bfloat16, device=DEV)
+    xg[..., :cin] = torch.randn(N, H, W, cin).to(DEV, torch.bfloat16)
+    OH, OW = spec.out_hw(H, W)
+    outs = []
+    for bits in (0, 1 << 10, 1 << 11, 3 << 10):
+        y = torch.full((N, OH, OW, nat.round_up(cout, 8)), 7.0, device=DEV)
+        t, i, al = nat.conv_args(spec, xg, N, H, W, y, cfg=cfg)
+        i[20] = cfg | bits   # (the op's cfg int; tools/microbench.py --ablate patches it the same way)
+        nat.ops().conv(t, i, al)
+        outs.append(y)
+    torch.cuda.synchronize()
+    for bits, y in zip((1 << 10, 1 << 11, 3 << 10), outs[1:]):
+        assert torch.equal(y, outs[0]), (cfg, bits)
+
+
 @pytest.mark.parametrize("cfg", [0, 4, 6, 7, 9, 10, 11, 12, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34,
                                  35, 36, 37, 38, 39, 40, 41, 42, 43])
 def test_conv_epilogues(cfg):
@@ -143,16 +170,15 @@ def test_gru_fused_epilogues(hidden, xin, ks, pad, cfg):
     assert (hx[:, :hidden].float().cpu() - ref.reshape(M, hidden)).abs().max().item() < 2.5e-2
 
 
-@pytest.mark.parametrize("g2", ["0", "1"])
+@pytest.mark.parametrize("g2", [0, 1])
 @pytest.mark.parametrize("map_dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("B,h,w,vertical", [(2, 7, 13, 0), (2, 7, 13, 1), (2, 9, 12, 1), (1, 55, 128, 0),
                                             (1, 55, 128, 1), (3, 5, 3, 1), (1, 64, 20, 1), (1, 4, 128, 0)])
-def test_gru_stage_fused_kernel(B, h, w, vertical, map_dtype, g2, monkeypatch):
+def test_gru_stage_fused_kernel(B, h, w, vertical, map_dtype, g2):
     """gru_fused.hip (one launch per ConvGRU stage, r*h and z kept in the CU) vs the fp32
     ConvGRU of the reference with the context share as a per-pixel bias map (model.py:301-312):
     row tiles (1x5) and 1- / 2-column tiles (5x1), incl. the headline's 55 x 128 grid."""
     nat = _nat()
-    monkeypatch.setenv("JR_GRU_G2", g2)   # GEMM 2 on the 8 z waves (0) or all 16 waves (1)
     torch.manual_seed(5)
     hd, M = 128, B * h * w
     ks = (5, 1) if vertical else (1, 5)
@@ -177,7 +203,8 @@ def test_gru_stage_fused_kernel(B, h, w, vertical, map_dtype, g2, monkeypatch):
     assert nat.ops().gru_fused_fits(h, w, vertical)
     hm = torch.full((M, hd), 7.0, dtype=torch.bfloat16, device=DEV)
     bmg = bm.reshape(M, 384).to(DEV, map_dtype).contiguous()
-    nat.ops().gru_fused([hx, sa.w, sb.w, bmg, h32, hx, hm], [B, h, w, vertical])
+    # g2: GEMM 2 on the 8 z waves (0) or all 16 waves (1, the engine's choice)
+    nat.ops().gru_fused([hx, sa.w, sb.w, bmg, h32, hx, hm], [B, h, w, vertical, g2])
     torch.cuda.synchronize()
     assert (h32.cpu() - ref).abs().max().item() < 2e-2
     assert (hx[:, :hd].float().cpu() - ref).abs().max().item() < 2.5e-2

@@ -25,7 +25,6 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--g2", type=int, default=1, help="GEMM 2 on all 16 waves (1) or the 8 z waves (0)")
     a = ap.parse_args()
-    os.environ["JR_GRU_G2"] = str(a.g2)
     nat.require()
     dev = "cuda"
     B, h, w, hd = a.batch, a.h, a.w, 128
@@ -42,7 +41,7 @@ def main():
         sb = nat.make_spec(torch.randn(*ks, 256, 128) / math.sqrt(1280), torch.zeros(128), (1, 1), pad, cin8=256, device=dev)
         tiles = B * h if not vertical else B * (w // 2 if 2 * h <= 128 and w % 2 == 0 else w)
         dbg = torch.zeros(tiles * 6, dtype=torch.long, device=dev)
-        args = ([hx, sa.w, sb.w, bm, h32, hx, None, dbg], [B, h, w, vertical])
+        args = ([hx, sa.w, sb.w, bm, h32, hx, None, dbg], [B, h, w, vertical, a.g2])
         for _ in range(3):
             nat.ops().gru_fused(*args)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

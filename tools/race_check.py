@@ -93,9 +93,7 @@ def main():
         db = str(tunedb.save(tunedb.gpu_arch(), os.path.join(d, "tuned.json")))
         for name, env in (("serialised", {"AMD_SERIALIZE_KERNEL": "3"}), ("plan-check", {"JR_PLAN_CHECK": "1"})):
             path = os.path.join(d, name + ".pt")
-            e = dict(os.environ, JR_TUNE_DB=db, **env)
-            if name == "plan-check":
-                e["JR_FUSED_GRAPH"] = "0"   # eager plans: the per-op check runs outside graph capture
+            e = dict(os.environ, JR_TUNE_DB=db, **env)   # (JR_PLAN_CHECK=1 makes the fused plans eager)
             r = subprocess.run([sys.executable, __file__, "--size", *map(str, a.size), "--iters", str(a.iters),
                                 "--child", path], env=e, timeout=900)
             if r.returncode != 0:
