@@ -31,7 +31,7 @@ gradient all-reduce for N>1, synthetic data generated inside each timed step).
 Weights are random-init (no network for checkpoints), data is synthetic, so
 EPE is not measurable here and is reported as null; the numerical drift of the
 bf16 engine against the fp32 golden model at this configuration is in
-profiles/r3_drift.md (tools/drift.py).
+profiles/r5_drift.md (tools/drift.py).
 """
 from __future__ import annotations
 

@@ -311,7 +311,7 @@ static Launch make_conv_halo(const TList& t, const IList& i, double alpha, std::
 
 static Launch make_conv(const TList& t, const IList& i, double alpha, std::vector<at::Tensor>* keep,
                         const TList* tx = nullptr, const IList* ix = nullptr) {
-  if (i.size() >= 22 && i[20] >= kHaloCfg0 && tx == nullptr) return make_conv_halo(t, i, alpha, keep);
+  if (i.size() >= 22 && (i[20] & 255) >= kHaloCfg0 && tx == nullptr) return make_conv_halo(t, i, alpha, keep);
   int epi = 0, cfg = 0;
   const ConvParams p = build_conv(t, i, alpha, keep, tx, ix, &epi, &cfg);
   return [p, epi, cfg](hipStream_t s, int) { return jr_conv_forward(&p, cfg, epi, s); };
@@ -321,7 +321,7 @@ static Launch make_conv(const TList& t, const IList& i, double alpha, std::vecto
 // that ping-pongs between two buffers (raft_small's FlowHead after the single-stage halo GRU).
 static Launch make_conv_alt(const TList& t, const IList& i, double alpha, const at::Tensor& x_alt,
                             std::vector<at::Tensor>* keep) {
-  if (i.size() >= 22 && i[20] >= kHaloCfg0) {   // halo kernel: two launch closures
+  if (i.size() >= 22 && (i[20] & 255) >= kHaloCfg0) {   // halo kernel: two launch closures (cfg bits 8+: igemm variants)
     TList t2 = t.copy();
     t2.set(0, c10::optional<at::Tensor>(x_alt));
     Launch a = make_conv_halo(t, i, alpha, keep), b = make_conv_halo(t2, i, alpha, keep);

@@ -10,7 +10,7 @@ SURVEY.md 5.6).  This engine lowers the same model onto fp32 kernels only:
   pooling), lookups, hidden state, flow and x8 upsampling
   (``csrc/kernels/f32.hip``).
 
-It exists to bisect the bf16 engine's numerics on the device (profiles/r3_drift.md:
+It exists to bisect the bf16 engine's numerics on the device (profiles/r5_drift.md:
 the bf16 drift vs this engine vs the fp32 CPU golden) and for users who need the
 reference's own precision; the bf16 engine is the throughput path.  One lane,
 no deferral: each iteration runs in the reference's order (lookup, motion

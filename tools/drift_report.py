@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Render tools/drift.py's JSON (per-iteration EPE of the native engine vs the
 fp32 golden model at 440x1024, 32 iterations) as the markdown table of
-profiles/r3_drift.md.
+profiles/r5_drift.md.
 
-    python tools/drift_report.py gpurun_out/r3_drift.json > profiles/r3_drift_table.md
+    python tools/drift_report.py gpurun_out/r5_drift/drift.json > /tmp/table.md   # -> profiles/r5_drift.md
 """
 import json
 import sys
