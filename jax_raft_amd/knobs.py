@@ -7,7 +7,8 @@ A/B (the profile is cited where the choice is made) and the ones tests flip to c
 alternative are class or module attributes -- ``RaftEngine.GRU``, ``.PRO_LANES``,
 ``.HALO_NORM``, ``.MERGED_UP``, ``.CONV_GROUP``, ``.MASK_PARITY``, ``.HOST_GATE``,
 ``.AUTO_STREAMS_MIN_BATCH``, ``.GATE_MIN_ITERS``, ``.max_plans`` (runtime/engine.py) and
-``FUSED_ENCODERS``, ``FUSED_GRAPH``, ``FUSED_TRAIN`` (train/fused.py) -- and per-kernel variants
+``FUSED_ENCODERS``, ``FUSED_GRAPH``, ``FUSED_TRAIN`` (train/fused.py), ``HALO_NORM``
+(train/fused_encoder.py) -- and per-kernel variants
 are op arguments (``conv_f32_args(ksplit=)``, ``gru_fused``'s fifth int, conv cfg bits 10 / 11).
 
 ===================  =====================================================================
@@ -15,7 +16,7 @@ JR_NATIVE_SO         path of another build of the native library (e.g. the host-
                      build ``python -m jax_raft_amd._build --sanitize``); default: in-tree _C.so
 JR_OFFLOAD_ARCH      offload target of ``jax_raft_amd._build`` (default gfx950)
 JR_TUNE_DB           path of a tuned-config table to use instead of the packaged
-                     ``runtime/tuned/<arch>.json`` (tools/race_check.py hands its table to its
+                     ``jax_raft_amd/tuned/<arch>.json`` (tools/race_check.py hands its table to its
                      child processes this way)
 JR_TUNE              ``fresh``: ignore the persisted table, time every conv's candidates again
                      (tools/autotune_db.py)

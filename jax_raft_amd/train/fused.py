@@ -196,11 +196,14 @@ class Packer:
 
 def record_conv(plan, spec, x, N, H, W, y, *, tx=None, ix=None, extra=None, **kw):
     """Append one conv to ``plan`` (``plan=None``: launch it now) with its tile
-    config autotuned once per problem signature.  ``extra`` = [OH, OW, log2
-    dil_h, log2 dil_w] selects the input-dilation (strided data-gradient) mode.
-    Timing runs the same problem with the plain epilogue into a scratch
+    config autotuned once per problem signature; returns the config.  ``extra`` = [OH, OW, log2
+    dil_h, log2 dil_w] selects the input-dilation (strided data-gradient) mode.  The halo
+    kernel's fused norm operands (``stats_part``: output statistics partials; ``in_stats`` /
+    ``in_res`` / ``xn``: the input normalised on load, conv_halo.hip) restrict the candidates
+    to halo configs.  Timing runs the same problem with the plain epilogue into a scratch
     output, so epilogues that accumulate into their buffers are never re-run."""
     x_coff = kw.get("x_coff", 0)
+    fused_norm = any(kw.get(k) is not None for k in ("stats_part", "in_stats", "xn"))
     OH, OW = (extra[0], extra[1]) if extra else spec.out_hw(H, W)
     arch = tunedb.gpu_arch(x.device)
     key = ("train", N, H, W, OH, OW, spec.kh, spec.kw, spec.sh, spec.sw, spec.ph, spec.pw, spec.cin8, spec.cout,
@@ -209,7 +212,11 @@ def record_conv(plan, spec, x, N, H, W, y, *, tx=None, ix=None, extra=None, **kw
     # decisions made before it was a candidate
     halo = nat.halo_cfgs_for(spec, dict(kw, y=y)) if tx is None and not extra and x_coff == 0 else ()
     cands = tuple(nat.TUNE_CFGS) + tuple(halo)
-    if halo:
+    if fused_norm:
+        if not halo:
+            raise ValueError("fused norm operands need a halo-kernel conv")
+        cands, key = tuple(halo), key + ("halo_norm",)
+    elif halo:
         key = key + ("halo",)
     cfg = _CFG_CACHE.get(key + (str(x.device),))
     if cfg is None:
@@ -244,6 +251,7 @@ def record_conv(plan, spec, x, N, H, W, y, *, tx=None, ix=None, extra=None, **kw
         (plan.add_conv if plan is not None else ops.conv)(t, i, a)
     else:
         (plan.add_conv_train if plan is not None else ops.conv_train)(t, i, a, tx, ix)
+    return cfg
 
 
 def supported(model) -> bool:

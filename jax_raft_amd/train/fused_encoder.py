@@ -35,6 +35,12 @@ from ..ops.native import ACT_NONE, round_up
 BF16, F32 = torch.bfloat16, torch.float32
 EPI_BWD = 5
 EPS = 1e-5
+# The inference engine's encoder fusions in the training forward (instance-norm encoders,
+# stride-1 3x3 convs on the halo kernel, conv_halo.hip): the conv writes its output's channel-
+# statistics partials in its epilogue (no statistics pass) and normalises (+ residual, relu) its
+# raw input while loading it, writing the activation the backward keeps (xn) -- no norm_act
+# pass.  False: the separate statistics / norm_act passes (tests compare both).
+HALO_NORM = True
 
 
 def _log2(s: int) -> int:
@@ -157,37 +163,85 @@ class EncoderTrain:
         return None, None
 
     # ------------------------------------------------------------ forward
-    def _conv_unit(self, conv, norm_mod, x, N, H, W) -> _Unit:
+    def _halo_ok(self, sp) -> bool:
+        return HALO_NORM and self.device.type == "cuda" and bool(nat.halo_cfgs_for(sp, {}))
+
+    def _conv_unit(self, conv, norm_mod, xin, N, H, W) -> _Unit:
+        """One conv unit.  ``xin``: a tensor or a pending activation (:meth:`_norm_act`) that
+        this conv normalises while loading when it runs on the halo kernel, else materialised
+        first by a norm_act pass."""
+        sp = self._specs[id(conv)]
+        halo = self._halo_ok(sp)
+        pend = xin if isinstance(xin, dict) else None
+        fuse_in = (halo and pend is not None and not pend["done"] and self.mode == 1
+                   and pend["u"].cout == sp.cin8 and self._affine(pend["u"])[0] is None)
+        if pend is not None and not fuse_in:
+            self._materialise(pend)
+        x = pend["out"] if pend is not None else xin
         u = _Unit(conv, norm_mod, self.mode, x, N, H, W)
         u.y = self._z(N, u.OH, u.OW, u.cout)
-        sp = self._specs[id(conv)]
-        self.tuner(self.plan_f, sp, x, N, H, W, u.y, act=ACT_NONE)
-        if self.mode:
-            u.st = self._z(N, u.cout, 2, dtype=F32)
-            self.plan_f.add_stats([u.y, u.st], [N, u.OH * u.OW, u.cout])
+        u.st = self._z(N, u.cout, 2, dtype=F32) if self.mode else None
+        if halo and (self.mode or fuse_in):
+            kw = {}
+            if self.mode:
+                nb_max = max(-(-u.OH // c[4]) * -(-u.OW // c[5]) * c[2] for c in nat.HALO_CFGS if c[0] == sp.cin8)
+                kw["stats_part"] = part = self._z(N, nb_max, u.cout, 2, dtype=F32)
+            src = x
+            if fuse_in:
+                p = pend["u"]
+                has_res = pend["res"] is not None or pend["ru"] is not None
+                r = pend["relu"]
+                # norm_act's relu bits (0: on the normalised value, 1: on the sum) -> the halo
+                # loader's (1: before the residual add, 0: after it)
+                in_relu = (((r & 1) << 1) | ((r >> 1) & 1)) if has_res else (1 if r else 0)
+                res = pend["res"]
+                if isinstance(res, dict):
+                    assert res["done"], "a residual must be materialised before its consumer"
+                    res = res["out"]
+                kw.update(in_stats=p.st, in_relu=in_relu, in_hw=p.OH * p.OW, xn=pend["out"],
+                          in_res=pend["ru"].y if pend["ru"] is not None else res,
+                          in_res_stats=pend["ru"].st if pend["ru"] is not None else None)
+                src = p.y
+                pend["done"] = True
+            cfg = self.tuner(self.plan_f, sp, src, N, H, W, u.y, act=ACT_NONE, **kw)
+            if self.mode:
+                c = nat.HALO_CFGS[cfg - nat.HALO_CFG0]
+                self.plan_f.add_stats_final([part, u.st], [N, -(-u.OH // c[4]) * -(-u.OW // c[5]) * c[2], u.cout])
         else:
-            u.st = None
+            self.tuner(self.plan_f, sp, x, N, H, W, u.y, act=ACT_NONE)
+            if self.mode:
+                self.plan_f.add_stats([u.y, u.st], [N, u.OH * u.OW, u.cout])
         self.units.append(u)
         return u
 
-    def _norm_act(self, u: _Unit, relu: int, res=None, ru: Optional[_Unit] = None) -> torch.Tensor:
-        a = self._z(u.N, u.OH, u.OW, u.cout)
-        g, b = self._affine(u)
-        if ru is not None:
-            gr, br = self._affine(ru)
-            self.plan_f.add_norm_act([u.y, u.st, g, b, ru.y, ru.st, gr, br, a],
-                                     [self.mode, self.mode, u.N, u.OH * u.OW, u.cout, relu], EPS)
-        else:
-            self.plan_f.add_norm_act([u.y, u.st, g, b, res, None, None, None, a],
-                                     [self.mode, 0, u.N, u.OH * u.OW, u.cout, relu], EPS)
-        return a
+    def _norm_act(self, u: _Unit, relu: int, res=None, ru: Optional[_Unit] = None) -> dict:
+        """The unit's normalised (+ residual, relu) output, pending: materialised by its first
+        consumer (a halo conv's loader or :meth:`_materialise`)."""
+        return dict(u=u, relu=relu, res=res, ru=ru, out=self._z(u.N, u.OH, u.OW, u.cout), done=False)
+
+    def _materialise(self, pend) -> torch.Tensor:
+        if isinstance(pend, torch.Tensor):
+            return pend
+        if not pend["done"]:
+            u, relu, res, ru, a = pend["u"], pend["relu"], pend["res"], pend["ru"], pend["out"]
+            g, b = self._affine(u)
+            if ru is not None:
+                gr, br = self._affine(ru)
+                self.plan_f.add_norm_act([u.y, u.st, g, b, ru.y, ru.st, gr, br, a],
+                                         [self.mode, self.mode, u.N, u.OH * u.OW, u.cout, relu], EPS)
+            else:
+                self.plan_f.add_norm_act([u.y, u.st, g, b, None if res is None else self._materialise(res), None,
+                                          None, None, a],
+                                         [self.mode, 0, u.N, u.OH * u.OW, u.cout, relu], EPS)
+            pend["done"] = True
+        return pend["out"]
 
     def _record_fwd(self):
         enc = self.enc
         N, H, W = self.x.shape[:3]
         stem = self._conv_unit(enc.convnormrelu.layers_0, getattr(enc.convnormrelu, "layers_1", None), self.x, N, H, W)
         x = self._norm_act(stem, relu=1)
-        stem.a = x
+        stem.a = x["out"]
         self.stem = stem
         H, W = stem.OH, stem.OW
         for li in (1, 2, 3):
@@ -206,19 +260,21 @@ class EncoderTrain:
                     hh, ww = u.OH, u.OW
                     if j + 1 < len(names):
                         y = self._norm_act(u, relu=1)
-                        u.a = y
+                        u.a = y["out"]
                 ds = None
                 if blk.stride != (1, 1):
                     cna = blk.downsample
                     ds = self._conv_unit(cna.layers_0, getattr(cna, "layers_1", None), xin, N, h_in, w_in)
                 last = units[-1]
+                xin_t = self._materialise(xin)   # (the block's first conv materialised it already)
                 if ds is not None:
                     out = self._norm_act(last, relu=3, ru=ds)
                 else:
-                    out = self._norm_act(last, relu=3, res=xin)
-                last.a = out
-                self.blocks.append(dict(units=units, ds=ds, x=xin, out=out, H=h_in, W=w_in))
+                    out = self._norm_act(last, relu=3, res=xin_t)
+                last.a = out["out"]
+                self.blocks.append(dict(units=units, ds=ds, x=xin_t, out=out["out"], H=h_in, W=w_in))
                 x, H, W = out, hh, ww
+        x = self._materialise(x)
         self.tuner(self.plan_f, self._specs[id(enc.conv)], x, N, H, W, self.y_out, act=ACT_NONE)
         self.final_x = x
         if self.mode == 2:   # BatchNorm running statistics (Flax momentum semantics), one launch

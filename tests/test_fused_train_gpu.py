@@ -365,3 +365,43 @@ def test_race_check_tool():
                         "--iters", "2"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "race check ok" in r.stdout
+
+
+@pytest.mark.parametrize("halo_norm", [True, False], ids=["fused-norms", "norm-passes"])
+def test_fused_encoder_norms_on_halo_convs(halo_norm, monkeypatch):
+    """raft_large's instance-norm feature encoder in the training forward: with HALO_NORM the
+    stride-1 3x3 convs write their output statistics partials in the epilogue and normalise
+    (+ residual, relu) their raw input while loading it, writing back the activation the backward
+    keeps (no statistics / norm_act passes); without it the separate passes.  Both: gradients
+    against fp32 CPU autograd of the golden model as in test_fused_matches_cpu_fp32, and the
+    forward plan's op list shows which lowering ran."""
+    from jax_raft_amd.train import fused as F
+    from jax_raft_amd.train import fused_encoder as FE
+
+    monkeypatch.setattr(FE, "HALO_NORM", halo_norm)
+    F._LOOPS.clear()
+    model, i1, i2, target = _setup(raft_large, seed=6)
+    mc = raft_large()[0]
+    mc.load_state_dict(model.state_dict())
+    mc.train()
+    out = mc(i1, i2, train=True, num_flow_updates=2)
+    w = torch.tensor([0.8, 1.0]).view(-1, 1, 1, 1, 1)
+    (w * (out - target).abs()).mean().backward()
+    ref = {n: p.grad for n, p in mc.named_parameters() if p.grad is not None}
+    outg, gg = _run(model, i1, i2, target, 2, fused=True)
+    assert _rel(outg, out) < 5e-2
+    scale = max(v.norm().item() for v in ref.values())
+    fe = {n: _cos(gg[n], ref[n]) for n in ref if n.startswith("feature_encoder.") and ref[n].norm().item() > 1e-4 * scale}
+    cos = torch.tensor(list(fe.values()))
+    assert cos.median() > 0.97 and cos.min() > 0.7, fe
+    fm = next(iter(F._LOOPS[model].values()))
+    names = fm.fe.plan_f.op_names(0)
+    n_norm, n_stats, n_final = names.count("norm_act"), names.count("stats"), names.count("stats_final")
+    # 15 normalised convs; the two downsample norms fold into their block's residual norm_act.
+    # Fused: the 10 stride-1 3x3 convs (layer 1, and 3 in each of layers 2 / 3) produce their
+    # statistics and normalise their input; norm_act passes remain for the inputs of the two
+    # stride-2 convs and of the final 1x1 conv
+    if halo_norm:
+        assert (n_norm, n_stats, n_final) == (3, 5, 10), (n_norm, n_stats, n_final)
+    else:
+        assert (n_norm, n_stats, n_final) == (13, 15, 0), (n_norm, n_stats, n_final)
