@@ -39,16 +39,19 @@ constexpr int HD = 128;            // hidden channels
 constexpr int CIN = 256;           // [h | x] channels per tap
 constexpr int KPAD = 5 * CIN;      // packed K of both GEMMs
 constexpr int NSTG = KPAD / BK;    // 20 stages
-constexpr int TP = 128;            // pixel rows per tile
 constexpr int AROWS = 2 * HD;      // GEMM 1 rows
-constexpr int STAGE = (AROWS + TP) * BK;
-constexpr int RH_ROWS = 136;       // r*h image rows: J * (L + 4) <= 136
+constexpr int ASTAGE = AROWS * BK; // one GEMM 1 weight stage (GEMM 2: HD * BK)
+constexpr int IMG_ROWS = 136;      // tile image rows: J * (L + 4) <= 136
 constexpr unsigned OOB = 0x80000000u;
-constexpr int G2ST = 2 * HD * BK;  // G2ALL: GEMM 2 staging buffer (128 weight + 128 pixel rows)
-static_assert(3 * G2ST <= 2 * STAGE, "G2ALL: two GEMM 2 buffers + the z image fit GEMM 1's staging");
+// GEMM 2: two HD-row weight buffers + the z image (HD pixel rows x HD channels) in GEMM 1's staging
+static_assert(2 * HD * BK + 128 * HD <= 2 * ASTAGE, "G2ALL: GEMM 2 buffers + the z image fit GEMM 1's staging");
 
-// r*h image: rows of 128 channels (16 chunks of 16 B), chunk c of row R at c ^ (R & 15)
+// z image: rows of 128 channels (16 chunks of 16 B), chunk c of row R at c ^ (R & 15)
 JR_DEVICE int rh_off(int row, int chunk) { return row * HD + ((chunk ^ (row & 15)) << 3); }
+// tile image: rows of 256 channels (32 chunks); the XOR spreads the 32-row B-fragment reads of one
+// chunk (row stride 512 B = 2 x 64 banks) over 16 distinct 16-B slots: conflict-free
+// ds_read_b128 lane groups ({0-3, 12-15, 20-27} / {4-11, 16-19, 28-31} -> rows mod 16 distinct)
+JR_DEVICE int img_off(int row, int chunk) { return row * CIN + ((chunk ^ (row & 15)) << 3); }
 
 template <int NV>
 JR_DEVICE void load_map(const GruFusedParams& p, int m, int c, float* v) {
@@ -59,8 +62,8 @@ JR_DEVICE void load_map(const GruFusedParams& p, int m, int c, float* v) {
 
 template <bool G2ALL>
 __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE + RH_ROWS * HD];
-  bf16* const rh = smem + 2 * STAGE;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * ASTAGE + IMG_ROWS * CIN];
+  bf16* const img = smem + 2 * ASTAGE;   // the tile's [h | x] rows (+ zero pad rows); h -> r*h after GEMM 1
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wco = wave & 3, wp = wave >> 2;   // 64-channel group, 32-pixel group
@@ -84,54 +87,42 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
   const __amdgpu_buffer_rsrc_t was = __builtin_amdgcn_make_buffer_rsrc((void*)p.wa, (short)0, (int)p.wa_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wbs = __builtin_amdgcn_make_buffer_rsrc((void*)p.wb, (short)0, (int)p.wb_bytes, 0x00020000);
 
-  // zero rows of the r*h image (the conv's zero padding at both ends of each run)
-  if (tid < 4 * p.J * 16) {
-    const int q = tid >> 4, c = tid & 15, j = q >> 2, e = q & 3;
-    const int row = j * (p.L + 4) + (e < 2 ? e : p.L + e);
-    *(u32x4*)(rh + rh_off(row, c)) = u32x4{0u, 0u, 0u, 0u};
-  }
-
-  // loader: thread -> (pixel row lrow, 16-B chunk ch) of the B image, weight rows ar, ar + 128
+  // loader: thread -> weight row lrow (and lrow + 128), 16-B chunk ch of a 64-deep K stage
   const int lrow = tid >> 3, ch = tid & 7;
-  unsigned lbase = 0, lmask = 0;
-  {
-    const int lm = pix(lrow);
-    if (lm >= 0) {
-      lbase = (unsigned)lm * (unsigned)p.hx_cs * 2u + (unsigned)ch * 16u;
-      const int r = lrow % p.L;
-#pragma unroll
-      for (int k = 0; k < 5; ++k)
-        if ((unsigned)(r + k - 2) < (unsigned)p.L) lmask |= 1u << k;
-    }
-  }
-  const int tapd = (p.vertical ? p.W : 1) * p.hx_cs * 2;   // bytes between tap neighbours
   const unsigned aoff = (unsigned)(lrow * KPAD * 2 + ch * 16);
-
-  struct Regs { u32x4 a0, a1, b; };
-  auto xload = [&](int s) {   // B chunk of stage s from hx (channel block cb of tap s / 4)
-    const int tap = s >> 2, cb = s & 3;
-    const bool ok = s < NSTG && ((lmask >> tap) & 1u);
-    const unsigned off = lbase + (unsigned)((tap - 2) * tapd) + (unsigned)cb * 128u;
-    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xs, ok ? off : OOB, 0, 0));
-  };
   auto kofs = [&](int s) { return (unsigned)((s >> 2) * CIN + (s & 3) * 64) * 2u; };
-  auto sA_of = [&](int buf) { return smem + buf * STAGE; };
-  auto sB_of = [&](int buf) { return smem + buf * STAGE + AROWS * BK; };
-  auto put = [&](bf16* base, int row, const u32x4& v) { *(u32x4*)(base + row * BK + ((ch ^ swzB(row)) << 3)) = v; };
+  auto sA_of = [&](int buf) { return smem + buf * ASTAGE; };
   auto putA = [&](bf16* base, int row, const u32x4& v) { *(u32x4*)(base + row * BK + ((ch ^ swzA(row)) << 3)) = v; };
 
+  // The tile image: run j's rows j (L + 4) .. j (L + 4) + L + 3 hold the run's L pixels between two
+  // zero rows at each end (the conv's zero padding along the tap axis), all 256 channels.  Loaded
+  // once: GEMM 1's B fragment of tap t is row (pixel row + t), GEMM 2's x channels are read from
+  // it too and its r*h channels from the h part, which epilogue 1 overwrites with r*h.  (The
+  // round-4 form staged B per K stage from global memory: 5 x the tile's bytes per GEMM.)
+  constexpr int NIMG = (IMG_ROWS * 32 + 1023) / 1024;
+  u32x4 iv[NIMG];
+  const int nrow = p.J * (p.L + 4);
+#pragma unroll
+  for (int k = 0; k < NIMG; ++k) {
+    const int idx = k * 1024 + tid, R = idx >> 5, c = idx & 31;
+    const int j = R / (p.L + 4), r = R - j * (p.L + 4) - 2;
+    const bool in = R < nrow && (unsigned)r < (unsigned)p.L;
+    const int m = in ? pix(j * p.L + r) : 0;
+    iv[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+        xs, in ? (unsigned)m * (unsigned)p.hx_cs * 2u + (unsigned)c * 16u : OOB, 0, 0));
+  }
+
   // ---------------------------------------------------------------- GEMM 1
+  struct Regs { u32x4 a0, a1; };
   auto issue1 = [&](Regs& r, int s) {
     const bool kin = s < NSTG;
     r.a0 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(was, kin ? aoff + kofs(s) : OOB, 0, 0));
     r.a1 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
         was, kin ? aoff + (unsigned)(128 * KPAD * 2) + kofs(s) : OOB, 0, 0));
-    r.b = xload(s);
   };
   auto store1 = [&](const Regs& r, int buf) {
     putA(sA_of(buf), lrow, r.a0);
     putA(sA_of(buf), lrow + 128, r.a1);
-    put(sB_of(buf), lrow, r.b);
   };
   f32x16 acc[2];
 #pragma unroll
@@ -142,6 +133,11 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
   const int m = pix(prow);
   const int jrun = prow / p.L;
   const int rh_row = prow < npx ? jrun * (p.L + 4) + (prow - jrun * p.L) : 0;   // + tap = shifted row
+  // B fragment of stage s (tap s / 4, 64-channel block s % 4): this lane's pixel row shifted by the tap
+  auto bimg = [&](int s, int chunk) {
+    const int row = rh_row + (s >> 2);
+    return *(const bf16x8*)(img + img_off(row, (s & 3) * 8 + chunk));
+  };
   // bf16 bias-map chunks of this lane's pixel, loaded during the last K stages of a GEMM
   // (its epilogue then starts without a dependent global load)
   // Unconditional loads (pixel clamped, an fp32 map read as bf16 chunks stays in bounds): a
@@ -164,11 +160,11 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
       load_map<16>(p, m, c, v);
     }
   };
-  auto mma_stage = [&](const bf16* sA, int arow0, auto&& bfrag) {
+  auto mma_stage = [&](const bf16* sA, int arow0, int s) {
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int chunk = kk * 2 + hh;
-      const bf16x8 b = bfrag(chunk);
+      const bf16x8 b = bimg(s, chunk);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int row = arow0 + m32_arow(t, rho);
@@ -177,54 +173,53 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
       }
     }
   };
-  auto compute1 = [&](int buf) {
-    const bf16* sB = sB_of(buf);
-    mma_stage(sA_of(buf), wco * 64, [&](int chunk) {
-      return *(const bf16x8*)(sB + prow * BK + ((chunk ^ swzB(prow)) << 3));
-    });
-  };
   u32x4 bm1[2][2];
   {
     Regs ra, rb;
     issue1(ra, 0);
     issue1(rb, 1);
+#pragma unroll
+    for (int k = 0; k < NIMG; ++k) {
+      const int idx = k * 1024 + tid, R = idx >> 5, c = idx & 31;
+      if (R < IMG_ROWS) *(u32x4*)(img + img_off(R, c)) = iv[k];
+    }
     store1(ra, 0);
     __syncthreads();
+#pragma nounroll
     for (int s = 0; s < NSTG - 2; s += 2) {
       issue1(ra, s + 2);
-      compute1(0);
+      mma_stage(sA_of(0), wco * 64, s);
       store1(rb, 1);
       __syncthreads();
       issue1(rb, s + 3);
-      compute1(1);
+      mma_stage(sA_of(1), wco * 64, s + 1);
       store1(ra, 0);
       __syncthreads();
     }
     // last two stages: no operand loads left; the epilogue's bias-map chunks load instead
 #pragma unroll
     for (int t = 0; t < 2; ++t) pre_map(bm1[t], wco * 64 + 32 * t + 16 * hh);
-    compute1(0);
+    mma_stage(sA_of(0), wco * 64, NSTG - 2);
     store1(rb, 1);
     __syncthreads();
-    compute1(1);
-    __syncthreads();   // GEMM 1 staging free (G2ALL writes the z image into it)
+    mma_stage(sA_of(1), wco * 64, NSTG - 1);
+    __syncthreads();   // GEMM 1 staging and the image's h part free
   }
 
   stamp(1);
-  // GEMM 2's first two stages (weights only: the r*h blocks of tap 0) load during epilogue 1
-  auto issue2 = [&](Regs& r, int s) {
-    const bool kin = s < NSTG;
-    r.a0 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wbs, kin ? aoff + kofs(s) : OOB, 0, 0));
-    if ((s & 3) >= 2) r.b = xload(s);
+  // GEMM 2's first two stages' weights load during epilogue 1
+  auto sA2 = [&](int buf) { return smem + buf * (HD * BK); };
+  auto issue2 = [&](u32x4& r, int s) {
+    r = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wbs, s < NSTG ? aoff + kofs(s) : OOB, 0, 0));
   };
-  Regs ra2, rb2;
+  u32x4 ra2, rb2;
   issue2(ra2, 0);
   issue2(rb2, 1);
 
   // ------------------------------------------------------------ epilogue 1
   // lane: channels c0 + [0, 16) (c0 = 64 wco + 32 t + 16 hh) of tile pixel prow
-  // G2ALL: z goes to an LDS image in the part of GEMM 1's staging that GEMM 2 leaves free
-  bf16* const zimg = smem + 2 * G2ST;
+  // G2ALL: z goes to an LDS image behind GEMM 2's two weight buffers
+  bf16* const zimg = smem + 2 * HD * BK;
   [[maybe_unused]] bf16x8 z[2][2];   // z as bf16 (the unfused path's default gate storage, EPI_GRU_A z_bf16)
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -252,71 +247,62 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
         z[t][0] = o0;
         z[t][1] = o1;
       }
-    } else if (m >= 0) {   // r * h (h from the bf16 loop buffer, as the unfused EPI_GRU_A) -> r*h image
-      float hv[16];
-      load_bf16<16>((const bf16*)p.hx + (long)m * p.hx_cs + (c0 - HD), hv);
+    } else if (m >= 0) {   // r * h (h: this pixel's bf16 row of the image, as the unfused EPI_GRU_A)
+      // the lane reads and then replaces the same 16 h channels of its own pixel: no other lane
+      // touches them, and GEMM 1's readers are past the barrier above
+      const int chunk = (c0 - HD) >> 3;
+      bf16x8* const d0 = (bf16x8*)(img + img_off(rh_row + 2, chunk));
+      bf16x8* const d1 = (bf16x8*)(img + img_off(rh_row + 2, chunk + 1));
+      const bf16x8 h0 = *d0, h1 = *d1;
       bf16x8 o0, o1;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        o0[k] = f2bf(v[k] * hv[k]);
-        o1[k] = f2bf(v[8 + k] * hv[8 + k]);
+        o0[k] = f2bf(v[k] * bf2f(h0[k]));
+        o1[k] = f2bf(v[8 + k] * bf2f(h1[k]));
       }
-      const int chunk = (c0 - HD) >> 3;
-      *(bf16x8*)(rh + rh_off(rh_row + 2, chunk)) = o0;
-      *(bf16x8*)(rh + rh_off(rh_row + 2, chunk + 1)) = o1;
+      *d0 = o0;
+      *d1 = o1;
     }
   }
 
   // ---------------------------------------------------------------- GEMM 2
-  // stages s = (tap, cb): cb 0, 1 = the r*h channels (B from the image), cb 2, 3 = x (staged).
-  // G2ALL: all 16 waves, 32 x 32 (channel, pixel) tiles, staging buffers of 128 + 128 rows;
-  // else the 8 z waves keep GEMM 1's 64 x 32 tiles (z in registers), the others only stage.
-  auto sA2 = [&](int buf) { return G2ALL ? smem + buf * G2ST : sA_of(buf); };
-  auto sB2 = [&](int buf) { return G2ALL ? smem + buf * G2ST + HD * BK : sB_of(buf); };
-  auto store2 = [&](const Regs& r, int buf, int s) {
-    putA(sA2(buf), lrow, r.a0);
-    if ((s & 3) >= 2) put(sB2(buf), lrow, r.b);
-  };
+  // stages s = (tap, cb): cb 0, 1 = the r*h channels, cb 2, 3 = x -- both from the image.
+  // G2ALL: all 16 waves, 32 x 32 (channel, pixel) tiles; else the 8 z waves keep GEMM 1's
+  // 64 x 32 tiles (z in registers), the others only stage the weights.
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int k = 0; k < 16; ++k) acc[t][k] = 0.f;
-  auto mma1 = [&](const bf16* sA, int arow, auto&& bfrag) {   // one 32-row A tile (G2ALL)
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int chunk = kk * 2 + hh;
-      const bf16x8 b = bfrag(chunk);
-      const bf16x8 a = *(const bf16x8*)(sA + arow * BK + ((chunk ^ swzA(arow)) << 3));
-      acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[0], 0, 0, 0);
-    }
-  };
+  auto putA2 = [&](int buf, const u32x4& v) { putA(sA2(buf), lrow, v); };
   const int arow2 = 64 * (wco >> 1) + m32_arow(wco & 1, rho);   // G2ALL: channels 32 wco + ..
   auto compute2 = [&](int buf, int s) {
-    if (!G2ALL && wco >= 2) return;   // waves 8-15 only stage operands
-    const int tap = s >> 2, cb = s & 3;
-    const bf16* sB = sB2(buf);
-    auto from_rh = [&](int chunk) { return *(const bf16x8*)(rh + rh_off(rh_row + tap, cb * 8 + chunk)); };
-    auto from_st = [&](int chunk) { return *(const bf16x8*)(sB + prow * BK + ((chunk ^ swzB(prow)) << 3)); };
     if constexpr (G2ALL) {
-      if (cb < 2) mma1(sA2(buf), arow2, from_rh);
-      else mma1(sA2(buf), arow2, from_st);
+      const bf16* sA = sA2(buf);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int chunk = kk * 2 + hh;
+        const bf16x8 b = bimg(s, chunk);
+        const bf16x8 a = *(const bf16x8*)(sA + arow2 * BK + ((chunk ^ swzA(arow2)) << 3));
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[0], 0, 0, 0);
+      }
     } else {
-      if (cb < 2) mma_stage(sA2(buf), wco * 64, from_rh);
-      else mma_stage(sA2(buf), wco * 64, from_st);
+      if (wco >= 2) return;   // waves 8-15 only stage operands
+      mma_stage(sA2(buf), wco * 64, s);
     }
   };
-  __syncthreads();   // r*h (and z) images complete; GEMM 1 staging free
+  __syncthreads();   // r*h (and z) images complete
   stamp(2);
-  store2(ra2, 0, 0);
+  putA2(0, ra2);
   __syncthreads();
+#pragma nounroll
   for (int s = 0; s < NSTG - 2; s += 2) {
     issue2(ra2, s + 2);
     compute2(0, s);
-    store2(rb2, 1, s + 1);
+    putA2(1, rb2);
     __syncthreads();
     issue2(rb2, s + 3);
     compute2(1, s + 1);
-    store2(ra2, 0, s + 2);
+    putA2(0, ra2);
     __syncthreads();
   }
   // last two stages: the epilogue's bias-map chunks and fp32 state load instead of operands
@@ -336,7 +322,7 @@ __global__ __launch_bounds__(1024) void gru_fused_kernel(const GruFusedParams p)
     }
   }
   compute2(0, NSTG - 2);
-  store2(rb2, 1, NSTG - 1);
+  putA2(1, rb2);
   __syncthreads();
   compute2(1, NSTG - 1);
 

@@ -3,7 +3,9 @@
 ``small_b1_fps_12it``: p50 1.23 ms, p99 4.5 ms)?  Runs the same graph-pipelined batch-1 stream,
 records every step's device time and the host time of every Python garbage collection
 (gc.callbacks), and prints the slow steps next to the collections that overlapped them; then the
-same stream with the collector disabled.
+same stream with the collector disabled; then with the inputs copied from pinned host memory
+each step (bench.py's protocol: runtime/pipeline.py:InputPrefetcher on a copy stream, or a
+non-blocking copy on the compute stream).
 
     python dev/probes/p99_probe.py [--steps 200] [--iters 12]
 """
@@ -20,7 +22,7 @@ import torch  # noqa: E402
 from jax_raft_amd import raft_small  # noqa: E402
 
 
-def run(eng, frames, iters, steps, dev):
+def run(eng, frames, iters, steps, dev, h2d=None):
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     host = [0.0] * steps
     gcs = []
@@ -33,11 +35,26 @@ def run(eng, frames, iters, steps, dev):
             gcs.append((len([h for h in host if h > 0]), info["generation"], (time.perf_counter() - t_gc["t"]) * 1e3))
 
     gc.callbacks.append(cb)
+    pf = None
+    if h2d == "prefetch":
+        from jax_raft_amd.runtime.pipeline import InputPrefetcher
+
+        pf = InputPrefetcher([tuple(frames[0][0].shape)] * 2, dev)
+        pf.put(0, list(frames[0]))
     ev[0].record()
     for k in range(steps):
         t = time.perf_counter()
-        x, y = frames[k % len(frames)]
+        if pf is not None:
+            x, y = pf.get(k)
+        elif h2d == "stream":
+            x, y = (v.to(dev, non_blocking=True) for v in frames[k % len(frames)])
+        else:
+            x, y = frames[k % len(frames)]
         eng.pipelined(x, y, iters)
+        if pf is not None:
+            pf.release(k)
+            if k + 1 < steps:
+                pf.put(k + 1, list(frames[(k + 1) % len(frames)]))
         host[k] = (time.perf_counter() - t) * 1e3
         ev[k + 1].record()
     eng.flush()
@@ -61,11 +78,15 @@ def main():
         eng.pipelined(*frames[0], a.iters)
     eng.flush()
     torch.cuda.synchronize(dev)
-    for mode in ("gc on", "gc off"):
+    pinned = [tuple(v.cpu().pin_memory() for v in f) for f in frames]
+    for mode in ("gc on", "gc off", "h2d prefetch", "h2d same stream"):
         if mode == "gc off":
             gc.collect()
             gc.disable()
-        dev_ms, host, gcs = run(eng, frames, a.iters, a.steps, dev)
+        if mode == "h2d prefetch":
+            gc.enable()
+        h2d = {"h2d prefetch": "prefetch", "h2d same stream": "stream"}.get(mode)
+        dev_ms, host, gcs = run(eng, pinned if h2d else frames, a.iters, a.steps, dev, h2d)
         srt = sorted(dev_ms)
         p50, p99 = srt[len(srt) // 2], srt[int(0.99 * len(srt))]
         slow = [k for k, t in enumerate(dev_ms) if t > 2 * p50]
