@@ -64,7 +64,6 @@ class RaftEngineF32(RaftEngine):
     def _pack(self):
         """(Re)pack every conv as fp32 [cout, K]; BN folded (eval mode); packed
         tensors are updated in place so captured graphs stay valid."""
-        self._sig_modules = None
         if not self._sources:
             self._define_specs()
         for name, fn in self._sources.items():
@@ -81,7 +80,7 @@ class RaftEngineF32(RaftEngine):
                 sp.b.copy_(b.float().to(self.device))
             else:
                 self._specs[name] = nat.make_spec_f32(k, b.to(self.device), stride, pad, cin4=cin4, device=self.device)
-        self._sig = self._signature()
+        self._snap = self._snapshot()
 
     def uses_lanes(self, B: int, all_iters: bool = True) -> bool:
         return False

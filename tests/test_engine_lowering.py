@@ -334,3 +334,34 @@ def test_final_only_schedule_batch1(factory, fake):
     assert len(ints) == 15 and ints[11] == 1 and ints[12] == 0   # bilinear, iteration stride 0
     ep = p.names(2)   # (raft_large: + the mask head's 3x3 conv before the convex head)
     assert ep[0] == "flow_taps" and ep[-1] == ("convex_head" if factory is raft_large else "upsample_bilinear")
+
+
+def test_stale_check_sees_every_change(fake):
+    """The per-forward staleness check (RaftEngine._stale, a flat snapshot walk instead of the
+    tuple signature) notices in-place updates, replaced parameters / buffers / submodules and
+    new entries -- and nothing else."""
+    import torch.nn as nn
+
+    model = raft_small()[0].eval()
+    eng = E.RaftEngine(model, "cpu", autotune=False)
+    assert not eng._stale()
+    p = next(model.parameters())
+    with torch.no_grad():
+        p.add_(1.0)                                  # optimizer-style in-place update
+    assert eng._stale()
+    eng._pack()
+    assert not eng._stale()
+    conv = model.update_block.flow_head.conv2
+    conv.kernel = nn.Parameter(conv.kernel.detach().clone())   # replaced parameter
+    assert eng._stale()
+    eng._pack()
+    model.update_block.flow_head.register_buffer("extra", torch.zeros(1))   # a new entry
+    assert eng._stale()
+    eng._pack()
+    import copy
+    model.update_block.flow_head.conv2 = copy.deepcopy(model.update_block.flow_head.conv2)   # replaced submodule
+    assert eng._stale()
+    eng._pack()
+    assert not eng._stale()
+    model(torch.zeros(1, 128, 128, 3), torch.zeros(1, 128, 128, 3), num_flow_updates=1)   # a CPU forward: no change
+    assert not eng._stale()

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Convergence sanity check of the GPU training paths: overfit one fixed
 synthetic batch for --steps steps with the fused native path and with the
-unfused autograd path from the same initial weights; print both loss curves
-(JSON).  The two must descend alike (bf16 rounding differs, trajectories
-need not match exactly)."""
+unfused autograd path from the same initial weights, and (``--cpu-ref``) with fp32 CPU
+autograd of the golden model (models/reference.py) as the reference trajectory; print the loss
+curves (JSON).  They must descend alike (bf16 rounding differs, trajectories need not match
+exactly)."""
 import argparse
 import json
 import os
@@ -19,11 +20,12 @@ from jax_raft_amd.train.data import SyntheticFlow  # noqa: E402
 from jax_raft_amd.train.loss import sequence_loss  # noqa: E402
 
 
-def run(fused, state, factory, batch, steps, iters, lr):
+def run(fused, state, factory, batch, steps, iters, lr, device="cuda"):
     torch.manual_seed(0)
     model, _ = factory()
     model.load_state_dict(state)
-    model = model.cuda().train()
+    model = model.to(device).train()
+    batch = [t.to(device) for t in batch]
     opt = torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=1e-4)
     F._LOOPS.clear()
     img1, img2, flow, valid = batch
@@ -47,6 +49,7 @@ def main():
     ap.add_argument("--batch", type=int, default=2)
     ap.add_argument("--size", type=int, nargs=2, default=[192, 256])
     ap.add_argument("--lr", type=float, default=2e-4)
+    ap.add_argument("--cpu-ref", action="store_true", help="also the fp32 CPU golden trajectory")
     a = ap.parse_args()
     factory = raft_large if a.arch == "raft_large" else raft_small
     state = {k: v.clone() for k, v in factory()[0].state_dict().items()}
@@ -54,6 +57,9 @@ def main():
     batch = data.batch(list(range(a.batch)))
     res = {"fused": run(True, state, factory, batch, a.steps, a.iters, a.lr),
            "unfused": run(False, state, factory, batch, a.steps, a.iters, a.lr)}
+    if a.cpu_ref:
+        torch.set_num_threads(min(16, os.cpu_count() or 8))
+        res["fp32_cpu"] = run(False, state, factory, batch, a.steps, a.iters, a.lr, device="cpu")
     print(json.dumps(res))
 
 
