@@ -399,6 +399,8 @@ def main():
                     help="secondary configs after the headline (auto: on for the default headline config)")
     ap.add_argument("--extra-steps", type=int, default=20)
     ap.add_argument("--step-times", action="store_true", help="print every timed step's device time (stderr)")
+    ap.add_argument("--skip-extras", default="", help="comma list of extras to leave out (diagnostics)")
+    ap.add_argument("--extra-pause", type=float, default=0.0, help="seconds of idle before each extra (diagnostics)")
     ap.add_argument("--train-batch", type=int, default=6, help="extras: training batch per GPU (config 5: 6)")
     ap.add_argument("--train-size", type=int, nargs=2, default=[384, 512], help="extras: training image size")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -451,7 +453,19 @@ def main():
                 ("small_b1_fps_12it", "raft_small", 12, None, "bf16", "stream", (H, W)),
                 ("fp32_b1_fps", "raft_large", 32, BASELINE_FPS, "fp32", "stream", (H, W)),
                 ("hires_b1", "raft_large", 32, None, "bf16", "stream", (1088, 1920))]
+        skip = set(filter(None, args.skip_extras.split(",")))
         for key, arch, it, base, prec, proto, (eh, ew) in plan:
+            if key in skip:
+                continue
+            if args.extra_pause:   # diagnostics: idle the GPU before each extra
+                time.sleep(args.extra_pause)
+            if args.step_times:   # diagnostics: what earlier extras left alive
+                import gc
+
+                from jax_raft_amd.runtime.engine import RaftEngine
+                live = sum(isinstance(o, RaftEngine) for o in gc.get_objects())
+                print(f"extra {key}: {live} live engines, {torch.cuda.memory_allocated(ctx.dev) / 2**20:.0f} MiB "
+                      f"allocated", file=sys.stderr, flush=True)
             # the short forwards (raft_small: 1.2-2.3 ms) get more steps, so that one host-side
             # hiccup in a ~25 ms timed region does not decide the number
             mul = 3 if arch == "raft_small" else 1
