@@ -17,6 +17,8 @@ def main():
     ap.add_argument("--arch", default="raft_small")
     ap.add_argument("--iters", type=int, default=32)
     ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--pool-first", action="store_true",
+                    help="create a torch side stream (torch's per-device stream pool) before the engine")
     a = ap.parse_args()
     root = os.path.abspath(a.root)
     sys.path.insert(0, root)
@@ -28,12 +30,16 @@ def main():
 
     assert os.path.dirname(os.path.dirname(os.path.abspath(jax_raft_amd.__file__))) == root, jax_raft_amd.__file__
     ctx = bench.Ctx(types.SimpleNamespace(dist_backend="nccl", step_times=False))
+    if a.pool_first:
+        side = torch.cuda.Stream(device=ctx.dev)
+        with torch.cuda.stream(side):
+            torch.zeros(1, device=ctx.dev)
     model = (raft_small if a.arch == "raft_small" else raft_large)(seed=0)[0].to(ctx.dev).eval()
     kw = dict(use_graph=True, streams="auto", split=1, gate_dtype=torch.bfloat16, corr_dtype=torch.bfloat16,
               copy_output=True, precision="bf16")
     r = bench.run_sync_latency(ctx, model, H=440, W=1024, iters=a.iters, steps=a.steps, warmup=15, seed=99,
                                engine_kw=kw)
-    print(f"{root}: {a.arch} {a.iters} it sync: {r['value']} FPS, p50 {r['latency_ms_p50']} ms, "
+    print(f"{root}{' (pool first)' if a.pool_first else ''}: {a.arch} {a.iters} it sync: {r['value']} FPS, p50 {r['latency_ms_p50']} ms, "
           f"p99 {r['latency_ms_p99']} ms", flush=True)
 
 
