@@ -11,6 +11,9 @@ counter is merged over the passes, then derived columns are printed:
   matrix pipes were busy (GRBM_GUI_ACTIVE counts per XCD: divided by 8 here);
 * ``valu/mfma`` = SQ_INSTS_VALU / SQ_INSTS_MFMA;
 * ``lds_conf%`` = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE;
+* ``lds%`` = SQ_LDS_IDX_ACTIVE / (GRBM_GUI_ACTIVE * CUs): the share of the dispatch's CU-cycles
+  the LDS array was busy (256 B/clk/CU for ds_read_b128; compare with ``mfma%``: a kernel whose
+  lds% reaches its mfma% feeds its MFMAs from LDS at the array's rate);
 * ``fetch_MB`` = FETCH_SIZE (KB) / 1024 x 2 (gfx950 tallies wide streaming reads at half their
   bytes, MI355X_MICROARCH.md "HBM"), ``write_MB`` = WRITE_SIZE / 1024;
 * ``wait%`` = SQ_WAIT_ANY / SQ_WAVE_CYCLES, ``stall%`` = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES.
@@ -85,13 +88,14 @@ def main():
             mfma=(busy / (gui / 8 * NUM_CUS * 4) * 100) if busy and gui else None,
             vpm=(iva / imf) if iva and imf else None,
             conf=(conf / lact * 100) if conf is not None and lact else None,
+            lds=(lact / (gui / 8 * NUM_CUS) * 100) if lact is not None and gui else None,
             fetch=(fe / 1024 * 2) if fe is not None else None,
             write=(wr / 1024) if wr is not None else None,
             wait=(wa / wc * 100) if wa is not None and wc else None,
             stall=(wi / wc * 100) if wi is not None and wc else None,
         ))
     rows.sort(key=lambda r: -(r["us"] or 0) * r["n"])
-    hdr = f"{'kernel':60s} {'grid':>8s} {'n':>5s} {'~us':>7s} {'mfma%':>6s} {'valu/mfma':>9s} {'ldsconf%':>8s} " \
+    hdr = f"{'kernel':60s} {'grid':>8s} {'n':>5s} {'~us':>7s} {'mfma%':>6s} {'valu/mfma':>9s} {'ldsconf%':>8s} {'lds%':>6s} " \
           f"{'fetchMB':>8s} {'writeMB':>8s} {'wait%':>6s} {'stall%':>6s}"
     print(hdr)
 
@@ -100,7 +104,7 @@ def main():
 
     for r in rows:
         print(f"{r['kernel']:60s} {r['grid']:>8s} {r['n']:5d} {f(r['us'], 7)} {f(r['mfma'], 6)} {f(r['vpm'], 9, 2)} "
-              f"{f(r['conf'], 8)} {f(r['fetch'], 8, 2)} {f(r['write'], 8, 2)} {f(r['wait'], 6)} {f(r['stall'], 6)}")
+              f"{f(r['conf'], 8)} {f(r['lds'], 6)} {f(r['fetch'], 8, 2)} {f(r['write'], 8, 2)} {f(r['wait'], 6)} {f(r['stall'], 6)}")
 
 
 if __name__ == "__main__":
