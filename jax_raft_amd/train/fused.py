@@ -535,8 +535,11 @@ class FusedLoop:
             else:
                 nat.pack_weight(k, sp.cin8, out=sp.w)
                 sp.b.copy_(b)
-                if sp.wh is not None and name[:2] in ("gA", "gB") and name[2:].isdigit():
-                    nat.pack_gru_halo(k, sp.cin8, out=sp.wh)
+                if sp.wh is not None:   # the halo kernels' weight streams (gru_halo / conv_halo)
+                    if name[:2] in ("gA", "gB") and name[2:].isdigit():
+                        nat.pack_gru_halo(k, sp.cin8, out=sp.wh)
+                    else:
+                        nat.pack_halo_conv(k, sp.cin8, out=sp.wh)
         fb = self.fh.conv2.bias.detach().float().to(self.device)
         if not hasattr(self, "_fh2_bias"):
             self._fh2_bias = fb.contiguous()
@@ -548,9 +551,16 @@ class FusedLoop:
         pk, sp, hd, C = Packer(), self._specs, self.hd, self.ctx_ch
         me, fh, mp = self.me, self.fh, self.mp
 
+        def modes(name):
+            # 4: the halo-kernel weight stream too -- record_conv may run a plain-epilogue 3x3 conv on
+            # conv_halo.hip, which reads spec.wh (left out before round 5: those convs ran on the
+            # weights of the plan's first step after every optimizer update)
+            return (0, 4) if sp[name].wh is not None else (0,)
+
         def fwd(name, c, co=None, ci=None):
             kh, kw, cin, cout = c.kernel.shape
-            pk.piece(c.kernel, sp[name], 0, co or (0, cout), ci or (0, cin))
+            for mode in modes(name):
+                pk.piece(c.kernel, sp[name], mode, co or (0, cout), ci or (0, cin))
             pk.bias(c.bias, sp[name].b, (0, cout))
 
         def bwd(name, c):
@@ -591,8 +601,9 @@ class FusedLoop:
         if self.has_mask:
             mr = mp.convrelu.layers_0
             fh_, mh = self.fh_hidden, self.mask_hidden
-            pk.piece(fh.conv1.kernel, sp["fh1"], 0, (0, fh_), (0, hd))
-            pk.piece(mr.kernel, sp["fh1"], 0, (fh_, fh_ + mh), (0, hd))
+            for mode in modes("fh1"):
+                pk.piece(fh.conv1.kernel, sp["fh1"], mode, (0, fh_), (0, hd))
+                pk.piece(mr.kernel, sp["fh1"], mode, (fh_, fh_ + mh), (0, hd))
             pk.bias(fh.conv1.bias, sp["fh1"].b, (0, fh_))
             pk.bias(mr.bias, sp["fh1"].b, (fh_, fh_ + mh))
             pk.piece(fh.conv1.kernel, sp["fh1T"], 1, (0, hd), (0, fh_))

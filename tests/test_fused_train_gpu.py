@@ -405,3 +405,31 @@ def test_fused_encoder_norms_on_halo_convs(halo_norm, monkeypatch):
         assert (n_norm, n_stats, n_final) == (3, 5, 10), (n_norm, n_stats, n_final)
     else:
         assert (n_norm, n_stats, n_final) == (13, 15, 0), (n_norm, n_stats, n_final)
+
+
+def test_plans_follow_optimizer_updates():
+    """After optimizer steps the persistent fused plans must compute what freshly built plans
+    compute on the updated weights: every packed weight buffer -- the halo kernels' weight
+    streams of the loop's 3x3 convs included -- is refreshed by the per-step repack
+    (train/fused.py:Packer).  (Round 5 found those streams left at the first step's weights,
+    dev/probes/converge_step2.py: 39.8 vs 78.3.)"""
+    from jax_raft_amd.train import fused as F
+    from jax_raft_amd.train.data import SyntheticFlow
+    from jax_raft_amd.train.loss import sequence_loss
+
+    torch.manual_seed(0)
+    model = raft_large()[0].cuda().train()
+    img1, img2, flow, valid = SyntheticFlow(size=(192, 256), seed=0, device=torch.device("cuda")).batch([0, 1])
+    opt = torch.optim.AdamW(model.parameters(), lr=2e-4, weight_decay=1e-4)
+    F._LOOPS.clear()
+    for _ in range(2):
+        opt.zero_grad(set_to_none=True)
+        loss, _ = sequence_loss(model(img1, img2, train=True, num_flow_updates=4, fused=True), flow, valid)
+        loss.backward()
+        opt.step()
+    with torch.no_grad():
+        a = model(img1, img2, train=True, num_flow_updates=4, fused=True).float()
+        F._LOOPS.clear()
+        b = model(img1, img2, train=True, num_flow_updates=4, fused=True).float()
+    torch.cuda.synchronize()
+    assert _rel(a, b) < 1e-3, _rel(a, b)
