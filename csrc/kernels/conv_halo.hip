@@ -42,8 +42,17 @@ constexpr int pitch_of() { return CIN <= 64 ? 8 : CIN <= 128 ? 16 : 32; }
 
 // INN: the input is normalised (+ residual) while loading (p.in_stats set); a separate
 // instantiation so the plain convs keep their register budget
+// occupancy floor of the normalising variants (3 waves / SIMD for the 64-channel loader, else
+// 2; the workgroup counts are the ones hipcc caps at <= 256 VGPRs without spilling): without it the small-tile configs took 300-420 VGPRs there, i.e. one
+// wave per SIMD (the 96-channel encoder layer among them)
+template <int CIN, int WCO, int WPX, int TN, bool INN>
+constexpr int halo_min_blocks() {
+  return !INN || TN >= 4 ? 1 : CIN <= 64 ? 3 : WCO * WPX == 1 ? 4 : WCO * WPX <= 4 ? 2 : 1;
+}
+
 template <int CIN, int WCO, int WPX, int TN, int TR, int TC, bool INN>
-__global__ __launch_bounds__(64 * WCO * WPX, (INN && CIN <= 64 && TN <= 2) ? 3 : 1) void conv_halo_kernel(const ConvHaloParams p) {
+__global__ __launch_bounds__(64 * WCO * WPX, (halo_min_blocks<CIN, WCO, WPX, TN, INN>()))
+void conv_halo_kernel(const ConvHaloParams p) {
   constexpr int NT = 64 * WCO * WPX;
   constexpr int P = pitch_of<CIN>();
   constexpr int CC = CIN / 8;
@@ -243,21 +252,47 @@ __global__ __launch_bounds__(64 * WCO * WPX, (INN && CIN <= 64 && TN <= 2) ? 3 :
     }
   }
   if (p.stats_part) {
-    // sum over the 32 pixel lanes of each lane half (channels 16 hh + k), then lane rho 0 writes
+    // sum over the 32 pixel lanes of each lane half (channels 16 hh + k) as a transposing
+    // butterfly: every exchange step hands the partner half of the channels the lane still
+    // carries, so 2 x (8 + 4 + 2 + 1 + 1) exchanges replace 2 x 16 x 5 lane shuffles (the 5-step
+    // all-reduce per channel cost +16 us on the encoder's 64-channel layer, profiles/
+    // r5_halo_epi_costs.txt).  Only the first step crosses a 16-lane row (ds_swizzle); the
+    // others are DPP row permutes whose pairing (xor 15, xor 7, xor 2, xor 1) flips the bit
+    // that picks the half.  Lane rho ends with channel 8 b4 + 4 b3 + 2 b2 + b1 (b = bits of rho).
+    const int b4 = (rho >> 4) & 1, b3 = (rho >> 3) & 1, b2 = (rho >> 2) & 1, b1 = (rho >> 1) & 1;
+    auto swz16 = [](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x401F)); };
+    auto dpp = [](float v, auto ctrl) {
+      return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), decltype(ctrl)::value, 0xF, 0xF, false));
+    };
+    using Mirror = std::integral_constant<int, 0x140>;
+    using HalfMirror = std::integral_constant<int, 0x141>;
+    using Xor2 = std::integral_constant<int, 0x4E>;
+    using Xor1 = std::integral_constant<int, 0xB1>;
+    float s8[8], q8[8], s4[4], q4[4], s2[2], q2[2];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-#pragma unroll
-      for (int o = 1; o < 32; o <<= 1) {
-        ssum[k] += __shfl_xor(ssum[k], o, 64);
-        ssq[k] += __shfl_xor(ssq[k], o, 64);
-      }
+    for (int j = 0; j < 8; ++j) {
+      s8[j] = (b4 ? ssum[8 + j] : ssum[j]) + swz16(b4 ? ssum[j] : ssum[8 + j]);
+      q8[j] = (b4 ? ssq[8 + j] : ssq[j]) + swz16(b4 ? ssq[j] : ssq[8 + j]);
     }
-    if (rho == 0) {
-      const int nb = per_img * WPX;
-      float* o = p.stats_part + (((long)n * nb + rem * WPX + wp) * p.cout + c0) * 2;
 #pragma unroll
-      for (int k = 0; k < 16; ++k)
-        if (c0 + k < p.cout) *(float2*)(o + 2 * k) = make_float2(ssum[k], ssq[k]);
+    for (int j = 0; j < 4; ++j) {
+      s4[j] = (b3 ? s8[4 + j] : s8[j]) + dpp(b3 ? s8[j] : s8[4 + j], Mirror{});
+      q4[j] = (b3 ? q8[4 + j] : q8[j]) + dpp(b3 ? q8[j] : q8[4 + j], Mirror{});
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      s2[j] = (b2 ? s4[2 + j] : s4[j]) + dpp(b2 ? s4[j] : s4[2 + j], HalfMirror{});
+      q2[j] = (b2 ? q4[2 + j] : q4[j]) + dpp(b2 ? q4[j] : q4[2 + j], HalfMirror{});
+    }
+    float s1 = (b1 ? s2[1] : s2[0]) + dpp(b1 ? s2[0] : s2[1], Xor2{});
+    float q1 = (b1 ? q2[1] : q2[0]) + dpp(b1 ? q2[0] : q2[1], Xor2{});
+    s1 += dpp(s1, Xor1{});
+    q1 += dpp(q1, Xor1{});
+    const int ch = 8 * b4 + 4 * b3 + 2 * b2 + b1;
+    if ((rho & 1) == 0 && c0 + ch < p.cout) {
+      const int nb = per_img * WPX;
+      float* o = p.stats_part + (((long)n * nb + rem * WPX + wp) * p.cout + c0 + ch) * 2;
+      *(float2*)o = make_float2(s1, q1);
     }
   }
 }

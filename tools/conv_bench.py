@@ -65,19 +65,36 @@ def main():
     ap.add_argument("--cfg", type=int, default=None)
     ap.add_argument("--run", type=int, default=0)
     ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--fused", default="", help="halo configs only: comma list of stats (output statistics "
+                    "partials), inn (input instance norm on load), res (+ normalised residual), xn (write-back)")
     a = ap.parse_args()
+    fz = set(filter(None, a.fused.split(",")))
     for name in a.problems:
         nat, spec, x, y, (N, H, W), flop = setup(name)
 
+        cin, cout = PROBLEMS[name][3], PROBLEMS[name][4]
+        dev = x.device
+        kw = {}
+        if fz:   # encoder-style fused norms (train/fused_encoder.py, runtime/engine.py:_encoder)
+            if "stats" in fz:
+                kw["stats_part"] = torch.zeros(N * (H + 8) * (W + 16) // 4 * cout * 2, device=dev)
+            if "inn" in fz:
+                st = torch.stack([torch.zeros(N, cin, device=dev), torch.full((N, cin), float(H * W), device=dev)], -1)
+                kw.update(in_stats=st.contiguous(), in_relu=1, in_hw=H * W)
+                if "res" in fz:
+                    kw.update(in_res=torch.randn_like(x), in_res_stats=st.contiguous(), in_relu=3)
+                if "xn" in fz:
+                    kw["xn"] = torch.empty_like(x)
+
         def launch(cfg):
-            nat.ops().conv(*nat.conv_args(spec, x, N, H, W, y, act=nat.ACT_RELU, cfg=cfg))
+            nat.ops().conv(*nat.conv_args(spec, x, N, H, W, y, act=nat.ACT_NONE if fz else nat.ACT_RELU, cfg=cfg, **kw))
 
         if a.run:
             for _ in range(a.run):
                 launch(a.cfg)
             torch.cuda.synchronize()
             continue
-        cfgs = [a.cfg] if a.cfg is not None else list(nat.halo_cfgs_for(spec, {})) + list(nat.TUNE_CFGS)
+        cfgs = [a.cfg] if a.cfg is not None else list(nat.halo_cfgs_for(spec, {})) + ([] if fz else list(nat.TUNE_CFGS))
         res = []
         for c in cfgs:
             try:
@@ -87,8 +104,11 @@ def main():
             res.append((t, c))
         res.sort()
         best_igemm = next(((t, c) for t, c in res if c < nat.HALO_CFG0), None)
-        print(f"{name} {PROBLEMS[name]}: best igemm cfg {best_igemm[1]} {best_igemm[0]:.1f} us "
-              f"({flop / best_igemm[0] / 1e6:.0f} TF/s)")
+        if best_igemm is None:
+            print(f"{name} {PROBLEMS[name]} fused {sorted(fz)}:")
+        else:
+            print(f"{name} {PROBLEMS[name]}: best igemm cfg {best_igemm[1]} {best_igemm[0]:.1f} us "
+                  f"({flop / best_igemm[0] / 1e6:.0f} TF/s)")
         for t, c in res:
             if c >= nat.HALO_CFG0:
                 print(f"   halo {c} {nat.HALO_CFGS[c - nat.HALO_CFG0]}: {t:7.1f} us  {flop / t / 1e6:6.0f} TF/s")
