@@ -283,22 +283,32 @@ JR_DEVICE void norm_co(NormCo& o, const float* st, int mode, const float* gam, c
   }
 }
 
-// g and xhat of 8 channels of one row
-JR_DEVICE void norm_g(const NormCo& co, const bf16* gp, const bf16* op, const bf16* yp, int relu, float (&g)[8],
-                      float (&xh)[8]) {
-  const bf16x8 gv = *(const bf16x8*)gp;
-  const bf16x8 yv = *(const bf16x8*)yp;
-  bf16x8 ov;
-  if (op) ov = *(const bf16x8*)op;
+// raw operands of 8 channels of one row, and g / xhat from them
+struct NormRow {
+  bf16x8 g, o, y;
+};
+
+JR_DEVICE void norm_load(NormRow& r, const bf16* gp, const bf16* op, const bf16* yp) {
+  r.g = *(const bf16x8*)gp;
+  r.y = *(const bf16x8*)yp;
+  if (op) r.o = *(const bf16x8*)op;
+}
+
+JR_DEVICE void norm_eval(const NormCo& co, const NormRow& r, bool has_o, int relu, float (&g)[8], float (&xh)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    xh[j] = (bf2f(yv[j]) - co.mean[j]) * co.rstd[j];
-    float v = bf2f(gv[j]);
-    if (op && !(bf2f(ov[j]) > 0.f)) v = 0.f;
+    xh[j] = (bf2f(r.y[j]) - co.mean[j]) * co.rstd[j];
+    float v = bf2f(r.g[j]);
+    if (has_o && !(bf2f(r.o[j]) > 0.f)) v = 0.f;
     if ((relu & 1) && !(co.gam[j] * xh[j] + co.bet[j] > 0.f)) v = 0.f;
     g[j] = v;
   }
 }
+
+// rows per thread whose loads are issued together: the row loop is a 3-stream copy, and one row
+// (48 B per thread) in flight per iteration ran both kernels at about a third of HBM bandwidth
+// (profiles/r5_train_breakdown.txt: 1.34 + 0.74 ms per step for ~0.65 ms of bytes)
+constexpr int NORM_U = 4;
 
 __global__ __launch_bounds__(256) void norm_bwd_partial_kernel(const bf16* __restrict__ gout, const bf16* __restrict__ om,
                                                                const bf16* __restrict__ y, const float* __restrict__ st,
@@ -319,13 +329,21 @@ __global__ __launch_bounds__(256) void norm_bwd_partial_kernel(const bf16* __res
     NormCo co;
     norm_co(co, st, mode, gam, bet, n, N, HW, C, g8 * 8, eps);
     const long base = (long)n * HW * C + g8 * 8;
-#pragma unroll 4
-    for (int r = r0 + rg; r < r1; r += nrg) {
-      const long off = base + (long)r * C;
-      float g[8], xh[8];
-      norm_g(co, gout + off, om ? om + off : nullptr, y + off, relu, g, xh);
+    for (int r = r0 + rg; r < r1; r += NORM_U * nrg) {
+      NormRow v[NORM_U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { s[j] += g[j]; q[j] += g[j] * xh[j]; }
+      for (int u = 0; u < NORM_U; ++u) {   // all loads first (clamped rows; only valid ones count)
+        const long off = base + (long)min(r + u * nrg, r1 - 1) * C;
+        norm_load(v[u], gout + off, om ? om + off : nullptr, y + off);
+      }
+#pragma unroll
+      for (int u = 0; u < NORM_U; ++u) {
+        if (r + u * nrg >= r1) break;
+        float g[8], xh[8];
+        norm_eval(co, v[u], om != nullptr, relu, g, xh);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { s[j] += g[j]; q[j] += g[j] * xh[j]; }
+      }
     }
   }
 #pragma unroll
@@ -410,30 +428,37 @@ __global__ __launch_bounds__(256) void norm_bwd_apply_kernel(const bf16* __restr
   const long base = (long)n * HW * C + c0;
   const int r0 = blockIdx.x * rows;
   const int r1 = min(r0 + rows, HW);
-#pragma unroll 2
-  for (int row = r0 + rg; row < r1; row += nrg) {
-    const long off = base + (long)row * C;
-    float g[8], xh[8];
-    norm_g(co, gout + off, om ? om + off : nullptr, y + off, relu, g, xh);
-    bf16x8 o;
+  for (int row0 = r0 + rg; row0 < r1; row0 += NORM_U * nrg) {
+    NormRow v[NORM_U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(mode == 0 ? g[j] : a[j] * (g[j] - m1[j] - xh[j] * m2[j]));
-    *(bf16x8*)(dy + off) = o;
-    if (gres) {
-      const bf16x8 gv = *(const bf16x8*)(gout + off);
-      bf16x8 ov;
-      if (om) ov = *(const bf16x8*)(om + off);
-      float r[8];
+    for (int u = 0; u < NORM_U; ++u) {   // all loads first (clamped rows; only valid ones are stored)
+      const long off = base + (long)min(row0 + u * nrg, r1 - 1) * C;
+      norm_load(v[u], gout + off, om ? om + off : nullptr, y + off);
+    }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] = (om && !(bf2f(ov[j]) > 0.f)) ? 0.f : bf2f(gv[j]);
-      if (gres_bf16) {   // exact: a masked bf16 gradient
-        bf16x8 rb;
+    for (int u = 0; u < NORM_U; ++u) {
+      const int row = row0 + u * nrg;
+      if (row >= r1) break;
+      const long off = base + (long)row * C;
+      float g[8], xh[8];
+      norm_eval(co, v[u], om != nullptr, relu, g, xh);
+      bf16x8 o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) rb[j] = f2bf(r[j]);
-        *(bf16x8*)((bf16*)gres + off) = rb;
-      } else {
-        *(f32x4*)((float*)gres + off) = f32x4{r[0], r[1], r[2], r[3]};
-        *(f32x4*)((float*)gres + off + 4) = f32x4{r[4], r[5], r[6], r[7]};
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(mode == 0 ? g[j] : a[j] * (g[j] - m1[j] - xh[j] * m2[j]));
+      *(bf16x8*)(dy + off) = o;
+      if (gres) {
+        float r[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = (om && !(bf2f(v[u].o[j]) > 0.f)) ? 0.f : bf2f(v[u].g[j]);
+        if (gres_bf16) {   // exact: a masked bf16 gradient
+          bf16x8 rb;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) rb[j] = f2bf(r[j]);
+          *(bf16x8*)((bf16*)gres + off) = rb;
+        } else {
+          *(f32x4*)((float*)gres + off) = f32x4{r[0], r[1], r[2], r[3]};
+          *(f32x4*)((float*)gres + off + 4) = f32x4{r[4], r[5], r[6], r[7]};
+        }
       }
     }
   }
