@@ -87,10 +87,9 @@ void conv_halo_kernel(const ConvHaloParams p) {
   for (int d = 0; d < PD; ++d) ring[d] = __builtin_bit_cast(bf16x8, bload(ws, w_base + (unsigned)d * 1024u));
 
   // footprint -> LDS: batches of up to 16 loads per thread in flight; the input instance norm
-  // (per-channel scale / shift of image n, tables after the footprint) and the optional
-  // residual are applied on the way, the tile's own pixels optionally written back (xn)
+  // (per-channel scale / shift of image n) and the optional residual are applied on the way, the
+  // tile's own pixels optionally written back (xn)
   {
-    float* const nrm = (float*)(lds_b + NFP * RB);   // [CIN][2] input, [CIN][2] residual
     const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)p.in_res, (short)0, (int)p.in_res_bytes, 0x00020000);
     constexpr int TOTAL = NFP * CC;
@@ -99,6 +98,41 @@ void conv_halo_kernel(const ConvHaloParams p) {
     constexpr int NBAT = NL < NBMAX ? NL : NBMAX;
     constexpr bool norm = INN;
     const bool resid = INN && p.in_res != nullptr;
+    // Normalisation constants in registers: NT is a multiple of CC, so the 16-B chunk (8 channels)
+    // a thread loads is the same for every footprint pixel it handles, c = tid % CC.  Scale / shift
+    // of the input and of the residual (1 / 0 when it is not normalised), and the two relus as
+    // max(v, lo) with lo = 0 or -inf: branch-free arithmetic per element instead of an LDS table
+    // read per chunk (3-way bank conflicts) and per-element flag tests (profiles/
+    // r5_halo_norm_pmc.txt: encoder layer 2 VALU / MFMA 13.5 -> 11.3, LDS conflicts 17 -> 3.6 %,
+    // 38.2 -> 34.2 us; packed v_pk_fma_f32 pairs measured slower).
+    static_assert(!INN || NT % CC == 0, "normalising loader: fixed chunk per thread");
+    float na[8], nb[8], ra[8], rb[8];
+    float lo_pre = 0.f, lo_post = 0.f;
+    if constexpr (INN) {
+      const int c = tid % CC;
+      const float inv = 1.0f / (float)p.in_hw;
+      auto coef = [&](const float* stt, float (&A)[8], float (&Bv)[8]) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float* t = stt + ((long)n * CIN + 8 * c + j) * 2;
+          const float mu = t[0] * inv;
+          const float var = fmaxf(t[1] * inv - mu * mu, 0.f);
+          A[j] = rsqrtf(var + p.in_eps);
+          Bv[j] = -mu * A[j];
+        }
+      };
+      coef(p.in_stats, na, nb);
+      if (resid && p.in_res_stats != nullptr) {
+        coef(p.in_res_stats, ra, rb);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { ra[j] = 1.f; rb[j] = 0.f; }
+      }
+      // in_relu bit 1: the relu of the block's last ConvNormActivation, before the residual add
+      // (model.py:171-180: relu(x + relu(IN(conv2)))); bit 0: the relu after it
+      lo_pre = (p.in_relu & 2) ? 0.f : -__builtin_inff();
+      lo_post = (p.in_relu & 1) ? 0.f : -__builtin_inff();
+    }
 #pragma unroll
     for (int l0 = 0; l0 < NL; l0 += NBAT) {
       u32x4 v[NBAT], vr[NBAT];
@@ -114,25 +148,12 @@ void conv_halo_kernel(const ConvHaloParams p) {
         const int m = (n * p.H + y) * p.W + x;
         const unsigned off = (unsigned)m * (unsigned)p.xcs * 2u + (unsigned)(p.xoff + 8 * c) * 2u;
         v[k] = bload(xs, in ? off : HOOB);
-        if (resid) vr[k] = bload(rs, in ? (unsigned)m * (unsigned)p.in_rcs * 2u + (unsigned)(16 * c) : HOOB);
+        // zero (out-of-range read) without a residual: it then adds 0 * 1 + 0
+        if (INN) vr[k] = bload(rs, in && resid ? (unsigned)m * (unsigned)p.in_rcs * 2u + (unsigned)(16 * c) : HOOB);
         // destination byte offset; bit 30: padding (stays zero through the norm), -1: none
         dst[k] = !live ? -1 : (f * RB + ((c ^ key_x<P>(fx + TC * fy)) << 4)) | (in ? 0 : 1 << 30) | (c << 20);
         // image pixel of a tile-own footprint pixel (xn write-back), else -1
         pix[k] = in && fy >= 1 && fy <= TR && fx >= 1 && fx <= TC ? m : -1;
-      }
-      if (l0 == 0 && INN) {
-        for (int c = tid; c < 2 * CIN; c += NT) {
-          const float* stt = c < CIN ? p.in_stats : p.in_res_stats;
-          const int cc = c < CIN ? c : c - CIN;
-          if (stt == nullptr) continue;
-          const float inv = 1.0f / (float)p.in_hw;
-          const float mu = stt[((long)n * CIN + cc) * 2] * inv;
-          const float var = fmaxf(stt[((long)n * CIN + cc) * 2 + 1] * inv - mu * mu, 0.f);
-          const float a = rsqrtf(var + p.in_eps);
-          nrm[2 * c] = a;
-          nrm[2 * c + 1] = -mu * a;
-        }
-        __syncthreads();
       }
 #pragma unroll
       for (int k = 0; k < NBAT; ++k) {
@@ -140,24 +161,12 @@ void conv_halo_kernel(const ConvHaloParams p) {
         if (norm && !(dst[k] >> 30)) {
           const int c = (dst[k] >> 20) & 63;
           bf16x8 e = __builtin_bit_cast(bf16x8, v[k]);
-          const bf16x8 er = __builtin_bit_cast(bf16x8, resid ? vr[k] : u32x4{0u, 0u, 0u, 0u});
-          const f32x4* ab = (const f32x4*)(nrm + 16 * c);
-          const f32x4* abr = (const f32x4*)(nrm + 2 * CIN + 16 * c);
-          const bool rn = resid && p.in_res_stats != nullptr;
+          const bf16x8 er = __builtin_bit_cast(bf16x8, vr[k]);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const f32x4 t = ab[q];   // (a, b) of channels 8c + 2q, 8c + 2q + 1
-            const f32x4 tr = rn ? abr[q] : f32x4{1.f, 0.f, 1.f, 0.f};
-#pragma unroll
-            for (int h2 = 0; h2 < 2; ++h2) {
-              float fv = bf2f(e[2 * q + h2]) * t[2 * h2] + t[2 * h2 + 1];
-              // in_relu bit 1: the relu of the block's last ConvNormActivation, before the residual
-              // add (model.py:171-180: relu(x + relu(IN(conv2)))); bit 0: the relu after it
-              if (p.in_relu & 2) fv = fmaxf(fv, 0.f);
-              if (resid) fv += bf2f(er[2 * q + h2]) * tr[2 * h2] + tr[2 * h2 + 1];
-              if (p.in_relu & 1) fv = fmaxf(fv, 0.f);
-              e[2 * q + h2] = f2bf(fv);
-            }
+          for (int j = 0; j < 8; ++j) {
+            float fv = fmaxf(fmaf(bf2f(e[j]), na[j], nb[j]), lo_pre);
+            fv = fmaxf(fv + fmaf(bf2f(er[j]), ra[j], rb[j]), lo_post);
+            e[j] = f2bf(fv);
           }
           v[k] = __builtin_bit_cast(u32x4, e);
           if (p.xn && pix[k] >= 0) *(u32x4*)((bf16*)p.xn + (long)pix[k] * p.xncs + 8 * c) = v[k];
