@@ -44,12 +44,14 @@ constexpr int pitch_of() { return CIN <= 64 ? 8 : CIN <= 128 ? 16 : 32; }
 // instantiation so the plain convs keep their register budget
 // occupancy floors: the 64-channel configs 4 waves / SIMD plain (ring 8 deep, 120 VGPRs: encoder
 // layer 1 44.2 -> 41.4 us, with stats 48.3 -> 43.5, profiles/r5_halo_l1_occupancy.txt), 3 with the
-// normalising loader (at 4 it spills); the normalising variants of the other small-tile configs 2 (without
-// it they took 300-420 VGPRs, one wave per SIMD, the 96-channel encoder layer among them).  The
-// workgroup counts are the ones hipcc caps at these budgets without spilling.
+// normalising loader (at 4 it spills); the 96-channel normalising ones 3 (ring 8 deep: layer 2 with
+// norm + stats 35.6 -> 30.3 us, profiles/r5_halo_l2_occupancy.txt; the same for the 128-channel
+// ones measured slower); the other normalising small-tile configs 2 (without it they took 300-420
+// VGPRs, one wave per SIMD).  The workgroup counts are the ones hipcc caps at these budgets
+// without spilling.
 template <int CIN, int WCO, int WPX, int TN, bool INN>
 constexpr int halo_min_blocks() {
-  return CIN <= 64 && TN <= 2 ? (INN ? 3 : 4) : !INN || TN >= 4 ? 1 : WCO * WPX == 1 ? 4 : WCO * WPX <= 4 ? 2 : 1;
+  return TN > 2 ? 1 : CIN <= 64 ? (INN ? 3 : 4) : CIN <= 96 ? (INN ? 3 : 1) : !INN ? 1 : WCO * WPX == 1 ? 4 : WCO * WPX <= 4 ? 2 : 1;
 }
 
 template <int CIN, int WCO, int WPX, int TN, int TR, int TC, bool INN>
@@ -63,7 +65,7 @@ void conv_halo_kernel(const ConvHaloParams p) {
   // weight ring depth: 16 fragments, 8 for the 4-block waves at 2 waves / SIMD (256 VGPRs; each
   // fragment there feeds 4 MFMAs, so 8 in flight still cover ~1000 cycles of L2 latency)
   constexpr bool WIDE = TN >= 4 && WCO * WPX > 4;
-  constexpr int PD = S >= 16 ? ((WIDE || CIN <= 64) ? 8 : 16) : S;   // (64 ch: 4 waves / SIMD)
+  constexpr int PD = S >= 16 ? ((WIDE || CIN <= 96) ? 8 : 16) : S;   // (64 / 96 ch: 4 waves / SIMD)
   constexpr int FW = TC + 2;
   constexpr int NFP = (TR + 2) * FW;
   constexpr int RB = P * 16;              // footprint row bytes
