@@ -7,7 +7,8 @@
 // row of every K stage; on the encoder shapes that per-tile address arithmetic, not MFMA
 // or memory, bounds it (~1400 VALU + 1050 SALU per wave for 72 MFMAs, profiles/
 // r3_encoder_conv_study.md).  Here a workgroup owns a TR x TC block of output pixels,
-// loads its (TR + 2) x (TC + 2) input footprint into LDS once (zero outside the image),
+// loads its (TR + 2) x (TC + 2) input footprint into LDS once (zero outside the image; (TR + 3) x
+// (TC + 3) for the 4x4 stem),
 // and reads the B fragment of tap (u, v) for output pixel (i, j) from footprint row
 // (i + u) * (TC + 2) + j + v: a constant offset per tap, no per-stage descriptors.  The
 // weights stream per wave from L2 in MFMA fragment order (ops/native.py:pack_gru_halo,
@@ -54,20 +55,23 @@ constexpr int halo_min_blocks() {
   return TN > 2 ? 1 : CIN <= 64 ? (INN ? 3 : 4) : CIN <= 96 ? (INN ? 3 : 1) : !INN ? 1 : WCO * WPX == 1 ? 4 : WCO * WPX <= 4 ? 2 : 1;
 }
 
-template <int CIN, int WCO, int WPX, int TN, int TR, int TC, bool INN>
+// KS: the kernel size (3: every 3x3 / pad-1 conv; 4: the encoders' 7x7 / stride-2 stem as a 4x4 conv
+// over the 2x2 space-to-depth input, pads 2 / 1, ops/native.py:s2d_stem_kernel)
+template <int CIN, int WCO, int WPX, int TN, int TR, int TC, bool INN, int KS = 3>
 __global__ __launch_bounds__(64 * WCO * WPX, (halo_min_blocks<CIN, WCO, WPX, TN, INN>()))
 void conv_halo_kernel(const ConvHaloParams p) {
   constexpr int NT = 64 * WCO * WPX;
   constexpr int P = pitch_of<CIN>();
   constexpr int CC = CIN / 8;
   constexpr int SPT = CIN / 16;           // k-steps per tap
-  constexpr int S = 9 * SPT;
+  constexpr int S = KS * KS * SPT;
+  constexpr int PAD = KS / 2;             // top / left padding (the footprint's first row / column)
   // weight ring depth: 16 fragments, 8 for the 4-block waves at 2 waves / SIMD (256 VGPRs; each
   // fragment there feeds 4 MFMAs, so 8 in flight still cover ~1000 cycles of L2 latency)
   constexpr bool WIDE = TN >= 4 && WCO * WPX > 4;
   constexpr int PD = S >= 16 ? ((WIDE || CIN <= 96) ? 8 : 16) : S;   // (64 / 96 ch: 4 waves / SIMD)
-  constexpr int FW = TC + 2;
-  constexpr int NFP = (TR + 2) * FW;
+  constexpr int FW = TC + KS - 1;
+  constexpr int NFP = (TR + KS - 1) * FW;
   constexpr int RB = P * 16;              // footprint row bytes
   static_assert(TR * TC <= 32 * WPX * TN && (TC == 16 || TC == 8), "tile");
   extern __shared__ __attribute__((aligned(16))) bf16 lds[];
@@ -146,7 +150,7 @@ void conv_halo_kernel(const ConvHaloParams p) {
         const int idx = (l0 + k) * NT + tid;
         const int f = idx / CC, c = idx - f * CC;
         const int fy = f / FW, fx = f - fy * FW;
-        const int y = y0 - 1 + fy, x = x0 - 1 + fx;
+        const int y = y0 - PAD + fy, x = x0 - PAD + fx;
         const bool live = l0 + k < NL && idx < TOTAL;
         const bool in = live && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
         const int m = (n * p.H + y) * p.W + x;
@@ -157,7 +161,7 @@ void conv_halo_kernel(const ConvHaloParams p) {
         // destination byte offset; bit 30: padding (stays zero through the norm), -1: none
         dst[k] = !live ? -1 : (f * RB + ((c ^ key_x<P>(fx + TC * fy)) << 4)) | (in ? 0 : 1 << 30) | (c << 20);
         // image pixel of a tile-own footprint pixel (xn write-back), else -1
-        pix[k] = in && fy >= 1 && fy <= TR && fx >= 1 && fx <= TC ? m : -1;
+        pix[k] = in && fy >= PAD && fy < PAD + TR && fx >= PAD && fx < PAD + TC ? m : -1;
       }
 #pragma unroll
       for (int k = 0; k < NBAT; ++k) {
@@ -199,7 +203,7 @@ void conv_halo_kernel(const ConvHaloParams p) {
       [&](int s) { return __builtin_bit_cast(bf16x8, bload(ws, w_base + (unsigned)s * 1024u)); },
       [&](int s, int b) {
         const int tap = s / SPT, kc = s - tap * SPT;
-        const int u = tap / 3, v = tap % 3;
+        const int u = tap / KS, v = tap % KS;
         // slot of chunk 2 kc + hh: (2 kc) ^ (kx ^ hh); the tap's row shift is an immediate offset
         const int kxh = (key_x<P>(key0[b] + v + TC * u) ^ hh) << 4;
         return *(const bf16x8*)(lds_b + (rb0[b] + (((2 * kc) << 4) ^ kxh)) + (u * FW + v) * RB);
@@ -312,6 +316,7 @@ void conv_halo_kernel(const ConvHaloParams p) {
 
 struct HaloCfg {
   int cin, wco, wpx, tn, tr, tc;
+  int ks = 3;
 };
 
 // tile configs (cfg id = index): encoder shapes (64 / 96 / 128 channels, large pixel tiles
@@ -331,30 +336,32 @@ constexpr HaloCfg kCfgs[] = {
     // weights a whole-cout tile needs (the per-CU L2 stream bounds the 7040-pixel loop convs), the
     // footprint is re-read per channel block from L2 instead
     {256, 1, 2, 2, 8, 16},  {256, 1, 4, 1, 8, 16},  {128, 1, 2, 2, 8, 16},  {128, 1, 4, 1, 8, 16},
+    // the space-to-depth stem (4x4 over 16 input channels, 64 outputs)
+    {16, 2, 2, 2, 8, 16, 4},  {16, 2, 2, 4, 16, 16, 4},
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
 int lds_bytes(const HaloCfg& c) {
   const int P = c.cin <= 64 ? 8 : c.cin <= 128 ? 16 : 32;
-  return (c.tr + 2) * (c.tc + 2) * P * 16 + c.cin * 16;   // footprint + input / residual norm tables
+  return (c.tr + c.ks - 1) * (c.tc + c.ks - 1) * P * 16 + c.cin * 16;   // footprint (+ slack)
 }
 
-template <int CIN, int WCO, int WPX, int TN, int TR, int TC, bool INN>
+template <int CIN, int WCO, int WPX, int TN, int TR, int TC, bool INN, int KS>
 int launch_v(const ConvHaloParams& p, hipStream_t s, int lds) {
-  static const bool attr = hipFuncSetAttribute((const void*)conv_halo_kernel<CIN, WCO, WPX, TN, TR, TC, INN>,
+  static const bool attr = hipFuncSetAttribute((const void*)conv_halo_kernel<CIN, WCO, WPX, TN, TR, TC, INN, KS>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   if (!attr) return (int)hipErrorInvalidValue;
   const int cpad = (p.cout + 32 * WCO - 1) / (32 * WCO);
-  hipLaunchKernelGGL((conv_halo_kernel<CIN, WCO, WPX, TN, TR, TC, INN>), dim3(p.ntiles, cpad), dim3(64 * WCO * WPX), lds,
+  hipLaunchKernelGGL((conv_halo_kernel<CIN, WCO, WPX, TN, TR, TC, INN, KS>), dim3(p.ntiles, cpad), dim3(64 * WCO * WPX), lds,
                      s, p);
   return (int)hipGetLastError();
 }
 
-template <int CIN, int WCO, int WPX, int TN, int TR, int TC>
+template <int CIN, int WCO, int WPX, int TN, int TR, int TC, int KS = 3>
 int launch(const ConvHaloParams& p, hipStream_t s, int lds) {
   if (p.TR != TR || p.TC != TC) return (int)hipErrorInvalidValue;
-  return p.in_stats ? launch_v<CIN, WCO, WPX, TN, TR, TC, true>(p, s, lds)
-                    : launch_v<CIN, WCO, WPX, TN, TR, TC, false>(p, s, lds);
+  return p.in_stats ? launch_v<CIN, WCO, WPX, TN, TR, TC, true, KS>(p, s, lds)
+                    : launch_v<CIN, WCO, WPX, TN, TR, TC, false, KS>(p, s, lds);
 }
 
 }  // namespace
@@ -368,13 +375,18 @@ extern "C" int jr_conv_halo_cfg(int cfg, int* o) {
 
 extern "C" int jr_conv_halo_lds(int cfg) { return cfg < 0 || cfg >= kNumCfgs ? 0 : lds_bytes(kCfgs[cfg]); }
 
+extern "C" int jr_conv_halo_ks(int cfg) { return cfg < 0 || cfg >= kNumCfgs ? 0 : kCfgs[cfg].ks; }
+
 extern "C" int jr_conv_halo(const ConvHaloParams* p, int cfg, hipStream_t stream) {
   if (cfg < 0 || cfg >= kNumCfgs || p->ntiles <= 0) return (int)hipErrorInvalidValue;
   const HaloCfg& c = kCfgs[cfg];
   const int lds = lds_bytes(c);
 #define JR_HALO_CONV(CIN_, WCO_, WPX_, TN_, TR_, TC_) \
-  if (c.cin == CIN_ && c.wco == WCO_ && c.wpx == WPX_ && c.tn == TN_ && c.tr == TR_ && c.tc == TC_) \
+  if (c.ks == 3 && c.cin == CIN_ && c.wco == WCO_ && c.wpx == WPX_ && c.tn == TN_ && c.tr == TR_ && c.tc == TC_) \
     return launch<CIN_, WCO_, WPX_, TN_, TR_, TC_>(*p, stream, lds);
+#define JR_HALO_CONV4(CIN_, WCO_, WPX_, TN_, TR_, TC_) \
+  if (c.ks == 4 && c.cin == CIN_ && c.wco == WCO_ && c.wpx == WPX_ && c.tn == TN_ && c.tr == TR_ && c.tc == TC_) \
+    return launch<CIN_, WCO_, WPX_, TN_, TR_, TC_, 4>(*p, stream, lds);
   JR_HALO_CONV(64, 2, 2, 4, 16, 16) JR_HALO_CONV(64, 2, 2, 2, 8, 16) JR_HALO_CONV(96, 3, 2, 2, 8, 16)
   JR_HALO_CONV(96, 3, 1, 2, 4, 16) JR_HALO_CONV(128, 4, 2, 2, 8, 16) JR_HALO_CONV(128, 4, 1, 2, 4, 16)
   JR_HALO_CONV(128, 2, 2, 2, 8, 16) JR_HALO_CONV(128, 2, 1, 1, 4, 8) JR_HALO_CONV(256, 2, 2, 2, 8, 16)
@@ -383,6 +395,8 @@ extern "C" int jr_conv_halo(const ConvHaloParams* p, int cfg, hipStream_t stream
   JR_HALO_CONV(128, 8, 1, 4, 8, 16) JR_HALO_CONV(128, 2, 1, 4, 8, 16) JR_HALO_CONV(256, 6, 1, 2, 4, 16)
   JR_HALO_CONV(256, 4, 1, 2, 4, 16) JR_HALO_CONV(256, 1, 2, 2, 8, 16) JR_HALO_CONV(256, 1, 4, 1, 8, 16)
   JR_HALO_CONV(128, 1, 2, 2, 8, 16) JR_HALO_CONV(128, 1, 4, 1, 8, 16)
+  JR_HALO_CONV4(16, 2, 2, 2, 8, 16) JR_HALO_CONV4(16, 2, 2, 4, 16, 16)
+#undef JR_HALO_CONV4
 #undef JR_HALO_CONV
   return (int)hipErrorInvalidValue;
 }

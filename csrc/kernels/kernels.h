@@ -437,6 +437,8 @@ int jr_conv_halo(const ConvHaloParams* p, int cfg, hipStream_t stream);
 // table entry: {cin, WCO, WPX, TN, TR, TC} (returns 0 for an unknown cfg); LDS bytes
 int jr_conv_halo_cfg(int cfg, int* out6);
 int jr_conv_halo_lds(int cfg);
+// kernel size of a table entry (3, or 4 for the space-to-depth stem configs; 0 for an unknown cfg)
+int jr_conv_halo_ks(int cfg);
 // per-channel stats [N][C][2] from partials [N][nb][C][2] (channel_stats_final_kernel)
 int jr_channel_stats_final(const float* part, int N, int nb, int C, float* stats, hipStream_t stream);
 

@@ -210,7 +210,7 @@ constexpr int kHaloCfg0 = 100;
 
 bool conv_halo_ok_cfg(int64_t cfg, int64_t cin8, int64_t cout) {
   int c[6];
-  if (!jr_conv_halo_cfg((int)(cfg - kHaloCfg0), c)) return false;
+  if (!jr_conv_halo_cfg((int)(cfg - kHaloCfg0), c) || jr_conv_halo_ks((int)(cfg - kHaloCfg0)) != 3) return false;
   return c[0] == cin8 && cout <= 512 && jr_conv_halo_lds((int)(cfg - kHaloCfg0)) <= 160 * 1024;
 }
 
@@ -225,13 +225,19 @@ static Launch make_conv_halo(const TList& t, const IList& i, double alpha, std::
   const int N = (int)i[0], H = (int)i[1], W = (int)i[2], xoff = (int)i[3], cin8 = (int)i[4];
   const int KH = (int)i[5], KW = (int)i[6], SH = (int)i[7], SW = (int)i[8], PH = (int)i[9], PW = (int)i[10];
   const int cout = (int)i[11], act = (int)i[12], epi = (int)i[19];
-  TORCH_CHECK(KH == 3 && KW == 3 && SH == 1 && SW == 1 && PH == 1 && PW == 1 && epi == EPI_STD &&
+  // kernel size 3 (pad 1) or 4: the space-to-depth stem, pads 2 (top / left) and 1, i.e. a
+  // 4x4 / pad-2 spec whose output size is forced to the input's (out_hw = (H, W))
+  const int ks = jr_conv_halo_ks(cfg);
+  const bool geom3 = ks == 3 && PH == 1 && PW == 1 && (i.size() < 26 || (i[22] <= 0 && i[23] <= 0));
+  const bool geom4 = ks == 4 && PH == 2 && PW == 2 && i.size() >= 26 && i[22] == H && i[23] == W;
+  TORCH_CHECK(KH == ks && KW == ks && SH == 1 && SW == 1 && (geom3 || geom4) && epi == EPI_STD &&
                   (act == 0 || act == 1) && alpha == 1.0 && !opt(t, 11).defined() &&   // ACT_NONE / ACT_RELU
-                  !opt(t, 6).defined() && (i.size() < 26 || (i[22] <= 0 && i[23] <= 0 && i[24] == 0 && i[25] == 0)),
-              "conv_halo: a 3x3 / stride-1 / pad-1 EPI_STD conv (relu / none, no alpha / bias map / state)");
+                  !opt(t, 6).defined() && (i.size() < 26 || (i[24] == 0 && i[25] == 0)),
+              "conv_halo: a 3x3 / stride-1 / pad-1 (or stem 4x4 / pad-2, output = input size) EPI_STD conv "
+              "(relu / none, no alpha / bias map / state)");
   TORCH_CHECK(c[0] == cin8 && cin8 % 16 == 0, "conv_halo: config ", i[20], " is for ", c[0], " input channels, got ", cin8);
   const int cpad = (cout + 31) / 32 * 32;
-  TORCH_CHECK(wh.numel() == (int64_t)cpad * 9 * cin8, "conv_halo: halo weights (pack_gru_halo, cout padded to 32)");
+  TORCH_CHECK(wh.numel() == (int64_t)cpad * ks * ks * cin8, "conv_halo: halo weights (pack_gru_halo, cout padded to 32)");
   TORCH_CHECK(cs(x) % 8 == 0 && xoff % 8 == 0 && xoff + cin8 <= cs(x) && x.numel() >= (int64_t)N * H * W * cs(x),
               "conv_halo: input channel slice");
   const int64_t M = (int64_t)N * H * W;

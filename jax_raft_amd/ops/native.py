@@ -239,7 +239,18 @@ class ConvSpec:
 
     @property
     def halo_shape(self) -> bool:
-        return (self.kh, self.kw, self.sh, self.sw, self.ph, self.pw) == (3, 3, 1, 1, 1, 1) and self.cin8 % 16 == 0
+        return self.halo_ks != 0
+
+    @property
+    def halo_ks(self) -> int:
+        """3: a 3x3 / stride-1 / pad-1 conv the halo kernel runs; 4: the space-to-depth stem
+        (4x4 / pad 2, output cropped to the input size, 16 input channels); else 0."""
+        g = (self.kh, self.kw, self.sh, self.sw, self.ph, self.pw)
+        if g == (3, 3, 1, 1, 1, 1) and self.cin8 % 16 == 0:
+            return 3
+        if g == (4, 4, 1, 1, 2, 2) and self.cin8 == 16:
+            return 4
+        return 0
 
 
 # halo 3x3 conv tile configs (csrc/kernels/conv_halo.hip kCfgs; conv op cfg id = HALO_CFG0 + index):
@@ -251,6 +262,13 @@ HALO_CFGS = ((64, 2, 2, 4, 16, 16), (64, 2, 2, 2, 8, 16), (96, 3, 2, 2, 8, 16), 
              (256, 2, 1, 2, 4, 16), (256, 6, 1, 4, 8, 16), (256, 4, 1, 4, 8, 16), (128, 8, 1, 4, 8, 16),
              (128, 2, 1, 4, 8, 16), (256, 6, 1, 2, 4, 16), (256, 4, 1, 2, 4, 16), (256, 1, 2, 2, 8, 16),
              (256, 1, 4, 1, 8, 16), (128, 1, 2, 2, 8, 16), (128, 1, 4, 1, 8, 16))
+# the 4x4 space-to-depth stem (kCfgs entries with ks = 4): conv op cfg id -> the same fields
+HALO_STEM_CFGS = {HALO_CFG0 + len(HALO_CFGS): (16, 2, 2, 2, 8, 16), HALO_CFG0 + len(HALO_CFGS) + 1: (16, 2, 2, 4, 16, 16)}
+
+
+def halo_cfg(cfg: int) -> Tuple[int, int, int, int, int, int]:
+    """(cin, waves along cout, waves along pixels, blocks per wave, tile rows, tile cols) of a halo cfg id."""
+    return HALO_STEM_CFGS[cfg] if cfg in HALO_STEM_CFGS else HALO_CFGS[cfg - HALO_CFG0]
 
 
 def pack_halo_conv(kernel: torch.Tensor, cin8: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -272,7 +290,13 @@ def halo_cfgs_for(spec: "ConvSpec", kw: dict) -> Tuple[int, ...]:
         return ()
     if kw.get("alpha", 1.0) != 1.0 or kw.get("bmap") is not None or kw.get("h32") is not None:
         return ()
-    if kw.get("out_hw") is not None or kw.get("y") is not None and kw["y"].dtype != torch.bfloat16:
+    if kw.get("y") is not None and kw["y"].dtype != torch.bfloat16:
+        return ()
+    if spec.halo_ks == 4:   # the stem: its output is the input's size (out_hw given by the caller)
+        if kw.get("out_hw") is None or spec.cout > 512:
+            return ()
+        return tuple(HALO_STEM_CFGS)
+    if kw.get("out_hw") is not None:
         return ()
     return tuple(HALO_CFG0 + i for i, c in enumerate(HALO_CFGS) if c[0] == spec.cin8 and spec.cout <= 512)
 
@@ -339,7 +363,7 @@ def make_spec(kernel: torch.Tensor, bias: torch.Tensor, stride=(1, 1), padding=(
     w = pack_weight(k, cin8)
     b = bias.detach().float().to(w.device).contiguous()
     spec = ConvSpec(w, b, kh, kw, stride[0], stride[1], padding[0], padding[1], cin, cin8, cout)
-    if spec.halo_shape and any(c[0] == cin8 for c in HALO_CFGS):
+    if spec.halo_ks == 4 or (spec.halo_shape and any(c[0] == cin8 for c in HALO_CFGS)):
         spec.wh = pack_halo_conv(k, cin8)
     return spec
 

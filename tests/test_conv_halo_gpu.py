@@ -190,3 +190,32 @@ def test_training_repack_of_halo_weights(cin, cout):
     assert torch.equal(sp.wh, want_f)
     if want_t is not None:
         assert torch.equal(tp.wh, want_t)
+
+
+@pytest.mark.parametrize("cfg", sorted(__import__("jax_raft_amd.ops.native", fromlist=["x"]).HALO_STEM_CFGS))
+def test_conv_halo_stem_matches_reference(cfg):
+    """The encoders' 7x7 / stride-2 / pad-3 stem as the halo kernel's 4x4 configs over the 2x2
+    space-to-depth input (ops/native.py:s2d_stem_kernel; pads 2 / 1, output = input size)
+    against the fp32 golden 7x7 conv, with relu, on maps that are not tile multiples."""
+    nat = _nat()
+    torch.manual_seed(cfg)
+    for (N, H, W) in ((1, 38, 74), (2, 22, 36)):
+        x = torch.randn(N, H, W, 3)
+        k = torch.randn(7, 7, 3, 64) / math.sqrt(147)
+        b = torch.randn(64) * 0.1
+        ref = torch.relu(R.conv2d_nhwc(_bf(x), _bf(k), b, (2, 2), (3, 3)))
+        h, w = H // 2, W // 2
+        xs = torch.zeros(N, h, w, 16)
+        for sy in range(2):
+            for sx in range(2):
+                c0 = (sy * 2 + sx) * 3
+                xs[..., c0:c0 + 3] = x[:, sy::2, sx::2]
+        spec = nat.make_spec(nat.s2d_stem_kernel(k), b, (1, 1), (2, 2), cin8=16, device=DEV)
+        assert spec.halo_ks == 4 and cfg in nat.halo_cfgs_for(spec, {"out_hw": (h, w)})
+        xg = xs.to(DEV, torch.bfloat16)
+        for c in (cfg, None):   # the halo stem and the implicit GEMM it replaces
+            y = torch.full((N * h * w, 64), 7.0, dtype=torch.bfloat16, device=DEV)
+            t, i, a = nat.conv_args(spec, xg, N, h, w, y, act=nat.ACT_RELU, out_hw=(h, w), cfg=c)
+            nat.ops().conv(t, i, a)
+            torch.cuda.synchronize()
+            assert _rel(y.float().cpu().reshape(N, h, w, 64), ref) < 1e-2, (cfg, c, N, H, W)

@@ -111,7 +111,7 @@ def main():
                   f"({flop / best_igemm[0] / 1e6:.0f} TF/s)")
         for t, c in res:
             if c >= nat.HALO_CFG0:
-                print(f"   halo {c} {nat.HALO_CFGS[c - nat.HALO_CFG0]}: {t:7.1f} us  {flop / t / 1e6:6.0f} TF/s")
+                print(f"   halo {c} {nat.halo_cfg(c)}: {t:7.1f} us  {flop / t / 1e6:6.0f} TF/s")
 
 
 if __name__ == "__main__":
