@@ -43,16 +43,17 @@ constexpr int pitch_of() { return CIN <= 64 ? 8 : CIN <= 128 ? 16 : 32; }
 
 // INN: the input is normalised (+ residual) while loading (p.in_stats set); a separate
 // instantiation so the plain convs keep their register budget
-// occupancy floors: the 64-channel configs 4 waves / SIMD plain (ring 8 deep, 120 VGPRs: encoder
-// layer 1 44.2 -> 41.4 us, with stats 48.3 -> 43.5, profiles/r5_halo_l1_occupancy.txt), 3 with the
-// normalising loader (at 4 it spills); the 96-channel normalising ones 3 (ring 8 deep: layer 2 with
+// occupancy floors: the 64-channel configs 4 waves / SIMD (ring 8 deep, 120 VGPRs: encoder layer 1
+// 44.2 -> 41.4 us, with stats 48.3 -> 43.5, profiles/r5_halo_l1_occupancy.txt; the normalising
+// loader too, with its footprint loads in batches of 3 to fit: 52.9 -> 51.3 us with norm + stats,
+// 58.4 -> 55.9 with the residual); the 96-channel normalising ones 3 (ring 8 deep: layer 2 with
 // norm + stats 35.6 -> 30.3 us, profiles/r5_halo_l2_occupancy.txt; the same for the 128-channel
 // ones measured slower); the other normalising small-tile configs 2 (without it they took 300-420
 // VGPRs, one wave per SIMD).  The workgroup counts are the ones hipcc caps at these budgets
 // without spilling.
 template <int CIN, int WCO, int WPX, int TN, bool INN>
 constexpr int halo_min_blocks() {
-  return TN > 2 ? 1 : CIN <= 64 ? (INN ? 3 : 4) : CIN <= 96 ? (INN ? 3 : 1) : !INN ? 1 : WCO * WPX == 1 ? 4 : WCO * WPX <= 4 ? 2 : 1;
+  return TN > 2 ? 1 : CIN <= 64 ? 4 : CIN <= 96 ? (INN ? 3 : 1) : !INN ? 1 : WCO * WPX == 1 ? 4 : WCO * WPX <= 4 ? 2 : 1;
 }
 
 // KS: the kernel size (3: every 3x3 / pad-1 conv; 4: the encoders' 7x7 / stride-2 stem as a 4x4 conv
@@ -102,7 +103,7 @@ void conv_halo_kernel(const ConvHaloParams p) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)p.in_res, (short)0, (int)p.in_res_bytes, 0x00020000);
     constexpr int TOTAL = NFP * CC;
     constexpr int NL = (TOTAL + NT - 1) / NT;
-    constexpr int NBMAX = INN || WIDE ? 8 : 16;   // the normalising loader holds the residual chunks too
+    constexpr int NBMAX = INN && CIN <= 64 ? 3 : INN || WIDE ? 8 : 16;   // the normalising loader holds the residual chunks too
     constexpr int NBAT = NL < NBMAX ? NL : NBMAX;
     constexpr bool norm = INN;
     const bool resid = INN && p.in_res != nullptr;
