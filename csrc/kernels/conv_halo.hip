@@ -70,7 +70,9 @@ void conv_halo_kernel(const ConvHaloParams p) {
   // weight ring depth: 16 fragments, 8 for the 4-block waves at 2 waves / SIMD (256 VGPRs; each
   // fragment there feeds 4 MFMAs, so 8 in flight still cover ~1000 cycles of L2 latency)
   constexpr bool WIDE = TN >= 4 && WCO * WPX > 4;
-  constexpr int PD = S >= 16 ? ((WIDE || CIN <= 96) ? 8 : 16) : S;   // (64 / 96 ch: 4 waves / SIMD)
+  // 12- / 16-wave workgroups (3 / 4 waves per SIMD, <= 168 / 128 VGPRs): 8-deep rings too
+  constexpr bool MANY = WCO * WPX >= 12;
+  constexpr int PD = S >= 16 ? (WCO * WPX >= 16 ? 4 : (WIDE || MANY || CIN <= 96) ? 8 : 16) : S;   // (64 / 96 ch: 4 waves / SIMD)
   constexpr int FW = TC + KS - 1;
   constexpr int NFP = (TR + KS - 1) * FW;
   constexpr int RB = P * 16;              // footprint row bytes
@@ -103,7 +105,8 @@ void conv_halo_kernel(const ConvHaloParams p) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)p.in_res, (short)0, (int)p.in_res_bytes, 0x00020000);
     constexpr int TOTAL = NFP * CC;
     constexpr int NL = (TOTAL + NT - 1) / NT;
-    constexpr int NBMAX = INN && CIN <= 64 ? 3 : INN || WIDE ? 8 : 16;   // the normalising loader holds the residual chunks too
+    // the normalising loader holds the residual chunks too
+    constexpr int NBMAX = MANY ? 4 : INN && CIN <= 64 ? 3 : INN || WIDE ? 8 : 16;
     constexpr int NBAT = NL < NBMAX ? NL : NBMAX;
     constexpr bool norm = INN;
     const bool resid = INN && p.in_res != nullptr;
@@ -339,6 +342,11 @@ constexpr HaloCfg kCfgs[] = {
     {256, 1, 2, 2, 8, 16},  {256, 1, 4, 1, 8, 16},  {128, 1, 2, 2, 8, 16},  {128, 1, 4, 1, 8, 16},
     // the space-to-depth stem (4x4 over 16 input channels, 64 outputs)
     {16, 2, 2, 2, 8, 16, 4},  {16, 2, 2, 4, 16, 16, 4},
+    // round 6: 128-pixel tiles with 2-block waves split over the pixels (WPX = 2), so every SIMD
+    // holds the same number of waves (the 6-wave whole-cout tiles above leave two SIMDs with
+    // twice the MFMAs of the other two), and 256-pixel tiles for the 128-channel convs
+    {256, 6, 2, 2, 8, 16},  {256, 4, 2, 2, 8, 16},  {128, 8, 2, 2, 8, 16},  {128, 4, 2, 4, 16, 16},
+    {128, 2, 4, 2, 16, 16},
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -396,6 +404,8 @@ extern "C" int jr_conv_halo(const ConvHaloParams* p, int cfg, hipStream_t stream
   JR_HALO_CONV(128, 8, 1, 4, 8, 16) JR_HALO_CONV(128, 2, 1, 4, 8, 16) JR_HALO_CONV(256, 6, 1, 2, 4, 16)
   JR_HALO_CONV(256, 4, 1, 2, 4, 16) JR_HALO_CONV(256, 1, 2, 2, 8, 16) JR_HALO_CONV(256, 1, 4, 1, 8, 16)
   JR_HALO_CONV(128, 1, 2, 2, 8, 16) JR_HALO_CONV(128, 1, 4, 1, 8, 16)
+  JR_HALO_CONV(256, 6, 2, 2, 8, 16) JR_HALO_CONV(256, 4, 2, 2, 8, 16) JR_HALO_CONV(128, 8, 2, 2, 8, 16)
+  JR_HALO_CONV(128, 4, 2, 4, 16, 16) JR_HALO_CONV(128, 2, 4, 2, 16, 16)
   JR_HALO_CONV4(16, 2, 2, 2, 8, 16) JR_HALO_CONV4(16, 2, 2, 4, 16, 16)
 #undef JR_HALO_CONV4
 #undef JR_HALO_CONV

@@ -14,6 +14,7 @@ from jax_raft_amd.ops import native as nat  # noqa: E402
 
 def main():
     B, h, w = int(sys.argv[1]) if len(sys.argv) > 1 else 4, 55, 128
+    tiles = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     M = B * h * w
     dev = torch.device("cuda", 0)
     feat = torch.randn(M, 256, device=dev).to(torch.bfloat16)
@@ -23,7 +24,7 @@ def main():
     out = torch.empty(B, 8 * h, 8 * w, 2, device=dev)
 
     def run():
-        nat.ops().convex_head([feat, wpk, bias, flow, out], [B, h, w, 0, 0], 0.25)
+        nat.ops().convex_head([feat, wpk, bias, flow, out], [B, h, w, 0, 0, tiles], 0.25)
 
     run()
     torch.cuda.synchronize()
@@ -40,7 +41,7 @@ def main():
         e.synchronize()
         t = s.elapsed_time(e) * 1000 / 30
         best = t if best is None else min(best, t)
-    print(f"convex_head B={B}: {best:.1f} us, "
+    print(f"convex_head B={B} tiles={tiles}: {best:.1f} us, "
           f"checksum {out.double().abs().sum().item():.6e}")
 
 

@@ -79,7 +79,8 @@ def epe_metrics(epe_all: np.ndarray) -> Dict[str, float]:
 @torch.no_grad()
 def validate_sintel(model, data_root: str, iters: int = 32, dstypes: Sequence[str] = ("clean", "final"),
                     device: Optional[torch.device] = None, max_pairs: Optional[int] = None, verbose: bool = True,
-                    batch_size: int = 1, **engine_kw) -> Dict[str, Dict[str, float]]:
+                    batch_size: int = 1, device_prep: Optional[bool] = None,
+                    **engine_kw) -> Dict[str, Dict[str, float]]:
     """Reference-methodology Sintel validation of a RAFT model.
 
     ``batch_size`` pairs (consecutive pairs of this rank's shard; all Sintel
@@ -88,6 +89,10 @@ def validate_sintel(model, data_root: str, iters: int = 32, dstypes: Sequence[st
     first one, and a smaller tail batch: a new plan build, autotune, graph
     capture) is excluded, as the reference excludes its JIT compile.
     ``batch_size=1`` is exactly the reference's per-pair protocol.
+
+    ``device_prep`` (default: on for a GPU device) hands the model the raw uint8 frames: the
+    normalisation and the replicate padding run on the device (the engine's prep kernel) and the
+    model returns unpadded flows; off, they run on the host as in the reference script.
 
     Data parallel (an initialised process group): each rank takes every
     world-th pair; ``fps`` is the mean per-GPU rate (comparable to the
@@ -98,6 +103,8 @@ def validate_sintel(model, data_root: str, iters: int = 32, dstypes: Sequence[st
     device = device or (torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
     model = model.to(device).eval()
     bs = max(1, int(batch_size))
+    # on the GPU the engine takes the raw uint8 frames (device-side normalise + pad)
+    u8 = device.type == "cuda" if device_prep is None else bool(device_prep)
     results = {}
     for dstype in dstypes:
         ds = MpiSintel(data_root, "training", dstype)
@@ -108,10 +115,18 @@ def validate_sintel(model, data_root: str, iters: int = 32, dstypes: Sequence[st
         seen_shapes = set()
         for k in range(0, len(idx), bs):
             items = [ds[i] for i in idx[k:k + bs]]
-            i1 = torch.cat([normalize_image(a) for a, _, _ in items])
-            i2 = torch.cat([normalize_image(b) for _, b, _ in items])
-            padder = InputPadder(i1.shape, channels_last=True)
-            i1, i2 = padder.pad(i1, i2)
+            if u8:
+                # raw uint8 frames: x / 255 * 2 - 1 and the 'sintel' replicate padding run in the
+                # engine's prep kernel, the flows come back unpadded (models/raft.py:_forward_u8);
+                # the timed H2D moves 1 byte per channel instead of 4
+                i1 = torch.from_numpy(np.stack([a for a, _, _ in items]))
+                i2 = torch.from_numpy(np.stack([b for _, b, _ in items]))
+                padder = None
+            else:
+                i1 = torch.cat([normalize_image(a) for a, _, _ in items])
+                i2 = torch.cat([normalize_image(b) for _, b, _ in items])
+                padder = InputPadder(i1.shape, channels_last=True)
+                i1, i2 = padder.pad(i1, i2)
             if device.type == "cuda":
                 torch.cuda.synchronize(device)
             t0 = time.perf_counter()
@@ -122,7 +137,8 @@ def validate_sintel(model, data_root: str, iters: int = 32, dstypes: Sequence[st
                 t_sum += time.perf_counter() - t0
                 t_pairs += len(items)
             seen_shapes.add(tuple(i1.shape))
-            flows = padder.unpad(pred.float().cpu()).numpy()
+            pred = pred.float().cpu()
+            flows = (pred if padder is None else padder.unpad(pred)).numpy()
             for f, (_, _, gt) in zip(flows, items):
                 epe = np.sqrt(((f - gt) ** 2).sum(-1)).reshape(-1)
                 sums += [epe.sum(), (epe < 1).sum(), (epe < 3).sum(), (epe < 5).sum(), epe.size]

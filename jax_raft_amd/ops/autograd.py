@@ -316,7 +316,7 @@ def index_pyramid(pyramid: Sequence[torch.Tensor], coords, radius: int):
 def raft_forward_autograd(model, image1, image2, train: bool, num_flow_updates: int, fused=None):
     """GPU forward with autograd.  Default: the correlation pyramid + refinement
     loop as one fused native node (:mod:`jax_raft_amd.train.fused`; encoders on
-    the Functions above).  ``fused=False`` (or ``JR_FUSED_TRAIN=0``): the module
+    the Functions above).  ``fused=False`` (or ``train.fused.FUSED_TRAIN = False``): the module
     graph of :meth:`RAFT.forward_reference` with its conv / correlation / lookup
     nodes dispatched to the native Functions above (see
     :mod:`jax_raft_amd.ops.functional`)."""

@@ -264,11 +264,23 @@ HALO_CFGS = ((64, 2, 2, 4, 16, 16), (64, 2, 2, 2, 8, 16), (96, 3, 2, 2, 8, 16), 
              (256, 1, 4, 1, 8, 16), (128, 1, 2, 2, 8, 16), (128, 1, 4, 1, 8, 16))
 # the 4x4 space-to-depth stem (kCfgs entries with ks = 4): conv op cfg id -> the same fields
 HALO_STEM_CFGS = {HALO_CFG0 + len(HALO_CFGS): (16, 2, 2, 2, 8, 16), HALO_CFG0 + len(HALO_CFGS) + 1: (16, 2, 2, 4, 16, 16)}
+# round-6 3x3 configs, after the stem entries of kCfgs (ids of the older configs unchanged)
+HALO_CFGS_R6 = ((256, 6, 2, 2, 8, 16), (256, 4, 2, 2, 8, 16), (128, 8, 2, 2, 8, 16), (128, 4, 2, 4, 16, 16),
+                (128, 2, 4, 2, 16, 16))
+# every 3x3 config: cfg id -> (cin, waves along cout, waves along pixels, blocks per wave, tile rows, tile cols)
+HALO_3X3 = {**{HALO_CFG0 + i: c for i, c in enumerate(HALO_CFGS)},
+            **{HALO_CFG0 + len(HALO_CFGS) + len(HALO_STEM_CFGS) + i: c for i, c in enumerate(HALO_CFGS_R6)}}
 
 
 def halo_cfg(cfg: int) -> Tuple[int, int, int, int, int, int]:
     """(cin, waves along cout, waves along pixels, blocks per wave, tile rows, tile cols) of a halo cfg id."""
-    return HALO_STEM_CFGS[cfg] if cfg in HALO_STEM_CFGS else HALO_CFGS[cfg - HALO_CFG0]
+    return HALO_STEM_CFGS[cfg] if cfg in HALO_STEM_CFGS else HALO_3X3[cfg]
+
+
+def halo_max_blocks(cin8: int, H: int, W: int) -> int:
+    """The most statistics-partial blocks per image any 3x3 config of ``cin8`` input channels
+    writes for an H x W output (tiles x pixel waves): the size of a ``stats_part`` buffer."""
+    return max(-(-H // c[4]) * -(-W // c[5]) * c[2] for c in HALO_3X3.values() if c[0] == cin8)
 
 
 def pack_halo_conv(kernel: torch.Tensor, cin8: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -298,7 +310,7 @@ def halo_cfgs_for(spec: "ConvSpec", kw: dict) -> Tuple[int, ...]:
         return tuple(HALO_STEM_CFGS)
     if kw.get("out_hw") is not None:
         return ()
-    return tuple(HALO_CFG0 + i for i, c in enumerate(HALO_CFGS) if c[0] == spec.cin8 and spec.cout <= 512)
+    return tuple(i for i, c in HALO_3X3.items() if c[0] == spec.cin8 and spec.cout <= 512)
 
 
 def _row_perm(cout_pad: int) -> torch.Tensor:

@@ -403,9 +403,17 @@ class RaftEngine:
             self._drop_group(g)
             n -= 1
 
+    def _quiesce(self) -> None:
+        """Wait for this engine's launched work before plans are destroyed: Plan::~Plan destroys
+        graph execs, events and lane streams, and HIP does not document that destroying a graph
+        exec still running is deferred until it finishes.  Eviction / release are rare."""
+        if self.device.type == "cuda" and self._states and not torch.cuda.is_current_stream_capturing():
+            torch.cuda.synchronize(self.device)
+
     def _drop_group(self, g: tuple) -> None:
         # a plan's pipelined graph holds the other slot's kernel nodes (its buffers): the whole
         # group goes at once
+        self._quiesce()
         for k in [k for k in self._states if self._group(k) == g]:
             del self._states[k]
         if self._pp is not None and self._pp["key"] == g:
@@ -416,6 +424,7 @@ class RaftEngine:
         now (the next forward rebuilds).  Not while a :meth:`pipelined` batch is pending."""
         if self._pp is not None and self._pp["pending"] is not None:
             raise RuntimeError("release(): flush() the pending pipelined batch first")
+        self._quiesce()
         self._states.clear()
         self._pp = None
         self._done_ev = None
@@ -780,7 +789,7 @@ class RaftEngine:
             output relu(IN(x) + [IN](res)), built on the fly and written to ``xn``."""
             s = sp[name]
             y = alloc(name + ".y", (N, H, W, s.cout))
-            nb_max = max(-(-H // c[4]) * -(-W // c[5]) * c[2] for c in nat.HALO_CFGS if c[0] == s.cin8)
+            nb_max = nat.halo_max_blocks(s.cin8, H, W)
             part = alloc(name + ".part", (N, nb_max, s.cout, 2), F32)
             # a residual block's output: relu(res + relu(IN(raw))) (model.py:171-180), in_relu bits 0 + 1
             kw = dict(stats_part=part, in_stats=in_stats, in_relu=3 if in_res is not None else 1, in_hw=H * W,
@@ -789,7 +798,7 @@ class RaftEngine:
             if kw.get("cfg") is None or kw["cfg"] < nat.HALO_CFG0:   # an override chose another kernel
                 return None
             plan.add_conv(*conv_args(s, x, N, H, W, y, **kw))
-            c = nat.HALO_CFGS[kw["cfg"] - nat.HALO_CFG0]
+            c = nat.halo_cfg(kw["cfg"])
             nb = -(-H // c[4]) * -(-W // c[5]) * c[2]
             st_ = alloc(name + ".stats", (N, s.cout, 2), F32)
             plan.add_stats_final([part, st_], [N, nb, s.cout])
@@ -815,7 +824,7 @@ class RaftEngine:
         # Instance-norm encoders keep a block's output lazy -- (raw, stats, residual, its stats)
         # -- and build it inside the next block's first conv when that is a stride-1 halo conv
         # (which also writes it out for the next residual); otherwise one norm_act pass
-        # materialises it (JR_HALO_NORM=0: always).
+        # materialises it (RaftEngine.HALO_NORM = False: always).
         pend = None
 
         def materialise(p_):

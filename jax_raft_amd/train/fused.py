@@ -224,9 +224,19 @@ def record_conv(plan, spec, x, N, H, W, y, *, tx=None, ix=None, extra=None, **kw
     ops = nat.ops()
     if cfg is None:
         scratch = torch.empty(N * OH * OW, round_up(spec.cout, 8), dtype=BF16, device=x.device)
+        # fused-norm convs are timed as the kernel that will run (the normalising loader / the
+        # statistics epilogue have their own occupancy and ring depth): the real read-only norm
+        # operands, scratch copies of what the conv writes (statistics partials, xn)
+        tkw = {}
+        if fused_norm:
+            tkw = {k: kw[k] for k in ("in_stats", "in_relu", "in_hw", "in_res", "in_res_stats") if k in kw}
+            if kw.get("stats_part") is not None:
+                tkw["stats_part"] = torch.zeros_like(kw["stats_part"])
+            if kw.get("xn") is not None:
+                tkw["xn"] = torch.empty_like(kw["xn"])
         best = None
         for c in cands:
-            t, i, a = nat.conv_args(spec, x, N, H, W, scratch, x_coff=x_coff, cfg=c)
+            t, i, a = nat.conv_args(spec, x, N, H, W, scratch, x_coff=x_coff, cfg=c, **tkw)
             if extra:
                 i = i + list(extra)
             ops.conv(t, i, a)
@@ -1273,7 +1283,10 @@ def _cached(kind, model, B, H, W, T, device):
     obj = plans.get(key) if plans is not None else None
     sig = _tensor_sig(model)
     if obj is None or getattr(obj, "_sig", None) != sig or obj.stale():
-        # one plan set per model: drop other shapes / kinds first (their buffers), then build
+        # one plan set per model: drop other shapes / kinds first (their buffers), then build --
+        # after the device has finished their replays (Plan::~Plan destroys graph execs / streams)
+        if plans and torch.device(device).type == "cuda" and not torch.cuda.is_current_stream_capturing():
+            torch.cuda.synchronize(device)
         _LOOPS.pop(model, None)
         obj = None
         g = FUSED_GRAPH and not knobs.flag("JR_PLAN_CHECK")

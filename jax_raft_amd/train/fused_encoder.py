@@ -184,7 +184,7 @@ class EncoderTrain:
         if halo and (self.mode or fuse_in):
             kw = {}
             if self.mode:
-                nb_max = max(-(-u.OH // c[4]) * -(-u.OW // c[5]) * c[2] for c in nat.HALO_CFGS if c[0] == sp.cin8)
+                nb_max = nat.halo_max_blocks(sp.cin8, u.OH, u.OW)
                 kw["stats_part"] = part = self._z(N, nb_max, u.cout, 2, dtype=F32)
             src = x
             if fuse_in:
@@ -205,7 +205,7 @@ class EncoderTrain:
                 pend["done"] = True
             cfg = self.tuner(self.plan_f, sp, src, N, H, W, u.y, act=ACT_NONE, **kw)
             if self.mode:
-                c = nat.HALO_CFGS[cfg - nat.HALO_CFG0]
+                c = nat.halo_cfg(cfg)
                 self.plan_f.add_stats_final([part, u.st], [N, -(-u.OH // c[4]) * -(-u.OW // c[5]) * c[2], u.cout])
         else:
             self.tuner(self.plan_f, sp, x, N, H, W, u.y, act=ACT_NONE)

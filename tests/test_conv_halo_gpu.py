@@ -9,7 +9,9 @@ import pytest
 import torch
 
 from jax_raft_amd.models import reference as R
-from jax_raft_amd.ops.native import HALO_CFGS as _HALO
+from jax_raft_amd.ops.native import HALO_3X3 as _HALO
+
+_IDS = sorted(_HALO)   # every 3x3 config id
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -30,12 +32,11 @@ def _rel(a, b):
     return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
 
 
-@pytest.mark.parametrize("idx", range(len(_HALO)))
-def test_conv_halo_matches_reference(idx):
+@pytest.mark.parametrize("cfg", _IDS)
+def test_conv_halo_matches_reference(cfg):
     nat = _nat()
-    cfg = nat.HALO_CFG0 + idx
-    cin = nat.HALO_CFGS[idx][0]
-    torch.manual_seed(idx)
+    cin = nat.halo_cfg(cfg)[0]
+    torch.manual_seed(cfg)
     for (N, H, W, cout) in ((1, 19, 37, 64 if cin != 256 else 192), (2, 9, 20, 126)):
         x = torch.randn(N, H, W, cin)
         k = torch.randn(3, 3, cin, cout) / math.sqrt(9 * cin)
@@ -68,13 +69,12 @@ def test_conv_halo_matches_reference(idx):
             assert torch.equal(y2[:, :cout], y[:, :cout])
 
 
-@pytest.mark.parametrize("idx", range(len(_HALO)))
-def test_conv_halo_stats_partials(idx):
+@pytest.mark.parametrize("cfg", _IDS)
+def test_conv_halo_stats_partials(cfg):
     """Per-channel (sum, sumsq) of the stored outputs, per tile, reduced by the stats final
     kernel: equals the statistics of the output tensor (what channel_stats computes)."""
     nat = _nat()
-    cfg = nat.HALO_CFG0 + idx
-    cin, wco, wpx, tn, tr, tc = nat.HALO_CFGS[idx]
+    cin, wco, wpx, tn, tr, tc = nat.halo_cfg(cfg)
     torch.manual_seed(3)
     N, H, W, cout = 2, 21, 35, 96 if cin == 96 else 64
     x = torch.randn(N, H, W, cin).to(DEV, torch.bfloat16)
@@ -93,13 +93,12 @@ def test_conv_halo_stats_partials(idx):
     assert torch.allclose(stats, want, rtol=1e-4, atol=1e-2), (stats - want).abs().max()
 
 
-@pytest.mark.parametrize("idx", range(len(_HALO)))
-def test_conv_halo_input_instance_norm(idx):
+@pytest.mark.parametrize("cfg", _IDS)
+def test_conv_halo_input_instance_norm(cfg):
     """The producer's instance norm + relu applied while the footprint is loaded equals
     norm_act (jr_norm_act mode 1, relu) followed by the conv; padding stays zero."""
     nat = _nat()
-    cfg = nat.HALO_CFG0 + idx
-    cin = nat.HALO_CFGS[idx][0]
+    cin = nat.halo_cfg(cfg)[0]
     torch.manual_seed(4)
     N, H, W, cout = 2, 13, 30, 64
     x = (torch.randn(N, H, W, cin) * 2 + 0.5).to(DEV, torch.bfloat16)
@@ -120,16 +119,15 @@ def test_conv_halo_input_instance_norm(idx):
     assert _rel(y.float().cpu().reshape(N, H, W, cout), ref) < 1.5e-2
 
 
-@pytest.mark.parametrize("idx,res_norm", [(i, rn) for i in range(len(_HALO)) for rn in (False, True)])
-def test_conv_halo_builds_residual_block_output(idx, res_norm):
+@pytest.mark.parametrize("cfg,res_norm", [(i, rn) for i in _IDS for rn in (False, True)])
+def test_conv_halo_builds_residual_block_output(cfg, res_norm):
     """A residual block's output relu(relu(IN(x)) + r) (model.py:171-180; r the identity input
     or an instance-normalised downsample output) built while the footprint is loaded
     (in_relu = 3) equals norm_act + the conv, and the tile-own pixels of it are written out
     (xn) exactly once."""
     nat = _nat()
-    cfg = nat.HALO_CFG0 + idx
-    cin = nat.HALO_CFGS[idx][0]
-    torch.manual_seed(5 + idx)
+    cin = nat.halo_cfg(cfg)[0]
+    torch.manual_seed(5 + cfg)
     N, H, W, cout = 2, 13, 30, 64
     x = (torch.randn(N, H, W, cin) * 2 + 0.5).to(DEV, torch.bfloat16)
     r = (torch.randn(N, H, W, cin) * 1.5 - 0.2).to(DEV, torch.bfloat16)

@@ -14,8 +14,9 @@ import drift  # noqa: E402
 
 # measured on MI355X (profiles/r5_drift.md, round-5 tree; round 3: 1.69e-2 / 4.20e-2):
 # final-iteration EPE / mean |golden flow| = 1.70e-2 (raft_large) and 4.22e-2 (raft_small) with
-# the default bf16 engine; the bound leaves 1.2x headroom for tile-config / device differences
-REL_BOUND = {"raft_large": 1.2 * 1.70e-2, "raft_small": 1.2 * 4.22e-2}
+# the default bf16 engine; the bound leaves 1.5x headroom for tile-config (a re-tuned table picks
+# other configs, whose summation orders differ) and device differences
+REL_BOUND = {"raft_large": 1.5 * 1.70e-2, "raft_small": 1.5 * 4.22e-2}
 # fp32 engine (precision="fp32"): measured 5.5e-6 / 9.4e-6 (fp32 summation order only)
 REL_BOUND_FP32 = 3e-5
 

@@ -79,7 +79,7 @@ def test_lane_schedule_fused_gru_parity(fake, monkeypatch):
     copy into hm / hm2 by iteration parity, the update writes the flow into flow32 / flow32b,
     the lane's mask conv and convex head read the matching buffer -- and the E_MASK join is
     gone (two waits per iteration: the lane's E_FH fork and the E_FLOW join).  Opt-in
-    (JR_MASK_PARITY=1): measured slower on MI355X."""
+    (RaftEngine.MASK_PARITY = True): measured slower on MI355X."""
     monkeypatch.setattr(E.RaftEngine, "GRU", "fused")
     monkeypatch.setattr(E.RaftEngine, "MASK_PARITY", True)
     eng, p = _plan(raft_large, 4)
@@ -281,7 +281,7 @@ def test_grouped_launch_uses_the_pair_config(fake, monkeypatch):
 
 @pytest.mark.parametrize("fuse", ["1", "0"])
 def test_encoder_instance_norm_fused_into_halo_convs(fake, monkeypatch, fuse):
-    """raft_large's feature encoder (instance norm): with JR_HALO_NORM=1 every 3x3 / stride-1
+    """raft_large's feature encoder (instance norm): with RaftEngine.HALO_NORM on, every 3x3 / stride-1
     conv runs on a halo config that writes its statistics partials (one stats_final each, no
     channel_stats pass) and the conv after it normalises on load (the block-internal norm_act
     passes disappear); a block output (or the stem's) is built inside the next block's first
@@ -310,7 +310,7 @@ def test_encoder_instance_norm_fused_into_halo_convs(fake, monkeypatch, fuse):
 @pytest.mark.parametrize("arch", [raft_large, raft_small])
 def test_prologue_lanes_at_batch_one(fake, monkeypatch, arch):
     """At batch 1 the loop runs on one lane, the prologue on three: context encoder (lane 1),
-    feature encoder of image 2 (lane 2), image 1 + pyramid (lane 0); JR_PRO_LANES=0 keeps the
+    feature encoder of image 2 (lane 2), image 1 + pyramid (lane 0); RaftEngine.PRO_LANES = "off" keeps the
     whole forward on lane 0."""
     eng, p = _plan(arch, 1)
     pro_lanes = {ln for s, ln, d, op, a in p.ops if s == 0}

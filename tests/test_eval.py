@@ -97,3 +97,16 @@ def test_demo_and_convert_cli(tmp_path):
     assert out.exists()
     r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "convert_checkpoint.py")], capture_output=True, text=True)
     assert r.returncode == 1 and "Usage" in r.stdout
+
+
+def test_validate_u8_prep_equals_host_prep(tmp_path):
+    """device_prep: the model receives raw uint8 frames (normalise + 'sintel' replicate padding
+    inside the model, unpadded flows back; the GPU default) -- the same metrics as the
+    reference's host-side protocol (validate_sintel.py:177-191)."""
+    _make_sintel(str(tmp_path), scenes=1, frames=3)
+    model, _ = raft_small()
+    kw = dict(iters=2, device=torch.device("cpu"), verbose=False, dstypes=("clean",))
+    rh = validate_sintel(model, str(tmp_path), device_prep=False, **kw)["clean"]
+    ru = validate_sintel(model, str(tmp_path), device_prep=True, **kw)["clean"]
+    for k in ("epe", "1px", "3px", "5px"):
+        assert abs(rh[k] - ru[k]) < 1e-5 * max(1.0, abs(rh[k])), k
