@@ -221,7 +221,8 @@ def run_inference(ctx: Ctx, model, *, B: int, H: int, W: int, iters: int, steps:
     try:
         eng = model.engine(dev, **engine_kw)
         if mode == "auto":
-            mode = "off" if (eng.uses_lanes(B, not final_only) or engine_kw.get("split", 1) > 1) else "graph"
+            mode = "off" if (eng.uses_lanes(B, not final_only) or engine_kw.get("split", 1) > 1
+                             or getattr(eng, "fe_external", False)) else "graph"
         copipe = mode == "graph" and engine_kw.get("use_graph", True)
         if copipe:   # fill the pipeline: the first batch's prologue (its loop runs in the first step)
             eng.pipelined(img1.to(dev), img2.to(dev), iters, return_all_iters=all_iters)
@@ -385,8 +386,9 @@ def main():
     ap.add_argument("--gate-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="storage of the GRU z gate / folded context bias map (the hidden state is fp32 either way)")
     ap.add_argument("--corr-dtype", default="bf16", choices=["bf16", "fp32"], help="correlation pyramid storage")
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
-                    help="engine compute precision: bf16 MFMA operands (default) or the fp32 parity mode")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "mixed"],
+                    help="engine compute precision: bf16 MFMA operands (default), the fp32 parity mode, or "
+                         "mixed (fp32 feature encoder, bf16 rest: runtime/engine_f32.py:RaftEngineMixed)")
     ap.add_argument("--no-copy-output", action="store_true",
                     help="return the engine's static output buffer instead of a fresh tensor (measurement knob)")
     ap.add_argument("--split", type=int, default=1, help="independent batch parts captured into one hipGraph")
@@ -451,6 +453,8 @@ def main():
                 ("small_b1_fps_32it", "raft_small", 32, BASELINE_SMALL_FPS, "bf16", "stream", (H, W)),
                 ("small_b1_sync_32it", "raft_small", 32, BASELINE_SMALL_FPS, "bf16", "sync", (H, W)),
                 ("small_b1_fps_12it", "raft_small", 12, None, "bf16", "stream", (H, W)),
+                # precision="mixed": fp32 feature encoder (raft_small's bf16 drift, profiles/r6_drift_mixed.md)
+                ("small_b1_sync_32it_mixed", "raft_small", 32, BASELINE_SMALL_FPS, "mixed", "sync", (H, W)),
                 ("fp32_b1_fps", "raft_large", 32, BASELINE_FPS, "fp32", "stream", (H, W)),
                 ("hires_b1", "raft_large", 32, None, "bf16", "stream", (1088, 1920))]
         skip = set(filter(None, args.skip_extras.split(",")))

@@ -660,13 +660,16 @@ extern "C" int jr_corr_pyramid(const void* f1, const void* f2, int B, int h, int
   // the persistent kernel (corr_pyr.hip) holds every CU for the whole build: at batch 1 the
   // pipelined graph runs the previous pair's loop concurrently, and the short-lived tiles of
   // the kernel below interleave with it (measured b1 stream 227 vs 200-204 FPS)
-  if (blocked && nq == h * w && B >= 2) {
+  // blocked == 2: the plan is never replayed next to another forward's loop (runtime/engine.py,
+  // not a pipelined slot), so the persistent kernel also serves batch 1
+  if (blocked && nq == h * w && (B >= 2 || blocked == 2)) {
     const int e = jr_corr_pyramid_blocked(f1, f2, B, h, w, C, cs, lvl0, lvl1, lvl2, lvl3, num_levels, scale, stream);
     if (e != (int)hipErrorNotSupported) return e;
   }
   if (wide)
     hipLaunchKernelGGL((corr_pyramid_kernel<bf16, true>), grid, dim3(256), 0, stream, (const bf16*)f1, (const bf16*)f2,
-                       h, w, nq, C, cs, (bf16*)lvl0, (bf16*)lvl1, (bf16*)lvl2, (bf16*)lvl3, num_levels, scale, blocked);
+                       h, w, nq, C, cs, (bf16*)lvl0, (bf16*)lvl1, (bf16*)lvl2, (bf16*)lvl3, num_levels, scale,
+                       blocked ? 1 : 0);
   else if (out_bf16)
     hipLaunchKernelGGL((corr_pyramid_kernel<bf16, false>), grid, dim3(256), 0, stream, (const bf16*)f1,
                        (const bf16*)f2, h, w, nq, C, cs, (bf16*)lvl0, (bf16*)lvl1, (bf16*)lvl2, (bf16*)lvl3,

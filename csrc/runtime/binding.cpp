@@ -975,7 +975,7 @@ static Launch make_corr(const TList& t, const IList& i, double scale, std::vecto
   check_bf16(f1, "f1"); check_bf16(f2, "f2");
   const int B = (int)i[0], h = (int)i[1], w = (int)i[2], C = (int)i[3], L = (int)i[4];
   // optional i[5]: query pixels per image in f1 (a slab of query rows; default all h*w);
-  // optional i[6]: 1 = blocked level layout (kernels.h)
+  // optional i[6]: 1 = blocked level layout (kernels.h), 2 = blocked + the persistent kernel at any batch
   const int nq = i.size() > 5 ? (int)i[5] : h * w;
   const int blocked = i.size() > 6 ? (int)i[6] : 0;
   TORCH_CHECK(!blocked || (w % 16 == 0 && (h * w) % 8 == 0 && nq == h * w),

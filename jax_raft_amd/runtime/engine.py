@@ -234,14 +234,18 @@ class RaftEngine:
     """
 
     def __new__(cls, *args, precision: str = "bf16", **kwargs):
-        if precision not in ("bf16", "fp32"):
-            raise ValueError(f"precision must be 'bf16' or 'fp32', got {precision!r}")
+        if precision not in ("bf16", "fp32", "mixed"):
+            raise ValueError(f"precision must be 'bf16', 'fp32' or 'mixed', got {precision!r}")
         if precision == "fp32" and cls is RaftEngine:
             from .engine_f32 import RaftEngineF32
             cls = RaftEngineF32
+        elif precision == "mixed" and cls is RaftEngine:
+            from .engine_f32 import RaftEngineMixed
+            cls = RaftEngineMixed
         return super().__new__(cls)
 
     precision = "bf16"
+    fe_external = False   # the feature encoder runs outside the plan (RaftEngineMixed: fp32), fmap filled before it
 
     # Lowering choices.  Each is the measured winner of an A/B (the profile is cited where the
     # choice is used); they are class attributes rather than environment switches so that tests
@@ -253,6 +257,7 @@ class RaftEngine:
     MERGED_UP = True      # one-lane loop: 7x7 flow conv merged with the x8 upsampling (merged.hip)
     CONV_GROUP = True     # one-lane loop: last correlation conv + convflow2 as one grouped grid
     MASK_PARITY = False   # lane schedule: parity-buffered h copy for the mask lane (slower at b4)
+    CORR_PERSIST_B1 = True   # the persistent blocked pyramid kernel at batch 1 too (plans outside pipelined slots)
     HOST_GATE = True      # host gate of long replays (see GATE_MIN_ITERS)
 
     def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True,
@@ -1216,7 +1221,9 @@ class RaftEngine:
         plan.add_record(E_CTX)
 
         fmap = alloc("fmap", (2 * B, h, w, self.fmap_ch))
-        if p_on:
+        if self.fe_external:
+            lane(p_main)   # fmap is written before each replay (RaftEngineMixed._pre_launch)
+        elif p_on:
             # the feature encoder of image2 on a third lane, concurrent with image1's
             # (and the context encoder): per-image instance norms, so the halves are
             # exact, and the sequential encoder chain that gates the correlation
@@ -1257,7 +1264,11 @@ class RaftEngine:
                 plan.add_corr([fmap[b, r0:r1], fmap[B + b]] + [v[b * nq:(b + 1) * nq] for v in levels] + [None] * (4 - L),
                               [1, h, w, self.fmap_ch, L, nq, 0], scale)
         else:
-            plan.add_corr([fmap[:B], fmap[B:]] + levels + [None] * (4 - L), [B, h, w, self.fmap_ch, L, h * w, blocked],
+            # blocked 2: the persistent pyramid kernel (corr_pyr.hip) also at batch 1 -- not in a
+            # pipelined slot, whose graph runs it next to the previous pair's loop (there the
+            # short-lived tiles interleave better: b1 stream 227 vs 200-204 FPS, round 4)
+            bl = 2 if (blocked and self.CORR_PERSIST_B1 and not getattr(self, "_slot_build", False)) else blocked
+            plan.add_corr([fmap[:B], fmap[B:]] + levels + [None] * (4 - L), [B, h, w, self.fmap_ch, L, h * w, bl],
                           scale)
         plan.add_wait(E_CTX)
 
@@ -1568,6 +1579,7 @@ class RaftEngine:
         st = self._plan_state(key, lambda: self._build_key(key))
         st.inp1.copy_(image1)
         st.inp2.copy_(image2)
+        self._pre_launch(st)
         fresh = self.copy_output and st.slot_ok
         out = torch.empty_like(st.out) if fresh else st.out
         self._point_slot(st, out)
@@ -1591,6 +1603,9 @@ class RaftEngine:
         if fresh:
             return self._crop(st, out)
         return self._crop(st, st.out.clone() if self.copy_output else st.out)
+
+    def _pre_launch(self, st: _PlanState) -> None:
+        """Work a forward runs before replaying its plan (RaftEngineMixed: the fp32 feature encoder)."""
 
     GATE_MIN_ITERS = 20
 
@@ -1617,10 +1632,12 @@ class RaftEngine:
     def _slot_state(self, key, slot: int) -> _PlanState:
         def build():
             saved, self.split = self.split, 1
+            self._slot_build = True
             try:
                 return self._build_key(key)
             finally:
                 self.split = saved
+                self._slot_build = False
 
         return self._plan_state(key + ("pslot", slot), build)
 
@@ -1649,6 +1666,8 @@ class RaftEngine:
                 raise RuntimeError("pipelined(): the weights changed while a batch is pending; flush() it first")
             self._pack()
         assert self.use_graph, "pipelined() replays captured graphs (use_graph=True)"
+        if self.fe_external:
+            raise NotImplementedError("pipelined(): not with precision='mixed' (its fp32 encoder runs before the plan)")
         assert not self.cp, "pipelined(): not with context parallelism (a host-driven loop)"
         if image1.dtype == torch.uint8 and not self._native_u8:
             a, b, src = self._host_u8(image1, image2)

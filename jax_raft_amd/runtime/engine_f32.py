@@ -305,3 +305,69 @@ class RaftEngineF32(RaftEngine):
         if not all_iters:
             upsample(0)
         return st
+
+
+class RaftEngineMixed(RaftEngine):
+    """``RaftEngine(..., precision="mixed")``: the feature encoder in fp32 (this module's fp32
+    lowering, one plan of its own), everything else on the bf16 engine.
+
+    raft_small's bf16 drift at 32 iterations (4.2 % relative EPE vs the fp32 golden against
+    1.7 % for raft_large, profiles/r5_drift.md) comes from its feature encoder's high-resolution
+    layers (profiles/r5_precision_bisect.md): 32 / 64 channels at 1/2 and 1/4 resolution, whose
+    instance norms amplify the bf16 rounding of the correlation features.  Here the feature maps
+    come from the fp32 encoder (fp32 convs, statistics and norms) and are rounded to bf16 once,
+    as the correlation pyramid's input; the context encoder, the pyramid and the refinement loop
+    are the bf16 engine's.  Per forward: the fp32 plan (prep, encoder, final 1x1 conv), one
+    cast of the feature maps into the bf16 plan's buffer, then the bf16 plan without its feature
+    encoder.  Cost and drift: profiles/r6_drift_mixed.md.  One-lane prologue, no
+    :meth:`pipelined`, no batch split."""
+
+    precision = "mixed"
+    fe_external = True
+    _native_u8 = False   # uint8 frames: normalised + padded by framework ops (the fp32 prep reads fp32)
+
+    def __init__(self, model, device, use_graph: bool = True, copy_output: bool = True, **kw):
+        kw.pop("precision", None)
+        kw["split"] = 1
+        super().__init__(model, device, use_graph=use_graph, copy_output=copy_output, **kw)
+        self._f32 = RaftEngineF32(model, device, use_graph=use_graph, copy_output=False, precision="fp32")
+
+    def _hold_model_weakly(self) -> None:
+        super()._hold_model_weakly()
+        self._f32._hold_model_weakly()
+
+    def _build(self, B: int, H: int, W: int, n_iters: int, all_iters: bool = True, src=None) -> _PlanState:
+        assert src is None, "mixed engine: uint8 frames are prepared by RaftEngine._host_u8"
+        st = super()._build(B, H, W, n_iters, all_iters, src)
+        f = self._f32
+        if f._stale():
+            f._pack()
+        h, w = H // 8, W // 8
+        plan = nat.new_plan()
+        plan.set_segment(0)
+        plan.set_lane(0)
+        fst = _PlanState(plan=plan, plans=[plan], n_iters=0)
+        x0 = torch.zeros((2 * B, H, W, 4), dtype=F32, device=self.device)
+        fst.bufs["x0"] = x0
+        plan.add_prep_f32([st.inp1, st.inp2, x0], [B, H, W])
+        feat, fh_, fw_ = f._encoder_f32(fst, plan, "fe", self.model.feature_encoder, x0, 2 * B, H, W)
+        assert (fh_, fw_) == (h, w), "The feature encoder should downsample H and W by 8"
+        fmap32 = torch.zeros((2 * B, h, w, self.fmap_ch), dtype=F32, device=self.device)
+        fst.bufs["fmap32"] = fmap32
+        f._conv(plan, f._specs["fe.conv"], feat, 2 * B, h, w, fmap32)
+        plan.set_segment(2)
+        st.fe32 = (plan, fst, fmap32, st.bufs["p0.fmap"])
+        return st
+
+    def _pre_launch(self, st: _PlanState) -> None:
+        f = self._f32
+        if f._stale():
+            f._pack()
+        plan, _, fmap32, fmap = st.fe32
+        if self.use_graph:
+            if plan.captured_iters() != 0:
+                plan.capture(0)
+            plan.replay()
+        else:
+            plan.run(0)
+        fmap.copy_(fmap32)   # the one bf16 rounding of the feature maps (the pyramid's input)

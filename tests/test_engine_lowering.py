@@ -365,3 +365,26 @@ def test_stale_check_sees_every_change(fake):
     assert not eng._stale()
     model(torch.zeros(1, 128, 128, 3), torch.zeros(1, 128, 128, 3), num_flow_updates=1)   # a CPU forward: no change
     assert not eng._stale()
+
+
+@pytest.mark.parametrize("factory", [raft_small, raft_large])
+def test_mixed_precision_lowering(fake, factory):
+    """precision="mixed" (runtime/engine_f32.py:RaftEngineMixed): the bf16 plan has no feature
+    encoder (its fmap buffer is filled before each replay) but keeps the context encoder, the
+    pyramid and the loop; the fp32 plan holds the feature encoder of both images and its final
+    1x1 conv on the fp32 kernels."""
+    model = factory()[0].eval()
+    eng = E.RaftEngine(model, "cpu", autotune=False, precision="mixed")
+    ref = E.RaftEngine(model, "cpu", autotune=False)
+    st = eng._build(1, 128, 256, 3)
+    st_ref = ref._build(1, 128, 256, 3)
+    pro = [op for s, _, _, op, _ in st.plan.ops if s == 0]
+    pro_ref = [op for s, _, _, op, _ in st_ref.plan.ops if s == 0]
+    assert len(pro) < len(pro_ref) and "corr" in pro and "prep" in pro
+    # the loop is the bf16 engine's
+    assert st.plan.names(1) == st_ref.plan.names(1)
+    fplan = st.fe32[0]
+    fops = fplan.names(0)
+    assert fops[0] == "prep_f32" and fops.count("conv_f32") == sum(
+        1 for n in eng._f32._specs if n.startswith("fe.") and not n.endswith("stem_s2d"))
+    assert st.fe32[2].dtype == torch.float32 and st.fe32[3] is st.bufs["p0.fmap"]

@@ -712,3 +712,42 @@ def test_bgemm(batch, M, N, K, a_kmajor, out_dtype):
     torch.cuda.synchronize()
     assert not torch.isnan(c.float()).any()
     assert _rel(c.float().cpu(), ref) < (3e-3 if out_dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("C", [128, 256])
+def test_corr_blocked_persistent_batch1(C):
+    """Blocked layout 2 (runtime/engine.py CORR_PERSIST_B1): the persistent pyramid kernel of
+    corr_pyr.hip at batch 1 (the tile kernel of corr.hip served batch 1 before) -- every level
+    equals the row-major reference pyramid once un-blocked, and equals the tile kernel's output
+    (layout 1) within bf16 rounding."""
+    nat = _nat()
+    torch.manual_seed(31 + C)
+    B, h, w, L = 1, 55, 128, 4
+    f1 = torch.randn(B, h, w, C)
+    f2 = torch.randn(B, h, w, C)
+    ref = R.build_pyramid(_bf(f1), _bf(f2), L)
+    M = B * h * w
+    nty, ntx = -(-h // 8), -(-w // 16)
+    outs = []
+    for mode in (1, 2):
+        lv, hl, wl = [], h, w
+        for l in range(L):
+            shape = (M, nty * (8 >> l), ntx * (16 >> l)) if l < 2 else (M, hl, wl)
+            lv.append(torch.full(shape, float("nan"), device=DEV, dtype=torch.bfloat16))
+            hl //= 2
+            wl //= 2
+        nat.ops().corr([f1.to(DEV, torch.bfloat16), f2.to(DEV, torch.bfloat16)] + lv,
+                       [B, h, w, C, L, h * w, mode], 1.0 / math.sqrt(C))
+        torch.cuda.synchronize()
+        outs.append(lv)
+    hl, wl = h, w
+    for l in range(L):
+        for lv in outs:
+            got = lv[l].float().cpu()
+            if l < 2:
+                bh, bw = 8 >> l, 16 >> l
+                got = got.reshape(M, nty, ntx, bh, bw).permute(0, 1, 3, 2, 4).reshape(M, nty * bh, ntx * bw)[:, :hl, :wl]
+            assert not torch.isnan(got).any(), f"level {l} has unwritten cells"
+            assert (got - ref[l]).abs().max().item() < 8e-3 * max(1.0, ref[l].abs().max().item()), l
+        hl //= 2
+        wl //= 2

@@ -125,6 +125,7 @@ VARIANTS = {
     "corr_fp32": dict(corr_dtype=torch.float32),     # fp32 pyramid
     "corr_gate_fp32": dict(corr_dtype=torch.float32, gate_dtype=torch.float32),
     "fp32": dict(precision="fp32"),                  # fp32 engine (runtime/engine_f32.py)
+    "mixed": dict(precision="mixed"),                # fp32 feature encoder, bf16 rest (RaftEngineMixed)
 }
 
 
