@@ -126,6 +126,8 @@ VARIANTS = {
     "corr_gate_fp32": dict(corr_dtype=torch.float32, gate_dtype=torch.float32),
     "fp32": dict(precision="fp32"),                  # fp32 engine (runtime/engine_f32.py)
     "mixed": dict(precision="mixed"),                # fp32 feature encoder, bf16 rest (RaftEngineMixed)
+    "mixed_corr_fp32": dict(precision="mixed", corr_dtype=torch.float32),   # + fp32 pyramid
+    "mixed_corr_gate_fp32": dict(precision="mixed", corr_dtype=torch.float32, gate_dtype=torch.float32),
 }
 
 
