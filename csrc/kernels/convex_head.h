@@ -193,102 +193,4 @@ __global__ __launch_bounds__(256, 2) void convex_head_kernel(const bf16* __restr
   convex_head_block<NC>(feat, fcs, fcoff, wpk, bias, alpha, flow, B, h, w, out, out_slot, out_off, nblk, blockIdx.x,
                         sA);
 }
-// Round-6 form: NW waves per block share the group's A fragments in LDS (NW = 8: twice the
-// pixels per 72 KB copy), and the 3x3 flow neighbourhood of every pixel is loaded BEFORE the
-// GEMM (it depends only on the pixel), so the epilogue starts without a dependent global load;
-// one block per (pixel block, group), no persistence.
-template <int NC, int NW>
-__global__ __launch_bounds__(64 * NW, 2) void convex_head2_kernel(const bf16* __restrict__ feat, int fcs, int fcoff,
-                                                                  const u32x4* __restrict__ wpk,
-                                                                  const float* __restrict__ bias, float alpha,
-                                                                  const float* __restrict__ flow, int B, int h, int w,
-                                                                  float* __restrict__ out,
-                                                                  const long long* __restrict__ out_slot,
-                                                                  long out_off, int nblk) {
-  __shared__ u32x4 sA[8 * 9 * 64];
-  const int id = blockIdx.x;
-  const int g = (id >> 3) & 3, pb = (id >> 5) * 8 + (id & 7);
-  if (pb >= nblk) return;
-  if (out_slot) out = (float*)(*out_slot) + out_off;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  for (int f = wave; f < 72; f += NW)
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(wpk + (f * 4 + g) * 64 + lane),
-                                     (__attribute__((address_space(3))) void*)(sA + f * 64), 16, 0, 0);
-  const int HW = h * w, M = B * HW;
-  const int col = lane & 15, q = lane >> 4;
-  const int p0 = (pb * NW + wave) * 16 * NC;
-  u32x4 b[NC][8];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const bf16* bp = feat + (long)min(p0 + 16 * c + col, M - 1) * fcs + fcoff + 8 * q;
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) b[c][ks] = *(const u32x4*)(bp + 32 * ks);
-  }
-  float2 fl[NC][9];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const int m = min(p0 + 16 * c + col, M - 1);
-    const int b_ = m / HW, rem = m - b_ * HW;
-    const int y = rem / w, x = rem - y * w;
-    const float* fb = flow + 2L * b_ * HW;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-      const int yy = y + k / 3 - 1, xx = x + k % 3 - 1;
-      const bool in = (unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w;
-      const float2 f = *(const float2*)(fb + 2 * (in ? yy * w + xx : 0));
-      fl[c][k] = in ? f : make_float2(0.f, 0.f);
-    }
-  }
-  f32x4 acc[9][NC];
-#pragma unroll
-  for (int k = 0; k < 9; ++k)
-#pragma unroll
-    for (int c = 0; c < NC; ++c) acc[k][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  __syncthreads();   // the LDS weight copies of every wave
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-      const bf16x8 a = __builtin_bit_cast(bf16x8, sA[(ks * 9 + k) * 64 + lane]);
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-        acc[k][c] =
-            __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, b[c][ks]), acc[k][c], 0, 0, 0);
-    }
-  }
-  const float a2 = alpha * 1.4426950408889634f;
-  const int sy = 2 * g + (q >> 1), sx0 = 4 * (q & 1);
-  const long W8 = 8L * w;
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const int m = p0 + 16 * c + col;
-    if (m >= M) continue;
-    const int b_ = m / HW, rem = m - b_ * HW;
-    const int y = rem / w, x = rem - y * w;
-    float o[8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float lg[9];
-#pragma unroll
-      for (int k = 0; k < 9; ++k) lg[k] = fmaf(acc[k][c][j], a2, bias[k * 64 + 16 * g + 4 * q + j] * a2);
-      const float mx = fmaxf(fmaxf(fmaxf(lg[0], lg[1]), fmaxf(lg[2], lg[3])),
-                             fmaxf(fmaxf(lg[4], lg[5]), fmaxf(fmaxf(lg[6], lg[7]), lg[8])));
-      float sm = 0.f, ux = 0.f, uy = 0.f;
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        const float e = __builtin_amdgcn_exp2f(lg[k] - mx);
-        sm += e;
-        ux = fmaf(e, fl[c][k].x, ux);
-        uy = fmaf(e, fl[c][k].y, uy);
-      }
-      const float inv = 8.0f * rcpf_(sm);
-      o[2 * j] = ux * inv;
-      o[2 * j + 1] = uy * inv;
-    }
-    float4* op = (float4*)(out + 2 * (((long)b_ * 8 * h + 8 * y + sy) * W8 + 8 * x + sx0));
-    op[0] = make_float4(o[0], o[1], o[2], o[3]);
-    op[1] = make_float4(o[4], o[5], o[6], o[7]);
-  }
-}
-
 }  // namespace

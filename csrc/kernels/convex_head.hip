@@ -10,21 +10,6 @@ extern "C" int jr_convex_head(const void* feat, int feat_cstride, int feat_coff,
   const int M = B * h * w;
   // pixel tiles per wave (`tiles` 1 / 2, or 0 = auto): 2 when that still gives
   // >= 384 blocks (2 per CU fit: 72 KB of LDS each), else 1
-  // tiles 3 / 4 / 5: the round-6 form (convex_head2_kernel) with 8 waves x 1 tile, 4 x 2, 8 x 2
-  if (tiles >= 3 && tiles <= 5) {
-    const int nw = tiles == 4 ? 4 : 8, nc = tiles == 3 ? 1 : 2;
-    const int nblk = (M + 16 * nw * nc - 1) / (16 * nw * nc);
-    const dim3 grid((nblk + 7) / 8 * 32);
-#define JR_CH2(NC_, NW_)                                                                                           \
-  hipLaunchKernelGGL((convex_head2_kernel<NC_, NW_>), grid, dim3(64 * NW_), 0, stream, (const bf16*)feat,          \
-                     feat_cstride, feat_coff, (const u32x4*)wpk, bias, alpha, flow, B, h, w, out,                  \
-                     (const long long*)out_slot, out_off, nblk)
-    if (tiles == 3) JR_CH2(1, 8);
-    else if (tiles == 4) JR_CH2(2, 4);
-    else JR_CH2(2, 8);
-#undef JR_CH2
-    return (int)hipGetLastError();
-  }
   auto blocks = [M](int nc) { return (M + 64 * nc - 1) / (64 * nc); };
   const int nc = tiles == 1 || tiles == 2 ? tiles : blocks(2) * 4 >= 384 ? 2 : 1;
   const int nblk = blocks(nc);

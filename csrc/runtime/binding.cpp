@@ -1124,7 +1124,7 @@ static Launch make_convex_head(const TList& t, const IList& i, double alpha, std
   const int64_t slot_off = i.size() >= 7 ? i[6] : 0;
   TORCH_CHECK(!slot.defined() || (slot.is_cuda() && slot.scalar_type() == at::kLong && slot.numel() == 1),
               "convex_head: out_slot must be one device int64");
-  TORCH_CHECK(tiles >= 0 && tiles <= 5, "convex_head: tiles per wave 0/1/2 (3..5: the round-6 forms)");
+  TORCH_CHECK(tiles == 0 || tiles == 1 || tiles == 2, "convex_head: tiles per wave 0/1/2");
   const int B = (int)i[0], h = (int)i[1], w = (int)i[2], coff = (int)i[3];
   const int64_t stride = i[4];
   const int64_t M = (int64_t)B * h * w;

@@ -270,7 +270,7 @@ def test_small_with_mask_predictor_matches_golden(B, final_only):
         assert _epe(out[it], ref[it]) < REL_EPE["raft_small"] * mag, (it, _epe(out[it], ref[it]), mag)
 
 
-@pytest.mark.parametrize("tiles", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("tiles", [0, 1, 2])
 @pytest.mark.parametrize("B,h,w,cs,coff", [(1, 9, 13, 256, 0), (2, 55, 16, 512, 256), (4, 17, 128, 264, 8)])
 def test_convex_head_kernel_matches_fp32(B, h, w, cs, coff, tiles):
     """convex_head.hip (1x1 conv 256 -> 576 on MFMA + softmax over the 9 taps +
