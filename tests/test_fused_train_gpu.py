@@ -113,21 +113,28 @@ def test_fused_matches_unfused(factory, encoders, monkeypatch):
     ef, eu = _rel(out_f, out_r), _rel(out_u, out_r)
     assert ef < max(2e-2, 1.5 * eu), (ef, eu)
     assert set(g_f) == set(g_u) == set(g_r)
+    _assert_as_accurate(g_f, g_u, g_r)
+
+
+def _assert_as_accurate(g_f, g_u, g_r):
+    """Per parameter, the fused gradient's relative error against fp32 autograd is within 1.3x
+    (+ 0.03) of the unfused path's, and the median error within 1.1x (+ 0.005).  (The whole-model
+    errors themselves are large -- median ~0.2 for raft_large -- because the early encoder layers'
+    weight gradients cancel through the instance norms and carry the bf16 noise of both paths;
+    measured: dev/probes/fused_rel_errors.py.  The loop alone is held to tighter absolute bounds by
+    test_fused_loop_gradient_oracle.)"""
     scale = max(v.norm().item() for v in g_r.values())
-    bad, cfs, cus = [], [], []
+    bad, efs, eus = [], [], []
     for n in g_r:
         if g_r[n].norm().item() < 1e-4 * scale:
             continue  # e.g. biases feeding an InstanceNorm: exactly-zero true gradient, rounding noise
-        cf, cu = _cos(g_f[n], g_r[n]), _cos(g_u[n], g_r[n])
-        cfs.append(cf)
-        cus.append(cu)
-        r = g_f[n].norm().item() / g_r[n].norm().item()
-        # per parameter within bf16 noise of the unfused path (raft_small's 8-channel
-        # bottleneck convs sit at cos ~0.9 for both paths), and no worse on the median
-        if cf < cu - 0.03 or not (0.85 < r < 1.15):
-            bad.append((n, round(cf, 4), round(cu, 4), round(r, 4)))
+        ef, eu = _rel(g_f[n], g_r[n]), _rel(g_u[n], g_r[n])
+        efs.append(ef)
+        eus.append(eu)
+        if ef > 1.3 * eu + 0.03:
+            bad.append((n, round(ef, 4), round(eu, 4)))
     assert not bad, bad
-    assert torch.tensor(cfs).median() >= torch.tensor(cus).median() - 0.005
+    assert sorted(efs)[len(efs) // 2] <= 1.1 * sorted(eus)[len(eus) // 2] + 0.005, (efs, eus)
 
 
 @pytest.mark.parametrize("factory", [raft_large, raft_small])
@@ -140,12 +147,12 @@ def test_fused_matches_cpu_fp32(factory):
     w = torch.tensor([0.8, 1.0]).view(-1, 1, 1, 1, 1)
     (w * (out - target).abs()).mean().backward()
     ref = {n: p.grad for n, p in mc.named_parameters() if p.grad is not None}
+    state = {k: v.clone() for k, v in model.state_dict().items()}
     outg, gg = _run(model, i1, i2, target, 2, fused=True)
     assert _rel(outg, out) < 5e-2  # bf16 convs vs the fp32 golden model (random-init raft_small: ~3 %)
-    scale = max(v.norm().item() for v in ref.values())
-    cos = torch.tensor([_cos(gg[n], ref[n]) for n in ref if ref[n].norm().item() > 1e-4 * scale])
-    assert cos.median() > 0.97, cos
-    assert cos.min() > 0.7, cos
+    model.load_state_dict(state)
+    _, gu = _run(model, i1, i2, target, 2, fused=False)
+    _assert_as_accurate(gg, gu, ref)
 
 
 def test_fused_graph_equals_eager(monkeypatch):
