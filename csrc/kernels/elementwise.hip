@@ -144,39 +144,36 @@ __global__ __launch_bounds__(256) void channel_stats_final_kernel(const float* _
 }
 
 // y = act(xn + rn).  Block = (row chunk, image n); thread = (8-channel group g,
-// row lane): the per-channel scale/shift of x (and of the residual) are derived
-// from the statistics once per thread and reused for every row it visits, and
-// all indexing is 32-bit within one image (no 64-bit divisions per element).
-struct NormSide {
-  float a[8], b[8];
-};
+// row lane).  The per-channel scale/shift of x (and of the residual) are derived
+// from the statistics ONCE per block, one channel per thread, into LDS: each row
+// lane deriving them itself was 8 x (2 .. 2N + 2) scalar loads per thread, and
+// over ~2000 blocks that load stream (not the bytes) bounded the small maps and
+// the BatchNorm (mode 2) form.  Rows are then visited NORM_ACT_U at a time with
+// all their loads issued first; all indexing is 32-bit within one image.
+constexpr int NORM_ACT_U = 4;
 
-JR_DEVICE void norm_coeffs(NormSide& o, const float* st, int mode, const float* gam, const float* bet, int n, int N,
-                           int HW, int C, int c0, float eps) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c = c0 + j;
-    float a = 1.f, b = 0.f;
-    if (mode == 1) {
-      const float inv = 1.0f / (float)HW;
-      const float m = st[((long)n * C + c) * 2] * inv;
-      const float var = fmaxf(st[((long)n * C + c) * 2 + 1] * inv - m * m, 0.f);
-      a = rsqrtf(var + eps);
-      b = -m * a;
-    } else if (mode == 2) {
-      float s0 = 0.f, s1 = 0.f;
-      for (int k = 0; k < N; ++k) { s0 += st[((long)k * C + c) * 2]; s1 += st[((long)k * C + c) * 2 + 1]; }
-      const float inv = 1.0f / ((float)HW * (float)N);
-      const float m = s0 * inv;
-      const float var = fmaxf(s1 * inv - m * m, 0.f);
-      a = rsqrtf(var + eps);
-      b = -m * a;
-    }
-    if (gam) { a *= gam[c]; b *= gam[c]; }
-    if (bet) b += bet[c];
-    o.a[j] = a;
-    o.b[j] = b;
+JR_DEVICE void norm_coeff(float& ao, float& bo, const float* st, int mode, const float* gam, const float* bet, int n,
+                          int N, int HW, int C, int c, float eps) {
+  float a = 1.f, b = 0.f;
+  if (mode == 1) {
+    const float inv = 1.0f / (float)HW;
+    const float m = st[((long)n * C + c) * 2] * inv;
+    const float var = fmaxf(st[((long)n * C + c) * 2 + 1] * inv - m * m, 0.f);
+    a = rsqrtf(var + eps);
+    b = -m * a;
+  } else if (mode == 2) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int k = 0; k < N; ++k) { s0 += st[((long)k * C + c) * 2]; s1 += st[((long)k * C + c) * 2 + 1]; }
+    const float inv = 1.0f / ((float)HW * (float)N);
+    const float m = s0 * inv;
+    const float var = fmaxf(s1 * inv - m * m, 0.f);
+    a = rsqrtf(var + eps);
+    b = -m * a;
   }
+  if (gam) { a *= gam[c]; b *= gam[c]; }
+  if (bet) b += bet[c];
+  ao = a;
+  bo = b;
 }
 
 __global__ __launch_bounds__(256) void norm_act_kernel(const bf16* __restrict__ x, const float* __restrict__ sx,
@@ -186,39 +183,57 @@ __global__ __launch_bounds__(256) void norm_act_kernel(const bf16* __restrict__ 
                                                        const float* __restrict__ gr, const float* __restrict__ br,
                                                        bf16* __restrict__ y, int N, int HW, int C, float eps, int relu,
                                                        int rows) {
+  extern __shared__ float cof[];   // [4][C]: x scale, x shift, residual scale, residual shift
   const int n = blockIdx.y;
   const int cg = C >> 3;
   const int tid = threadIdx.x;
   const int g = tid % cg, rg = tid / cg, nrg = 256 / cg;
+  for (int c = tid; c < C; c += blockDim.x) {
+    norm_coeff(cof[c], cof[C + c], sx, mode_x, gx, bx, n, N, HW, C, c, eps);
+    if (r) norm_coeff(cof[2 * C + c], cof[3 * C + c], sr, mode_r, gr, br, n, N, HW, C, c, eps);
+  }
+  __syncthreads();
   if (rg >= nrg) return;
   const int c0 = g * 8;
-  NormSide nx, nr;
-  norm_coeffs(nx, sx, mode_x, gx, bx, n, N, HW, C, c0, eps);
-  if (r) norm_coeffs(nr, sr, mode_r, gr, br, n, N, HW, C, c0, eps);
+  float xa[8], xb_[8], ra[8], rb_[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    xa[j] = cof[c0 + j];
+    xb_[j] = cof[C + c0 + j];
+    ra[j] = r ? cof[2 * C + c0 + j] : 0.f;
+    rb_[j] = r ? cof[3 * C + c0 + j] : 0.f;
+  }
   const long base = (long)n * HW * C + c0;
   const bf16* xb = x + base;
   const bf16* rb = r ? r + base : nullptr;
   bf16* yb = y + base;
   const int r0 = blockIdx.x * rows;
   const int r1 = min(r0 + rows, HW);
-#pragma unroll 2
-  for (int row = r0 + rg; row < r1; row += nrg) {
-    const int off = row * C;
-    const bf16x8 v = *(const bf16x8*)(xb + off);
-    bf16x8 w;
-    if (rb) w = *(const bf16x8*)(rb + off);
-    float a[8];
+  for (int row0 = r0 + rg; row0 < r1; row0 += NORM_ACT_U * nrg) {
+    bf16x8 v[NORM_ACT_U], w[NORM_ACT_U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      a[j] = fmaf(bf2f(v[j]), nx.a[j], nx.b[j]);
-      if (relu & 1) a[j] = fmaxf(a[j], 0.f);
-      if (rb) a[j] += fmaf(bf2f(w[j]), nr.a[j], nr.b[j]);
-      if (relu & 2) a[j] = fmaxf(a[j], 0.f);
+    for (int u = 0; u < NORM_ACT_U; ++u) {   // all loads first (clamped rows; only valid ones are stored)
+      const int off = min(row0 + u * nrg, r1 - 1) * C;
+      v[u] = *(const bf16x8*)(xb + off);
+      if (rb) w[u] = *(const bf16x8*)(rb + off);
     }
-    bf16x8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(a[j]);
-    *(bf16x8*)(yb + off) = o;
+    for (int u = 0; u < NORM_ACT_U; ++u) {
+      const int row = row0 + u * nrg;
+      if (row >= r1) break;
+      float a[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        a[j] = fmaf(bf2f(v[u][j]), xa[j], xb_[j]);
+        if (relu & 1) a[j] = fmaxf(a[j], 0.f);
+        if (rb) a[j] += fmaf(bf2f(w[u][j]), ra[j], rb_[j]);
+        if (relu & 2) a[j] = fmaxf(a[j], 0.f);
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(a[j]);
+      *(bf16x8*)(yb + row * C) = o;
+    }
   }
 }
 
@@ -425,7 +440,7 @@ extern "C" int jr_norm_act(const void* x, const float* sx, int mode_x, const flo
   const long want = ((long)N * HW + 2047) / 2048;
   const int rows = (int)std::max<long>(nrg, (want + nrg - 1) / nrg * nrg);
   const unsigned nb = (unsigned)((HW + rows - 1) / rows);
-  hipLaunchKernelGGL(norm_act_kernel, dim3(nb, N), dim3(256), 0, stream, (const bf16*)x, sx, mode_x, gamma, beta,
+  hipLaunchKernelGGL(norm_act_kernel, dim3(nb, N), dim3(256), 4 * C * sizeof(float), stream, (const bf16*)x, sx, mode_x, gamma, beta,
                      (const bf16*)res, sr, mode_r, gamma_r, beta_r, (bf16*)y, N, HW, C, eps, relu, rows);
   return (int)hipGetLastError();
 }

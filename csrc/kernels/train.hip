@@ -259,27 +259,50 @@ struct NormCo {
   float mean[8], rstd[8], gam[8], bet[8];
 };
 
-JR_DEVICE void norm_co(NormCo& o, const float* st, int mode, const float* gam, const float* bet, int n, int N, int HW,
-                       int C, int c0, float eps) {
+// (mean, rstd) of channel c of sample n: mode 1 over the map, mode 2 over the batch and map,
+// mode 0 (no norm) identity
+JR_DEVICE void norm_stat(const float* st, int mode, int n, int N, int HW, int C, int c, float eps, float& m,
+                         float& r) {
+  m = 0.f;
+  r = 1.f;
+  if (mode == 1) {
+    const float inv = 1.0f / (float)HW;
+    m = st[((long)n * C + c) * 2] * inv;
+    r = rsqrtf(fmaxf(st[((long)n * C + c) * 2 + 1] * inv - m * m, 0.f) + eps);
+  } else if (mode == 2) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int k = 0; k < N; ++k) { s0 += st[((long)k * C + c) * 2]; s1 += st[((long)k * C + c) * 2 + 1]; }
+    const float inv = 1.0f / ((float)HW * (float)N);
+    m = s0 * inv;
+    r = rsqrtf(fmaxf(s1 * inv - m * m, 0.f) + eps);
+  }
+}
+
+// Per-channel coefficients are computed ONCE per block, one channel per thread, into LDS
+// (cof[k * C + c], k = mean, rstd, gamma, beta[, a, m1, m2]) and read back 8 channels at a time:
+// each of the block's 256 / (C / 8) row groups evaluating them itself cost 48 scalar loads per
+// thread (2 N + ... for BatchNorm, whose statistics sum over the batch), and at ~2000 blocks
+// that load-instruction stream, not the bytes, bounded the small maps and the BatchNorm
+// backward (dev/probes/norm_bwd_bench.py: 2.1-2.6 TB/s vs 4.5-5.2 on the large IN maps).
+JR_DEVICE void norm_co_lds(float* cof, const float* st, int mode, const float* gam, const float* bet, int n, int N,
+                           int HW, int C, float eps) {
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float m, r;
+    norm_stat(st, mode, n, N, HW, C, c, eps, m, r);
+    cof[c] = m;
+    cof[C + c] = r;
+    cof[2 * C + c] = gam ? gam[c] : 1.f;
+    cof[3 * C + c] = bet ? bet[c] : 0.f;
+  }
+}
+
+JR_DEVICE void norm_co(NormCo& o, const float* cof, int C, int c0) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int c = c0 + j;
-    float m = 0.f, r = 1.f;
-    if (mode == 1) {
-      const float inv = 1.0f / (float)HW;
-      m = st[((long)n * C + c) * 2] * inv;
-      r = rsqrtf(fmaxf(st[((long)n * C + c) * 2 + 1] * inv - m * m, 0.f) + eps);
-    } else if (mode == 2) {
-      float s0 = 0.f, s1 = 0.f;
-      for (int k = 0; k < N; ++k) { s0 += st[((long)k * C + c) * 2]; s1 += st[((long)k * C + c) * 2 + 1]; }
-      const float inv = 1.0f / ((float)HW * (float)N);
-      m = s0 * inv;
-      r = rsqrtf(fmaxf(s1 * inv - m * m, 0.f) + eps);
-    }
-    o.mean[j] = m;
-    o.rstd[j] = r;
-    o.gam[j] = gam ? gam[c] : 1.f;
-    o.bet[j] = bet ? bet[c] : 0.f;
+    o.mean[j] = cof[c0 + j];
+    o.rstd[j] = cof[C + c0 + j];
+    o.gam[j] = cof[2 * C + c0 + j];
+    o.bet[j] = cof[3 * C + c0 + j];
   }
 }
 
@@ -316,18 +339,21 @@ __global__ __launch_bounds__(256) void norm_bwd_partial_kernel(const bf16* __res
                                                                const float* __restrict__ bet, int relu, int N, int HW,
                                                                int C, float eps, float* __restrict__ part, int rows) {
   __shared__ float red[256][17];
+  extern __shared__ float cof[];   // [4][C]
   const int n = blockIdx.y;
   const int cg = C >> 3;
   const int tid = threadIdx.x;
   const int g8 = tid % cg, rg = tid / cg, nrg = 256 / cg;
   const int r0 = blockIdx.x * rows;
   const int r1 = min(r0 + rows, HW);
+  norm_co_lds(cof, st, mode, gam, bet, n, N, HW, C, eps);
+  __syncthreads();
   float s[8], q[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
   if (rg < nrg) {
     NormCo co;
-    norm_co(co, st, mode, gam, bet, n, N, HW, C, g8 * 8, eps);
+    norm_co(co, cof, C, g8 * 8);
     const long base = (long)n * HW * C + g8 * 8;
     for (int r = r0 + rg; r < r1; r += NORM_U * nrg) {
       NormRow v[NORM_U];
@@ -401,18 +427,13 @@ __global__ __launch_bounds__(256) void norm_bwd_apply_kernel(const bf16* __restr
                                                              float eps, bf16* __restrict__ dy, void* __restrict__ gres,
                                                              int gres_bf16,
                                                              int rows) {
+  extern __shared__ float cof[];   // [7][C]: mean, rstd, gamma, beta, a, m1, m2
   const int n = blockIdx.y;
   const int cg = C >> 3;
   const int tid = threadIdx.x;
   const int g8 = tid % cg, rg = tid / cg, nrg = 256 / cg;
-  if (rg >= nrg) return;
-  const int c0 = g8 * 8;
-  NormCo co;
-  norm_co(co, st, mode, gam, bet, n, N, HW, C, c0, eps);
-  float a[8], m1[8], m2[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c = c0 + j;
+  norm_co_lds(cof, st, mode, gam, bet, n, N, HW, C, eps);
+  for (int c = tid; c < C; c += blockDim.x) {
     float S1 = 0.f, S2 = 0.f, cnt = (float)HW;
     if (mode == 1) {
       S1 = red[((long)n * C + c) * 2];
@@ -421,9 +442,21 @@ __global__ __launch_bounds__(256) void norm_bwd_apply_kernel(const bf16* __restr
       for (int k = 0; k < N; ++k) { S1 += red[((long)k * C + c) * 2]; S2 += red[((long)k * C + c) * 2 + 1]; }
       cnt *= (float)N;
     }
-    a[j] = co.rstd[j] * co.gam[j];
-    m1[j] = S1 / cnt;
-    m2[j] = S2 / cnt;
+    cof[4 * C + c] = cof[C + c] * cof[2 * C + c];
+    cof[5 * C + c] = S1 / cnt;
+    cof[6 * C + c] = S2 / cnt;
+  }
+  __syncthreads();
+  if (rg >= nrg) return;
+  const int c0 = g8 * 8;
+  NormCo co;
+  norm_co(co, cof, C, c0);
+  float a[8], m1[8], m2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = cof[4 * C + c0 + j];
+    m1[j] = cof[5 * C + c0 + j];
+    m2[j] = cof[6 * C + c0 + j];
   }
   const long base = (long)n * HW * C + c0;
   const int r0 = blockIdx.x * rows;
@@ -707,7 +740,7 @@ extern "C" int jr_norm_bwd(const void* gout, const void* om, const void* y, cons
   if (mode != 0) {
     const int prow = norm_bwd_rows(N, HW, C);
     const int nb = (HW + prow - 1) / prow;
-    hipLaunchKernelGGL(norm_bwd_partial_kernel, dim3(nb, N), dim3(256), 0, stream, (const bf16*)gout,
+    hipLaunchKernelGGL(norm_bwd_partial_kernel, dim3(nb, N), dim3(256), 4 * C * sizeof(float), stream, (const bf16*)gout,
                        (const bf16*)om, (const bf16*)y, stats, mode, gamma, beta, relu, N, HW, C, eps, partial, prow);
     hipLaunchKernelGGL(norm_bwd_final_kernel, dim3((2 * C + 7) / 8, N), dim3(256), 0, stream, partial, nb, C, red);
   }
@@ -715,7 +748,7 @@ extern "C" int jr_norm_bwd(const void* gout, const void* om, const void* y, cons
   const long want = ((long)N * HW + 2047) / 2048;
   const int rows = (int)std::max<long>(nrg, (want + nrg - 1) / nrg * nrg);
   const unsigned nbk = (unsigned)((HW + rows - 1) / rows);
-  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(nbk, N), dim3(256), 0, stream, (const bf16*)gout, (const bf16*)om,
+  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(nbk, N), dim3(256), 7 * C * sizeof(float), stream, (const bf16*)gout, (const bf16*)om,
                      (const bf16*)y, stats, mode, gamma, beta, relu, red, N, HW, C, eps, (bf16*)dy, gres, gres_bf16, rows);
   return (int)hipGetLastError();
 }

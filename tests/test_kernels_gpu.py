@@ -330,6 +330,16 @@ def test_instance_norm_stats_apply(C):
     torch.cuda.synchronize()
     ref2 = torch.relu(R.instance_norm_nhwc(x) + r)
     assert (y2.float().cpu() - ref2).abs().max().item() < 3e-2
+    # BatchNorm statistics (mode 2: over batch and map) with an affine, relu only
+    gam = torch.rand(C) + 0.5
+    bet = torch.randn(C) * 0.1
+    y3 = torch.empty_like(xg)
+    nat.ops().norm_act([xg, st, gam.to(DEV), bet.to(DEV), None, None, None, None, y3], [2, 0, N, H * W, C, 1], 1e-5)
+    torch.cuda.synchronize()
+    xb = x.to(torch.bfloat16).float()
+    m, v = xb.mean((0, 1, 2)), xb.var((0, 1, 2), unbiased=False)
+    ref3 = torch.relu((xb - m) * torch.rsqrt(v + 1e-5) * gam + bet)
+    assert (y3.float().cpu() - ref3).abs().max().item() < 3e-2
 
 
 @pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 33, 34,

@@ -27,11 +27,18 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--marker", default="prep_images", help="kernel that starts a step ('' = whole trace / steps)")
+    ap.add_argument("--between", action="store_true",
+                    help="count the --steps whole cycles between the last --steps + 1 markers (a marker "
+                         "in the middle of a step, e.g. the training loss kernel)")
     a = ap.parse_args()
     rows = sorted(_load(a.trace), key=lambda r: int(r["Start_Timestamp"]))
     starts = [i for i, r in enumerate(rows) if a.marker and a.marker in r["Kernel_Name"]]
-    first = starts[-a.steps] if len(starts) >= a.steps else 0
-    rows = rows[first:]
+    if a.between:
+        assert len(starts) > a.steps, f"{len(starts)} markers for {a.steps} cycles"
+        rows = rows[starts[-a.steps - 1]:starts[-1]]
+    else:
+        first = starts[-a.steps] if len(starts) >= a.steps else 0
+        rows = rows[first:]
     agg = collections.defaultdict(lambda: [0, 0.0])
     for r in rows:
         n = re.sub(r"\(anonymous namespace\)::", "", r["Kernel_Name"])

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--graph-step", action="store_true", help="replay the whole step as one captured graph")
+    ap.add_argument("--cprofile", default="", help="write the host-side cProfile of the timed steps (top 40) here")
     a = ap.parse_args()
     cfg = TrainConfig(arch=a.arch, steps=a.steps + a.warmup, batch=a.batch, iters=a.iters, size=tuple(a.size),
                       log_every=10 ** 9, graph_step=a.graph_step)
@@ -36,10 +37,26 @@ def main():
     torch.cuda.synchronize()
     if dp.is_dist():
         torch.distributed.barrier()
+    prof = None
+    if a.cprofile:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
+    host = 0.0
     t0 = time.perf_counter()
     for i in range(a.steps):
+        h0 = time.perf_counter()
         m = tr.train_step(batches[i % 2])
+        host += time.perf_counter() - h0
     torch.cuda.synchronize()
+    if prof is not None:
+        import io
+        import pstats
+        prof.disable()
+        buf = io.StringIO()
+        pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(40)
+        with open(a.cprofile, "w") as f:
+            f.write(buf.getvalue())
     dt = torch.tensor([time.perf_counter() - t0], device=tr.device, dtype=torch.float64)
     if dp.is_dist():
         torch.distributed.all_reduce(dt, op=torch.distributed.ReduceOp.MAX)
@@ -47,6 +64,8 @@ def main():
     if tr.rank == 0:
         print(json.dumps({"metric": "training image-pairs/sec (config 5)", "value": round(tr.world * a.batch * a.steps / el, 3),
                           "unit": "image-pairs/s", "n_gpus": tr.world, "ms_per_step": round(1000 * el / a.steps, 2),
+                          # host time inside train_step (includes its one wait on the previous step's flag)
+                          "host_ms_per_step": round(1000 * host / a.steps, 2),
                           "loss": float(m["loss"]), "config": {"model": a.arch, "per_gpu_batch": a.batch,
                           "image_size": list(a.size), "num_flow_updates": a.iters, "parallelism": f"dp{tr.world}",
                           "dtype": "bf16 (fp32 master weights)"}}), flush=True)
