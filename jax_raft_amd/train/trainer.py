@@ -86,6 +86,10 @@ def _adamw(params, cfg: TrainConfig, device, capturable: bool = False):
 
 
 class Trainer:
+    # steps the host may run ahead of the GPU's non-finite flags (each step waits for the flag of
+    # the step SETTLE_LAG before it, so the launch queue holds about that many steps)
+    SETTLE_LAG = 1
+
     def __init__(self, cfg: TrainConfig, device: Optional[torch.device] = None):
         self.cfg = cfg
         self.rank, self.world, dev = dp.init_distributed()
@@ -231,8 +235,8 @@ class Trainer:
 
     def _settle(self, keep_last: bool = False) -> None:
         """Fold the non-finite flags of finished steps into the skip counters
-        (``keep_last``: leave the newest pending step, which may still run)."""
-        while len(self._pending) > (1 if keep_last else 0):
+        (``keep_last``: leave the newest ``SETTLE_LAG`` pending steps, which may still run)."""
+        while len(self._pending) > (self.SETTLE_LAG if keep_last else 0):
             step, flag, ev = self._pending.pop(0)
             ev.synchronize()
             self._record_skip(step, bool(flag.item()))

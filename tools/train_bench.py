@@ -26,10 +26,13 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--graph-step", action="store_true", help="replay the whole step as one captured graph")
+    ap.add_argument("--settle-lag", type=int, default=None, help="Trainer.SETTLE_LAG override (A/B)")
     ap.add_argument("--cprofile", default="", help="write the host-side cProfile of the timed steps (top 40) here")
     a = ap.parse_args()
     cfg = TrainConfig(arch=a.arch, steps=a.steps + a.warmup, batch=a.batch, iters=a.iters, size=tuple(a.size),
                       log_every=10 ** 9, graph_step=a.graph_step)
+    if a.settle_lag is not None:
+        Trainer.SETTLE_LAG = a.settle_lag
     tr = Trainer(cfg)
     batches = [tr.batch_for(i) for i in range(2)]
     for i in range(a.warmup):
