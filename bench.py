@@ -337,6 +337,28 @@ def _gather_ms(ctx: Ctx, gat: FlowGather, flows, shape) -> float:
     return 1000.0 * ctx.max_all(sum(ts) / len(ts))
 
 
+def run_training_child(*, arch: str, B: int, size, iters: int, steps: int, warmup: int) -> dict:
+    """Single GPU: the training extra in a fresh child process (tools/train_bench.py; the parent
+    has finished its GPU work and waits).  In-process, after the inference extras, the step's
+    side streams share hardware queues with whatever streams the process created before
+    (GPU_MAX_HW_QUEUES = 4), and the same step measured 174-376 pairs/s depending on which
+    extras ran first (profiles/r6_hwq_ab.txt); a training job starts in a fresh process."""
+    import subprocess
+
+    cmd = [sys.executable, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "train_bench.py"),
+           "--arch", arch, "--batch", str(B), "--iters", str(iters), "--size", str(size[0]), str(size[1]),
+           "--steps", str(steps), "--warmup", str(warmup), "--fresh-batches"]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError(f"train_bench.py exited {r.returncode}: {r.stderr[-2000:]}")
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    return dict(value=d["value"], ms_per_step=d["ms_per_step"], steps=steps, warmup=warmup, loss=round(d["loss"], 4),
+                per_rank_ms_per_step=[d["ms_per_step"]], process="fresh child (tools/train_bench.py)",
+                config=dict(model=arch, per_gpu_batch=B, global_batch=B, image_size=list(size), num_flow_updates=iters,
+                            optimizer="AdamW + one-cycle, clip 1.0", loss="sequence loss gamma 0.8",
+                            grad_allreduce=None, data="synthetic, generated on the GPU inside each timed step"))
+
+
 def run_training(ctx: Ctx, *, arch: str, B: int, size, iters: int, steps: int, warmup: int) -> dict:
     """BASELINE config 5 through the Trainer (fused native step, AdamW, RCCL
     gradient all-reduce for N>1); each step synthesises its batch on the GPU."""
@@ -497,9 +519,14 @@ def main():
                 print(f"bench.py: extra {key} failed: {type(e).__name__}: {e}", file=sys.stderr)
             torch.cuda.empty_cache()
         try:
-            extras["train_pairs_per_s"] = run_training(ctx, arch="raft_large", B=args.train_batch,
-                                                       size=tuple(args.train_size), iters=12,
-                                                       steps=max(2, ks // 2), warmup=3)
+            if ctx.world == 1:
+                extras["train_pairs_per_s"] = run_training_child(arch="raft_large", B=args.train_batch,
+                                                                 size=tuple(args.train_size), iters=12,
+                                                                 steps=max(10, ks), warmup=3)
+            else:
+                extras["train_pairs_per_s"] = run_training(ctx, arch="raft_large", B=args.train_batch,
+                                                           size=tuple(args.train_size), iters=12,
+                                                           steps=max(2, ks // 2), warmup=3)
         except Exception as e:  # noqa: BLE001
             if ctx.world > 1:
                 raise   # the DP step's gradient all-reduce cannot be left mid-way on one rank

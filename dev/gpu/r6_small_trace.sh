@@ -11,5 +11,6 @@ f=$(find $o/t -name '*kernel_trace.csv' | head -1)
 python3 tools/kernel_breakdown.py $f --steps 5 --top 40 > $o/breakdown.txt 2>&1
 python3 tools/timeline.py $f --iter 10 > $o/timeline.txt 2>&1 || true
 python3 tools/timeline.py $f --prologue > $o/prologue.txt 2>&1 || true
+python3 tools/prologue_timeline.py $f > $o/prologue_q.txt 2>&1 || true
 rm -f $f
 head -3 $o/timeline.txt; wc -l $o/prologue.txt

@@ -1164,16 +1164,23 @@ class RaftEngine:
         main, side, side2 = lanes
         lanes_on = main != side
         # the prologue's branches (context encoder, feature encoder of each image) run on
-        # their own lanes even when the loop runs on one, up to Sintel-size batch 4 worth of
-        # pixels: there its ~100 kernels are small and latency-bound.  Measured at batch 1
-        # (profiles/r4_prologue_lanes_ab.txt): raft_small 12 iterations 667 -> 861 pairs/s,
-        # per-pair sync latency -1..-2 %; 1088x1920 frames 67.6 -> 63.7 (so: off there).
+        # their own lanes even when the loop runs on one, for batch 2 .. Sintel-size batch 4
+        # worth of pixels.  At batch 1 (round 6, profiles/r6_prolanes_ab.txt) the replayed
+        # branches ran one after another (rocprofv3: context encoder, then image 1's feature
+        # encoder, then image 2's, on three hardware queues), so the lanes only doubled the
+        # feature encoder's ~70 latency-bound launches; one batch-2 feature-encoder chain
+        # measured raft_small sync 297 -> 330 pairs/s, its 32-iteration stream 439 -> 462,
+        # raft_large sync 216 -> 224 (1088x1920 frames: 67.6 -> 63.7 with lanes, round 4).
         # PRO_LANES = "off": never, "on": always.
         pl = self.PRO_LANES
         assert pl in ("auto", "on", "off"), pl
-        pro_on = pl == "on" or (pl == "auto" and B * h * w <= 4 * 55 * 128)
+        pro_on = pl == "on" or (pl == "auto" and 2 <= B and B * h * w <= 4 * 55 * 128)
         p_main, p_side, p_side2 = lanes if lanes_on or self.cp or not pro_on else (main, 1, 2)
         p_on = p_main != p_side
+        # the per-image feature-encoder split (lane 2) -- never at batch 1 under "auto", also not in
+        # a pipelined slot's multi-lane plan, so that its kernels (tile configs of the batch-2
+        # chain) and results equal the synchronous forward's bit for bit
+        fe_split = p_on and not (pl == "auto" and B == 1)
 
         def lane(l):
             plan.set_lane(l)
@@ -1223,7 +1230,7 @@ class RaftEngine:
         fmap = alloc("fmap", (2 * B, h, w, self.fmap_ch))
         if self.fe_external:
             lane(p_main)   # fmap is written before each replay (RaftEngineMixed._pre_launch)
-        elif p_on:
+        elif fe_split:
             # the feature encoder of image2 on a third lane, concurrent with image1's
             # (and the context encoder): per-image instance norms, so the halves are
             # exact, and the sequential encoder chain that gates the correlation

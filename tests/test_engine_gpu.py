@@ -175,11 +175,16 @@ def test_final_only_mode_equals_last_iteration(factory, use_graph):
 
 @pytest.mark.parametrize("factory,B", [(raft_large, 4), (raft_large, 1), (raft_small, 2)])
 @pytest.mark.parametrize("final_only", [False, True])
-def test_graph_pipelined_matches_forward(factory, B, final_only):
+def test_graph_pipelined_matches_forward(factory, B, final_only, monkeypatch):
     """Graph-pipelined steps (one hipGraph = batch i's loop || batch i+1's
     prologue, two plan slots): call k returns batch k-1's flows, flush() the
     last; each equals the synchronous forward of the same batch, bitwise.  A
-    shape change without flush() raises."""
+    shape change without flush() raises.  (At batch 1 the synchronous forward's
+    pyramid is the persistent kernel, RaftEngine.CORR_PERSIST_B1, the slots' the
+    tile kernel -- equal within bf16 rounding, test_pipelined_b1_persistent_pyramid;
+    the bitwise check runs both on the tile kernel.)"""
+    if B == 1:
+        monkeypatch.setattr(RaftEngine, "CORR_PERSIST_B1", False)
     model, _ = factory()
     model = model.cuda()
     eng = model.engine(torch.device("cuda", 0))
@@ -202,6 +207,21 @@ def test_graph_pipelined_matches_forward(factory, B, final_only):
     with pytest.raises(RuntimeError):
         eng.pipelined(a, b, 5, return_all_iters=not final_only)
     eng.flush()
+
+
+def test_pipelined_b1_persistent_pyramid():
+    """Default batch-1 engine: the synchronous forward (persistent pyramid kernel) and the
+    pipelined slots (tile kernel) give the same flows within bf16 rounding."""
+    model, _ = raft_large()
+    model = model.cuda()
+    eng = model.engine(torch.device("cuda", 0))
+    batches = [tuple(t.cuda() for t in _inputs(1, 128, 256, seed=60 + k)) for k in range(3)]
+    refs = [eng.forward(a, b, 4) for a, b in batches]
+    outs = [eng.pipelined(a, b, 4) for a, b in batches][1:] + [eng.flush()]
+    torch.cuda.synchronize()
+    for r, o in zip(refs, outs):
+        mag = r[-1].norm(dim=-1).mean().item()
+        assert _epe(o[-1], r[-1]) < 0.1 * REL_EPE["raft_large"] * mag
 
 
 def test_split_mask_head_matches_fused():
@@ -321,9 +341,9 @@ def test_streams_auto_matches_lanes_and_single_lane(factory):
             assert _epe(a, b if B >= 4 else c) < 1e-4 and _epe(b, c) < 0.5 * REL_EPE["raft_large"] * mag
         eng = model.engine(torch.device("cuda", 0), streams="auto")
         st = eng._states[(B, 128, 128, 3, True)]
-        # loop lanes (the prologue's branches run on lanes at every batch, RaftEngine.PRO_LANES)
+        # loop lanes (the prologue's branches run on lanes from batch 2, RaftEngine.PRO_LANES)
         assert eng.uses_lanes(B) == (B >= eng.AUTO_STREAMS_MIN_BATCH and eng.has_mask)
-        assert st.plan.num_lanes() > 1
+        assert (st.plan.num_lanes() > 1) == (B >= 2)
         # final-only (serving) mode: "auto" keeps one lane at every batch
         d = model(i1, i2, num_flow_updates=3, streams="auto", return_all_iters=False)
         torch.cuda.synchronize()

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--graph-step", action="store_true", help="replay the whole step as one captured graph")
+    ap.add_argument("--fresh-batches", action="store_true",
+                    help="synthesise every step's batch inside the timed loop (bench.py's train extra)")
     ap.add_argument("--settle-lag", type=int, default=None, help="Trainer.SETTLE_LAG override (A/B)")
     ap.add_argument("--cprofile", default="", help="write the host-side cProfile of the timed steps (top 40) here")
     a = ap.parse_args()
@@ -49,7 +51,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.steps):
         h0 = time.perf_counter()
-        m = tr.train_step(batches[i % 2])
+        m = tr.train_step(tr.batch_for(a.warmup + i) if a.fresh_batches else batches[i % 2])
         host += time.perf_counter() - h0
     torch.cuda.synchronize()
     if prof is not None:
