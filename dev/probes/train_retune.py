@@ -14,8 +14,17 @@ sys.path.insert(0, os.path.join(root, "tools"))
 src = os.path.join(root, "jax_raft_amd", "tuned", "gfx950.json")
 d = json.load(open(src))
 drop = [k for k in d["entries"] if k.startswith('["train"') and tuple(json.loads(k)[6:8]) in ((1, 5), (5, 1))]
+setcfg = None
+if "--set" in sys.argv:   # --set C: pin the 256-output-channel data-gradient keys to config C instead
+    i = sys.argv.index("--set")
+    setcfg = int(sys.argv[i + 1])
+    del sys.argv[i:i + 2]
+    drop = [k for k in drop if json.loads(k)[13] == 256]
 for k in drop:
-    del d["entries"][k]
+    if setcfg is None:
+        del d["entries"][k]
+    else:
+        d["entries"][k] = setcfg
 tmp = os.path.join(tempfile.mkdtemp(), "db.json")
 json.dump(d, open(tmp, "w"))
 os.environ["JR_TUNE_DB"] = tmp
