@@ -651,6 +651,54 @@ __global__ __launch_bounds__(256) void bn_table_kernel(const BnRow* __restrict__
   }
 }
 
+// Same, 32-bit indexing and vector level reads (w % 8 == 0, M * h * w / 8 < 2^31): the 8 outputs
+// of a thread read 4 / 2 / 1 consecutive cells of levels 1 / 2 / 3 (one 16-B, 8-B, 4-B load each)
+// instead of 24 scalar gathers, and no 64-bit divisions (config 5: 356 us at 1.2 TB/s before).
+__global__ __launch_bounds__(256) void pyr_bwd_dc8v_kernel(const float* __restrict__ g0, const float* __restrict__ g1,
+                                                           const float* __restrict__ g2, const float* __restrict__ g3,
+                                                           int L, unsigned n8, unsigned hw8, int h, int w, float scale,
+                                                           bf16* __restrict__ dc) {
+  const unsigned e8 = blockIdx.x * 256u + threadIdx.x;
+  if (e8 >= n8) return;
+  const unsigned q = e8 / hw8;
+  const unsigned r8 = e8 - q * hw8;
+  const unsigned w8 = (unsigned)w >> 3;
+  const int y = (int)(r8 / w8);
+  const int x0 = (int)(r8 - (unsigned)y * w8) * 8;
+  const long e = (long)e8 * 8;
+  const f32x4 a = *(const f32x4*)(g0 + e);
+  const f32x4 b = *(const f32x4*)(g0 + e + 4);
+  float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  if (L > 1) {
+    const int hl = h >> 1, wl = w >> 1, yy = y >> 1;
+    if (yy < hl) {
+      const f32x4 t = *(const f32x4*)(g1 + ((long)q * hl + yy) * wl + (x0 >> 1));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += t[j >> 1] * 0.25f;
+    }
+  }
+  if (L > 2) {
+    const int hl = h >> 2, wl = w >> 2, yy = y >> 2;
+    if (yy < hl) {
+      const float2 t = *(const float2*)(g2 + ((long)q * hl + yy) * wl + (x0 >> 2));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += (j < 4 ? t.x : t.y) * 0.0625f;
+    }
+  }
+  if (L > 3) {
+    const int hl = h >> 3, wl = w >> 3, yy = y >> 3;
+    if (yy < hl) {
+      const float t = g3[((long)q * hl + yy) * wl + (x0 >> 3)];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += t * 0.015625f;
+    }
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j] * scale);
+  *(bf16x8*)(dc + e) = o;
+}
+
 inline unsigned nblk(long total, int bs) { return (unsigned)((total + bs - 1) / bs); }
 
 }  // namespace
@@ -665,6 +713,12 @@ extern "C" int jr_bn_table(const void* rows, int n, int max_c, hipStream_t strea
 extern "C" int jr_pyr_bwd_dc(const float* g0, const float* g1, const float* g2, const float* g3, int L, long M, int h,
                              int w, float scale, void* dc, hipStream_t stream) {
   if (L < 1 || L > 4) return (int)hipErrorInvalidValue;
+  if (w % 8 == 0 && M * h * w / 8 < (1L << 31)) {
+    const long n8 = M * h * w / 8;
+    hipLaunchKernelGGL(pyr_bwd_dc8v_kernel, dim3(nblk(n8, 256)), dim3(256), 0, stream, g0, g1, g2, g3, L,
+                       (unsigned)n8, (unsigned)((long)h * w / 8), h, w, scale, (bf16*)dc);
+    return (int)hipGetLastError();
+  }
   if (w % 8 == 0) {
     hipLaunchKernelGGL(pyr_bwd_dc8_kernel, dim3(nblk(M * h * w / 8, 256)), dim3(256), 0, stream, g0, g1, g2, g3, L, M,
                        h, w, scale, (bf16*)dc);

@@ -681,9 +681,9 @@ def test_s2d_stem_matches_7x7_stride2(B, H, W):
     assert _rel(y.cpu(), ref) < 3e-3
 
 
-@pytest.mark.parametrize("B,h,w,L", [(2, 12, 16, 4), (1, 9, 12, 3), (2, 16, 24, 4)])
+@pytest.mark.parametrize("B,h,w,L", [(2, 12, 16, 4), (1, 9, 12, 3), (2, 16, 24, 4), (1, 9, 16, 4), (1, 13, 40, 2)])
 def test_pyr_bwd_dc(B, h, w, L):
-    """Correlation-pyramid backward, first half (train.hip: pyr_bwd_dc / pyr_bwd_dc8 for w % 8 == 0):
+    """Correlation-pyramid backward, first half (train.hip: pyr_bwd_dc, pyr_bwd_dc8v for w % 8 == 0):
     dC = s (g0 + sum_l nearest-upsampled g_l / 4^l) over the floor-pooled region, bf16."""
     nat = _nat()
     torch.manual_seed(7)
