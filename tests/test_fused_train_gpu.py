@@ -20,11 +20,11 @@ def _cos(a, b):
     return (torch.dot(a, b) / (a.norm() * b.norm() + 1e-12)).item()
 
 
-def test_upsample_convex_bwd_kernel():
+@pytest.mark.parametrize("B,h,w", [(2, 5, 7), (1, 5, 7), (3, 6, 16)])   # odd pixel counts: a half-idle last wave
+def test_upsample_convex_bwd_kernel(B, h, w):
     from jax_raft_amd.ops import native as nat
 
     torch.manual_seed(0)
-    B, h, w = 2, 5, 7
     M = B * h * w
     mask = (torch.randn(B, h, w, 576) * 2).to(torch.bfloat16).float()
     flow = torch.randn(B, h, w, 2) * 3
