@@ -937,10 +937,13 @@ class FusedLoop:
         self.gen += 1
         return self.out.clone()
 
-    def backward(self, gout: torch.Tensor, gen: int, fe_dy=None, defer_weights: bool = False):
+    def backward(self, gout: torch.Tensor, gen: int, fe_dy=None, defer_weights: bool = False, on_dctx=None):
         """The loop's backward: (dfmap1, dfmap2, d context-encoder output, parameter
         gradients); ``defer_weights``: the parameter gradients are None here and come from
-        :meth:`finish_weights` (their kernels overlap whatever the caller enqueues meanwhile)."""
+        :meth:`finish_weights` (their kernels overlap whatever the caller enqueues meanwhile);
+        ``on_dctx(dc)``: called with the context-encoder output gradient as soon as it is
+        enqueued, before the pyramid backward (the caller's context-encoder backward can then
+        overlap it)."""
         if gen != self.gen or self.done_gen == gen:
             raise RuntimeError("fused refinement loop: this backward's saved activations were overwritten by a "
                                "later forward of the same loop (run backward before the next forward) or it "
@@ -961,7 +964,7 @@ class FusedLoop:
         with torch.cuda.stream(ws):   # the stacked weight gradients: they overlap the caller's encoder backward
             self._run(self.plan_w)
         self._w_pending = True
-        data = self._finish_data(fe_dy)
+        data = self._finish_data(fe_dy, on_dctx)
         # the gate / flow-head kernel assembly (~30 small copies) on the weight-gradient stream too,
         # after the context-share weight gradients of _finish_data: off the critical path
         with torch.cuda.stream(ws):
@@ -1047,7 +1050,7 @@ class FusedLoop:
         return g1.reshape(B, h, w, C), g2.reshape(B, h, w, C)
 
     # ---------------------------------------------------- weight gradients
-    def _finish_data(self, fe_dy=None):
+    def _finish_data(self, fe_dy=None, on_dctx=None):
         """After the backward plan: the context share of the ConvGRU gates (iteration sums,
         weight gradient kept for :meth:`finish_weights`), the pyramid and context-encoder
         input gradients."""
@@ -1069,16 +1072,20 @@ class FusedLoop:
             self._conv(None, f"gCT{g}", Sb, dctx, tx=tx, ix=ix, epi=EPI_BWD, hidden=0)
         self._ev_gc = torch.cuda.Event()   # the context-share weight gradients are done (_assemble)
         self._ev_gc.record()
-        if fe_dy is not None:   # whole-model path: straight into the feature encoder's bf16 output gradient
-            g1, g2 = self._pyramid_backward(fe_dy[: self.B], fe_dy[self.B:])
-        else:
-            g1, g2 = self._pyramid_backward()
-        # context-encoder output gradient: [tanh'(h0) dh | relu'(ctx) dctx]
+        # context-encoder output gradient: [tanh'(h0) dh | relu'(ctx) dctx] -- complete before the
+        # pyramid backward, which does not touch it
         h0 = self.hf[0, 0]
         dc = torch.empty(M, hd + C, device=self.device, dtype=F32)
         dc[:, :hd] = self.dh_next * (1 - h0 * h0)
         dc[:, hd:] = dctx[:, :C] * (self.ctx_in[:, :C] > 0)
-        return g1, g2, dc.reshape(self.B, self.h, self.w, hd + C)
+        dc = dc.reshape(self.B, self.h, self.w, hd + C)
+        if on_dctx is not None:
+            on_dctx(dc)
+        if fe_dy is not None:   # whole-model path: straight into the feature encoder's bf16 output gradient
+            g1, g2 = self._pyramid_backward(fe_dy[: self.B], fe_dy[self.B:])
+        else:
+            g1, g2 = self._pyramid_backward()
+        return g1, g2, dc
 
 
 class FusedRefine(torch.autograd.Function):
@@ -1107,6 +1114,13 @@ class FusedModel:
     write straight into the loop's feature-map / context buffers, and the
     loop's input gradients are handed back to the encoders' backward plans
     without leaving the device or the persistent buffers."""
+
+    # the context encoder's forward / backward plans on a side stream next to the feature
+    # encoder's (False: both on the caller's stream, in order -- A/B switch)
+    SIDE_ENCODER = True
+    # the context encoder's backward launched as soon as the loop has its gradient, next to the
+    # pyramid backward (False: after the whole loop backward -- A/B switch)
+    EARLY_CE = True
 
     def __init__(self, model, B: int, H: int, W: int, T: int, device, use_graph: bool = True):
         from .fused_encoder import EncoderTrain
@@ -1144,7 +1158,8 @@ class FusedModel:
         self.img1.copy_(image1)
         self.img2.copy_(image2)
         nat.ops().prep([self.img1, self.img2, self.x0], [self.B, self.H, self.W])
-        cur, side = torch.cuda.current_stream(self.loop.device), self._side()
+        cur = torch.cuda.current_stream(self.loop.device)
+        side = self._side() if self.SIDE_ENCODER else cur
         side.wait_stream(cur)
         with torch.cuda.stream(side):
             self.ce.forward(update_stats=train)
@@ -1156,12 +1171,19 @@ class FusedModel:
         comm = _ACTIVE_COMM.get(id(self.model))
         # the loop's stacked weight gradients run on their own stream, overlapping the encoders'
         # backward (bandwidth-bound norm passes next to MFMA-bound GEMMs)
-        _, _, dctx, _ = self.loop.backward(gout, gen, fe_dy=self.fe.dy_out, defer_weights=True)
-        self.ce.dy_out.copy_(dctx)
-        cur, side = torch.cuda.current_stream(self.loop.device), self._side()
-        side.wait_stream(cur)
-        with torch.cuda.stream(side):
-            self.ce.run_backward()
+        cur = torch.cuda.current_stream(self.loop.device)
+        side = self._side() if self.SIDE_ENCODER else cur
+
+        def ce_backward(dctx):   # as soon as the loop has the context gradient: next to the pyramid backward
+            self.ce.dy_out.copy_(dctx)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self.ce.run_backward()
+
+        if self.EARLY_CE:
+            self.loop.backward(gout, gen, fe_dy=self.fe.dy_out, defer_weights=True, on_dctx=ce_backward)
+        else:
+            ce_backward(self.loop.backward(gout, gen, fe_dy=self.fe.dy_out, defer_weights=True)[2])
         self.fe.run_backward()
         pgrads = self.loop.finish_weights()
         if comm is not None:   # data parallel: the loop's gradients reduce while the encoders' snapshot
