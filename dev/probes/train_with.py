@@ -8,7 +8,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
-from jax_raft_amd.train import fused  # noqa: E402
+from jax_raft_amd.train import fused, fused_encoder  # noqa: E402
 
 
 def main():
@@ -17,7 +17,7 @@ def main():
     for item in argv[:cut]:
         k, v = item.split("=")
         cls, attr = k.split(".")
-        obj = getattr(fused, cls)
+        obj = getattr(fused, cls, None) or getattr(fused_encoder, cls)
         old = getattr(obj, attr)
         val = (v not in ("0", "false", "False")) if isinstance(old, bool) else type(old)(v)
         setattr(obj, attr, val)
