@@ -68,3 +68,6 @@ def test_bench_extras_keys():
     assert ex["fp32_b1_fps"]["config"]["dtype"] == "fp32"
     for k in ("b1_fps", "small_b1_fps_32it", "small_b1_fps_12it", "fp32_b1_fps", "train_pairs_per_s"):
         assert ex[k] is not None and ex[k]["value"] > 0, (k, r.stderr[-1500:])
+    # single GPU: the training extra runs in a fresh child process (bench.py:run_training_child)
+    assert ex["train_pairs_per_s"]["process"].startswith("fresh child"), ex["train_pairs_per_s"]
+    assert ex["train_pairs_per_s"]["config"]["image_size"] == [128, 256]
