@@ -1163,18 +1163,18 @@ class RaftEngine:
         E_PREP, E_CTX, E_FLOW, E_FH, E_MASK, E_FE2 = range(ev0, ev0 + 6)
         main, side, side2 = lanes
         lanes_on = main != side
-        # the prologue's branches (context encoder, feature encoder of each image) run on
-        # their own lanes even when the loop runs on one, for batch 2 .. Sintel-size batch 4
-        # worth of pixels.  At batch 1 (round 6, profiles/r6_prolanes_ab.txt) the replayed
-        # branches ran one after another (rocprofv3: context encoder, then image 1's feature
-        # encoder, then image 2's, on three hardware queues), so the lanes only doubled the
-        # feature encoder's ~70 latency-bound launches; one batch-2 feature-encoder chain
-        # measured raft_small sync 297 -> 330 pairs/s, its 32-iteration stream 439 -> 462,
-        # raft_large sync 216 -> 224 (1088x1920 frames: 67.6 -> 63.7 with lanes, round 4).
-        # PRO_LANES = "off": never, "on": always.
+        # the prologue's branches (context encoder, feature encoder per image) run on their own
+        # lanes even when the loop runs on one, up to Sintel-size batch 4 worth of pixels.  At
+        # batch 1 ("auto") the feature encoder runs as ONE batch-2 chain next to the context
+        # encoder's lane (round 6, profiles/r6_prolanes_ab.txt, r6_ce_lane_b1_ab.txt): per-image
+        # lanes of its ~70 short kernels only added dispatch cost (the replayed branches ran one
+        # after another, r6_graph_branches.txt); raft_small sync 297 -> 334-340 pairs/s, its
+        # 12-iteration stream 662-758 -> 782-796, raft_large sync 216 -> 218-222.  (1088x1920
+        # frames: 67.6 -> 63.7 with lanes, round 4, so off there.)
+        # PRO_LANES = "off": never, "on": always (per-image feature-encoder lanes at batch 1 too).
         pl = self.PRO_LANES
         assert pl in ("auto", "on", "off"), pl
-        pro_on = pl == "on" or (pl == "auto" and 2 <= B and B * h * w <= 4 * 55 * 128)
+        pro_on = pl == "on" or (pl == "auto" and B * h * w <= 4 * 55 * 128)
         p_main, p_side, p_side2 = lanes if lanes_on or self.cp or not pro_on else (main, 1, 2)
         p_on = p_main != p_side
         # the per-image feature-encoder split (lane 2) -- never at batch 1 under "auto", also not in

@@ -309,17 +309,20 @@ def test_encoder_instance_norm_fused_into_halo_convs(fake, monkeypatch, fuse):
 
 @pytest.mark.parametrize("arch", [raft_large, raft_small])
 def test_prologue_lanes_at_batch_one(fake, monkeypatch, arch):
-    """At batch 1 ("auto") the whole forward runs on lane 0, the feature encoder as one batch-2
-    chain over both images (measured faster, profiles/r6_prolanes_ab.txt); RaftEngine.PRO_LANES =
-    "on" puts the prologue on three lanes: context encoder (lane 1), feature encoder of image 2
-    (lane 2), image 1 + pyramid (lane 0), the loop staying on one."""
-    eng, p = _plan(arch, 1)
-    assert {ln for s, ln, d, op, a in p.ops} == {0}
-    monkeypatch.setattr(E.RaftEngine, "PRO_LANES", "on")
+    """At batch 1 ("auto") the context encoder runs on lane 1 and the feature encoder as ONE
+    batch-2 chain over both images on lane 0 with the pyramid (measured faster,
+    profiles/r6_ce_lane_b1_ab.txt); RaftEngine.PRO_LANES = "on" adds image 2's feature encoder
+    on lane 2; "off" keeps the whole forward on lane 0.  The loop stays on one lane."""
     eng, p = _plan(arch, 1)
     pro_lanes = {ln for s, ln, d, op, a in p.ops if s == 0}
     loop_lanes = {ln for s, ln, d, op, a in p.ops if s == 1}
-    assert pro_lanes == {0, 1, 2} and loop_lanes == {0}
+    assert pro_lanes == {0, 1} and loop_lanes == {0}
+    monkeypatch.setattr(E.RaftEngine, "PRO_LANES", "on")
+    eng, p = _plan(arch, 1)
+    assert {ln for s, ln, d, op, a in p.ops if s == 0} == {0, 1, 2}
+    monkeypatch.setattr(E.RaftEngine, "PRO_LANES", "off")
+    eng, p = _plan(arch, 1)
+    assert {ln for s, ln, d, op, a in p.ops} == {0}
 
 
 @pytest.mark.parametrize("factory", [raft_large, raft_small])
