@@ -1168,8 +1168,8 @@ class RaftEngine:
         # batch 1 ("auto") the feature encoder runs as ONE batch-2 chain next to the context
         # encoder's lane (round 6, profiles/r6_prolanes_ab.txt, r6_ce_lane_b1_ab.txt): per-image
         # lanes of its ~70 short kernels only added dispatch cost (the replayed branches ran one
-        # after another, r6_graph_branches.txt); raft_small sync 297 -> 334-340 pairs/s, its
-        # 12-iteration stream 662-758 -> 782-796, raft_large sync 216 -> 218-222.  (1088x1920
+        # after another, r6_graph_branches.txt); raft_small sync 297 -> 330-344 pairs/s, its
+        # 12-iteration stream 662-758 -> 782-805, raft_large sync 216 -> 218-223.  (1088x1920
         # frames: 67.6 -> 63.7 with lanes, round 4, so off there.)
         # PRO_LANES = "off": never, "on": always (per-image feature-encoder lanes at batch 1 too).
         pl = self.PRO_LANES
