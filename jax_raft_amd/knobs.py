@@ -7,8 +7,9 @@ A/B (the profile is cited where the choice is made) and the ones tests flip to c
 alternative are class or module attributes -- ``RaftEngine.GRU``, ``.PRO_LANES``,
 ``.HALO_NORM``, ``.MERGED_UP``, ``.CONV_GROUP``, ``.MASK_PARITY``, ``.HOST_GATE``,
 ``.AUTO_STREAMS_MIN_BATCH``, ``.GATE_MIN_ITERS``, ``.max_plans`` (runtime/engine.py) and
-``FUSED_ENCODERS``, ``FUSED_GRAPH``, ``FUSED_TRAIN`` (train/fused.py), ``HALO_NORM``
-(train/fused_encoder.py) -- and per-kernel variants
+``FUSED_ENCODERS``, ``FUSED_GRAPH``, ``FUSED_TRAIN``, ``FusedModel.SIDE_ENCODER``,
+``FusedModel.EARLY_CE``, ``FusedLoop.LANES`` / ``.FWD_LANES`` (train/fused.py), ``HALO_NORM``
+(train/fused_encoder.py), ``Trainer.SETTLE_LAG`` (train/trainer.py) -- and per-kernel variants
 are op arguments (``conv_f32_args(ksplit=)``, ``gru_fused``'s fifth int, conv cfg bits 10 / 11).
 
 ===================  =====================================================================
