@@ -424,6 +424,8 @@ def main():
     ap.add_argument("--extra-steps", type=int, default=20)
     ap.add_argument("--step-times", action="store_true", help="print every timed step's device time (stderr)")
     ap.add_argument("--skip-extras", default="", help="comma list of extras to leave out (diagnostics)")
+    ap.add_argument("--only-extra", default="", help="run just this extra in this process (no headline; prints "
+                                                     "its record as one JSON line) -- diagnostics / child runs")
     ap.add_argument("--extra-pause", type=float, default=0.0, help="seconds of idle before each extra (diagnostics)")
     ap.add_argument("--train-batch", type=int, default=6, help="extras: training batch per GPU (config 5: 6)")
     ap.add_argument("--train-size", type=int, nargs=2, default=[384, 512], help="extras: training image size")
@@ -451,17 +453,20 @@ def main():
                      corr_dtype=torch.bfloat16 if args.corr_dtype == "bf16" else torch.float32,
                      copy_output=not args.no_copy_output, precision=args.precision)
     B, H, W = args.batch, args.height, args.width
-    head = run_inference(ctx, model, B=B, H=H, W=W, iters=args.iters, steps=args.steps, warmup=args.warmup,
-                         final_only=args.final_only, gather=not args.no_gather, seed=1234, engine_kw=engine_kw,
-                         pipeline=args.pipeline, h2d=not args.no_h2d, sync_h2d=args.sync_h2d)
-    rccl_world = ctx.world_check()
+    if args.only_extra:
+        head, rccl_world = None, ctx.world
+    else:
+        head = run_inference(ctx, model, B=B, H=H, W=W, iters=args.iters, steps=args.steps, warmup=args.warmup,
+                             final_only=args.final_only, gather=not args.no_gather, seed=1234, engine_kw=engine_kw,
+                             pipeline=args.pipeline, h2d=not args.no_h2d, sync_h2d=args.sync_h2d)
+        rccl_world = ctx.world_check()
     del model
     torch.cuda.empty_cache()
 
     default_cfg = (args.arch == "raft_large" and (B, H, W, args.iters) == (4, 440, 1024, 32) and not args.final_only
                    and not args.no_graph and args.precision == "bf16")
     extras = {}
-    if args.extras == "on" or (args.extras == "auto" and default_cfg):
+    if args.extras == "on" or (args.extras == "auto" and default_cfg) or args.only_extra:
         t_ex = time.perf_counter()
         ks, kw_ = args.extra_steps, max(3, args.warmup)
         # *_b1_fps: batch-1 stream throughput (graph-pipelined: pair i's loop overlaps pair i+1's
@@ -481,7 +486,7 @@ def main():
                 ("hires_b1", "raft_large", 32, None, "bf16", "stream", (1088, 1920))]
         skip = set(filter(None, args.skip_extras.split(",")))
         for key, arch, it, base, prec, proto, (eh, ew) in plan:
-            if key in skip:
+            if key in skip or (args.only_extra and key != args.only_extra):
                 continue
             if args.extra_pause:   # diagnostics: idle the GPU before each extra
                 time.sleep(args.extra_pause)
@@ -518,6 +523,10 @@ def main():
                 extras[key] = None
                 print(f"bench.py: extra {key} failed: {type(e).__name__}: {e}", file=sys.stderr)
             torch.cuda.empty_cache()
+        if args.only_extra:
+            if ctx.rank == 0:
+                print(json.dumps({args.only_extra: extras.get(args.only_extra)}), flush=True)
+            return
         try:
             if ctx.world == 1:
                 extras["train_pairs_per_s"] = run_training_child(arch="raft_large", B=args.train_batch,
